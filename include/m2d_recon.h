@@ -1,0 +1,130 @@
+/*
+ * m2dec_amd — the parse -> reconstruction record ABI (plain C, no torch types).
+ *
+ * The reference fuses parse and reconstruction per macroblock (h264.cpp:2005-2022,
+ * 3131-3143, 6438-6454, 7366-7371); this boundary does not exist there.  The host parser
+ * (m2dec_amd/csrc/host) emits, per picture, one record arena; a reconstruction back end (the
+ * gfx950 HIP back end in m2dec_amd/csrc/hip, or the CPU oracle in oracle/) turns it into NV12.
+ * Record fields map 1:1 onto the arguments the reference's recon call sites receive:
+ *   m2r_mb_t       : mb_code dispatch (h264.h:429-433), avail/avail_intra (h264.cpp:3271-3292),
+ *                    qmat selection via qp (set_qp, h264.cpp:1092-1119)
+ *   m2r_inter_t    : mb->inter_pred(mb, ref_idx[2], mv[2], size, ox, oy) (h264.h:396)
+ *   m2r_slice_t    : pred_weight_table / implicit weights (h264.cpp:1686-1712, 7001-7025)
+ *   m2r_deblock_t  : deblock_info_t (h264.h:344-348) with the raster carry of idc/slicehdr and the
+ *                    picture-final firstline test of deblock_pb (h264.cpp:10553-10612) resolved.
+ */
+#ifndef M2DEC_AMD_M2D_RECON_H
+#define M2DEC_AMD_M2D_RECON_H
+
+#include <stdint.h>
+#include "m2d.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+	M2R_MB_I4x4 = 0,
+	M2R_MB_I8x8 = 1,
+	M2R_MB_I16x16 = 2,
+	M2R_MB_PCM = 3,
+	M2R_MB_INTER = 4
+};
+
+/* nz bit layout of m2r_mb_t.nz (one bit per coefficient block present in the pool, in pool order) */
+#define M2R_NZ_LUMA(blk) (1u << (blk))       /* blkIdx 0..15 (4x4) ; 8x8 block b uses bit 4*b */
+#define M2R_NZ_LUMA_DC (1u << 16)            /* Intra16x16 DC block */
+#define M2R_NZ_CDC(c) (1u << (17 + (c)))     /* chroma DC, c = 0 Cb / 1 Cr */
+#define M2R_NZ_CAC(c, b) (1u << (19 + 4 * (c) + (b)))
+
+#define M2R_FLAG_T8x8 1u
+
+/* One macroblock, 32 bytes. */
+typedef struct m2r_mb {
+	uint8_t kind;         /* M2R_MB_* */
+	uint8_t cbp;          /* bits 0-3 luma 8x8 coded, bits 4-5 chroma cbp (0, 1 = DC, 2 = DC+AC) */
+	uint8_t avail_luma;   /* avail bits handed to the luma predictor (1 left, 2 top, 4 top-right, 8 top-left) */
+	uint8_t avail_chroma; /* avail bits handed to the chroma predictor */
+	int8_t qpy;
+	int8_t qpc[2];
+	uint8_t pred_mode;    /* I16x16: 0 V, 1 H, 2 DC, 3 plane */
+	uint8_t chroma_mode;  /* 0 DC, 1 H, 2 V, 3 plane */
+	uint8_t flags;        /* M2R_FLAG_T8x8 */
+	uint16_t slice;       /* index into m2r_picture_t.slice */
+	uint32_t ipred[2];    /* Intra4x4 (blkIdx order) / Intra8x8 (first 4) modes, 4 bits each */
+	uint32_t coef;        /* offset in int16 units into the coefficient pool */
+	uint32_t nz;          /* coded blocks present in the pool (M2R_NZ_*) */
+	uint32_t inter;       /* index into m2r_picture_t.inter (kind == INTER) */
+} m2r_mb_t;
+
+/* Motion of one inter macroblock, 144 bytes. */
+typedef struct m2r_inter {
+	int16_t mv[2][16][2]; /* [list][4x4 raster idx = y*4 + x][x, y], quarter-pel */
+	int8_t slot[2][4];    /* [list][8x8 raster idx] frame slot of the reference, -1 = list unused */
+	int8_t refidx[2][4];  /* [list][8x8] ref_idx (weight table lookup) */
+} m2r_inter_t;
+
+enum { M2R_WP_DEFAULT = 0, M2R_WP_EXPLICIT = 1, M2R_WP_IMPLICIT = 2 };
+
+/* Per-slice weighted-prediction state. */
+typedef struct m2r_slice {
+	uint8_t wp_mode;
+	uint8_t log2wd[2];    /* explicit: luma / chroma log2 weight denominator */
+	uint8_t pad[5];
+	int8_t w[2][32][3];   /* explicit weight [list][ref_idx][Y, Cb, Cr] (int8 as stored by the reference) */
+	int8_t o[2][32][3];   /* explicit offset */
+	int8_t iw[32][32][2]; /* implicit (w0, w1) per (refIdxL0, refIdxL1), int8 wrap as the reference */
+} m2r_slice_t;
+
+#define M2R_DBK_LEFT 1u     /* filter the left MB edge */
+#define M2R_DBK_TOP 2u      /* filter the top MB edge */
+#define M2R_DBK_LEFT_BS4 4u /* left MB edge is bS 4 (strong) */
+#define M2R_DBK_TOP_BS4 8u  /* top MB edge is bS 4 */
+#define M2R_DBK_OFF 16u     /* disable_deblocking_filter_idc == 1: MB not filtered */
+
+/* Deblocking input of one macroblock, 16 bytes. */
+typedef struct m2r_deblock {
+	uint32_t bs_v;        /* vertical edges x = 0,4,8,12: byte e = edge, 2 bits per 4-row segment (LSB = top), bS 0..3 */
+	uint32_t bs_h;        /* horizontal edges y = 0,4,8,12: byte e = edge, 2 bits per 4-column segment (LSB = left) */
+	int8_t qpy;
+	int8_t qpc[2];
+	uint8_t flags;        /* M2R_DBK_* */
+	int8_t alpha_off;     /* FilterOffsetA = slice_alpha_c0_offset_div2 * 2 */
+	int8_t beta_off;      /* FilterOffsetB */
+	uint8_t pad[2];
+} m2r_deblock_t;
+
+/* One picture's records.  Arrays live in one arena owned by the back end (pinned for the GPU). */
+typedef struct m2r_picture {
+	int32_t width_mbs, height_mbs;
+	int32_t slot;          /* destination frame slot */
+	int32_t n_inter;       /* used entries of inter[] */
+	int32_t n_coef;        /* used int16 of coef[] */
+	int32_t n_slices;      /* used entries of slice[] */
+	int32_t n_intra;       /* number of intra (I4x4/I8x8/I16x16/PCM) macroblocks */
+	int32_t deblock;       /* 0: no macroblock needs filtering */
+	m2r_mb_t *mb;          /* [width_mbs * height_mbs] raster order */
+	m2r_deblock_t *dbk;    /* [width_mbs * height_mbs] */
+	m2r_slice_t *slice;    /* [cap_slices] */
+	m2r_inter_t *inter;    /* [cap_inter] */
+	int16_t *coef;         /* [cap_coef] */
+	int32_t cap_slices, cap_inter, cap_coef;
+	int32_t pad;
+} m2r_picture_t;
+
+/* A reconstruction back end.  The parser acquires an arena, fills it, and submits it; frames are
+ * caller-owned NV12 buffers (set_frames), synchronised on demand (sync_frame) before the caller
+ * reads them through peek/get_decoded_frame. */
+typedef struct m2r_backend {
+	void *self;
+	int (*set_frames)(void *self, int n, const m2d_frame_t *frames, int width, int height);
+	m2r_picture_t *(*acquire)(void *self, int width_mbs, int height_mbs);
+	int (*submit)(void *self, m2r_picture_t *pic);
+	int (*sync_frame)(void *self, int slot);
+	void (*destroy)(void *self);
+} m2r_backend_t;
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,65 @@
+/*
+ * m2dec_amd — extra C ABI of libm2dec_amd.so beyond the reference's m2d_func_table_t.
+ *
+ * Nothing here replaces a reference entry point; these are the hooks a maintainer needs to wire
+ * the GPU back end into the reference's callers:
+ *   - back-end selection (default: gfx950 HIP back end on `device`),
+ *   - explicit release of GPU / heap resources (the reference's context is caller memory only),
+ *   - a whole-stream driver equivalent to src/app/h264dec.cpp + m2decoder.h (used by bench/tests),
+ *   - direct record-level access to the HIP reconstruction kernels (kernel parity tests).
+ */
+#ifndef M2DEC_AMD_H
+#define M2DEC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "m2d.h"
+#include "m2d_recon.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+	int frames_out;
+	int pictures;
+	int last_error;
+	int pad;
+} m2dec_amd_stats_t;
+
+/* Use `be` instead of the default HIP back end for this decoder context (call after init). */
+int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
+/* GPU ordinal used by the default back end (call after init, before the first SPS). */
+int m2dec_amd_h264_set_device(void *ctx, int device);
+/* Free heap and GPU resources owned by a context. */
+void m2dec_amd_h264_release(void *ctx);
+
+/* Decode a whole Annex-B stream exactly like `h264dec` (m2decoder.h:132-157 output loop).
+ * on_frame receives every output frame in output order.  backend may be NULL (HIP back end).
+ * Returns the number of frames output, or -1 on error. */
+int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                            m2dec_amd_stats_t *stats);
+
+/* HIP back end constructor (m2dec_amd/csrc/hip/recon_hip.hip). */
+int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device);
+/* Non-zero if a gfx950 device is usable by this process. */
+int m2dec_amd_hip_available(void);
+
+/* Per-kernel timing of the HIP back end since creation (microseconds, HIP events). */
+typedef struct {
+	double inter_us, intra_us, deblock_us, h2d_us, d2h_us;
+	int64_t pictures, inter_launches, intra_launches, deblock_launches;
+	int64_t record_bytes;   /* bytes of records uploaded (R_pic summed) */
+	int64_t ref_bytes;      /* algorithmic reference bytes read by MC (sum over PUs and lists) */
+	int64_t frame_bytes;    /* NV12 bytes written (1.5 W H per picture) */
+} m2dec_amd_hip_timing_t;
+int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out);
+
+/* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
+void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

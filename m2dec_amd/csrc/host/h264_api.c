@@ -1,0 +1,372 @@
+/*
+ * h264d_func — the reference's m2d_func_table_t for H.264 (h264.cpp:12057-12068), backed by the
+ * m2dec_amd host parser + a reconstruction back end (the gfx950 HIP back end by default).
+ *
+ *   init                  h264.cpp:446-464
+ *   get_info              h264.cpp:505-525
+ *   set_frames            h264.cpp:647-661
+ *   decode_picture        h264.cpp:663-693  (returns 1 per picture, -1 error, -2 end of data)
+ *   peek/get_decoded_frame h264.cpp:817-867
+ *
+ * Extra C-ABI entry points (include/m2dec_amd.h): back-end selection, release, and a driver that
+ * mirrors src/app/h264dec.cpp + m2decoder.h so tests and bench.py can decode a whole stream.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "h264_dec.h"
+#include "m2dec_amd.h"
+
+int h264_nal_next(h264_dec_t *d);
+
+static int hdr_dummy(void *a, void *b)
+{
+	(void)a;
+	(void)b;
+	return 0;
+}
+
+static h264_dec_t *CTX(void *p) { return (h264_dec_t *)p; }
+
+static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d) return -1;
+	memset(d, 0, sizeof(*d));
+	d->stream = &d->stream_i;
+	d->header_callback = cb ? cb : hdr_dummy;
+	d->header_callback_arg = arg;
+	d->dpb_max_arg = dpb_max;
+	h264_dpb_init(&d->dpb, dpb_max);
+	dec_bits_open(d->stream, m2d_load_bytes_skip03);
+	for (int i = 0; i < 16; ++i) d->refs[1][i].col = (int16_t)i;
+	d->curr_col = 16;
+	d->sh.first_mb = -1;
+	return 0;
+}
+
+static dec_bits *api_stream_pos(void *ctx)
+{
+	return CTX(ctx)->stream;
+}
+
+static int api_get_info(void *ctx, m2d_info_t *info)
+{
+	h264_dec_t *d = CTX(ctx);
+	const h264_sps_t *s;
+	if (!d || !info) return -1;
+	/* the reference reads the SPS of the current slice's PPS (h264.cpp:511) */
+	s = &d->sps[d->pps[d->sh.pps_id].sps_id];
+	if (!s->valid) s = &d->sps[d->active_sps];
+	info->src_width = (int16_t)s->width;
+	info->src_height = (int16_t)s->height;
+	info->disp_width = (int16_t)s->width;
+	info->disp_height = (int16_t)s->height;
+	info->frame_num = (int16_t)(s->num_ref_frames + 1);
+	for (int i = 0; i < 4; ++i) info->crop[i] = (int16_t)s->crop[i];
+	info->additional_size = 16; /* parser state lives in the context / back end, not the caller's work buffer */
+	return 0;
+}
+
+static int ensure_backend(h264_dec_t *d)
+{
+	if (d->have_backend) return 0;
+	if (m2dec_amd_hip_backend_create(&d->backend, d->device) < 0) {
+		fprintf(stderr, "m2dec_amd: HIP reconstruction back end unavailable (no gfx950 device / HIP runtime); "
+		                "install an explicit back end with m2dec_amd_h264_set_backend() for CPU checking\n");
+		return -1;
+	}
+	d->have_backend = 1;
+	return 0;
+}
+
+static int alloc_geometry(h264_dec_t *d, int w, int h)
+{
+	int mb_w = w >> 4, mb_h = h >> 4, n = mb_w * mb_h;
+	if (mb_w <= 0 || mb_h <= 0) return -1;
+	if (d->mb_w == mb_w && d->mb_h == mb_h && d->mbi) return 0;
+	free(d->mbi);
+	d->mbi = (h264_mbinfo_t *)calloc((size_t)n, sizeof(h264_mbinfo_t));
+	for (int i = 0; i < 17; ++i) {
+		free(d->colpic[i].mb);
+		d->colpic[i].mb = (h264_colmb_t *)calloc((size_t)n, sizeof(h264_colmb_t));
+		memset(d->colpic[i].map_col_frameidx, 0, sizeof(d->colpic[i].map_col_frameidx));
+		if (!d->colpic[i].mb) return -1;
+	}
+	if (!d->mbi) return -1;
+	d->mb_w = mb_w;
+	d->mb_h = mb_h;
+	d->n_mbs = n;
+	return 0;
+}
+
+static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, int work_len)
+{
+	h264_dec_t *d = CTX(ctx);
+	const h264_sps_t *s;
+	(void)work_len;
+	if (!d || n < 3 || n > H264D_MAX_FRAME_NUM || !frames || !work) return -1;
+	d->num_frames = n;
+	memcpy(d->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
+	memset(d->lru, 0, sizeof(d->lru));
+	s = &d->sps[d->active_sps];
+	if (alloc_geometry(d, s->width, s->height) < 0) return -1;
+	if (ensure_backend(d) < 0) return -1;
+	if (d->backend.set_frames(d->backend.self, n, d->frames, s->width, s->height) < 0) return -1;
+	d->frames_ready = 1;
+	return 0;
+}
+
+/* one slice NAL */
+static int read_slice(h264_dec_t *d, int nal_unit_type, int nal_ref_idc)
+{
+	const h264_sps_t *s;
+	int prev_first = d->in_picture ? d->sh.first_mb : -1;
+	int err;
+	hb_init(&d->bs, d->nal + 1, d->nal_len - 1);
+	d->slice_rbsp = d->nal + 1;
+	d->slice_rbsp_end = d->nal + d->nal_len;
+	{
+		/* bit position of the rbsp_stop_one_bit */
+		size_t len = d->nal_len - 1;
+		const uint8_t *p = d->slice_rbsp;
+		d->slice_rbsp_bits = len ? (len - 1) * 8 + (size_t)(7 - __builtin_ctz(p[len - 1])) : 0;
+	}
+	err = h264_slice_header(d, &d->bs, nal_unit_type, nal_ref_idc);
+	if (err < 0) return err;
+	if (d->in_picture && d->sh.first_mb <= prev_first) return -2; /* h264.cpp:1427-1430 */
+	s = &d->sps[d->active_sps];
+	if (!d->frames_ready) return -1;
+	if (alloc_geometry(d, s->width, s->height) < 0) return -1;
+	if (!d->in_picture) {
+		if (h264_picture_begin(d) < 0) return -1;
+	}
+	err = h264_slice_data(d);
+	if (err < 0) return err;
+	if (err == 1) return h264_picture_finish(d);
+	return 0;
+}
+
+static int api_decode_picture(void *ctx)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d) return -1;
+	for (;;) {
+		int type, ref_idc, err = 0;
+		if (h264_nal_next(d) < 0) return -2;
+		if (d->nal_len == 0) continue;
+		type = d->nal[0] & 31;
+		ref_idc = (d->nal[0] >> 5) & 3;
+		switch (type) {
+		case 1:
+		case 5:
+			err = read_slice(d, type, ref_idc);
+			if (err != 0) return err;
+			break;
+		case 7: {
+			h264_bits_t b;
+			int id;
+			hb_init(&b, d->nal + 1, d->nal_len - 1);
+			id = h264_parse_sps(d, &b);
+			if (id < 0) return id;
+			if (!d->in_picture) d->active_sps = id;
+			d->header_callback(d->header_callback_arg, d->stream->id);
+			break;
+		}
+		case 8: {
+			h264_bits_t b;
+			hb_init(&b, d->nal + 1, d->nal_len - 1);
+			err = h264_parse_pps(d, &b, d->nal_len - 1);
+			if (err < 0) return err;
+			break;
+		}
+		default:
+			break;
+		}
+	}
+}
+
+static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
+{
+	if (idx < 0) return 0;
+	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) return -1;
+	*frame = d->frames[idx];
+	return 1;
+}
+
+static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d || !frame) return -1;
+	return deliver(d, h264_dpb_peek(&d->dpb, bypass), frame);
+}
+
+static int api_get(void *ctx, m2d_frame_t *frame, int bypass)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d || !frame) return -1;
+	return deliver(d, h264_dpb_pop(&d->dpb, bypass), frame);
+}
+
+static const m2d_func_table_t h264d_func_ = {
+	sizeof(h264_dec_t),
+	api_init,
+	api_stream_pos,
+	api_get_info,
+	api_set_frames,
+	api_decode_picture,
+	api_peek,
+	api_get,
+};
+
+const m2d_func_table_t * const h264d_func = &h264d_func_;
+
+/* ------------------------------------------------------------------ extra C ABI */
+int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d || !be) return -1;
+	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
+	d->backend = *be;
+	d->have_backend = 1;
+	return 0;
+}
+
+int m2dec_amd_h264_set_device(void *ctx, int device)
+{
+	CTX(ctx)->device = device;
+	return 0;
+}
+
+void m2dec_amd_h264_release(void *ctx)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d) return;
+	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
+	d->have_backend = 0;
+	free(d->mbi);
+	d->mbi = NULL;
+	for (int i = 0; i < 17; ++i) {
+		free(d->colpic[i].mb);
+		d->colpic[i].mb = NULL;
+	}
+	free(d->nal);
+	d->nal = NULL;
+}
+
+/* ------------------------------------------------------------------ stream driver (h264dec.cpp + m2decoder.h) */
+typedef struct {
+	h264_dec_t *d;
+	const uint8_t *data;
+	size_t len;
+	size_t pos;
+	int outbuf;
+	uint8_t *frame_mem;
+	m2d_frame_t frames[H264D_MAX_FRAME_NUM];
+	int nframes;
+	size_t luma_len;
+	uint8_t work[64];
+	int failed;
+} driver_t;
+
+static int drv_reread(void *arg)
+{
+	driver_t *v = (driver_t *)arg;
+	if (v->pos < v->len) {
+		dec_bits_set_data(v->d->stream, v->data + v->pos, v->len - v->pos, 0);
+		v->pos = v->len;
+		return 0;
+	}
+	return -1;
+}
+
+/* M2Decoder::SetFrames, m2decoder.h:54-80 */
+static int drv_header(void *arg, void *id)
+{
+	driver_t *v = (driver_t *)arg;
+	m2d_info_t info;
+	int w, h, bufnum;
+	size_t luma_len;
+	(void)id;
+	h264d_func->get_info(v->d, &info);
+	w = (info.src_width + 15) & ~15;
+	h = (info.src_height + 15) & ~15;
+	luma_len = (size_t)w * (size_t)h;
+	bufnum = v->outbuf + info.frame_num + 16;
+	if (bufnum > H264D_MAX_FRAME_NUM) bufnum = H264D_MAX_FRAME_NUM;
+	if (v->frame_mem && bufnum <= v->nframes && luma_len <= v->luma_len) return 0;
+	free(v->frame_mem);
+	v->frame_mem = (uint8_t *)aligned_alloc(4096, ((luma_len * 3 / 2 + 4095) & ~(size_t)4095) * (size_t)bufnum);
+	if (!v->frame_mem) {
+		v->failed = 1;
+		return -1;
+	}
+	{
+		size_t fsz = (luma_len * 3 / 2 + 4095) & ~(size_t)4095;
+		for (int i = 0; i < bufnum; ++i) {
+			memset(&v->frames[i], 0, sizeof(v->frames[i]));
+			v->frames[i].luma = v->frame_mem + fsz * (size_t)i;
+			v->frames[i].chroma = v->frames[i].luma + luma_len;
+		}
+	}
+	v->nframes = bufnum;
+	v->luma_len = luma_len;
+	if (h264d_func->set_frames(v->d, bufnum, v->frames, v->work, info.additional_size) < 0) v->failed = 1;
+	return 0;
+}
+
+int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
+{
+	driver_t v;
+	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
+	m2d_frame_t frm;
+	int err = 0, n = 0;
+	if (!d) return -1;
+	memset(&v, 0, sizeof(v));
+	v.d = d;
+	v.data = data;
+	v.len = len;
+	h264d_func->init(d, -1, drv_header, &v);
+	d->device = device;
+	if (backend) m2dec_amd_h264_set_backend(d, backend);
+	dec_bits_set_callback(d->stream, drv_reread, &v);
+	/* h264dec.cpp:251-257 + M2Decoder::decode / decode_residual (m2decoder.h:132-157) */
+	for (;;) {
+		err = 0;
+		while (h264d_func->peek_decoded_frame(d, &frm, 0) <= 0) {
+			err = h264d_func->decode_picture(d);
+			if (v.failed) { err = -1; break; }
+			if (err < 0) {
+				while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
+					if (on_frame) on_frame(arg, &frm);
+					n++;
+					h264d_func->get_decoded_frame(d, &frm, 1);
+				}
+				goto done;
+			}
+		}
+		h264d_func->get_decoded_frame(d, &frm, 0);
+		if (on_frame) on_frame(arg, &frm);
+		n++;
+		err = h264d_func->decode_picture(d);
+		if (err < 0) {
+			while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
+				if (on_frame) on_frame(arg, &frm);
+				n++;
+				h264d_func->get_decoded_frame(d, &frm, 1);
+			}
+			break;
+		}
+	}
+done:
+	if (stats) {
+		stats->frames_out = n;
+		stats->pictures = (int)d->pictures;
+		stats->last_error = err;
+	}
+	m2dec_amd_h264_release(d);
+	free(d);
+	free(v.frame_mem);
+	return (err == -2) ? n : -1;
+}

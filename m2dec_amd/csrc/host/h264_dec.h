@@ -1,0 +1,338 @@
+/*
+ * m2dec_amd host-side H.264 parser: internal state.
+ *
+ * The parser reproduces the reference's bitstream semantics (h264.cpp) and emits per-picture
+ * reconstruction records (include/m2d_recon.h).  Reference anchors are cited per function.
+ */
+#ifndef M2DEC_AMD_H264_DEC_H
+#define M2DEC_AMD_H264_DEC_H
+
+#include <stdint.h>
+#include <string.h>
+#include "m2d.h"
+#include "m2d_recon.h"
+#include "h264_spec_tables.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- bit reader (RBSP) */
+typedef struct {
+	const uint8_t *p;   /* next byte to load */
+	const uint8_t *end;
+	uint64_t cache;     /* MSB-aligned */
+	int bits;           /* valid bits in cache */
+} h264_bits_t;
+
+static inline void hb_init(h264_bits_t *b, const uint8_t *p, size_t len)
+{
+	b->p = p;
+	b->end = p + len;
+	b->cache = 0;
+	b->bits = 0;
+}
+
+static inline void hb_fill(h264_bits_t *b)
+{
+	while (b->bits <= 56) {
+		uint64_t byte = (b->p < b->end) ? *b->p : 0;
+		b->p++;
+		b->cache |= byte << (56 - b->bits);
+		b->bits += 8;
+	}
+}
+
+static inline uint32_t hb_show(h264_bits_t *b, int n)
+{
+	if (b->bits < n) hb_fill(b);
+	return n ? (uint32_t)(b->cache >> (64 - n)) : 0;
+}
+
+static inline void hb_skip(h264_bits_t *b, int n)
+{
+	if (b->bits < n) hb_fill(b);
+	b->cache <<= n;
+	b->bits -= n;
+}
+
+static inline uint32_t hb_get(h264_bits_t *b, int n)
+{
+	uint32_t v;
+	if (n == 0) return 0;
+	if (n > 32) n = 32;
+	if (b->bits < n) hb_fill(b);
+	v = (uint32_t)(b->cache >> (64 - n));
+	b->cache <<= n;
+	b->bits -= n;
+	return v;
+}
+
+static inline uint32_t hb_get1(h264_bits_t *b)
+{
+	return hb_get(b, 1);
+}
+
+static inline uint32_t hb_ue(h264_bits_t *b)
+{
+	int lz;
+	if (b->bits < 32) hb_fill(b);
+	if (b->cache == 0) { hb_skip(b, 32); return 0xffffffffu; }
+	lz = __builtin_clzll(b->cache);
+	if (lz > 31) { hb_skip(b, 32); return 0xffffffffu; }
+	hb_skip(b, lz);
+	return hb_get(b, lz + 1) - 1;
+}
+
+static inline int32_t hb_se(h264_bits_t *b)
+{
+	uint32_t ue = hb_ue(b);
+	int32_t t = (int32_t)((ue + 1) >> 1);
+	return (ue & 1) ? t : -t;
+}
+
+/* bits consumed so far (position) */
+static inline size_t hb_pos(const h264_bits_t *b, const uint8_t *start)
+{
+	return (size_t)(b->p - start) * 8 - (size_t)b->bits;
+}
+
+/* ---------------------------------------------------------------- CABAC engine */
+typedef struct {
+	uint64_t value;     /* codIOffset in the top, `bits` look-ahead bits below */
+	uint32_t range;     /* codIRange, 9 bits */
+	int bits;
+	const uint8_t *p, *end;
+	uint8_t ctx[H264_NUM_CTX]; /* (pStateIdx << 1) | valMPS */
+} h264_cabac_t;
+
+/* ---------------------------------------------------------------- parameter sets */
+typedef struct {
+	int valid;
+	int profile_idc, level_idc, constraint_flags;
+	int poc_type;
+	int log2_max_frame_num;
+	int log2_max_poc_lsb;
+	int num_ref_frames;
+	int delta_pic_order_always_zero_flag;
+	int offset_for_non_ref_pic;
+	int offset_for_top_to_bottom_field;
+	int num_ref_frames_in_poc_cycle;
+	int32_t offset_for_ref_frame[256]; /* cumulative, as the reference stores it (h264.cpp:291-299) */
+	int gaps_allowed;
+	int width, height; /* coded, samples */
+	int max_dpb_in_mbs;
+	int frame_mbs_only_flag;
+	int direct_8x8_inference_flag;
+	int crop[4];       /* left, right, top, bottom in samples (h264.cpp:351) */
+} h264_sps_t;
+
+typedef struct {
+	int valid;
+	int sps_id;
+	int entropy_coding_mode_flag;
+	int pic_order_present_flag;
+	int num_ref_idx_active[2];
+	int weighted_pred_flag;
+	int weighted_bipred_idc;
+	int pic_init_qp;
+	int chroma_qp_index[2];
+	int deblocking_filter_control_present_flag;
+	int constrained_intra_pred_flag;
+	int redundant_pic_cnt_present_flag;
+	int transform_8x8_mode_flag;
+} h264_pps_t;
+
+/* ---------------------------------------------------------------- references / DPB (reference h264.h:236-320) */
+enum { REF_UNUSED = 0, REF_SHORT = 1, REF_LONG = 2 };
+
+typedef struct {
+	int16_t in_use;
+	int16_t frame_idx;
+	uint32_t num;  /* frame_num (short) / long-term idx */
+	int32_t poc;
+	int16_t col;   /* index of the co-located motion store attached to this entry (list 1 only) */
+} h264_ref_t;
+
+typedef struct {
+	int poc;
+	int16_t frame_idx;
+	int8_t is_idr;
+	int8_t is_terminal;
+} h264_dpb_elem_t;
+
+typedef struct {
+	int size, max, output, is_ready;
+	h264_dpb_elem_t data[16];
+} h264_dpb_t;
+
+/* co-located motion store of one decoded picture (reference h264d_col_pic_t, h264.h:200-215) */
+typedef struct {
+	int8_t ref[4];          /* ref_idx per 8x8 (-1 intra) */
+	int16_t mv[16][2];      /* raster 4x4 */
+} h264_colmb_t;
+
+typedef struct {
+	int8_t map_col_frameidx[16];
+	h264_colmb_t *mb;       /* [n_mbs] */
+} h264_colpic_t;
+
+/* ---------------------------------------------------------------- per-MB neighbour state */
+enum {
+	MBT_INxN = 0,       /* I4x4 / I8x8 */
+	MBT_I16 = 1,        /* 1..24 */
+	MBT_IPCM = 25,
+	MBT_P16x16 = 26,
+	MBT_P16x8 = 27,
+	MBT_P8x16 = 28,
+	MBT_P8x8 = 29,
+	MBT_P8x8REF0 = 30,
+	MBT_SKIP = 31,      /* P_Skip / B_Skip / B_Direct_16x16 (reference h264.h:77-80) */
+	MBT_B_FIRST = 32,   /* B_L0_16x16 ... */
+	MBT_B8x8 = 53
+};
+
+typedef struct {
+	int8_t type;        /* unified type (reference adjust_mb_type, h264.cpp:9689) ; -1 = not decoded */
+	uint8_t skip;
+	uint8_t t8x8;
+	uint8_t cbp;
+	uint8_t cpm;        /* intra_chroma_pred_mode */
+	uint8_t direct;     /* bit per 8x8 partition coded as direct (or skip / direct16x16: 0xf) */
+	int16_t slice;      /* slice number in the picture */
+	uint32_t cbf;       /* coded_block_flag: 0-15 luma blkIdx, 16 luma DC, 17-18 chroma DC, 19-26 chroma AC */
+	uint8_t nnz[16];    /* TotalCoeff per luma 4x4 blkIdx (capped 15) */
+	uint8_t nnzc[8];    /* chroma AC: Cb 0-3, Cr 0-3 */
+	int8_t ipred[16];   /* Intra4x4PredMode per blkIdx (2 if not intra NxN) */
+	int8_t ref[2][4];   /* ref_idx per 8x8 */
+	int16_t fidx[2][4]; /* frame_idx of the reference per 8x8 (-1 unused) */
+	int16_t mv[2][16][2];
+	uint8_t mvd[2][16][2]; /* |mvd| clipped to 255 */
+} h264_mbinfo_t;
+
+/* ---------------------------------------------------------------- slice header */
+typedef struct {
+	int op;
+	uint32_t arg1, arg2;
+} h264_mmco_t;
+
+typedef struct {
+	int first_mb;
+	int slice_type;     /* 0 P, 1 B, 2 I */
+	int pps_id;
+	uint32_t frame_num;
+	uint32_t prev_frame_num;
+	int idr;
+	int nal_ref_idc;
+	int nal_unit_type;
+	int idr_pic_id;
+	int poc;
+	/* POC state carried across pictures (reference h264d_slice_header union) */
+	uint32_t poc0_lsb, poc0_msb;
+	int32_t delta_poc_bottom;
+	uint32_t poc1_num_offset;
+	int32_t delta_poc[2];
+	uint32_t poc2_prev_frameoffset;
+	int direct_spatial;
+	int num_ref_idx_active[2];
+	int cabac_init_idc;
+	int qp;
+	int disable_deblocking_filter_idc;
+	int alpha_off, beta_off; /* *2 */
+	/* marking */
+	int no_output_of_prior_pics;
+	int long_term_reference_flag;
+	int adaptive_marking;
+	int mmco5;
+	h264_mmco_t mmco[16];
+	/* weighted prediction */
+	int wp_mode;
+	int log2wd[2];
+	int8_t w[2][32][3];
+	int8_t o[2][32][3];
+} h264_slice_t;
+
+/* ---------------------------------------------------------------- decoder context */
+typedef struct h264_dec h264_dec_t;
+
+struct h264_dec {
+	/* input */
+	dec_bits stream_i;
+	dec_bits *stream;
+	int device;
+	int (*header_callback)(void *, void *);
+	void *header_callback_arg;
+	uint8_t *nal;            /* current NAL as RBSP (emulation prevention removed) */
+	size_t nal_len, nal_cap;
+	int nal_pending;         /* a NAL was read but not consumed (new picture detected) */
+	int eos;
+
+	h264_sps_t sps[32];
+	h264_pps_t pps[256];
+	int active_sps;
+
+	/* frames */
+	int num_frames;
+	m2d_frame_t frames[H264D_MAX_FRAME_NUM];
+	int8_t lru[H264D_MAX_FRAME_NUM];
+	int frames_ready;
+	int curr_idx;            /* frame slot of the current picture */
+	h264_ref_t refs[2][16];  /* the two reference arrays (reference h264d_frame_info_t.refs) */
+	h264_dpb_t dpb;
+	int dpb_max_arg;
+
+	/* co-located stores: 16 attached to refs[1][i] + 1 current (reference init_mb_buffer) */
+	h264_colpic_t colpic[17];
+	int curr_col;            /* index into colpic of the current picture's store */
+
+	/* picture geometry / state */
+	int mb_w, mb_h, n_mbs;
+	int mbs_decoded;
+	int slice_num;
+	int in_picture;
+	int last_firstline;      /* picture-final `firstline` (deblock idc 2 quirk) */
+	h264_slice_t sh;
+	h264_mbinfo_t *mbi;      /* [n_mbs] */
+	size_t mbi_cap;
+
+	/* per-slice derived */
+	int8_t map_col_to_list0[16];
+	int16_t dist_scale[16];
+
+	/* records */
+	m2r_backend_t backend;
+	int have_backend;
+	m2r_picture_t *pic;
+	int slice_rec;           /* index of the current slice record */
+
+	/* per-picture deblock parameters per slice number */
+	int8_t slice_idc[1024];
+	int8_t slice_alpha[1024], slice_beta[1024];
+
+	/* CABAC / bit reader of the current slice */
+	h264_bits_t bs;
+	h264_cabac_t cabac;
+	const uint8_t *slice_rbsp, *slice_rbsp_end, *cabac_start;
+	size_t slice_rbsp_bits;     /* bit position of the rbsp_stop_one_bit */
+
+	/* statistics */
+	uint64_t pictures;
+};
+
+/* h264_syntax.c */
+int h264_parse_sps(h264_dec_t *d, h264_bits_t *b);
+int h264_parse_pps(h264_dec_t *d, h264_bits_t *b, size_t rbsp_len);
+int h264_slice_header(h264_dec_t *d, h264_bits_t *b, int nal_unit_type, int nal_ref_idc);
+int h264_picture_begin(h264_dec_t *d);
+int h264_picture_finish(h264_dec_t *d);
+void h264_dpb_init(h264_dpb_t *dpb, int maxsize);
+int h264_dpb_peek(h264_dpb_t *dpb, int bypass);
+int h264_dpb_pop(h264_dpb_t *dpb, int bypass);
+
+/* h264_mb.c */
+int h264_slice_data(h264_dec_t *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1085 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.  A plain-C restatement of the reference decoder's macroblock
+ * reconstruction, consuming the record ABI of include/m2d_recon.h.  Used only by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg, as the checker; it is never linked
+ * into libm2dec_amd.so.
+ *
+ * Parity anchoring: the reference itself is not buildable in this image (its bitio.h includes the
+ * autoconf-generated config.h, which the image lacks), so this restatement is pinned by the
+ * reference outputs recorded in SURVEY.md §8c (fixture F1 per-frame MD5s) — see DESIGN.md.
+ *
+ * Each function cites the reference code it restates (paths under /root/reference/src/lib):
+ *   dequant          h264.cpp:964-1054 (qp_matrix / qp_matrix8x8 incl. the qp<12 truncation),
+ *                    2005-2022 / 11538-11576 (level * qmat at parse)
+ *   DC transforms    h264.cpp:4309-4365 (luma DC, (x+2)>>2), 4387-4404 (chroma DC, >>1)
+ *   4x4 transform    h264.cpp:2145-2197 (SSE2: saturating add), 2199-2269 (chroma, gap 2)
+ *   8x8 transform    h264.cpp:3942-4080 (CLIP255C add; DC-only SWAR when one DC coefficient)
+ *   DC-only SWAR     m2d.h:286-341 (byte-replicated saturating add/sub, Appendix A #17)
+ *   intra 4x4        h264.cpp:2463-2997, 3121-3254 (per-block avail constants)
+ *   intra 8x8        h264.cpp:3301-3929, 4083-4127
+ *   intra 16x16      h264.cpp:3042, 2510-2555, 4224-4304, 4407-4555
+ *   intra chroma     h264.cpp:4559-4706 (NV12)
+ *   PCM              h264.cpp:4708-4761
+ *   luma / chroma MC h264.cpp:4763-6406 (UMV == coordinate clamp)
+ *   bi / weighted    h264.cpp:5298-5318, 6726-7118 (SSE2 int16 saturation, int8 weights)
+ *   deblocking       h264.cpp:10253-10663 (deblock_pb), tables h264vld.h:932-4627 (spec 8.7)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "m2d_recon.h"
+
+static inline int clip255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+static inline int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+static inline int sat16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+static inline int iabs(int v) { return v < 0 ? -v : v; }
+
+/* ======================================================================== dequantisation */
+static const int norm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+static const int norm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                                {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+
+static int scale4(int qp, int x, int y)
+{
+	int cls = ((x & 1) == 0 && (y & 1) == 0) ? 0 : (((x & 1) && (y & 1)) ? 1 : 2);
+	return norm4[qp % 6][cls] << (qp / 6);
+}
+
+static int scale8(int qp, int x, int y)
+{
+	int cls;
+	int sh = qp / 6 - 2;
+	int v;
+	if ((x & 3) == 0 && (y & 3) == 0) cls = 0;
+	else if ((x & 1) && (y & 1)) cls = 1;
+	else if ((x & 3) == 2 && (y & 3) == 2) cls = 2;
+	else if (((x & 3) == 0 && (y & 1)) || ((x & 1) && (y & 3) == 0)) cls = 3;
+	else if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) cls = 4;
+	else cls = 5;
+	v = norm8[qp % 6][cls];
+	return sh >= 0 ? v << sh : v >> (-sh); /* truncation below qp 12: Appendix A #3 */
+}
+
+/* ======================================================================== transforms */
+/* spec 8.5.12.2: rows then columns; returns r_ij = (h + 32) >> 6 */
+static void idct4(const int *c, int *r)
+{
+	int t[16];
+	for (int i = 0; i < 4; ++i) {
+		const int *s = c + i * 4;
+		int e0 = s[0] + s[2], e1 = s[0] - s[2];
+		int e2 = (s[1] >> 1) - s[3], e3 = s[1] + (s[3] >> 1);
+		t[i * 4 + 0] = e0 + e3;
+		t[i * 4 + 1] = e1 + e2;
+		t[i * 4 + 2] = e1 - e2;
+		t[i * 4 + 3] = e0 - e3;
+	}
+	for (int j = 0; j < 4; ++j) {
+		int s0 = t[j], s1 = t[4 + j], s2 = t[8 + j], s3 = t[12 + j];
+		int e0 = s0 + s2, e1 = s0 - s2;
+		int e2 = (s1 >> 1) - s3, e3 = s1 + (s3 >> 1);
+		r[0 + j] = (e0 + e3 + 32) >> 6;
+		r[4 + j] = (e1 + e2 + 32) >> 6;
+		r[8 + j] = (e1 - e2 + 32) >> 6;
+		r[12 + j] = (e0 - e3 + 32) >> 6;
+	}
+}
+
+static void idct8_1d(const int *s, int st, int *o, int ost)
+{
+	int a0 = s[0] + s[4 * st];
+	int a4 = s[0] - s[4 * st];
+	int a2 = (s[2 * st] >> 1) - s[6 * st];
+	int a6 = s[2 * st] + (s[6 * st] >> 1);
+	int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+	int a1 = -s[3 * st] + s[5 * st] - s[7 * st] - (s[7 * st] >> 1);
+	int a3 = s[1 * st] + s[7 * st] - s[3 * st] - (s[3 * st] >> 1);
+	int a5 = -s[1 * st] + s[7 * st] + s[5 * st] + (s[5 * st] >> 1);
+	int a7 = s[3 * st] + s[5 * st] + s[1 * st] + (s[1 * st] >> 1);
+	int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2);
+	int b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+	o[0 * ost] = b0 + b7;
+	o[1 * ost] = b2 + b5;
+	o[2 * ost] = b4 + b3;
+	o[3 * ost] = b6 + b1;
+	o[4 * ost] = b6 - b1;
+	o[5 * ost] = b4 - b3;
+	o[6 * ost] = b2 - b5;
+	o[7 * ost] = b0 - b7;
+}
+
+static void idct8(const int *c, int *r)
+{
+	int t[64], u[64];
+	for (int i = 0; i < 8; ++i) idct8_1d(c + i * 8, 1, t + i * 8, 1);
+	for (int j = 0; j < 8; ++j) idct8_1d(t + j, 8, u + j, 8);
+	for (int k = 0; k < 64; ++k) r[k] = (u[k] + 32) >> 6;
+}
+
+/* m2d.h:286-341: DC-only add through byte replication + per-byte saturation */
+static void dconly_swar(uint8_t *dst, int gap, int stride, int n, int dc)
+{
+	int adj = (dc + 32) >> 6;
+	uint64_t v = (uint64_t)(adj < 0 ? -(int64_t)adj : adj);
+	uint64_t w = (n == 4) ? (uint64_t)(uint32_t)(v * 0x01010101u) : v * 0x0101010101010101ull;
+	for (int y = 0; y < n; ++y)
+		for (int x = 0; x < n; ++x) {
+			int b = (int)((w >> (8 * x)) & 255);
+			uint8_t *p = dst + y * stride + x * gap;
+			*p = (uint8_t)(adj < 0 ? (*p - b < 0 ? 0 : *p - b) : (*p + b > 255 ? 255 : *p + b));
+		}
+}
+
+/* ======================================================================== frame access */
+typedef struct {
+	uint8_t *luma, *chroma;
+	int w, h; /* luma samples; chroma plane is w bytes x h/2 rows, interleaved CbCr */
+} plane_t;
+
+/* ======================================================================== intra prediction */
+/* 4x4 (h264.cpp:2510-2997); avail: 1 left, 2 top, 4 top-right.  Returns without writing when a
+ * mode's required neighbours are missing (the reference returns -1). */
+static void pred4x4(uint8_t *dst, int stride, int mode, int avail)
+{
+	uint8_t *T = dst - stride;
+	int L[4], P[8], tl;
+	for (int i = 0; i < 4; ++i) L[i] = dst[i * stride - 1];
+	for (int i = 0; i < 4; ++i) P[i] = T[i];
+	for (int i = 4; i < 8; ++i) P[i] = (avail & 4) ? T[i] : T[3];
+	tl = T[-1];
+	switch (mode) {
+	case 0: /* vertical */
+		if (!(avail & 2)) return;
+		for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) dst[y * stride + x] = (uint8_t)P[x];
+		break;
+	case 1: /* horizontal */
+		if (!(avail & 1)) return;
+		for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) dst[y * stride + x] = (uint8_t)L[y];
+		break;
+	case 2: { /* DC */
+		int dc;
+		if ((avail & 3) == 3) dc = (P[0] + P[1] + P[2] + P[3] + L[0] + L[1] + L[2] + L[3] + 4) >> 3;
+		else if (avail & 1) dc = (L[0] + L[1] + L[2] + L[3] + 2) >> 2;
+		else if (avail & 2) dc = (P[0] + P[1] + P[2] + P[3] + 2) >> 2;
+		else dc = 128;
+		for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) dst[y * stride + x] = (uint8_t)dc;
+		break;
+	}
+	case 3: /* diagonal down left */
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int v = (x == 3 && y == 3) ? (P[6] + 3 * P[7] + 2) >> 2 : (P[x + y] + 2 * P[x + y + 1] + P[x + y + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 4: /* diagonal down right */
+		if ((avail & 3) != 3) return;
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int v;
+				if (x > y) v = (x - y - 2 >= 0 ? P[x - y - 2] : tl) + 2 * P[x - y - 1] + P[x - y];
+				else if (x < y) v = (y - x - 2 >= 0 ? L[y - x - 2] : tl) + 2 * L[y - x - 1] + L[y - x];
+				else v = P[0] + 2 * tl + L[0];
+				dst[y * stride + x] = (uint8_t)((v + 2) >> 2);
+			}
+		break;
+	case 5: /* vertical right */
+		if ((avail & 3) != 3) return;
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int z = 2 * x - y, v;
+				if (z >= 0 && !(z & 1)) v = ((x - (y >> 1) - 1 >= 0 ? P[x - (y >> 1) - 1] : tl) + P[x - (y >> 1)] + 1) >> 1;
+				else if (z >= 0) v = ((x - (y >> 1) - 2 >= 0 ? P[x - (y >> 1) - 2] : tl) + 2 * (x - (y >> 1) - 1 >= 0 ? P[x - (y >> 1) - 1] : tl) + P[x - (y >> 1)] + 2) >> 2;
+				else if (z == -1) v = (L[0] + 2 * tl + P[0] + 2) >> 2;
+				else v = (L[y - 1] + 2 * L[y - 2] + (y - 3 >= 0 ? L[y - 3] : tl) + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 6: /* horizontal down */
+		if ((avail & 3) != 3) return;
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int z = 2 * y - x, v;
+				if (z >= 0 && !(z & 1)) v = ((y - (x >> 1) - 1 >= 0 ? L[y - (x >> 1) - 1] : tl) + L[y - (x >> 1)] + 1) >> 1;
+				else if (z >= 0) v = ((y - (x >> 1) - 2 >= 0 ? L[y - (x >> 1) - 2] : tl) + 2 * (y - (x >> 1) - 1 >= 0 ? L[y - (x >> 1) - 1] : tl) + L[y - (x >> 1)] + 2) >> 2;
+				else if (z == -1) v = (L[0] + 2 * tl + P[0] + 2) >> 2;
+				else v = (P[x - 1] + 2 * P[x - 2] + (x - 3 >= 0 ? P[x - 3] : tl) + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 7: /* vertical left */
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int i = x + (y >> 1), v;
+				if (!(y & 1)) v = (P[i] + P[i + 1] + 1) >> 1;
+				else v = (P[i] + 2 * P[i + 1] + P[i + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 8: /* horizontal up */
+		if (!(avail & 1)) return;
+		for (int y = 0; y < 4; ++y)
+			for (int x = 0; x < 4; ++x) {
+				int z = x + 2 * y, v;
+				if (z > 5) v = L[3];
+				else if (z == 5) v = (L[2] + 3 * L[3] + 2) >> 2;
+				else if (!(z & 1)) v = (L[y + (x >> 1)] + L[y + (x >> 1) + 1] + 1) >> 1;
+				else v = (L[y + (x >> 1)] + 2 * L[y + (x >> 1) + 1] + L[y + (x >> 1) + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	}
+}
+
+/* 8x8 with reference sample filtering (spec 8.3.2.2); avail: 1 left, 2 top, 4 top-right, 8 top-left */
+static void pred8x8(uint8_t *dst, int stride, int mode, int avail)
+{
+	uint8_t *T = dst - stride;
+	int p[16], l[8], pt[16], lf[8], tl = 0, tlf = 0;
+	int hasL = avail & 1, hasT = avail & 2, hasTR = avail & 4, hasTL = avail & 8;
+	for (int i = 0; i < 8; ++i) l[i] = dst[i * stride - 1];
+	for (int i = 0; i < 8; ++i) p[i] = T[i];
+	for (int i = 8; i < 16; ++i) p[i] = hasTR ? T[i] : T[7];
+	if (hasTL) tl = T[-1];
+	if (hasT) {
+		pt[0] = hasTL ? (tl + 2 * p[0] + p[1] + 2) >> 2 : (3 * p[0] + p[1] + 2) >> 2;
+		for (int x = 1; x < 15; ++x) pt[x] = (p[x - 1] + 2 * p[x] + p[x + 1] + 2) >> 2;
+		pt[15] = (p[14] + 3 * p[15] + 2) >> 2;
+	}
+	if (hasTL) {
+		if (hasT && hasL) tlf = (p[0] + 2 * tl + l[0] + 2) >> 2;
+		else if (hasT) tlf = (3 * tl + p[0] + 2) >> 2;
+		else if (hasL) tlf = (3 * tl + l[0] + 2) >> 2;
+		else tlf = tl;
+	}
+	if (hasL) {
+		lf[0] = hasTL ? (tl + 2 * l[0] + l[1] + 2) >> 2 : (3 * l[0] + l[1] + 2) >> 2;
+		for (int y = 1; y < 7; ++y) lf[y] = (l[y - 1] + 2 * l[y] + l[y + 1] + 2) >> 2;
+		lf[7] = (l[6] + 3 * l[7] + 2) >> 2;
+	}
+#define PT(i) ((i) < 0 ? tlf : pt[i])
+#define LF(i) ((i) < 0 ? tlf : lf[i])
+	switch (mode) {
+	case 0:
+		if (!hasT) return;
+		for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)pt[x];
+		break;
+	case 1:
+		if (!hasL) return;
+		for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)lf[y];
+		break;
+	case 2: {
+		int dc = 0;
+		if (hasT && hasL) {
+			for (int i = 0; i < 8; ++i) dc += pt[i] + lf[i];
+			dc = (dc + 8) >> 4;
+		} else if (hasL) {
+			for (int i = 0; i < 8; ++i) dc += lf[i];
+			dc = (dc + 4) >> 3;
+		} else if (hasT) {
+			for (int i = 0; i < 8; ++i) dc += pt[i];
+			dc = (dc + 4) >> 3;
+		} else {
+			dc = 128;
+		}
+		for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)dc;
+		break;
+	}
+	case 3:
+		if (!hasT) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int v = (x == 7 && y == 7) ? (pt[14] + 3 * pt[15] + 2) >> 2 : (pt[x + y] + 2 * pt[x + y + 1] + pt[x + y + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 4:
+		if (!(hasT && hasL && hasTL)) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int v;
+				if (x > y) v = (PT(x - y - 2) + 2 * PT(x - y - 1) + pt[x - y] + 2) >> 2;
+				else if (x < y) v = (LF(y - x - 2) + 2 * LF(y - x - 1) + lf[y - x] + 2) >> 2;
+				else v = (pt[0] + 2 * tlf + lf[0] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 5:
+		if (!(hasT && hasL && hasTL)) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int z = 2 * x - y, v;
+				if (z >= 0 && !(z & 1)) v = (PT(x - (y >> 1) - 1) + pt[x - (y >> 1)] + 1) >> 1;
+				else if (z >= 0) v = (PT(x - (y >> 1) - 2) + 2 * PT(x - (y >> 1) - 1) + pt[x - (y >> 1)] + 2) >> 2;
+				else if (z == -1) v = (lf[0] + 2 * tlf + pt[0] + 2) >> 2;
+				else v = (LF(y - 2 * x - 1) + 2 * LF(y - 2 * x - 2) + LF(y - 2 * x - 3) + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 6:
+		if (!(hasT && hasL && hasTL)) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int z = 2 * y - x, v;
+				if (z >= 0 && !(z & 1)) v = (LF(y - (x >> 1) - 1) + lf[y - (x >> 1)] + 1) >> 1;
+				else if (z >= 0) v = (LF(y - (x >> 1) - 2) + 2 * LF(y - (x >> 1) - 1) + lf[y - (x >> 1)] + 2) >> 2;
+				else if (z == -1) v = (lf[0] + 2 * tlf + pt[0] + 2) >> 2;
+				else v = (PT(x - 2 * y - 1) + 2 * PT(x - 2 * y - 2) + PT(x - 2 * y - 3) + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 7:
+		if (!hasT) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int i = x + (y >> 1), v;
+				if (!(y & 1)) v = (pt[i] + pt[i + 1] + 1) >> 1;
+				else v = (pt[i] + 2 * pt[i + 1] + pt[i + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	case 8:
+		if (!hasL) return;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) {
+				int z = x + 2 * y, v;
+				if (z > 13) v = lf[7];
+				else if (z == 13) v = (lf[6] + 3 * lf[7] + 2) >> 2;
+				else if (!(z & 1)) v = (lf[y + (x >> 1)] + lf[y + (x >> 1) + 1] + 1) >> 1;
+				else v = (lf[y + (x >> 1)] + 2 * lf[y + (x >> 1) + 1] + lf[y + (x >> 1) + 2] + 2) >> 2;
+				dst[y * stride + x] = (uint8_t)v;
+			}
+		break;
+	}
+#undef PT
+#undef LF
+}
+
+/* 16x16 (h264.cpp:3042, 2510-2555, 4224-4304); avail 1 left, 2 top, 8 top-left */
+static void pred16x16(uint8_t *dst, int stride, int mode, int avail)
+{
+	uint8_t *T = dst - stride;
+	switch (mode) {
+	case 0:
+		if (!(avail & 2)) return;
+		for (int y = 0; y < 16; ++y) memcpy(dst + y * stride, T, 16);
+		break;
+	case 1:
+		if (!(avail & 1)) return;
+		for (int y = 0; y < 16; ++y) memset(dst + y * stride, dst[y * stride - 1], 16);
+		break;
+	case 2: {
+		int st = 0, sl = 0, dc;
+		for (int i = 0; i < 16; ++i) { st += T[i]; sl += dst[i * stride - 1]; }
+		if ((avail & 3) == 3) dc = (st + sl + 16) >> 5;
+		else if (avail & 1) dc = (sl + 8) >> 4;
+		else if (avail & 2) dc = (st + 8) >> 4;
+		else dc = 128;
+		for (int y = 0; y < 16; ++y) memset(dst + y * stride, dc, 16);
+		break;
+	}
+	case 3: {
+		int H = 0, V = 0, a, b, c;
+		for (int i = 0; i < 8; ++i) {
+			H += (i + 1) * (T[8 + i] - T[6 - i]);
+			V += (i + 1) * (dst[(8 + i) * stride - 1] - dst[(6 - i) * stride - 1]);
+		}
+		a = 16 * (dst[15 * stride - 1] + T[15]);
+		b = (5 * H + 32) >> 6;
+		c = (5 * V + 32) >> 6;
+		for (int y = 0; y < 16; ++y)
+			for (int x = 0; x < 16; ++x) dst[y * stride + x] = (uint8_t)clip255((a + b * (x - 7) + c * (y - 7) + 16) >> 5);
+		break;
+	}
+	}
+}
+
+/* NV12 chroma (h264.cpp:4559-4706); gap 2 interleaved, dst points at the component */
+static void predchroma(uint8_t *dst, int stride, int mode, int avail)
+{
+	uint8_t *T = dst - stride;
+#define CT(i) T[(i) * 2]
+#define CL(i) dst[(i) * stride - 2]
+	switch (mode) {
+	case 0: /* DC per 4x4 quadrant (spec 8.3.4.1-3) */
+		for (int blk = 0; blk < 4; ++blk) {
+			int xo = (blk & 1) * 4, yo = (blk >> 1) * 4, st = 0, sl = 0, dc;
+			int ht = (avail & 2) != 0, hl = (avail & 1) != 0;
+			for (int i = 0; i < 4; ++i) { st += CT(xo + i); sl += CL(yo + i); }
+			if (blk == 0 || blk == 3) {
+				if (ht && hl) dc = (st + sl + 4) >> 3;
+				else if (hl) dc = (sl + 2) >> 2;
+				else if (ht) dc = (st + 2) >> 2;
+				else dc = 128;
+			} else if (blk == 1) {
+				if (ht) dc = (st + 2) >> 2;
+				else if (hl) dc = (sl + 2) >> 2;
+				else dc = 128;
+			} else {
+				if (hl) dc = (sl + 2) >> 2;
+				else if (ht) dc = (st + 2) >> 2;
+				else dc = 128;
+			}
+			for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) dst[(yo + y) * stride + (xo + x) * 2] = (uint8_t)dc;
+		}
+		break;
+	case 1:
+		if (!(avail & 1)) return;
+		for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) dst[y * stride + x * 2] = CL(y);
+		break;
+	case 2:
+		if (!(avail & 2)) return;
+		for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) dst[y * stride + x * 2] = CT(x);
+		break;
+	case 3: {
+		int H = 0, V = 0, a, b, c;
+		for (int i = 0; i < 4; ++i) {
+			H += (i + 1) * (CT(4 + i) - CT(2 - i));
+			V += (i + 1) * (CL(4 + i) - CL(2 - i));
+		}
+		a = 16 * (CL(7) + CT(7));
+		b = (34 * H + 32) >> 6;
+		c = (34 * V + 32) >> 6;
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) dst[y * stride + x * 2] = (uint8_t)clip255((a + b * (x - 3) + c * (y - 3) + 16) >> 5);
+		break;
+	}
+	}
+#undef CT
+#undef CL
+}
+
+/* ======================================================================== residual helpers */
+static void add4x4(uint8_t *dst, int stride, int gap, const int *r)
+{
+	for (int y = 0; y < 4; ++y)
+		for (int x = 0; x < 4; ++x) dst[y * stride + x * gap] = (uint8_t)clip255(dst[y * stride + x * gap] + r[y * 4 + x]);
+}
+
+/* luma 4x4 block: dequant (qmat[pos]) + transform + saturating add (h264.cpp:2145-2197) */
+static void luma4x4_residual(uint8_t *dst, int stride, const int16_t *lv, int qp, int dc_present, int dc)
+{
+	int c[16], r[16];
+	for (int k = 0; k < 16; ++k) c[k] = lv[k] * scale4(qp, k & 3, k >> 2);
+	if (dc_present) c[0] = dc;
+	idct4(c, r);
+	add4x4(dst, stride, 1, r);
+}
+
+static int count_nz(const int16_t *lv, int n)
+{
+	int k = 0;
+	for (int i = 0; i < n; ++i) k += lv[i] != 0;
+	return k;
+}
+
+/* 8x8 (h264.cpp:4072-4080): one nonzero DC -> SWAR DC-only, else full transform + CLIP255C */
+static void luma8x8_residual(uint8_t *dst, int stride, const int16_t *lv, int qp)
+{
+	int c[64], r[64];
+	for (int k = 0; k < 64; ++k) c[k] = lv[k] * scale8(qp, k & 7, k >> 3);
+	if (count_nz(lv, 64) == 1 && c[0] != 0) {
+		dconly_swar(dst, 1, stride, 8, c[0]);
+		return;
+	}
+	idct8(c, r);
+	for (int y = 0; y < 8; ++y)
+		for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)clip255(dst[y * stride + x] + r[y * 8 + x]);
+}
+
+/* per-block avail constants of luma_intra4x4_with_residual (h264.cpp:3121-3230) */
+static int avail4x4(int blk, int a)
+{
+	switch (blk) {
+	case 0: return a | ((a & 2) ? 4 : 0);
+	case 1: return a | ((a & 2) ? 5 : 1);
+	case 2: return a | 6;
+	case 3: return 3;
+	case 4: return a | ((a & 2) ? 5 : 1);
+	case 5: return a | 1;
+	case 6: return 7;
+	case 7: return 3;
+	case 8: return a | 6;
+	case 9: return 7;
+	case 10: return a | 6;
+	case 11: return 3;
+	case 12: return 7;
+	case 13: return 3;
+	case 14: return 7;
+	default: return 3;
+	}
+}
+
+/* per-block avail of luma_intra8x8_with_residual (h264.cpp:4093-4118) */
+static int avail8x8(int b, int a)
+{
+	switch (b) {
+	case 0: return (a & ~4) | ((a & 2) * 2);
+	case 1: return (a & ~8) | ((a & 2) * 4) | 1;
+	case 2: return 6 | ((a & 1) * 9);
+	default: return 11;
+	}
+}
+
+static const uint8_t blk_x4[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+static const uint8_t blk_y4[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+
+static inline int popc(uint32_t v) { return __builtin_popcount(v); }
+
+/* chroma residual of one MB (residual_chroma, h264.cpp:2374-2461) */
+static void chroma_residual(uint8_t *cbase, int stride, const m2r_mb_t *m, const int16_t *pool)
+{
+	int ccbp = m->cbp >> 4;
+	uint32_t nz = m->nz;
+	if (!ccbp) return;
+	for (int c = 0; c < 2; ++c) {
+		int qp = m->qpc[c];
+		int dcl[4] = {0, 0, 0, 0}, dc[4];
+		if (nz & M2R_NZ_CDC(c)) {
+			const int16_t *p = pool + m->coef + 16 * 0; /* located below */
+			(void)p;
+		}
+		{
+			/* locate the DC block: everything before it in pool order */
+			uint32_t before = nz & (M2R_NZ_CDC(c) - 1);
+			int off = 0;
+			/* luma DC (16), luma blocks (16 or 64 each), chroma DC Cb (4) */
+			off += (before & M2R_NZ_LUMA_DC) ? 16 : 0;
+			off += popc(before & 0xffffu) * ((m->flags & M2R_FLAG_T8x8) ? 64 : 16);
+			if (c == 1 && (nz & M2R_NZ_CDC(0))) off += 4;
+			if (nz & M2R_NZ_CDC(c)) {
+				const int16_t *p = pool + m->coef + off;
+				int s = scale4(qp, 0, 0);
+				int c0 = p[0] * s, c1 = p[1] * s, c2 = p[2] * s, c3 = p[3] * s;
+				dcl[0] = (c0 + c1 + c2 + c3) >> 1;
+				dcl[1] = (c0 - c1 + c2 - c3) >> 1;
+				dcl[2] = (c0 + c1 - c2 - c3) >> 1;
+				dcl[3] = (c0 - c1 - c2 + c3) >> 1;
+			}
+		}
+		for (int b = 0; b < 4; ++b) dc[b] = dcl[b];
+		for (int b = 0; b < 4; ++b) {
+			uint8_t *dst = cbase + c + (b >> 1) * 4 * stride + (b & 1) * 8;
+			uint32_t bit = M2R_NZ_CAC(c, b);
+			if (ccbp >= 2 && (nz & bit)) {
+				int off = 0;
+				uint32_t before = nz & (bit - 1);
+				int cc[16], r[16];
+				const int16_t *p;
+				off += (before & M2R_NZ_LUMA_DC) ? 16 : 0;
+				off += popc(before & 0xffffu) * ((m->flags & M2R_FLAG_T8x8) ? 64 : 16);
+				off += popc(before & (M2R_NZ_CDC(0) | M2R_NZ_CDC(1))) * 4;
+				off += popc(before & (0xffu << 19)) * 16;
+				p = pool + m->coef + off;
+				for (int k = 0; k < 16; ++k) cc[k] = p[k] * scale4(qp, k & 3, k >> 2);
+				cc[0] = dc[b];
+				idct4(cc, r);
+				add4x4(dst, stride, 2, r);
+			} else {
+				/* ac4x4transform_dconly_chroma: CLIP255C(p + ((dc + 32) >> 6)) */
+				int adj = (dc[b] + 32) >> 6;
+				if (adj)
+					for (int y = 0; y < 4; ++y)
+						for (int x = 0; x < 4; ++x) dst[y * stride + x * 2] = (uint8_t)clip255(dst[y * stride + x * 2] + adj);
+			}
+		}
+	}
+}
+
+/* offset (int16 units) of coded luma block `bit` inside the MB's pool segment */
+static int luma_off(const m2r_mb_t *m, int bit)
+{
+	uint32_t before = m->nz & ((1u << bit) - 1);
+	int off = (m->nz & M2R_NZ_LUMA_DC) ? 16 : 0;
+	return off + popc(before & 0xffffu) * ((m->flags & M2R_FLAG_T8x8) ? 64 : 16);
+}
+
+static void intra_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, int mbx, int mby)
+{
+	int stride = f->w;
+	uint8_t *luma = f->luma + (mby * 16) * stride + mbx * 16;
+	uint8_t *chroma = f->chroma + (mby * 8) * stride + mbx * 16;
+	const int16_t *pool = pic->coef;
+	int qp = m->qpy;
+	predchroma(chroma, stride, m->chroma_mode, m->avail_chroma);
+	predchroma(chroma + 1, stride, m->chroma_mode, m->avail_chroma);
+	if (m->kind == M2R_MB_I4x4) {
+		for (int blk = 0; blk < 16; ++blk) {
+			uint8_t *dst = luma + blk_y4[blk] * 4 * stride + blk_x4[blk] * 4;
+			int mode = (m->ipred[blk >> 3] >> (4 * (blk & 7))) & 15;
+			pred4x4(dst, stride, mode, avail4x4(blk, m->avail_luma));
+			if (m->nz & M2R_NZ_LUMA(blk)) luma4x4_residual(dst, stride, pool + m->coef + luma_off(m, blk), qp, 0, 0);
+		}
+	} else if (m->kind == M2R_MB_I8x8) {
+		for (int b = 0; b < 4; ++b) {
+			uint8_t *dst = luma + (b >> 1) * 8 * stride + (b & 1) * 8;
+			int mode = (m->ipred[0] >> (4 * b)) & 15;
+			pred8x8(dst, stride, mode, avail8x8(b, m->avail_luma));
+			if (m->nz & M2R_NZ_LUMA(b * 4)) luma8x8_residual(dst, stride, pool + m->coef + luma_off(m, b * 4), qp);
+		}
+	} else {
+		/* Intra16x16 (h264.cpp:4407-4555) */
+		int dc[16];
+		pred16x16(luma, stride, m->pred_mode, m->avail_luma);
+		memset(dc, 0, sizeof(dc));
+		if (m->nz & M2R_NZ_LUMA_DC) {
+			const int16_t *p = pool + m->coef;
+			int s = scale4(qp, 0, 0), c[16], t[16];
+			for (int k = 0; k < 16; ++k) c[k] = p[k] * s;
+			/* 4x4 Hadamard, rows then columns, (x + 2) >> 2; c is raster over the 4x4 DC grid */
+			for (int i = 0; i < 4; ++i) {
+				int *r = c + i * 4;
+				int a0 = r[0] + r[1], a1 = r[0] - r[1], a2 = r[2] + r[3], a3 = r[2] - r[3];
+				t[i * 4 + 0] = a0 + a2;
+				t[i * 4 + 1] = a1 + a3;
+				t[i * 4 + 2] = a1 - a3;
+				t[i * 4 + 3] = a0 - a2;
+			}
+			for (int j = 0; j < 4; ++j) {
+				int a0 = t[j] + t[4 + j], a1 = t[j] - t[4 + j], a2 = t[8 + j] + t[12 + j], a3 = t[8 + j] - t[12 + j];
+				c[j] = (a0 + a2 + 2) >> 2;
+				c[4 + j] = (a1 + a3 + 2) >> 2;
+				c[8 + j] = (a1 - a3 + 2) >> 2;
+				c[12 + j] = (a0 - a2 + 2) >> 2;
+			}
+			for (int k = 0; k < 16; ++k) dc[k] = c[k];
+		}
+		for (int blk = 0; blk < 16; ++blk) {
+			int bx = blk_x4[blk], by = blk_y4[blk];
+			uint8_t *dst = luma + by * 4 * stride + bx * 4;
+			int d = dc[by * 4 + bx];
+			if ((m->cbp & 15) && (m->nz & M2R_NZ_LUMA(blk))) {
+				luma4x4_residual(dst, stride, pool + m->coef + luma_off(m, blk), qp, 1, d);
+			} else if ((m->cbp & 15) || (m->nz & M2R_NZ_LUMA_DC)) {
+				dconly_swar(dst, 1, stride, 4, d);
+			}
+		}
+	}
+	chroma_residual(chroma, stride, m, pool);
+}
+
+/* ======================================================================== motion compensation */
+static inline int pixc(const uint8_t *p, int stride, int w, int h, int x, int y)
+{
+	x = clip3(0, w - 1, x);
+	y = clip3(0, h - 1, y);
+	return p[y * stride + x];
+}
+
+/* one luma sample at integer (x, y) + fraction (fx, fy) quarter units (spec 8.4.2.2.1) */
+static int luma_sample(const uint8_t *ref, int stride, int w, int h, int x, int y, int fx, int fy)
+{
+#define P(dx, dy) pixc(ref, stride, w, h, x + (dx), y + (dy))
+#define TAPH(dy, dx0) (P(dx0 - 2, dy) - 5 * P(dx0 - 1, dy) + 20 * P(dx0, dy) + 20 * P(dx0 + 1, dy) - 5 * P(dx0 + 2, dy) + P(dx0 + 3, dy))
+#define TAPV(dx, dy0) (P(dx, dy0 - 2) - 5 * P(dx, dy0 - 1) + 20 * P(dx, dy0) + 20 * P(dx, dy0 + 1) - 5 * P(dx, dy0 + 2) + P(dx, dy0 + 3))
+	int G = P(0, 0);
+	int b1, h1, b, hh, j1, j, s, m;
+	if (fx == 0 && fy == 0) return G;
+	b1 = TAPH(0, 0);
+	b = clip255((b1 + 16) >> 5);
+	h1 = TAPV(0, 0);
+	hh = clip255((h1 + 16) >> 5);
+	{
+		int t[6];
+		for (int k = 0; k < 6; ++k) t[k] = TAPH(k - 2, 0);
+		j1 = t[0] - 5 * t[1] + 20 * t[2] + 20 * t[3] - 5 * t[4] + t[5];
+		j = clip255((j1 + 512) >> 10);
+	}
+	s = clip255((TAPH(1, 0) + 16) >> 5);
+	m = clip255((TAPV(1, 0) + 16) >> 5);
+	switch (fy * 4 + fx) {
+	case 1: return (G + b + 1) >> 1;
+	case 2: return b;
+	case 3: return (b + P(1, 0) + 1) >> 1;
+	case 4: return (G + hh + 1) >> 1;
+	case 5: return (b + hh + 1) >> 1;
+	case 6: return (b + j + 1) >> 1;
+	case 7: return (b + m + 1) >> 1;
+	case 8: return hh;
+	case 9: return (hh + j + 1) >> 1;
+	case 10: return j;
+	case 11: return (j + m + 1) >> 1;
+	case 12: return (hh + P(0, 1) + 1) >> 1;
+	case 13: return (hh + s + 1) >> 1;
+	case 14: return (j + s + 1) >> 1;
+	default: return (m + s + 1) >> 1;
+	}
+#undef P
+#undef TAPH
+#undef TAPV
+}
+
+/* predict luma 4x4 + chroma 2x2 (both components) of one list into l[16], cb[4], cr[4] */
+static void mc_block(const plane_t *ref, int bx, int by, const int16_t *mv, int *l, int *cb, int *cr)
+{
+	int w = ref->w, h = ref->h, stride = ref->w;
+	int mx = mv[0], my = mv[1];
+	int fx = mx & 3, fy = my & 3;
+	int ix = bx + (mx >> 2), iy = by + (my >> 2);
+	for (int y = 0; y < 4; ++y)
+		for (int x = 0; x < 4; ++x) l[y * 4 + x] = luma_sample(ref->luma, stride, w, h, ix + x, iy + y, fx, fy);
+	{
+		int cw = w / 2, ch = h / 2;
+		int cx0 = bx / 2 + (mx >> 3), cy0 = by / 2 + (my >> 3);
+		int dx = mx & 7, dy = my & 7;
+		for (int c = 0; c < 2; ++c) {
+			int *o = c ? cr : cb;
+			for (int y = 0; y < 2; ++y)
+				for (int x = 0; x < 2; ++x) {
+					int xa = clip3(0, cw - 1, cx0 + x), xb = clip3(0, cw - 1, cx0 + x + 1);
+					int ya = clip3(0, ch - 1, cy0 + y), yb = clip3(0, ch - 1, cy0 + y + 1);
+					const uint8_t *cp = ref->chroma + c;
+					int A = cp[ya * stride + xa * 2], B = cp[ya * stride + xb * 2];
+					int C = cp[yb * stride + xa * 2], D = cp[yb * stride + xb * 2];
+					o[y * 2 + x] = ((8 - dx) * (8 - dy) * A + dx * (8 - dy) * B + (8 - dx) * dy * C + dx * dy * D + 32) >> 6;
+				}
+		}
+	}
+}
+
+static int wp_uni(int p, int w, int o, int shift)
+{
+	int rnd = shift ? 1 << (shift - 1) : 0;
+	return clip255(((p * w + rnd) >> shift) + o);
+}
+
+/* add_bidir_weighted_type1 SSE2 (h264.cpp:6893-6949): int16 saturating adds */
+static int wp_bi_explicit(int p0, int p1, int w0, int w1, int o0, int o1, int shift)
+{
+	int t = sat16(p0 * w0 + (1 << shift));
+	t = sat16(t + p1 * w1);
+	t >>= shift + 1;
+	t = sat16(t + ((o0 + o1 + 1) >> 1));
+	return clip255(t);
+}
+
+/* add_bidir_weighted_type2 SSE2 (h264.cpp:7027-7066) */
+static int wp_bi_implicit(int p0, int p1, int w0, int w1)
+{
+	int t = sat16(p0 * w0 + 32);
+	t = sat16(t + p1 * w1);
+	return clip255(t >> 6);
+}
+
+static void inter_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, const plane_t *frames, int mbx, int mby)
+{
+	const m2r_inter_t *it = &pic->inter[m->inter];
+	const m2r_slice_t *sl = &pic->slice[m->slice];
+	int stride = f->w;
+	for (int b = 0; b < 16; ++b) {
+		int bx = b & 3, by = b >> 2, b8 = (by >> 1) * 2 + (bx >> 1);
+		int L[2][16], CB[2][4], CR[2][4];
+		int use[2];
+		int px = mbx * 16 + bx * 4, py = mby * 16 + by * 4;
+		uint8_t *dl = f->luma + py * stride + px;
+		uint8_t *dc = f->chroma + (py / 2) * stride + px;
+		for (int lx = 0; lx < 2; ++lx) {
+			int slot = it->slot[lx][b8];
+			use[lx] = slot >= 0;
+			if (use[lx]) mc_block(&frames[slot], px, py, it->mv[lx][b], L[lx], CB[lx], CR[lx]);
+		}
+		if (sl->wp_mode == M2R_WP_EXPLICIT) {
+			if (use[0] && use[1]) {
+				int r0 = it->refidx[0][b8], r1 = it->refidx[1][b8];
+				for (int k = 0; k < 16; ++k)
+					dl[(k >> 2) * stride + (k & 3)] = (uint8_t)wp_bi_explicit(L[0][k], L[1][k], sl->w[0][r0][0], sl->w[1][r1][0], sl->o[0][r0][0], sl->o[1][r1][0], sl->log2wd[0]);
+				for (int k = 0; k < 4; ++k) {
+					dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)wp_bi_explicit(CB[0][k], CB[1][k], sl->w[0][r0][1], sl->w[1][r1][1], sl->o[0][r0][1], sl->o[1][r1][1], sl->log2wd[1]);
+					dc[(k >> 1) * stride + (k & 1) * 2 + 1] = (uint8_t)wp_bi_explicit(CR[0][k], CR[1][k], sl->w[0][r0][2], sl->w[1][r1][2], sl->o[0][r0][2], sl->o[1][r1][2], sl->log2wd[1]);
+				}
+			} else {
+				int lx = use[0] ? 0 : 1;
+				int r = it->refidx[lx][b8];
+				for (int k = 0; k < 16; ++k)
+					dl[(k >> 2) * stride + (k & 3)] = (uint8_t)wp_uni(L[lx][k], sl->w[lx][r][0], sl->o[lx][r][0], sl->log2wd[0]);
+				for (int k = 0; k < 4; ++k) {
+					dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)wp_uni(CB[lx][k], sl->w[lx][r][1], sl->o[lx][r][1], sl->log2wd[1]);
+					dc[(k >> 1) * stride + (k & 1) * 2 + 1] = (uint8_t)wp_uni(CR[lx][k], sl->w[lx][r][2], sl->o[lx][r][2], sl->log2wd[1]);
+				}
+			}
+		} else if (use[0] && use[1]) {
+			if (sl->wp_mode == M2R_WP_IMPLICIT) {
+				int r0 = it->refidx[0][b8], r1 = it->refidx[1][b8];
+				int w0 = sl->iw[r0][r1][0], w1 = sl->iw[r0][r1][1];
+				for (int k = 0; k < 16; ++k) dl[(k >> 2) * stride + (k & 3)] = (uint8_t)wp_bi_implicit(L[0][k], L[1][k], w0, w1);
+				for (int k = 0; k < 4; ++k) {
+					dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)wp_bi_implicit(CB[0][k], CB[1][k], w0, w1);
+					dc[(k >> 1) * stride + (k & 1) * 2 + 1] = (uint8_t)wp_bi_implicit(CR[0][k], CR[1][k], w0, w1);
+				}
+			} else {
+				for (int k = 0; k < 16; ++k) dl[(k >> 2) * stride + (k & 3)] = (uint8_t)((L[0][k] + L[1][k] + 1) >> 1);
+				for (int k = 0; k < 4; ++k) {
+					dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)((CB[0][k] + CB[1][k] + 1) >> 1);
+					dc[(k >> 1) * stride + (k & 1) * 2 + 1] = (uint8_t)((CR[0][k] + CR[1][k] + 1) >> 1);
+				}
+			}
+		} else {
+			int lx = use[0] ? 0 : 1;
+			for (int k = 0; k < 16; ++k) dl[(k >> 2) * stride + (k & 3)] = (uint8_t)L[lx][k];
+			for (int k = 0; k < 4; ++k) {
+				dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)CB[lx][k];
+				dc[(k >> 1) * stride + (k & 1) * 2 + 1] = (uint8_t)CR[lx][k];
+			}
+		}
+	}
+	/* luma residual (residual_luma_inter4x4 / 8x8, h264.cpp:6421-6580) */
+	{
+		uint8_t *luma = f->luma + (mby * 16) * stride + mbx * 16;
+		uint8_t *chroma = f->chroma + (mby * 8) * stride + mbx * 16;
+		if (m->flags & M2R_FLAG_T8x8) {
+			for (int b = 0; b < 4; ++b)
+				if (m->nz & M2R_NZ_LUMA(b * 4))
+					luma8x8_residual(luma + (b >> 1) * 8 * stride + (b & 1) * 8, stride, pic->coef + m->coef + luma_off(m, b * 4), m->qpy);
+		} else {
+			for (int blk = 0; blk < 16; ++blk)
+				if (m->nz & M2R_NZ_LUMA(blk))
+					luma4x4_residual(luma + blk_y4[blk] * 4 * stride + blk_x4[blk] * 4, stride, pic->coef + m->coef + luma_off(m, blk), m->qpy, 0, 0);
+		}
+		chroma_residual(chroma, stride, m, pic->coef);
+	}
+}
+
+static void pcm_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, int mbx, int mby)
+{
+	const uint8_t *s = (const uint8_t *)(pic->coef + m->coef);
+	int stride = f->w;
+	uint8_t *luma = f->luma + (mby * 16) * stride + mbx * 16;
+	uint8_t *chroma = f->chroma + (mby * 8) * stride + mbx * 16;
+	for (int y = 0; y < 16; ++y) memcpy(luma + y * stride, s + y * 16, 16);
+	for (int c = 0; c < 2; ++c)
+		for (int y = 0; y < 8; ++y)
+			for (int x = 0; x < 8; ++x) chroma[y * stride + x * 2 + c] = s[256 + c * 64 + y * 8 + x];
+}
+
+/* ======================================================================== deblocking (spec 8.7) */
+static const uint8_t ALPHA[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 5, 6, 7, 8, 9, 10, 12, 13, 15, 17, 20, 22, 25, 28,
+                                  32, 36, 40, 45, 50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+static const uint8_t BETA[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 6, 6, 7, 7, 8, 8,
+                                 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+static const uint8_t TC0[52][3] = {
+	{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+	{0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1},
+	{0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2},
+	{1, 1, 2}, {1, 2, 3}, {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4}, {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6},
+	{4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11}, {6, 8, 13}, {7, 10, 14}, {8, 11, 16}, {9, 12, 18}, {10, 13, 20},
+	{11, 15, 23}, {13, 17, 25}};
+
+/* filter one line of samples across an edge: q0 at s[0], p0 at s[-d]; luma selects the 3-tap paths */
+static void filter_line(uint8_t *s, int d, int bs, int alpha, int beta, int ia, int luma)
+{
+	int p0 = s[-d], p1 = s[-2 * d], q0 = s[0], q1 = s[d];
+	if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+	if (bs < 4) {
+		int tc0 = TC0[ia][bs - 1], tc, delta;
+		if (luma) {
+			int p2 = s[-3 * d], q2 = s[2 * d];
+			int ap = iabs(p2 - p0) < beta, aq = iabs(q2 - q0) < beta;
+			tc = tc0 + ap + aq;
+			if (ap) s[-2 * d] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+			if (aq) s[d] = (uint8_t)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+		} else {
+			tc = tc0 + 1;
+		}
+		delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+		s[-d] = (uint8_t)clip255(p0 + delta);
+		s[0] = (uint8_t)clip255(q0 - delta);
+	} else if (luma) {
+		int p2 = s[-3 * d], q2 = s[2 * d], p3 = s[-4 * d], q3 = s[3 * d];
+		int small = iabs(p0 - q0) < ((alpha >> 2) + 2);
+		if (iabs(p2 - p0) < beta && small) {
+			s[-d] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+			s[-2 * d] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
+			s[-3 * d] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+		} else {
+			s[-d] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+		}
+		if (iabs(q2 - q0) < beta && small) {
+			s[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+			s[d] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
+			s[2 * d] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+		} else {
+			s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+		}
+	} else {
+		s[-d] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+		s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+	}
+}
+
+/* AlphaBeta (h264.cpp:10253-10258): indexA/B = min(qp + offset, 51); alpha 0 below 16 */
+static int ab_index(int qp, int off)
+{
+	int v = qp + off;
+	return v > 51 ? 51 : (v < 0 ? 0 : v);
+}
+
+/* one edge: dir 0 = vertical edge (filter across columns), dir 1 = horizontal; e = edge index
+ * bs4: strong edge; str: 2-bit bS per 4-sample luma segment */
+static void filter_edge(plane_t *f, int mbx, int mby, int dir, int e, uint32_t str, int bs4, int qpl, const int *qpc, int ao, int bo, int chroma_only)
+{
+	int stride = f->w;
+	if (!chroma_only) {
+		int ia = ab_index(qpl, ao), ib = ab_index(qpl, bo);
+		int alpha = ALPHA[ia], beta = BETA[ib];
+		uint8_t *base = f->luma + (mby * 16) * stride + mbx * 16;
+		for (int k = 0; k < 16; ++k) {
+			int bs = bs4 ? 4 : (int)((str >> ((k >> 2) * 2)) & 3);
+			uint8_t *s;
+			if (!bs) continue;
+			s = dir == 0 ? base + k * stride + e * 4 : base + (e * 4) * stride + k;
+			filter_line(s, dir == 0 ? 1 : stride, bs, alpha, beta, ia, 1);
+		}
+	}
+	if (e == 0 || e == 2) {
+		for (int c = 0; c < 2; ++c) {
+			int ia = ab_index(qpc[c], ao), ib = ab_index(qpc[c], bo);
+			int alpha = ALPHA[ia], beta = BETA[ib];
+			uint8_t *base = f->chroma + (mby * 8) * stride + mbx * 16 + c;
+			for (int k = 0; k < 8; ++k) {
+				int bs = bs4 ? 4 : (int)((str >> ((k >> 1) * 2)) & 3);
+				uint8_t *s;
+				if (!bs) continue;
+				s = dir == 0 ? base + k * stride + (e * 2) * 2 : base + (e * 2) * stride + k * 2;
+				filter_line(s, dir == 0 ? 2 : stride, bs, alpha, beta, ia, 0);
+			}
+		}
+	}
+}
+
+/* deblock_pb (h264.cpp:10540-10663): MB raster order; per MB left edge, inner vertical, top edge,
+ * inner horizontal; chroma inner edge uses luma edge 2 strengths */
+static void deblock_picture(const m2r_picture_t *pic, plane_t *f)
+{
+	int W = pic->width_mbs, H = pic->height_mbs;
+	for (int mby = 0; mby < H; ++mby)
+		for (int mbx = 0; mbx < W; ++mbx) {
+			const m2r_deblock_t *q = &pic->dbk[mby * W + mbx];
+			int qpc[2];
+			if (q->flags & M2R_DBK_OFF) continue;
+			for (int dir = 0; dir < 2; ++dir) {
+				uint32_t str = dir ? q->bs_h : q->bs_v;
+				int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
+				int bs4_flag = dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
+				if ((q->flags & edge_flag) && (str & 255)) {
+					const m2r_deblock_t *p = dir ? q - W : q - 1;
+					int qpl = (q->qpy + p->qpy + 1) >> 1;
+					qpc[0] = (q->qpc[0] + p->qpc[0] + 1) >> 1;
+					qpc[1] = (q->qpc[1] + p->qpc[1] + 1) >> 1;
+					filter_edge(f, mbx, mby, dir, 0, str & 255, (q->flags & bs4_flag) != 0, qpl, qpc, q->alpha_off, q->beta_off, 0);
+				}
+				if (str & ~255u) {
+					qpc[0] = q->qpc[0];
+					qpc[1] = q->qpc[1];
+					for (int e = 1; e < 4; ++e) {
+						uint32_t s = (str >> (8 * e)) & 255;
+						if (s) filter_edge(f, mbx, mby, dir, e, s, 0, q->qpy, qpc, q->alpha_off, q->beta_off, 1 - 1);
+					}
+				}
+			}
+		}
+}
+
+/* ======================================================================== picture / back end */
+void oracle_recon_picture(const m2r_picture_t *pic, const m2d_frame_t *frames, int nframes)
+{
+	plane_t fr[64];
+	int W = pic->width_mbs, H = pic->height_mbs;
+	plane_t *cur;
+	for (int i = 0; i < nframes && i < 64; ++i) {
+		fr[i].luma = frames[i].luma;
+		fr[i].chroma = frames[i].chroma;
+		fr[i].w = W * 16;
+		fr[i].h = H * 16;
+	}
+	cur = &fr[pic->slot];
+	for (int mby = 0; mby < H; ++mby)
+		for (int mbx = 0; mbx < W; ++mbx) {
+			const m2r_mb_t *m = &pic->mb[mby * W + mbx];
+			if (m->kind == M2R_MB_INTER) inter_mb(pic, m, cur, fr, mbx, mby);
+			else if (m->kind == M2R_MB_PCM) pcm_mb(pic, m, cur, mbx, mby);
+			else intra_mb(pic, m, cur, mbx, mby);
+		}
+	if (pic->deblock) deblock_picture(pic, cur);
+}
+
+typedef struct {
+	m2d_frame_t frames[64];
+	int n;
+	m2r_picture_t pic;
+	void *mem;
+	size_t mem_size;
+} oracle_be_t;
+
+static int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
+{
+	oracle_be_t *b = (oracle_be_t *)self;
+	(void)width;
+	(void)height;
+	b->n = n > 64 ? 64 : n;
+	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)b->n);
+	return 0;
+}
+
+static m2r_picture_t *be_acquire(void *self, int wm, int hm)
+{
+	oracle_be_t *b = (oracle_be_t *)self;
+	int n = wm * hm;
+	size_t need = (size_t)n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t) + sizeof(m2r_inter_t) + 416 * sizeof(int16_t)) +
+	              256 * sizeof(m2r_slice_t) + 4096;
+	if (need > b->mem_size) {
+		free(b->mem);
+		b->mem = malloc(need);
+		b->mem_size = need;
+		if (!b->mem) return NULL;
+	}
+	{
+		uint8_t *p = (uint8_t *)b->mem;
+		m2r_picture_t *pic = &b->pic;
+		memset(pic, 0, sizeof(*pic));
+		pic->width_mbs = wm;
+		pic->height_mbs = hm;
+		pic->mb = (m2r_mb_t *)p; p += (size_t)n * sizeof(m2r_mb_t);
+		pic->dbk = (m2r_deblock_t *)p; p += (size_t)n * sizeof(m2r_deblock_t);
+		pic->slice = (m2r_slice_t *)p; p += 256 * sizeof(m2r_slice_t);
+		pic->inter = (m2r_inter_t *)p; p += (size_t)n * sizeof(m2r_inter_t);
+		pic->coef = (int16_t *)p;
+		pic->cap_slices = 256;
+		pic->cap_inter = n;
+		pic->cap_coef = n * 416;
+		return pic;
+	}
+}
+
+static int be_submit(void *self, m2r_picture_t *pic)
+{
+	oracle_be_t *b = (oracle_be_t *)self;
+	oracle_recon_picture(pic, b->frames, b->n);
+	return 0;
+}
+
+static int be_sync(void *self, int slot)
+{
+	(void)self;
+	(void)slot;
+	return 0;
+}
+
+static void be_destroy(void *self)
+{
+	oracle_be_t *b = (oracle_be_t *)self;
+	free(b->mem);
+	free(b);
+}
+
+int oracle_backend_create(m2r_backend_t *out)
+{
+	oracle_be_t *b = (oracle_be_t *)calloc(1, sizeof(oracle_be_t));
+	if (!b) return -1;
+	out->self = b;
+	out->set_frames = be_set_frames;
+	out->acquire = be_acquire;
+	out->submit = be_submit;
+	out->sync_frame = be_sync;
+	out->destroy = be_destroy;
+	return 0;
+}

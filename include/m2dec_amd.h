@@ -27,7 +27,8 @@ typedef struct {
 	int pad;
 } m2dec_amd_stats_t;
 
-/* Use `be` instead of the default HIP back end for this decoder context (call after init). */
+/* Use `be` instead of the default HIP back end for this decoder context (call after init).
+ * The context takes ownership: m2dec_amd_h264_release() calls be->destroy. */
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
 /* GPU ordinal used by the default back end (call after init, before the first SPS). */
 int m2dec_amd_h264_set_device(void *ctx, int device);
@@ -35,7 +36,8 @@ int m2dec_amd_h264_set_device(void *ctx, int device);
 void m2dec_amd_h264_release(void *ctx);
 
 /* Decode a whole Annex-B stream exactly like `h264dec` (m2decoder.h:132-157 output loop).
- * on_frame receives every output frame in output order.  backend may be NULL (HIP back end).
+ * on_frame receives every output frame in output order.  backend may be NULL (a HIP back end is
+ * created on `device` and destroyed at the end); a non-NULL backend is borrowed, not destroyed.
  * Returns the number of frames output, or -1 on error. */
 int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device,
                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,

@@ -1,0 +1,192 @@
+"""m2dec_amd — MI355X (gfx950) macroblock-reconstruction back end for the m2dec H.264 decoder.
+
+Host-side mirror of the reference's decoder API (``m2d_func_table_t h264d_func``,
+/root/reference/src/lib/m2d.h:66-75, h264.cpp:12057-12068) and of its stream driver
+(src/app/h264dec.cpp + m2decoder.h), bound over ctypes to ``m2dec_amd/lib/libm2dec_amd.so``.
+
+The product path is: host C parser (CABAC/CAVLC/MV/DPB) -> per-picture records (include/m2d_recon.h)
+-> hand-written HIP kernels (m2dec_amd/csrc/hip/recon_hip.hip) -> NV12 frames in the caller's host
+buffers.  There is no CPU reconstruction in this package: ``decode_stream`` without an explicit
+back end uses the HIP back end and raises if no gfx950 device is usable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Callable, List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libm2dec_amd.so")
+
+__all__ = [
+    "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",
+    "decode_stream", "frame_md5", "frame_nv12", "H264Decoder",
+]
+
+
+class Frame(ctypes.Structure):
+    """m2d_frame_t (reference m2d.h:35-42)."""
+    _fields_ = [("luma", ctypes.c_void_p), ("chroma", ctypes.c_void_p), ("id", ctypes.c_void_p),
+                ("cnt", ctypes.c_int32), ("width", ctypes.c_int16), ("height", ctypes.c_int16),
+                ("crop", ctypes.c_int16 * 4)]
+
+
+class Info(ctypes.Structure):
+    """m2d_info_t (reference m2d.h:44-50)."""
+    _fields_ = [("src_width", ctypes.c_int16), ("src_height", ctypes.c_int16), ("disp_width", ctypes.c_int16),
+                ("disp_height", ctypes.c_int16), ("frame_num", ctypes.c_int16), ("crop", ctypes.c_int16 * 4),
+                ("additional_size", ctypes.c_int)]
+
+
+class Backend(ctypes.Structure):
+    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy."""
+    _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("acquire", ctypes.c_void_p),
+                ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("frames_out", ctypes.c_int), ("pictures", ctypes.c_int), ("last_error", ctypes.c_int),
+                ("pad", ctypes.c_int)]
+
+
+class HipTiming(ctypes.Structure):
+    """m2dec_amd_hip_timing_t (include/m2dec_amd.h)."""
+    _fields_ = [("inter_us", ctypes.c_double), ("intra_us", ctypes.c_double), ("deblock_us", ctypes.c_double),
+                ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("pictures", ctypes.c_int64),
+                ("inter_launches", ctypes.c_int64), ("intra_launches", ctypes.c_int64),
+                ("deblock_launches", ctypes.c_int64), ("record_bytes", ctypes.c_int64),
+                ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+ON_FRAME = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Frame))
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libm2dec_amd.so (built in-tree by ``make`` / ``__graft_entry__.build()``)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"m2dec_amd: {LIB_PATH} is not built (run `make` or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        L.m2dec_amd_decode_stream.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend), ctypes.c_int,
+                                              ON_FRAME, ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.m2dec_amd_decode_stream.restype = ctypes.c_int
+        L.m2dec_amd_hip_backend_create.argtypes = [ctypes.POINTER(Backend), ctypes.c_int]
+        L.m2dec_amd_hip_backend_create.restype = ctypes.c_int
+        L.m2dec_amd_hip_available.argtypes = []
+        L.m2dec_amd_hip_available.restype = ctypes.c_int
+        L.m2dec_amd_hip_backend_timing.argtypes = [ctypes.POINTER(Backend), ctypes.POINTER(HipTiming)]
+        L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
+        L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
+        L.m2dec_amd_frame_md5.restype = None
+        _lib = L
+    return _lib
+
+
+def hip_available() -> bool:
+    return bool(lib().m2dec_amd_hip_available())
+
+
+def _call_destroy(be: Backend) -> None:
+    if be.destroy:
+        ctypes.CFUNCTYPE(None, ctypes.c_void_p)(be.destroy)(be.self)
+        be.destroy = None
+
+
+class HipBackend:
+    """The gfx950 reconstruction back end (m2dec_amd_hip_backend_create).  Raises if unavailable."""
+
+    def __init__(self, device: int = 0):
+        self.be = Backend()
+        if lib().m2dec_amd_hip_backend_create(ctypes.byref(self.be), device) < 0:
+            raise RuntimeError(f"m2dec_amd: HIP back end unavailable on device {device} (needs a gfx950 GPU)")
+
+    def timing(self) -> dict:
+        t = HipTiming()
+        lib().m2dec_amd_hip_backend_timing(ctypes.byref(self.be), ctypes.byref(t))
+        return t.as_dict()
+
+    def close(self) -> None:
+        _call_destroy(self.be)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def frame_md5(f: Frame) -> str:
+    """FileWriterMd5 line for one frame (reference filewrite.h:99-124), without the CRLF."""
+    buf = ctypes.create_string_buffer(35)
+    lib().m2dec_amd_frame_md5(ctypes.byref(f), buf)
+    return buf.raw[:32].decode()
+
+
+def frame_nv12(f: Frame) -> bytes:
+    """Cropped Y rows then cropped interleaved CbCr rows (FileWriter, filewrite.h:11-29)."""
+    w, h = f.width, f.height
+    l, r, t, b = f.crop[0], f.crop[1], f.crop[2], f.crop[3]
+    out = bytearray()
+    luma = ctypes.cast(f.luma, ctypes.POINTER(ctypes.c_uint8))
+    chroma = ctypes.cast(f.chroma, ctypes.POINTER(ctypes.c_uint8))
+    for y in range(t, h - b):
+        out += ctypes.string_at(ctypes.addressof(luma.contents) + y * w + l, w - l - r)
+    for y in range(t // 2, (h - b) // 2):
+        out += ctypes.string_at(ctypes.addressof(chroma.contents) + y * w + l, w - l - r)
+    return bytes(out)
+
+
+def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 0,
+                  on_frame: Optional[Callable[[Frame], None]] = None, md5: bool = True) -> List[str]:
+    """Decode an Annex-B H.264 stream exactly like ``h264dec -O`` and return the per-frame MD5 list.
+
+    ``backend`` None -> the HIP back end on ``device`` (raises if absent).  Any other m2r_backend_t
+    (e.g. the oracle's, in tests) is borrowed.
+    """
+    L = lib()
+    if backend is None and not L.m2dec_amd_hip_available():
+        raise RuntimeError("m2dec_amd: no usable gfx950 device for the HIP back end")
+    md5s: List[str] = []
+    errs: List[BaseException] = []
+
+    def _cb(_arg, fp):
+        try:
+            f = fp.contents
+            if md5:
+                md5s.append(frame_md5(f))
+            if on_frame is not None:
+                on_frame(f)
+        except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
+            errs.append(e)
+
+    cb = ON_FRAME(_cb)
+    st = Stats()
+    n = L.m2dec_amd_decode_stream(data, len(data), ctypes.byref(backend) if backend is not None else None, device, cb,
+                                  None, ctypes.byref(st))
+    if errs:
+        raise errs[0]
+    if n < 0:
+        raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
+    return md5s
+
+
+class H264Decoder:
+    """Thin object over the reference-shaped ``h264d_func`` table for callers that drive
+    decode_picture / get_decoded_frame themselves (mirrors M2Decoder, m2decoder.h:33-223)."""
+
+    class _Table(ctypes.Structure):
+        _fields_ = [("context_size", ctypes.c_size_t), ("init", ctypes.c_void_p), ("stream_pos", ctypes.c_void_p),
+                    ("get_info", ctypes.c_void_p), ("set_frames", ctypes.c_void_p),
+                    ("decode_picture", ctypes.c_void_p), ("peek_decoded_frame", ctypes.c_void_p),
+                    ("get_decoded_frame", ctypes.c_void_p)]
+
+    @classmethod
+    def table(cls):
+        p = ctypes.c_void_p.in_dll(lib(), "h264d_func")
+        return ctypes.cast(p, ctypes.POINTER(cls._Table)).contents

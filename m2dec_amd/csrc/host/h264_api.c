@@ -288,7 +288,10 @@ static int drv_header(void *arg, void *id)
 	int w, h, bufnum;
 	size_t luma_len;
 	(void)id;
-	h264d_func->get_info(v->d, &info);
+	if (h264d_func->get_info(v->d, &info) < 0) {
+		v->failed = 1;
+		return -1;
+	}
 	w = (info.src_width + 15) & ~15;
 	h = (info.src_height + 15) & ~15;
 	luma_len = (size_t)w * (size_t)h;
@@ -365,6 +368,7 @@ done:
 		stats->pictures = (int)d->pictures;
 		stats->last_error = err;
 	}
+	if (backend) d->have_backend = 0; /* borrowed: the caller destroys it */
 	m2dec_amd_h264_release(d);
 	free(d);
 	free(v.frame_mem);

@@ -1487,7 +1487,7 @@ static int decode_inter(slice_ctx_t *s, int type)
 		if (type >= MBT_B_FIRST) {
 			int bt = type - MBT_B_FIRST; /* 0.. */
 			pm = b_predmap[bt];
-			shape = (bt < 3) ? 0 : ((bt & 1) ? 2 : 1);
+			shape = (bt < 3) ? 0 : ((bt & 1) ? 1 : 2); /* bt 3 = B_L0_L0_16x8, bt 4 = B_L0_L0_8x16 */
 			if (bt < 3) pm = (pm & 1) | ((pm & 2) << 1); /* per partition bits: L0 part0, L1 part0 */
 		} else {
 			shape = type - MBT_P16x16; /* 0 16x16, 1 16x8, 2 8x16 */

@@ -630,17 +630,17 @@ static void intra_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, in
 			for (int i = 0; i < 4; ++i) {
 				int *r = c + i * 4;
 				int a0 = r[0] + r[1], a1 = r[0] - r[1], a2 = r[2] + r[3], a3 = r[2] - r[3];
-				t[i * 4 + 0] = a0 + a2;
-				t[i * 4 + 1] = a1 + a3;
+				t[i * 4 + 0] = a0 + a2; /* Hadamard rows [1 1 1 1], [1 1 -1 -1], [1 -1 -1 1], [1 -1 1 -1] */
+				t[i * 4 + 1] = a0 - a2;
 				t[i * 4 + 2] = a1 - a3;
-				t[i * 4 + 3] = a0 - a2;
+				t[i * 4 + 3] = a1 + a3;
 			}
 			for (int j = 0; j < 4; ++j) {
 				int a0 = t[j] + t[4 + j], a1 = t[j] - t[4 + j], a2 = t[8 + j] + t[12 + j], a3 = t[8 + j] - t[12 + j];
 				c[j] = (a0 + a2 + 2) >> 2;
-				c[4 + j] = (a1 + a3 + 2) >> 2;
+				c[4 + j] = (a0 - a2 + 2) >> 2;
 				c[8 + j] = (a1 - a3 + 2) >> 2;
-				c[12 + j] = (a0 - a2 + 2) >> 2;
+				c[12 + j] = (a1 + a3 + 2) >> 2;
 			}
 			for (int k = 0; k < 16; ++k) dc[k] = c[k];
 		}

@@ -1,0 +1,43 @@
+"""Test-only access to the CPU oracle (oracle/recon_oracle.c) as an m2r_backend_t.
+
+The oracle is the parity checker; it is never the thing measured or shipped."""
+import ctypes
+import os
+
+from m2dec_amd import Backend
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_PATH = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+_orc = None
+
+
+def oracle_lib():
+    global _orc
+    if _orc is None:
+        _orc = ctypes.CDLL(ORACLE_PATH)
+        _orc.oracle_backend_create.argtypes = [ctypes.POINTER(Backend)]
+        _orc.oracle_backend_create.restype = ctypes.c_int
+    return _orc
+
+
+class OracleBackend:
+    def __init__(self):
+        self.be = Backend()
+        assert oracle_lib().oracle_backend_create(ctypes.byref(self.be)) == 0
+
+    def close(self):
+        if self.be.destroy:
+            ctypes.CFUNCTYPE(None, ctypes.c_void_p)(self.be.destroy)(self.be.self)
+            self.be.destroy = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def golden_md5s(path):
+    data = open(path, "rb").read()
+    assert len(data) % 34 == 0
+    return [data[i:i + 32].decode() for i in range(0, len(data), 34)]

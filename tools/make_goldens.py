@@ -1,0 +1,53 @@
+"""Regenerate tests/golden/synthetic.json: for each synthetic stream (preset, seed, frames) record
+the stream's sha256 and the per-frame NV12 MD5s from the CPU oracle (oracle/recon_oracle.c) over
+the host parser.  These goldens are oracle-derived ("partially pinned": the oracle itself is pinned
+to the reference decoder by the F1 fixture)."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import m2dec_amd  # noqa: E402
+from tests._oracle import OracleBackend  # noqa: E402
+
+GEN = os.path.join(ROOT, "tools", "_build", "h264gen")
+STREAMS = [
+    # name, preset, seed, frames
+    ("cov_cavlc_s1", "cov_cavlc", 1, 16),
+    ("cov_cavlc_s2", "cov_cavlc", 2, 16),
+    ("cov_cabac_s1", "cov_cabac", 1, 16),
+    ("cov_cabac_s2", "cov_cabac", 2, 16),
+    ("cov_cabac4x4_s1", "cov_cabac4x4", 1, 16),
+    ("cov_wp_s1", "cov_wp", 1, 16),
+    ("cov_slices_s1", "cov_slices", 1, 12),
+    ("c2_720p_s1", "c2", 1, 60),
+    ("c3_1080p_s1", "c3", 1, 60),
+]
+
+
+def gen(preset, seed, frames, out):
+    subprocess.run([GEN, "--preset", preset, "--seed", str(seed), "--frames", str(frames), "-o", out], check=True,
+                   stderr=subprocess.DEVNULL)
+    return open(out, "rb").read()
+
+
+def main():
+    res = {}
+    tmp = "/tmp/m2dec_goldens"
+    os.makedirs(tmp, exist_ok=True)
+    for name, preset, seed, frames in STREAMS:
+        data = gen(preset, seed, frames, os.path.join(tmp, name + ".264"))
+        with OracleBackend() as ob:
+            md5s = m2dec_amd.decode_stream(data, backend=ob.be)
+        res[name] = {"preset": preset, "seed": seed, "frames": frames, "bytes": len(data),
+                     "sha256": hashlib.sha256(data).hexdigest(), "md5": md5s}
+        print(name, len(data), len(md5s))
+    with open(os.path.join(ROOT, "tests", "golden", "synthetic.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

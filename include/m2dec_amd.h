@@ -61,6 +61,38 @@ int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t
 /* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
 
+/* ---- record traces (m2dec_amd/csrc/host/trace.c): a stream parsed once, records kept in memory */
+typedef struct m2dec_amd_trace m2dec_amd_trace_t;
+typedef struct {
+	int32_t slot, width_mbs, height_mbs, n_inter, n_coef, n_slices, n_intra, deblock;
+	uint64_t off_mb, off_dbk, off_slice, off_inter, off_coef; /* byte offsets into the record buffer */
+	int64_t record_bytes;  /* R_pic */
+	int64_t ref_bytes;     /* sum over PUs and lists of 1.5 w h */
+	int64_t frame_bytes;   /* 1.5 W H */
+} m2dec_amd_trace_pic_t;
+/* Parse `data` (Annex B) with the host parser; returns the number of pictures or -1. */
+int m2dec_amd_trace_capture(const uint8_t *data, size_t len, m2dec_amd_trace_t **out);
+int m2dec_amd_trace_info(const m2dec_amd_trace_t *t, int *npics, int *width, int *height, int *nslots, int *nout);
+const m2dec_amd_trace_pic_t *m2dec_amd_trace_pictures(const m2dec_amd_trace_t *t);
+const uint8_t *m2dec_amd_trace_records(const m2dec_amd_trace_t *t, size_t *len);
+const int *m2dec_amd_trace_output_order(const m2dec_amd_trace_t *t); /* picture index per output frame */
+int m2dec_amd_trace_crop(const m2dec_amd_trace_t *t, int crop[4]);   /* output crop (m2d_frame_t.crop) */
+void m2dec_amd_trace_free(m2dec_amd_trace_t *t);
+
+/* ---- GPU replay of a trace with the records resident in HBM (recon_hip.hip) */
+typedef struct m2dec_amd_hip_replay m2dec_amd_hip_replay_t;
+int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out);
+/* Enqueue `passes` reconstructions of every picture in decoding order (asynchronous). */
+int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes);
+/* Wait for the enqueued work; returns -1 on a device error or wavefront hand-off timeout. */
+int m2dec_amd_hip_replay_sync(m2dec_amd_hip_replay_t *r);
+/* Per-kernel HIP-event times accumulated by runs since the last reset (call after sync). */
+int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_hip_timing_t *out, int reset);
+/* One checked pass: after every picture, download it and write its MD5 line (35 bytes per picture,
+ * decoding order) into md5s. */
+int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s);
+void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r);
+
 #ifdef __cplusplus
 }
 #endif

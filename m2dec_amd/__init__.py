@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libm2dec_amd.so")
 
 __all__ = [
     "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",
-    "decode_stream", "frame_md5", "frame_nv12", "H264Decoder",
+    "decode_stream", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
 ]
 
 
@@ -61,6 +61,16 @@ class HipTiming(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class TracePic(ctypes.Structure):
+    """m2dec_amd_trace_pic_t (include/m2dec_amd.h)."""
+    _fields_ = [("slot", ctypes.c_int32), ("width_mbs", ctypes.c_int32), ("height_mbs", ctypes.c_int32),
+                ("n_inter", ctypes.c_int32), ("n_coef", ctypes.c_int32), ("n_slices", ctypes.c_int32),
+                ("n_intra", ctypes.c_int32), ("deblock", ctypes.c_int32), ("off_mb", ctypes.c_uint64),
+                ("off_dbk", ctypes.c_uint64), ("off_slice", ctypes.c_uint64), ("off_inter", ctypes.c_uint64),
+                ("off_coef", ctypes.c_uint64), ("record_bytes", ctypes.c_int64), ("ref_bytes", ctypes.c_int64),
+                ("frame_bytes", ctypes.c_int64)]
+
+
 ON_FRAME = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(Frame))
 
 _lib = None
@@ -84,6 +94,33 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
         L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
         L.m2dec_amd_frame_md5.restype = None
+        vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
+        L.m2dec_amd_trace_capture.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.m2dec_amd_trace_capture.restype = ctypes.c_int
+        L.m2dec_amd_trace_info.argtypes = [vp, ip, ip, ip, ip, ip]
+        L.m2dec_amd_trace_info.restype = ctypes.c_int
+        L.m2dec_amd_trace_pictures.argtypes = [vp]
+        L.m2dec_amd_trace_pictures.restype = ctypes.POINTER(TracePic)
+        L.m2dec_amd_trace_records.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t)]
+        L.m2dec_amd_trace_records.restype = vp
+        L.m2dec_amd_trace_output_order.argtypes = [vp]
+        L.m2dec_amd_trace_output_order.restype = ip
+        L.m2dec_amd_trace_crop.argtypes = [vp, ip]
+        L.m2dec_amd_trace_crop.restype = ctypes.c_int
+        L.m2dec_amd_trace_free.argtypes = [vp]
+        L.m2dec_amd_trace_free.restype = None
+        L.m2dec_amd_hip_replay_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+        L.m2dec_amd_hip_replay_create.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_run.argtypes = [vp, ctypes.c_int]
+        L.m2dec_amd_hip_replay_run.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_sync.argtypes = [vp]
+        L.m2dec_amd_hip_replay_sync.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_timing.argtypes = [vp, ctypes.POINTER(HipTiming), ctypes.c_int]
+        L.m2dec_amd_hip_replay_timing.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_md5.argtypes = [vp, ctypes.c_char_p]
+        L.m2dec_amd_hip_replay_md5.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_destroy.argtypes = [vp]
+        L.m2dec_amd_hip_replay_destroy.restype = None
         _lib = L
     return _lib
 
@@ -190,3 +227,84 @@ class H264Decoder:
     def table(cls):
         p = ctypes.c_void_p.in_dll(lib(), "h264d_func")
         return ctypes.cast(p, ctypes.POINTER(cls._Table)).contents
+
+
+class Trace:
+    """A stream parsed once by the host parser; every picture's records kept in host memory
+    (m2dec_amd_trace_capture).  Replayed on the GPU by HipReplay."""
+
+    def __init__(self, data: bytes):
+        L = lib()
+        self.h = ctypes.c_void_p()
+        n = L.m2dec_amd_trace_capture(data, len(data), ctypes.byref(self.h))
+        if n < 0:
+            raise RuntimeError("m2dec_amd: trace capture (host parse) failed")
+        v = [ctypes.c_int() for _ in range(5)]
+        L.m2dec_amd_trace_info(self.h, *[ctypes.byref(x) for x in v])
+        self.npics, self.width, self.height, self.nslots, self.nout = [x.value for x in v]
+        p = L.m2dec_amd_trace_pictures(self.h)
+        self.pics = [p[i] for i in range(self.npics)]
+        o = L.m2dec_amd_trace_output_order(self.h)
+        self.output_order = [o[i] for i in range(self.nout)]
+        ln = ctypes.c_size_t()
+        self.records_ptr = L.m2dec_amd_trace_records(self.h, ctypes.byref(ln))
+        self.records_len = ln.value
+
+    def records(self) -> bytes:
+        return ctypes.string_at(self.records_ptr, self.records_len)
+
+    def close(self):
+        if self.h:
+            lib().m2dec_amd_trace_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class HipReplay:
+    """GPU reconstruction of a Trace with its records resident in HBM (m2dec_amd_hip_replay_*)."""
+
+    def __init__(self, trace: Trace, device: int = 0):
+        self.trace = trace
+        self.h = ctypes.c_void_p()
+        if lib().m2dec_amd_hip_replay_create(trace.h, device, ctypes.byref(self.h)) < 0:
+            raise RuntimeError(f"m2dec_amd: HIP replay unavailable on device {device}")
+
+    def run(self, passes: int = 1) -> None:
+        if lib().m2dec_amd_hip_replay_run(self.h, passes) < 0:
+            raise RuntimeError("m2dec_amd: replay launch failed")
+
+    def sync(self) -> None:
+        if lib().m2dec_amd_hip_replay_sync(self.h) < 0:
+            raise RuntimeError("m2dec_amd: replay failed on the device")
+
+    def timing(self, reset: bool = True) -> dict:
+        t = HipTiming()
+        lib().m2dec_amd_hip_replay_timing(self.h, ctypes.byref(t), 1 if reset else 0)
+        return t.as_dict()
+
+    def md5_decode_order(self) -> List[str]:
+        buf = ctypes.create_string_buffer(35 * self.trace.npics)
+        if lib().m2dec_amd_hip_replay_md5(self.h, buf) < 0:
+            raise RuntimeError("m2dec_amd: replay md5 pass failed")
+        raw = buf.raw
+        return [raw[35 * i:35 * i + 32].decode() for i in range(self.trace.npics)]
+
+    def md5_output_order(self) -> List[str]:
+        d = self.md5_decode_order()
+        return [d[i] for i in self.trace.output_order]
+
+    def close(self):
+        if self.h:
+            lib().m2dec_amd_hip_replay_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

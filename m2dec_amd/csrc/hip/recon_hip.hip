@@ -1020,6 +1020,52 @@ static void flush_timing(HipBackend *b, int k)
 	b->ev_pending[k] = false;
 }
 
+struct RecPtrs {
+	const m2r_mb_t *mb;
+	const m2r_deblock_t *dbk;
+	const m2r_slice_t *sl;
+	const m2r_inter_t *it;
+	const int16_t *coef;
+};
+
+struct Geometry {
+	uint8_t *frames;
+	size_t fsz;
+	int W, H, Wmb, Hmb;
+	int *prog; /* [2][Hmb] */
+	int *err;
+};
+
+/* Enqueue one picture (k_inter -> k_intra -> k_deblock) on stream s.  ev (optional) receives
+ * three records: after k_inter, after k_intra, after k_deblock. */
+static int launch_picture(hipStream_t s, const Geometry &g, const RecPtrs &r, int slot, int n_inter, int n_intra,
+                          int deblock, hipEvent_t *ev, m2dec_amd_hip_timing_t *tm)
+{
+	uint8_t *cur = g.frames + (size_t)slot * g.fsz;
+	const int n = g.Wmb * g.Hmb;
+	if (n_inter) {
+		hipLaunchKernelGGL(k_inter, dim3(n), dim3(256), 0, s, r.mb, r.it, r.sl, r.coef, g.frames, g.fsz, g.W, g.H, g.Wmb, slot);
+		CHECK(hipGetLastError());
+		tm->inter_launches++;
+	}
+	if (ev) CHECK(hipEventRecord(ev[0], s));
+	if (n_intra) {
+		CHECK(hipMemsetAsync(g.prog, 0, sizeof(int) * g.Hmb, s));
+		hipLaunchKernelGGL(k_intra, dim3(g.Hmb), dim3(64), 0, s, r.mb, r.coef, cur, g.W, g.H, g.Wmb, g.prog, g.err);
+		CHECK(hipGetLastError());
+		tm->intra_launches++;
+	}
+	if (ev) CHECK(hipEventRecord(ev[1], s));
+	if (deblock) {
+		CHECK(hipMemsetAsync(g.prog + g.Hmb, 0, sizeof(int) * g.Hmb, s));
+		hipLaunchKernelGGL(k_deblock, dim3(g.Hmb), dim3(64), 0, s, r.dbk, cur, g.W, g.H, g.Wmb, g.prog + g.Hmb, g.err);
+		CHECK(hipGetLastError());
+		tm->deblock_launches++;
+	}
+	if (ev) CHECK(hipEventRecord(ev[2], s));
+	return 0;
+}
+
 static const int kSlicesCap = 64;
 
 static void unregister_frames(HipBackend *b)
@@ -1158,32 +1204,15 @@ static int be_submit(void *self, m2r_picture_t *pic)
 	CHECK(hipEventRecord(a->uploaded, s));
 	a->pending = true;
 	if (b->timing) CHECK(hipEventRecord(ev[1], s));
-	const m2r_mb_t *d_mb = (const m2r_mb_t *)(a->dev + a->off_mb);
-	const m2r_deblock_t *d_dbk = (const m2r_deblock_t *)(a->dev + a->off_dbk);
-	const m2r_slice_t *d_sl = (const m2r_slice_t *)(a->dev + a->off_slice);
-	const m2r_inter_t *d_it = (const m2r_inter_t *)(a->dev + a->off_inter);
-	const int16_t *d_coef = (const int16_t *)(a->dev + a->off_coef);
+	RecPtrs rp;
+	rp.mb = (const m2r_mb_t *)(a->dev + a->off_mb);
+	rp.dbk = (const m2r_deblock_t *)(a->dev + a->off_dbk);
+	rp.sl = (const m2r_slice_t *)(a->dev + a->off_slice);
+	rp.it = (const m2r_inter_t *)(a->dev + a->off_inter);
+	rp.coef = (const int16_t *)(a->dev + a->off_coef);
 	uint8_t *cur = b->d_frames + (size_t)pic->slot * b->fsz;
-	if (pic->n_inter) {
-		hipLaunchKernelGGL(k_inter, dim3(n), dim3(256), 0, s, d_mb, d_it, d_sl, d_coef, b->d_frames, b->fsz, b->W, b->H, b->Wmb, pic->slot);
-		CHECK(hipGetLastError());
-		b->tm.inter_launches++;
-	}
-	if (b->timing) CHECK(hipEventRecord(ev[2], s));
-	if (pic->n_intra) {
-		CHECK(hipMemsetAsync(b->d_prog, 0, sizeof(int) * b->Hmb, s));
-		hipLaunchKernelGGL(k_intra, dim3(b->Hmb), dim3(64), 0, s, d_mb, d_coef, cur, b->W, b->H, b->Wmb, b->d_prog, b->d_err);
-		CHECK(hipGetLastError());
-		b->tm.intra_launches++;
-	}
-	if (b->timing) CHECK(hipEventRecord(ev[3], s));
-	if (pic->deblock) {
-		CHECK(hipMemsetAsync(b->d_prog + b->Hmb, 0, sizeof(int) * b->Hmb, s));
-		hipLaunchKernelGGL(k_deblock, dim3(b->Hmb), dim3(64), 0, s, d_dbk, cur, b->W, b->H, b->Wmb, b->d_prog + b->Hmb, b->d_err);
-		CHECK(hipGetLastError());
-		b->tm.deblock_launches++;
-	}
-	if (b->timing) CHECK(hipEventRecord(ev[4], s));
+	Geometry gm{b->d_frames, b->fsz, b->W, b->H, b->Wmb, b->Hmb, b->d_prog, b->d_err};
+	if (launch_picture(s, gm, rp, pic->slot, pic->n_inter, pic->n_intra, pic->deblock, b->timing ? ev + 2 : nullptr, &b->tm) < 0) return -1;
 	const m2d_frame_t &f = b->frames[pic->slot];
 	size_t ls = (size_t)b->W * b->H;
 	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
@@ -1284,4 +1313,181 @@ extern "C" int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_h
 	for (int k = 0; k < 4; ++k) flush_timing(b, k);
 	*out = b->tm;
 	return 0;
+}
+
+/* ======================================================================== trace replay */
+struct m2dec_amd_hip_replay {
+	int dev = 0;
+	hipStream_t stream = nullptr;
+	int W = 0, H = 0, Wmb = 0, Hmb = 0, nslots = 0, npics = 0;
+	int crop[4] = {0, 0, 0, 0};
+	size_t fsz = 0;
+	uint8_t *d_frames = nullptr, *d_rec = nullptr;
+	int *d_prog = nullptr, *d_err = nullptr;
+	m2dec_amd_trace_pic_t *pics = nullptr;
+	/* timing: 4 events per enqueued picture (start, after inter, after intra, after deblock) */
+	hipEvent_t *ev = nullptr;
+	int ev_cap = 0, ev_used = 0;
+	m2dec_amd_hip_timing_t tm;
+};
+
+static void replay_free(m2dec_amd_hip_replay_t *r)
+{
+	(void)hipSetDevice(r->dev);
+	if (r->stream) (void)hipStreamSynchronize(r->stream);
+	for (int i = 0; i < r->ev_cap; ++i) (void)hipEventDestroy(r->ev[i]);
+	free(r->ev);
+	free(r->pics);
+	if (r->d_frames) (void)hipFree(r->d_frames);
+	if (r->d_rec) (void)hipFree(r->d_rec);
+	if (r->d_prog) (void)hipFree(r->d_prog);
+	if (r->d_err) (void)hipFree(r->d_err);
+	if (r->stream) (void)hipStreamDestroy(r->stream);
+	delete r;
+}
+
+extern "C" int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out)
+{
+	int npics, W, H, nslots, nout;
+	size_t len;
+	if (!t || !out || !m2dec_amd_hip_available()) return -1;
+	if (m2dec_amd_trace_info(t, &npics, &W, &H, &nslots, &nout) < 0 || npics <= 0 || W <= 0 || H <= 0) return -1;
+	const uint8_t *rec = m2dec_amd_trace_records(t, &len);
+	const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(t);
+	for (int i = 0; i < npics; ++i)
+		if (pics[i].slot < 0 || pics[i].slot >= nslots || pics[i].width_mbs != W / 16 || pics[i].height_mbs != H / 16) return -1;
+	m2dec_amd_hip_replay_t *r = new m2dec_amd_hip_replay_t();
+	memset(&r->tm, 0, sizeof(r->tm));
+	r->dev = device;
+	r->W = W;
+	r->H = H;
+	r->Wmb = W / 16;
+	r->Hmb = H / 16;
+	r->nslots = nslots;
+	r->npics = npics;
+	m2dec_amd_trace_crop(t, r->crop);
+	r->fsz = ((size_t)W * H * 3 / 2 + 4095) & ~(size_t)4095;
+	r->pics = (m2dec_amd_trace_pic_t *)malloc(sizeof(*pics) * (size_t)npics);
+	memcpy(r->pics, pics, sizeof(*pics) * (size_t)npics);
+#define RCHECK(x) do { if ((x) != hipSuccess) { fprintf(stderr, "m2dec_amd replay: %s failed\n", #x); replay_free(r); return -1; } } while (0)
+	RCHECK(hipSetDevice(device));
+	RCHECK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+	RCHECK(hipMalloc(&r->d_frames, r->fsz * (size_t)nslots));
+	RCHECK(hipMemset(r->d_frames, 0, r->fsz * (size_t)nslots));
+	RCHECK(hipMalloc(&r->d_rec, len));
+	RCHECK(hipMemcpy(r->d_rec, rec, len, hipMemcpyHostToDevice));
+	RCHECK(hipMalloc(&r->d_prog, sizeof(int) * 2 * (size_t)r->Hmb));
+	RCHECK(hipMalloc(&r->d_err, sizeof(int)));
+	RCHECK(hipMemset(r->d_err, 0, sizeof(int)));
+#undef RCHECK
+	*out = r;
+	return 0;
+}
+
+static int replay_enqueue(m2dec_amd_hip_replay_t *r, int i, bool timed)
+{
+	const m2dec_amd_trace_pic_t &p = r->pics[i];
+	RecPtrs rp;
+	rp.mb = (const m2r_mb_t *)(r->d_rec + p.off_mb);
+	rp.dbk = (const m2r_deblock_t *)(r->d_rec + p.off_dbk);
+	rp.sl = (const m2r_slice_t *)(r->d_rec + p.off_slice);
+	rp.it = (const m2r_inter_t *)(r->d_rec + p.off_inter);
+	rp.coef = (const int16_t *)(r->d_rec + p.off_coef);
+	Geometry gm{r->d_frames, r->fsz, r->W, r->H, r->Wmb, r->Hmb, r->d_prog, r->d_err};
+	hipEvent_t *ev = nullptr;
+	if (timed) {
+		if (r->ev_used + 4 > r->ev_cap) {
+			int nc = r->ev_cap ? r->ev_cap * 2 : 1024;
+			hipEvent_t *ne = (hipEvent_t *)realloc(r->ev, sizeof(hipEvent_t) * (size_t)nc);
+			if (!ne) return -1;
+			r->ev = ne;
+			for (int k = r->ev_cap; k < nc; ++k) CHECK(hipEventCreate(&r->ev[k]));
+			r->ev_cap = nc;
+		}
+		ev = r->ev + r->ev_used;
+		r->ev_used += 4;
+		CHECK(hipEventRecord(ev[0], r->stream));
+	}
+	if (launch_picture(r->stream, gm, rp, p.slot, p.n_inter, p.n_intra, p.deblock, ev ? ev + 1 : nullptr, &r->tm) < 0) return -1;
+	r->tm.pictures++;
+	r->tm.record_bytes += p.record_bytes;
+	r->tm.ref_bytes += p.ref_bytes;
+	r->tm.frame_bytes += p.frame_bytes;
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
+{
+	if (!r) return -1;
+	CHECK(hipSetDevice(r->dev));
+	for (int k = 0; k < passes; ++k)
+		for (int i = 0; i < r->npics; ++i)
+			if (replay_enqueue(r, i, true) < 0) return -1;
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_sync(m2dec_amd_hip_replay_t *r)
+{
+	int err = 0;
+	if (!r) return -1;
+	CHECK(hipSetDevice(r->dev));
+	CHECK(hipStreamSynchronize(r->stream));
+	CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
+	if (err) {
+		fprintf(stderr, "m2dec_amd replay: wavefront hand-off timed out (err=%d)\n", err);
+		return -1;
+	}
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_hip_timing_t *out, int reset)
+{
+	if (!r || !out) return -1;
+	CHECK(hipSetDevice(r->dev));
+	for (int i = 0; i + 4 <= r->ev_used; i += 4) {
+		float ms;
+		hipEvent_t *e = r->ev + i;
+		CHECK(hipEventSynchronize(e[3]));
+		if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) r->tm.inter_us += ms * 1e3;
+		if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess) r->tm.intra_us += ms * 1e3;
+		if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess) r->tm.deblock_us += ms * 1e3;
+	}
+	r->ev_used = 0;
+	*out = r->tm;
+	if (reset) memset(&r->tm, 0, sizeof(r->tm));
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
+{
+	if (!r || !md5s) return -1;
+	size_t ls = (size_t)r->W * r->H;
+	uint8_t *host = (uint8_t *)malloc(ls * 3 / 2);
+	if (!host) return -1;
+	CHECK(hipSetDevice(r->dev));
+	for (int i = 0; i < r->npics; ++i) {
+		if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) {
+			free(host);
+			return -1;
+		}
+		if (hipMemcpy(host, r->d_frames + (size_t)r->pics[i].slot * r->fsz, ls * 3 / 2, hipMemcpyDeviceToHost) != hipSuccess) {
+			free(host);
+			return -1;
+		}
+		m2d_frame_t f;
+		memset(&f, 0, sizeof(f));
+		f.luma = host;
+		f.chroma = host + ls;
+		f.width = (int16_t)r->W;
+		f.height = (int16_t)r->H;
+		for (int k = 0; k < 4; ++k) f.crop[k] = (int16_t)r->crop[k];
+		m2dec_amd_frame_md5(&f, md5s + 35 * (size_t)i);
+	}
+	free(host);
+	return 0;
+}
+
+extern "C" void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r)
+{
+	if (r) replay_free(r);
 }

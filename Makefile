@@ -12,7 +12,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -g -fPIC -std=c++17 $(INC) -Wno-unused-re
 HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)
 HOST_OBJ := $(patsubst m2dec_amd/csrc/host/%.c,build/host/%.o,$(HOST_SRC))
 HIP_SRC := m2dec_amd/csrc/hip/recon_hip.hip
-HIP_OBJ := build/hip/recon_hip.o
+HIP_HDR := m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h
+HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o
 
 LIB := m2dec_amd/lib/libm2dec_amd.so
 ORACLE := oracle/_build/liboracle.so
@@ -24,13 +25,13 @@ build/host/%.o: m2dec_amd/csrc/host/%.c $(wildcard m2dec_amd/csrc/host/*.h) $(wi
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(HIP_OBJ): $(HIP_SRC) m2dec_amd/csrc/hip/recon_kernels.h $(wildcard include/*.h)
+build/hip/%.o: m2dec_amd/csrc/hip/%.hip $(HIP_HDR) $(wildcard include/*.h)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libm2dec_amd.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libm2dec_amd.so -Wl,--no-undefined
 
 $(ORACLE): oracle/recon_oracle.c include/m2d_recon.h include/m2d.h
 	@mkdir -p $(dir $@)
@@ -40,7 +41,15 @@ $(GEN): $(wildcard tools/h264gen/*.c) $(wildcard tools/h264gen/*.h) m2dec_amd/cs
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ $(wildcard tools/h264gen/*.c) m2dec_amd/csrc/host/h264_spec_tables.c -lm
 
+DBG_LIB := build/dbg/libm2dec_amd_stamps.so
+$(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -c $(HIP_SRC) -o build/dbg/recon_hip_stamps.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stamps.o build/hip/runtime.o -Wl,--no-undefined
+
+stamps: $(DBG_LIB)
+
 clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build
 
-.PHONY: all clean
+.PHONY: all clean stamps

@@ -16,7 +16,7 @@ import os
 from typing import Callable, List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libm2dec_amd.so")
+LIB_PATH = os.environ.get("M2DEC_AMD_LIB") or os.path.join(_HERE, "lib", "libm2dec_amd.so")
 
 __all__ = [
     "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",

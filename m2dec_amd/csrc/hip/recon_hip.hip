@@ -23,11 +23,27 @@
 #include <stdlib.h>
 #include <string.h>
 #include "recon_kernels.h"
+#include "recon_internal.h"
 #include "m2dec_amd.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
-#define SPIN_LIMIT (1 << 24)
+#define SPIN_LIMIT (1 << 20) /* ~1 s of polling: a hand-off that never comes is an error, not a hang */
+
+/* Diagnostic timestamps (build with -DM2DEC_STAMPS; never in the product build): per MB row and
+ * role, s_memrealtime (100 MHz) at events, read back with m2dec_amd_debug_stamps(). */
+#define STAMP_ROWS 160
+#define STAMP_EV 256
+#ifdef M2DEC_STAMPS
+__device__ unsigned long long g_stamps[STAMP_ROWS][4][STAMP_EV];
+#define STAMP(row, role, idx, val)                                                                                   \
+	do {                                                                                                             \
+		if ((row) < STAMP_ROWS && (idx) < STAMP_EV && (threadIdx.x & 63) == 0)                                       \
+			g_stamps[row][role][idx] = (__builtin_amdgcn_s_memrealtime() << 16) | (unsigned long long)((val) & 0xffff); \
+	} while (0)
+#else
+#define STAMP(row, role, idx, val) do { } while (0)
+#endif
 
 /* ======================================================================== motion compensation */
 struct RefPlane {
@@ -287,28 +303,50 @@ __global__ __launch_bounds__(256) void k_inter(const m2r_mb_t *__restrict__ mbs,
 	if (t < 128) *dc = (uint8_t)d_clip255(predc + s_res[256 + cc * 64 + cy * 8 + cx]);
 }
 
-/* ======================================================================== wavefront hand-off */
-__device__ __forceinline__ bool wait_progress(int *flag, int need, int *err)
+/* write-through hand-off primitives (cdna_hip_programming.md §6 Guideline 16, R1): every shared word is
+ * a global-address-space agent-scope access; payload 8-byte sc1 stores, drained before one lane's
+ * sc1 flag store; consumer polls the flag with sc1 loads and reads the payload with sc1 loads. */
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
+__device__ __forceinline__ void st_sc1(void *p, unsigned long long v)
 {
-	unsigned spins = 0;
-	while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-		__builtin_amdgcn_s_sleep(1);
-		if (++spins > SPIN_LIMIT) {
-			atomicOr(err, 1);
-			return false;
-		}
+	__hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1(const void *p)
+{
+	return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* bounded spin step: false once the spin budget is spent or another workgroup has flagged an error
+ * (so one failure drains the whole grid quickly instead of every row timing out in turn) */
+__device__ __forceinline__ bool spin_ok(unsigned &spins, int *err, int code)
+{
+	__builtin_amdgcn_s_sleep(1);
+	++spins;
+	if ((spins & 255) == 0 && __hip_atomic_load((gi32 *)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+	if (spins > SPIN_LIMIT) {
+		if ((threadIdx.x & 63) == 0) atomicOr(err, code);
+		return false;
 	}
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 	return true;
 }
 
-__device__ __forceinline__ void publish_progress(int *flag, int value)
+__device__ __forceinline__ bool poll_ge(int *flag, int need, int *err)
 {
-	/* every storing wave drained + workgroup barrier happened before this call */
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	unsigned spins = 0;
+	while (__hip_atomic_load((gi32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+		if (!spin_ok(spins, err, 2)) return false;
+	}
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the payload loads below the poll */
+	return true;
+}
+
+__device__ __forceinline__ void signal_progress(int *flag, int value)
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the (single) storing wave drains its sc1 stores */
+	if ((threadIdx.x & 63) == 0) __hip_atomic_store((gi32 *)flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* ======================================================================== intra prediction (per sample) */
@@ -457,8 +495,18 @@ __device__ __forceinline__ int avail8(int b, int a)
 /* ======================================================================== k_intra */
 #define LW 25 /* luma context row: [0] = x0 - 1, [1..24] = x0 .. x0 + 23 */
 
+/*
+ * Intra / PCM macroblocks, one 64-lane workgroup per MB row, intra MBs left to right.  An intra MB
+ * reads unfiltered samples of its left, top-left, top and top-right neighbours.  Inter neighbours
+ * were reconstructed by k_inter before this launch (plain loads); intra neighbours of the row above
+ * were written in this launch by another workgroup and are read from their 32-byte hand-off record
+ * (bottom luma row + bottom chroma row, sc1 stores / sc1 loads, G16 R1), after polling that row's
+ * progress word only up to the rightmost intra MB among the three upper neighbours.  P/B pictures
+ * with few intra MBs therefore carry no row-to-row chain through their inter MBs.
+ */
+
 __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
-                                              uint8_t *cur, int W, int H, int Wmb, int *progress, int *err)
+                                              uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, int *err)
 {
 	const int y = blockIdx.x;
 	const int t = threadIdx.x;
@@ -468,20 +516,38 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 	__shared__ int DC[16];
 	__shared__ int F[32];           /* filtered 8x8 neighbours: [0..15] top, [16..23] left, [24] top-left */
 	__shared__ int HV[4];
-	int left_in_lds = 0;
 	uint8_t *chroma = cur + (size_t)W * H;
-	const int x_last = Wmb - 1;
+	int prev_x = -2;
+	const int y0 = y * 16;
 
-	for (int x = 0; x < Wmb; ++x) {
-		const m2r_mb_t m = mbs[y * Wmb + x];
-		const int x0 = x * 16, y0 = y * 16;
-		if (m.kind == M2R_MB_INTER) {
-			left_in_lds = 0;
-			continue;
-		}
+	for (int xb = 0; xb < Wmb; xb += 64) {
+		/* intra MBs of this row in [xb, xb + 64) and of the row above in [xb - 1, xb + 65) */
+		const int xi = xb + t;
+		unsigned long long cur_mask = __ballot(xi < Wmb && mbs[y * Wmb + xi].kind != M2R_MB_INTER);
+		unsigned long long up_mask = 0, up_lo = 0, up_hi = 0;
 		if (y > 0) {
-			if (t == 0) wait_progress(&progress[y - 1], min(x + 2, Wmb), err);
-			__syncthreads();
+			up_mask = __ballot(xi < Wmb && mbs[(y - 1) * Wmb + xi].kind != M2R_MB_INTER);
+			up_lo = (xb > 0) ? (mbs[(y - 1) * Wmb + xb - 1].kind != M2R_MB_INTER) : 0;
+			up_hi = (xb + 64 < Wmb) ? (mbs[(y - 1) * Wmb + xb + 64].kind != M2R_MB_INTER) : 0;
+		}
+		auto up_intra = [&](int xx) -> bool {
+			if (y == 0 || xx < 0 || xx >= Wmb) return false;
+			int k = xx - xb;
+			if (k < 0) return up_lo != 0;
+			if (k >= 64) return up_hi != 0;
+			return (up_mask >> k) & 1;
+		};
+		while (cur_mask) {
+		const int x = xb + __builtin_ctzll(cur_mask);
+		cur_mask &= cur_mask - 1;
+		const m2r_mb_t m = mbs[y * Wmb + x];
+		const int x0 = x * 16;
+		const int left_in_lds = (prev_x == x - 1);
+		if (y > 0) {
+			int need = 0;
+			for (int d = -1; d <= 1; ++d)
+				if (up_intra(x + d)) need = x + d + 1;
+			if (need) poll_ge(&progress[y - 1], need, err);
 		}
 		/* ---- gather the neighbourhood */
 		if (left_in_lds) {
@@ -489,26 +555,32 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 			if (t < 18) { int c = t / 9, r = t % 9; C[c][r][0] = C[c][r][8]; }
 		}
 		__syncthreads();
-		if (y > 0) {
-			if (t < 24) {
-				int xx = x0 + t;
-				if (t < 16 || x < x_last) L[0][1 + t] = cur[(size_t)(y0 - 1) * W + xx];
+		if (y > 0 && t < 7) {
+			/* granules of the row above: 0,1 luma MB x; 2 luma MB x+1 (bytes 0..7); 3 luma MB x-1 (bytes 8..15);
+			 * 4,5 chroma MB x; 6 chroma MB x-1 (bytes 8..15) */
+			const int xs = (t == 2) ? x + 1 : ((t == 3 || t == 6) ? x - 1 : x);
+			const int isc = (t >= 4);
+			const int half = (t == 1 || t == 3 || t == 5 || t == 6) ? 1 : 0;
+			if (xs >= 0 && xs < Wmb) {
+				unsigned long long v;
+				if (up_intra(xs)) v = ld_sc1(hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + isc * 16 + half * 8);
+				else v = *(const unsigned long long *)((isc ? chroma + (size_t)(y0 / 2 - 1) * W : cur + (size_t)(y0 - 1) * W) + xs * 16 + half * 8);
+				for (int b = 0; b < 8; ++b) {
+					uint8_t s8 = (uint8_t)(v >> (8 * b));
+					int j = half * 8 + b; /* byte within the 16-byte MB row */
+					if (t == 0 || t == 1) L[0][1 + j] = s8;
+					else if (t == 2) L[0][17 + b] = s8;
+					else if (t == 3) { if (j == 15) L[0][0] = s8; }
+					else if (t == 4 || t == 5) C[j & 1][0][1 + (j >> 1)] = s8;
+					else if (j >= 14) C[j & 1][0][0] = s8;
+				}
 			}
-			if (t == 24 && x > 0 && !left_in_lds) L[0][0] = cur[(size_t)(y0 - 1) * W + x0 - 1];
-			if (t >= 32 && t < 48) { int k = t - 32; C[k & 1][0][1 + (k >> 1)] = chroma[(size_t)(y0 / 2 - 1) * W + x0 + k]; }
-			if (t == 48 && x > 0 && !left_in_lds) { C[0][0][0] = chroma[(size_t)(y0 / 2 - 1) * W + x0 - 2]; C[1][0][0] = chroma[(size_t)(y0 / 2 - 1) * W + x0 - 1]; }
 		}
 		if (x > 0 && !left_in_lds) {
 			if (t < 16) L[1 + t][0] = cur[(size_t)(y0 + t) * W + x0 - 1];
 			if (t >= 16 && t < 32) { int k = t - 16; C[k & 1][1 + (k >> 1)][0] = chroma[(size_t)(y0 / 2 + (k >> 1)) * W + x0 - 2 + (k & 1)]; }
 		}
 		__syncthreads();
-		if (left_in_lds && y > 0) {
-			/* the top-left sample moved with the left column copy only for row 0 of L; refresh it from the row above */
-			if (t == 0) L[0][0] = cur[(size_t)(y0 - 1) * W + x0 - 1];
-			if (t == 1) { C[0][0][0] = chroma[(size_t)(y0 / 2 - 1) * W + x0 - 2]; C[1][0][0] = chroma[(size_t)(y0 / 2 - 1) * W + x0 - 1]; }
-			__syncthreads();
-		}
 
 		if (m.kind == M2R_MB_PCM) {
 			const uint8_t *s = (const uint8_t *)(pool + m.coef);
@@ -807,63 +879,71 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 			}
 		}
 
-		/* ---- write back and publish */
+		/* ---- write back and hand off the bottom rows */
 		for (int k = t; k < 256; k += 64) cur[(size_t)(y0 + (k >> 4)) * W + x0 + (k & 15)] = L[1 + (k >> 4)][1 + (k & 15)];
 		for (int k = t; k < 128; k += 64) {
 			int cy = k >> 4, bx = k & 15;
 			chroma[(size_t)(y0 / 2 + cy) * W + x0 + bx] = C[bx & 1][1 + cy][1 + (bx >> 1)];
 		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if (t < 4) {
+			unsigned long long v = 0;
+			for (int b = 0; b < 8; ++b) {
+				int j = (t & 1) * 8 + b;
+				uint8_t s8 = (t < 2) ? L[16][1 + j] : C[j & 1][8][1 + (j >> 1)];
+				v |= (unsigned long long)s8 << (8 * b);
+			}
+			st_sc1(hbi + ((size_t)y * Wmb + x) * HBI_BYTES + t * 8, v);
+		}
+		signal_progress(&progress[y], x + 1);
+		prev_x = x;
 		__syncthreads();
-		if (t == 0) publish_progress(&progress[y], x + 1);
-		left_in_lds = 1;
-		/* keep this MB's right column (col 16 / chroma col 8) for the next MB's left neighbours */
+		}
 	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	if (t == 0) publish_progress(&progress[y], Wmb);
+	signal_progress(&progress[y], Wmb);
 }
 
 /* ======================================================================== k_deblock */
-/* filter one line across an edge: q0 at s[0], p0 at s[-d] (spec 8.7.2.3 / 8.7.2.4) */
-__device__ __forceinline__ void filter_line(uint8_t *s, int d, int bs, int alpha, int beta, int ia, int luma)
+
+/* one edge, register form (spec 8.7.2.3 / 8.7.2.4; deblock_*_str4 / _str1_3, h264.cpp:10337-10520).
+ * p[0..3] = p0..p3, q[0..3] = q0..q3; only p0..p2 / q0..q2 change. */
+__device__ __forceinline__ void filter_regs(int *p, int *q, int bs, int alpha, int beta, int ia, bool luma)
 {
-	int p0 = s[-d], p1 = s[-2 * d], q0 = s[0], q1 = s[d];
+	const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
 	if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
 	if (bs < 4) {
-		int tc0 = c_tc0[ia][bs - 1], tc, delta;
+		int tc0 = c_tc0[ia][bs - 1], tc;
 		if (luma) {
-			int p2 = s[-3 * d], q2 = s[2 * d];
+			const int p2 = p[2], q2 = q[2];
 			int ap = abs(p2 - p0) < beta, aq = abs(q2 - q0) < beta;
 			tc = tc0 + ap + aq;
-			if (ap) s[-2 * d] = (uint8_t)(p1 + d_clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-			if (aq) s[d] = (uint8_t)(q1 + d_clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+			if (ap) p[1] = p1 + d_clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
+			if (aq) q[1] = q1 + d_clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
 		} else {
 			tc = tc0 + 1;
 		}
-		delta = d_clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-		s[-d] = (uint8_t)d_clip255(p0 + delta);
-		s[0] = (uint8_t)d_clip255(q0 - delta);
+		int delta = d_clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+		p[0] = d_clip255(p0 + delta);
+		q[0] = d_clip255(q0 - delta);
 	} else if (luma) {
-		int p2 = s[-3 * d], q2 = s[2 * d], p3 = s[-4 * d], q3 = s[3 * d];
+		const int p2 = p[2], q2 = q[2], p3 = p[3], q3 = q[3];
 		int small = abs(p0 - q0) < ((alpha >> 2) + 2);
 		if (abs(p2 - p0) < beta && small) {
-			s[-d] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-			s[-2 * d] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
-			s[-3 * d] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+			p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+			p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
+			p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
 		} else {
-			s[-d] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
+			p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
 		}
 		if (abs(q2 - q0) < beta && small) {
-			s[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-			s[d] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
-			s[2 * d] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+			q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+			q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
+			q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
 		} else {
-			s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+			q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
 		}
 	} else {
-		s[-d] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-		s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
+		p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
+		q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
 	}
 }
 
@@ -872,622 +952,303 @@ __device__ __forceinline__ int ab_idx(int qp, int off)
 	return min(max(qp + off, 0), 51);
 }
 
-#define TLW 20 /* luma tile: rows y0-4 .. y0+15, cols x0-4 .. x0+15 */
-#define TCW 20 /* chroma tile: rows y0/2-2 .. y0/2+7, bytes x0-4 .. x0+15 */
-
-__global__ __launch_bounds__(64) void k_deblock(const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W, int H, int Wmb,
-                                                int *progress, int *err)
+/* filter the samples v[0..n) of one line across edge positions; (p3..p0 | q0..q3) around `at` */
+__device__ __forceinline__ void edge_on_line(int *v, int at, int step, int bs, int qp, int aoff, int boff, bool luma)
 {
+	if (!bs) return;
+	int ia = ab_idx(qp, aoff), ib = ab_idx(qp, boff);
+	int p[4], q[4];
+	for (int i = 0; i < 4; ++i) {
+		p[i] = (at - (i + 1) * step >= 0) ? v[at - (i + 1) * step] : 0;
+		q[i] = v[at + i * step];
+	}
+	filter_regs(p, q, bs, c_alpha[ia], c_beta[ib], ia, luma);
+	for (int i = 0; i < 3; ++i) {
+		if (at - (i + 1) * step >= 0) v[at - (i + 1) * step] = p[i];
+		v[at + i * step] = q[i];
+	}
+}
+
+
+/*
+ * In-loop deblocking (deblock_pb, h264.cpp:10540-10663), one workgroup of three waves per MB row:
+ *   wave 0 (loader) : polls the row above's progress word and copies the hand-off records of every
+ *                     newly finished MB (its bottom 4 luma / 2 chroma rows after that row's filtering)
+ *                     into the top halo of this row's LDS buffer (sc1 loads, G16 R1);
+ *   wave 1 (filter) : filters MB after MB in LDS, in raster order: vertical edges with one row per
+ *                     lane held in registers, then horizontal edges with one column per lane;
+ *   wave 2 (storer) : writes every sample that became final to the frame, the hand-off records for
+ *                     the row below (write-through sc1), drains, and publishes progress.
+ * The whole MB row (20 luma / 10 chroma lines incl. the halo) lives in dynamic LDS, loaded once at
+ * entry, so the filter wave never touches global memory and never waits on a memory round trip;
+ * loader and storer batch every MB that is ready.  Waves talk through LDS words (workgroup-scope
+ * release / acquire); workgroups through progress words (agent scope, sc1).
+ * Frame writes: rows 0..12 (chroma 0..6) of an MB by its own row, rows 13..15 (7) by the row below.
+ */
+__global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W,
+                                                            int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int y = blockIdx.x;
-	const int t = threadIdx.x;
-	__shared__ uint8_t T[20][TLW];
-	__shared__ uint8_t TC[10][TCW];
+	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+	const int S = W + 2 * DBK_PAD;           /* LDS line stride: DBK_PAD bytes of pad each side */
+	uint8_t *RL = smem;                      /* 20 luma lines: frame rows y0-4 .. y0+15 */
+	uint8_t *RC = smem + 20 * S;             /* 10 chroma lines: rows yc0-2 .. yc0+7 */
+	m2r_deblock_t *rq = (m2r_deblock_t *)(smem + 30 * S); /* [Wmb] this row's records, [Wmb] the row above's */
+	m2r_deblock_t *rt = rq + Wmb;
+	int *flags = (int *)(rt + Wmb);          /* [0] top halos ready, [1] MBs filtered */
 	uint8_t *chroma = cur + (size_t)W * H;
 	const int y0 = y * 16, yc0 = y * 8;
+	const bool last_row = (y == Hmb - 1);
 
-	for (int x = 0; x < Wmb; ++x) {
-		const int x0 = x * 16;
-		const m2r_deblock_t q = dbk[y * Wmb + x];
-		if (y > 0) {
-			if (t == 0) wait_progress(&progress[y - 1], min(x + 2, Wmb), err);
-			__syncthreads();
-		}
-		/* left halo from the previous tile (already final w.r.t. this workgroup's writes) */
-		if (x > 0) {
-			if (t < 20) { for (int i = 0; i < 4; ++i) T[t][i] = T[t][16 + i]; }
-			else if (t < 30) { int r = t - 20; for (int i = 0; i < 4; ++i) TC[r][i] = TC[r][16 + i]; }
-		}
-		__syncthreads();
-		/* top halo (row above, other workgroup) and the MB itself */
-		for (int k = t; k < 20 * 16; k += 64) {
-			int r = k >> 4, c = k & 15;
-			if (r >= 4 || y > 0) T[r][4 + c] = cur[(size_t)(y0 - 4 + r) * W + x0 + c];
-		}
-		for (int k = t; k < 10 * 16; k += 64) {
-			int r = k >> 4, c = k & 15;
-			if (r >= 2 || y > 0) TC[r][4 + c] = chroma[(size_t)(yc0 - 2 + r) * W + x0 + c];
-		}
-		__syncthreads();
+	/* ---- prologue: this MB row and its records into LDS (all waves) */
+	for (int k = threadIdx.x; k < 16 * (W >> 4); k += 64 * DBK_WAVES) {
+		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
+		*(uint4 *)(RL + (4 + r) * S + DBK_PAD + c) = *(const uint4 *)(cur + (size_t)(y0 + r) * W + c);
+	}
+	for (int k = threadIdx.x; k < 8 * (W >> 4); k += 64 * DBK_WAVES) {
+		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
+		*(uint4 *)(RC + (2 + r) * S + DBK_PAD + c) = *(const uint4 *)(chroma + (size_t)(yc0 + r) * W + c);
+	}
+	for (int k = threadIdx.x; k < Wmb; k += 64 * DBK_WAVES) {
+		rq[k] = dbk[y * Wmb + k];
+		rt[k] = y > 0 ? dbk[(y - 1) * Wmb + k] : rq[k];
+	}
+	if (threadIdx.x == 0) {
+		flags[0] = (y == 0) ? Wmb : 0;
+		flags[1] = 0;
+	}
+	__syncthreads();
 
-		if (!(q.flags & M2R_DBK_OFF)) {
-			for (int dir = 0; dir < 2; ++dir) {
-				const uint32_t str = dir ? q.bs_h : q.bs_v;
-				const int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
-				const int bs4_flag = dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
-				int qpn = q.qpy, qpcn0 = q.qpc[0], qpcn1 = q.qpc[1];
-				if ((q.flags & edge_flag) && (str & 255)) {
-					const m2r_deblock_t p = dir ? dbk[(y - 1) * Wmb + x] : dbk[y * Wmb + x - 1];
-					qpn = (q.qpy + p.qpy + 1) >> 1;
-					qpcn0 = (q.qpc[0] + p.qpc[0] + 1) >> 1;
-					qpcn1 = (q.qpc[1] + p.qpc[1] + 1) >> 1;
+	if (wave == 0) {
+		/* ---------------- loader */
+		if (y == 0) return;
+		int got = 0, nld = 0;
+		unsigned spins = 0;
+		while (got < Wmb) {
+			int avail = __hip_atomic_load((gi32 *)&progress[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (avail <= got) {
+				if (!spin_ok(spins, err, 4)) {
+					/* give up (the launch is flagged bad): release the filter wave */
+					if (t == 0) __hip_atomic_store(&flags[0], Wmb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+					return;
 				}
-				for (int e = 0; e < 4; ++e) {
-					uint32_t s = (str >> (8 * e)) & 255;
-					int bs4 = 0;
-					if (e == 0) {
-						if (!((q.flags & edge_flag) && s)) continue;
-						bs4 = (q.flags & bs4_flag) != 0;
-					} else if (!s) {
-						continue;
-					}
-					int ql = e ? q.qpy : qpn;
-					if (t < 16) {
-						int bs = bs4 ? 4 : (int)((s >> ((t >> 2) * 2)) & 3);
-						if (bs) {
-							int ia = ab_idx(ql, q.alpha_off), ib = ab_idx(ql, q.beta_off);
-							uint8_t *pt = dir ? &T[4 + 4 * e][4 + t] : &T[4 + t][4 + 4 * e];
-							filter_line(pt, dir ? TLW : 1, bs, c_alpha[ia], c_beta[ib], ia, 1);
-						}
-					} else if (t < 32 && (e == 0 || e == 2)) {
-						int k = t - 16, comp = k >> 3, line = k & 7;
-						int bs = bs4 ? 4 : (int)((s >> ((line >> 1) * 2)) & 3);
-						if (bs) {
-							int qc = e ? q.qpc[comp] : (comp ? qpcn1 : qpcn0);
-							int ia = ab_idx(qc, q.alpha_off), ib = ab_idx(qc, q.beta_off);
-							uint8_t *pt = dir ? &TC[2 + 2 * e][4 + line * 2 + comp] : &TC[2 + line][4 + 4 * e + comp];
-							filter_line(pt, dir ? TCW : 2, bs, c_alpha[ia], c_beta[ib], ia, 0);
-						}
-					}
-					__syncthreads();
+				continue;
+			}
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			/* 12 granules per MB: 8 luma (rows 12..15 x 2 halves), 4 chroma (rows 6..7 x 2 halves) */
+			for (int g0 = got * 12; g0 < avail * 12; g0 += 64) {
+				int g = g0 + t;
+				if (g < avail * 12) {
+					int mb = g / 12, k = g % 12;
+					unsigned long long v = ld_sc1(hbd + ((size_t)(y - 1) * Wmb + mb) * HBD_BYTES + k * 8);
+					uint8_t *d = (k < 8) ? RL + (k >> 1) * S + DBK_PAD + mb * 16 + (k & 1) * 8
+					                     : RC + ((k - 8) >> 1) * S + DBK_PAD + mb * 16 + (k & 1) * 8;
+					*(uint2 *)d = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 				}
 			}
+			got = avail;
+			if (t == 0) __hip_atomic_store(&flags[0], got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			STAMP(y, 0, nld, got);
+			nld++;
 		}
-		/* write back: top rows y0-3..y0-1 (cols x0..x0+15) and the MB incl. left cols x0-3..x0-1 */
-		for (int k = t; k < 19 * 19; k += 64) {
-			int r = 1 + k / 19, c = 1 + k % 19;
-			if (r < 4 && c < 4) continue;
-			if (r < 4 && y == 0) continue;
-			if (c < 4 && x == 0) continue;
-			cur[(size_t)(y0 - 4 + r) * W + x0 - 4 + c] = T[r][c];
+		return;
+	}
+
+	if (wave == 1) {
+		/* ---------------- filter: one instruction stream for 16 luma lines (lanes 0..15) and 16 chroma
+		 * lines (lanes 16..31: Cb 16..23, Cr 24..31), branch-free per edge.  A chroma line keeps its
+		 * samples 0..3 / 4..7 at v[2..5] / v[10..13] so that its two edges sit where luma edges 0 and 2 do. */
+		__shared__ uint8_t s_alpha[52], s_beta[52], s_tc0[52][3];
+		for (int i = t; i < 52; i += 64) {
+			s_alpha[i] = c_alpha[i];
+			s_beta[i] = c_beta[i];
+			s_tc0[i][0] = c_tc0[i][0];
+			s_tc0[i][1] = c_tc0[i][1];
+			s_tc0[i][2] = c_tc0[i][2];
 		}
-		for (int k = t; k < 9 * 18; k += 64) {
-			int r = 1 + k / 18, c = 2 + k % 18;
-			if (r < 2 && c < 4) continue;
-			if (r < 2 && y == 0) continue;
-			if (c < 4 && x == 0) continue;
-			chroma[(size_t)(yc0 - 2 + r) * W + x0 - 4 + c] = TC[r][c];
-		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		if (t == 0) publish_progress(&progress[y], x + 1);
-	}
-}
-
-/* ======================================================================== host back end */
-namespace {
-
-struct Arena {
-	m2r_picture_t pic;
-	uint8_t *host = nullptr, *dev = nullptr;
-	size_t size = 0, off_mb = 0, off_dbk = 0, off_slice = 0, off_inter = 0, off_coef = 0;
-	hipEvent_t uploaded = nullptr;
-	bool pending = false;
-};
-
-struct HipBackend {
-	int dev = 0;
-	hipStream_t stream = nullptr;
-	int W = 0, H = 0, Wmb = 0, Hmb = 0, nframes = 0;
-	size_t fsz = 0;
-	uint8_t *d_frames = nullptr;
-	m2d_frame_t frames[64];
-	void *reg[64][2];
-	hipEvent_t slot_ev[64];
-	bool slot_pending[64];
-	Arena ar[3];
-	int next = 0;
-	int *d_prog = nullptr; /* [2][Hmb] */
-	int *d_err = nullptr;
-	hipEvent_t ev[4][6]; /* timing ring: picture k uses ev[k % 4] */
-	bool ev_pending[4];
-	int ev_next = 0;
-	m2dec_amd_hip_timing_t tm;
-	bool timing = true;
-};
-
-/* accumulate the kernel times of timing-ring entry k (blocks until that picture finished) */
-static void flush_timing(HipBackend *b, int k)
-{
-	if (!b->ev_pending[k]) return;
-	hipEvent_t *e = b->ev[k];
-	float ms;
-	(void)hipEventSynchronize(e[5]);
-	if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) b->tm.h2d_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess) b->tm.inter_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess) b->tm.intra_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, e[3], e[4]) == hipSuccess) b->tm.deblock_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, e[4], e[5]) == hipSuccess) b->tm.d2h_us += ms * 1e3;
-	b->ev_pending[k] = false;
-}
-
-struct RecPtrs {
-	const m2r_mb_t *mb;
-	const m2r_deblock_t *dbk;
-	const m2r_slice_t *sl;
-	const m2r_inter_t *it;
-	const int16_t *coef;
-};
-
-struct Geometry {
-	uint8_t *frames;
-	size_t fsz;
-	int W, H, Wmb, Hmb;
-	int *prog; /* [2][Hmb] */
-	int *err;
-};
-
-/* Enqueue one picture (k_inter -> k_intra -> k_deblock) on stream s.  ev (optional) receives
- * three records: after k_inter, after k_intra, after k_deblock. */
-static int launch_picture(hipStream_t s, const Geometry &g, const RecPtrs &r, int slot, int n_inter, int n_intra,
-                          int deblock, hipEvent_t *ev, m2dec_amd_hip_timing_t *tm)
-{
-	uint8_t *cur = g.frames + (size_t)slot * g.fsz;
-	const int n = g.Wmb * g.Hmb;
-	if (n_inter) {
-		hipLaunchKernelGGL(k_inter, dim3(n), dim3(256), 0, s, r.mb, r.it, r.sl, r.coef, g.frames, g.fsz, g.W, g.H, g.Wmb, slot);
-		CHECK(hipGetLastError());
-		tm->inter_launches++;
-	}
-	if (ev) CHECK(hipEventRecord(ev[0], s));
-	if (n_intra) {
-		CHECK(hipMemsetAsync(g.prog, 0, sizeof(int) * g.Hmb, s));
-		hipLaunchKernelGGL(k_intra, dim3(g.Hmb), dim3(64), 0, s, r.mb, r.coef, cur, g.W, g.H, g.Wmb, g.prog, g.err);
-		CHECK(hipGetLastError());
-		tm->intra_launches++;
-	}
-	if (ev) CHECK(hipEventRecord(ev[1], s));
-	if (deblock) {
-		CHECK(hipMemsetAsync(g.prog + g.Hmb, 0, sizeof(int) * g.Hmb, s));
-		hipLaunchKernelGGL(k_deblock, dim3(g.Hmb), dim3(64), 0, s, r.dbk, cur, g.W, g.H, g.Wmb, g.prog + g.Hmb, g.err);
-		CHECK(hipGetLastError());
-		tm->deblock_launches++;
-	}
-	if (ev) CHECK(hipEventRecord(ev[2], s));
-	return 0;
-}
-
-static const int kSlicesCap = 64;
-
-static void unregister_frames(HipBackend *b)
-{
-	for (int i = 0; i < 64; ++i)
-		for (int k = 0; k < 2; ++k)
-			if (b->reg[i][k]) {
-				(void)hipHostUnregister(b->reg[i][k]);
-				b->reg[i][k] = nullptr;
+		const bool active = t < 32;
+		const bool luma = t < 16;
+		const int comp = (t >> 3) & 1;        /* chroma lanes */
+		const int cl = t & 7;                 /* chroma line (row for dir 0, column for dir 1) */
+		const int seg_l = (t & 15) >> 2, seg_c = cl >> 1;
+		const int seg = luma ? seg_l : seg_c;
+		unsigned spins = 0;
+		for (int x = 0; x < Wmb; ++x) {
+			while (__hip_atomic_load(&flags[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= x) {
+				if (!spin_ok(spins, err, 16)) break;
 			}
-}
-
-static int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
-{
-	HipBackend *b = (HipBackend *)self;
-	CHECK(hipSetDevice(b->dev));
-	CHECK(hipStreamSynchronize(b->stream));
-	unregister_frames(b);
-	if (n > 64) n = 64;
-	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
-	size_t fsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
-	if (b->d_frames && (fsz != b->fsz || n > b->nframes)) {
-		(void)hipFree(b->d_frames);
-		b->d_frames = nullptr;
-	}
-	if (!b->d_frames) {
-		CHECK(hipMalloc(&b->d_frames, fsz * (size_t)n));
-		CHECK(hipMemset(b->d_frames, 0, fsz * (size_t)n));
-	}
-	if (b->d_prog && height / 16 != b->Hmb) {
-		(void)hipFree(b->d_prog);
-		b->d_prog = nullptr;
-	}
-	b->W = width;
-	b->H = height;
-	b->Wmb = width / 16;
-	b->Hmb = height / 16;
-	b->fsz = fsz;
-	b->nframes = n;
-	if (!b->d_prog) CHECK(hipMalloc(&b->d_prog, sizeof(int) * 2 * (size_t)b->Hmb));
-	size_t ls = (size_t)width * height, cs = ls / 2;
-	for (int i = 0; i < n; ++i) {
-		b->slot_pending[i] = false;
-		if (b->frames[i].chroma == b->frames[i].luma + ls) {
-			if (hipHostRegister(b->frames[i].luma, ls + cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-		} else {
-			if (hipHostRegister(b->frames[i].luma, ls, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-			if (hipHostRegister(b->frames[i].chroma, cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][1] = b->frames[i].chroma;
+			STAMP(y, 1, x, x);
+			const m2r_deblock_t q = rq[x];
+			if (!(q.flags & M2R_DBK_OFF)) {
+				const m2r_deblock_t pl = x > 0 ? rq[x - 1] : q, pt = rt[x];
+				const int base = DBK_PAD + x * 16; /* LDS column of the MB's first sample */
+				for (int dir = 0; dir < 2; ++dir) {
+					const uint32_t str = dir ? q.bs_h : q.bs_v;
+					const int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
+					const int bs4 = (q.flags & (dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4)) != 0;
+					const bool e0 = (q.flags & edge_flag) && (str & 255);
+					const int nqpy = dir ? pt.qpy : pl.qpy, nqc0 = dir ? pt.qpc[0] : pl.qpc[0], nqc1 = dir ? pt.qpc[1] : pl.qpc[1];
+					const int qc = comp ? q.qpc[1] : q.qpc[0];
+					const int nqc = comp ? nqc1 : nqc0;
+					const int qp_edge0 = e0 ? (luma ? (q.qpy + nqpy + 1) >> 1 : (qc + nqc + 1) >> 1) : 0;
+					const int qp_inner = luma ? q.qpy : qc;
+					/* line addressing: luma V row t / H column t; chroma V row cl / H byte column 2 cl + comp */
+					uint8_t *lb;
+					int st;
+					if (dir == 0) {
+						lb = luma ? RL + (4 + t) * S + base - 4 : RC + (2 + cl) * S + base - 4 + comp;
+						st = luma ? 1 : 2;
+					} else {
+						lb = luma ? RL + base + t : RC + base + 2 * cl + comp;
+						st = S;
+					}
+					int v[20];
+#pragma unroll
+					for (int i = 0; i < 20; ++i) {
+						const int ci = (i < 6) ? i - 2 : i - 6; /* chroma sample index for v[i] */
+						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
+						v[i] = 0;
+						if (active && (luma || cv)) v[i] = lb[(luma ? i : ci) * st];
+					}
+#pragma unroll
+					for (int e = 0; e < 4; ++e) {
+						int bs = active ? (int)((str >> (8 * e + 2 * seg)) & 3) : 0;
+						if (e == 0) bs = e0 ? (bs4 ? 4 : bs) : 0;
+						if (!luma && (e & 1)) bs = 0;
+						if (!__any(bs)) continue;
+						const int qp = e ? qp_inner : qp_edge0;
+						const int ia = min(max(qp + q.alpha_off, 0), 51), ib = min(max(qp + q.beta_off, 0), 51);
+						const int A = s_alpha[ia], B = s_beta[ib];
+						const int tc0 = bs ? s_tc0[ia][min(bs, 3) - 1] : 0;
+						const int at = 4 + 4 * e;
+						const int p0 = v[at - 1], p1 = v[at - 2], p2 = v[at - 3], p3 = v[at - 4];
+						const int q0 = v[at], q1 = v[at + 1], q2 = v[at + 2], q3 = v[at + 3];
+						const bool filt = bs && abs(p0 - q0) < A && abs(p1 - p0) < B && abs(q1 - q0) < B;
+						const bool ap = abs(p2 - p0) < B, aq = abs(q2 - q0) < B;
+						/* bS < 4 */
+						const int tc = tc0 + (luma ? (int)ap + (int)aq : 1);
+						const int delta = d_clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+						const int avg = (p0 + q0 + 1) >> 1;
+						int np0 = d_clip255(p0 + delta), nq0 = d_clip255(q0 - delta);
+						int np1 = (luma && ap) ? p1 + d_clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1) : p1;
+						int nq1 = (luma && aq) ? q1 + d_clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1) : q1;
+						int np2 = p2, nq2 = q2;
+						/* bS == 4 */
+						if (bs == 4) {
+							const bool small = abs(p0 - q0) < ((A >> 2) + 2);
+							const bool sp = luma && ap && small, sq = luma && aq && small;
+							np0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
+							np1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
+							np2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
+							nq0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
+							nq1 = sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1;
+							nq2 = sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
+						}
+						if (filt) {
+							v[at - 1] = np0;
+							v[at - 2] = np1;
+							v[at - 3] = np2;
+							v[at] = nq0;
+							v[at + 1] = nq1;
+							v[at + 2] = nq2;
+						}
+					}
+#pragma unroll
+					for (int i = 1; i < 19; ++i) {
+						const int ci = (i < 6) ? i - 2 : i - 6;
+						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
+						if (active && (luma || cv)) lb[(luma ? i : ci) * st] = (uint8_t)v[i];
+					}
+					__builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): this direction's LDS writes landed */
+					__builtin_amdgcn_wave_barrier();
+				}
+			}
+			if (t == 0) __hip_atomic_store(&flags[1], x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 		}
-		(void)hipGetLastError();
+		STAMP(y, 1, Wmb, Wmb);
+		return;
 	}
-	return 0;
-}
 
-static int arena_alloc(Arena &a, int wm, int hm)
-{
-	size_t n = (size_t)wm * hm;
-	size_t off = 0;
-	auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-	a.off_mb = off; off = al(off + n * sizeof(m2r_mb_t));
-	a.off_dbk = off; off = al(off + n * sizeof(m2r_deblock_t));
-	a.off_slice = off; off = al(off + kSlicesCap * sizeof(m2r_slice_t));
-	a.off_inter = off; off = al(off + n * sizeof(m2r_inter_t));
-	a.off_coef = off; off = al(off + n * 416 * sizeof(int16_t));
-	if (a.size < off) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
-		a.host = nullptr;
-		a.dev = nullptr;
-		CHECK(hipHostMalloc(&a.host, off, hipHostMallocDefault));
-		CHECK(hipMalloc(&a.dev, off));
-		a.size = off;
-	}
-	if (!a.uploaded) CHECK(hipEventCreateWithFlags(&a.uploaded, hipEventDisableTiming));
-	m2r_picture_t &p = a.pic;
-	memset(&p, 0, sizeof(p));
-	p.width_mbs = wm;
-	p.height_mbs = hm;
-	p.mb = (m2r_mb_t *)(a.host + a.off_mb);
-	p.dbk = (m2r_deblock_t *)(a.host + a.off_dbk);
-	p.slice = (m2r_slice_t *)(a.host + a.off_slice);
-	p.inter = (m2r_inter_t *)(a.host + a.off_inter);
-	p.coef = (int16_t *)(a.host + a.off_coef);
-	p.cap_slices = kSlicesCap;
-	p.cap_inter = (int)n;
-	p.cap_coef = (int)(n * 416);
-	return 0;
-}
-
-static m2r_picture_t *be_acquire(void *self, int wm, int hm)
-{
-	HipBackend *b = (HipBackend *)self;
-	Arena &a = b->ar[b->next];
-	b->next = (b->next + 1) % 3;
-	if (a.pending) {
-		if (hipEventSynchronize(a.uploaded) != hipSuccess) return nullptr;
-		a.pending = false;
-	}
-	if (arena_alloc(a, wm, hm) < 0) return nullptr;
-	return &a.pic;
-}
-
-static int64_t ref_bytes_of(const m2r_picture_t *pic)
-{
-	/* algorithmic MC input: one reference byte per predicted sample per list */
-	int64_t s = 0;
-	for (int i = 0; i < pic->n_inter; ++i)
-		for (int l = 0; l < 2; ++l)
-			for (int b8 = 0; b8 < 4; ++b8)
-				if (pic->inter[i].slot[l][b8] >= 0) s += 64 + 32;
-	return s;
-}
-
-static int be_submit(void *self, m2r_picture_t *pic)
-{
-	HipBackend *b = (HipBackend *)self;
-	Arena *a = nullptr;
-	for (auto &x : b->ar)
-		if (&x.pic == pic) a = &x;
-	if (!a) return -1;
-	const int n = pic->width_mbs * pic->height_mbs;
-	if (pic->width_mbs != b->Wmb || pic->height_mbs != b->Hmb || pic->slot < 0 || pic->slot >= b->nframes) return -1;
-	CHECK(hipSetDevice(b->dev));
-	hipStream_t s = b->stream;
-	size_t rec_bytes = n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t)) + pic->n_slices * sizeof(m2r_slice_t) +
-	                   pic->n_inter * sizeof(m2r_inter_t) + pic->n_coef * sizeof(int16_t);
-	hipEvent_t *ev = b->ev[b->ev_next];
-	if (b->timing) {
-		flush_timing(b, b->ev_next);
-		CHECK(hipEventRecord(ev[0], s));
-	}
-	CHECK(hipMemcpyAsync(a->dev + a->off_mb, a->host + a->off_mb, a->off_slice - a->off_mb, hipMemcpyHostToDevice, s));
-	if (pic->n_slices) CHECK(hipMemcpyAsync(a->dev + a->off_slice, a->host + a->off_slice, pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
-	if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, a->host + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
-	if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
-	CHECK(hipEventRecord(a->uploaded, s));
-	a->pending = true;
-	if (b->timing) CHECK(hipEventRecord(ev[1], s));
-	RecPtrs rp;
-	rp.mb = (const m2r_mb_t *)(a->dev + a->off_mb);
-	rp.dbk = (const m2r_deblock_t *)(a->dev + a->off_dbk);
-	rp.sl = (const m2r_slice_t *)(a->dev + a->off_slice);
-	rp.it = (const m2r_inter_t *)(a->dev + a->off_inter);
-	rp.coef = (const int16_t *)(a->dev + a->off_coef);
-	uint8_t *cur = b->d_frames + (size_t)pic->slot * b->fsz;
-	Geometry gm{b->d_frames, b->fsz, b->W, b->H, b->Wmb, b->Hmb, b->d_prog, b->d_err};
-	if (launch_picture(s, gm, rp, pic->slot, pic->n_inter, pic->n_intra, pic->deblock, b->timing ? ev + 2 : nullptr, &b->tm) < 0) return -1;
-	const m2d_frame_t &f = b->frames[pic->slot];
-	size_t ls = (size_t)b->W * b->H;
-	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
-	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
-	CHECK(hipEventRecord(b->slot_ev[pic->slot], s));
-	b->slot_pending[pic->slot] = true;
-	if (b->timing) {
-		CHECK(hipEventRecord(ev[5], s));
-		b->ev_pending[b->ev_next] = true;
-		b->ev_next = (b->ev_next + 1) % 4;
-	}
-	b->tm.pictures++;
-	b->tm.record_bytes += (int64_t)rec_bytes;
-	b->tm.ref_bytes += ref_bytes_of(pic);
-	b->tm.frame_bytes += (int64_t)(ls * 3 / 2);
-	return 0;
-}
-
-static int be_sync(void *self, int slot)
-{
-	HipBackend *b = (HipBackend *)self;
-	if (slot < 0 || slot >= 64) return -1;
-	if (b->slot_pending[slot]) {
-		CHECK(hipEventSynchronize(b->slot_ev[slot]));
-		b->slot_pending[slot] = false;
-		int err = 0;
-		CHECK(hipMemcpy(&err, b->d_err, sizeof(int), hipMemcpyDeviceToHost));
-		if (err) {
-			fprintf(stderr, "m2dec_amd: wavefront hand-off timed out (err=%d)\n", err);
-			return -1;
+	/* ---------------- storer (wave 2) */
+	{
+		int done = 0, nst = 0;
+		unsigned spins = 0;
+		while (done < Wmb) {
+			int f = __hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			int lim = (f >= Wmb) ? Wmb : f - 1; /* MB f-1 waits for MB f's vertical edges */
+			if (lim <= done) {
+				if (!spin_ok(spins, err, 8)) {
+					if (!last_row) signal_progress(&progress[y], Wmb); /* release the row below */
+					return;
+				}
+				continue;
+			}
+			const int n = lim - done;
+			/* the row below waits on the hand-off records: write them first, drain, publish */
+			if (!last_row) {
+				for (int g0 = 0; g0 < n * 12; g0 += 64) {
+					int g = g0 + t;
+					if (g < n * 12) {
+						int mb = done + g / 12, k = g % 12;
+						const uint8_t *sp = (k < 8) ? RL + (16 + (k >> 1)) * S + DBK_PAD + mb * 16 + (k & 1) * 8
+						                            : RC + (8 + ((k - 8) >> 1)) * S + DBK_PAD + mb * 16 + (k & 1) * 8;
+						uint2 v = *(const uint2 *)sp;
+						st_sc1(hbd + ((size_t)y * Wmb + mb) * HBD_BYTES + k * 8, ((unsigned long long)v.y << 32) | v.x);
+					}
+				}
+				signal_progress(&progress[y], lim);
+			}
+			/* final samples to the frame: luma rows 0..12 (all on the last row), the row above's rows 13..15 */
+			for (int k = t; k < n * 64; k += 64) {
+				int mb = done + (k >> 6), r = (k >> 2) & 15, c = (k & 3) * 4;
+				if (last_row || r <= 12)
+					*(uint32_t *)(cur + (size_t)(y0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (4 + r) * S + DBK_PAD + mb * 16 + c);
+			}
+			if (y > 0)
+				for (int k = t; k < n * 16; k += 64) {
+					int mb = done + (k >> 4), r = (k >> 2) & 3, c = (k & 3) * 4;
+					if (r < 3) *(uint32_t *)(cur + (size_t)(y0 - 3 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (1 + r) * S + DBK_PAD + mb * 16 + c);
+					else *(uint32_t *)(chroma + (size_t)(yc0 - 1) * W + mb * 16 + c) = *(const uint32_t *)(RC + 1 * S + DBK_PAD + mb * 16 + c);
+				}
+			for (int k = t; k < n * 32; k += 64) {
+				int mb = done + (k >> 5), r = (k >> 2) & 7, c = (k & 3) * 4;
+				if (last_row || r <= 6)
+					*(uint32_t *)(chroma + (size_t)(yc0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RC + (2 + r) * S + DBK_PAD + mb * 16 + c);
+			}
+			STAMP(y, 2, nst, lim);
+			nst++;
+			done = lim;
 		}
 	}
+}
+
+size_t m2r_deblock_lds_bytes(int W, int Wmb)
+{
+	return (size_t)30 * (W + 2 * DBK_PAD) + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16;
+}
+
+extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)
+{
+#ifdef M2DEC_STAMPS
+	size_t bytes = sizeof(unsigned long long) * STAMP_ROWS * 4 * STAMP_EV;
+	if (n * sizeof(unsigned long long) < bytes) return -1;
+	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
+	return (int)(bytes / sizeof(unsigned long long));
+#else
+	(void)out;
+	(void)n;
+	return -1;
+#endif
+}
+
+extern "C" int m2dec_amd_debug_stamps_clear(void)
+{
+#ifdef M2DEC_STAMPS
+	static unsigned long long zero[STAMP_ROWS][4][STAMP_EV];
+	CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice));
 	return 0;
-}
-
-static void be_destroy(void *self)
-{
-	HipBackend *b = (HipBackend *)self;
-	(void)hipSetDevice(b->dev);
-	(void)hipStreamSynchronize(b->stream);
-	unregister_frames(b);
-	for (auto &a : b->ar) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
-		if (a.uploaded) (void)hipEventDestroy(a.uploaded);
-	}
-	for (int i = 0; i < 64; ++i) (void)hipEventDestroy(b->slot_ev[i]);
-	for (int k = 0; k < 4; ++k)
-		for (int i = 0; i < 6; ++i) (void)hipEventDestroy(b->ev[k][i]);
-	if (b->d_frames) (void)hipFree(b->d_frames);
-	if (b->d_prog) (void)hipFree(b->d_prog);
-	if (b->d_err) (void)hipFree(b->d_err);
-	(void)hipStreamDestroy(b->stream);
-	delete b;
-}
-
-} // namespace
-
-extern "C" int m2dec_amd_hip_available(void)
-{
-	int n = 0;
-	if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-	return n > 0;
-}
-
-extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
-{
-	if (!m2dec_amd_hip_available()) return -1;
-	HipBackend *b = new HipBackend();
-	memset(&b->tm, 0, sizeof(b->tm));
-	memset(b->reg, 0, sizeof(b->reg));
-	memset(b->slot_pending, 0, sizeof(b->slot_pending));
-	b->dev = device;
-	CHECK(hipSetDevice(device));
-	CHECK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-	for (int i = 0; i < 64; ++i) CHECK(hipEventCreateWithFlags(&b->slot_ev[i], hipEventDisableTiming));
-	for (int k = 0; k < 4; ++k) {
-		b->ev_pending[k] = false;
-		for (int i = 0; i < 6; ++i) CHECK(hipEventCreate(&b->ev[k][i]));
-	}
-	CHECK(hipMalloc(&b->d_err, sizeof(int)));
-	CHECK(hipMemset(b->d_err, 0, sizeof(int)));
-	const char *tm = getenv("M2DEC_AMD_TIMING");
-	b->timing = tm ? atoi(tm) != 0 : true;
-	out->self = b;
-	out->set_frames = be_set_frames;
-	out->acquire = be_acquire;
-	out->submit = be_submit;
-	out->sync_frame = be_sync;
-	out->destroy = be_destroy;
-	return 0;
-}
-
-extern "C" int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out)
-{
-	if (!be || !be->self || !out) return -1;
-	HipBackend *b = (HipBackend *)be->self;
-	for (int k = 0; k < 4; ++k) flush_timing(b, k);
-	*out = b->tm;
-	return 0;
-}
-
-/* ======================================================================== trace replay */
-struct m2dec_amd_hip_replay {
-	int dev = 0;
-	hipStream_t stream = nullptr;
-	int W = 0, H = 0, Wmb = 0, Hmb = 0, nslots = 0, npics = 0;
-	int crop[4] = {0, 0, 0, 0};
-	size_t fsz = 0;
-	uint8_t *d_frames = nullptr, *d_rec = nullptr;
-	int *d_prog = nullptr, *d_err = nullptr;
-	m2dec_amd_trace_pic_t *pics = nullptr;
-	/* timing: 4 events per enqueued picture (start, after inter, after intra, after deblock) */
-	hipEvent_t *ev = nullptr;
-	int ev_cap = 0, ev_used = 0;
-	m2dec_amd_hip_timing_t tm;
-};
-
-static void replay_free(m2dec_amd_hip_replay_t *r)
-{
-	(void)hipSetDevice(r->dev);
-	if (r->stream) (void)hipStreamSynchronize(r->stream);
-	for (int i = 0; i < r->ev_cap; ++i) (void)hipEventDestroy(r->ev[i]);
-	free(r->ev);
-	free(r->pics);
-	if (r->d_frames) (void)hipFree(r->d_frames);
-	if (r->d_rec) (void)hipFree(r->d_rec);
-	if (r->d_prog) (void)hipFree(r->d_prog);
-	if (r->d_err) (void)hipFree(r->d_err);
-	if (r->stream) (void)hipStreamDestroy(r->stream);
-	delete r;
-}
-
-extern "C" int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out)
-{
-	int npics, W, H, nslots, nout;
-	size_t len;
-	if (!t || !out || !m2dec_amd_hip_available()) return -1;
-	if (m2dec_amd_trace_info(t, &npics, &W, &H, &nslots, &nout) < 0 || npics <= 0 || W <= 0 || H <= 0) return -1;
-	const uint8_t *rec = m2dec_amd_trace_records(t, &len);
-	const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(t);
-	for (int i = 0; i < npics; ++i)
-		if (pics[i].slot < 0 || pics[i].slot >= nslots || pics[i].width_mbs != W / 16 || pics[i].height_mbs != H / 16) return -1;
-	m2dec_amd_hip_replay_t *r = new m2dec_amd_hip_replay_t();
-	memset(&r->tm, 0, sizeof(r->tm));
-	r->dev = device;
-	r->W = W;
-	r->H = H;
-	r->Wmb = W / 16;
-	r->Hmb = H / 16;
-	r->nslots = nslots;
-	r->npics = npics;
-	m2dec_amd_trace_crop(t, r->crop);
-	r->fsz = ((size_t)W * H * 3 / 2 + 4095) & ~(size_t)4095;
-	r->pics = (m2dec_amd_trace_pic_t *)malloc(sizeof(*pics) * (size_t)npics);
-	memcpy(r->pics, pics, sizeof(*pics) * (size_t)npics);
-#define RCHECK(x) do { if ((x) != hipSuccess) { fprintf(stderr, "m2dec_amd replay: %s failed\n", #x); replay_free(r); return -1; } } while (0)
-	RCHECK(hipSetDevice(device));
-	RCHECK(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-	RCHECK(hipMalloc(&r->d_frames, r->fsz * (size_t)nslots));
-	RCHECK(hipMemset(r->d_frames, 0, r->fsz * (size_t)nslots));
-	RCHECK(hipMalloc(&r->d_rec, len));
-	RCHECK(hipMemcpy(r->d_rec, rec, len, hipMemcpyHostToDevice));
-	RCHECK(hipMalloc(&r->d_prog, sizeof(int) * 2 * (size_t)r->Hmb));
-	RCHECK(hipMalloc(&r->d_err, sizeof(int)));
-	RCHECK(hipMemset(r->d_err, 0, sizeof(int)));
-#undef RCHECK
-	*out = r;
-	return 0;
-}
-
-static int replay_enqueue(m2dec_amd_hip_replay_t *r, int i, bool timed)
-{
-	const m2dec_amd_trace_pic_t &p = r->pics[i];
-	RecPtrs rp;
-	rp.mb = (const m2r_mb_t *)(r->d_rec + p.off_mb);
-	rp.dbk = (const m2r_deblock_t *)(r->d_rec + p.off_dbk);
-	rp.sl = (const m2r_slice_t *)(r->d_rec + p.off_slice);
-	rp.it = (const m2r_inter_t *)(r->d_rec + p.off_inter);
-	rp.coef = (const int16_t *)(r->d_rec + p.off_coef);
-	Geometry gm{r->d_frames, r->fsz, r->W, r->H, r->Wmb, r->Hmb, r->d_prog, r->d_err};
-	hipEvent_t *ev = nullptr;
-	if (timed) {
-		if (r->ev_used + 4 > r->ev_cap) {
-			int nc = r->ev_cap ? r->ev_cap * 2 : 1024;
-			hipEvent_t *ne = (hipEvent_t *)realloc(r->ev, sizeof(hipEvent_t) * (size_t)nc);
-			if (!ne) return -1;
-			r->ev = ne;
-			for (int k = r->ev_cap; k < nc; ++k) CHECK(hipEventCreate(&r->ev[k]));
-			r->ev_cap = nc;
-		}
-		ev = r->ev + r->ev_used;
-		r->ev_used += 4;
-		CHECK(hipEventRecord(ev[0], r->stream));
-	}
-	if (launch_picture(r->stream, gm, rp, p.slot, p.n_inter, p.n_intra, p.deblock, ev ? ev + 1 : nullptr, &r->tm) < 0) return -1;
-	r->tm.pictures++;
-	r->tm.record_bytes += p.record_bytes;
-	r->tm.ref_bytes += p.ref_bytes;
-	r->tm.frame_bytes += p.frame_bytes;
-	return 0;
-}
-
-extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
-{
-	if (!r) return -1;
-	CHECK(hipSetDevice(r->dev));
-	for (int k = 0; k < passes; ++k)
-		for (int i = 0; i < r->npics; ++i)
-			if (replay_enqueue(r, i, true) < 0) return -1;
-	return 0;
-}
-
-extern "C" int m2dec_amd_hip_replay_sync(m2dec_amd_hip_replay_t *r)
-{
-	int err = 0;
-	if (!r) return -1;
-	CHECK(hipSetDevice(r->dev));
-	CHECK(hipStreamSynchronize(r->stream));
-	CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
-	if (err) {
-		fprintf(stderr, "m2dec_amd replay: wavefront hand-off timed out (err=%d)\n", err);
-		return -1;
-	}
-	return 0;
-}
-
-extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_hip_timing_t *out, int reset)
-{
-	if (!r || !out) return -1;
-	CHECK(hipSetDevice(r->dev));
-	for (int i = 0; i + 4 <= r->ev_used; i += 4) {
-		float ms;
-		hipEvent_t *e = r->ev + i;
-		CHECK(hipEventSynchronize(e[3]));
-		if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) r->tm.inter_us += ms * 1e3;
-		if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess) r->tm.intra_us += ms * 1e3;
-		if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess) r->tm.deblock_us += ms * 1e3;
-	}
-	r->ev_used = 0;
-	*out = r->tm;
-	if (reset) memset(&r->tm, 0, sizeof(r->tm));
-	return 0;
-}
-
-extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
-{
-	if (!r || !md5s) return -1;
-	size_t ls = (size_t)r->W * r->H;
-	uint8_t *host = (uint8_t *)malloc(ls * 3 / 2);
-	if (!host) return -1;
-	CHECK(hipSetDevice(r->dev));
-	for (int i = 0; i < r->npics; ++i) {
-		if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) {
-			free(host);
-			return -1;
-		}
-		if (hipMemcpy(host, r->d_frames + (size_t)r->pics[i].slot * r->fsz, ls * 3 / 2, hipMemcpyDeviceToHost) != hipSuccess) {
-			free(host);
-			return -1;
-		}
-		m2d_frame_t f;
-		memset(&f, 0, sizeof(f));
-		f.luma = host;
-		f.chroma = host + ls;
-		f.width = (int16_t)r->W;
-		f.height = (int16_t)r->H;
-		for (int k = 0; k < 4; ++k) f.crop[k] = (int16_t)r->crop[k];
-		m2dec_amd_frame_md5(&f, md5s + 35 * (size_t)i);
-	}
-	free(host);
-	return 0;
-}
-
-extern "C" void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r)
-{
-	if (r) replay_free(r);
+#else
+	return -1;
+#endif
 }

@@ -1,0 +1,651 @@
+/*
+ * Host runtime of the gfx950 reconstruction back end: the picture scheduler, the m2r_backend_t
+ * behind h264d_func (decode path), and the trace replay used by bench.py.
+ *
+ * Picture scheduler.  A picture is three launches (k_inter -> k_intra -> k_deblock) that must run in
+ * order; different pictures only depend on each other through frame slots:
+ *   - read-after-write : a picture's k_inter reads its reference slots, so it waits for the launch
+ *                        sequence that last wrote each of them;
+ *   - write-after-read : a picture overwrites its destination slot only after every k_inter that
+ *                        read the slot's previous content has finished (and after that content's
+ *                        own writer and device-to-host copy).
+ * Pictures are dealt round-robin over NSTREAMS HIP streams with exactly those event waits, so a
+ * B picture runs beside the next anchor picture and other B pictures (IBBP: three pictures in
+ * flight), each wavefront kernel using ~Hmb CUs of the 256.  Each stream owns its progress words and
+ * hand-off records; the frame pool and the error word are shared.
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include "recon_internal.h"
+#include "m2dec_amd.h"
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
+
+namespace {
+
+const int NSTREAMS = 4;
+const int NEVENTS = 4096; /* recycled sync events: far more than the pictures a dependency can span */
+
+struct RecPtrs {
+	const m2r_mb_t *mb;
+	const m2r_deblock_t *dbk;
+	const m2r_slice_t *sl;
+	const m2r_inter_t *it;
+	const int16_t *coef;
+};
+
+/* per-picture launch description */
+struct PicJob {
+	RecPtrs r;
+	int slot, n_inter, n_intra, deblock;
+	uint64_t refs; /* bit per reference slot read by k_inter */
+};
+
+struct Sched {
+	int dev = 0;
+	int W = 0, H = 0, Wmb = 0, Hmb = 0, nslots = 0;
+	size_t fsz = 0;
+	uint8_t *frames = nullptr; /* device frame pool [nslots] x fsz */
+	hipStream_t st[NSTREAMS] = {};
+	int *prog = nullptr;       /* [NSTREAMS][2][Hmb] */
+	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
+	int *err = nullptr;
+	int rr = 0;
+	hipEvent_t ev[NEVENTS] = {};
+	int ev_next = 0;
+	hipEvent_t slot_write[64] = {};
+	std::vector<hipEvent_t> readers[64];
+	size_t lds_set = 0;
+	m2dec_amd_hip_timing_t tm;
+
+	int init(int device)
+	{
+		dev = device;
+		memset(&tm, 0, sizeof(tm));
+		CHECK(hipSetDevice(dev));
+		for (auto &s : st) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+		for (auto &e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+		CHECK(hipMalloc(&err, 16));
+		CHECK(hipMemset(err, 0, 16));
+		return 0;
+	}
+
+	/* (re)size the frame pool and per-stream scratch */
+	int configure(int width, int height, int n)
+	{
+		CHECK(hipSetDevice(dev));
+		for (auto &s : st) CHECK(hipStreamSynchronize(s));
+		size_t nfsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
+		if (frames && (nfsz != fsz || n > nslots)) {
+			(void)hipFree(frames);
+			frames = nullptr;
+		}
+		if (!frames) {
+			CHECK(hipMalloc(&frames, nfsz * (size_t)n));
+			CHECK(hipMemset(frames, 0, nfsz * (size_t)n));
+			nslots = n;
+		}
+		if (prog && (width / 16 != Wmb || height / 16 != Hmb)) {
+			(void)hipFree(prog);
+			(void)hipFree(hand);
+			prog = nullptr;
+			hand = nullptr;
+		}
+		W = width;
+		H = height;
+		Wmb = width / 16;
+		Hmb = height / 16;
+		fsz = nfsz;
+		if (!prog) {
+			CHECK(hipMalloc(&prog, sizeof(int) * 2 * (size_t)Hmb * NSTREAMS));
+			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
+		}
+		for (int i = 0; i < 64; ++i) {
+			slot_write[i] = nullptr;
+			readers[i].clear();
+		}
+		size_t lds = m2r_deblock_lds_bytes(W, Wmb);
+		if (lds > 65536 && lds > lds_set) {
+			CHECK(hipFuncSetAttribute((const void *)k_deblock, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+			lds_set = lds;
+		}
+		return 0;
+	}
+
+	size_t hand_bytes() const { return (size_t)Hmb * Wmb * (HBI_BYTES + HBD_BYTES); }
+
+	hipEvent_t next_event()
+	{
+		hipEvent_t e = ev[ev_next];
+		ev_next = (ev_next + 1) % NEVENTS;
+		return e;
+	}
+
+	/* pick a stream for a picture writing `slot` and reading `refs`; enqueue its dependency waits */
+	int begin(int slot, uint64_t refs)
+	{
+		int k = rr;
+		rr = (rr + 1) % NSTREAMS;
+		hipStream_t s = st[k];
+		for (int r = 0; r < 64; ++r)
+			if (((refs >> r) & 1) && slot_write[r]) CHECK(hipStreamWaitEvent(s, slot_write[r], 0));
+		for (hipEvent_t e : readers[slot]) CHECK(hipStreamWaitEvent(s, e, 0));
+		if (slot_write[slot]) CHECK(hipStreamWaitEvent(s, slot_write[slot], 0));
+		return k;
+	}
+
+	/* k_inter, k_intra, k_deblock of one picture on stream k; tev (optional) gets records after
+	 * each of the three; returns the event recorded after k_inter (reader event) through inter_done */
+	int launch(int k, const PicJob &j, hipEvent_t *tev, hipEvent_t *inter_done)
+	{
+		hipStream_t s = st[k];
+		uint8_t *cur = frames + (size_t)j.slot * fsz;
+		int *pr = prog + (size_t)k * 2 * Hmb;
+		uint8_t *hbi = hand + (size_t)k * hand_bytes();
+		uint8_t *hbd = hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+		if (j.n_inter) {
+			hipLaunchKernelGGL(k_inter, dim3(Wmb * Hmb), dim3(256), 0, s, j.r.mb, j.r.it, j.r.sl, j.r.coef, frames, fsz, W, H,
+			                   Wmb, j.slot);
+			CHECK(hipGetLastError());
+			tm.inter_launches++;
+		}
+		*inter_done = next_event();
+		CHECK(hipEventRecord(*inter_done, s));
+		if (tev) CHECK(hipEventRecord(tev[0], s));
+		if (j.n_intra) {
+			CHECK(hipMemsetAsync(pr, 0, sizeof(int) * Hmb, s));
+			hipLaunchKernelGGL(k_intra, dim3(Hmb), dim3(64), 0, s, j.r.mb, j.r.coef, cur, W, H, Wmb, hbi, pr, err);
+			CHECK(hipGetLastError());
+			tm.intra_launches++;
+		}
+		if (tev) CHECK(hipEventRecord(tev[1], s));
+		if (j.deblock) {
+			CHECK(hipMemsetAsync(pr + Hmb, 0, sizeof(int) * Hmb, s));
+			hipLaunchKernelGGL(k_deblock, dim3(Hmb), dim3(64 * DBK_WAVES), m2r_deblock_lds_bytes(W, Wmb), s, j.r.dbk, cur, W,
+			                   H, Wmb, Hmb, hbd, pr + Hmb, err);
+			CHECK(hipGetLastError());
+			tm.deblock_launches++;
+		}
+		if (tev) CHECK(hipEventRecord(tev[2], s));
+		return 0;
+	}
+
+	/* after everything that touches the picture's slot on stream k was enqueued (incl. any copy) */
+	int end(int k, const PicJob &j, hipEvent_t inter_done)
+	{
+		hipEvent_t w = next_event();
+		CHECK(hipEventRecord(w, st[k]));
+		for (int r = 0; r < 64; ++r)
+			if ((j.refs >> r) & 1) readers[r].push_back(inter_done);
+		readers[j.slot].clear();
+		slot_write[j.slot] = w;
+		return 0;
+	}
+
+	int sync_all()
+	{
+		CHECK(hipSetDevice(dev));
+		for (auto &s : st) CHECK(hipStreamSynchronize(s));
+		return 0;
+	}
+
+	int check_err()
+	{
+		int e = 0;
+		CHECK(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
+		if (e) {
+			fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e);
+			return -1;
+		}
+		return 0;
+	}
+
+	void destroy()
+	{
+		(void)hipSetDevice(dev);
+		for (auto &s : st)
+			if (s) (void)hipStreamSynchronize(s);
+		for (auto &e : ev)
+			if (e) (void)hipEventDestroy(e);
+		if (frames) (void)hipFree(frames);
+		if (prog) (void)hipFree(prog);
+		if (hand) (void)hipFree(hand);
+		if (err) (void)hipFree(err);
+		for (auto &s : st)
+			if (s) (void)hipStreamDestroy(s);
+	}
+};
+
+uint64_t refs_of(const m2r_inter_t *it, int n)
+{
+	uint64_t m = 0;
+	for (int i = 0; i < n; ++i)
+		for (int l = 0; l < 2; ++l)
+			for (int b = 0; b < 4; ++b)
+				if (it[i].slot[l][b] >= 0) m |= 1ull << (it[i].slot[l][b] & 63);
+	return m;
+}
+
+int64_t ref_bytes_of(const m2r_inter_t *it, int n)
+{
+	/* algorithmic MC input: one reference byte per predicted sample per list */
+	int64_t s = 0;
+	for (int i = 0; i < n; ++i)
+		for (int l = 0; l < 2; ++l)
+			for (int b = 0; b < 4; ++b)
+				if (it[i].slot[l][b] >= 0) s += 64 + 32;
+	return s;
+}
+
+/* ======================================================================== decode-path back end */
+const int kSlicesCap = 64;
+const int kArenas = 2 * NSTREAMS;
+
+struct Arena {
+	m2r_picture_t pic;
+	uint8_t *host = nullptr, *dev = nullptr;
+	size_t size = 0, off_mb = 0, off_dbk = 0, off_slice = 0, off_inter = 0, off_coef = 0;
+	hipEvent_t consumed = nullptr; /* the picture's kernels finished reading the device copy */
+	bool pending = false;
+};
+
+struct TimingSlot {
+	hipEvent_t e[6]; /* start, uploaded, after inter, after intra, after deblock, after D2H */
+	bool pending = false;
+};
+
+struct HipBackend {
+	Sched sc;
+	m2d_frame_t frames[64];
+	void *reg[64][2];
+	hipEvent_t slot_ev[64];
+	bool slot_pending[64];
+	Arena ar[kArenas];
+	int next = 0;
+	TimingSlot tr[16];
+	int tr_next = 0;
+	bool timing = true;
+};
+
+void flush_timing(HipBackend *b, TimingSlot &t)
+{
+	if (!t.pending) return;
+	float ms;
+	(void)hipEventSynchronize(t.e[5]);
+	m2dec_amd_hip_timing_t &tm = b->sc.tm;
+	if (hipEventElapsedTime(&ms, t.e[0], t.e[1]) == hipSuccess) tm.h2d_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) tm.inter_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[2], t.e[3]) == hipSuccess) tm.intra_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[3], t.e[4]) == hipSuccess) tm.deblock_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[4], t.e[5]) == hipSuccess) tm.d2h_us += ms * 1e3;
+	t.pending = false;
+}
+
+void unregister_frames(HipBackend *b)
+{
+	for (int i = 0; i < 64; ++i)
+		for (int k = 0; k < 2; ++k)
+			if (b->reg[i][k]) {
+				(void)hipHostUnregister(b->reg[i][k]);
+				b->reg[i][k] = nullptr;
+			}
+}
+
+int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
+{
+	HipBackend *b = (HipBackend *)self;
+	if (b->sc.sync_all() < 0) return -1;
+	unregister_frames(b);
+	if (n > 64) n = 64;
+	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
+	if (b->sc.configure(width, height, n) < 0) return -1;
+	size_t ls = (size_t)width * height, cs = ls / 2;
+	for (int i = 0; i < n; ++i) {
+		b->slot_pending[i] = false;
+		if (b->frames[i].chroma == b->frames[i].luma + ls) {
+			if (hipHostRegister(b->frames[i].luma, ls + cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
+		} else {
+			if (hipHostRegister(b->frames[i].luma, ls, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
+			if (hipHostRegister(b->frames[i].chroma, cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][1] = b->frames[i].chroma;
+		}
+		(void)hipGetLastError();
+	}
+	return 0;
+}
+
+int arena_alloc(Arena &a, int wm, int hm)
+{
+	size_t n = (size_t)wm * hm;
+	size_t off = 0;
+	auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+	a.off_mb = off; off = al(off + n * sizeof(m2r_mb_t));
+	a.off_dbk = off; off = al(off + n * sizeof(m2r_deblock_t));
+	a.off_slice = off; off = al(off + kSlicesCap * sizeof(m2r_slice_t));
+	a.off_inter = off; off = al(off + n * sizeof(m2r_inter_t));
+	a.off_coef = off; off = al(off + n * 416 * sizeof(int16_t));
+	if (a.size < off) {
+		if (a.host) (void)hipHostFree(a.host);
+		if (a.dev) (void)hipFree(a.dev);
+		a.host = nullptr;
+		a.dev = nullptr;
+		CHECK(hipHostMalloc(&a.host, off, hipHostMallocDefault));
+		CHECK(hipMalloc(&a.dev, off));
+		a.size = off;
+	}
+	if (!a.consumed) CHECK(hipEventCreateWithFlags(&a.consumed, hipEventDisableTiming));
+	m2r_picture_t &p = a.pic;
+	memset(&p, 0, sizeof(p));
+	p.width_mbs = wm;
+	p.height_mbs = hm;
+	p.mb = (m2r_mb_t *)(a.host + a.off_mb);
+	p.dbk = (m2r_deblock_t *)(a.host + a.off_dbk);
+	p.slice = (m2r_slice_t *)(a.host + a.off_slice);
+	p.inter = (m2r_inter_t *)(a.host + a.off_inter);
+	p.coef = (int16_t *)(a.host + a.off_coef);
+	p.cap_slices = kSlicesCap;
+	p.cap_inter = (int)n;
+	p.cap_coef = (int)(n * 416);
+	return 0;
+}
+
+m2r_picture_t *be_acquire(void *self, int wm, int hm)
+{
+	HipBackend *b = (HipBackend *)self;
+	Arena &a = b->ar[b->next];
+	b->next = (b->next + 1) % kArenas;
+	if (a.pending) {
+		/* the host copy is overwritten next: wait until that picture's kernels are done with it */
+		if (hipEventSynchronize(a.consumed) != hipSuccess) return nullptr;
+		a.pending = false;
+	}
+	if (arena_alloc(a, wm, hm) < 0) return nullptr;
+	return &a.pic;
+}
+
+int be_submit(void *self, m2r_picture_t *pic)
+{
+	HipBackend *b = (HipBackend *)self;
+	Sched &sc = b->sc;
+	Arena *a = nullptr;
+	for (auto &x : b->ar)
+		if (&x.pic == pic) a = &x;
+	if (!a) return -1;
+	const int n = pic->width_mbs * pic->height_mbs;
+	if (pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots) return -1;
+	if (pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) return -1;
+	CHECK(hipSetDevice(sc.dev));
+	PicJob j;
+	j.slot = pic->slot;
+	j.n_inter = pic->n_inter;
+	j.n_intra = pic->n_intra;
+	j.deblock = pic->deblock;
+	j.refs = refs_of(pic->inter, pic->n_inter) & ~(1ull << pic->slot);
+	j.r.mb = (const m2r_mb_t *)(a->dev + a->off_mb);
+	j.r.dbk = (const m2r_deblock_t *)(a->dev + a->off_dbk);
+	j.r.sl = (const m2r_slice_t *)(a->dev + a->off_slice);
+	j.r.it = (const m2r_inter_t *)(a->dev + a->off_inter);
+	j.r.coef = (const int16_t *)(a->dev + a->off_coef);
+	size_t rec_bytes = n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t)) + pic->n_slices * sizeof(m2r_slice_t) +
+	                   pic->n_inter * sizeof(m2r_inter_t) + pic->n_coef * sizeof(int16_t);
+
+	const int k = sc.begin(j.slot, j.refs);
+	if (k < 0) return -1;
+	hipStream_t s = sc.st[k];
+	TimingSlot *ts = nullptr;
+	if (b->timing) {
+		ts = &b->tr[b->tr_next];
+		b->tr_next = (b->tr_next + 1) % 16;
+		flush_timing(b, *ts);
+		CHECK(hipEventRecord(ts->e[0], s));
+	}
+	CHECK(hipMemcpyAsync(a->dev + a->off_mb, a->host + a->off_mb, a->off_slice - a->off_mb, hipMemcpyHostToDevice, s));
+	if (pic->n_slices) CHECK(hipMemcpyAsync(a->dev + a->off_slice, a->host + a->off_slice, pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
+	if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, a->host + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
+	if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+	if (ts) CHECK(hipEventRecord(ts->e[1], s));
+	hipEvent_t inter_done;
+	if (sc.launch(k, j, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
+	CHECK(hipEventRecord(a->consumed, s));
+	a->pending = true;
+	const m2d_frame_t &f = b->frames[pic->slot];
+	uint8_t *cur = sc.frames + (size_t)pic->slot * sc.fsz;
+	size_t ls = (size_t)sc.W * sc.H;
+	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
+	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
+	CHECK(hipEventRecord(b->slot_ev[pic->slot], s));
+	b->slot_pending[pic->slot] = true;
+	if (ts) {
+		CHECK(hipEventRecord(ts->e[5], s));
+		ts->pending = true;
+	}
+	if (sc.end(k, j, inter_done) < 0) return -1;
+	sc.tm.pictures++;
+	sc.tm.record_bytes += (int64_t)rec_bytes;
+	sc.tm.ref_bytes += ref_bytes_of(pic->inter, pic->n_inter);
+	sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
+	return 0;
+}
+
+int be_sync(void *self, int slot)
+{
+	HipBackend *b = (HipBackend *)self;
+	if (slot < 0 || slot >= 64) return -1;
+	if (b->slot_pending[slot]) {
+		CHECK(hipEventSynchronize(b->slot_ev[slot]));
+		b->slot_pending[slot] = false;
+		if (b->sc.check_err() < 0) return -1;
+	}
+	return 0;
+}
+
+void be_destroy(void *self)
+{
+	HipBackend *b = (HipBackend *)self;
+	b->sc.sync_all();
+	unregister_frames(b);
+	for (auto &a : b->ar) {
+		if (a.host) (void)hipHostFree(a.host);
+		if (a.dev) (void)hipFree(a.dev);
+		if (a.consumed) (void)hipEventDestroy(a.consumed);
+	}
+	for (int i = 0; i < 64; ++i) (void)hipEventDestroy(b->slot_ev[i]);
+	for (auto &t : b->tr)
+		for (auto &e : t.e) (void)hipEventDestroy(e);
+	b->sc.destroy();
+	delete b;
+}
+
+} // namespace
+
+extern "C" int m2dec_amd_hip_available(void)
+{
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+	return n > 0;
+}
+
+extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
+{
+	if (!out || !m2dec_amd_hip_available()) return -1;
+	HipBackend *b = new HipBackend();
+	memset(b->reg, 0, sizeof(b->reg));
+	memset(b->slot_pending, 0, sizeof(b->slot_pending));
+	if (b->sc.init(device) < 0) {
+		delete b;
+		return -1;
+	}
+	for (int i = 0; i < 64; ++i) CHECK(hipEventCreateWithFlags(&b->slot_ev[i], hipEventDisableTiming));
+	for (auto &t : b->tr)
+		for (auto &e : t.e) CHECK(hipEventCreate(&e));
+	const char *tm = getenv("M2DEC_AMD_TIMING");
+	b->timing = tm ? atoi(tm) != 0 : true;
+	out->self = b;
+	out->set_frames = be_set_frames;
+	out->acquire = be_acquire;
+	out->submit = be_submit;
+	out->sync_frame = be_sync;
+	out->destroy = be_destroy;
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out)
+{
+	if (!be || !be->self || !out) return -1;
+	HipBackend *b = (HipBackend *)be->self;
+	for (auto &t : b->tr) flush_timing(b, t);
+	*out = b->sc.tm;
+	return 0;
+}
+
+/* ======================================================================== trace replay */
+struct m2dec_amd_hip_replay {
+	Sched sc;
+	int npics = 0;
+	int crop[4] = {0, 0, 0, 0};
+	uint8_t *d_rec = nullptr;
+	std::vector<m2dec_amd_trace_pic_t> pics;
+	std::vector<uint64_t> refs;
+	/* timing: 4 events per enqueued picture (start, after inter, after intra, after deblock) */
+	std::vector<hipEvent_t> tev;
+	size_t tev_used = 0;
+};
+
+static void replay_free(m2dec_amd_hip_replay_t *r)
+{
+	r->sc.sync_all();
+	for (hipEvent_t e : r->tev) (void)hipEventDestroy(e);
+	if (r->d_rec) (void)hipFree(r->d_rec);
+	r->sc.destroy();
+	delete r;
+}
+
+extern "C" int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out)
+{
+	int npics, W, H, nslots, nout;
+	size_t len;
+	if (!t || !out || !m2dec_amd_hip_available()) return -1;
+	if (m2dec_amd_trace_info(t, &npics, &W, &H, &nslots, &nout) < 0 || npics <= 0 || W <= 0 || H <= 0) return -1;
+	const uint8_t *rec = m2dec_amd_trace_records(t, &len);
+	const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(t);
+	for (int i = 0; i < npics; ++i)
+		if (pics[i].slot < 0 || pics[i].slot >= nslots || pics[i].width_mbs != W / 16 || pics[i].height_mbs != H / 16) return -1;
+	m2dec_amd_hip_replay_t *r = new m2dec_amd_hip_replay_t();
+	r->npics = npics;
+	m2dec_amd_trace_crop(t, r->crop);
+	r->pics.assign(pics, pics + npics);
+	for (int i = 0; i < npics; ++i)
+		r->refs.push_back(refs_of((const m2r_inter_t *)(rec + pics[i].off_inter), pics[i].n_inter) & ~(1ull << pics[i].slot));
+#define RCHECK(x) do { if ((x) != hipSuccess) { fprintf(stderr, "m2dec_amd replay: %s failed\n", #x); replay_free(r); return -1; } } while (0)
+	if (r->sc.init(device) < 0 || r->sc.configure(W, H, nslots) < 0) {
+		replay_free(r);
+		return -1;
+	}
+	RCHECK(hipMalloc(&r->d_rec, len));
+	RCHECK(hipMemcpy(r->d_rec, rec, len, hipMemcpyHostToDevice));
+#undef RCHECK
+	*out = r;
+	return 0;
+}
+
+static int replay_enqueue(m2dec_amd_hip_replay_t *r, int i, bool timed)
+{
+	const m2dec_amd_trace_pic_t &p = r->pics[i];
+	Sched &sc = r->sc;
+	PicJob j;
+	j.r.mb = (const m2r_mb_t *)(r->d_rec + p.off_mb);
+	j.r.dbk = (const m2r_deblock_t *)(r->d_rec + p.off_dbk);
+	j.r.sl = (const m2r_slice_t *)(r->d_rec + p.off_slice);
+	j.r.it = (const m2r_inter_t *)(r->d_rec + p.off_inter);
+	j.r.coef = (const int16_t *)(r->d_rec + p.off_coef);
+	j.slot = p.slot;
+	j.n_inter = p.n_inter;
+	j.n_intra = p.n_intra;
+	j.deblock = p.deblock;
+	j.refs = r->refs[i];
+	const int k = sc.begin(j.slot, j.refs);
+	if (k < 0) return -1;
+	hipEvent_t *ev = nullptr;
+	if (timed) {
+		while (r->tev_used + 4 > r->tev.size()) {
+			hipEvent_t e;
+			CHECK(hipEventCreate(&e));
+			r->tev.push_back(e);
+		}
+		ev = &r->tev[r->tev_used];
+		r->tev_used += 4;
+		CHECK(hipEventRecord(ev[0], sc.st[k]));
+	}
+	hipEvent_t inter_done;
+	if (sc.launch(k, j, ev ? ev + 1 : nullptr, &inter_done) < 0) return -1;
+	if (sc.end(k, j, inter_done) < 0) return -1;
+	sc.tm.pictures++;
+	sc.tm.record_bytes += p.record_bytes;
+	sc.tm.ref_bytes += p.ref_bytes;
+	sc.tm.frame_bytes += p.frame_bytes;
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
+{
+	if (!r) return -1;
+	CHECK(hipSetDevice(r->sc.dev));
+	for (int k = 0; k < passes; ++k)
+		for (int i = 0; i < r->npics; ++i)
+			if (replay_enqueue(r, i, true) < 0) return -1;
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_sync(m2dec_amd_hip_replay_t *r)
+{
+	if (!r) return -1;
+	if (r->sc.sync_all() < 0) return -1;
+	return r->sc.check_err();
+}
+
+extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_hip_timing_t *out, int reset)
+{
+	if (!r || !out) return -1;
+	CHECK(hipSetDevice(r->sc.dev));
+	for (size_t i = 0; i + 4 <= r->tev_used; i += 4) {
+		float ms;
+		hipEvent_t *e = &r->tev[i];
+		CHECK(hipEventSynchronize(e[3]));
+		if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) r->sc.tm.inter_us += ms * 1e3;
+		if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess) r->sc.tm.intra_us += ms * 1e3;
+		if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess) r->sc.tm.deblock_us += ms * 1e3;
+	}
+	r->tev_used = 0;
+	*out = r->sc.tm;
+	if (reset) memset(&r->sc.tm, 0, sizeof(r->sc.tm));
+	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
+{
+	if (!r || !md5s) return -1;
+	Sched &sc = r->sc;
+	size_t ls = (size_t)sc.W * sc.H;
+	std::vector<uint8_t> host(ls * 3 / 2);
+	CHECK(hipSetDevice(sc.dev));
+	for (int i = 0; i < r->npics; ++i) {
+		if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) return -1;
+		CHECK(hipMemcpy(host.data(), sc.frames + (size_t)r->pics[i].slot * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost));
+		m2d_frame_t f;
+		memset(&f, 0, sizeof(f));
+		f.luma = host.data();
+		f.chroma = host.data() + ls;
+		f.width = (int16_t)sc.W;
+		f.height = (int16_t)sc.H;
+		for (int k = 0; k < 4; ++k) f.crop[k] = (int16_t)r->crop[k];
+		m2dec_amd_frame_md5(&f, md5s + 35 * (size_t)i);
+	}
+	return 0;
+}
+
+extern "C" void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r)
+{
+	if (r) replay_free(r);
+}

@@ -2,7 +2,7 @@
 # GPU parity run: pytest -m gpu; on failure, per-picture HIP-vs-oracle diffs of every synthetic stream.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 240 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 tail -15 gpurun_out/pytest_gpu.log

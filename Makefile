@@ -19,7 +19,12 @@ LIB := m2dec_amd/lib/libm2dec_amd.so
 ORACLE := oracle/_build/liboracle.so
 GEN := tools/_build/h264gen
 
-all: $(LIB) $(ORACLE) $(GEN)
+APP := m2dec_amd/lib/h264dec
+
+all: $(LIB) $(ORACLE) $(GEN) $(APP)
+
+$(APP): m2dec_amd/csrc/app/h264dec.c $(LIB) include/m2dec_amd.h
+	$(CC) -O2 -Wall -std=gnu11 -Iinclude -o $@ $< -Lm2dec_amd/lib -lm2dec_amd -Wl,-rpath,'$$ORIGIN'
 
 build/host/%.o: m2dec_amd/csrc/host/%.c $(wildcard m2dec_amd/csrc/host/*.h) $(wildcard include/*.h)
 	@mkdir -p $(dir $@)

@@ -46,16 +46,20 @@ typedef struct {
 /* Bit-stream feeder.  The decoder pulls data through this object; when it runs dry it calls
  * error_func(error_arg), which is expected to call dec_bits_set_data() with the next chunk and
  * return 0, or return <0 at end of stream (reference bitio.c:112-126 protocol). */
+typedef uintptr_t cache_t;
+/* Field order and types follow the reference's struct dec_bits_t (bitio.h:39-50) so that code
+ * compiled against the reference's bitio.h (inline readers) sees the same layout. */
 typedef struct dec_bits_t {
+	cache_t cache_;
+	int cache_len_;
+	int8_t prev_[2];
 	const byte_t *buf_;
+	void (*load_bytes)(struct dec_bits_t *, int bytes);
 	const byte_t *buf_tail_;
 	const byte_t *buf_head_;
 	int (*error_func_)(void *);
 	void *error_arg_;
 	void *id;
-	void (*load_bytes)(struct dec_bits_t *, int bytes);
-	uint64_t cache_;
-	int cache_len_;
 	jmp_buf jmp;
 } dec_bits;
 

@@ -42,6 +42,11 @@ void m2dec_amd_h264_release(void *ctx);
 int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device,
                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
                             m2dec_amd_stats_t *stats);
+/* Same with an explicit DPB size (h264d_func->init's dpb_max: -1 = from the level, 1 = bypass; the
+ * reference's `h264dec -b / -d n`). */
+int m2dec_amd_decode_stream2(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                             m2dec_amd_stats_t *stats);
 
 /* HIP back end constructor (m2dec_amd/csrc/hip/recon_hip.hip). */
 int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device);

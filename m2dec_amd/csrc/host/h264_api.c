@@ -321,6 +321,12 @@ static int drv_header(void *arg, void *id)
 int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device,
                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
 {
+	return m2dec_amd_decode_stream2(data, len, backend, device, -1, on_frame, arg, stats);
+}
+
+int m2dec_amd_decode_stream2(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
+{
 	driver_t v;
 	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
 	m2d_frame_t frm;
@@ -330,7 +336,7 @@ int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t
 	v.d = d;
 	v.data = data;
 	v.len = len;
-	h264d_func->init(d, -1, drv_header, &v);
+	h264d_func->init(d, dpb, drv_header, &v);
 	d->device = device;
 	if (backend) m2dec_amd_h264_set_backend(d, backend);
 	dec_bits_set_callback(d->stream, drv_reread, &v);

@@ -54,7 +54,13 @@ $(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o
 
 stamps: $(DBG_LIB)
 
+# diagnostic variants: make variant V=NAME FLAGS="-DX"
+variant: $(HOST_OBJ) build/hip/runtime.o
+	@mkdir -p build/var
+	$(HIPCC) $(HIPFLAGS) $(FLAGS) -c $(HIP_SRC) -o build/var/recon_$(V).o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/var/lib_$(V).so $(HOST_OBJ) build/var/recon_$(V).o build/hip/runtime.o -Wl,--no-undefined
+
 clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build
 
-.PHONY: all clean stamps
+.PHONY: all clean stamps variant

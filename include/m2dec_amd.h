@@ -55,7 +55,8 @@ int m2dec_amd_hip_available(void);
 
 /* Per-kernel timing of the HIP back end since creation (microseconds, HIP events). */
 typedef struct {
-	double inter_us, intra_us, deblock_us, h2d_us, d2h_us;
+	double picture_us;      /* k_picture (inter + intra + deblock of one picture, overlapped row by row) */
+	double h2d_us, d2h_us;  /* decode path only: record upload, frame download */
 	int64_t pictures, inter_launches, intra_launches, deblock_launches;
 	int64_t record_bytes;   /* bytes of records uploaded (R_pic summed) */
 	int64_t ref_bytes;      /* algorithmic reference bytes read by MC (sum over PUs and lists) */

@@ -51,8 +51,8 @@ class Stats(ctypes.Structure):
 
 class HipTiming(ctypes.Structure):
     """m2dec_amd_hip_timing_t (include/m2dec_amd.h)."""
-    _fields_ = [("inter_us", ctypes.c_double), ("intra_us", ctypes.c_double), ("deblock_us", ctypes.c_double),
-                ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("pictures", ctypes.c_int64),
+    _fields_ = [("picture_us", ctypes.c_double), ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double),
+                ("pictures", ctypes.c_int64),
                 ("inter_launches", ctypes.c_int64), ("intra_launches", ctypes.c_int64),
                 ("deblock_launches", ctypes.c_int64), ("record_bytes", ctypes.c_int64),
                 ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64)]

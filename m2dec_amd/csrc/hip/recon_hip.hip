@@ -44,6 +44,11 @@ __device__ unsigned long long g_stamps[STAMP_ROWS][4][STAMP_EV];
 #else
 #define STAMP(row, role, idx, val) do { } while (0)
 #endif
+#if defined(M2DEC_STAMPS) && !defined(M2DEC_NO_STAMPI)
+#define STAMPI(row, role, idx, val) STAMP(row, role, idx, val)
+#else
+#define STAMPI(row, role, idx, val) do { } while (0)
+#endif
 
 /* ======================================================================== motion compensation */
 struct RefPlane {
@@ -142,14 +147,63 @@ __device__ __forceinline__ int combine(const m2r_slice_t *sl, const m2r_inter_t 
 	return use0 ? v0 : v1;
 }
 
-/* ======================================================================== k_inter */
-__global__ __launch_bounds__(256) void k_inter(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters,
-                                               const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool,
-                                               uint8_t *frames, size_t fsz, int W, int H, int Wmb, int slot)
+/* write-through hand-off primitives (cdna_hip_programming.md §6 Guideline 16, R1): every shared word is
+ * a global-address-space agent-scope access; payload 8-byte sc1 stores, drained before one lane's
+ * sc1 flag store; consumer polls the flag with sc1 loads and reads the payload with sc1 loads. */
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
+__device__ __forceinline__ void st_sc1(void *p, unsigned long long v)
 {
-	const int addr = blockIdx.x;
-	const m2r_mb_t m = mbs[addr];
-	if (m.kind != M2R_MB_INTER) return;
+	__hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long ld_sc1(const void *p)
+{
+	return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* bounded spin step: false once the spin budget is spent or another workgroup has flagged an error
+ * (so one failure drains the whole grid quickly instead of every row timing out in turn) */
+__device__ __forceinline__ bool spin_ok(unsigned &spins, int *err, int code)
+{
+	__builtin_amdgcn_s_sleep(1);
+	++spins;
+	if ((spins & 255) == 0 && __hip_atomic_load((gi32 *)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+	if (spins > SPIN_LIMIT) {
+		if ((threadIdx.x & 63) == 0) atomicOr(err, code);
+		return false;
+	}
+	return true;
+}
+
+__device__ __forceinline__ bool poll_ge(int *flag, int need, int *err)
+{
+	unsigned spins = 0;
+	while (__hip_atomic_load((gi32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+		if (!spin_ok(spins, err, 2)) return false;
+	}
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the payload loads below the poll */
+	return true;
+}
+
+__device__ __forceinline__ void signal_progress(int *flag, int value)
+{
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the (single) storing wave drains its sc1 stores */
+	if ((threadIdx.x & 63) == 0) __hip_atomic_store((gi32 *)flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* ======================================================================== k_inter */
+#ifdef M2DEC_NOINLINE
+#define M2DEC_INTER_MB_ATTR __attribute__((noinline))
+#else
+#define M2DEC_INTER_MB_ATTR
+#endif
+/* one inter macroblock, all 256 lanes of the workgroup (uniform call) */
+__device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t *__restrict__ inters,
+                         const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
+                         size_t fsz, int W, int H, int Wmb, int slot)
+{
 	__shared__ int s_res[256 + 128];
 	__shared__ int s_cnt[4];
 	const int t = threadIdx.x;
@@ -197,11 +251,13 @@ __global__ __launch_bounds__(256) void k_inter(const m2r_mb_t *__restrict__ mbs,
 
 	uint8_t *dl = cur + (size_t)(mby * 16 + ly) * W + mbx * 16 + lx;
 	uint8_t *dc = cur + (size_t)W * H + (size_t)(mby * 8 + cy) * W + mbx * 16 + cx * 2 + cc;
-	if (m.cbp == 0) {
+#ifndef M2DEC_NO_EARLYRET
+	if (__builtin_amdgcn_readfirstlane(m.cbp) == 0) {
 		*dl = (uint8_t)predl;
 		if (t < 128) *dc = (uint8_t)predc;
-		return;
+		return; /* uniform: m is the same in every lane */
 	}
+#endif
 
 	/* ---- residual: dequantise into LDS */
 	const int t8 = (m.flags & M2R_FLAG_T8x8) != 0;
@@ -303,50 +359,126 @@ __global__ __launch_bounds__(256) void k_inter(const m2r_mb_t *__restrict__ mbs,
 	if (t < 128) *dc = (uint8_t)d_clip255(predc + s_res[256 + cc * 64 + cy * 8 + cx]);
 }
 
-/* write-through hand-off primitives (cdna_hip_programming.md §6 Guideline 16, R1): every shared word is
- * a global-address-space agent-scope access; payload 8-byte sc1 stores, drained before one lane's
- * sc1 flag store; consumer polls the flag with sc1 loads and reads the payload with sc1 loads. */
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) int gi32;
-
-__device__ __forceinline__ void st_sc1(void *p, unsigned long long v)
+/*
+ * Inter MBs as a bounded persistent grid.  Work items are (MB row, 8-MB segment) in raster order,
+ * dequeued from a per-launch counter.  Before its MBs, an item waits until every reference picture
+ * it reads has finished deblocking all the MB rows its motion vectors reach (rowflag[picture][row]
+ * = seq + 1, written by k_deblock after the row's last store and an agent release; polled with sc1
+ * loads, then ONE agent acquire): a picture's MC starts while its references are still being
+ * deblocked further down, so consecutive anchor pictures overlap row by row.  The grid is kept
+ * small (a fraction of the CUs) so that the spinning items can never keep the k_deblock they wait
+ * for off the device.
+ */
+__device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters,
+                             const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
+                             size_t fsz, int W, int H, int Wmb, int Hmb, int slot, const SlotSeq &ss, const int *rowflag,
+                             int *queue, int *inter_cnt, int *err)
 {
-	__hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ unsigned long long ld_sc1(const void *p)
-{
-	return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-/* bounded spin step: false once the spin budget is spent or another workgroup has flagged an error
- * (so one failure drains the whole grid quickly instead of every row timing out in turn) */
-__device__ __forceinline__ bool spin_ok(unsigned &spins, int *err, int code)
-{
-	__builtin_amdgcn_s_sleep(1);
-	++spins;
-	if ((spins & 255) == 0 && __hip_atomic_load((gi32 *)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-	if (spins > SPIN_LIMIT) {
-		if ((threadIdx.x & 63) == 0) atomicOr(err, code);
-		return false;
+	__shared__ int s_item, s_rmin, s_rmax;
+	__shared__ unsigned int s_refs[2];
+	const int t = threadIdx.x;
+	/* Single-lane work in this loop is done by the whole of wave 0 under a SCALAR branch, the one
+	 * lane picked by value (atomic operand 0 on lanes 1..63).  An `if (t == 0)` here lets the
+	 * compiler thread lanes 1..63 of wave 0 straight back to the next barrier while lane 0 is still
+	 * dequeueing, which deadlocks the workgroup (seen on gfx950 with ROCm 7.2). */
+	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
+	const int nseg = (Wmb + 7) >> 3, nitems = Hmb * nseg;
+	int nst_dbg = 0;
+	for (;;) {
+		if (wave0) {
+			const int v = __hip_atomic_fetch_add((gi32 *)queue, t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			s_item = __builtin_amdgcn_readfirstlane(v);
+			s_rmin = 1 << 30;
+			s_rmax = -1;
+			s_refs[0] = s_refs[1] = 0;
+		}
+		__syncthreads();
+		const int item = __builtin_amdgcn_readfirstlane(s_item);
+		if (item >= nitems) break;
+		const int y = item / nseg, x0 = (item % nseg) * 8, x1 = min(x0 + 8, Wmb);
+		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
+	/* ---- vertical reach of this segment's motion into each reference (8 lanes per MB) */
+		if (t < 64) {
+			const int mbi = x0 + (t >> 3);
+			int rmin = 1 << 30, rmax = -1;
+			unsigned int r0 = 0, r1 = 0;
+			if (mbi < x1) {
+				const m2r_mb_t m = mbs[y * Wmb + mbi];
+				if (m.kind == M2R_MB_INTER) {
+					const m2r_inter_t &it = inters[m.inter];
+					for (int k = (t & 7) * 4; k < (t & 7) * 4 + 4; ++k) {
+						const int l = k >> 4, blk = k & 15;
+						const int sl = it.slot[l][(blk >> 3) * 2 + ((blk & 3) >> 1)];
+						if (sl < 0) continue;
+						const int py = y * 16 + (blk >> 2) * 4 + (it.mv[l][blk][1] >> 2);
+						const int top = py - 2, bot = py + 3 + 3;
+						rmin = min(rmin, top < 0 ? 0 : min(top >> 4, Hmb - 1));
+						rmax = max(rmax, bot < 0 ? 0 : min(bot >> 4, Hmb - 1));
+						if (sl < 32) r0 |= 1u << sl;
+						else r1 |= 1u << (sl - 32);
+					}
+				}
+			}
+			if (rmax >= 0) {
+				atomicMin(&s_rmin, rmin);
+				atomicMax(&s_rmax, rmax);
+				atomicOr(&s_refs[0], r0);
+				atomicOr(&s_refs[1], r1);
+			}
+		}
+		__syncthreads();
+#ifndef M2DEC_NO_REFWAIT
+		const int rmin_u = __builtin_amdgcn_readfirstlane(s_rmin), rmax_u = __builtin_amdgcn_readfirstlane(s_rmax);
+		if (rmax_u >= 0 && wave0) {
+			/* rows rmin .. rmax final: their own stores and the next row's (rows 13..15) done */
+			const int rlast = min(rmax_u + 1, Hmb - 1);
+			for (int k = 0; k < 2; ++k) {
+				unsigned int bits = __builtin_amdgcn_readfirstlane(s_refs[k]);
+				while (bits) {
+					const int sl = k * 32 + __builtin_ctz(bits);
+					bits &= bits - 1;
+					const int want = ss.s[sl];
+					if (want <= 0) continue;
+					/* entry (seq & 63) only ever grows: a later picture's value also means "final" */
+					const int *fl = rowflag + (size_t)((want - 1) & 63) * Hmb;
+					unsigned spins = 0;
+					for (int r0 = rmin_u; r0 <= rlast; r0 += 64) {
+						const int r = r0 + t;
+						for (;;) {
+							const bool ok = (r > rlast) ||
+							                __hip_atomic_load((gi32 *)&fl[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+							if (__all(ok)) break;
+							if (!spin_ok(spins, err, 32)) break;
+						}
+					}
+				}
+			}
+			/* ALWAYS acquire, even when every flag was already set: this XCD's L2 may hold lines of
+			 * rows 13..15 that the row's own deblock workgroup loaded before the row below filtered
+			 * and rewrote them from another XCD */
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+#endif
+		__syncthreads();
+		STAMPI(96 + (blockIdx.x & 63), 1, nst_dbg & 255, item);
+		for (int x = x0; x < x1; ++x) {
+			const m2r_mb_t m = mbs[y * Wmb + x];
+			if (__builtin_amdgcn_readfirstlane(m.kind) == M2R_MB_INTER)
+				inter_mb(y * Wmb + x, m, inters, slices, pool, frames, fsz, W, H, Wmb, slot);
+			__syncthreads();
+		}
+		/* segment done: every wave drained, then ONE agent release and the row's counter */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		if (wave0) {
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__hip_atomic_fetch_add((gi32 *)&inter_cnt[y], t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		STAMPI(96 + (blockIdx.x & 63), 2, nst_dbg & 255, item);
+		nst_dbg++;
 	}
-	return true;
-}
-
-__device__ __forceinline__ bool poll_ge(int *flag, int need, int *err)
-{
-	unsigned spins = 0;
-	while (__hip_atomic_load((gi32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-		if (!spin_ok(spins, err, 2)) return false;
-	}
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the payload loads below the poll */
-	return true;
-}
-
-__device__ __forceinline__ void signal_progress(int *flag, int value)
-{
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the (single) storing wave drains its sc1 stores */
-	if ((threadIdx.x & 63) == 0) __hip_atomic_store((gi32 *)flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* ======================================================================== intra prediction (per sample) */
@@ -505,11 +637,17 @@ __device__ __forceinline__ int avail8(int b, int a)
  * with few intra MBs therefore carry no row-to-row chain through their inter MBs.
  */
 
-__global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
-                                              uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, int *err)
+/* wave-level sync for the intra wavefront, which runs on ONE wave of its workgroup */
+#define WSYNC()                                                  \
+	do {                                                         \
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+		__builtin_amdgcn_wave_barrier();                         \
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
+	} while (0)
+
+__device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
+                          uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
 {
-	const int y = blockIdx.x;
-	const int t = threadIdx.x;
 	__shared__ uint8_t L[17][LW];   /* row 0: top neighbours; rows 1..16: MB rows; col 0: left neighbour */
 	__shared__ uint8_t C[2][9][9];  /* per component: row 0 top (col 0 top-left), col 0 left */
 	__shared__ int R[256 + 128];
@@ -548,13 +686,14 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 			for (int d = -1; d <= 1; ++d)
 				if (up_intra(x + d)) need = x + d + 1;
 			if (need) poll_ge(&progress[y - 1], need, err);
+			poll_ge((int *)&hbi_ready[y - 1], 1, err); /* the row above's inter MBs' bottom rows */
 		}
 		/* ---- gather the neighbourhood */
 		if (left_in_lds) {
 			if (t < 17) L[t][0] = L[t][16];
 			if (t < 18) { int c = t / 9, r = t % 9; C[c][r][0] = C[c][r][8]; }
 		}
-		__syncthreads();
+		WSYNC();
 		if (y > 0 && t < 7) {
 			/* granules of the row above: 0,1 luma MB x; 2 luma MB x+1 (bytes 0..7); 3 luma MB x-1 (bytes 8..15);
 			 * 4,5 chroma MB x; 6 chroma MB x-1 (bytes 8..15) */
@@ -562,9 +701,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 			const int isc = (t >= 4);
 			const int half = (t == 1 || t == 3 || t == 5 || t == 6) ? 1 : 0;
 			if (xs >= 0 && xs < Wmb) {
-				unsigned long long v;
-				if (up_intra(xs)) v = ld_sc1(hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + isc * 16 + half * 8);
-				else v = *(const unsigned long long *)((isc ? chroma + (size_t)(y0 / 2 - 1) * W : cur + (size_t)(y0 - 1) * W) + xs * 16 + half * 8);
+				const unsigned long long v = ld_sc1(hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + isc * 16 + half * 8);
 				for (int b = 0; b < 8; ++b) {
 					uint8_t s8 = (uint8_t)(v >> (8 * b));
 					int j = half * 8 + b; /* byte within the 16-byte MB row */
@@ -580,13 +717,13 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 			if (t < 16) L[1 + t][0] = cur[(size_t)(y0 + t) * W + x0 - 1];
 			if (t >= 16 && t < 32) { int k = t - 16; C[k & 1][1 + (k >> 1)][0] = chroma[(size_t)(y0 / 2 + (k >> 1)) * W + x0 - 2 + (k & 1)]; }
 		}
-		__syncthreads();
+		WSYNC();
 
 		if (m.kind == M2R_MB_PCM) {
 			const uint8_t *s = (const uint8_t *)(pool + m.coef);
 			for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
 			for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
-			__syncthreads();
+			WSYNC();
 		} else {
 			/* ---- chroma prediction (h264.cpp:4559-4706); thread t: sample (t & 7, t >> 3) of both components */
 			{
@@ -618,12 +755,12 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 					R[256 + c * 64 + t] = v;
 				}
 			}
-			__syncthreads();
+			WSYNC();
 			for (int c = 0; c < 2; ++c) {
 				int v = R[256 + c * 64 + t];
 				if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
 			}
-			__syncthreads();
+			WSYNC();
 
 			/* ---- luma */
 			const int qp = m.qpy;
@@ -642,7 +779,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						R[64 + t] = v;
 						if (coded) R[t] = pool[m.coef + d_luma_off(m, blk) + t] * d_scale4(qp, t & 3, t >> 2);
 					}
-					__syncthreads();
+					WSYNC();
 					if (t < 16) {
 						int v = R[64 + t];
 						if (v >= 0) L[oy + 1 + (t >> 2)][1 + ox + (t & 3)] = (uint8_t)v;
@@ -654,20 +791,20 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 							d_idct4_1d(a0, a1, a2, a3);
 							p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
 						}
-						__syncthreads();
+						WSYNC();
 						if (t < 4) {
 							int *p = &R[t];
 							int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
 							d_idct4_1d(a0, a1, a2, a3);
 							p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
 						}
-						__syncthreads();
+						WSYNC();
 						if (t < 16) {
 							uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
 							*d = (uint8_t)d_clip255(*d + R[t]);
 						}
 					}
-					__syncthreads();
+					WSYNC();
 				}
 			} else if (m.kind == M2R_MB_I8x8) {
 				for (int b = 0; b < 4; ++b) {
@@ -714,7 +851,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						R[128 + t] = (lv != 0);
 						if (t == 0) DC[0] = lv;
 					}
-					__syncthreads();
+					WSYNC();
 					{
 						int mode = (m.ipred[0] >> (4 * b)) & 15;
 						int v = pred8_px(mode, av, t & 7, t >> 3, F, F + 16, F[24]);
@@ -733,7 +870,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 							for (int k = 0; k < 64; ++k) n += R[128 + k];
 							HV[0] = n;
 						}
-						__syncthreads();
+						WSYNC();
 						if (t < 8) {
 							int v[8];
 							int *p = &R[t];
@@ -741,14 +878,14 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 							d_idct8_1d(v);
 							for (int k = 0; k < 8; ++k) p[k * 8] = (v[k] + 32) >> 6;
 						}
-						__syncthreads();
+						WSYNC();
 						{
 							uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
 							if (HV[0] == 1 && DC[0] != 0) *d = (uint8_t)d_swar(*d, DC[0] * d_scale8(qp, 0, 0), t & 7, 8);
 							else *d = (uint8_t)d_clip255(*d + R[t]);
 						}
 					}
-					__syncthreads();
+					WSYNC();
 				}
 			} else {
 				/* Intra16x16 (h264.cpp:4407-4555) */
@@ -770,7 +907,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 				}
 				/* DC levels */
 				if (t < 16) DC[t] = (m.nz & M2R_NZ_LUMA_DC) ? pool[m.coef + t] * d_scale4(qp, 0, 0) : 0;
-				__syncthreads();
+				WSYNC();
 				for (int k = t; k < 256; k += 64) {
 					int px = k & 15, py = k >> 4, v = -1;
 					if (mode == 0) { if (av & 2) v = L[0][1 + px]; }
@@ -779,7 +916,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 					else v = d_clip255((HV[0] + HV[1] * (px - 7) + HV[2] * (py - 7) + 16) >> 5);
 					R[k] = v;
 				}
-				__syncthreads();
+				WSYNC();
 				for (int k = t; k < 256; k += 64) {
 					int v = R[k];
 					if (v >= 0) L[1 + (k >> 4)][1 + (k & 15)] = (uint8_t)v;
@@ -790,13 +927,13 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 					int a0 = r[0] + r[1], a1 = r[0] - r[1], a2 = r[2] + r[3], a3 = r[2] - r[3];
 					r[0] = a0 + a2; r[1] = a0 - a2; r[2] = a1 - a3; r[3] = a1 + a3;
 				}
-				__syncthreads();
+				WSYNC();
 				if (t < 4) {
 					int *r = &DC[t];
 					int a0 = r[0] + r[4], a1 = r[0] - r[4], a2 = r[8] + r[12], a3 = r[8] - r[12];
 					r[0] = (a0 + a2 + 2) >> 2; r[4] = (a0 - a2 + 2) >> 2; r[8] = (a1 - a3 + 2) >> 2; r[12] = (a1 + a3 + 2) >> 2;
 				}
-				__syncthreads();
+				WSYNC();
 				if (m.cbp & 15) {
 					/* AC blocks with coefficients: full transform with the DC inserted; others DC-only SWAR */
 					for (int k = t; k < 256; k += 64) {
@@ -807,7 +944,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						else if (m.nz & (1u << blk)) v = pool[m.coef + d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
 						R[k] = v;
 					}
-					__syncthreads();
+					WSYNC();
 					{
 						int blk = t >> 2, row = t & 3;
 						int *p = &R[blk * 16 + row * 4];
@@ -815,7 +952,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						d_idct4_1d(a0, a1, a2, a3);
 						p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
 					}
-					__syncthreads();
+					WSYNC();
 					{
 						int blk = t >> 2, col = t & 3;
 						int *p = &R[blk * 16 + col];
@@ -823,7 +960,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						d_idct4_1d(a0, a1, a2, a3);
 						p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
 					}
-					__syncthreads();
+					WSYNC();
 					for (int k = t; k < 256; k += 64) {
 						int blk = k >> 4, pos = k & 15;
 						int bx = c_blk_x[blk], by = c_blk_y[blk];
@@ -838,7 +975,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						*d = (uint8_t)d_swar(*d, DC[(py >> 2) * 4 + (px >> 2)], px & 3, 4);
 					}
 				}
-				__syncthreads();
+				WSYNC();
 			}
 
 			/* ---- chroma residual (residual_chroma, h264.cpp:2374-2461) */
@@ -853,7 +990,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 						v = pool[m.coef + d_chroma_off(m, 19 + 4 * c + cblk) + pos] * d_scale4(m.qpc[c], cx & 3, cy & 3);
 					R[256 + c * 64 + cy * 8 + cx] = v;
 				}
-				__syncthreads();
+				WSYNC();
 				if (t < 32) {
 					int comp = t >> 4, b = (t >> 2) & 3, row = t & 3;
 					int *p = &R[256 + comp * 64 + ((b >> 1) * 4 + row) * 8 + (b & 1) * 4];
@@ -861,7 +998,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 					d_idct4_1d(a0, a1, a2, a3);
 					p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
 				}
-				__syncthreads();
+				WSYNC();
 				if (t < 32) {
 					int comp = t >> 4, b = (t >> 2) & 3, col = t & 3;
 					int *p = &R[256 + comp * 64 + ((b >> 1) * 4) * 8 + (b & 1) * 4 + col];
@@ -869,13 +1006,13 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 					d_idct4_1d(a0, a1, a2, a3);
 					p[0] = (a0 + 32) >> 6; p[8] = (a1 + 32) >> 6; p[16] = (a2 + 32) >> 6; p[24] = (a3 + 32) >> 6;
 				}
-				__syncthreads();
+				WSYNC();
 				for (int k = t; k < 128; k += 64) {
 					int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
 					uint8_t *d = &C[c][1 + cy][1 + cx];
 					*d = (uint8_t)d_clip255(*d + R[256 + c * 64 + cy * 8 + cx]);
 				}
-				__syncthreads();
+				WSYNC();
 			}
 		}
 
@@ -896,7 +1033,7 @@ __global__ __launch_bounds__(64) void k_intra(const m2r_mb_t *__restrict__ mbs, 
 		}
 		signal_progress(&progress[y], x + 1);
 		prev_x = x;
-		__syncthreads();
+		WSYNC();
 		}
 	}
 	signal_progress(&progress[y], Wmb);
@@ -985,12 +1122,11 @@ __device__ __forceinline__ void edge_on_line(int *v, int at, int step, int bs, i
  * release / acquire); workgroups through progress words (agent scope, sc1).
  * Frame writes: rows 0..12 (chroma 0..6) of an MB by its own row, rows 13..15 (7) by the row below.
  */
-__global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W,
-                                                            int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err)
+__device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W, int H,
+                            int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err, int *rowflag, int seq)
 {
-	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-	const int y = blockIdx.x;
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
+	const int nthr = blockDim.x;
 	const int S = W + 2 * DBK_PAD;           /* LDS line stride: DBK_PAD bytes of pad each side */
 	uint8_t *RL = smem;                      /* 20 luma lines: frame rows y0-4 .. y0+15 */
 	uint8_t *RC = smem + 20 * S;             /* 10 chroma lines: rows yc0-2 .. yc0+7 */
@@ -1002,15 +1138,15 @@ __global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t 
 	const bool last_row = (y == Hmb - 1);
 
 	/* ---- prologue: this MB row and its records into LDS (all waves) */
-	for (int k = threadIdx.x; k < 16 * (W >> 4); k += 64 * DBK_WAVES) {
+	for (int k = threadIdx.x; k < 16 * (W >> 4); k += nthr) {
 		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
 		*(uint4 *)(RL + (4 + r) * S + DBK_PAD + c) = *(const uint4 *)(cur + (size_t)(y0 + r) * W + c);
 	}
-	for (int k = threadIdx.x; k < 8 * (W >> 4); k += 64 * DBK_WAVES) {
+	for (int k = threadIdx.x; k < 8 * (W >> 4); k += nthr) {
 		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
 		*(uint4 *)(RC + (2 + r) * S + DBK_PAD + c) = *(const uint4 *)(chroma + (size_t)(yc0 + r) * W + c);
 	}
-	for (int k = threadIdx.x; k < Wmb; k += 64 * DBK_WAVES) {
+	for (int k = threadIdx.x; k < Wmb; k += nthr) {
 		rq[k] = dbk[y * Wmb + k];
 		rt[k] = y > 0 ? dbk[(y - 1) * Wmb + k] : rq[k];
 	}
@@ -1020,6 +1156,7 @@ __global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t 
 	}
 	__syncthreads();
 
+	if (wave >= DBK_WAVES) return;
 	if (wave == 0) {
 		/* ---------------- loader */
 		if (y == 0) return;
@@ -1180,6 +1317,7 @@ __global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t 
 			if (lim <= done) {
 				if (!spin_ok(spins, err, 8)) {
 					if (!last_row) signal_progress(&progress[y], Wmb); /* release the row below */
+					if (t == 0) __hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + y], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					return;
 				}
 				continue;
@@ -1220,7 +1358,90 @@ __global__ __launch_bounds__(64 * DBK_WAVES) void k_deblock(const m2r_deblock_t 
 			nst++;
 			done = lim;
 		}
+		/* every store of this row (its rows 0..12, the row above's 13..15) is in: publish for the MC of
+		 * later pictures (plain stores -> drain -> agent release -> sc1 flag, G16 valid form) */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		if (t == 0) {
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + y], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
 	}
+}
+
+
+/* ======================================================================== k_picture */
+/*
+ * One launch per picture, all three stages overlapped row by row.  Workgroups [0, G) are persistent
+ * inter workers (work items = 8-MB segments in raster order); workgroup G + y owns MB row y:
+ *   phase A: waits until every inter segment of its row is stored (per-row counter, agent release /
+ *            acquire), publishes the unfiltered bottom rows of its inter MBs (hand-off records read
+ *            by the intra MBs of the row below, which may only run once this row is deblocking),
+ *            then reconstructs its intra / PCM MBs on wave 0 (2-MB-lag wavefront on the row above);
+ *   phase B: deblocks the row on waves 0..2 (loader / filter / storer, as described at deblock_row)
+ *            and finally flags the row final for the motion compensation of later pictures.
+ * Every wait points at a lower block index of the same launch or at an earlier launch, so FIFO
+ * queues and in-order dispatch cannot deadlock; the host keeps at most NSTREAMS pictures in flight
+ * so that they all fit on the device.
+ */
+__global__ __launch_bounds__(256) void k_picture(PictureArgs a)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	if ((int)blockIdx.x < a.inter_workers) {
+		if (a.n_inter)
+			inter_worker(a.mbs, a.inters, a.slices, a.pool, a.frames, a.fsz, a.W, a.H, a.Wmb, a.Hmb, a.slot, a.ss, a.rowflag,
+			             a.scratch + SCR_QUEUE(a.Hmb), a.scratch + SCR_INTER(a.Hmb), a.err);
+		return;
+	}
+	const int t = threadIdx.x;
+	const int y = blockIdx.x - a.inter_workers;
+	const int Wmb = a.Wmb, nseg = (Wmb + 7) >> 3;
+	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
+	uint8_t *chroma = cur + (size_t)a.W * a.H;
+	int *inter_cnt = a.scratch + SCR_INTER(a.Hmb);
+	int *hbi_ready = a.scratch + SCR_HBIRDY(a.Hmb);
+	STAMP(y, 3, 0, 1);
+	/* ---- phase A.1: this row's inter MBs are all stored (inter workers of this launch) */
+	if (a.n_inter) {
+		if (t == 0) {
+			unsigned spins = 0;
+			while (__hip_atomic_load((gi32 *)&inter_cnt[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nseg)
+				if (!spin_ok(spins, a.err, 64)) break;
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+		__syncthreads();
+	}
+	STAMP(y, 3, 1, 2);
+	/* ---- phase A.2: unfiltered bottom rows of the inter MBs -> hand-off records */
+	if (y + 1 < a.Hmb) {
+		for (int k = t; k < Wmb * 4; k += blockDim.x) {
+			const int x = k >> 2, g = k & 3;
+			if (a.mbs[y * Wmb + x].kind != M2R_MB_INTER) continue;
+			const uint8_t *src = (g < 2) ? cur + (size_t)(y * 16 + 15) * a.W + x * 16 + (g & 1) * 8
+			                             : chroma + (size_t)(y * 8 + 7) * a.W + x * 16 + (g & 1) * 8;
+			st_sc1(a.hbi + ((size_t)y * Wmb + x) * HBI_BYTES + g * 8, *(const unsigned long long *)src);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		if (t == 0) __hip_atomic_store((gi32 *)&hbi_ready[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+	STAMP(y, 3, 2, 3);
+	/* ---- phase A.3: intra / PCM MBs on wave 0 */
+	if (a.n_intra && t < 64) {
+		intra_row(y, t, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi, a.scratch + SCR_IPROG(a.Hmb), hbi_ready, a.err);
+		/* write the intra samples back out of this XCD's L2 now: rows 13..15 of this MB row are
+		 * rewritten (filtered) by the row below's deblock storer, possibly from another XCD, and a
+		 * later write-back of our dirty unfiltered bytes would land on top of them */
+		if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+	}
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+	__syncthreads();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+	STAMP(y, 3, 3, 4);
+	/* ---- phase B: deblocking (always: it also publishes the row flags) */
+	deblock_row(y, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq);
+	STAMP(y, 3, 4, 5);
 }
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)

@@ -13,13 +13,39 @@
 #define DBK_WAVES 3  /* k_deblock workgroup: loader, filter, storer waves */
 #define DBK_PAD 16   /* k_deblock LDS pad each side of a line (keeps 16-B rows aligned) */
 
-__global__ void k_inter(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters,
-                        const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                        size_t fsz, int W, int H, int Wmb, int slot);
-__global__ void k_intra(const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H,
-                        int Wmb, uint8_t *hbi, int *progress, int *err);
-__global__ void k_deblock(const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W, int H, int Wmb, int Hmb,
-                          uint8_t *hbd, int *progress, int *err);
+/* seq + 1 of the picture currently held by each frame slot (0: none) */
+struct SlotSeq {
+	int s[64];
+};
+
+/* per-launch scratch words (zeroed before every launch): intra progress, deblock progress, inter
+ * segment counters, hand-off-ready flags ([Hmb] each), then the work-queue head */
+#define SCR_IPROG(Hmb) 0
+#define SCR_DPROG(Hmb) (Hmb)
+#define SCR_INTER(Hmb) (2 * (Hmb))
+#define SCR_HBIRDY(Hmb) (3 * (Hmb))
+#define SCR_QUEUE(Hmb) (4 * (Hmb))
+#define SCR_WORDS(Hmb) ((4 * (Hmb) + 4 + 3) & ~3)
+
+struct PictureArgs {
+	const m2r_mb_t *mbs;
+	const m2r_inter_t *inters;
+	const m2r_slice_t *slices;
+	const int16_t *pool;
+	const m2r_deblock_t *dbk;
+	uint8_t *frames;
+	size_t fsz;
+	int W, H, Wmb, Hmb;
+	int slot, seq, n_inter, n_intra;
+	int inter_workers;
+	int *scratch;     /* SCR_* words of this launch */
+	uint8_t *hbi, *hbd; /* hand-off records of this launch's stream */
+	int *rowflag;     /* [64][Hmb] picture row flags (seq + 1 when final) */
+	int *err;
+	SlotSeq ss;
+};
+
+__global__ void k_picture(PictureArgs a); /* grid: inter_workers + Hmb, dynamic LDS m2r_deblock_lds_bytes */
 
 /* dynamic LDS bytes of one k_deblock workgroup for a W-sample-wide picture */
 size_t m2r_deblock_lds_bytes(int W, int Wmb);

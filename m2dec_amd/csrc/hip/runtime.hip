@@ -2,17 +2,18 @@
  * Host runtime of the gfx950 reconstruction back end: the picture scheduler, the m2r_backend_t
  * behind h264d_func (decode path), and the trace replay used by bench.py.
  *
- * Picture scheduler.  A picture is three launches (k_inter -> k_intra -> k_deblock) that must run in
- * order; different pictures only depend on each other through frame slots:
- *   - read-after-write : a picture's k_inter reads its reference slots, so it waits for the launch
- *                        sequence that last wrote each of them;
- *   - write-after-read : a picture overwrites its destination slot only after every k_inter that
+ * Picture scheduler.  A picture is ONE launch, k_picture (inter workers + one workgroup per MB row:
+ * intra, then deblocking).  Pictures depend on each other only through frame slots:
+ *   - read-after-write : NOT a stream wait.  The inter workers poll the reference pictures' row
+ *                        flags on the device, so a picture's motion compensation starts while its
+ *                        references are still being deblocked further down;
+ *   - write-after-read : a picture overwrites its destination slot only after every picture that
  *                        read the slot's previous content has finished (and after that content's
- *                        own writer and device-to-host copy).
- * Pictures are dealt round-robin over NSTREAMS HIP streams with exactly those event waits, so a
- * B picture runs beside the next anchor picture and other B pictures (IBBP: three pictures in
- * flight), each wavefront kernel using ~Hmb CUs of the 256.  Each stream owns its progress words and
- * hand-off records; the frame pool and the error word are shared.
+ *                        own writer and device-to-host copy): stream event waits.
+ * Pictures are dealt round-robin over NSTREAMS HIP streams (one hardware queue each with the
+ * default GPU_MAX_HW_QUEUES=4), each owning its scratch words and hand-off records; the frame pool,
+ * the row flags and the error word are shared.  Every wait points at an earlier launch, so the
+ * oldest unfinished picture can always run.
  */
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -26,7 +27,13 @@
 
 namespace {
 
-const int NSTREAMS = 4;
+static int dbg_knob(const char *name)
+{
+	const char *v = getenv(name);
+	return v && atoi(v);
+}
+
+const int NSTREAMS = 3; /* pictures in flight: all of their k_inter + k_rows workgroups fit on the device */
 const int NEVENTS = 4096; /* recycled sync events: far more than the pictures a dependency can span */
 
 struct RecPtrs {
@@ -49,10 +56,14 @@ struct Sched {
 	int W = 0, H = 0, Wmb = 0, Hmb = 0, nslots = 0;
 	size_t fsz = 0;
 	uint8_t *frames = nullptr; /* device frame pool [nslots] x fsz */
-	hipStream_t st[NSTREAMS] = {};
-	int *prog = nullptr;       /* [NSTREAMS][2][Hmb] */
+	hipStream_t st[NSTREAMS] = {}; /* per in-flight index: uploads, k_picture, downloads */
+	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb)] per-launch scratch words */
 	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
 	int *err = nullptr;
+	int *rowflag = nullptr;    /* [64][Hmb]: seq + 1 once an MB row of picture seq is final */
+	int seq = 0;               /* pictures launched */
+	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
+	int inter_grid = 64;       /* persistent inter workers per picture (a quarter of the CUs) */
 	int rr = 0;
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
@@ -70,6 +81,10 @@ struct Sched {
 		for (auto &e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 		CHECK(hipMalloc(&err, 16));
 		CHECK(hipMemset(err, 0, 16));
+		memset(&slot_seq, 0, sizeof(slot_seq));
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+			inter_grid = cus / 4;
 		return 0;
 	}
 
@@ -91,8 +106,10 @@ struct Sched {
 		if (prog && (width / 16 != Wmb || height / 16 != Hmb)) {
 			(void)hipFree(prog);
 			(void)hipFree(hand);
+			(void)hipFree(rowflag);
 			prog = nullptr;
 			hand = nullptr;
+			rowflag = nullptr;
 		}
 		W = width;
 		H = height;
@@ -100,16 +117,20 @@ struct Sched {
 		Hmb = height / 16;
 		fsz = nfsz;
 		if (!prog) {
-			CHECK(hipMalloc(&prog, sizeof(int) * 2 * (size_t)Hmb * NSTREAMS));
+			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb) * NSTREAMS));
 			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
+			CHECK(hipMalloc(&rowflag, sizeof(int) * 64 * (size_t)Hmb));
 		}
+		CHECK(hipMemset(rowflag, 0, sizeof(int) * 64 * (size_t)Hmb));
+		seq = 0;
+		memset(&slot_seq, 0, sizeof(slot_seq));
 		for (int i = 0; i < 64; ++i) {
 			slot_write[i] = nullptr;
 			readers[i].clear();
 		}
 		size_t lds = m2r_deblock_lds_bytes(W, Wmb);
 		if (lds > 65536 && lds > lds_set) {
-			CHECK(hipFuncSetAttribute((const void *)k_deblock, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+			CHECK(hipFuncSetAttribute((const void *)k_picture, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 			lds_set = lds;
 		}
 		return 0;
@@ -124,52 +145,63 @@ struct Sched {
 		return e;
 	}
 
-	/* pick a stream for a picture writing `slot` and reading `refs`; enqueue its dependency waits */
+	/* pick a stream for a picture writing `slot`; enqueue its write-after-read / write-after-write
+	 * waits.  Read-after-write on the reference slots is NOT a stream wait: k_inter polls the
+	 * references' row flags on the device, so it overlaps their deblocking. */
 	int begin(int slot, uint64_t refs)
 	{
+		(void)refs;
 		int k = rr;
 		rr = (rr + 1) % NSTREAMS;
 		hipStream_t s = st[k];
-		for (int r = 0; r < 64; ++r)
-			if (((refs >> r) & 1) && slot_write[r]) CHECK(hipStreamWaitEvent(s, slot_write[r], 0));
 		for (hipEvent_t e : readers[slot]) CHECK(hipStreamWaitEvent(s, e, 0));
 		if (slot_write[slot]) CHECK(hipStreamWaitEvent(s, slot_write[slot], 0));
+		if (dbg_knob("M2DEC_AMD_RAW"))
+			for (int i = 0; i < 64; ++i)
+				if (((refs >> i) & 1) && slot_write[i]) CHECK(hipStreamWaitEvent(st[k], slot_write[i], 0));
+		if (dbg_knob("M2DEC_AMD_SYNC")) CHECK(hipDeviceSynchronize());
 		return k;
 	}
 
-	/* k_inter, k_intra, k_deblock of one picture on stream k; tev (optional) gets records after
-	 * each of the three; returns the event recorded after k_inter (reader event) through inter_done */
+	/* one k_picture launch on stream k; tev (optional): [0] recorded after it; inter_done: the event
+	 * after which the picture's reference reads are over */
 	int launch(int k, const PicJob &j, hipEvent_t *tev, hipEvent_t *inter_done)
 	{
 		hipStream_t s = st[k];
-		uint8_t *cur = frames + (size_t)j.slot * fsz;
-		int *pr = prog + (size_t)k * 2 * Hmb;
-		uint8_t *hbi = hand + (size_t)k * hand_bytes();
-		uint8_t *hbd = hbi + (size_t)Hmb * Wmb * HBI_BYTES;
-		if (j.n_inter) {
-			hipLaunchKernelGGL(k_inter, dim3(Wmb * Hmb), dim3(256), 0, s, j.r.mb, j.r.it, j.r.sl, j.r.coef, frames, fsz, W, H,
-			                   Wmb, j.slot);
-			CHECK(hipGetLastError());
-			tm.inter_launches++;
-		}
+		PictureArgs a;
+		memset(&a, 0, sizeof(a));
+		a.mbs = j.r.mb;
+		a.inters = j.r.it;
+		a.slices = j.r.sl;
+		a.pool = j.r.coef;
+		a.dbk = j.r.dbk;
+		a.frames = frames;
+		a.fsz = fsz;
+		a.W = W;
+		a.H = H;
+		a.Wmb = Wmb;
+		a.Hmb = Hmb;
+		a.slot = j.slot;
+		a.seq = seq++;
+		a.n_inter = j.n_inter;
+		a.n_intra = j.n_intra;
+		a.inter_workers = inter_grid;
+		a.scratch = prog + (size_t)k * SCR_WORDS(Hmb);
+		a.hbi = hand + (size_t)k * hand_bytes();
+		a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+		a.rowflag = rowflag;
+		a.err = err;
+		a.ss = slot_seq;
+		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb), s));
+		hipLaunchKernelGGL(k_picture, dim3(inter_grid + Hmb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, a);
+		CHECK(hipGetLastError());
+		tm.inter_launches += j.n_inter ? 1 : 0;
+		tm.intra_launches += j.n_intra ? 1 : 0;
+		tm.deblock_launches++;
+		slot_seq.s[j.slot] = a.seq + 1;
 		*inter_done = next_event();
 		CHECK(hipEventRecord(*inter_done, s));
 		if (tev) CHECK(hipEventRecord(tev[0], s));
-		if (j.n_intra) {
-			CHECK(hipMemsetAsync(pr, 0, sizeof(int) * Hmb, s));
-			hipLaunchKernelGGL(k_intra, dim3(Hmb), dim3(64), 0, s, j.r.mb, j.r.coef, cur, W, H, Wmb, hbi, pr, err);
-			CHECK(hipGetLastError());
-			tm.intra_launches++;
-		}
-		if (tev) CHECK(hipEventRecord(tev[1], s));
-		if (j.deblock) {
-			CHECK(hipMemsetAsync(pr + Hmb, 0, sizeof(int) * Hmb, s));
-			hipLaunchKernelGGL(k_deblock, dim3(Hmb), dim3(64 * DBK_WAVES), m2r_deblock_lds_bytes(W, Wmb), s, j.r.dbk, cur, W,
-			                   H, Wmb, Hmb, hbd, pr + Hmb, err);
-			CHECK(hipGetLastError());
-			tm.deblock_launches++;
-		}
-		if (tev) CHECK(hipEventRecord(tev[2], s));
 		return 0;
 	}
 
@@ -214,6 +246,7 @@ struct Sched {
 		if (prog) (void)hipFree(prog);
 		if (hand) (void)hipFree(hand);
 		if (err) (void)hipFree(err);
+		if (rowflag) (void)hipFree(rowflag);
 		for (auto &s : st)
 			if (s) (void)hipStreamDestroy(s);
 	}
@@ -277,10 +310,8 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 	(void)hipEventSynchronize(t.e[5]);
 	m2dec_amd_hip_timing_t &tm = b->sc.tm;
 	if (hipEventElapsedTime(&ms, t.e[0], t.e[1]) == hipSuccess) tm.h2d_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) tm.inter_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[2], t.e[3]) == hipSuccess) tm.intra_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[3], t.e[4]) == hipSuccess) tm.deblock_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[4], t.e[5]) == hipSuccess) tm.d2h_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) tm.picture_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[2], t.e[5]) == hipSuccess) tm.d2h_us += ms * 1e3;
 	t.pending = false;
 }
 
@@ -508,7 +539,7 @@ struct m2dec_amd_hip_replay {
 	uint8_t *d_rec = nullptr;
 	std::vector<m2dec_amd_trace_pic_t> pics;
 	std::vector<uint64_t> refs;
-	/* timing: 4 events per enqueued picture (start, after inter, after intra, after deblock) */
+	/* timing: 2 events per enqueued picture (before / after its k_inter + k_rows pair) */
 	std::vector<hipEvent_t> tev;
 	size_t tev_used = 0;
 };
@@ -569,13 +600,13 @@ static int replay_enqueue(m2dec_amd_hip_replay_t *r, int i, bool timed)
 	if (k < 0) return -1;
 	hipEvent_t *ev = nullptr;
 	if (timed) {
-		while (r->tev_used + 4 > r->tev.size()) {
+		while (r->tev_used + 2 > r->tev.size()) {
 			hipEvent_t e;
 			CHECK(hipEventCreate(&e));
 			r->tev.push_back(e);
 		}
 		ev = &r->tev[r->tev_used];
-		r->tev_used += 4;
+		r->tev_used += 2;
 		CHECK(hipEventRecord(ev[0], sc.st[k]));
 	}
 	hipEvent_t inter_done;
@@ -609,13 +640,11 @@ extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_
 {
 	if (!r || !out) return -1;
 	CHECK(hipSetDevice(r->sc.dev));
-	for (size_t i = 0; i + 4 <= r->tev_used; i += 4) {
+	for (size_t i = 0; i + 2 <= r->tev_used; i += 2) {
 		float ms;
 		hipEvent_t *e = &r->tev[i];
-		CHECK(hipEventSynchronize(e[3]));
-		if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) r->sc.tm.inter_us += ms * 1e3;
-		if (hipEventElapsedTime(&ms, e[1], e[2]) == hipSuccess) r->sc.tm.intra_us += ms * 1e3;
-		if (hipEventElapsedTime(&ms, e[2], e[3]) == hipSuccess) r->sc.tm.deblock_us += ms * 1e3;
+		CHECK(hipEventSynchronize(e[1]));
+		if (hipEventElapsedTime(&ms, e[0], e[1]) == hipSuccess) r->sc.tm.picture_us += ms * 1e3;
 	}
 	r->tev_used = 0;
 	*out = r->sc.tm;
@@ -630,7 +659,9 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	size_t ls = (size_t)sc.W * sc.H;
 	std::vector<uint8_t> host(ls * 3 / 2);
 	CHECK(hipSetDevice(sc.dev));
+	const bool dbg = getenv("M2DEC_AMD_DEBUG") != nullptr;
 	for (int i = 0; i < r->npics; ++i) {
+		if (dbg) fprintf(stderr, "replay_md5: picture %d slot %d n_inter %d n_intra %d\n", i, r->pics[i].slot, r->pics[i].n_inter, r->pics[i].n_intra);
 		if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) return -1;
 		CHECK(hipMemcpy(host.data(), sc.frames + (size_t)r->pics[i].slot * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost));
 		m2d_frame_t f;
@@ -648,4 +679,21 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 extern "C" void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r)
 {
 	if (r) replay_free(r);
+}
+
+/* Diagnostic: copy the per-stream scratch words and the error word while kernels may still run
+ * (separate non-blocking stream). */
+extern "C" int m2dec_amd_hip_replay_debug_scratch(m2dec_amd_hip_replay_t *r, int *out, int n)
+{
+	if (!r) return -1;
+	Sched &sc = r->sc;
+	int need = SCR_WORDS(sc.Hmb) * NSTREAMS + 1;
+	if (n < need) return -1;
+	hipStream_t s;
+	CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+	CHECK(hipMemcpyAsync(out, sc.prog, sizeof(int) * SCR_WORDS(sc.Hmb) * NSTREAMS, hipMemcpyDeviceToHost, s));
+	CHECK(hipMemcpyAsync(out + need - 1, sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
+	CHECK(hipStreamSynchronize(s));
+	CHECK(hipStreamDestroy(s));
+	return need;
 }

@@ -1108,18 +1108,18 @@ __device__ __forceinline__ void edge_on_line(int *v, int at, int step, int bs, i
 
 
 /*
- * In-loop deblocking (deblock_pb, h264.cpp:10540-10663), one workgroup of three waves per MB row:
- *   wave 0 (loader) : polls the row above's progress word and copies the hand-off records of every
- *                     newly finished MB (its bottom 4 luma / 2 chroma rows after that row's filtering)
- *                     into the top halo of this row's LDS buffer (sc1 loads, G16 R1);
- *   wave 1 (filter) : filters MB after MB in LDS, in raster order: vertical edges with one row per
+ * In-loop deblocking (deblock_pb, h264.cpp:10540-10663), three waves of the MB row's workgroup:
+ *   wave 0 (loader) : copies MB after MB into a ring of DBK_RING MB slots in LDS: the MB's own
+ *                     16 luma / 8 chroma rows from the frame (final inter + intra samples) and, below
+ *                     row 0, the row above's hand-off record (its bottom 4 luma / 2 chroma rows after
+ *                     that row's filtering; sc1 loads, G16 R1) once the row above has published it;
+ *   wave 1 (filter) : filters MB after MB in LDS, in raster order: vertical edges with one line per
  *                     lane held in registers, then horizontal edges with one column per lane;
  *   wave 2 (storer) : writes every sample that became final to the frame, the hand-off records for
- *                     the row below (write-through sc1), drains, and publishes progress.
- * The whole MB row (20 luma / 10 chroma lines incl. the halo) lives in dynamic LDS, loaded once at
- * entry, so the filter wave never touches global memory and never waits on a memory round trip;
- * loader and storer batch every MB that is ready.  Waves talk through LDS words (workgroup-scope
- * release / acquire); workgroups through progress words (agent scope, sc1).
+ *                     the row below (write-through sc1), drains, publishes progress, frees the slots.
+ * The filter wave never touches global memory; loader and storer batch every MB that is ready.
+ * Ring columns wrap modulo DBK_RW, so the 4 columns left of an MB are the previous slot's.  Waves
+ * talk through LDS words (workgroup-scope release / acquire); workgroups through progress words.
  * Frame writes: rows 0..12 (chroma 0..6) of an MB by its own row, rows 13..15 (7) by the row below.
  */
 __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W, int H,
@@ -1127,44 +1127,35 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 {
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
 	const int nthr = blockDim.x;
-	const int S = W + 2 * DBK_PAD;           /* LDS line stride: DBK_PAD bytes of pad each side */
+	constexpr int S = DBK_RW;                /* ring line: DBK_RING MB columns, wrapping */
+	constexpr int M = DBK_RW - 1;
 	uint8_t *RL = smem;                      /* 20 luma lines: frame rows y0-4 .. y0+15 */
 	uint8_t *RC = smem + 20 * S;             /* 10 chroma lines: rows yc0-2 .. yc0+7 */
 	m2r_deblock_t *rq = (m2r_deblock_t *)(smem + 30 * S); /* [Wmb] this row's records, [Wmb] the row above's */
 	m2r_deblock_t *rt = rq + Wmb;
-	int *flags = (int *)(rt + Wmb);          /* [0] top halos ready, [1] MBs filtered */
+	int *flags = (int *)(rt + Wmb);          /* [0] MBs loaded, [1] MBs filtered, [2] MBs stored */
 	uint8_t *chroma = cur + (size_t)W * H;
 	const int y0 = y * 16, yc0 = y * 8;
 	const bool last_row = (y == Hmb - 1);
 
-	/* ---- prologue: this MB row and its records into LDS (all waves) */
-	for (int k = threadIdx.x; k < 16 * (W >> 4); k += nthr) {
-		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
-		*(uint4 *)(RL + (4 + r) * S + DBK_PAD + c) = *(const uint4 *)(cur + (size_t)(y0 + r) * W + c);
-	}
-	for (int k = threadIdx.x; k < 8 * (W >> 4); k += nthr) {
-		int r = k / (W >> 4), c = (k % (W >> 4)) * 16;
-		*(uint4 *)(RC + (2 + r) * S + DBK_PAD + c) = *(const uint4 *)(chroma + (size_t)(yc0 + r) * W + c);
-	}
+	/* ---- prologue: this row's (and the row above's) deblocking records into LDS */
 	for (int k = threadIdx.x; k < Wmb; k += nthr) {
 		rq[k] = dbk[y * Wmb + k];
 		rt[k] = y > 0 ? dbk[(y - 1) * Wmb + k] : rq[k];
 	}
-	if (threadIdx.x == 0) {
-		flags[0] = (y == 0) ? Wmb : 0;
-		flags[1] = 0;
-	}
+	if (threadIdx.x < 3) flags[threadIdx.x] = 0;
 	__syncthreads();
 
 	if (wave >= DBK_WAVES) return;
 	if (wave == 0) {
 		/* ---------------- loader */
-		if (y == 0) return;
+		const int per = (y > 0) ? 36 : 24; /* granules per MB: 16 luma + 8 chroma rows, 12 hand-off */
 		int got = 0, nld = 0;
 		unsigned spins = 0;
 		while (got < Wmb) {
-			int avail = __hip_atomic_load((gi32 *)&progress[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if (avail <= got) {
+			int lim = min(Wmb, __hip_atomic_load(&flags[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + DBK_RING);
+			if (y > 0) lim = min(lim, __hip_atomic_load((gi32 *)&progress[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+			if (lim <= got) {
 				if (!spin_ok(spins, err, 4)) {
 					/* give up (the launch is flagged bad): release the filter wave */
 					if (t == 0) __hip_atomic_store(&flags[0], Wmb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1173,18 +1164,25 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 				continue;
 			}
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-			/* 12 granules per MB: 8 luma (rows 12..15 x 2 halves), 4 chroma (rows 6..7 x 2 halves) */
-			for (int g0 = got * 12; g0 < avail * 12; g0 += 64) {
-				int g = g0 + t;
-				if (g < avail * 12) {
-					int mb = g / 12, k = g % 12;
-					unsigned long long v = ld_sc1(hbd + ((size_t)(y - 1) * Wmb + mb) * HBD_BYTES + k * 8);
-					uint8_t *d = (k < 8) ? RL + (k >> 1) * S + DBK_PAD + mb * 16 + (k & 1) * 8
-					                     : RC + ((k - 8) >> 1) * S + DBK_PAD + mb * 16 + (k & 1) * 8;
-					*(uint2 *)d = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+			const int ng = (lim - got) * per;
+			for (int g0 = 0; g0 < ng; g0 += 64) {
+				const int g = g0 + t;
+				if (g < ng) {
+					const int mb = got + g / per, k = g % per;
+					const int col = (mb & (DBK_RING - 1)) * 16;
+					if (k < 16) {
+						*(uint4 *)(RL + (4 + k) * S + col) = *(const uint4 *)(cur + (size_t)(y0 + k) * W + mb * 16);
+					} else if (k < 24) {
+						*(uint4 *)(RC + (2 + k - 16) * S + col) = *(const uint4 *)(chroma + (size_t)(yc0 + k - 16) * W + mb * 16);
+					} else {
+						const int h = k - 24; /* 8 luma granules (rows 12..15 x 2 halves), 4 chroma (rows 6..7) */
+						const unsigned long long v = ld_sc1(hbd + ((size_t)(y - 1) * Wmb + mb) * HBD_BYTES + h * 8);
+						uint8_t *d = (h < 8) ? RL + (h >> 1) * S + col + (h & 1) * 8 : RC + ((h - 8) >> 1) * S + col + (h & 1) * 8;
+						*(uint2 *)d = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+					}
 				}
 			}
-			got = avail;
+			got = lim;
 			if (t == 0) __hip_atomic_store(&flags[0], got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(y, 0, nld, got);
 			nld++;
@@ -1219,7 +1217,7 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 			const m2r_deblock_t q = rq[x];
 			if (!(q.flags & M2R_DBK_OFF)) {
 				const m2r_deblock_t pl = x > 0 ? rq[x - 1] : q, pt = rt[x];
-				const int base = DBK_PAD + x * 16; /* LDS column of the MB's first sample */
+				const int base = (x & (DBK_RING - 1)) * 16; /* ring column of the MB's first sample */
 				for (int dir = 0; dir < 2; ++dir) {
 					const uint32_t str = dir ? q.bs_h : q.bs_v;
 					const int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
@@ -1230,23 +1228,27 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 					const int nqc = comp ? nqc1 : nqc0;
 					const int qp_edge0 = e0 ? (luma ? (q.qpy + nqpy + 1) >> 1 : (qc + nqc + 1) >> 1) : 0;
 					const int qp_inner = luma ? q.qpy : qc;
-					/* line addressing: luma V row t / H column t; chroma V row cl / H byte column 2 cl + comp */
+					/* sample addressing: V: line t (luma) / cl (chroma), columns from 4 left of the MB,
+					 * wrapping in the ring; H: column t / byte column 2 cl + comp, lines 0..19 */
 					uint8_t *lb;
-					int st;
+					int c0, cst;
 					if (dir == 0) {
-						lb = luma ? RL + (4 + t) * S + base - 4 : RC + (2 + cl) * S + base - 4 + comp;
-						st = luma ? 1 : 2;
+						lb = luma ? RL + (4 + t) * S : RC + (2 + cl) * S;
+						c0 = base - 4 + (luma ? 0 : comp);
+						cst = luma ? 1 : 2;
 					} else {
 						lb = luma ? RL + base + t : RC + base + 2 * cl + comp;
-						st = S;
+						c0 = 0;
+						cst = S;
 					}
+#define DBK_ADDR(j) (dir == 0 ? lb + ((c0 + (j) * cst) & M) : lb + (j) * cst)
 					int v[20];
 #pragma unroll
 					for (int i = 0; i < 20; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6; /* chroma sample index for v[i] */
 						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
 						v[i] = 0;
-						if (active && (luma || cv)) v[i] = lb[(luma ? i : ci) * st];
+						if (active && (luma || cv)) v[i] = *DBK_ADDR(luma ? i : ci);
 					}
 #pragma unroll
 					for (int e = 0; e < 4; ++e) {
@@ -1291,12 +1293,16 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 							v[at + 2] = nq2;
 						}
 					}
+					/* write back; at x == 0 the 4 columns left of the MB wrap onto the slot the loader
+					 * may be filling, and edge 0 is off there anyway */
+					const int i0 = (dir == 0 && x == 0) ? 4 : 1;
 #pragma unroll
 					for (int i = 1; i < 19; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6;
 						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
-						if (active && (luma || cv)) lb[(luma ? i : ci) * st] = (uint8_t)v[i];
+						if (i >= i0 && active && (luma || cv)) *DBK_ADDR(luma ? i : ci) = (uint8_t)v[i];
 					}
+#undef DBK_ADDR
 					__builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): this direction's LDS writes landed */
 					__builtin_amdgcn_wave_barrier();
 				}
@@ -1329,8 +1335,9 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 					int g = g0 + t;
 					if (g < n * 12) {
 						int mb = done + g / 12, k = g % 12;
-						const uint8_t *sp = (k < 8) ? RL + (16 + (k >> 1)) * S + DBK_PAD + mb * 16 + (k & 1) * 8
-						                            : RC + (8 + ((k - 8) >> 1)) * S + DBK_PAD + mb * 16 + (k & 1) * 8;
+						const int col = (mb & (DBK_RING - 1)) * 16;
+						const uint8_t *sp = (k < 8) ? RL + (16 + (k >> 1)) * S + col + (k & 1) * 8
+						                            : RC + (8 + ((k - 8) >> 1)) * S + col + (k & 1) * 8;
 						uint2 v = *(const uint2 *)sp;
 						st_sc1(hbd + ((size_t)y * Wmb + mb) * HBD_BYTES + k * 8, ((unsigned long long)v.y << 32) | v.x);
 					}
@@ -1341,19 +1348,22 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 			for (int k = t; k < n * 64; k += 64) {
 				int mb = done + (k >> 6), r = (k >> 2) & 15, c = (k & 3) * 4;
 				if (last_row || r <= 12)
-					*(uint32_t *)(cur + (size_t)(y0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (4 + r) * S + DBK_PAD + mb * 16 + c);
+					*(uint32_t *)(cur + (size_t)(y0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + c);
 			}
 			if (y > 0)
 				for (int k = t; k < n * 16; k += 64) {
 					int mb = done + (k >> 4), r = (k >> 2) & 3, c = (k & 3) * 4;
-					if (r < 3) *(uint32_t *)(cur + (size_t)(y0 - 3 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (1 + r) * S + DBK_PAD + mb * 16 + c);
-					else *(uint32_t *)(chroma + (size_t)(yc0 - 1) * W + mb * 16 + c) = *(const uint32_t *)(RC + 1 * S + DBK_PAD + mb * 16 + c);
+					const int col = (mb & (DBK_RING - 1)) * 16 + c;
+					if (r < 3) *(uint32_t *)(cur + (size_t)(y0 - 3 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (1 + r) * S + col);
+					else *(uint32_t *)(chroma + (size_t)(yc0 - 1) * W + mb * 16 + c) = *(const uint32_t *)(RC + 1 * S + col);
 				}
 			for (int k = t; k < n * 32; k += 64) {
 				int mb = done + (k >> 5), r = (k >> 2) & 7, c = (k & 3) * 4;
 				if (last_row || r <= 6)
-					*(uint32_t *)(chroma + (size_t)(yc0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RC + (2 + r) * S + DBK_PAD + mb * 16 + c);
+					*(uint32_t *)(chroma + (size_t)(yc0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + c);
 			}
+			/* the slots' LDS reads are done (their values fed the stores above): hand them back */
+			if (t == 0) __hip_atomic_store(&flags[2], lim, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 			STAMP(y, 2, nst, lim);
 			nst++;
 			done = lim;
@@ -1446,7 +1456,8 @@ __global__ __launch_bounds__(256) void k_picture(PictureArgs a)
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)
 {
-	return (size_t)30 * (W + 2 * DBK_PAD) + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16;
+	(void)W;
+	return (size_t)30 * DBK_RW + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16;
 }
 
 extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)

@@ -11,7 +11,8 @@
 #define HBI_BYTES 32 /* intra hand-off per MB: bottom luma row (16 B) + bottom chroma row (16 B) */
 #define HBD_BYTES 96 /* deblock hand-off per MB: luma rows 12..15 (4 x 16 B) + chroma rows 6..7 (2 x 16 B) */
 #define DBK_WAVES 3  /* k_deblock workgroup: loader, filter, storer waves */
-#define DBK_PAD 16   /* k_deblock LDS pad each side of a line (keeps 16-B rows aligned) */
+#define DBK_RING 16  /* deblocking: MB slots of the LDS ring (power of two) */
+#define DBK_RW (DBK_RING * 16) /* ring line width in bytes */
 
 /* seq + 1 of the picture currently held by each frame slot (0: none) */
 struct SlotSeq {

@@ -49,6 +49,8 @@ __device__ unsigned long long g_stamps[STAMP_ROWS][4][STAMP_EV];
 #else
 #define STAMPI(row, role, idx, val) do { } while (0)
 #endif
+/* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
+#define STAMPX(x, k) do { if ((x) < 16) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
 /* ======================================================================== motion compensation */
 struct RefPlane {
@@ -285,10 +287,10 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 		int r = 0;
 		if (ccbp) {
 			if (pos == 0) {
-				r = d_chroma_dc(m, pool, cc, cblk);
+				r = d_chroma_dc(m, pool + m.coef, cc, cblk);
 			} else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(cc, cblk))) {
 				int bit = 19 + 4 * cc + cblk;
-				r = pool[m.coef + d_chroma_off(m, bit) + pos] * d_scale4(m.qpc[cc], cx & 3, cy & 3);
+				r = pool[m.coef + d_chroma_off(m, bit) + pos] * d_scale4(cc ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
 			}
 		}
 		s_res[256 + cc * 64 + cy * 8 + cx] = r;
@@ -482,60 +484,70 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 }
 
 /* ======================================================================== intra prediction (per sample) */
-/* 4x4 (h264.cpp:2510-2997) on neighbours P[0..7] (top, top-right replicated when unavailable),
- * L[0..3] (left), tl; returns -1 where the reference writes nothing. */
-__device__ int pred4_px(int mode, int avail, int x, int y, const int *P, const int *L, int tl)
+#define LW 25 /* intra luma context row: [0] = x0 - 1, [1..24] = x0 .. x0 + 23 */
+
+/* 4x4 (h264.cpp:2510-2997) on neighbours read straight from the LDS MB context: top row `top`
+ * (top[-1] = top-left, top[0..7] = top / top-right, the latter replaced by top[3] when unavailable)
+ * and the left column left[i * LW] (i = 0..3); returns -1 where the reference writes nothing.
+ * (Per-lane register arrays indexed by x + y would be placed in scratch.) */
+__device__ int pred4_px(int mode, int avail, int x, int y, const uint8_t *top, const uint8_t *left)
 {
-#define PP(i) ((i) < 0 ? tl : P[i])
-#define LL(i) ((i) < 0 ? tl : L[i])
+	const bool tr = (avail & 4) != 0;
+#define P(i) ((int)(((i) < 4 || tr) ? top[(i)] : top[3]))
+#define L(i) ((int)left[(i) * LW])
+	const int tl = top[-1];
+#define PP(i) ((i) < 0 ? tl : P(i))
+#define LL(i) ((i) < 0 ? tl : L(i))
 	switch (mode) {
-	case 0: return (avail & 2) ? P[x] : -1;
-	case 1: return (avail & 1) ? L[y] : -1;
+	case 0: return (avail & 2) ? P(x) : -1;
+	case 1: return (avail & 1) ? L(y) : -1;
 	case 2:
-		if ((avail & 3) == 3) return (P[0] + P[1] + P[2] + P[3] + L[0] + L[1] + L[2] + L[3] + 4) >> 3;
-		if (avail & 1) return (L[0] + L[1] + L[2] + L[3] + 2) >> 2;
-		if (avail & 2) return (P[0] + P[1] + P[2] + P[3] + 2) >> 2;
+		if ((avail & 3) == 3) return (P(0) + P(1) + P(2) + P(3) + L(0) + L(1) + L(2) + L(3) + 4) >> 3;
+		if (avail & 1) return (L(0) + L(1) + L(2) + L(3) + 2) >> 2;
+		if (avail & 2) return (P(0) + P(1) + P(2) + P(3) + 2) >> 2;
 		return 128;
 	case 3:
-		if (x == 3 && y == 3) return (P[6] + 3 * P[7] + 2) >> 2;
-		return (P[x + y] + 2 * P[x + y + 1] + P[x + y + 2] + 2) >> 2;
+		if (x == 3 && y == 3) return (P(6) + 3 * P(7) + 2) >> 2;
+		return (P(x + y) + 2 * P(x + y + 1) + P(x + y + 2) + 2) >> 2;
 	case 4:
 		if ((avail & 3) != 3) return -1;
-		if (x > y) return (PP(x - y - 2) + 2 * PP(x - y - 1) + P[x - y] + 2) >> 2;
-		if (x < y) return (LL(y - x - 2) + 2 * LL(y - x - 1) + L[y - x] + 2) >> 2;
-		return (P[0] + 2 * tl + L[0] + 2) >> 2;
+		if (x > y) return (PP(x - y - 2) + 2 * PP(x - y - 1) + P(x - y) + 2) >> 2;
+		if (x < y) return (LL(y - x - 2) + 2 * LL(y - x - 1) + L(y - x) + 2) >> 2;
+		return (P(0) + 2 * tl + L(0) + 2) >> 2;
 	case 5: {
 		if ((avail & 3) != 3) return -1;
 		int z = 2 * x - y, i = x - (y >> 1);
-		if (z >= 0 && !(z & 1)) return (PP(i - 1) + P[i] + 1) >> 1;
-		if (z >= 0) return (PP(i - 2) + 2 * PP(i - 1) + P[i] + 2) >> 2;
-		if (z == -1) return (L[0] + 2 * tl + P[0] + 2) >> 2;
-		return (L[y - 1] + 2 * L[y - 2] + LL(y - 3) + 2) >> 2;
+		if (z >= 0 && !(z & 1)) return (PP(i - 1) + P(i) + 1) >> 1;
+		if (z >= 0) return (PP(i - 2) + 2 * PP(i - 1) + P(i) + 2) >> 2;
+		if (z == -1) return (L(0) + 2 * tl + P(0) + 2) >> 2;
+		return (L(y - 1) + 2 * L(y - 2) + LL(y - 3) + 2) >> 2;
 	}
 	case 6: {
 		if ((avail & 3) != 3) return -1;
 		int z = 2 * y - x, i = y - (x >> 1);
-		if (z >= 0 && !(z & 1)) return (LL(i - 1) + L[i] + 1) >> 1;
-		if (z >= 0) return (LL(i - 2) + 2 * LL(i - 1) + L[i] + 2) >> 2;
-		if (z == -1) return (L[0] + 2 * tl + P[0] + 2) >> 2;
-		return (P[x - 1] + 2 * P[x - 2] + PP(x - 3) + 2) >> 2;
+		if (z >= 0 && !(z & 1)) return (LL(i - 1) + L(i) + 1) >> 1;
+		if (z >= 0) return (LL(i - 2) + 2 * LL(i - 1) + L(i) + 2) >> 2;
+		if (z == -1) return (L(0) + 2 * tl + P(0) + 2) >> 2;
+		return (P(x - 1) + 2 * P(x - 2) + PP(x - 3) + 2) >> 2;
 	}
 	case 7: {
 		int i = x + (y >> 1);
-		if (!(y & 1)) return (P[i] + P[i + 1] + 1) >> 1;
-		return (P[i] + 2 * P[i + 1] + P[i + 2] + 2) >> 2;
+		if (!(y & 1)) return (P(i) + P(i + 1) + 1) >> 1;
+		return (P(i) + 2 * P(i + 1) + P(i + 2) + 2) >> 2;
 	}
 	default: {
 		if (!(avail & 1)) return -1;
 		int z = x + 2 * y, i = y + (x >> 1);
-		if (z > 5) return L[3];
-		if (z == 5) return (L[2] + 3 * L[3] + 2) >> 2;
-		if (!(z & 1)) return (L[i] + L[i + 1] + 1) >> 1;
-		return (L[i] + 2 * L[i + 1] + L[i + 2] + 2) >> 2;
+		if (z > 5) return L(3);
+		if (z == 5) return (L(2) + 3 * L(3) + 2) >> 2;
+		if (!(z & 1)) return (L(i) + L(i + 1) + 1) >> 1;
+		return (L(i) + 2 * L(i + 1) + L(i + 2) + 2) >> 2;
 	}
 	}
 #undef PP
 #undef LL
+#undef P
+#undef L
 }
 
 /* 8x8 on filtered neighbours pt[0..15], lf[0..7], tlf (spec 8.3.2.2; h264.cpp:3301-3929) */
@@ -625,7 +637,6 @@ __device__ __forceinline__ int avail8(int b, int a)
 }
 
 /* ======================================================================== k_intra */
-#define LW 25 /* luma context row: [0] = x0 - 1, [1..24] = x0 .. x0 + 23 */
 
 /*
  * Intra / PCM macroblocks, one 64-lane workgroup per MB row, intra MBs left to right.  An intra MB
@@ -637,13 +648,28 @@ __device__ __forceinline__ int avail8(int b, int a)
  * with few intra MBs therefore carry no row-to-row chain through their inter MBs.
  */
 
-/* wave-level sync for the intra wavefront, which runs on ONE wave of its workgroup */
+/* wave-level sync for the intra wavefront, which runs on ONE wave of its workgroup: lanes talk
+ * through LDS only, so an LDS drain + wave barrier suffices (outstanding global prefetches are not
+ * waited for) */
 #define WSYNC()                                                  \
 	do {                                                         \
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
 		__builtin_amdgcn_wave_barrier();                         \
-		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
 	} while (0)
+
+union MbWords {
+	m2r_mb_t m;
+	int w[8];
+};
+
+/* lane `lane`'s record, as wave-uniform values */
+__device__ __forceinline__ m2r_mb_t lane_mb(const MbWords &mine, int lane)
+{
+	MbWords r;
+#pragma unroll
+	for (int i = 0; i < 8; ++i) r.w[i] = __builtin_amdgcn_readlane(mine.w[i], lane);
+	return r.m;
+}
 
 __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
                           uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
@@ -654,14 +680,20 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 	__shared__ int DC[16];
 	__shared__ int F[32];           /* filtered 8x8 neighbours: [0..15] top, [16..23] left, [24] top-left */
 	__shared__ int HV[4];
+	__shared__ int16_t Q[2][M2R_MB_COEF_MAX]; /* the current / next intra MB's coefficients */
 	uint8_t *chroma = cur + (size_t)W * H;
 	int prev_x = -2;
+	int qb = 0;
 	const int y0 = y * 16;
 
 	for (int xb = 0; xb < Wmb; xb += 64) {
-		/* intra MBs of this row in [xb, xb + 64) and of the row above in [xb - 1, xb + 65) */
+		/* this chunk's records, one per lane; intra MBs of this row in [xb, xb + 64) and of the row above in [xb - 1, xb + 65) */
 		const int xi = xb + t;
-		unsigned long long cur_mask = __ballot(xi < Wmb && mbs[y * Wmb + xi].kind != M2R_MB_INTER);
+		MbWords mine;
+#pragma unroll
+		for (int i = 0; i < 8; ++i) mine.w[i] = 0;
+		if (xi < Wmb) mine.m = mbs[y * Wmb + xi];
+		unsigned long long cur_mask = __ballot(xi < Wmb && mine.m.kind != M2R_MB_INTER);
 		unsigned long long up_mask = 0, up_lo = 0, up_hi = 0;
 		if (y > 0) {
 			up_mask = __ballot(xi < Wmb && mbs[(y - 1) * Wmb + xi].kind != M2R_MB_INTER);
@@ -675,10 +707,28 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 			if (k >= 64) return up_hi != 0;
 			return (up_mask >> k) & 1;
 		};
+		if (cur_mask) {
+			/* the chunk's first intra MB: stage its coefficients now (later ones are prefetched) */
+			const m2r_mb_t m0 = lane_mb(mine, __builtin_ctzll(cur_mask));
+			const int nq = d_mb_ncoef(m0);
+			for (int k = t; k < nq; k += 64) Q[qb][k] = pool[m0.coef + k];
+			WSYNC();
+		}
 		while (cur_mask) {
-		const int x = xb + __builtin_ctzll(cur_mask);
+		const int lx = __builtin_ctzll(cur_mask);
+		const int x = xb + lx;
 		cur_mask &= cur_mask - 1;
-		const m2r_mb_t m = mbs[y * Wmb + x];
+		const m2r_mb_t m = lane_mb(mine, lx);
+		const int16_t *q = Q[qb];
+		/* prefetch the next intra MB's coefficients into registers; they land in Q[qb ^ 1] at the end */
+		int16_t qv[7];
+		int nqn = 0;
+		if (cur_mask) {
+			const m2r_mb_t mn = lane_mb(mine, __builtin_ctzll(cur_mask));
+			nqn = d_mb_ncoef(mn);
+#pragma unroll
+			for (int i = 0; i < 7; ++i) qv[i] = (t + 64 * i < nqn) ? pool[mn.coef + t + 64 * i] : (int16_t)0;
+		}
 		const int x0 = x * 16;
 		const int left_in_lds = (prev_x == x - 1);
 		if (y > 0) {
@@ -718,9 +768,10 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 			if (t >= 16 && t < 32) { int k = t - 16; C[k & 1][1 + (k >> 1)][0] = chroma[(size_t)(y0 / 2 + (k >> 1)) * W + x0 - 2 + (k & 1)]; }
 		}
 		WSYNC();
+		STAMPX(x, 0);
 
 		if (m.kind == M2R_MB_PCM) {
-			const uint8_t *s = (const uint8_t *)(pool + m.coef);
+			const uint8_t *s = (const uint8_t *)q;
 			for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
 			for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
 			WSYNC();
@@ -761,56 +812,79 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 				if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
 			}
 			WSYNC();
+			STAMPX(x, 1);
 
 			/* ---- luma */
 			const int qp = m.qpy;
 			if (m.kind == M2R_MB_I4x4) {
+				/* residual of all 16 blocks first (independent of the prediction), then the serial
+				 * block chain: predict + add, one wave sync per block */
+				for (int k = t; k < 256; k += 64) {
+					const int blk = k >> 4, pos = k & 15;
+					int v = 0;
+					if ((m.nz >> blk) & 1) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
+					R[k] = v;
+				}
+				WSYNC();
+				{
+					int *p = &R[(t >> 2) * 16 + (t & 3) * 4];
+					int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+					d_idct4_1d(a0, a1, a2, a3);
+					p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
+				}
+				WSYNC();
+				{
+					int *p = &R[(t >> 2) * 16 + (t & 3)];
+					int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
+					d_idct4_1d(a0, a1, a2, a3);
+					p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
+				}
+				WSYNC();
 				for (int blk = 0; blk < 16; ++blk) {
 					const int ox = c_blk_x[blk] * 4, oy = c_blk_y[blk] * 4;
 					const int av = avail4(blk, m.avail_luma);
-					const int coded = (m.nz >> blk) & 1;
 					if (t < 16) {
-						int P[8], Lf[4];
-						for (int i = 0; i < 4; ++i) P[i] = L[oy][1 + ox + i];
-						for (int i = 4; i < 8; ++i) P[i] = (av & 4) ? L[oy][1 + ox + i] : P[3];
-						for (int i = 0; i < 4; ++i) Lf[i] = L[oy + 1 + i][ox];
-						int mode = (m.ipred[blk >> 3] >> (4 * (blk & 7))) & 15;
-						int v = pred4_px(mode, av, t & 3, t >> 2, P, Lf, L[oy][ox]);
-						R[64 + t] = v;
-						if (coded) R[t] = pool[m.coef + d_luma_off(m, blk) + t] * d_scale4(qp, t & 3, t >> 2);
-					}
-					WSYNC();
-					if (t < 16) {
-						int v = R[64 + t];
-						if (v >= 0) L[oy + 1 + (t >> 2)][1 + ox + (t & 3)] = (uint8_t)v;
-					}
-					if (coded) {
-						if (t < 4) {
-							int *p = &R[t * 4];
-							int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-							d_idct4_1d(a0, a1, a2, a3);
-							p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
-						}
-						WSYNC();
-						if (t < 4) {
-							int *p = &R[t];
-							int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
-							d_idct4_1d(a0, a1, a2, a3);
-							p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
-						}
-						WSYNC();
-						if (t < 16) {
-							uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
-							*d = (uint8_t)d_clip255(*d + R[t]);
-						}
+						const int mode = (((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15;
+						const int v = pred4_px(mode, av, t & 3, t >> 2, &L[oy][1 + ox], &L[oy + 1][ox]);
+						uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
+						const int base = (v >= 0) ? v : *d; /* the reference leaves the sample as it was */
+						*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
 					}
 					WSYNC();
 				}
 			} else if (m.kind == M2R_MB_I8x8) {
+				/* residual of all four 8x8 blocks first; per block: reference filtering, predict + add */
+				/* per block: nonzero count and DC level (the SWAR DC-only quirk), in LDS: a register
+				 * array indexed by the block loop would live in scratch */
+				for (int b = 0; b < 4; ++b) {
+					const int lv = ((m.nz >> (4 * b)) & 1) ? q[d_luma_off(m, 4 * b) + t] : 0;
+					R[b * 64 + t] = lv * d_scale8(qp, t & 7, t >> 3);
+					const int cnt = __popcll(__ballot(lv != 0));
+					if (t == 0) {
+						DC[b] = lv; /* lane 0 = coefficient 0 */
+						DC[4 + b] = cnt;
+					}
+				}
+				WSYNC();
+				if (t < 32) {
+					int v[8];
+					int *p = &R[(t >> 3) * 64 + (t & 7) * 8];
+					for (int k = 0; k < 8; ++k) v[k] = p[k];
+					d_idct8_1d(v);
+					for (int k = 0; k < 8; ++k) p[k] = v[k];
+				}
+				WSYNC();
+				if (t < 32) {
+					int v[8];
+					int *p = &R[(t >> 3) * 64 + (t & 7)];
+					for (int k = 0; k < 8; ++k) v[k] = p[k * 8];
+					d_idct8_1d(v);
+					for (int k = 0; k < 8; ++k) p[k * 8] = (v[k] + 32) >> 6;
+				}
+				WSYNC();
 				for (int b = 0; b < 4; ++b) {
 					const int ox = (b & 1) * 8, oy = (b >> 1) * 8;
 					const int av = avail8(b, m.avail_luma);
-					const int coded = (m.nz >> (4 * b)) & 1;
 					/* reference sample filtering (spec 8.3.2.2.1) */
 					if (t < 25) {
 						int hasL = av & 1, hasT = av & 2, hasTR = av & 4, hasTL = av & 8;
@@ -845,45 +919,15 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 #undef TP
 #undef LP
 					}
-					if (coded) {
-						int lv = pool[m.coef + d_luma_off(m, 4 * b) + t];
-						R[t] = lv * d_scale8(qp, t & 7, t >> 3);
-						R[128 + t] = (lv != 0);
-						if (t == 0) DC[0] = lv;
-					}
 					WSYNC();
 					{
-						int mode = (m.ipred[0] >> (4 * b)) & 15;
-						int v = pred8_px(mode, av, t & 7, t >> 3, F, F + 16, F[24]);
-						if (v >= 0) L[oy + 1 + (t >> 3)][1 + ox + (t & 7)] = (uint8_t)v;
-					}
-					if (coded) {
-						if (t < 8) {
-							int v[8];
-							int *p = &R[t * 8];
-							for (int k = 0; k < 8; ++k) v[k] = p[k];
-							d_idct8_1d(v);
-							for (int k = 0; k < 8; ++k) p[k] = v[k];
-						}
-						if (t == 8) {
-							int n = 0;
-							for (int k = 0; k < 64; ++k) n += R[128 + k];
-							HV[0] = n;
-						}
-						WSYNC();
-						if (t < 8) {
-							int v[8];
-							int *p = &R[t];
-							for (int k = 0; k < 8; ++k) v[k] = p[k * 8];
-							d_idct8_1d(v);
-							for (int k = 0; k < 8; ++k) p[k * 8] = (v[k] + 32) >> 6;
-						}
-						WSYNC();
-						{
-							uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
-							if (HV[0] == 1 && DC[0] != 0) *d = (uint8_t)d_swar(*d, DC[0] * d_scale8(qp, 0, 0), t & 7, 8);
-							else *d = (uint8_t)d_clip255(*d + R[t]);
-						}
+						const int mode = (m.ipred[0] >> (4 * b)) & 15;
+						const int v = pred8_px(mode, av, t & 7, t >> 3, F, F + 16, F[24]);
+						uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
+						const int base = (v >= 0) ? v : *d;
+						const int dcl = DC[b];
+						if (DC[4 + b] == 1 && dcl != 0) *d = (uint8_t)d_swar(base, dcl * d_scale8(qp, 0, 0), t & 7, 8);
+						else *d = (uint8_t)d_clip255(base + R[b * 64 + t]);
 					}
 					WSYNC();
 				}
@@ -906,7 +950,7 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 					HV[3] = ((av & 3) == 3) ? (st + sl + 16) >> 5 : ((av & 1) ? (sl + 8) >> 4 : ((av & 2) ? (st + 8) >> 4 : 128));
 				}
 				/* DC levels */
-				if (t < 16) DC[t] = (m.nz & M2R_NZ_LUMA_DC) ? pool[m.coef + t] * d_scale4(qp, 0, 0) : 0;
+				if (t < 16) DC[t] = (m.nz & M2R_NZ_LUMA_DC) ? q[t] * d_scale4(qp, 0, 0) : 0;
 				WSYNC();
 				for (int k = t; k < 256; k += 64) {
 					int px = k & 15, py = k >> 4, v = -1;
@@ -941,7 +985,7 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 						int bx = c_blk_x[blk], by = c_blk_y[blk];
 						int v = 0;
 						if (pos == 0) v = DC[by * 4 + bx];
-						else if (m.nz & (1u << blk)) v = pool[m.coef + d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
+						else if (m.nz & (1u << blk)) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
 						R[k] = v;
 					}
 					WSYNC();
@@ -978,6 +1022,7 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 				WSYNC();
 			}
 
+			STAMPX(x, 2);
 			/* ---- chroma residual (residual_chroma, h264.cpp:2374-2461) */
 			if (m.cbp >> 4) {
 				int ccbp = m.cbp >> 4;
@@ -985,9 +1030,9 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 					int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
 					int cblk = (cy >> 2) * 2 + (cx >> 2), pos = (cy & 3) * 4 + (cx & 3);
 					int v = 0;
-					if (pos == 0) v = d_chroma_dc(m, pool, c, cblk);
+					if (pos == 0) v = d_chroma_dc(m, q, c, cblk);
 					else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(c, cblk)))
-						v = pool[m.coef + d_chroma_off(m, 19 + 4 * c + cblk) + pos] * d_scale4(m.qpc[c], cx & 3, cy & 3);
+						v = q[d_chroma_off(m, 19 + 4 * c + cblk) + pos] * d_scale4(c ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
 					R[256 + c * 64 + cy * 8 + cx] = v;
 				}
 				WSYNC();
@@ -1016,6 +1061,7 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 			}
 		}
 
+		STAMPX(x, 3);
 		/* ---- write back and hand off the bottom rows */
 		for (int k = t; k < 256; k += 64) cur[(size_t)(y0 + (k >> 4)) * W + x0 + (k & 15)] = L[1 + (k >> 4)][1 + (k & 15)];
 		for (int k = t; k < 128; k += 64) {
@@ -1031,7 +1077,17 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 			}
 			st_sc1(hbi + ((size_t)y * Wmb + x) * HBI_BYTES + t * 8, v);
 		}
+		STAMPX(x, 4);
 		signal_progress(&progress[y], x + 1);
+		STAMP(y, 3, 16 + x, x);
+		STAMPX(x, 5);
+		/* the prefetched coefficients of the next intra MB */
+		if (nqn) {
+#pragma unroll
+			for (int i = 0; i < 7; ++i)
+				if (t + 64 * i < nqn) Q[qb ^ 1][t + 64 * i] = qv[i];
+		}
+		qb ^= 1;
 		prev_x = x;
 		WSYNC();
 		}
@@ -1040,72 +1096,6 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 }
 
 /* ======================================================================== k_deblock */
-
-/* one edge, register form (spec 8.7.2.3 / 8.7.2.4; deblock_*_str4 / _str1_3, h264.cpp:10337-10520).
- * p[0..3] = p0..p3, q[0..3] = q0..q3; only p0..p2 / q0..q2 change. */
-__device__ __forceinline__ void filter_regs(int *p, int *q, int bs, int alpha, int beta, int ia, bool luma)
-{
-	const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
-	if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-	if (bs < 4) {
-		int tc0 = c_tc0[ia][bs - 1], tc;
-		if (luma) {
-			const int p2 = p[2], q2 = q[2];
-			int ap = abs(p2 - p0) < beta, aq = abs(q2 - q0) < beta;
-			tc = tc0 + ap + aq;
-			if (ap) p[1] = p1 + d_clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
-			if (aq) q[1] = q1 + d_clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
-		} else {
-			tc = tc0 + 1;
-		}
-		int delta = d_clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-		p[0] = d_clip255(p0 + delta);
-		q[0] = d_clip255(q0 - delta);
-	} else if (luma) {
-		const int p2 = p[2], q2 = q[2], p3 = p[3], q3 = q[3];
-		int small = abs(p0 - q0) < ((alpha >> 2) + 2);
-		if (abs(p2 - p0) < beta && small) {
-			p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-			p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
-			p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
-		} else {
-			p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
-		}
-		if (abs(q2 - q0) < beta && small) {
-			q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-			q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
-			q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-		} else {
-			q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
-		}
-	} else {
-		p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
-		q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
-	}
-}
-
-__device__ __forceinline__ int ab_idx(int qp, int off)
-{
-	return min(max(qp + off, 0), 51);
-}
-
-/* filter the samples v[0..n) of one line across edge positions; (p3..p0 | q0..q3) around `at` */
-__device__ __forceinline__ void edge_on_line(int *v, int at, int step, int bs, int qp, int aoff, int boff, bool luma)
-{
-	if (!bs) return;
-	int ia = ab_idx(qp, aoff), ib = ab_idx(qp, boff);
-	int p[4], q[4];
-	for (int i = 0; i < 4; ++i) {
-		p[i] = (at - (i + 1) * step >= 0) ? v[at - (i + 1) * step] : 0;
-		q[i] = v[at + i * step];
-	}
-	filter_regs(p, q, bs, c_alpha[ia], c_beta[ib], ia, luma);
-	for (int i = 0; i < 3; ++i) {
-		if (at - (i + 1) * step >= 0) v[at - (i + 1) * step] = p[i];
-		v[at + i * step] = q[i];
-	}
-}
-
 
 /*
  * In-loop deblocking (deblock_pb, h264.cpp:10540-10663), three waves of the MB row's workgroup:

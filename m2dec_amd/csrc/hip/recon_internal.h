@@ -50,3 +50,4 @@ __global__ void k_picture(PictureArgs a); /* grid: inter_workers + Hmb, dynamic 
 
 /* dynamic LDS bytes of one k_deblock workgroup for a W-sample-wide picture */
 size_t m2r_deblock_lds_bytes(int W, int Wmb);
+extern "C" int m2dec_amd_debug_stamps_clear(void); /* no-op unless built with M2DEC_STAMPS */

@@ -111,12 +111,20 @@ __device__ __forceinline__ int d_chroma_off(const m2r_mb_t &m, int bit)
 	return off;
 }
 
+/* int16 words of the pool an MB owns (PCM: 384 sample bytes) */
+#define M2R_MB_COEF_MAX 416
+__device__ __forceinline__ int d_mb_ncoef(const m2r_mb_t &m)
+{
+	return m.kind == M2R_MB_PCM ? 192 : d_chroma_off(m, 27);
+}
+
 /* chroma DC of 4x4 block b of component c (intra_chroma_dc_transform, h264.cpp:4387-4404) */
-__device__ __forceinline__ int d_chroma_dc(const m2r_mb_t &m, const int16_t *pool, int c, int b)
+/* `q` points at the MB's own coefficients (pool + m.coef, or a staged copy) */
+__device__ __forceinline__ int d_chroma_dc(const m2r_mb_t &m, const int16_t *q, int c, int b)
 {
 	if (!(m.nz & M2R_NZ_CDC(c))) return 0;
-	const int16_t *p = pool + m.coef + d_chroma_off(m, 17 + c);
-	int s = d_scale4(m.qpc[c], 0, 0);
+	const int16_t *p = q + d_chroma_off(m, 17 + c);
+	int s = d_scale4(c ? m.qpc[1] : m.qpc[0], 0, 0);
 	int c0 = p[0] * s, c1 = p[1] * s, c2 = p[2] * s, c3 = p[3] * s;
 	switch (b) {
 	case 0: return (c0 + c1 + c2 + c3) >> 1;

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <vector>
 #include "recon_internal.h"
 #include "m2dec_amd.h"
@@ -623,9 +624,17 @@ extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
 {
 	if (!r) return -1;
 	CHECK(hipSetDevice(r->sc.dev));
+	const char *lim_env = getenv("M2DEC_AMD_REPLAY_LIMIT"); /* debug: first N pictures only */
+	const int lim = lim_env && atoi(lim_env) > 0 ? std::min(atoi(lim_env), r->npics) : r->npics;
+	const bool isolate = getenv("M2DEC_AMD_REPLAY_ISOLATE_LAST") != nullptr; /* debug: last picture alone */
 	for (int k = 0; k < passes; ++k)
-		for (int i = 0; i < r->npics; ++i)
+		for (int i = 0; i < lim; ++i) {
+			if (isolate && i == lim - 1) {
+				if (r->sc.sync_all() < 0) return -1;
+				m2dec_amd_debug_stamps_clear();
+			}
 			if (replay_enqueue(r, i, true) < 0) return -1;
+		}
 	return 0;
 }
 

@@ -1124,6 +1124,7 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 	m2r_deblock_t *rq = (m2r_deblock_t *)(smem + 30 * S); /* [Wmb] this row's records, [Wmb] the row above's */
 	m2r_deblock_t *rt = rq + Wmb;
 	int *flags = (int *)(rt + Wmb);          /* [0] MBs loaded, [1] MBs filtered, [2] MBs stored */
+	uint8_t *dummy = (uint8_t *)(flags + 4);  /* [64] per-lane sink for the filter's masked-off samples */
 	uint8_t *chroma = cur + (size_t)W * H;
 	const int y0 = y * 16, yc0 = y * 8;
 	const bool last_row = (y == Hmb - 1);
@@ -1208,6 +1209,7 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 			if (!(q.flags & M2R_DBK_OFF)) {
 				const m2r_deblock_t pl = x > 0 ? rq[x - 1] : q, pt = rt[x];
 				const int base = (x & (DBK_RING - 1)) * 16; /* ring column of the MB's first sample */
+#pragma unroll
 				for (int dir = 0; dir < 2; ++dir) {
 					const uint32_t str = dir ? q.bs_h : q.bs_v;
 					const int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
@@ -1232,13 +1234,16 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 						cst = S;
 					}
 #define DBK_ADDR(j) (dir == 0 ? lb + ((c0 + (j) * cst) & M) : lb + (j) * cst)
+					/* branch-free sample access: a masked-off sample goes to the lane's dummy byte (an
+					 * exec-masked load/store per sample would cost a branch each) */
+					uint8_t *const sink = dummy + t;
 					int v[20];
 #pragma unroll
 					for (int i = 0; i < 20; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6; /* chroma sample index for v[i] */
 						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
-						v[i] = 0;
-						if (active && (luma || cv)) v[i] = *DBK_ADDR(luma ? i : ci);
+						const bool ok = active && (luma || cv);
+						v[i] = *(ok ? DBK_ADDR(luma ? i : ci) : sink);
 					}
 #pragma unroll
 					for (int e = 0; e < 4; ++e) {
@@ -1290,7 +1295,8 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 					for (int i = 1; i < 19; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6;
 						const bool cv = (i >= 2 && i <= 5) || (i >= 10 && i <= 13);
-						if (i >= i0 && active && (luma || cv)) *DBK_ADDR(luma ? i : ci) = (uint8_t)v[i];
+						const bool ok = i >= i0 && active && (luma || cv);
+						*(ok ? DBK_ADDR(luma ? i : ci) : sink) = (uint8_t)v[i];
 					}
 #undef DBK_ADDR
 					__builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): this direction's LDS writes landed */
@@ -1447,7 +1453,7 @@ __global__ __launch_bounds__(256) void k_picture(PictureArgs a)
 size_t m2r_deblock_lds_bytes(int W, int Wmb)
 {
 	(void)W;
-	return (size_t)30 * DBK_RW + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16;
+	return (size_t)30 * DBK_RW + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
 }
 
 extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)

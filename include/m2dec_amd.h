@@ -55,12 +55,14 @@ int m2dec_amd_hip_available(void);
 
 /* Per-kernel timing of the HIP back end since creation (microseconds, HIP events). */
 typedef struct {
-	double picture_us;      /* k_picture (inter + intra + deblock of one picture, overlapped row by row) */
+	double picture_us;      /* kernel time: k_picture launches (decode path) / k_batch launches (replay) */
 	double h2d_us, d2h_us;  /* decode path only: record upload, frame download */
-	int64_t pictures, inter_launches, intra_launches, deblock_launches;
+	int64_t pictures;       /* pictures reconstructed */
+	int64_t inter_launches, intra_launches, deblock_launches; /* pictures with inter MBs / intra MBs / deblocked */
 	int64_t record_bytes;   /* bytes of records uploaded (R_pic summed) */
 	int64_t ref_bytes;      /* algorithmic reference bytes read by MC (sum over PUs and lists) */
 	int64_t frame_bytes;    /* NV12 bytes written (1.5 W H per picture) */
+	int64_t kernel_launches; /* k_picture / k_batch launches timed in picture_us */
 } m2dec_amd_hip_timing_t;
 int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out);
 

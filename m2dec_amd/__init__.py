@@ -55,7 +55,7 @@ class HipTiming(ctypes.Structure):
                 ("pictures", ctypes.c_int64),
                 ("inter_launches", ctypes.c_int64), ("intra_launches", ctypes.c_int64),
                 ("deblock_launches", ctypes.c_int64), ("record_bytes", ctypes.c_int64),
-                ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64)]
+                ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64), ("kernel_launches", ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -671,16 +671,27 @@ __device__ __forceinline__ m2r_mb_t lane_mb(const MbWords &mine, int lane)
 	return r.m;
 }
 
-__device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
+/* one intra wave's LDS context (carved from the dynamic LDS: two rows run their intra at once) */
+struct IntraLDS {
+	uint8_t L[17][LW];   /* row 0: top neighbours; rows 1..16: MB rows; col 0: left neighbour */
+	uint8_t C[2][9][9];  /* per component: row 0 top (col 0 top-left), col 0 left */
+	int R[256 + 128];
+	int DC[16];
+	int F[32];           /* filtered 8x8 neighbours: [0..15] top, [16..23] left, [24] top-left */
+	int HV[4];
+	int16_t Q[2][M2R_MB_COEF_MAX]; /* the current / next intra MB's coefficients */
+};
+
+__device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
                           uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
 {
-	__shared__ uint8_t L[17][LW];   /* row 0: top neighbours; rows 1..16: MB rows; col 0: left neighbour */
-	__shared__ uint8_t C[2][9][9];  /* per component: row 0 top (col 0 top-left), col 0 left */
-	__shared__ int R[256 + 128];
-	__shared__ int DC[16];
-	__shared__ int F[32];           /* filtered 8x8 neighbours: [0..15] top, [16..23] left, [24] top-left */
-	__shared__ int HV[4];
-	__shared__ int16_t Q[2][M2R_MB_COEF_MAX]; /* the current / next intra MB's coefficients */
+	uint8_t(&L)[17][LW] = ctx->L;
+	uint8_t(&C)[2][9][9] = ctx->C;
+	int(&R)[256 + 128] = ctx->R;
+	int(&DC)[16] = ctx->DC;
+	int(&F)[32] = ctx->F;
+	int(&HV)[4] = ctx->HV;
+	int16_t(&Q)[2][M2R_MB_COEF_MAX] = ctx->Q;
 	uint8_t *chroma = cur + (size_t)W * H;
 	int prev_x = -2;
 	int qb = 0;
@@ -1098,54 +1109,100 @@ __device__ void intra_row(const int y, const int t, const m2r_mb_t *__restrict__
 /* ======================================================================== k_deblock */
 
 /*
- * In-loop deblocking (deblock_pb, h264.cpp:10540-10663), three waves of the MB row's workgroup:
- *   wave 0 (loader) : copies MB after MB into a ring of DBK_RING MB slots in LDS: the MB's own
- *                     16 luma / 8 chroma rows from the frame (final inter + intra samples) and, below
- *                     row 0, the row above's hand-off record (its bottom 4 luma / 2 chroma rows after
- *                     that row's filtering; sc1 loads, G16 R1) once the row above has published it;
- *   wave 1 (filter) : filters MB after MB in LDS, in raster order: vertical edges with one line per
- *                     lane held in registers, then horizontal edges with one column per lane;
- *   wave 2 (storer) : writes every sample that became final to the frame, the hand-off records for
- *                     the row below (write-through sc1), drains, publishes progress, frees the slots.
- * The filter wave never touches global memory; loader and storer batch every MB that is ready.
- * Ring columns wrap modulo DBK_RW, so the 4 columns left of an MB are the previous slot's.  Waves
- * talk through LDS words (workgroup-scope release / acquire); workgroups through progress words.
- * Frame writes: rows 0..12 (chroma 0..6) of an MB by its own row, rows 13..15 (7) by the row below.
+ * In-loop deblocking (deblock_pb, h264.cpp:10540-10663) of TWO MB rows, A = yA and B = yA + 1, by
+ * the four waves of the rows' workgroup:
+ *   wave 0 (loader)   : copies MB after MB into a ring of DBK_RING MB slots in LDS: both rows' own
+ *                       16 luma / 8 chroma rows from the frame (final inter + intra samples) and, below
+ *                       row 0, the hand-off record of the row above A (its bottom 4 luma / 2 chroma
+ *                       rows after that row's filtering; sc1 loads, G16 R1) once that row published it;
+ *   wave 1 (filter A) / wave 3 (filter B): MB after MB in raster order, lanes 0..15 luma lines,
+ *                       16..31 chroma lines; vertical edges with one line per lane, then horizontal
+ *                       edges with one column per lane.  Row B's MB x waits (LDS word) until row A
+ *                       finished MB x + 1: its top halo is row A's bottom lines in the same ring, so
+ *                       the A -> B hand-off never leaves LDS, and the two filters run side by side;
+ *   wave 2 (storer)   : writes every sample that became final to the frame, the hand-off records of
+ *                       row B for the next workgroup (write-through sc1), drains, publishes progress,
+ *                       frees the ring slots.
+ * Ring lines: luma 0..3 halo (row above A, rows 12..15), 4..19 row A, 20..35 row B; chroma 0..1 halo,
+ * 2..9 row A, 10..17 row B.  Ring columns wrap modulo DBK_RW.  Frame writes: rows 0..12 (chroma 0..6)
+ * of an MB once its own row filtered it and its right neighbour, rows 13..15 (7) once the row below
+ * filtered it.
  */
-__device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur, int W, int H,
-                            int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err, int *rowflag, int seq)
+__device__ __forceinline__ int dbk_done012(int c, int Wmb) { return c >= Wmb ? Wmb : max(c - 1, 0); }
+
+__device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur,
+                             int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err, int *rowflag, int seq)
 {
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
 	const int nthr = blockDim.x;
 	constexpr int S = DBK_RW;                /* ring line: DBK_RING MB columns, wrapping */
 	constexpr int M = DBK_RW - 1;
-	uint8_t *RL = smem;                      /* 20 luma lines: frame rows y0-4 .. y0+15 */
-	uint8_t *RC = smem + 20 * S;             /* 10 chroma lines: rows yc0-2 .. yc0+7 */
-	m2r_deblock_t *rq = (m2r_deblock_t *)(smem + 30 * S); /* [Wmb] this row's records, [Wmb] the row above's */
-	m2r_deblock_t *rt = rq + Wmb;
-	int *flags = (int *)(rt + Wmb);          /* [0] MBs loaded, [1] MBs filtered, [2] MBs stored */
+	uint8_t *RL = smem;                      /* 36 luma lines */
+	uint8_t *RC = smem + 36 * S;             /* 18 chroma lines */
+	m2r_deblock_t *rT = (m2r_deblock_t *)(smem + 54 * S); /* [Wmb] records of the row above A (A's own if yA == 0) */
+	m2r_deblock_t *rA = rT + Wmb;            /* [Wmb] row A */
+	m2r_deblock_t *rB = rA + Wmb;            /* [Wmb] row B */
+	int *flags = (int *)(rB + Wmb);          /* [0] MBs loaded, [1] row A MBs filtered, [2] MBs stored, [3] row B MBs filtered */
 	uint8_t *dummy = (uint8_t *)(flags + 4);  /* [64] per-lane sink for the filter's masked-off samples */
 	uint8_t *chroma = cur + (size_t)W * H;
-	const int y0 = y * 16, yc0 = y * 8;
-	const bool last_row = (y == Hmb - 1);
+	const int yB = yA + 1;
+	const bool lastA = !hasB;                /* row A is the picture's last row */
+	const bool lastB = hasB && yB == Hmb - 1;
 
-	/* ---- prologue: this row's (and the row above's) deblocking records into LDS */
-	for (int k = threadIdx.x; k < Wmb; k += nthr) {
-		rq[k] = dbk[y * Wmb + k];
-		rt[k] = y > 0 ? dbk[(y - 1) * Wmb + k] : rq[k];
+	__shared__ uint8_t s_alpha[52], s_beta[52], s_tc0[52][3];
+	/* ---- prologue: the deblocking records and the tables into LDS */
+	for (int i = threadIdx.x; i < 52; i += nthr) {
+		s_alpha[i] = c_alpha[i];
+		s_beta[i] = c_beta[i];
+		s_tc0[i][0] = c_tc0[i][0];
+		s_tc0[i][1] = c_tc0[i][1];
+		s_tc0[i][2] = c_tc0[i][2];
 	}
-	if (threadIdx.x < 3) flags[threadIdx.x] = 0;
+	for (int k = threadIdx.x; k < Wmb; k += nthr) {
+		rA[k] = dbk[yA * Wmb + k];
+		rT[k] = dbk[(yA > 0 ? yA - 1 : yA) * Wmb + k]; /* (a struct-valued ?: would go through scratch) */
+		if (hasB) rB[k] = dbk[yB * Wmb + k];
+	}
+	if (threadIdx.x < 4) flags[threadIdx.x] = 0;
 	__syncthreads();
 
-	if (wave >= DBK_WAVES) return;
+	/* the deblocking chain is the picture's critical path: let its waves win the SIMD arbitration
+	 * over co-resident inter workers (filters highest) */
+	if (wave == 1 || wave == 3) __builtin_amdgcn_s_setprio(3);
+	else __builtin_amdgcn_s_setprio(2);
 	if (wave == 0) {
-		/* ---------------- loader */
-		const int per = (y > 0) ? 36 : 24; /* granules per MB: 16 luma + 8 chroma rows, 12 hand-off */
-		int got = 0, nld = 0;
+		/* ---------------- loader: own samples run ahead as far as the ring allows (prep); only the
+		 * hand-off record of the row above A waits for that row (got) */
+		const int per = hasB ? 48 : 24; /* granules per MB: 16 luma + 8 chroma rows per row */
+		int prep = 0, got = 0, nld = 0;
 		unsigned spins = 0;
 		while (got < Wmb) {
-			int lim = min(Wmb, __hip_atomic_load(&flags[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + DBK_RING);
-			if (y > 0) lim = min(lim, __hip_atomic_load((gi32 *)&progress[y - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+			const int ring = min(Wmb, __hip_atomic_load(&flags[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + DBK_RING);
+			if (prep < ring) {
+				const int ng = (ring - prep) * per;
+				for (int g0 = 0; g0 < ng; g0 += 64) {
+					const int g = g0 + t;
+					if (g < ng) {
+						const int mb = prep + g / per, k = g % per;
+						const int r = k >= 24, kk = k - 24 * r; /* row A / B, granule within the row */
+						const int col = (mb & (DBK_RING - 1)) * 16;
+						const int y0 = (yA + r) * 16, yc0 = (yA + r) * 8;
+						if (kk < 16) *(uint4 *)(RL + (4 + 16 * r + kk) * S + col) = *(const uint4 *)(cur + (size_t)(y0 + kk) * W + mb * 16);
+						else *(uint4 *)(RC + (2 + 8 * r + kk - 16) * S + col) = *(const uint4 *)(chroma + (size_t)(yc0 + kk - 16) * W + mb * 16);
+					}
+				}
+				prep = ring;
+				if (yA == 0) {
+					got = prep;
+					if (t == 0) __hip_atomic_store(&flags[0], got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+				}
+				continue;
+			}
+			if (yA == 0) {
+				if (!spin_ok(spins, err, 4)) return;
+				continue;
+			}
+			const int lim = min(prep, __hip_atomic_load((gi32 *)&progress[yA - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 			if (lim <= got) {
 				if (!spin_ok(spins, err, 4)) {
 					/* give up (the launch is flagged bad): release the filter wave */
@@ -1155,56 +1212,52 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 				continue;
 			}
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-			const int ng = (lim - got) * per;
+			/* 12 hand-off granules per MB: 8 luma (rows 12..15 x 2 halves), 4 chroma (rows 6..7) */
+			const int ng = (lim - got) * 12;
 			for (int g0 = 0; g0 < ng; g0 += 64) {
 				const int g = g0 + t;
 				if (g < ng) {
-					const int mb = got + g / per, k = g % per;
+					const int mb = got + g / 12, h = g % 12;
 					const int col = (mb & (DBK_RING - 1)) * 16;
-					if (k < 16) {
-						*(uint4 *)(RL + (4 + k) * S + col) = *(const uint4 *)(cur + (size_t)(y0 + k) * W + mb * 16);
-					} else if (k < 24) {
-						*(uint4 *)(RC + (2 + k - 16) * S + col) = *(const uint4 *)(chroma + (size_t)(yc0 + k - 16) * W + mb * 16);
-					} else {
-						const int h = k - 24; /* 8 luma granules (rows 12..15 x 2 halves), 4 chroma (rows 6..7) */
-						const unsigned long long v = ld_sc1(hbd + ((size_t)(y - 1) * Wmb + mb) * HBD_BYTES + h * 8);
-						uint8_t *d = (h < 8) ? RL + (h >> 1) * S + col + (h & 1) * 8 : RC + ((h - 8) >> 1) * S + col + (h & 1) * 8;
-						*(uint2 *)d = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-					}
+					const unsigned long long v = ld_sc1(hbd + ((size_t)(yA - 1) * Wmb + mb) * HBD_BYTES + h * 8);
+					uint8_t *d = (h < 8) ? RL + (h >> 1) * S + col + (h & 1) * 8 : RC + ((h - 8) >> 1) * S + col + (h & 1) * 8;
+					*(uint2 *)d = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 				}
 			}
 			got = lim;
 			if (t == 0) __hip_atomic_store(&flags[0], got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-			STAMP(y, 0, nld, got);
+			STAMP(yA, 0, nld, got);
 			nld++;
 		}
 		return;
 	}
 
-	if (wave == 1) {
-		/* ---------------- filter: one instruction stream for 16 luma lines (lanes 0..15) and 16 chroma
-		 * lines (lanes 16..31: Cb 16..23, Cr 24..31), branch-free per edge.  A chroma line keeps its
-		 * samples 0..3 / 4..7 at v[2..5] / v[10..13] so that its two edges sit where luma edges 0 and 2 do. */
-		__shared__ uint8_t s_alpha[52], s_beta[52], s_tc0[52][3];
-		for (int i = t; i < 52; i += 64) {
-			s_alpha[i] = c_alpha[i];
-			s_beta[i] = c_beta[i];
-			s_tc0[i][0] = c_tc0[i][0];
-			s_tc0[i][1] = c_tc0[i][1];
-			s_tc0[i][2] = c_tc0[i][2];
-		}
+	if (wave == 1 || wave == 3) {
+		/* ---------------- filter (one row per wave): lanes 0..15 luma lines, 16..31 chroma lines (Cb
+		 * 16..23, Cr 24..31), branch-free per edge.  A chroma line keeps its samples 0..3 / 4..7 at
+		 * v[2..5] / v[10..13] so that its two edges sit where luma edges 0 and 2 do. */
+		const bool rowB = wave == 3;
+		if (rowB && !hasB) return;
+		const m2r_deblock_t *rq = rowB ? rB : rA, *rt = rowB ? rA : rT;
+		const int lumaL0 = rowB ? 20 : 4, chromaL0 = rowB ? 10 : 2; /* first own line of this row */
+		int *done = &flags[rowB ? 3 : 1];
 		const bool active = t < 32;
 		const bool luma = t < 16;
 		const int comp = (t >> 3) & 1;        /* chroma lanes */
 		const int cl = t & 7;                 /* chroma line (row for dir 0, column for dir 1) */
 		const int seg_l = (t & 15) >> 2, seg_c = cl >> 1;
 		const int seg = luma ? seg_l : seg_c;
+		uint8_t *const sink = dummy + t;
 		unsigned spins = 0;
 		for (int x = 0; x < Wmb; ++x) {
 			while (__hip_atomic_load(&flags[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= x) {
 				if (!spin_ok(spins, err, 16)) break;
 			}
-			STAMP(y, 1, x, x);
+			if (rowB) /* row A's MB x is final for us once A filtered MB x + 1 */
+				while (__hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < min(x + 2, Wmb)) {
+					if (!spin_ok(spins, err, 16)) break;
+				}
+			STAMP(yA + rowB, 1, x, x);
 			const m2r_deblock_t q = rq[x];
 			if (!(q.flags & M2R_DBK_OFF)) {
 				const m2r_deblock_t pl = x > 0 ? rq[x - 1] : q, pt = rt[x];
@@ -1220,23 +1273,22 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 					const int nqc = comp ? nqc1 : nqc0;
 					const int qp_edge0 = e0 ? (luma ? (q.qpy + nqpy + 1) >> 1 : (qc + nqc + 1) >> 1) : 0;
 					const int qp_inner = luma ? q.qpy : qc;
-					/* sample addressing: V: line t (luma) / cl (chroma), columns from 4 left of the MB,
-					 * wrapping in the ring; H: column t / byte column 2 cl + comp, lines 0..19 */
+					/* sample addressing: V: own line, columns from 4 left of the MB, wrapping in the ring;
+					 * H: column t / byte column 2 cl + comp, lines from 4 (2) above the row */
 					uint8_t *lb;
 					int c0, cst;
 					if (dir == 0) {
-						lb = luma ? RL + (4 + t) * S : RC + (2 + cl) * S;
+						lb = luma ? RL + (lumaL0 + t) * S : RC + (chromaL0 + cl) * S;
 						c0 = base - 4 + (luma ? 0 : comp);
 						cst = luma ? 1 : 2;
 					} else {
-						lb = luma ? RL + base + t : RC + base + 2 * cl + comp;
+						lb = luma ? RL + (lumaL0 - 4) * S + base + t : RC + (chromaL0 - 2) * S + base + 2 * cl + comp;
 						c0 = 0;
 						cst = S;
 					}
 #define DBK_ADDR(j) (dir == 0 ? lb + ((c0 + (j) * cst) & M) : lb + (j) * cst)
 					/* branch-free sample access: a masked-off sample goes to the lane's dummy byte (an
 					 * exec-masked load/store per sample would cost a branch each) */
-					uint8_t *const sink = dummy + t;
 					int v[20];
 #pragma unroll
 					for (int i = 0; i < 20; ++i) {
@@ -1254,42 +1306,43 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 						const int qp = e ? qp_inner : qp_edge0;
 						const int ia = min(max(qp + q.alpha_off, 0), 51), ib = min(max(qp + q.beta_off, 0), 51);
 						const int A = s_alpha[ia], B = s_beta[ib];
-						const int tc0 = bs ? s_tc0[ia][min(bs, 3) - 1] : 0;
+						const int tc0l = s_tc0[ia][max(min(bs, 3) - 1, 0)]; /* unconditional load, then select */
+						const int tc0 = bs ? tc0l : 0;
 						const int at = 4 + 4 * e;
 						const int p0 = v[at - 1], p1 = v[at - 2], p2 = v[at - 3], p3 = v[at - 4];
 						const int q0 = v[at], q1 = v[at + 1], q2 = v[at + 2], q3 = v[at + 3];
-						const bool filt = bs && abs(p0 - q0) < A && abs(p1 - p0) < B && abs(q1 - q0) < B;
+						/* bitwise, not short-circuit: && here becomes exec-mask branches */
+						const bool filt = (bs != 0) & (abs(p0 - q0) < A) & (abs(p1 - p0) < B) & (abs(q1 - q0) < B);
 						const bool ap = abs(p2 - p0) < B, aq = abs(q2 - q0) < B;
+						/* every candidate computed, then selected */
 						/* bS < 4 */
 						const int tc = tc0 + (luma ? (int)ap + (int)aq : 1);
 						const int delta = d_clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
 						const int avg = (p0 + q0 + 1) >> 1;
-						int np0 = d_clip255(p0 + delta), nq0 = d_clip255(q0 - delta);
-						int np1 = (luma && ap) ? p1 + d_clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1) : p1;
-						int nq1 = (luma && aq) ? q1 + d_clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1) : q1;
-						int np2 = p2, nq2 = q2;
+						const int w0 = d_clip255(p0 + delta), w1 = d_clip255(q0 - delta);
+						const int wp1 = p1 + d_clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1);
+						const int wq1 = q1 + d_clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1);
 						/* bS == 4 */
-						if (bs == 4) {
-							const bool small = abs(p0 - q0) < ((A >> 2) + 2);
-							const bool sp = luma && ap && small, sq = luma && aq && small;
-							np0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
-							np1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
-							np2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
-							nq0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
-							nq1 = sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1;
-							nq2 = sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
-						}
-						if (filt) {
-							v[at - 1] = np0;
-							v[at - 2] = np1;
-							v[at - 3] = np2;
-							v[at] = nq0;
-							v[at + 1] = nq1;
-							v[at + 2] = nq2;
-						}
+						const bool small = abs(p0 - q0) < ((A >> 2) + 2);
+						const bool sp = luma & ap & small, sq = luma & aq & small;
+						const int a0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, b0 = (2 * p1 + p0 + q1 + 2) >> 2;
+						const int a1 = (p2 + p1 + p0 + q0 + 2) >> 2, a2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+						const int c0_ = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, e0_ = (2 * q1 + q0 + p1 + 2) >> 2;
+						const int c1 = (p0 + q0 + q1 + q2 + 2) >> 2, c2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+						const bool strong = bs == 4;
+						const int np0 = d_sel(strong, d_sel(sp, a0, b0), w0), nq0 = d_sel(strong, d_sel(sq, c0_, e0_), w1);
+						const int np1 = d_sel(strong, d_sel(sp, a1, p1), d_sel(luma & ap, wp1, p1));
+						const int nq1 = d_sel(strong, d_sel(sq, c1, q1), d_sel(luma & aq, wq1, q1));
+						const int np2 = d_sel(strong & sp, a2, p2), nq2 = d_sel(strong & sq, c2, q2);
+						v[at - 1] = d_sel(filt, np0, p0);
+						v[at - 2] = d_sel(filt, np1, p1);
+						v[at - 3] = d_sel(filt, np2, p2);
+						v[at] = d_sel(filt, nq0, q0);
+						v[at + 1] = d_sel(filt, nq1, q1);
+						v[at + 2] = d_sel(filt, nq2, q2);
 					}
-					/* write back; at x == 0 the 4 columns left of the MB wrap onto the slot the loader
-					 * may be filling, and edge 0 is off there anyway */
+					/* write back; at x == 0 the 4 columns left of the MB wrap onto a slot the loader may
+					 * be filling, and edge 0 is off there anyway */
 					const int i0 = (dir == 0 && x == 0) ? 4 : 1;
 #pragma unroll
 					for (int i = 1; i < 19; ++i) {
@@ -1303,74 +1356,109 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 					__builtin_amdgcn_wave_barrier();
 				}
 			}
-			if (t == 0) __hip_atomic_store(&flags[1], x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (t == 0) __hip_atomic_store(done, x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 		}
-		STAMP(y, 1, Wmb, Wmb);
+		STAMP(yA + rowB, 1, Wmb, Wmb);
 		return;
 	}
 
 	/* ---------------- storer (wave 2) */
 	{
-		int done = 0, nst = 0;
+		int dA = 0, dA13 = 0, dB = 0, nst = 0;
 		unsigned spins = 0;
-		while (done < Wmb) {
-			int f = __hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-			int lim = (f >= Wmb) ? Wmb : f - 1; /* MB f-1 waits for MB f's vertical edges */
-			if (lim <= done) {
+		const int y0A = yA * 16, yc0A = yA * 8, y0B = yB * 16, yc0B = yB * 8;
+		for (;;) {
+			const int cA = __hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			const int cB = hasB ? __hip_atomic_load(&flags[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+			const int tA = dbk_done012(cA, Wmb);
+			const int tA13 = cB;                 /* row B filtered MB m (so row A had MB m + 1 done) */
+			const int tB = hasB ? dbk_done012(cB, Wmb) : 0;
+			if (tA <= dA && tA13 <= dA13 && tB <= dB) {
+				if ((hasB ? dB : dA) >= Wmb) break;
 				if (!spin_ok(spins, err, 8)) {
-					if (!last_row) signal_progress(&progress[y], Wmb); /* release the row below */
-					if (t == 0) __hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + y], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-					return;
+					if (hasB && !lastB) signal_progress(&progress[yB], Wmb); /* release the next workgroup */
+					break;
 				}
 				continue;
 			}
-			const int n = lim - done;
-			/* the row below waits on the hand-off records: write them first, drain, publish */
-			if (!last_row) {
+			/* the next workgroup waits on row B's hand-off records: write them first, drain, publish */
+			if (tB > dB && !lastB) {
+				const int n = tB - dB;
 				for (int g0 = 0; g0 < n * 12; g0 += 64) {
-					int g = g0 + t;
+					const int g = g0 + t;
 					if (g < n * 12) {
-						int mb = done + g / 12, k = g % 12;
+						const int mb = dB + g / 12, k = g % 12;
 						const int col = (mb & (DBK_RING - 1)) * 16;
-						const uint8_t *sp = (k < 8) ? RL + (16 + (k >> 1)) * S + col + (k & 1) * 8
-						                            : RC + (8 + ((k - 8) >> 1)) * S + col + (k & 1) * 8;
-						uint2 v = *(const uint2 *)sp;
-						st_sc1(hbd + ((size_t)y * Wmb + mb) * HBD_BYTES + k * 8, ((unsigned long long)v.y << 32) | v.x);
+						const uint8_t *sp = (k < 8) ? RL + (32 + (k >> 1)) * S + col + (k & 1) * 8
+						                            : RC + (16 + ((k - 8) >> 1)) * S + col + (k & 1) * 8;
+						const uint2 v = *(const uint2 *)sp;
+						st_sc1(hbd + ((size_t)yB * Wmb + mb) * HBD_BYTES + k * 8, ((unsigned long long)v.y << 32) | v.x);
 					}
 				}
-				signal_progress(&progress[y], lim);
+				signal_progress(&progress[yB], tB);
 			}
-			/* final samples to the frame: luma rows 0..12 (all on the last row), the row above's rows 13..15 */
-			for (int k = t; k < n * 64; k += 64) {
-				int mb = done + (k >> 6), r = (k >> 2) & 15, c = (k & 3) * 4;
-				if (last_row || r <= 12)
-					*(uint32_t *)(cur + (size_t)(y0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + c);
-			}
-			if (y > 0)
-				for (int k = t; k < n * 16; k += 64) {
-					int mb = done + (k >> 4), r = (k >> 2) & 3, c = (k & 3) * 4;
-					const int col = (mb & (DBK_RING - 1)) * 16 + c;
-					if (r < 3) *(uint32_t *)(cur + (size_t)(y0 - 3 + r) * W + mb * 16 + c) = *(const uint32_t *)(RL + (1 + r) * S + col);
-					else *(uint32_t *)(chroma + (size_t)(yc0 - 1) * W + mb * 16 + c) = *(const uint32_t *)(RC + 1 * S + col);
+			/* row A: rows 0..12 (all 16 if A is the last row) and the row above's rows 13..15 */
+			if (tA > dA) {
+				const int n = tA - dA;
+				for (int k = t; k < n * 64; k += 64) {
+					const int mb = dA + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
+					if (lastA || r <= 12)
+						*(uint32_t *)(cur + (size_t)(y0A + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
 				}
-			for (int k = t; k < n * 32; k += 64) {
-				int mb = done + (k >> 5), r = (k >> 2) & 7, c = (k & 3) * 4;
-				if (last_row || r <= 6)
-					*(uint32_t *)(chroma + (size_t)(yc0 + r) * W + mb * 16 + c) = *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + c);
+				for (int k = t; k < n * 32; k += 64) {
+					const int mb = dA + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
+					if (lastA || r <= 6)
+						*(uint32_t *)(chroma + (size_t)(yc0A + r) * W + mb * 16 + cc) = *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+				}
+				if (yA > 0)
+					for (int k = t; k < n * 16; k += 64) {
+						const int mb = dA + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
+						const int col = (mb & (DBK_RING - 1)) * 16 + cc;
+						if (r < 3) *(uint32_t *)(cur + (size_t)(y0A - 3 + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (1 + r) * S + col);
+						else *(uint32_t *)(chroma + (size_t)(yc0A - 1) * W + mb * 16 + cc) = *(const uint32_t *)(RC + 1 * S + col);
+					}
+				dA = tA;
+			}
+			/* row A's rows 13..15 (chroma 7), final once row B filtered its top edge */
+			if (tA13 > dA13) {
+				const int n = tA13 - dA13;
+				for (int k = t; k < n * 16; k += 64) {
+					const int mb = dA13 + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
+					const int col = (mb & (DBK_RING - 1)) * 16 + cc;
+					if (r < 3) *(uint32_t *)(cur + (size_t)(y0A + 13 + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (17 + r) * S + col);
+					else *(uint32_t *)(chroma + (size_t)(yc0A + 7) * W + mb * 16 + cc) = *(const uint32_t *)(RC + 9 * S + col);
+				}
+				dA13 = tA13;
+			}
+			/* row B: rows 0..12 (all 16 if B is the last row) */
+			if (tB > dB) {
+				const int n = tB - dB;
+				for (int k = t; k < n * 64; k += 64) {
+					const int mb = dB + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
+					if (lastB || r <= 12)
+						*(uint32_t *)(cur + (size_t)(y0B + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (20 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+				}
+				for (int k = t; k < n * 32; k += 64) {
+					const int mb = dB + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
+					if (lastB || r <= 6)
+						*(uint32_t *)(chroma + (size_t)(yc0B + r) * W + mb * 16 + cc) = *(const uint32_t *)(RC + (10 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+				}
+				dB = tB;
 			}
 			/* the slots' LDS reads are done (their values fed the stores above): hand them back */
-			if (t == 0) __hip_atomic_store(&flags[2], lim, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-			STAMP(y, 2, nst, lim);
+			if (t == 0) __hip_atomic_store(&flags[2], hasB ? dB : dA, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			STAMP(yA, 2, nst, hasB ? dB : dA);
 			nst++;
-			done = lim;
 		}
-		/* every store of this row (its rows 0..12, the row above's 13..15) is in: publish for the MC of
-		 * later pictures (plain stores -> drain -> agent release -> sc1 flag, G16 valid form) */
+		/* every store of these rows is in: publish both rows for the MC of later pictures (plain
+		 * stores -> drain -> agent release -> sc1 flags, G16 valid form).  rowflag[y]: row y's rows
+		 * 0..12 and row y-1's rows 13..15 are final */
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		if (t == 0) {
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + y], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (hasB) __hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 }
@@ -1379,48 +1467,80 @@ __device__ void deblock_row(const int y, uint8_t *smem, const m2r_deblock_t *__r
 /* ======================================================================== k_picture */
 /*
  * One launch per picture, all three stages overlapped row by row.  Workgroups [0, G) are persistent
- * inter workers (work items = 8-MB segments in raster order); workgroup G + y owns MB row y:
- *   phase A: waits until every inter segment of its row is stored (per-row counter, agent release /
- *            acquire), publishes the unfiltered bottom rows of its inter MBs (hand-off records read
- *            by the intra MBs of the row below, which may only run once this row is deblocking),
- *            then reconstructs its intra / PCM MBs on wave 0 (2-MB-lag wavefront on the row above);
- *   phase B: deblocks the row on waves 0..2 (loader / filter / storer, as described at deblock_row)
- *            and finally flags the row final for the motion compensation of later pictures.
+ * inter workers (work items = 8-MB segments in raster order); workgroup G + g owns MB rows 2g, 2g+1:
+ *   phase A: waits until every inter segment of its rows is stored (per-row counters, agent release /
+ *            acquire), publishes the unfiltered bottom rows of their inter MBs (hand-off records read
+ *            by the intra MBs of the row below), then reconstructs the intra / PCM MBs, one row per
+ *            wave (2-MB-lag wavefront on the row above);
+ *   phase B: deblocks both rows on waves 0..2 (loader / filter / storer, see deblock_pair) and
+ *            finally flags the rows final for the motion compensation of later pictures.
  * Every wait points at a lower block index of the same launch or at an earlier launch, so FIFO
  * queues and in-order dispatch cannot deadlock; the host keeps at most NSTREAMS pictures in flight
  * so that they all fit on the device.
  */
-__global__ __launch_bounds__(256) void k_picture(PictureArgs a)
+/* batch launches: before writing its slot, wait until the earlier batch pictures that read the
+ * slot's previous content have finished their motion compensation, and the previous content's
+ * writer has finished all its rows (their counters live at lower block indices: no deadlock) */
+__device__ void war_wait(const PictureArgs &a)
 {
-	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-	if ((int)blockIdx.x < a.inter_workers) {
+	if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) { /* wave 0, scalar branch */
+		const int t = threadIdx.x;
+		const int rows_wg = (a.Hmb + 1) / 2 + (a.capture ? 1 : 0); /* capture: + the copy-out */
+		unsigned spins = 0;
+		for (;;) {
+			bool ok = true;
+			if (t < a.n_war) ok = __hip_atomic_load((gi32 *)&a.fin[2 * a.war[t]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.inter_workers;
+			else if (t == a.n_war && a.war_writer >= 0)
+				ok = __hip_atomic_load((gi32 *)&a.fin[2 * a.war_writer + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= rows_wg;
+			if (__all(ok)) break;
+			if (!spin_ok(spins, a.err, 128)) break;
+		}
+	}
+	__syncthreads();
+}
+
+/* block b of one picture (k_picture: b = blockIdx.x; k_batch: the picture's own block index) */
+__device__ __forceinline__ void picture_block(const PictureArgs &a, const int b, uint8_t *smem)
+{
+	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
+	if (b < a.inter_workers) {
 		if (a.n_inter)
 			inter_worker(a.mbs, a.inters, a.slices, a.pool, a.frames, a.fsz, a.W, a.H, a.Wmb, a.Hmb, a.slot, a.ss, a.rowflag,
 			             a.scratch + SCR_QUEUE(a.Hmb), a.scratch + SCR_INTER(a.Hmb), a.err);
+		if (a.fin) {
+			/* every reference read of this worker has returned (its values were consumed) */
+			__syncthreads();
+			if (threadIdx.x == 0) __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
 		return;
 	}
 	const int t = threadIdx.x;
-	const int y = blockIdx.x - a.inter_workers;
+	const int yA = 2 * (b - a.inter_workers);
+	const bool hasB = yA + 1 < a.Hmb;
+	const int nrows = hasB ? 2 : 1;
 	const int Wmb = a.Wmb, nseg = (Wmb + 7) >> 3;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
 	uint8_t *chroma = cur + (size_t)a.W * a.H;
 	int *inter_cnt = a.scratch + SCR_INTER(a.Hmb);
 	int *hbi_ready = a.scratch + SCR_HBIRDY(a.Hmb);
-	STAMP(y, 3, 0, 1);
-	/* ---- phase A.1: this row's inter MBs are all stored (inter workers of this launch) */
+	STAMP(yA, 3, 0, 1);
+	/* ---- phase A.1: these rows' inter MBs are all stored (inter workers of this launch) */
 	if (a.n_inter) {
 		if (t == 0) {
 			unsigned spins = 0;
-			while (__hip_atomic_load((gi32 *)&inter_cnt[y], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nseg)
-				if (!spin_ok(spins, a.err, 64)) break;
+			for (int r = 0; r < nrows; ++r)
+				while (__hip_atomic_load((gi32 *)&inter_cnt[yA + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nseg)
+					if (!spin_ok(spins, a.err, 64)) break;
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		}
 		__syncthreads();
 	}
-	STAMP(y, 3, 1, 2);
-	/* ---- phase A.2: unfiltered bottom rows of the inter MBs -> hand-off records */
-	if (y + 1 < a.Hmb) {
+	STAMP(yA, 3, 1, 2);
+	/* ---- phase A.2: unfiltered bottom rows of the inter MBs -> hand-off records (intra neighbours) */
+	for (int r = 0; r < nrows; ++r) {
+		const int y = yA + r;
+		if (y + 1 >= a.Hmb) break;
 		for (int k = t; k < Wmb * 4; k += blockDim.x) {
 			const int x = k >> 2, g = k & 3;
 			if (a.mbs[y * Wmb + x].kind != M2R_MB_INTER) continue;
@@ -1428,32 +1548,73 @@ __global__ __launch_bounds__(256) void k_picture(PictureArgs a)
 			                             : chroma + (size_t)(y * 8 + 7) * a.W + x * 16 + (g & 1) * 8;
 			st_sc1(a.hbi + ((size_t)y * Wmb + x) * HBI_BYTES + g * 8, *(const unsigned long long *)src);
 		}
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		if (t == 0) __hip_atomic_store((gi32 *)&hbi_ready[y], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
-	STAMP(y, 3, 2, 3);
-	/* ---- phase A.3: intra / PCM MBs on wave 0 */
-	if (a.n_intra && t < 64) {
-		intra_row(y, t, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi, a.scratch + SCR_IPROG(a.Hmb), hbi_ready, a.err);
-		/* write the intra samples back out of this XCD's L2 now: rows 13..15 of this MB row are
-		 * rewritten (filtered) by the row below's deblock storer, possibly from another XCD, and a
-		 * later write-back of our dirty unfiltered bytes would land on top of them */
-		if (__builtin_amdgcn_readfirstlane(t) < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	STAMP(yA, 3, 2, 3);
+	/* ---- phase A.3: intra / PCM MBs, row A on wave 0 and row B on wave 1, each with its own LDS */
+	if (a.n_intra) {
+		const int w = __builtin_amdgcn_readfirstlane(t) >> 6;
+		if (w < nrows) {
+			intra_row(yA + w, t & 63, (IntraLDS *)smem + w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi, a.scratch + SCR_IPROG(a.Hmb),
+			          hbi_ready, a.err);
+			/* write the intra samples back out of this XCD's L2 now: rows 13..15 of an MB row are
+			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
+			 * write-back of our dirty unfiltered bytes would land on top of them */
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+		}
 	}
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__syncthreads();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-	STAMP(y, 3, 3, 4);
+	STAMP(yA, 3, 3, 4);
 	/* ---- phase B: deblocking (always: it also publishes the row flags) */
-	deblock_row(y, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq);
-	STAMP(y, 3, 4, 5);
+	deblock_pair(yA, hasB, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq);
+	STAMP(yA, 3, 4, 5);
+	if (a.fin) {
+		/* the storer drained and released every frame store before its row flags */
+		__shared__ int s_last;
+		__syncthreads();
+		if (t == 0) {
+			const int prev = __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+			s_last = a.capture && prev == (a.Hmb + 1) / 2 - 1;
+		}
+		__syncthreads();
+		if (s_last) {
+			/* verification mode: the last row workgroup copies the finished picture out, then
+			 * releases the slot to later writers (their war_wait counts this copy) */
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			const size_t n16 = (size_t)a.W * a.H * 3 / 2 / 16;
+			const uint4 *src = (const uint4 *)cur;
+			uint4 *dst = (uint4 *)a.capture;
+			for (size_t i = t; i < n16; i += blockDim.x) dst[i] = src[i];
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__syncthreads();
+			if (t == 0) __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_picture(PictureArgs a)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	picture_block(a, blockIdx.x, smem);
+}
+
+__global__ __launch_bounds__(256) void k_batch(const PictureArgs *pics, int bpp)
+{
+	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+	const int p = blockIdx.x / bpp;
+	picture_block(pics[p], blockIdx.x - p * bpp, smem);
 }
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)
 {
 	(void)W;
-	return (size_t)30 * DBK_RW + 2 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
+	const size_t dbk = (size_t)54 * DBK_RW + 3 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
+	const size_t intra = 2 * sizeof(IntraLDS);
+	return dbk > intra ? dbk : intra;
 }
 
 extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)

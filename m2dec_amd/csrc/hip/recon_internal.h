@@ -10,9 +10,11 @@
 
 #define HBI_BYTES 32 /* intra hand-off per MB: bottom luma row (16 B) + bottom chroma row (16 B) */
 #define HBD_BYTES 96 /* deblock hand-off per MB: luma rows 12..15 (4 x 16 B) + chroma rows 6..7 (2 x 16 B) */
-#define DBK_WAVES 3  /* k_deblock workgroup: loader, filter, storer waves */
+#define DBK_WAVES 4  /* deblocking workgroup: loader, filter A, storer, filter B waves */
 #define DBK_RING 16  /* deblocking: MB slots of the LDS ring (power of two) */
 #define DBK_RW (DBK_RING * 16) /* ring line width in bytes */
+
+#define WAR_MAX 16 /* readers of one slot's content a batch picture can wait for */
 
 /* seq + 1 of the picture currently held by each frame slot (0: none) */
 struct SlotSeq {
@@ -44,9 +46,21 @@ struct PictureArgs {
 	int *rowflag;     /* [64][Hmb] picture row flags (seq + 1 when final) */
 	int *err;
 	SlotSeq ss;
+	/* batch launches (k_batch) only: the slot's write-after-read / write-after-write on the device */
+	int *fin;         /* [2 * batch] zeroed per launch: [2p] inter workers done, [2p + 1] row workgroups done; null: single launch */
+	int pidx;         /* index of this picture in the batch */
+	int n_war;        /* earlier pictures of the batch that read the slot's previous content ... */
+	int war[WAR_MAX]; /* ... (their inter workers must be done) */
+	int war_writer;   /* the batch picture that wrote the previous content (its rows must be done), or -1 */
+	uint8_t *capture; /* verification only: the finished frame is copied here before the slot is released */
 };
 
-__global__ void k_picture(PictureArgs a); /* grid: inter_workers + Hmb, dynamic LDS m2r_deblock_lds_bytes */
+__global__ void k_picture(PictureArgs a); /* grid: picture_blocks(Hmb), dynamic LDS m2r_deblock_lds_bytes */
+/* a batch of pictures in decode order, picture p owning blocks [p * bpp, (p + 1) * bpp) */
+__global__ void k_batch(const PictureArgs *pics, int bpp);
+
+/* workgroups of one picture: persistent inter workers + one per pair of MB rows */
+static inline int picture_blocks(int inter_workers, int Hmb) { return inter_workers + (Hmb + 1) / 2; }
 
 /* dynamic LDS bytes of one k_deblock workgroup for a W-sample-wide picture */
 size_t m2r_deblock_lds_bytes(int W, int Wmb);

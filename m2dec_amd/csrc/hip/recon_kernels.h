@@ -111,6 +111,12 @@ __device__ __forceinline__ int d_chroma_off(const m2r_mb_t &m, int bit)
 	return off;
 }
 
+/* branch-free select: c ? a : b without letting the compiler sink a or b into a divergent branch */
+__device__ __forceinline__ int d_sel(bool c, int a, int b)
+{
+	return b ^ ((a ^ b) & -(int)c);
+}
+
 /* int16 words of the pool an MB owns (PCM: 384 sample bytes) */
 #define M2R_MB_COEF_MAX 416
 __device__ __forceinline__ int d_mb_ncoef(const m2r_mb_t &m)

@@ -105,6 +105,7 @@ struct Sched {
 			nslots = n;
 		}
 		if (prog && (width / 16 != Wmb || height / 16 != Hmb)) {
+			batch_free();
 			(void)hipFree(prog);
 			(void)hipFree(hand);
 			(void)hipFree(rowflag);
@@ -194,7 +195,7 @@ struct Sched {
 		a.err = err;
 		a.ss = slot_seq;
 		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb), s));
-		hipLaunchKernelGGL(k_picture, dim3(inter_grid + Hmb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, a);
+		hipLaunchKernelGGL(k_picture, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, a);
 		CHECK(hipGetLastError());
 		tm.inter_launches += j.n_inter ? 1 : 0;
 		tm.intra_launches += j.n_intra ? 1 : 0;
@@ -204,6 +205,116 @@ struct Sched {
 		CHECK(hipEventRecord(*inter_done, s));
 		if (tev) CHECK(hipEventRecord(tev[0], s));
 		return 0;
+	}
+
+	/* ---- batch launches (trace replay): one k_batch per run of pictures, slot reuse ordered on the
+	 * device (PictureArgs.war / war_writer), everything on stream 0 */
+	struct Batch {
+		int cap = 0;                 /* pictures */
+		int *words = nullptr;        /* [2 cap] completion counters, then [cap][SCR_WORDS] scratch */
+		uint8_t *hand = nullptr;     /* [cap][hand_bytes] */
+		static const int NB = 4;
+		PictureArgs *d_args[NB] = {}, *h_args[NB] = {};
+		hipEvent_t used[NB] = {};
+		int next = 0;
+	} bt;
+
+	int batch_reserve(int cap)
+	{
+		if (cap <= bt.cap) return 0;
+		batch_free();
+		CHECK(hipMalloc(&bt.words, sizeof(int) * ((size_t)2 * cap + (size_t)cap * SCR_WORDS(Hmb))));
+		CHECK(hipMalloc(&bt.hand, hand_bytes() * (size_t)cap));
+		for (int i = 0; i < Batch::NB; ++i) {
+			CHECK(hipMalloc(&bt.d_args[i], sizeof(PictureArgs) * cap));
+			CHECK(hipHostMalloc((void **)&bt.h_args[i], sizeof(PictureArgs) * cap, hipHostMallocDefault));
+			CHECK(hipEventCreateWithFlags(&bt.used[i], hipEventDisableTiming));
+		}
+		bt.cap = cap;
+		return 0;
+	}
+
+	void batch_free()
+	{
+		if (bt.words) (void)hipFree(bt.words);
+		if (bt.hand) (void)hipFree(bt.hand);
+		for (int i = 0; i < Batch::NB; ++i) {
+			if (bt.d_args[i]) (void)hipFree(bt.d_args[i]);
+			if (bt.h_args[i]) (void)hipHostFree(bt.h_args[i]);
+			if (bt.used[i]) (void)hipEventDestroy(bt.used[i]);
+			bt.d_args[i] = bt.h_args[i] = nullptr;
+			bt.used[i] = nullptr;
+		}
+		bt.words = nullptr;
+		bt.hand = nullptr;
+		bt.cap = 0;
+	}
+
+	/* launch up to n pictures as one k_batch on stream 0 (fewer if a slot's readers would exceed
+	 * WAR_MAX); capture: verification copy-out area [n][fsz] or null.  Returns the pictures taken. */
+	int launch_batch(const PicJob *jobs, int n, uint8_t *capture)
+	{
+		if (n > bt.cap) return -1;
+		hipStream_t s = st[0];
+		const int idx = bt.next;
+		bt.next = (bt.next + 1) % Batch::NB;
+		CHECK(hipEventSynchronize(bt.used[idx])); /* its host / device argument arrays are free again */
+		PictureArgs *ha = bt.h_args[idx];
+		int last_writer[64];
+		std::vector<int> rd[64];
+		for (int i = 0; i < 64; ++i) last_writer[i] = -1;
+		int taken = 0;
+		for (int p = 0; p < n; ++p) {
+			const PicJob &j = jobs[p];
+			if ((int)rd[j.slot].size() > WAR_MAX) break;
+			PictureArgs &a = ha[p];
+			memset(&a, 0, sizeof(a));
+			a.mbs = j.r.mb;
+			a.inters = j.r.it;
+			a.slices = j.r.sl;
+			a.pool = j.r.coef;
+			a.dbk = j.r.dbk;
+			a.frames = frames;
+			a.fsz = fsz;
+			a.W = W;
+			a.H = H;
+			a.Wmb = Wmb;
+			a.Hmb = Hmb;
+			a.slot = j.slot;
+			a.seq = seq++;
+			a.n_inter = j.n_inter;
+			a.n_intra = j.n_intra;
+			a.inter_workers = inter_grid;
+			a.scratch = bt.words + 2 * (size_t)bt.cap + (size_t)p * SCR_WORDS(Hmb);
+			a.hbi = bt.hand + (size_t)p * hand_bytes();
+			a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+			a.rowflag = rowflag;
+			a.err = err;
+			a.ss = slot_seq;
+			a.fin = bt.words;
+			a.pidx = p;
+			a.n_war = (int)rd[j.slot].size();
+			for (int i = 0; i < a.n_war; ++i) a.war[i] = rd[j.slot][i];
+			a.war_writer = last_writer[j.slot];
+			a.capture = capture ? capture + (size_t)p * fsz : nullptr;
+			rd[j.slot].clear();
+			last_writer[j.slot] = p;
+			for (int r = 0; r < 64; ++r)
+				if ((j.refs >> r) & 1) rd[r].push_back(p);
+			slot_seq.s[j.slot] = a.seq + 1;
+			tm.inter_launches += j.n_inter ? 1 : 0;
+			tm.intra_launches += j.n_intra ? 1 : 0;
+			tm.deblock_launches++;
+			taken++;
+		}
+		if (!taken) return -1;
+		CHECK(hipMemcpyAsync(bt.d_args[idx], ha, sizeof(PictureArgs) * taken, hipMemcpyHostToDevice, s));
+		CHECK(hipMemsetAsync(bt.words, 0, sizeof(int) * (2 * (size_t)bt.cap + (size_t)taken * SCR_WORDS(Hmb)), s));
+		const int bpp = picture_blocks(inter_grid, Hmb);
+		hipLaunchKernelGGL(k_batch, dim3(bpp * taken), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, (const PictureArgs *)bt.d_args[idx], bpp);
+		CHECK(hipGetLastError());
+		CHECK(hipEventRecord(bt.used[idx], s));
+		return taken;
 	}
 
 	/* after everything that touches the picture's slot on stream k was enqueued (incl. any copy) */
@@ -239,6 +350,9 @@ struct Sched {
 	void destroy()
 	{
 		(void)hipSetDevice(dev);
+		for (auto &s : st)
+			if (s) (void)hipStreamSynchronize(s);
+		batch_free();
 		for (auto &s : st)
 			if (s) (void)hipStreamSynchronize(s);
 		for (auto &e : ev)
@@ -311,7 +425,10 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 	(void)hipEventSynchronize(t.e[5]);
 	m2dec_amd_hip_timing_t &tm = b->sc.tm;
 	if (hipEventElapsedTime(&ms, t.e[0], t.e[1]) == hipSuccess) tm.h2d_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) tm.picture_us += ms * 1e3;
+	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) {
+		tm.picture_us += ms * 1e3;
+		tm.kernel_launches++;
+	}
 	if (hipEventElapsedTime(&ms, t.e[2], t.e[5]) == hipSuccess) tm.d2h_us += ms * 1e3;
 	t.pending = false;
 }
@@ -540,7 +657,8 @@ struct m2dec_amd_hip_replay {
 	uint8_t *d_rec = nullptr;
 	std::vector<m2dec_amd_trace_pic_t> pics;
 	std::vector<uint64_t> refs;
-	/* timing: 2 events per enqueued picture (before / after its k_inter + k_rows pair) */
+	std::vector<PicJob> jobs;
+	/* timing: 2 events per launch (before / after its k_batch) */
 	std::vector<hipEvent_t> tev;
 	size_t tev_used = 0;
 };
@@ -577,6 +695,25 @@ extern "C" int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int devic
 	}
 	RCHECK(hipMalloc(&r->d_rec, len));
 	RCHECK(hipMemcpy(r->d_rec, rec, len, hipMemcpyHostToDevice));
+	for (int i = 0; i < npics; ++i) {
+		const m2dec_amd_trace_pic_t &p = pics[i];
+		PicJob j;
+		j.r.mb = (const m2r_mb_t *)(r->d_rec + p.off_mb);
+		j.r.dbk = (const m2r_deblock_t *)(r->d_rec + p.off_dbk);
+		j.r.sl = (const m2r_slice_t *)(r->d_rec + p.off_slice);
+		j.r.it = (const m2r_inter_t *)(r->d_rec + p.off_inter);
+		j.r.coef = (const int16_t *)(r->d_rec + p.off_coef);
+		j.slot = p.slot;
+		j.n_inter = p.n_inter;
+		j.n_intra = p.n_intra;
+		j.deblock = p.deblock;
+		j.refs = r->refs[i];
+		r->jobs.push_back(j);
+	}
+	if (r->sc.batch_reserve(npics) < 0) {
+		replay_free(r);
+		return -1;
+	}
 #undef RCHECK
 	*out = r;
 	return 0;
@@ -620,6 +757,39 @@ static int replay_enqueue(m2dec_amd_hip_replay_t *r, int i, bool timed)
 	return 0;
 }
 
+/* pictures [i0, i1) of the trace as batch launches on stream 0 (timed: events around each) */
+static int replay_batches(m2dec_amd_hip_replay_t *r, int i0, int i1, bool timed, uint8_t *capture)
+{
+	Sched &sc = r->sc;
+	for (int i = i0; i < i1;) {
+		hipEvent_t *ev = nullptr;
+		if (timed) {
+			while (r->tev_used + 2 > r->tev.size()) {
+				hipEvent_t e;
+				CHECK(hipEventCreate(&e));
+				r->tev.push_back(e);
+			}
+			ev = &r->tev[r->tev_used];
+			r->tev_used += 2;
+			CHECK(hipEventRecord(ev[0], sc.st[0]));
+		}
+		const int n = sc.launch_batch(&r->jobs[i], i1 - i, capture ? capture + (size_t)(i - i0) * sc.fsz : nullptr);
+		if (n <= 0) return -1;
+		if (ev) {
+			CHECK(hipEventRecord(ev[1], sc.st[0]));
+			sc.tm.kernel_launches++;
+		}
+		for (int k = i; k < i + n; ++k) {
+			sc.tm.pictures++;
+			sc.tm.record_bytes += r->pics[k].record_bytes;
+			sc.tm.ref_bytes += r->pics[k].ref_bytes;
+			sc.tm.frame_bytes += r->pics[k].frame_bytes;
+		}
+		i += n;
+	}
+	return 0;
+}
+
 extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
 {
 	if (!r) return -1;
@@ -627,14 +797,15 @@ extern "C" int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes)
 	const char *lim_env = getenv("M2DEC_AMD_REPLAY_LIMIT"); /* debug: first N pictures only */
 	const int lim = lim_env && atoi(lim_env) > 0 ? std::min(atoi(lim_env), r->npics) : r->npics;
 	const bool isolate = getenv("M2DEC_AMD_REPLAY_ISOLATE_LAST") != nullptr; /* debug: last picture alone */
-	for (int k = 0; k < passes; ++k)
-		for (int i = 0; i < lim; ++i) {
-			if (isolate && i == lim - 1) {
-				if (r->sc.sync_all() < 0) return -1;
-				m2dec_amd_debug_stamps_clear();
-			}
-			if (replay_enqueue(r, i, true) < 0) return -1;
+	for (int k = 0; k < passes; ++k) {
+		if (isolate && lim > 1) {
+			if (replay_batches(r, 0, lim - 1, true, nullptr) < 0 || r->sc.sync_all() < 0) return -1;
+			m2dec_amd_debug_stamps_clear();
+			if (replay_batches(r, lim - 1, lim, true, nullptr) < 0) return -1;
+		} else if (replay_batches(r, 0, lim, true, nullptr) < 0) {
+			return -1;
 		}
+	}
 	return 0;
 }
 
@@ -661,6 +832,9 @@ extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_
 	return 0;
 }
 
+/* MD5 of every picture in decode order.  Default: ONE batch launch of the whole trace, exactly as
+ * replay_run runs it, each picture copied out by its last row workgroup before its slot is reused;
+ * M2DEC_AMD_DEBUG=1: one k_picture launch per picture, synchronised (the decode path's kernel). */
 extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 {
 	if (!r || !md5s) return -1;
@@ -668,11 +842,25 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	size_t ls = (size_t)sc.W * sc.H;
 	std::vector<uint8_t> host(ls * 3 / 2);
 	CHECK(hipSetDevice(sc.dev));
+	if (sc.sync_all() < 0) return -1; /* no earlier work of either launch path may still run */
 	const bool dbg = getenv("M2DEC_AMD_DEBUG") != nullptr;
+	uint8_t *cap = nullptr;
+	if (!dbg) {
+		CHECK(hipMalloc(&cap, sc.fsz * (size_t)r->npics));
+		if (replay_batches(r, 0, r->npics, false, cap) < 0 || m2dec_amd_hip_replay_sync(r) < 0) {
+			(void)hipFree(cap);
+			return -1;
+		}
+	}
 	for (int i = 0; i < r->npics; ++i) {
-		if (dbg) fprintf(stderr, "replay_md5: picture %d slot %d n_inter %d n_intra %d\n", i, r->pics[i].slot, r->pics[i].n_inter, r->pics[i].n_intra);
-		if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) return -1;
-		CHECK(hipMemcpy(host.data(), sc.frames + (size_t)r->pics[i].slot * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost));
+		if (dbg) {
+			fprintf(stderr, "replay_md5: picture %d slot %d n_inter %d n_intra %d\n", i, r->pics[i].slot, r->pics[i].n_inter, r->pics[i].n_intra);
+			if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) return -1;
+			CHECK(hipMemcpy(host.data(), sc.frames + (size_t)r->pics[i].slot * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost));
+		} else if (hipMemcpy(host.data(), cap + (size_t)i * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost) != hipSuccess) {
+			(void)hipFree(cap);
+			return -1;
+		}
 		m2d_frame_t f;
 		memset(&f, 0, sizeof(f));
 		f.luma = host.data();
@@ -682,6 +870,7 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 		for (int k = 0; k < 4; ++k) f.crop[k] = (int16_t)r->crop[k];
 		m2dec_amd_frame_md5(&f, md5s + 35 * (size_t)i);
 	}
+	if (cap) (void)hipFree(cap);
 	return 0;
 }
 

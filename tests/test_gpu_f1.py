@@ -17,3 +17,19 @@ def test_f1_hip_matches_reference(built):
     want = golden_md5s(os.path.join(GOLD, "f1_realshort.md5"))
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert len(got) == len(want) and not bad, f"mismatching frames {bad[:10]} of {len(want)}"
+
+
+@pytest.mark.gpu
+def test_f1_hip_batch_replay_matches_reference(built):
+    """F1 parsed once, then reconstructed by ONE k_batch launch (the bench path)."""
+    data = open(os.path.join(GOLD, "f1_realshort.264"), "rb").read()
+    tr = m2dec_amd.Trace(data)
+    rp = m2dec_amd.HipReplay(tr, 0)
+    try:
+        got = rp.md5_output_order()
+    finally:
+        rp.close()
+        tr.close()
+    want = golden_md5s(os.path.join(GOLD, "f1_realshort.md5"))
+    bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert len(got) == len(want) and not bad, f"mismatching frames {bad[:10]} of {len(want)}"

@@ -26,7 +26,7 @@ Hmb, Wmb = tr.height // 16, tr.width // 16
 t0 = t[t > 0].min()
 us = lambda x: round((x - t0) / 100.0, 1) if x > 0 else None
 print("row: start, A1 inter-done, A2, intra-done, deblock-done")
-for y in list(range(0, 6)) + list(range(Hmb // 2, Hmb // 2 + 3)) + list(range(Hmb - 3, Hmb)):
+for y in list(range(0, 12, 2)) + list(range(Hmb // 2 - 2, Hmb // 2 + 4, 2)) + list(range(Hmb - 6, Hmb, 2)):
     print(y, [us(t[y, 3, i]) for i in range(5)])
 ends = [t[y, 3, 4] for y in range(Hmb) if t[y, 3, 4] > 0]
 print("picture span us", us(max(ends)))
@@ -48,7 +48,7 @@ if items:
     print("first items (t, item, wait, work):", first[:8])
     print("last items:", first[-5:])
 print("deblock detail: rows 10, 11 - filter MB times (us), loader got-events, storer lim-events")
-for y in (10, 11):
+for y in (10, 12):
     f = t[y, 1, :Wmb + 1]
     print(y, "filter", [us(f[i]) for i in range(0, 24)])
     print(y, "loader", [(us(t[y, 0, i]), int(v[y, 0, i])) for i in range(0, 14) if t[y, 0, i] > 0])

@@ -23,6 +23,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include "recon_kernels.h"
+#include "intra_tables.h"
 #include "recon_internal.h"
 #include "m2dec_amd.h"
 
@@ -41,8 +42,12 @@ __device__ unsigned long long g_stamps[STAMP_ROWS][4][STAMP_EV];
 		if ((row) < STAMP_ROWS && (idx) < STAMP_EV && (threadIdx.x & 63) == 0)                                       \
 			g_stamps[row][role][idx] = (__builtin_amdgcn_s_memrealtime() << 16) | (unsigned long long)((val) & 0xffff); \
 	} while (0)
+/* per-picture events of a batch launch: [pidx][0 first block starts, 1 inter workers done, 2 rows done] */
+__device__ unsigned long long g_pstamps[256][4];
+#define STAMPP(p, k) do { if ((p) < 256) g_pstamps[p][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define STAMP(row, role, idx, val) do { } while (0)
+#define STAMPP(p, k) do { } while (0)
 #endif
 #if defined(M2DEC_STAMPS) && !defined(M2DEC_NO_STAMPI)
 #define STAMPI(row, role, idx, val) STAMP(row, role, idx, val)
@@ -486,71 +491,8 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 /* ======================================================================== intra prediction (per sample) */
 #define LW 25 /* intra luma context row: [0] = x0 - 1, [1..24] = x0 .. x0 + 23 */
 
-/* 4x4 (h264.cpp:2510-2997) on neighbours read straight from the LDS MB context: top row `top`
- * (top[-1] = top-left, top[0..7] = top / top-right, the latter replaced by top[3] when unavailable)
- * and the left column left[i * LW] (i = 0..3); returns -1 where the reference writes nothing.
- * (Per-lane register arrays indexed by x + y would be placed in scratch.) */
-__device__ int pred4_px(int mode, int avail, int x, int y, const uint8_t *top, const uint8_t *left)
-{
-	const bool tr = (avail & 4) != 0;
-#define P(i) ((int)(((i) < 4 || tr) ? top[(i)] : top[3]))
-#define L(i) ((int)left[(i) * LW])
-	const int tl = top[-1];
-#define PP(i) ((i) < 0 ? tl : P(i))
-#define LL(i) ((i) < 0 ? tl : L(i))
-	switch (mode) {
-	case 0: return (avail & 2) ? P(x) : -1;
-	case 1: return (avail & 1) ? L(y) : -1;
-	case 2:
-		if ((avail & 3) == 3) return (P(0) + P(1) + P(2) + P(3) + L(0) + L(1) + L(2) + L(3) + 4) >> 3;
-		if (avail & 1) return (L(0) + L(1) + L(2) + L(3) + 2) >> 2;
-		if (avail & 2) return (P(0) + P(1) + P(2) + P(3) + 2) >> 2;
-		return 128;
-	case 3:
-		if (x == 3 && y == 3) return (P(6) + 3 * P(7) + 2) >> 2;
-		return (P(x + y) + 2 * P(x + y + 1) + P(x + y + 2) + 2) >> 2;
-	case 4:
-		if ((avail & 3) != 3) return -1;
-		if (x > y) return (PP(x - y - 2) + 2 * PP(x - y - 1) + P(x - y) + 2) >> 2;
-		if (x < y) return (LL(y - x - 2) + 2 * LL(y - x - 1) + L(y - x) + 2) >> 2;
-		return (P(0) + 2 * tl + L(0) + 2) >> 2;
-	case 5: {
-		if ((avail & 3) != 3) return -1;
-		int z = 2 * x - y, i = x - (y >> 1);
-		if (z >= 0 && !(z & 1)) return (PP(i - 1) + P(i) + 1) >> 1;
-		if (z >= 0) return (PP(i - 2) + 2 * PP(i - 1) + P(i) + 2) >> 2;
-		if (z == -1) return (L(0) + 2 * tl + P(0) + 2) >> 2;
-		return (L(y - 1) + 2 * L(y - 2) + LL(y - 3) + 2) >> 2;
-	}
-	case 6: {
-		if ((avail & 3) != 3) return -1;
-		int z = 2 * y - x, i = y - (x >> 1);
-		if (z >= 0 && !(z & 1)) return (LL(i - 1) + L(i) + 1) >> 1;
-		if (z >= 0) return (LL(i - 2) + 2 * LL(i - 1) + L(i) + 2) >> 2;
-		if (z == -1) return (L(0) + 2 * tl + P(0) + 2) >> 2;
-		return (P(x - 1) + 2 * P(x - 2) + PP(x - 3) + 2) >> 2;
-	}
-	case 7: {
-		int i = x + (y >> 1);
-		if (!(y & 1)) return (P(i) + P(i + 1) + 1) >> 1;
-		return (P(i) + 2 * P(i + 1) + P(i + 2) + 2) >> 2;
-	}
-	default: {
-		if (!(avail & 1)) return -1;
-		int z = x + 2 * y, i = y + (x >> 1);
-		if (z > 5) return L(3);
-		if (z == 5) return (L(2) + 3 * L(3) + 2) >> 2;
-		if (!(z & 1)) return (L(i) + L(i + 1) + 1) >> 1;
-		return (L(i) + 2 * L(i + 1) + L(i + 2) + 2) >> 2;
-	}
-	}
-#undef PP
-#undef LL
-#undef P
-#undef L
-}
-
-/* 8x8 on filtered neighbours pt[0..15], lf[0..7], tlf (spec 8.3.2.2; h264.cpp:3301-3929) */
+/* 8x8 on filtered neighbours pt[0..15], lf[0..7], tlf (spec 8.3.2.2; h264.cpp:3301-3929); the
+ * directional modes go through intra_tables.h, this is used for DC */
 __device__ int pred8_px(int mode, int avail, int x, int y, const int *pt, const int *lf, int tlf)
 {
 #define PT(i) ((i) < 0 ? tlf : pt[i])
@@ -682,9 +624,28 @@ struct IntraLDS {
 	int16_t Q[2][M2R_MB_COEF_MAX]; /* the current / next intra MB's coefficients */
 };
 
-__device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool,
-                          uint8_t *cur, int W, int H, int Wmb, uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
+/* one part of the intra / PCM MBs of MB row y on one wave: luma (part 0) or chroma (part 1); the
+ * two parts of a row run on two waves side by side (chroma prediction only reads chroma
+ * neighbours).  progress: this part's per-row progress words; HBI granules 0,1 luma, 2,3 chroma. */
+/* the prediction tables of intra_tables.h, staged in LDS once per workgroup */
+struct IntraTables {
+	uint32_t p4[9][16];
+	uint32_t p8[9][64];
+};
+
+__device__ __forceinline__ int ipred_taps(uint32_t w, int bits, const int *nv)
 {
+	const int s = (int)((w >> (3 * bits + 6)) & 3);
+	const int v = (int)((w >> (3 * bits)) & 3) * nv[0] + (int)((w >> (3 * bits + 2)) & 3) * nv[1] +
+	              (int)((w >> (3 * bits + 4)) & 3) * nv[2];
+	return (v + ((1 << s) >> 1)) >> s;
+}
+
+__device__ void intra_row(const int y, const int t, const int part, IntraLDS *ctx, const IntraTables *tabs,
+                          const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
+                          uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
+{
+	const bool do_luma = part == 0, do_chroma = part != 0;
 	uint8_t(&L)[17][LW] = ctx->L;
 	uint8_t(&C)[2][9][9] = ctx->C;
 	int(&R)[256 + 128] = ctx->R;
@@ -751,11 +712,11 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 		}
 		/* ---- gather the neighbourhood */
 		if (left_in_lds) {
-			if (t < 17) L[t][0] = L[t][16];
-			if (t < 18) { int c = t / 9, r = t % 9; C[c][r][0] = C[c][r][8]; }
+			if (do_luma && t < 17) L[t][0] = L[t][16];
+			if (do_chroma && t < 18) { int c = t / 9, r = t % 9; C[c][r][0] = C[c][r][8]; }
 		}
 		WSYNC();
-		if (y > 0 && t < 7) {
+		if (y > 0 && t < 7 && (do_luma ? t < 4 : t >= 4)) {
 			/* granules of the row above: 0,1 luma MB x; 2 luma MB x+1 (bytes 0..7); 3 luma MB x-1 (bytes 8..15);
 			 * 4,5 chroma MB x; 6 chroma MB x-1 (bytes 8..15) */
 			const int xs = (t == 2) ? x + 1 : ((t == 3 || t == 6) ? x - 1 : x);
@@ -775,20 +736,22 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 			}
 		}
 		if (x > 0 && !left_in_lds) {
-			if (t < 16) L[1 + t][0] = cur[(size_t)(y0 + t) * W + x0 - 1];
-			if (t >= 16 && t < 32) { int k = t - 16; C[k & 1][1 + (k >> 1)][0] = chroma[(size_t)(y0 / 2 + (k >> 1)) * W + x0 - 2 + (k & 1)]; }
+			if (do_luma && t < 16) L[1 + t][0] = cur[(size_t)(y0 + t) * W + x0 - 1];
+			if (do_chroma && t >= 16 && t < 32) { int k = t - 16; C[k & 1][1 + (k >> 1)][0] = chroma[(size_t)(y0 / 2 + (k >> 1)) * W + x0 - 2 + (k & 1)]; }
 		}
 		WSYNC();
 		STAMPX(x, 0);
 
 		if (m.kind == M2R_MB_PCM) {
 			const uint8_t *s = (const uint8_t *)q;
-			for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
-			for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
+			if (do_luma)
+				for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
+			else
+				for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
 			WSYNC();
 		} else {
 			/* ---- chroma prediction (h264.cpp:4559-4706); thread t: sample (t & 7, t >> 3) of both components */
-			{
+			if (do_chroma) {
 				int ca = m.avail_chroma, mode = m.chroma_mode;
 				int px = t & 7, py = t >> 3;
 				for (int c = 0; c < 2; ++c) {
@@ -818,16 +781,19 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 				}
 			}
 			WSYNC();
-			for (int c = 0; c < 2; ++c) {
-				int v = R[256 + c * 64 + t];
-				if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
-			}
+			if (do_chroma)
+				for (int c = 0; c < 2; ++c) {
+					int v = R[256 + c * 64 + t];
+					if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
+				}
 			WSYNC();
 			STAMPX(x, 1);
 
 			/* ---- luma */
 			const int qp = m.qpy;
-			if (m.kind == M2R_MB_I4x4) {
+			if (!do_luma) {
+				/* chroma wave: no luma */
+			} else if (m.kind == M2R_MB_I4x4) {
 				/* residual of all 16 blocks first (independent of the prediction), then the serial
 				 * block chain: predict + add, one wave sync per block */
 				for (int k = t; k < 256; k += 64) {
@@ -851,14 +817,48 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 					p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
 				}
 				WSYNC();
+				/* the serial block chain, table-driven (intra_tables.h): per block one table word
+				 * (fetched a block ahead), three neighbour reads, one sync */
+				uint32_t wn = 0;
+				if (t < 16) {
+					const int mode0 = (int)(m.ipred[0] & 15);
+					wn = tabs->p4[mode0 == 2 ? 0 : mode0][t];
+				}
 				for (int blk = 0; blk < 16; ++blk) {
 					const int ox = c_blk_x[blk] * 4, oy = c_blk_y[blk] * 4;
 					const int av = avail4(blk, m.avail_luma);
+					const int mode = (int)((((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15);
+					const uint32_t w = wn;
+					if (t < 16 && blk < 15) {
+						const int nb = blk + 1;
+						const int mn = (int)((((nb >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (nb & 7))) & 15);
+						wn = tabs->p4[mn == 2 ? 0 : mn][t];
+					}
 					if (t < 16) {
-						const int mode = (((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15;
-						const int v = pred4_px(mode, av, t & 3, t >> 2, &L[oy][1 + ox], &L[oy + 1][ox]);
 						uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
-						const int base = (v >= 0) ? v : *d; /* the reference leaves the sample as it was */
+						int v;
+						bool ok;
+						if (mode == 2) {
+							/* DC: (avail & 3) picks the sum (pred4x4_dc family) */
+							const uint8_t *tp = &L[oy][1 + ox];
+							int st = tp[0] + tp[1] + tp[2] + tp[3];
+							int sl = L[oy + 1][ox] + L[oy + 2][ox] + L[oy + 3][ox] + L[oy + 4][ox];
+							v = ((av & 3) == 3) ? (st + sl + 4) >> 3 : ((av & 1) ? (sl + 2) >> 2 : ((av & 2) ? (st + 2) >> 2 : 128));
+							ok = true;
+						} else {
+							/* neighbour index -> LDS: 0 top-left, 1..8 top (top-right -> P3 if unavailable), 9..12 left */
+							int nv[3];
+#pragma unroll
+							for (int k = 0; k < 3; ++k) {
+								const int i = (int)((w >> (4 * k)) & 15);
+								const int pi = (i - 1 >= 4 && !(av & 4)) ? 3 : i - 1;
+								const uint8_t *a = (i == 0) ? &L[oy][ox] : (i <= 8) ? &L[oy][1 + ox + pi] : &L[oy + 1 + (i - 9)][ox];
+								nv[k] = *a;
+							}
+							v = ipred_taps(w, 4, nv);
+							ok = (av & c_req4[mode]) == c_req4[mode];
+						}
+						const int base = ok ? v : *d; /* the reference leaves the sample as it was */
 						*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
 					}
 					WSYNC();
@@ -933,7 +933,17 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 					WSYNC();
 					{
 						const int mode = (m.ipred[0] >> (4 * b)) & 15;
-						const int v = pred8_px(mode, av, t & 7, t >> 3, F, F + 16, F[24]);
+						int v;
+						if (mode == 2) {
+							v = pred8_px(2, av, t & 7, t >> 3, F, F + 16, F[24]);
+						} else {
+							/* table-driven (intra_tables.h) over the filtered neighbours F */
+							const uint32_t w = tabs->p8[mode][t];
+							int nv[3];
+#pragma unroll
+							for (int k = 0; k < 3; ++k) nv[k] = F[(w >> (5 * k)) & 31];
+							v = ((av & c_req8[mode]) == c_req8[mode]) ? ipred_taps(w, 5, nv) : -1;
+						}
 						uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
 						const int base = (v >= 0) ? v : *d;
 						const int dcl = DC[b];
@@ -1035,7 +1045,7 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 
 			STAMPX(x, 2);
 			/* ---- chroma residual (residual_chroma, h264.cpp:2374-2461) */
-			if (m.cbp >> 4) {
+			if (do_chroma && (m.cbp >> 4)) {
 				int ccbp = m.cbp >> 4;
 				for (int k = t; k < 128; k += 64) {
 					int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
@@ -1074,12 +1084,14 @@ __device__ void intra_row(const int y, const int t, IntraLDS *ctx, const m2r_mb_
 
 		STAMPX(x, 3);
 		/* ---- write back and hand off the bottom rows */
-		for (int k = t; k < 256; k += 64) cur[(size_t)(y0 + (k >> 4)) * W + x0 + (k & 15)] = L[1 + (k >> 4)][1 + (k & 15)];
-		for (int k = t; k < 128; k += 64) {
-			int cy = k >> 4, bx = k & 15;
-			chroma[(size_t)(y0 / 2 + cy) * W + x0 + bx] = C[bx & 1][1 + cy][1 + (bx >> 1)];
-		}
-		if (t < 4) {
+		if (do_luma)
+			for (int k = t; k < 256; k += 64) cur[(size_t)(y0 + (k >> 4)) * W + x0 + (k & 15)] = L[1 + (k >> 4)][1 + (k & 15)];
+		else
+			for (int k = t; k < 128; k += 64) {
+				int cy = k >> 4, bx = k & 15;
+				chroma[(size_t)(y0 / 2 + cy) * W + x0 + bx] = C[bx & 1][1 + cy][1 + (bx >> 1)];
+			}
+		if (t < 4 && (do_luma ? t < 2 : t >= 2)) {
 			unsigned long long v = 0;
 			for (int b = 0; b < 8; ++b) {
 				int j = (t & 1) * 8 + b;
@@ -1502,6 +1514,7 @@ __device__ void war_wait(const PictureArgs &a)
 /* block b of one picture (k_picture: b = blockIdx.x; k_batch: the picture's own block index) */
 __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b, uint8_t *smem)
 {
+	if (b == 0 && threadIdx.x == 0) STAMPP(a.pidx, 0);
 	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
 	if (b < a.inter_workers) {
 		if (a.n_inter)
@@ -1510,7 +1523,8 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 		if (a.fin) {
 			/* every reference read of this worker has returned (its values were consumed) */
 			__syncthreads();
-			if (threadIdx.x == 0) __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (threadIdx.x == 0 && __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.inter_workers - 1)
+				STAMPP(a.pidx, 1);
 		}
 		return;
 	}
@@ -1553,12 +1567,19 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	__syncthreads();
 	if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	STAMP(yA, 3, 2, 3);
-	/* ---- phase A.3: intra / PCM MBs, row A on wave 0 and row B on wave 1, each with its own LDS */
+	/* ---- phase A.3: intra / PCM MBs: luma of rows A / B on waves 0 / 1, their chroma on waves 2 / 3,
+	 * each wave with its own LDS context */
 	if (a.n_intra) {
+		IntraTables *tabs = (IntraTables *)((IntraLDS *)smem + 4);
+		for (int i = t; i < 9 * 16; i += blockDim.x) tabs->p4[i >> 4][i & 15] = c_ipred4[i >> 4][i & 15];
+		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
+		__syncthreads();
 		const int w = __builtin_amdgcn_readfirstlane(t) >> 6;
-		if (w < nrows) {
-			intra_row(yA + w, t & 63, (IntraLDS *)smem + w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi, a.scratch + SCR_IPROG(a.Hmb),
-			          hbi_ready, a.err);
+		const int r = w & 1, part = w >> 1;
+		if (r < nrows) {
+			__builtin_amdgcn_s_setprio(3); /* the intra wavefront is an I picture's critical path */
+			intra_row(yA + r, t & 63, part, (IntraLDS *)smem + w, tabs, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
+			          a.scratch + (part ? SCR_IPROGC(a.Hmb) : SCR_IPROG(a.Hmb)), hbi_ready, a.err);
 			/* write the intra samples back out of this XCD's L2 now: rows 13..15 of an MB row are
 			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
 			 * write-back of our dirty unfiltered bytes would land on top of them */
@@ -1579,6 +1600,7 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 		if (t == 0) {
 			const int prev = __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 			s_last = a.capture && prev == (a.Hmb + 1) / 2 - 1;
+			if (prev == (a.Hmb + 1) / 2 - 1) STAMPP(a.pidx, 2);
 		}
 		__syncthreads();
 		if (s_last) {
@@ -1613,7 +1635,7 @@ size_t m2r_deblock_lds_bytes(int W, int Wmb)
 {
 	(void)W;
 	const size_t dbk = (size_t)54 * DBK_RW + 3 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
-	const size_t intra = 2 * sizeof(IntraLDS);
+	const size_t intra = 4 * sizeof(IntraLDS) + sizeof(IntraTables);
 	return dbk > intra ? dbk : intra;
 }
 
@@ -1624,6 +1646,19 @@ extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)
 	if (n * sizeof(unsigned long long) < bytes) return -1;
 	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost));
 	return (int)(bytes / sizeof(unsigned long long));
+#else
+	(void)out;
+	(void)n;
+	return -1;
+#endif
+}
+
+extern "C" int m2dec_amd_debug_pstamps(unsigned long long *out, size_t n)
+{
+#ifdef M2DEC_STAMPS
+	if (n < 256 * 4) return -1;
+	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 256 * 4, 0, hipMemcpyDeviceToHost));
+	return 256 * 4;
 #else
 	(void)out;
 	(void)n;

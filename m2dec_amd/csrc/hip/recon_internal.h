@@ -21,14 +21,15 @@ struct SlotSeq {
 	int s[64];
 };
 
-/* per-launch scratch words (zeroed before every launch): intra progress, deblock progress, inter
- * segment counters, hand-off-ready flags ([Hmb] each), then the work-queue head */
+/* per-launch scratch words (zeroed before every launch): intra luma / chroma progress, deblock
+ * progress, inter segment counters, hand-off-ready flags ([Hmb] each), then the work-queue head */
 #define SCR_IPROG(Hmb) 0
-#define SCR_DPROG(Hmb) (Hmb)
-#define SCR_INTER(Hmb) (2 * (Hmb))
-#define SCR_HBIRDY(Hmb) (3 * (Hmb))
-#define SCR_QUEUE(Hmb) (4 * (Hmb))
-#define SCR_WORDS(Hmb) ((4 * (Hmb) + 4 + 3) & ~3)
+#define SCR_IPROGC(Hmb) (Hmb)
+#define SCR_DPROG(Hmb) (2 * (Hmb))
+#define SCR_INTER(Hmb) (3 * (Hmb))
+#define SCR_HBIRDY(Hmb) (4 * (Hmb))
+#define SCR_QUEUE(Hmb) (5 * (Hmb))
+#define SCR_WORDS(Hmb) ((5 * (Hmb) + 4 + 3) & ~3)
 
 struct PictureArgs {
 	const m2r_mb_t *mbs;

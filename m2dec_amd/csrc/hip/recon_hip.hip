@@ -280,7 +280,7 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 				if (lv) atomicAdd(&s_cnt[lb8], 1);
 			}
 		} else {
-			int blk = c_rast2blk[lb];
+			int blk = d_rast2blk(lb);
 			if (m.nz & (1u << blk)) r = pool[m.coef + d_luma_off(m, blk) + (ly & 3) * 4 + (lx & 3)] * d_scale4(m.qpy, lx & 3, ly & 3);
 		}
 		s_res[t] = r;
@@ -825,7 +825,7 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 					wn = tabs->p4[mode0 == 2 ? 0 : mode0][t];
 				}
 				for (int blk = 0; blk < 16; ++blk) {
-					const int ox = c_blk_x[blk] * 4, oy = c_blk_y[blk] * 4;
+					const int ox = d_blk_x(blk) * 4, oy = d_blk_y(blk) * 4;
 					const int av = avail4(blk, m.avail_luma);
 					const int mode = (int)((((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15);
 					const uint32_t w = wn;
@@ -1003,7 +1003,7 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 					/* AC blocks with coefficients: full transform with the DC inserted; others DC-only SWAR */
 					for (int k = t; k < 256; k += 64) {
 						int blk = k >> 4, pos = k & 15;
-						int bx = c_blk_x[blk], by = c_blk_y[blk];
+						int bx = d_blk_x(blk), by = d_blk_y(blk);
 						int v = 0;
 						if (pos == 0) v = DC[by * 4 + bx];
 						else if (m.nz & (1u << blk)) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
@@ -1028,7 +1028,7 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 					WSYNC();
 					for (int k = t; k < 256; k += 64) {
 						int blk = k >> 4, pos = k & 15;
-						int bx = c_blk_x[blk], by = c_blk_y[blk];
+						int bx = d_blk_x(blk), by = d_blk_y(blk);
 						uint8_t *d = &L[1 + by * 4 + (pos >> 2)][1 + bx * 4 + (pos & 3)];
 						if (m.nz & (1u << blk)) *d = (uint8_t)d_clip255(*d + R[k]);
 						else *d = (uint8_t)d_swar(*d, DC[by * 4 + bx], pos & 3, 4);
@@ -1618,13 +1618,13 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	}
 }
 
-__global__ __launch_bounds__(256) void k_picture(PictureArgs a)
+__global__ __launch_bounds__(256, 3) void k_picture(PictureArgs a)
 {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	picture_block(a, blockIdx.x, smem);
 }
 
-__global__ __launch_bounds__(256) void k_batch(const PictureArgs *pics, int bpp)
+__global__ __launch_bounds__(256, 3) void k_batch(const PictureArgs *pics, int bpp)
 {
 	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int p = blockIdx.x / bpp;

@@ -12,12 +12,15 @@ __device__ __forceinline__ int d_clip255(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int d_clip3(int lo, int hi, int v) { return min(max(v, lo), hi); }
 __device__ __forceinline__ int d_sat16(int v) { return min(max(v, -32768), 32767); }
 
-__constant__ static const uint8_t c_norm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
-__constant__ static const uint8_t c_norm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
-                                                   {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
-__constant__ static const uint8_t c_blk_x[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
-__constant__ static const uint8_t c_blk_y[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
-__constant__ static const uint8_t c_rast2blk[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};
+/* 4x4 block index (decoding order, spec 6.4.3) <-> position in the MB, as bit arithmetic (a per-lane
+ * index into a __constant__ table compiles to a vector memory load) */
+__device__ __forceinline__ int d_blk_x(int blk) { return (blk & 1) | ((blk >> 1) & 2); }
+__device__ __forceinline__ int d_blk_y(int blk) { return ((blk >> 1) & 1) | ((blk >> 2) & 2); }
+__device__ __forceinline__ int d_rast2blk(int lb) /* raster 4x4 position (ry * 4 + rx) -> block index */
+{
+	const int rx = lb & 3, ry = lb >> 2;
+	return (rx & 1) | ((ry & 1) << 1) | ((rx & 2) << 1) | ((ry & 2) << 2);
+}
 __constant__ static const uint8_t c_alpha[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 5, 6, 7, 8, 9, 10, 12, 13, 15, 17, 20, 22, 25, 28,
                                                  32, 36, 40, 45, 50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
 __constant__ static const uint8_t c_beta[52] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 6, 6, 7, 7, 8, 8,
@@ -31,23 +34,30 @@ __constant__ static const uint8_t c_tc0[52][3] = {
 	{11, 15, 23}, {13, 17, 25}};
 
 /* ---------------------------------------------------------------- dequantisation (h264.cpp:964-1054) */
+/* dequantisation scale LevelScale(qp % 6, x, y) << (qp / 6) (spec 8.5.9).  The norm columns are
+ * packed into immediates (6 x 5 / 6 bits, one per position class) so that a per-lane class never
+ * turns into a per-lane constant-memory load (norm4 / norm8 of the spec, columns = classes). */
 __device__ __forceinline__ int d_scale4(int qp, int x, int y)
 {
-	int cls = (((x | y) & 1) == 0) ? 0 : (((x & y) & 1) ? 1 : 2);
-	return (int)c_norm4[qp % 6][cls] << (qp / 6);
+	const uint32_t w0 = 0x2507356au, w1 = 0x3b9bd250u, w2 = 0x2f4941cdu;
+	const uint32_t w = (((x | y) & 1) == 0) ? w0 : (((x & y) & 1) ? w1 : w2);
+	return (int)((w >> (5 * (qp % 6))) & 31) << (qp / 6);
 }
 
 __device__ __forceinline__ int d_scale8(int qp, int x, int y)
 {
-	int cls;
-	if ((x & 3) == 0 && (y & 3) == 0) cls = 0;
-	else if ((x & 1) && (y & 1)) cls = 1;
-	else if ((x & 3) == 2 && (y & 3) == 2) cls = 2;
-	else if (((x & 3) == 0 && (y & 1)) || ((x & 1) && (y & 3) == 0)) cls = 3;
-	else if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) cls = 4;
-	else cls = 5;
-	int v = c_norm8[qp % 6][cls];
-	int sh = qp / 6 - 2;
+	const uint64_t w0 = 0x000000092071a594ull, w1 = 0x000000081c6574d2ull, w2 = 0x0000000eb3b6a8e0ull;
+	const uint64_t w3 = 0x000000089e698553ull, w4 = 0x0000000ba88e1719ull, w5 = 0x0000000ae685f698ull;
+	const int x3 = x & 3, y3 = y & 3;
+	uint64_t w;
+	if (x3 == 0 && y3 == 0) w = w0;
+	else if ((x & 1) && (y & 1)) w = w1;
+	else if (x3 == 2 && y3 == 2) w = w2;
+	else if ((x3 == 0 && (y & 1)) || ((x & 1) && y3 == 0)) w = w3;
+	else if ((x3 == 0 && y3 == 2) || (x3 == 2 && y3 == 0)) w = w4;
+	else w = w5;
+	const int v = (int)((w >> (6 * (qp % 6))) & 63);
+	const int sh = qp / 6 - 2;
 	return sh >= 0 ? v << sh : v >> (-sh);
 }
 

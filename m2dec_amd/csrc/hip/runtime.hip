@@ -86,6 +86,8 @@ struct Sched {
 		int cus = 0;
 		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
 			inter_grid = cus / 4;
+		if (const char *g = getenv("M2DEC_AMD_INTER_WG")) /* tuning knob: inter workers per picture */
+			if (atoi(g) > 0) inter_grid = atoi(g);
 		return 0;
 	}
 

@@ -31,3 +31,14 @@ def gather_counters(dist, world: int, frames: int, seconds: float, device: str) 
     dist.all_gather(outs, c)
     per = [(int(o[0].item()), float(o[1].item())) for o in outs]
     return sum(p[0] for p in per), max(p[1] for p in per), per
+
+
+def all_ranks(dist, world: int, ok: bool, device: str) -> bool:
+    """True iff `ok` holds on every rank (all-reduce MIN of one int); used for the per-rank parity gate."""
+    import torch
+
+    if dist is None or world == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())

@@ -30,7 +30,9 @@ def _worker(rank, world, port, q):
     tr = m2dec_amd.Trace(open(out, "rb").read())
     os.unlink(out)
     total, mx, per = md.gather_counters(dist, world, tr.npics, 0.5 + rank, "cpu")
-    q.put((rank, seeds, tr.npics, total, mx, per))
+    both = md.all_ranks(dist, world, True, "cpu")
+    one = md.all_ranks(dist, world, rank == 0, "cpu")
+    q.put((rank, seeds, tr.npics, total, mx, per, both, one))
     dist.destroy_process_group()
 
 
@@ -45,7 +47,8 @@ def test_job_table_and_counters_world2(built):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, seeds, npics, total, mx, per in res:
+    for rank, seeds, npics, total, mx, per, both, one in res:
+        assert both and not one
         assert seeds == [5, 6]
         assert npics == 6
         assert total == 12

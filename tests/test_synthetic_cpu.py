@@ -8,9 +8,12 @@ from tests._oracle import OracleBackend
 from tests._streams import GOLDEN, stream
 
 COV = [n for n in GOLDEN if n.startswith("cov_")]
+# the C4 set (c3 preset, seeds 2..8) is the same generator path as c3_1080p_s1; its goldens are checked
+# on the GPU (tests/test_gpu_streams.py) and by every bench rank, not re-decoded by the CPU oracle here
+CPU_SET = sorted(n for n in GOLDEN if not n.startswith("c4_"))
 
 
-@pytest.mark.parametrize("name", sorted(GOLDEN))
+@pytest.mark.parametrize("name", CPU_SET)
 def test_oracle_matches_golden(built, name):
     data = stream(name)
     with OracleBackend() as ob:

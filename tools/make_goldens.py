@@ -25,7 +25,8 @@ STREAMS = [
     ("cov_slices_s1", "cov_slices", 1, 12),
     ("c2_720p_s1", "c2", 1, 60),
     ("c3_1080p_s1", "c3", 1, 60),
-]
+    ("c5_4k_s1", "c5", 1, 16),
+] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)]  # C4: one c3 stream per GPU, seed 1 + rank
 
 
 def gen(preset, seed, frames, out):
@@ -35,17 +36,21 @@ def gen(preset, seed, frames, out):
 
 
 def main():
-    res = {}
+    """Only streams missing from the committed file are decoded, unless --all is given."""
+    path = os.path.join(ROOT, "tests", "golden", "synthetic.json")
+    res = {} if "--all" in sys.argv or not os.path.exists(path) else json.load(open(path))
     tmp = "/tmp/m2dec_goldens"
     os.makedirs(tmp, exist_ok=True)
     for name, preset, seed, frames in STREAMS:
+        if name in res:
+            continue
         data = gen(preset, seed, frames, os.path.join(tmp, name + ".264"))
         with OracleBackend() as ob:
             md5s = m2dec_amd.decode_stream(data, backend=ob.be)
         res[name] = {"preset": preset, "seed": seed, "frames": frames, "bytes": len(data),
                      "sha256": hashlib.sha256(data).hexdigest(), "md5": md5s}
         print(name, len(data), len(md5s))
-    with open(os.path.join(ROOT, "tests", "golden", "synthetic.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(res, f, indent=1)
 
 

@@ -1,0 +1,58 @@
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh) into per-launch HBM traffic of k_batch.
+
+Counters and corrections (MI355X_MICROARCH.md §HBM):
+  FETCH_SIZE, WRITE_SIZE are in KiB and count the L2's memory-side (fabric) requests, Infinity-Cache
+  hits included.  On gfx950 FETCH_SIZE reports half of the bytes of wide coalesced reads, so the
+  corrected read bytes are 2 x FETCH_SIZE x 1024; WRITE_SIZE is taken as is.
+The first k_batch dispatch of each bench run is the parity-gate pass (it also copies every frame
+out), so it is dropped; the remaining dispatches are the timed-path launches.
+Prints one JSON object: per-launch read/write bytes (median over launches), L2 hit rate.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def per_dispatch(d):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if not row["Kernel_Name"].startswith("k_batch"):
+                continue
+            key = int(row["Dispatch_Id"])
+            vals.setdefault(key, {})
+            name = row["Counter_Name"]
+            vals[key][name] = vals[key].get(name, 0.0) + float(row["Counter_Value"])
+    keys = sorted(vals)[1:]  # drop the parity-gate launch
+    return [vals[k] for k in keys]
+
+
+def main():
+    root = sys.argv[1]
+    out = {"kernel": "k_batch", "source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh)"}
+    fetch = per_dispatch(os.path.join(root, "FETCH_SIZE"))
+    write = per_dispatch(os.path.join(root, "WRITE_SIZE"))
+    hit = per_dispatch(os.path.join(root, "TCC_HIT_sum_TCC_MISS_sum"))
+    if fetch:
+        f = statistics.median(v["FETCH_SIZE"] for v in fetch)
+        out["fetch_size_kib"] = f
+        out["read_bytes"] = int(2 * f * 1024)
+        out["launches_read"] = len(fetch)
+    if write:
+        w = statistics.median(v["WRITE_SIZE"] for v in write)
+        out["write_size_kib"] = w
+        out["write_bytes"] = int(w * 1024)
+    if "read_bytes" in out and "write_bytes" in out:
+        out["traffic_bytes"] = out["read_bytes"] + out["write_bytes"]
+    if hit:
+        h = statistics.median(v["TCC_HIT_sum"] for v in hit)
+        m = statistics.median(v["TCC_MISS_sum"] for v in hit)
+        out["l2_hit_rate"] = round(h / max(1.0, h + m), 4)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -34,6 +34,24 @@ static inline int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? 
 static inline int sat16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
 static inline int iabs(int v) { return v < 0 ? -v : v; }
 
+/* CLIP255C (m2d_macro.h:100) is a lookup in m2d_cliptable (m2d.cpp:157-289), defined on [-256, 767]
+ * only; outside it the reference reads adjacent rodata.  The oracle clips
+ * like the table does inside the domain and counts every out-of-domain argument, so a stream whose
+ * output would depend on that UB is detected (oracle_domain_violations) instead of silently pinned. */
+static unsigned long g_domain_violations;
+static inline int clip255c(int v)
+{
+	if (v < -256 || v > 767) g_domain_violations++;
+	return clip255(v);
+}
+
+unsigned long oracle_domain_violations(int reset)
+{
+	unsigned long v = g_domain_violations;
+	if (reset) g_domain_violations = 0;
+	return v;
+}
+
 /* ======================================================================== dequantisation */
 static const int norm4[6][3] = {{10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
 static const int norm8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
@@ -388,7 +406,7 @@ static void pred16x16(uint8_t *dst, int stride, int mode, int avail)
 		b = (5 * H + 32) >> 6;
 		c = (5 * V + 32) >> 6;
 		for (int y = 0; y < 16; ++y)
-			for (int x = 0; x < 16; ++x) dst[y * stride + x] = (uint8_t)clip255((a + b * (x - 7) + c * (y - 7) + 16) >> 5);
+			for (int x = 0; x < 16; ++x) dst[y * stride + x] = (uint8_t)clip255c((a + b * (x - 7) + c * (y - 7) + 16) >> 5); /* h264.cpp:4297 */
 		break;
 	}
 	}
@@ -441,7 +459,7 @@ static void predchroma(uint8_t *dst, int stride, int mode, int avail)
 		b = (34 * H + 32) >> 6;
 		c = (34 * V + 32) >> 6;
 		for (int y = 0; y < 8; ++y)
-			for (int x = 0; x < 8; ++x) dst[y * stride + x * 2] = (uint8_t)clip255((a + b * (x - 3) + c * (y - 3) + 16) >> 5);
+			for (int x = 0; x < 8; ++x) dst[y * stride + x * 2] = (uint8_t)clip255c((a + b * (x - 3) + c * (y - 3) + 16) >> 5); /* h264.cpp:4693 */
 		break;
 	}
 	}
@@ -484,7 +502,7 @@ static void luma8x8_residual(uint8_t *dst, int stride, const int16_t *lv, int qp
 	}
 	idct8(c, r);
 	for (int y = 0; y < 8; ++y)
-		for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)clip255(dst[y * stride + x] + r[y * 8 + x]);
+		for (int x = 0; x < 8; ++x) dst[y * stride + x] = (uint8_t)clip255c(dst[y * stride + x] + r[y * 8 + x]); /* :4033 */
 }
 
 /* per-block avail constants of luma_intra4x4_with_residual (h264.cpp:3121-3230) */
@@ -580,7 +598,7 @@ static void chroma_residual(uint8_t *cbase, int stride, const m2r_mb_t *m, const
 				int adj = (dc[b] + 32) >> 6;
 				if (adj)
 					for (int y = 0; y < 4; ++y)
-						for (int x = 0; x < 4; ++x) dst[y * stride + x * 2] = (uint8_t)clip255(dst[y * stride + x * 2] + adj);
+						for (int x = 0; x < 4; ++x) dst[y * stride + x * 2] = (uint8_t)clip255c(dst[y * stride + x * 2] + adj); /* :2121 */
 			}
 		}
 	}

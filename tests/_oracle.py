@@ -17,7 +17,14 @@ def oracle_lib():
         _orc = ctypes.CDLL(ORACLE_PATH)
         _orc.oracle_backend_create.argtypes = [ctypes.POINTER(Backend)]
         _orc.oracle_backend_create.restype = ctypes.c_int
+        _orc.oracle_domain_violations.argtypes = [ctypes.c_int]
+        _orc.oracle_domain_violations.restype = ctypes.c_ulong
     return _orc
+
+
+def domain_violations(reset=True):
+    """CLIP255C arguments outside the reference table's domain since the last reset (Appendix A #2)."""
+    return int(oracle_lib().oracle_domain_violations(1 if reset else 0))
 
 
 class OracleBackend:

@@ -4,11 +4,16 @@
  * Written from ITU-T H.264 (05/2003+) clauses 7.3 (syntax), 8.4.1.3 (motion vector prediction),
  * 8.3.1.1 / 8.3.2.1 (intra mode prediction) and 9.2 / 9.3 (CAVLC / CABAC binarisations and context
  * selection).  See gen.h for the approach and SURVEY.md Appendix A for the constraints kept here:
- *   - no plane prediction unless params.planar (CLIP255C domain, A#2);
+ *   - no plane prediction unless params.planar (CLIP255C domain, A#2: streams with planar are kept
+ *     only where the oracle reports no out-of-domain CLIP255C argument);
  *   - per-block residual bounded so that prediction + residual stays in [-256, 767] and DC-only
  *     adds stay within +-255 (A#2, A#17);
- *   - no scaling matrices (A#4), no deblocking idc 2 (A#6), beta offset >= alpha offset (A#7);
- *   - no constrained intra prediction (A#8); only legal intra modes (A#9);
+ *   - scaling lists only in the SPS, in the reference's 6 + 8 list layout, and only with
+ *     params.scaling (the reference parses and ignores them; PPS lists desynchronise it, A#4); deblocking idc 2 only with params.idc2 (A#6);
+ *     beta offset >= alpha offset (A#7);
+ *   - constrained intra prediction only with params.cip: modes are chosen from the spec's masked
+ *     availability (every inter neighbour, top-left included, is unavailable), so the streams are
+ *     conforming; the decoder reproduces the reference's own masks (A#8); only legal intra modes (A#9);
  *   - moderate explicit weights (A#1, A#16); CABAC only for 8x8 transforms;
  *   - in transform-8x8 mode B_8x8 uses only 8x8 sub-partitions.
  */
@@ -488,10 +493,19 @@ static int nc_chroma(gctx_t *g, int c, int x, int y)
 }
 
 /* ------------------------------------------------------------------ intra mode choice */
+/* neighbour available for intra prediction: with constrained_intra_pred an inter neighbour is not
+ * (8.3.1.2 / 8.3.1.1 dcPredModePredictedFlag) */
+static gmb_t *ipnb(gctx_t *g, int x, int y, int *bx, int *by)
+{
+	gmb_t *n = nbmb(g, x, y, bx, by);
+	if (n && g->p->cip && !n->intra) return NULL;
+	return n;
+}
+
 static int pred_ipm(gctx_t *g, int x, int y)
 {
 	int ax, ay, bx, by, ma, mb;
-	gmb_t *a = nbmb(g, x - 1, y, &ax, &ay), *b = nbmb(g, x, y - 1, &bx, &by);
+	gmb_t *a = ipnb(g, x - 1, y, &ax, &ay), *b = ipnb(g, x, y - 1, &bx, &by);
 	if (!a || !b) return 2;
 	ma = a->inxn ? a->ipm[ay * 4 + ax] : 2;
 	mb = b->inxn ? b->ipm[by * 4 + bx] : 2;
@@ -591,8 +605,10 @@ static void choose_intra(gctx_t *g, mbsyn_t *s, gmb_t *m)
 {
 	int r = (int)(rnd() % 100u);
 	int bx, by;
-	int L = nbmb(g, -1, 0, &bx, &by) != NULL, T = nbmb(g, 0, -1, &bx, &by) != NULL;
+	int L, T;
 	m->intra = 1;
+	L = ipnb(g, -1, 0, &bx, &by) != NULL;
+	T = ipnb(g, 0, -1, &bx, &by) != NULL;
 	for (int lx = 0; lx < 2; ++lx)
 		for (int k = 0; k < 4; ++k) m->ref[lx][k] = -1;
 	if ((int)(rnd() % 1000u) < g->p->pcm_permille) {
@@ -614,8 +630,8 @@ static void choose_intra(gctx_t *g, mbsyn_t *s, gmb_t *m)
 		if (t8) {
 			for (int b8 = 0; b8 < 4; ++b8) {
 				int x = (b8 & 1) * 2, y = (b8 >> 1) * 2;
-				int l = nbmb(g, x - 1, y, &bx, &by) != NULL, t = nbmb(g, x, y - 1, &bx, &by) != NULL;
-				int tl = nbmb(g, x - 1, y - 1, &bx, &by) != NULL;
+				int l = ipnb(g, x - 1, y, &bx, &by) != NULL, t = ipnb(g, x, y - 1, &bx, &by) != NULL;
+				int tl = ipnb(g, x - 1, y - 1, &bx, &by) != NULL;
 				int pred = pred_ipm(g, x, y), mode = pick_mode9(l, t, tl);
 				s->ipm_flag[b8] = (mode == pred);
 				s->ipm_rem[b8] = mode < pred ? mode : mode - 1;
@@ -624,8 +640,8 @@ static void choose_intra(gctx_t *g, mbsyn_t *s, gmb_t *m)
 		} else {
 			for (int b = 0; b < 16; ++b) {
 				int x = blk_x[b], y = blk_y[b];
-				int l = nbmb(g, x - 1, y, &bx, &by) != NULL, t = nbmb(g, x, y - 1, &bx, &by) != NULL;
-				int tl = nbmb(g, x - 1, y - 1, &bx, &by) != NULL;
+				int l = ipnb(g, x - 1, y, &bx, &by) != NULL, t = ipnb(g, x, y - 1, &bx, &by) != NULL;
+				int tl = ipnb(g, x - 1, y - 1, &bx, &by) != NULL;
 				int pred = pred_ipm(g, x, y), mode = pick_mode9(l, t, tl);
 				s->ipm_flag[b] = (mode == pred);
 				s->ipm_rem[b] = mode < pred ? mode : mode - 1;
@@ -635,7 +651,7 @@ static void choose_intra(gctx_t *g, mbsyn_t *s, gmb_t *m)
 		m->cbp = (uint8_t)((pct(g->p->coef_pct + 20) ? rr(1, 15) : 0) | (rr(0, 2) << 4));
 	} else {
 		int modes[4], n = 0, lc;
-		int TL = nbmb(g, -1, -1, &bx, &by) != NULL;
+		int TL = ipnb(g, -1, -1, &bx, &by) != NULL;
 		s->kind = K_I16;
 		m->i16 = 1;
 		modes[n++] = 2;
@@ -649,7 +665,7 @@ static void choose_intra(gctx_t *g, mbsyn_t *s, gmb_t *m)
 	}
 	{
 		int modes[4], n = 0;
-		int TL = nbmb(g, -1, -1, &bx, &by) != NULL;
+		int TL = ipnb(g, -1, -1, &bx, &by) != NULL;
 		modes[n++] = 0;
 		if (L) modes[n++] = 1;
 		if (T) modes[n++] = 2;
@@ -1192,6 +1208,47 @@ static void write_mb_cavlc(gctx_t *g, mbsyn_t *s, gmb_t *m)
 }
 
 /* ------------------------------------------------------------------ headers */
+/* SPS scaling lists (7.3.2.1.1.1) in the layout the reference reads: 6 4x4 lists, then 8 (not 2)
+ * 8x8 lists for chroma_format_idc 1 (h264.cpp:280-296) — a spec layout would desynchronise it.
+ * Each list is present with p = 1/2 and is either the "use default" escape (first delta makes
+ * nextScale 0) or a random walk of delta_scale values, sometimes ended early by a nextScale of 0.
+ * The reference discards the lists (flat dequant), so the output equals the same stream without. */
+static uint32_t sl_rnd(uint64_t *x)
+{
+	/* own generator: the lists do not perturb the main RNG, so a stream with lists and the same
+	 * stream without them carry identical slice data (tests compare their outputs) */
+	*x ^= *x >> 12;
+	*x ^= *x << 25;
+	*x ^= *x >> 27;
+	return (uint32_t)((*x * 2685821657736338717ull) >> 32);
+}
+
+static void write_scaling_lists(bw_t *r, uint64_t seed)
+{
+	uint64_t st = seed * 0x9e3779b97f4a7c15ull + 1;
+#define rnd() sl_rnd(&st)
+	for (int i = 0; i < 6 + 8; ++i) {
+		int size = i < 6 ? 16 : 64, last = 8, next = 8;
+		int present = (rnd() & 1) != 0;
+		bw_bit(r, present);
+		if (!present) continue;
+		if (rnd() % 4u == 0) {
+			bw_se(r, -8); /* nextScale = 0 at j = 0: useDefaultScalingMatrixFlag */
+			continue;
+		}
+		for (int j = 0; j < size && next; ++j) {
+			int target = (j > 4 && rnd() % 16u == 0) ? 0 : 4 + (int)(rnd() % 60u);
+			int d = target - last;
+			if (d > 127) d -= 256;
+			if (d < -128) d += 256;
+			bw_se(r, d);
+			next = (last + d + 256) % 256;
+			last = next ? next : last;
+		}
+	}
+#undef rnd
+}
+
 static void write_sps(const params_t *p, bw_t *out, int log2_fn, int log2_poc)
 {
 	bw_t r;
@@ -1205,7 +1262,8 @@ static void write_sps(const params_t *p, bw_t *out, int log2_fn, int log2_poc)
 		bw_ue(&r, 0);
 		bw_ue(&r, 0);
 		bw_bit(&r, 0);
-		bw_bit(&r, 0); /* no scaling matrices */
+		bw_bit(&r, p->scaling != 0); /* seq_scaling_matrix_present_flag */
+		if (p->scaling) write_scaling_lists(&r, p->seed);
 	}
 	bw_ue(&r, (uint32_t)(log2_fn - 4));
 	bw_ue(&r, 0); /* poc type 0 */
@@ -1246,7 +1304,7 @@ static void write_pps(const params_t *p, bw_t *out, int cqp_off)
 	bw_se(&r, 0);
 	bw_se(&r, cqp_off);
 	bw_bit(&r, 1); /* deblocking_filter_control_present */
-	bw_bit(&r, 0); /* constrained_intra_pred */
+	bw_bit(&r, p->cip); /* constrained_intra_pred */
 	bw_bit(&r, 0);
 	if (p->profile >= 100) {
 		bw_bit(&r, p->t8x8);
@@ -1432,7 +1490,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			g->direct_spatial = (p->direct == 2) ? pct(50) : p->direct;
 			if (p->deblock) {
 				int r2 = (int)(rnd() % 100u);
-				didc = (r2 < 10) ? 1 : 0;
+				didc = (r2 < 10) ? 1 : ((p->idc2 && r2 < 40) ? 2 : 0);
 				aoff = rr(-3, 3);
 				boff = rr(aoff, 3);
 			}

@@ -37,6 +37,9 @@ typedef struct {
 	int sub8x8_pct;         /* share of 8x8 inter MBs */
 	int coef_pct;           /* probability that a cbp bit is set */
 	int planar;             /* allow plane prediction (off: Appendix A #2) */
+	int cip;                /* constrained_intra_pred_flag (reference quirk A#8 reproduced by the decoder) */
+	int idc2;               /* allow disable_deblocking_filter_idc 2 (reference quirk A#6) */
+	int scaling;            /* SPS seq_scaling_matrix_present_flag with random lists (parsed, ignored: A#4) */
 	uint64_t seed;
 } params_t;
 

@@ -1,6 +1,7 @@
 /* h264gen command line: deterministic synthetic H.264 streams for tests and bench.py.
  *
- *   h264gen --preset c2|c3|c5|cov_cabac|cov_cavlc|cov_wp|cov_slices [--seed N] [--frames N]
+ *   h264gen --preset c2|c3|c5|cov_cabac|cov_cavlc|cov_wp|cov_slices|cov_tools|cov_tools_cavlc
+ *           [--seed N] [--frames N]
  *           [--size WxH] [--set key=value ...] -o out.264
  *
  * Presets follow SURVEY.md §8(d): c2 = Baseline 720p CAVLC IPPP, c3 = 1080p CABAC IBBP 8x8,
@@ -54,6 +55,20 @@ static void preset(params_t *p, const char *name)
 		p->gop = 0;
 		return;
 	}
+	if (!strcmp(name, "cov_tools")) {
+		/* the reference paths no other preset reaches: plane prediction (luma 16x16 and chroma),
+		 * constrained intra prediction, deblocking idc 2 across 3 slices, SPS scaling lists */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 16; p->slices = 3; p->gop = 8;
+		p->planar = 1; p->cip = 1; p->idc2 = 1; p->scaling = 1; p->p_intra_pct = 25; p->i4_pct = 30;
+		p->i8_pct = 30; p->pcm_permille = 5;
+		return;
+	}
+	if (!strcmp(name, "cov_tools_cavlc")) {
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 16; p->slices = 3; p->gop = 8;
+		p->cabac = 0; p->t8x8 = 0; p->profile = 77; p->level = 30; p->i8_pct = 0; p->i4_pct = 50;
+		p->planar = 1; p->cip = 1; p->idc2 = 1; p->p_intra_pct = 25; p->pcm_permille = 5;
+		return;
+	}
 	if (!strcmp(name, "cov_slices")) {
 		p->width = 384; p->height = 256; p->crop_bottom = 0; p->frames = 12; p->slices = 5; p->gop = 6;
 		return;
@@ -75,7 +90,7 @@ static void set_kv(params_t *p, const char *kv)
 	F(width) F(height) F(crop_bottom) F(frames) F(cabac) F(bframes) F(t8x8) F(gop) F(idr_period) F(slices)
 	F(profile) F(level) F(wp_p) F(wp_b) F(direct) F(qp_min) F(qp_max) F(deblock) F(pcm_permille) F(mv_px)
 	F(num_ref_frames) F(l0_active) F(l1_active) F(p_skip_pct) F(p_intra_pct) F(i4_pct) F(i8_pct)
-	F(sub8x8_pct) F(coef_pct) F(planar)
+	F(sub8x8_pct) F(coef_pct) F(planar) F(cip) F(idc2) F(scaling)
 #undef F
 	fprintf(stderr, "h264gen: unknown key %s\n", key);
 	exit(2);

@@ -26,6 +26,11 @@ STREAMS = [
     ("c2_720p_s1", "c2", 1, 60),
     ("c3_1080p_s1", "c3", 1, 60),
     ("c5_4k_s1", "c5", 1, 16),
+    # plane prediction, constrained intra (incl. the A#8 no-residual quirk), deblocking idc 2,
+    # SPS scaling lists in the reference's layout
+    ("cov_tools_s1", "cov_tools", 1, 16),
+    ("cov_tools_s2", "cov_tools", 2, 16),
+    ("cov_tools_cavlc_s1", "cov_tools_cavlc", 1, 16),
 ] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)]  # C4: one c3 stream per GPU, seed 1 + rank
 
 

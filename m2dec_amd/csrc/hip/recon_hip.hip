@@ -165,6 +165,11 @@ __device__ __forceinline__ void st_sc1(void *p, unsigned long long v)
 	__hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void st32_sc1(void *p, uint32_t v)
+{
+	__hip_atomic_store((gi32 *)p, (int)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ unsigned long long ld_sc1(const void *p)
 {
 	return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -369,19 +374,20 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 /*
  * Inter MBs as a bounded persistent grid.  Work items are (MB row, 8-MB segment) in raster order,
  * dequeued from a per-launch counter.  Before its MBs, an item waits until every reference picture
- * it reads has finished deblocking all the MB rows its motion vectors reach (rowflag[picture][row]
- * = seq + 1, written by k_deblock after the row's last store and an agent release; polled with sc1
- * loads, then ONE agent acquire): a picture's MC starts while its references are still being
- * deblocked further down, so consecutive anchor pictures overlap row by row.  The grid is kept
+ * it reads has its final samples in all the MB rows and columns its motion vectors reach
+ * (rowflag[picture][row] = ROWFLAG(seq, columns final), raised by the deblocking storer as it
+ * writes; the columns are rounded up to whole 128-byte lines, so no partially final line is ever
+ * cached; polled with sc1 loads, then ONE agent acquire): a picture's MC follows its references'
+ * deblocking wavefront column by column, so consecutive anchor pictures overlap.  The grid is kept
  * small (a fraction of the CUs) so that the spinning items can never keep the k_deblock they wait
  * for off the device.
  */
 __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters,
                              const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                             size_t fsz, int W, int H, int Wmb, int Hmb, int slot, const SlotSeq &ss, const int *rowflag,
-                             int *queue, int *inter_cnt, int *err)
+                             size_t fsz, int W, int H, int Wmb, int Hmb, int slot, const SlotSeq &ss,
+                             const unsigned long long *rowflag, int *queue, int *inter_cnt, int *err)
 {
-	__shared__ int s_item, s_rmin, s_rmax;
+	__shared__ int s_item, s_rmin, s_rmax, s_cmax;
 	__shared__ unsigned int s_refs[2];
 	const int t = threadIdx.x;
 	/* Single-lane work in this loop is done by the whole of wave 0 under a SCALAR branch, the one
@@ -397,6 +403,7 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 			s_item = __builtin_amdgcn_readfirstlane(v);
 			s_rmin = 1 << 30;
 			s_rmax = -1;
+			s_cmax = 0;
 			s_refs[0] = s_refs[1] = 0;
 		}
 		__syncthreads();
@@ -404,10 +411,11 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 		if (item >= nitems) break;
 		const int y = item / nseg, x0 = (item % nseg) * 8, x1 = min(x0 + 8, Wmb);
 		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
-	/* ---- vertical reach of this segment's motion into each reference (8 lanes per MB) */
+	/* ---- vertical and rightward reach of this segment's motion into the references (8 lanes per MB;
+	 * luma 6-tap window; the chroma window never reaches further) */
 		if (t < 64) {
 			const int mbi = x0 + (t >> 3);
-			int rmin = 1 << 30, rmax = -1;
+			int rmin = 1 << 30, rmax = -1, cmax = 0;
 			unsigned int r0 = 0, r1 = 0;
 			if (mbi < x1) {
 				const m2r_mb_t m = mbs[y * Wmb + mbi];
@@ -421,6 +429,8 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 						const int top = py - 2, bot = py + 3 + 3;
 						rmin = min(rmin, top < 0 ? 0 : min(top >> 4, Hmb - 1));
 						rmax = max(rmax, bot < 0 ? 0 : min(bot >> 4, Hmb - 1));
+						const int right = mbi * 16 + (blk & 3) * 4 + (it.mv[l][blk][0] >> 2) + 3 + 3;
+						cmax = max(cmax, right < 0 ? 0 : min(right >> 4, Wmb - 1));
 						if (sl < 32) r0 |= 1u << sl;
 						else r1 |= 1u << (sl - 32);
 					}
@@ -429,6 +439,7 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 			if (rmax >= 0) {
 				atomicMin(&s_rmin, rmin);
 				atomicMax(&s_rmax, rmax);
+				atomicMax(&s_cmax, cmax);
 				atomicOr(&s_refs[0], r0);
 				atomicOr(&s_refs[1], r1);
 			}
@@ -437,8 +448,12 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 #ifndef M2DEC_NO_REFWAIT
 		const int rmin_u = __builtin_amdgcn_readfirstlane(s_rmin), rmax_u = __builtin_amdgcn_readfirstlane(s_rmax);
 		if (rmax_u >= 0 && wave0) {
-			/* rows rmin .. rmax final: their own stores and the next row's (rows 13..15) done */
+			/* rows rmin .. rmax final up to the reach: their own stores and the next row's (rows 13..15)
+			 * done.  Columns are whole 128-byte lines (8 MBs) when the stride allows, else whole rows:
+			 * a line cached while partly unfinal could outlive the acquire below */
 			const int rlast = min(rmax_u + 1, Hmb - 1);
+			const int cmax_u = __builtin_amdgcn_readfirstlane(s_cmax);
+			const int need = (W & 127) ? Wmb : min(Wmb, (cmax_u + 8) & ~7);
 			for (int k = 0; k < 2; ++k) {
 				unsigned int bits = __builtin_amdgcn_readfirstlane(s_refs[k]);
 				while (bits) {
@@ -447,13 +462,14 @@ __device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t
 					const int want = ss.s[sl];
 					if (want <= 0) continue;
 					/* entry (seq & 63) only ever grows: a later picture's value also means "final" */
-					const int *fl = rowflag + (size_t)((want - 1) & 63) * Hmb;
+					const unsigned long long *fl = rowflag + (size_t)((want - 1) & 63) * Hmb;
+					const unsigned long long wv = ROWFLAG(want - 1, need);
 					unsigned spins = 0;
 					for (int r0 = rmin_u; r0 <= rlast; r0 += 64) {
 						const int r = r0 + t;
 						for (;;) {
 							const bool ok = (r > rlast) ||
-							                __hip_atomic_load((gi32 *)&fl[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+							                __hip_atomic_load((gu64 *)&fl[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wv;
 							if (__all(ok)) break;
 							if (!spin_ok(spins, err, 32)) break;
 						}
@@ -1143,7 +1159,8 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 __device__ __forceinline__ int dbk_done012(int c, int Wmb) { return c >= Wmb ? Wmb : max(c - 1, 0); }
 
 __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur,
-                             int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err, int *rowflag, int seq)
+                             int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err,
+                             unsigned long long *rowflag, int seq)
 {
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
 	const int nthr = blockDim.x;
@@ -1376,7 +1393,7 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 
 	/* ---------------- storer (wave 2) */
 	{
-		int dA = 0, dA13 = 0, dB = 0, nst = 0;
+		int dA = 0, dA13 = 0, dB = 0, nst = 0, pubA = 0, pubB = 0;
 		unsigned spins = 0;
 		const int y0A = yA * 16, yc0A = yA * 8, y0B = yB * 16, yc0B = yB * 8;
 		for (;;) {
@@ -1415,19 +1432,19 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 				for (int k = t; k < n * 64; k += 64) {
 					const int mb = dA + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
 					if (lastA || r <= 12)
-						*(uint32_t *)(cur + (size_t)(y0A + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+						st32_sc1(cur + (size_t)(y0A + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
 				}
 				for (int k = t; k < n * 32; k += 64) {
 					const int mb = dA + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
 					if (lastA || r <= 6)
-						*(uint32_t *)(chroma + (size_t)(yc0A + r) * W + mb * 16 + cc) = *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+						st32_sc1(chroma + (size_t)(yc0A + r) * W + mb * 16 + cc, *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
 				}
 				if (yA > 0)
 					for (int k = t; k < n * 16; k += 64) {
 						const int mb = dA + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
 						const int col = (mb & (DBK_RING - 1)) * 16 + cc;
-						if (r < 3) *(uint32_t *)(cur + (size_t)(y0A - 3 + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (1 + r) * S + col);
-						else *(uint32_t *)(chroma + (size_t)(yc0A - 1) * W + mb * 16 + cc) = *(const uint32_t *)(RC + 1 * S + col);
+						if (r < 3) st32_sc1(cur + (size_t)(y0A - 3 + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (1 + r) * S + col));
+						else st32_sc1(chroma + (size_t)(yc0A - 1) * W + mb * 16 + cc, *(const uint32_t *)(RC + 1 * S + col));
 					}
 				dA = tA;
 			}
@@ -1437,8 +1454,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 				for (int k = t; k < n * 16; k += 64) {
 					const int mb = dA13 + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
 					const int col = (mb & (DBK_RING - 1)) * 16 + cc;
-					if (r < 3) *(uint32_t *)(cur + (size_t)(y0A + 13 + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (17 + r) * S + col);
-					else *(uint32_t *)(chroma + (size_t)(yc0A + 7) * W + mb * 16 + cc) = *(const uint32_t *)(RC + 9 * S + col);
+					if (r < 3) st32_sc1(cur + (size_t)(y0A + 13 + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (17 + r) * S + col));
+					else st32_sc1(chroma + (size_t)(yc0A + 7) * W + mb * 16 + cc, *(const uint32_t *)(RC + 9 * S + col));
 				}
 				dA13 = tA13;
 			}
@@ -1448,29 +1465,48 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 				for (int k = t; k < n * 64; k += 64) {
 					const int mb = dB + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
 					if (lastB || r <= 12)
-						*(uint32_t *)(cur + (size_t)(y0B + r) * W + mb * 16 + cc) = *(const uint32_t *)(RL + (20 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+						st32_sc1(cur + (size_t)(y0B + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (20 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
 				}
 				for (int k = t; k < n * 32; k += 64) {
 					const int mb = dB + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
 					if (lastB || r <= 6)
-						*(uint32_t *)(chroma + (size_t)(yc0B + r) * W + mb * 16 + cc) = *(const uint32_t *)(RC + (10 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc);
+						st32_sc1(chroma + (size_t)(yc0B + r) * W + mb * 16 + cc, *(const uint32_t *)(RC + (10 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
 				}
 				dB = tB;
 			}
 			/* the slots' LDS reads are done (their values fed the stores above): hand them back */
 			if (t == 0) __hip_atomic_store(&flags[2], hasB ? dB : dA, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			/* column progress for the MC of later pictures, whole 8-MB (128-byte) groups at a time: the
+			 * frame stores above are write-through (sc1); drain them, then raise the rows' words.
+			 * rowflag[yA]: A's rows 0..12 and the row above's rows 13..15 (both up to dA);
+			 * rowflag[yB]: B's rows 0..12 (dB) and A's rows 13..15 (dA13) */
+			{
+				const int cA = dA >= Wmb ? Wmb : (dA & ~7);
+				const int mB = min(dB, dA13);
+				const int cB = hasB ? (mB >= Wmb ? Wmb : (mB & ~7)) : 0;
+				if (cA > pubA || cB > pubB) {
+					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+					if (t == 0) {
+						if (cA > pubA)
+							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], ROWFLAG(seq, cA), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						if (cB > pubB)
+							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], ROWFLAG(seq, cB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					}
+					pubA = max(pubA, cA);
+					pubB = max(pubB, cB);
+				}
+			}
 			STAMP(yA, 2, nst, hasB ? dB : dA);
 			nst++;
 		}
-		/* every store of these rows is in: publish both rows for the MC of later pictures (plain
-		 * stores -> drain -> agent release -> sc1 flags, G16 valid form).  rowflag[y]: row y's rows
-		 * 0..12 and row y-1's rows 13..15 are final */
+		/* every store of these rows is in: both rows complete (a stalled launch that broke out of the
+		 * loop above still releases its waiters; the error word reports it) */
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		if (t == 0) {
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if (hasB) __hip_atomic_store((gi32 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (hasB) __hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 }
@@ -1514,7 +1550,7 @@ __device__ void war_wait(const PictureArgs &a)
 /* block b of one picture (k_picture: b = blockIdx.x; k_batch: the picture's own block index) */
 __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b, uint8_t *smem)
 {
-	if (b == 0 && threadIdx.x == 0) STAMPP(a.pidx, 0);
+	if (b == 0 && threadIdx.x == 0) STAMPP(a.didx, 0);
 	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
 	if (b < a.inter_workers) {
 		if (a.n_inter)
@@ -1524,7 +1560,7 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 			/* every reference read of this worker has returned (its values were consumed) */
 			__syncthreads();
 			if (threadIdx.x == 0 && __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.inter_workers - 1)
-				STAMPP(a.pidx, 1);
+				STAMPP(a.didx, 1);
 		}
 		return;
 	}
@@ -1600,7 +1636,7 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 		if (t == 0) {
 			const int prev = __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
 			s_last = a.capture && prev == (a.Hmb + 1) / 2 - 1;
-			if (prev == (a.Hmb + 1) / 2 - 1) STAMPP(a.pidx, 2);
+			if (prev == (a.Hmb + 1) / 2 - 1) STAMPP(a.didx, 2);
 		}
 		__syncthreads();
 		if (s_last) {

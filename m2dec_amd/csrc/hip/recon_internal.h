@@ -14,6 +14,10 @@
 #define DBK_RING 16  /* deblocking: MB slots of the LDS ring (power of two) */
 #define DBK_RW (DBK_RING * 16) /* ring line width in bytes */
 
+/* row progress word: picture seq's MB row has its first `cols` MB columns final (all 16 luma / 8 chroma
+ * sample rows).  An entry (seq & 63) only ever grows, also across pictures. */
+#define ROWFLAG(seq, cols) ((((unsigned long long)(seq) + 1) << 16) | (unsigned long long)(cols))
+
 #define WAR_MAX 16 /* readers of one slot's content a batch picture can wait for */
 
 /* seq + 1 of the picture currently held by each frame slot (0: none) */
@@ -44,12 +48,14 @@ struct PictureArgs {
 	int inter_workers;
 	int *scratch;     /* SCR_* words of this launch */
 	uint8_t *hbi, *hbd; /* hand-off records of this launch's stream */
-	int *rowflag;     /* [64][Hmb] picture row flags (seq + 1 when final) */
+	unsigned long long *rowflag; /* [64][Hmb] column progress of picture rows: ROWFLAG(seq, c) once MB
+	                               columns 0 .. c-1 of the row are final (entry seq & 63) */
 	int *err;
 	SlotSeq ss;
 	/* batch launches (k_batch) only: the slot's write-after-read / write-after-write on the device */
 	int *fin;         /* [2 * batch] zeroed per launch: [2p] inter workers done, [2p + 1] row workgroups done; null: single launch */
-	int pidx;         /* index of this picture in the batch */
+	int pidx;         /* dispatch position of this picture in the batch */
+	int didx;         /* decode-order index in the batch (diagnostics) */
 	int n_war;        /* earlier pictures of the batch that read the slot's previous content ... */
 	int war[WAR_MAX]; /* ... (their inter workers must be done) */
 	int war_writer;   /* the batch picture that wrote the previous content (its rows must be done), or -1 */

@@ -61,7 +61,7 @@ struct Sched {
 	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb)] per-launch scratch words */
 	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
 	int *err = nullptr;
-	int *rowflag = nullptr;    /* [64][Hmb]: seq + 1 once an MB row of picture seq is final */
+	unsigned long long *rowflag = nullptr; /* [64][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
 	int seq = 0;               /* pictures launched */
 	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
 	int inter_grid = 64;       /* persistent inter workers per picture (a quarter of the CUs) */
@@ -123,9 +123,9 @@ struct Sched {
 		if (!prog) {
 			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb) * NSTREAMS));
 			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
-			CHECK(hipMalloc(&rowflag, sizeof(int) * 64 * (size_t)Hmb));
+			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * 64 * (size_t)Hmb));
 		}
-		CHECK(hipMemset(rowflag, 0, sizeof(int) * 64 * (size_t)Hmb));
+		CHECK(hipMemset(rowflag, 0, sizeof(unsigned long long) * 64 * (size_t)Hmb));
 		seq = 0;
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		for (int i = 0; i < 64; ++i) {
@@ -252,6 +252,40 @@ struct Sched {
 		bt.cap = 0;
 	}
 
+	/* Dispatch order inside a batch.  Workgroups are dispatched in block order, so a picture starts
+	 * only once every earlier picture's blocks are resident.  An intra-only picture reads no
+	 * reference: it only has to follow the pictures that read its slot's previous content and that
+	 * content's writer.  Move each one up to right after those (its seq, and so every reference
+	 * relation, stays in decode order), so that an I picture — the longest wavefront of a GOP —
+	 * overlaps the previous GOP's tail instead of starting after it.  Every wait still points at a
+	 * lower dispatch position: no deadlock.  a[] is in decode order on entry, dispatch order on exit. */
+	void hoist_intra(PictureArgs *a, int n)
+	{
+		if (getenv("M2DEC_AMD_NO_HOIST")) return;
+		std::vector<int> order(n), pos(n);
+		for (int i = 0; i < n; ++i) order[i] = i;
+		for (int p = 0; p < n; ++p) {
+			if (a[p].n_inter) continue;
+			for (int i = 0; i < n; ++i) pos[order[i]] = i;
+			int e = 0;
+			for (int i = 0; i < a[p].n_war; ++i) e = std::max(e, pos[a[p].war[i]] + 1);
+			if (a[p].war_writer >= 0) e = std::max(e, pos[a[p].war_writer] + 1);
+			const int cur = pos[p];
+			if (e >= cur) continue;
+			order.erase(order.begin() + cur);
+			order.insert(order.begin() + e, p);
+		}
+		for (int i = 0; i < n; ++i) pos[order[i]] = i;
+		std::vector<PictureArgs> b(a, a + n);
+		for (int i = 0; i < n; ++i) {
+			PictureArgs &d = a[i];
+			d = b[order[i]];
+			d.pidx = i;
+			for (int k = 0; k < d.n_war; ++k) d.war[k] = pos[d.war[k]];
+			if (d.war_writer >= 0) d.war_writer = pos[d.war_writer];
+		}
+	}
+
 	/* launch up to n pictures as one k_batch on stream 0 (fewer if a slot's readers would exceed
 	 * WAR_MAX); capture: verification copy-out area [n][fsz] or null.  Returns the pictures taken. */
 	int launch_batch(const PicJob *jobs, int n, uint8_t *capture)
@@ -295,6 +329,7 @@ struct Sched {
 			a.ss = slot_seq;
 			a.fin = bt.words;
 			a.pidx = p;
+			a.didx = p;
 			a.n_war = (int)rd[j.slot].size();
 			for (int i = 0; i < a.n_war; ++i) a.war[i] = rd[j.slot][i];
 			a.war_writer = last_writer[j.slot];
@@ -310,6 +345,7 @@ struct Sched {
 			taken++;
 		}
 		if (!taken) return -1;
+		hoist_intra(ha, taken);
 		CHECK(hipMemcpyAsync(bt.d_args[idx], ha, sizeof(PictureArgs) * taken, hipMemcpyHostToDevice, s));
 		CHECK(hipMemsetAsync(bt.words, 0, sizeof(int) * (2 * (size_t)bt.cap + (size_t)taken * SCR_WORDS(Hmb)), s));
 		const int bpp = picture_blocks(inter_grid, Hmb);

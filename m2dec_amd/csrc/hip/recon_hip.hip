@@ -22,6 +22,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include "recon_kernels.h"
 #include "intra_tables.h"
 #include "recon_internal.h"
@@ -214,7 +215,7 @@ __device__ __forceinline__ void signal_progress(int *flag, int value)
 /* one inter macroblock, all 256 lanes of the workgroup (uniform call) */
 __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t *__restrict__ inters,
                          const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                         size_t fsz, int W, int H, int Wmb, int slot)
+                         size_t fsz, int W, int H, int Wmb, int slot, uint8_t *tile)
 {
 	__shared__ int s_res[256 + 128];
 	__shared__ int s_cnt[4];
@@ -267,6 +268,10 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 	if (__builtin_amdgcn_readfirstlane(m.cbp) == 0) {
 		*dl = (uint8_t)predl;
 		if (t < 128) *dc = (uint8_t)predc;
+		if (tile) {
+			tile[t] = (uint8_t)predl;
+			if (t < 128) tile[256 + cy * 16 + cx * 2 + cc] = (uint8_t)predc;
+		}
 		return; /* uniform: m is the same in every lane */
 	}
 #endif
@@ -367,140 +372,12 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 			out = d_clip255(predl + s_res[t]);
 		}
 		*dl = (uint8_t)out;
+		if (tile) tile[t] = (uint8_t)out;
 	}
-	if (t < 128) *dc = (uint8_t)d_clip255(predc + s_res[256 + cc * 64 + cy * 8 + cx]);
-}
-
-/*
- * Inter MBs as a bounded persistent grid.  Work items are (MB row, 8-MB segment) in raster order,
- * dequeued from a per-launch counter.  Before its MBs, an item waits until every reference picture
- * it reads has its final samples in all the MB rows and columns its motion vectors reach
- * (rowflag[picture][row] = ROWFLAG(seq, columns final), raised by the deblocking storer as it
- * writes; the columns are rounded up to whole 128-byte lines, so no partially final line is ever
- * cached; polled with sc1 loads, then ONE agent acquire): a picture's MC follows its references'
- * deblocking wavefront column by column, so consecutive anchor pictures overlap.  The grid is kept
- * small (a fraction of the CUs) so that the spinning items can never keep the k_deblock they wait
- * for off the device.
- */
-__device__ void inter_worker(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters,
-                             const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                             size_t fsz, int W, int H, int Wmb, int Hmb, int slot, const SlotSeq &ss,
-                             const unsigned long long *rowflag, int *queue, int *inter_cnt, int *err)
-{
-	__shared__ int s_item, s_rmin, s_rmax, s_cmax;
-	__shared__ unsigned int s_refs[2];
-	const int t = threadIdx.x;
-	/* Single-lane work in this loop is done by the whole of wave 0 under a SCALAR branch, the one
-	 * lane picked by value (atomic operand 0 on lanes 1..63).  An `if (t == 0)` here lets the
-	 * compiler thread lanes 1..63 of wave 0 straight back to the next barrier while lane 0 is still
-	 * dequeueing, which deadlocks the workgroup (seen on gfx950 with ROCm 7.2). */
-	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
-	const int nseg = (Wmb + 7) >> 3, nitems = Hmb * nseg;
-	int nst_dbg = 0;
-	for (;;) {
-		if (wave0) {
-			const int v = __hip_atomic_fetch_add((gi32 *)queue, t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			s_item = __builtin_amdgcn_readfirstlane(v);
-			s_rmin = 1 << 30;
-			s_rmax = -1;
-			s_cmax = 0;
-			s_refs[0] = s_refs[1] = 0;
-		}
-		__syncthreads();
-		const int item = __builtin_amdgcn_readfirstlane(s_item);
-		if (item >= nitems) break;
-		const int y = item / nseg, x0 = (item % nseg) * 8, x1 = min(x0 + 8, Wmb);
-		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
-	/* ---- vertical and rightward reach of this segment's motion into the references (8 lanes per MB;
-	 * luma 6-tap window; the chroma window never reaches further) */
-		if (t < 64) {
-			const int mbi = x0 + (t >> 3);
-			int rmin = 1 << 30, rmax = -1, cmax = 0;
-			unsigned int r0 = 0, r1 = 0;
-			if (mbi < x1) {
-				const m2r_mb_t m = mbs[y * Wmb + mbi];
-				if (m.kind == M2R_MB_INTER) {
-					const m2r_inter_t &it = inters[m.inter];
-					for (int k = (t & 7) * 4; k < (t & 7) * 4 + 4; ++k) {
-						const int l = k >> 4, blk = k & 15;
-						const int sl = it.slot[l][(blk >> 3) * 2 + ((blk & 3) >> 1)];
-						if (sl < 0) continue;
-						const int py = y * 16 + (blk >> 2) * 4 + (it.mv[l][blk][1] >> 2);
-						const int top = py - 2, bot = py + 3 + 3;
-						rmin = min(rmin, top < 0 ? 0 : min(top >> 4, Hmb - 1));
-						rmax = max(rmax, bot < 0 ? 0 : min(bot >> 4, Hmb - 1));
-						const int right = mbi * 16 + (blk & 3) * 4 + (it.mv[l][blk][0] >> 2) + 3 + 3;
-						cmax = max(cmax, right < 0 ? 0 : min(right >> 4, Wmb - 1));
-						if (sl < 32) r0 |= 1u << sl;
-						else r1 |= 1u << (sl - 32);
-					}
-				}
-			}
-			if (rmax >= 0) {
-				atomicMin(&s_rmin, rmin);
-				atomicMax(&s_rmax, rmax);
-				atomicMax(&s_cmax, cmax);
-				atomicOr(&s_refs[0], r0);
-				atomicOr(&s_refs[1], r1);
-			}
-		}
-		__syncthreads();
-#ifndef M2DEC_NO_REFWAIT
-		const int rmin_u = __builtin_amdgcn_readfirstlane(s_rmin), rmax_u = __builtin_amdgcn_readfirstlane(s_rmax);
-		if (rmax_u >= 0 && wave0) {
-			/* rows rmin .. rmax final up to the reach: their own stores and the next row's (rows 13..15)
-			 * done.  Columns are whole 128-byte lines (8 MBs) when the stride allows, else whole rows:
-			 * a line cached while partly unfinal could outlive the acquire below */
-			const int rlast = min(rmax_u + 1, Hmb - 1);
-			const int cmax_u = __builtin_amdgcn_readfirstlane(s_cmax);
-			const int need = (W & 127) ? Wmb : min(Wmb, (cmax_u + 8) & ~7);
-			for (int k = 0; k < 2; ++k) {
-				unsigned int bits = __builtin_amdgcn_readfirstlane(s_refs[k]);
-				while (bits) {
-					const int sl = k * 32 + __builtin_ctz(bits);
-					bits &= bits - 1;
-					const int want = ss.s[sl];
-					if (want <= 0) continue;
-					/* entry (seq & 63) only ever grows: a later picture's value also means "final" */
-					const unsigned long long *fl = rowflag + (size_t)((want - 1) & 63) * Hmb;
-					const unsigned long long wv = ROWFLAG(want - 1, need);
-					unsigned spins = 0;
-					for (int r0 = rmin_u; r0 <= rlast; r0 += 64) {
-						const int r = r0 + t;
-						for (;;) {
-							const bool ok = (r > rlast) ||
-							                __hip_atomic_load((gu64 *)&fl[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wv;
-							if (__all(ok)) break;
-							if (!spin_ok(spins, err, 32)) break;
-						}
-					}
-				}
-			}
-			/* ALWAYS acquire, even when every flag was already set: this XCD's L2 may hold lines of
-			 * rows 13..15 that the row's own deblock workgroup loaded before the row below filtered
-			 * and rewrote them from another XCD */
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		}
-#endif
-		__syncthreads();
-		STAMPI(96 + (blockIdx.x & 63), 1, nst_dbg & 255, item);
-		for (int x = x0; x < x1; ++x) {
-			const m2r_mb_t m = mbs[y * Wmb + x];
-			if (__builtin_amdgcn_readfirstlane(m.kind) == M2R_MB_INTER)
-				inter_mb(y * Wmb + x, m, inters, slices, pool, frames, fsz, W, H, Wmb, slot);
-			__syncthreads();
-		}
-		/* segment done: every wave drained, then ONE agent release and the row's counter */
-		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		__syncthreads();
-		if (wave0) {
-			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__hip_atomic_fetch_add((gi32 *)&inter_cnt[y], t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-		}
-		STAMPI(96 + (blockIdx.x & 63), 2, nst_dbg & 255, item);
-		nst_dbg++;
+	if (t < 128) {
+		const uint8_t v = (uint8_t)d_clip255(predc + s_res[256 + cc * 64 + cy * 8 + cx]);
+		*dc = v;
+		if (tile) tile[256 + cy * 16 + cx * 2 + cc] = v;
 	}
 }
 
@@ -657,6 +534,360 @@ __device__ __forceinline__ int ipred_taps(uint32_t w, int bits, const int *nv)
 	return (v + ((1 << s) >> 1)) >> s;
 }
 
+/* The reconstruction of ONE intra / PCM MB in an LDS context whose row 0 / column 0 already hold the
+ * unfiltered top / left neighbours (luma L[0][0] top-left, L[0][1..24] top and top-right, L[1..16][0]
+ * left; chroma C[c][0][*], C[c][*][0] likewise): luma on the wave(s) with do_luma, chroma on the
+ * wave(s) with do_chroma (disjoint LDS: L, R[0..255], DC, F, HV / C, R[256..383]).  q: the MB's pool
+ * segment (staged in LDS).  Reference: mb_intra4x4 / intraNxN / intra16x16 / intrapcm
+ * (h264.cpp:3121-3254, 4083-4127, 4407-4555, 4708-4761), residual_chroma (2374-2461). */
+__device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *q, const int t, const bool do_luma,
+                                              const bool do_chroma, IntraLDS *ctx, const IntraTables *tabs)
+{
+	uint8_t(&L)[17][LW] = ctx->L;
+	uint8_t(&C)[2][9][9] = ctx->C;
+	int(&R)[256 + 128] = ctx->R;
+	int(&DC)[16] = ctx->DC;
+	int(&F)[32] = ctx->F;
+	int(&HV)[4] = ctx->HV;
+	if (m.kind == M2R_MB_PCM) {
+		const uint8_t *s = (const uint8_t *)q;
+		if (do_luma)
+			for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
+		else
+			for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
+		WSYNC();
+	} else {
+		/* ---- chroma prediction (h264.cpp:4559-4706); thread t: sample (t & 7, t >> 3) of both components */
+		if (do_chroma) {
+			int ca = m.avail_chroma, mode = m.chroma_mode;
+			int px = t & 7, py = t >> 3;
+			for (int c = 0; c < 2; ++c) {
+				int v = -1;
+				if (mode == 0) {
+					int blk = (py >> 2) * 2 + (px >> 2), xo = (px >> 2) * 4, yo = (py >> 2) * 4, st = 0, sl = 0;
+					int ht = (ca & 2) != 0, hl = (ca & 1) != 0;
+					for (int i = 0; i < 4; ++i) { st += C[c][0][1 + xo + i]; sl += C[c][1 + yo + i][0]; }
+					if (blk == 0 || blk == 3) v = (ht && hl) ? (st + sl + 4) >> 3 : (hl ? (sl + 2) >> 2 : (ht ? (st + 2) >> 2 : 128));
+					else if (blk == 1) v = ht ? (st + 2) >> 2 : (hl ? (sl + 2) >> 2 : 128);
+					else v = hl ? (sl + 2) >> 2 : (ht ? (st + 2) >> 2 : 128);
+				} else if (mode == 1) {
+					if (ca & 1) v = C[c][1 + py][0];
+				} else if (mode == 2) {
+					if (ca & 2) v = C[c][0][1 + px];
+				} else {
+					int Hh = 0, Vv = 0;
+					for (int i = 0; i < 4; ++i) {
+						Hh += (i + 1) * (C[c][0][1 + 4 + i] - C[c][0][1 + 2 - i]);
+						Vv += (i + 1) * (C[c][1 + 4 + i][0] - C[c][1 + 2 - i][0]);
+					}
+					int a = 16 * (C[c][8][0] + C[c][0][8]);
+					int b = (34 * Hh + 32) >> 6, cc2 = (34 * Vv + 32) >> 6;
+					v = d_clip255((a + b * (px - 3) + cc2 * (py - 3) + 16) >> 5);
+				}
+				R[256 + c * 64 + t] = v;
+			}
+		}
+		WSYNC();
+		if (do_chroma)
+			for (int c = 0; c < 2; ++c) {
+				int v = R[256 + c * 64 + t];
+				if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
+			}
+		WSYNC();
+
+		/* ---- luma */
+		const int qp = m.qpy;
+		if (!do_luma) {
+			/* chroma wave: no luma */
+		} else if (m.kind == M2R_MB_I4x4) {
+			/* residual of all 16 blocks first (independent of the prediction), then the serial
+			 * block chain: predict + add, one wave sync per block */
+			for (int k = t; k < 256; k += 64) {
+				const int blk = k >> 4, pos = k & 15;
+				int v = 0;
+				if ((m.nz >> blk) & 1) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
+				R[k] = v;
+			}
+			WSYNC();
+			{
+				int *p = &R[(t >> 2) * 16 + (t & 3) * 4];
+				int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+				d_idct4_1d(a0, a1, a2, a3);
+				p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
+			}
+			WSYNC();
+			{
+				int *p = &R[(t >> 2) * 16 + (t & 3)];
+				int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
+				d_idct4_1d(a0, a1, a2, a3);
+				p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
+			}
+			WSYNC();
+			/* the serial block chain, table-driven (intra_tables.h): per block one table word
+			 * (fetched a block ahead), three neighbour reads, one sync */
+			uint32_t wn = 0;
+			if (t < 16) {
+				const int mode0 = (int)(m.ipred[0] & 15);
+				wn = tabs->p4[mode0 == 2 ? 0 : mode0][t];
+			}
+			for (int blk = 0; blk < 16; ++blk) {
+				const int ox = d_blk_x(blk) * 4, oy = d_blk_y(blk) * 4;
+				const int av = avail4(blk, m.avail_luma);
+				const int mode = (int)((((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15);
+				const uint32_t w = wn;
+				if (t < 16 && blk < 15) {
+					const int nb = blk + 1;
+					const int mn = (int)((((nb >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (nb & 7))) & 15);
+					wn = tabs->p4[mn == 2 ? 0 : mn][t];
+				}
+				if (t < 16) {
+					uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
+					int v;
+					bool ok;
+					if (mode == 2) {
+						/* DC: (avail & 3) picks the sum (pred4x4_dc family) */
+						const uint8_t *tp = &L[oy][1 + ox];
+						int st = tp[0] + tp[1] + tp[2] + tp[3];
+						int sl = L[oy + 1][ox] + L[oy + 2][ox] + L[oy + 3][ox] + L[oy + 4][ox];
+						v = ((av & 3) == 3) ? (st + sl + 4) >> 3 : ((av & 1) ? (sl + 2) >> 2 : ((av & 2) ? (st + 2) >> 2 : 128));
+						ok = true;
+					} else {
+						/* neighbour index -> LDS: 0 top-left, 1..8 top (top-right -> P3 if unavailable), 9..12 left */
+						int nv[3];
+#pragma unroll
+						for (int k = 0; k < 3; ++k) {
+							const int i = (int)((w >> (4 * k)) & 15);
+							const int pi = (i - 1 >= 4 && !(av & 4)) ? 3 : i - 1;
+							const uint8_t *a = (i == 0) ? &L[oy][ox] : (i <= 8) ? &L[oy][1 + ox + pi] : &L[oy + 1 + (i - 9)][ox];
+							nv[k] = *a;
+						}
+						v = ipred_taps(w, 4, nv);
+						ok = (av & c_req4[mode]) == c_req4[mode];
+					}
+					const int base = ok ? v : *d; /* the reference leaves the sample as it was */
+					*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
+				}
+				WSYNC();
+			}
+		} else if (m.kind == M2R_MB_I8x8) {
+			/* residual of all four 8x8 blocks first; per block: reference filtering, predict + add */
+			/* per block: nonzero count and DC level (the SWAR DC-only quirk), in LDS: a register
+			 * array indexed by the block loop would live in scratch */
+			for (int b = 0; b < 4; ++b) {
+				const int lv = ((m.nz >> (4 * b)) & 1) ? q[d_luma_off(m, 4 * b) + t] : 0;
+				R[b * 64 + t] = lv * d_scale8(qp, t & 7, t >> 3);
+				const int cnt = __popcll(__ballot(lv != 0));
+				if (t == 0) {
+					DC[b] = lv; /* lane 0 = coefficient 0 */
+					DC[4 + b] = cnt;
+				}
+			}
+			WSYNC();
+			if (t < 32) {
+				int v[8];
+				int *p = &R[(t >> 3) * 64 + (t & 7) * 8];
+				for (int k = 0; k < 8; ++k) v[k] = p[k];
+				d_idct8_1d(v);
+				for (int k = 0; k < 8; ++k) p[k] = v[k];
+			}
+			WSYNC();
+			if (t < 32) {
+				int v[8];
+				int *p = &R[(t >> 3) * 64 + (t & 7)];
+				for (int k = 0; k < 8; ++k) v[k] = p[k * 8];
+				d_idct8_1d(v);
+				for (int k = 0; k < 8; ++k) p[k * 8] = (v[k] + 32) >> 6;
+			}
+			WSYNC();
+			for (int b = 0; b < 4; ++b) {
+				const int ox = (b & 1) * 8, oy = (b >> 1) * 8;
+				const int av = avail8(b, m.avail_luma);
+				/* reference sample filtering (spec 8.3.2.2.1) */
+				if (t < 25) {
+					int hasL = av & 1, hasT = av & 2, hasTR = av & 4, hasTL = av & 8;
+					int tl = L[oy][ox];
+#define TP(i) ((i) < 8 ? (int)L[oy][1 + ox + (i)] : (hasTR ? (int)L[oy][1 + ox + (i)] : (int)L[oy][1 + ox + 7]))
+#define LP(i) ((int)L[oy + 1 + (i)][ox])
+					if (t < 16) {
+						if (hasT) {
+							int v;
+							if (t == 0) v = hasTL ? (tl + 2 * TP(0) + TP(1) + 2) >> 2 : (3 * TP(0) + TP(1) + 2) >> 2;
+							else if (t == 15) v = (TP(14) + 3 * TP(15) + 2) >> 2;
+							else v = (TP(t - 1) + 2 * TP(t) + TP(t + 1) + 2) >> 2;
+							F[t] = v;
+						}
+					} else if (t < 24) {
+						int i = t - 16;
+						if (hasL) {
+							int v;
+							if (i == 0) v = hasTL ? (tl + 2 * LP(0) + LP(1) + 2) >> 2 : (3 * LP(0) + LP(1) + 2) >> 2;
+							else if (i == 7) v = (LP(6) + 3 * LP(7) + 2) >> 2;
+							else v = (LP(i - 1) + 2 * LP(i) + LP(i + 1) + 2) >> 2;
+							F[t] = v;
+						}
+					} else if (hasTL) {
+						int v;
+						if (hasT && hasL) v = (TP(0) + 2 * tl + LP(0) + 2) >> 2;
+						else if (hasT) v = (3 * tl + TP(0) + 2) >> 2;
+						else if (hasL) v = (3 * tl + LP(0) + 2) >> 2;
+						else v = tl;
+						F[24] = v;
+					}
+#undef TP
+#undef LP
+				}
+				WSYNC();
+				{
+					const int mode = (m.ipred[0] >> (4 * b)) & 15;
+					int v;
+					if (mode == 2) {
+						v = pred8_px(2, av, t & 7, t >> 3, F, F + 16, F[24]);
+					} else {
+						/* table-driven (intra_tables.h) over the filtered neighbours F */
+						const uint32_t w = tabs->p8[mode][t];
+						int nv[3];
+#pragma unroll
+						for (int k = 0; k < 3; ++k) nv[k] = F[(w >> (5 * k)) & 31];
+						v = ((av & c_req8[mode]) == c_req8[mode]) ? ipred_taps(w, 5, nv) : -1;
+					}
+					uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
+					const int base = (v >= 0) ? v : *d;
+					const int dcl = DC[b];
+					if (DC[4 + b] == 1 && dcl != 0) *d = (uint8_t)d_swar(base, dcl * d_scale8(qp, 0, 0), t & 7, 8);
+					else *d = (uint8_t)d_clip255(base + R[b * 64 + t]);
+				}
+				WSYNC();
+			}
+		} else {
+			/* Intra16x16 (h264.cpp:4407-4555) */
+			const int av = m.avail_luma, mode = m.pred_mode;
+			if (t == 0 && mode == 3) {
+				int Hh = 0, Vv = 0;
+				for (int i = 0; i < 8; ++i) {
+					Hh += (i + 1) * (L[0][1 + 8 + i] - L[0][1 + 6 - i]);
+					Vv += (i + 1) * (L[1 + 8 + i][0] - L[1 + 6 - i][0]);
+				}
+				HV[0] = 16 * (L[16][0] + L[0][16]);
+				HV[1] = (5 * Hh + 32) >> 6;
+				HV[2] = (5 * Vv + 32) >> 6;
+			}
+			if (t == 1 && mode == 2) {
+				int st = 0, sl = 0;
+				for (int i = 0; i < 16; ++i) { st += L[0][1 + i]; sl += L[1 + i][0]; }
+				HV[3] = ((av & 3) == 3) ? (st + sl + 16) >> 5 : ((av & 1) ? (sl + 8) >> 4 : ((av & 2) ? (st + 8) >> 4 : 128));
+			}
+			/* DC levels */
+			if (t < 16) DC[t] = (m.nz & M2R_NZ_LUMA_DC) ? q[t] * d_scale4(qp, 0, 0) : 0;
+			WSYNC();
+			for (int k = t; k < 256; k += 64) {
+				int px = k & 15, py = k >> 4, v = -1;
+				if (mode == 0) { if (av & 2) v = L[0][1 + px]; }
+				else if (mode == 1) { if (av & 1) v = L[1 + py][0]; }
+				else if (mode == 2) v = HV[3];
+				else v = d_clip255((HV[0] + HV[1] * (px - 7) + HV[2] * (py - 7) + 16) >> 5);
+				R[k] = v;
+			}
+			WSYNC();
+			for (int k = t; k < 256; k += 64) {
+				int v = R[k];
+				if (v >= 0) L[1 + (k >> 4)][1 + (k & 15)] = (uint8_t)v;
+			}
+			/* DC Hadamard: rows then columns, (x + 2) >> 2 */
+			if (t < 4) {
+				int *r = &DC[t * 4];
+				int a0 = r[0] + r[1], a1 = r[0] - r[1], a2 = r[2] + r[3], a3 = r[2] - r[3];
+				r[0] = a0 + a2; r[1] = a0 - a2; r[2] = a1 - a3; r[3] = a1 + a3;
+			}
+			WSYNC();
+			if (t < 4) {
+				int *r = &DC[t];
+				int a0 = r[0] + r[4], a1 = r[0] - r[4], a2 = r[8] + r[12], a3 = r[8] - r[12];
+				r[0] = (a0 + a2 + 2) >> 2; r[4] = (a0 - a2 + 2) >> 2; r[8] = (a1 - a3 + 2) >> 2; r[12] = (a1 + a3 + 2) >> 2;
+			}
+			WSYNC();
+			if (m.cbp & 15) {
+				/* AC blocks with coefficients: full transform with the DC inserted; others DC-only SWAR */
+				for (int k = t; k < 256; k += 64) {
+					int blk = k >> 4, pos = k & 15;
+					int bx = d_blk_x(blk), by = d_blk_y(blk);
+					int v = 0;
+					if (pos == 0) v = DC[by * 4 + bx];
+					else if (m.nz & (1u << blk)) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
+					R[k] = v;
+				}
+				WSYNC();
+				{
+					int blk = t >> 2, row = t & 3;
+					int *p = &R[blk * 16 + row * 4];
+					int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+					d_idct4_1d(a0, a1, a2, a3);
+					p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
+				}
+				WSYNC();
+				{
+					int blk = t >> 2, col = t & 3;
+					int *p = &R[blk * 16 + col];
+					int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
+					d_idct4_1d(a0, a1, a2, a3);
+					p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
+				}
+				WSYNC();
+				for (int k = t; k < 256; k += 64) {
+					int blk = k >> 4, pos = k & 15;
+					int bx = d_blk_x(blk), by = d_blk_y(blk);
+					uint8_t *d = &L[1 + by * 4 + (pos >> 2)][1 + bx * 4 + (pos & 3)];
+					if (m.nz & (1u << blk)) *d = (uint8_t)d_clip255(*d + R[k]);
+					else *d = (uint8_t)d_swar(*d, DC[by * 4 + bx], pos & 3, 4);
+				}
+			} else if (m.nz & M2R_NZ_LUMA_DC) {
+				for (int k = t; k < 256; k += 64) {
+					int px = k & 15, py = k >> 4;
+					uint8_t *d = &L[1 + py][1 + px];
+					*d = (uint8_t)d_swar(*d, DC[(py >> 2) * 4 + (px >> 2)], px & 3, 4);
+				}
+			}
+			WSYNC();
+		}
+
+		/* ---- chroma residual (residual_chroma, h264.cpp:2374-2461) */
+		if (do_chroma && (m.cbp >> 4)) {
+			int ccbp = m.cbp >> 4;
+			for (int k = t; k < 128; k += 64) {
+				int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
+				int cblk = (cy >> 2) * 2 + (cx >> 2), pos = (cy & 3) * 4 + (cx & 3);
+				int v = 0;
+				if (pos == 0) v = d_chroma_dc(m, q, c, cblk);
+				else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(c, cblk)))
+					v = q[d_chroma_off(m, 19 + 4 * c + cblk) + pos] * d_scale4(c ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
+				R[256 + c * 64 + cy * 8 + cx] = v;
+			}
+			WSYNC();
+			if (t < 32) {
+				int comp = t >> 4, b = (t >> 2) & 3, row = t & 3;
+				int *p = &R[256 + comp * 64 + ((b >> 1) * 4 + row) * 8 + (b & 1) * 4];
+				int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+				d_idct4_1d(a0, a1, a2, a3);
+				p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
+			}
+			WSYNC();
+			if (t < 32) {
+				int comp = t >> 4, b = (t >> 2) & 3, col = t & 3;
+				int *p = &R[256 + comp * 64 + ((b >> 1) * 4) * 8 + (b & 1) * 4 + col];
+				int a0 = p[0], a1 = p[8], a2 = p[16], a3 = p[24];
+				d_idct4_1d(a0, a1, a2, a3);
+				p[0] = (a0 + 32) >> 6; p[8] = (a1 + 32) >> 6; p[16] = (a2 + 32) >> 6; p[24] = (a3 + 32) >> 6;
+			}
+			WSYNC();
+			for (int k = t; k < 128; k += 64) {
+				int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
+				uint8_t *d = &C[c][1 + cy][1 + cx];
+				*d = (uint8_t)d_clip255(*d + R[256 + c * 64 + cy * 8 + cx]);
+			}
+			WSYNC();
+		}
+	}
+}
+
 __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ctx, const IntraTables *tabs,
                           const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
                           uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
@@ -758,346 +989,7 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 		WSYNC();
 		STAMPX(x, 0);
 
-		if (m.kind == M2R_MB_PCM) {
-			const uint8_t *s = (const uint8_t *)q;
-			if (do_luma)
-				for (int k = t; k < 256; k += 64) L[1 + (k >> 4)][1 + (k & 15)] = s[k];
-			else
-				for (int k = t; k < 128; k += 64) C[k >> 6][1 + ((k >> 3) & 7)][1 + (k & 7)] = s[256 + k];
-			WSYNC();
-		} else {
-			/* ---- chroma prediction (h264.cpp:4559-4706); thread t: sample (t & 7, t >> 3) of both components */
-			if (do_chroma) {
-				int ca = m.avail_chroma, mode = m.chroma_mode;
-				int px = t & 7, py = t >> 3;
-				for (int c = 0; c < 2; ++c) {
-					int v = -1;
-					if (mode == 0) {
-						int blk = (py >> 2) * 2 + (px >> 2), xo = (px >> 2) * 4, yo = (py >> 2) * 4, st = 0, sl = 0;
-						int ht = (ca & 2) != 0, hl = (ca & 1) != 0;
-						for (int i = 0; i < 4; ++i) { st += C[c][0][1 + xo + i]; sl += C[c][1 + yo + i][0]; }
-						if (blk == 0 || blk == 3) v = (ht && hl) ? (st + sl + 4) >> 3 : (hl ? (sl + 2) >> 2 : (ht ? (st + 2) >> 2 : 128));
-						else if (blk == 1) v = ht ? (st + 2) >> 2 : (hl ? (sl + 2) >> 2 : 128);
-						else v = hl ? (sl + 2) >> 2 : (ht ? (st + 2) >> 2 : 128);
-					} else if (mode == 1) {
-						if (ca & 1) v = C[c][1 + py][0];
-					} else if (mode == 2) {
-						if (ca & 2) v = C[c][0][1 + px];
-					} else {
-						int Hh = 0, Vv = 0;
-						for (int i = 0; i < 4; ++i) {
-							Hh += (i + 1) * (C[c][0][1 + 4 + i] - C[c][0][1 + 2 - i]);
-							Vv += (i + 1) * (C[c][1 + 4 + i][0] - C[c][1 + 2 - i][0]);
-						}
-						int a = 16 * (C[c][8][0] + C[c][0][8]);
-						int b = (34 * Hh + 32) >> 6, cc2 = (34 * Vv + 32) >> 6;
-						v = d_clip255((a + b * (px - 3) + cc2 * (py - 3) + 16) >> 5);
-					}
-					R[256 + c * 64 + t] = v;
-				}
-			}
-			WSYNC();
-			if (do_chroma)
-				for (int c = 0; c < 2; ++c) {
-					int v = R[256 + c * 64 + t];
-					if (v >= 0) C[c][1 + (t >> 3)][1 + (t & 7)] = (uint8_t)v;
-				}
-			WSYNC();
-			STAMPX(x, 1);
-
-			/* ---- luma */
-			const int qp = m.qpy;
-			if (!do_luma) {
-				/* chroma wave: no luma */
-			} else if (m.kind == M2R_MB_I4x4) {
-				/* residual of all 16 blocks first (independent of the prediction), then the serial
-				 * block chain: predict + add, one wave sync per block */
-				for (int k = t; k < 256; k += 64) {
-					const int blk = k >> 4, pos = k & 15;
-					int v = 0;
-					if ((m.nz >> blk) & 1) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
-					R[k] = v;
-				}
-				WSYNC();
-				{
-					int *p = &R[(t >> 2) * 16 + (t & 3) * 4];
-					int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-					d_idct4_1d(a0, a1, a2, a3);
-					p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
-				}
-				WSYNC();
-				{
-					int *p = &R[(t >> 2) * 16 + (t & 3)];
-					int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
-					d_idct4_1d(a0, a1, a2, a3);
-					p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
-				}
-				WSYNC();
-				/* the serial block chain, table-driven (intra_tables.h): per block one table word
-				 * (fetched a block ahead), three neighbour reads, one sync */
-				uint32_t wn = 0;
-				if (t < 16) {
-					const int mode0 = (int)(m.ipred[0] & 15);
-					wn = tabs->p4[mode0 == 2 ? 0 : mode0][t];
-				}
-				for (int blk = 0; blk < 16; ++blk) {
-					const int ox = d_blk_x(blk) * 4, oy = d_blk_y(blk) * 4;
-					const int av = avail4(blk, m.avail_luma);
-					const int mode = (int)((((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15);
-					const uint32_t w = wn;
-					if (t < 16 && blk < 15) {
-						const int nb = blk + 1;
-						const int mn = (int)((((nb >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (nb & 7))) & 15);
-						wn = tabs->p4[mn == 2 ? 0 : mn][t];
-					}
-					if (t < 16) {
-						uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
-						int v;
-						bool ok;
-						if (mode == 2) {
-							/* DC: (avail & 3) picks the sum (pred4x4_dc family) */
-							const uint8_t *tp = &L[oy][1 + ox];
-							int st = tp[0] + tp[1] + tp[2] + tp[3];
-							int sl = L[oy + 1][ox] + L[oy + 2][ox] + L[oy + 3][ox] + L[oy + 4][ox];
-							v = ((av & 3) == 3) ? (st + sl + 4) >> 3 : ((av & 1) ? (sl + 2) >> 2 : ((av & 2) ? (st + 2) >> 2 : 128));
-							ok = true;
-						} else {
-							/* neighbour index -> LDS: 0 top-left, 1..8 top (top-right -> P3 if unavailable), 9..12 left */
-							int nv[3];
-#pragma unroll
-							for (int k = 0; k < 3; ++k) {
-								const int i = (int)((w >> (4 * k)) & 15);
-								const int pi = (i - 1 >= 4 && !(av & 4)) ? 3 : i - 1;
-								const uint8_t *a = (i == 0) ? &L[oy][ox] : (i <= 8) ? &L[oy][1 + ox + pi] : &L[oy + 1 + (i - 9)][ox];
-								nv[k] = *a;
-							}
-							v = ipred_taps(w, 4, nv);
-							ok = (av & c_req4[mode]) == c_req4[mode];
-						}
-						const int base = ok ? v : *d; /* the reference leaves the sample as it was */
-						*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
-					}
-					WSYNC();
-				}
-			} else if (m.kind == M2R_MB_I8x8) {
-				/* residual of all four 8x8 blocks first; per block: reference filtering, predict + add */
-				/* per block: nonzero count and DC level (the SWAR DC-only quirk), in LDS: a register
-				 * array indexed by the block loop would live in scratch */
-				for (int b = 0; b < 4; ++b) {
-					const int lv = ((m.nz >> (4 * b)) & 1) ? q[d_luma_off(m, 4 * b) + t] : 0;
-					R[b * 64 + t] = lv * d_scale8(qp, t & 7, t >> 3);
-					const int cnt = __popcll(__ballot(lv != 0));
-					if (t == 0) {
-						DC[b] = lv; /* lane 0 = coefficient 0 */
-						DC[4 + b] = cnt;
-					}
-				}
-				WSYNC();
-				if (t < 32) {
-					int v[8];
-					int *p = &R[(t >> 3) * 64 + (t & 7) * 8];
-					for (int k = 0; k < 8; ++k) v[k] = p[k];
-					d_idct8_1d(v);
-					for (int k = 0; k < 8; ++k) p[k] = v[k];
-				}
-				WSYNC();
-				if (t < 32) {
-					int v[8];
-					int *p = &R[(t >> 3) * 64 + (t & 7)];
-					for (int k = 0; k < 8; ++k) v[k] = p[k * 8];
-					d_idct8_1d(v);
-					for (int k = 0; k < 8; ++k) p[k * 8] = (v[k] + 32) >> 6;
-				}
-				WSYNC();
-				for (int b = 0; b < 4; ++b) {
-					const int ox = (b & 1) * 8, oy = (b >> 1) * 8;
-					const int av = avail8(b, m.avail_luma);
-					/* reference sample filtering (spec 8.3.2.2.1) */
-					if (t < 25) {
-						int hasL = av & 1, hasT = av & 2, hasTR = av & 4, hasTL = av & 8;
-						int tl = L[oy][ox];
-#define TP(i) ((i) < 8 ? (int)L[oy][1 + ox + (i)] : (hasTR ? (int)L[oy][1 + ox + (i)] : (int)L[oy][1 + ox + 7]))
-#define LP(i) ((int)L[oy + 1 + (i)][ox])
-						if (t < 16) {
-							if (hasT) {
-								int v;
-								if (t == 0) v = hasTL ? (tl + 2 * TP(0) + TP(1) + 2) >> 2 : (3 * TP(0) + TP(1) + 2) >> 2;
-								else if (t == 15) v = (TP(14) + 3 * TP(15) + 2) >> 2;
-								else v = (TP(t - 1) + 2 * TP(t) + TP(t + 1) + 2) >> 2;
-								F[t] = v;
-							}
-						} else if (t < 24) {
-							int i = t - 16;
-							if (hasL) {
-								int v;
-								if (i == 0) v = hasTL ? (tl + 2 * LP(0) + LP(1) + 2) >> 2 : (3 * LP(0) + LP(1) + 2) >> 2;
-								else if (i == 7) v = (LP(6) + 3 * LP(7) + 2) >> 2;
-								else v = (LP(i - 1) + 2 * LP(i) + LP(i + 1) + 2) >> 2;
-								F[t] = v;
-							}
-						} else if (hasTL) {
-							int v;
-							if (hasT && hasL) v = (TP(0) + 2 * tl + LP(0) + 2) >> 2;
-							else if (hasT) v = (3 * tl + TP(0) + 2) >> 2;
-							else if (hasL) v = (3 * tl + LP(0) + 2) >> 2;
-							else v = tl;
-							F[24] = v;
-						}
-#undef TP
-#undef LP
-					}
-					WSYNC();
-					{
-						const int mode = (m.ipred[0] >> (4 * b)) & 15;
-						int v;
-						if (mode == 2) {
-							v = pred8_px(2, av, t & 7, t >> 3, F, F + 16, F[24]);
-						} else {
-							/* table-driven (intra_tables.h) over the filtered neighbours F */
-							const uint32_t w = tabs->p8[mode][t];
-							int nv[3];
-#pragma unroll
-							for (int k = 0; k < 3; ++k) nv[k] = F[(w >> (5 * k)) & 31];
-							v = ((av & c_req8[mode]) == c_req8[mode]) ? ipred_taps(w, 5, nv) : -1;
-						}
-						uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
-						const int base = (v >= 0) ? v : *d;
-						const int dcl = DC[b];
-						if (DC[4 + b] == 1 && dcl != 0) *d = (uint8_t)d_swar(base, dcl * d_scale8(qp, 0, 0), t & 7, 8);
-						else *d = (uint8_t)d_clip255(base + R[b * 64 + t]);
-					}
-					WSYNC();
-				}
-			} else {
-				/* Intra16x16 (h264.cpp:4407-4555) */
-				const int av = m.avail_luma, mode = m.pred_mode;
-				if (t == 0 && mode == 3) {
-					int Hh = 0, Vv = 0;
-					for (int i = 0; i < 8; ++i) {
-						Hh += (i + 1) * (L[0][1 + 8 + i] - L[0][1 + 6 - i]);
-						Vv += (i + 1) * (L[1 + 8 + i][0] - L[1 + 6 - i][0]);
-					}
-					HV[0] = 16 * (L[16][0] + L[0][16]);
-					HV[1] = (5 * Hh + 32) >> 6;
-					HV[2] = (5 * Vv + 32) >> 6;
-				}
-				if (t == 1 && mode == 2) {
-					int st = 0, sl = 0;
-					for (int i = 0; i < 16; ++i) { st += L[0][1 + i]; sl += L[1 + i][0]; }
-					HV[3] = ((av & 3) == 3) ? (st + sl + 16) >> 5 : ((av & 1) ? (sl + 8) >> 4 : ((av & 2) ? (st + 8) >> 4 : 128));
-				}
-				/* DC levels */
-				if (t < 16) DC[t] = (m.nz & M2R_NZ_LUMA_DC) ? q[t] * d_scale4(qp, 0, 0) : 0;
-				WSYNC();
-				for (int k = t; k < 256; k += 64) {
-					int px = k & 15, py = k >> 4, v = -1;
-					if (mode == 0) { if (av & 2) v = L[0][1 + px]; }
-					else if (mode == 1) { if (av & 1) v = L[1 + py][0]; }
-					else if (mode == 2) v = HV[3];
-					else v = d_clip255((HV[0] + HV[1] * (px - 7) + HV[2] * (py - 7) + 16) >> 5);
-					R[k] = v;
-				}
-				WSYNC();
-				for (int k = t; k < 256; k += 64) {
-					int v = R[k];
-					if (v >= 0) L[1 + (k >> 4)][1 + (k & 15)] = (uint8_t)v;
-				}
-				/* DC Hadamard: rows then columns, (x + 2) >> 2 */
-				if (t < 4) {
-					int *r = &DC[t * 4];
-					int a0 = r[0] + r[1], a1 = r[0] - r[1], a2 = r[2] + r[3], a3 = r[2] - r[3];
-					r[0] = a0 + a2; r[1] = a0 - a2; r[2] = a1 - a3; r[3] = a1 + a3;
-				}
-				WSYNC();
-				if (t < 4) {
-					int *r = &DC[t];
-					int a0 = r[0] + r[4], a1 = r[0] - r[4], a2 = r[8] + r[12], a3 = r[8] - r[12];
-					r[0] = (a0 + a2 + 2) >> 2; r[4] = (a0 - a2 + 2) >> 2; r[8] = (a1 - a3 + 2) >> 2; r[12] = (a1 + a3 + 2) >> 2;
-				}
-				WSYNC();
-				if (m.cbp & 15) {
-					/* AC blocks with coefficients: full transform with the DC inserted; others DC-only SWAR */
-					for (int k = t; k < 256; k += 64) {
-						int blk = k >> 4, pos = k & 15;
-						int bx = d_blk_x(blk), by = d_blk_y(blk);
-						int v = 0;
-						if (pos == 0) v = DC[by * 4 + bx];
-						else if (m.nz & (1u << blk)) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
-						R[k] = v;
-					}
-					WSYNC();
-					{
-						int blk = t >> 2, row = t & 3;
-						int *p = &R[blk * 16 + row * 4];
-						int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-						d_idct4_1d(a0, a1, a2, a3);
-						p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
-					}
-					WSYNC();
-					{
-						int blk = t >> 2, col = t & 3;
-						int *p = &R[blk * 16 + col];
-						int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
-						d_idct4_1d(a0, a1, a2, a3);
-						p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
-					}
-					WSYNC();
-					for (int k = t; k < 256; k += 64) {
-						int blk = k >> 4, pos = k & 15;
-						int bx = d_blk_x(blk), by = d_blk_y(blk);
-						uint8_t *d = &L[1 + by * 4 + (pos >> 2)][1 + bx * 4 + (pos & 3)];
-						if (m.nz & (1u << blk)) *d = (uint8_t)d_clip255(*d + R[k]);
-						else *d = (uint8_t)d_swar(*d, DC[by * 4 + bx], pos & 3, 4);
-					}
-				} else if (m.nz & M2R_NZ_LUMA_DC) {
-					for (int k = t; k < 256; k += 64) {
-						int px = k & 15, py = k >> 4;
-						uint8_t *d = &L[1 + py][1 + px];
-						*d = (uint8_t)d_swar(*d, DC[(py >> 2) * 4 + (px >> 2)], px & 3, 4);
-					}
-				}
-				WSYNC();
-			}
-
-			STAMPX(x, 2);
-			/* ---- chroma residual (residual_chroma, h264.cpp:2374-2461) */
-			if (do_chroma && (m.cbp >> 4)) {
-				int ccbp = m.cbp >> 4;
-				for (int k = t; k < 128; k += 64) {
-					int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
-					int cblk = (cy >> 2) * 2 + (cx >> 2), pos = (cy & 3) * 4 + (cx & 3);
-					int v = 0;
-					if (pos == 0) v = d_chroma_dc(m, q, c, cblk);
-					else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(c, cblk)))
-						v = q[d_chroma_off(m, 19 + 4 * c + cblk) + pos] * d_scale4(c ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
-					R[256 + c * 64 + cy * 8 + cx] = v;
-				}
-				WSYNC();
-				if (t < 32) {
-					int comp = t >> 4, b = (t >> 2) & 3, row = t & 3;
-					int *p = &R[256 + comp * 64 + ((b >> 1) * 4 + row) * 8 + (b & 1) * 4];
-					int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-					d_idct4_1d(a0, a1, a2, a3);
-					p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
-				}
-				WSYNC();
-				if (t < 32) {
-					int comp = t >> 4, b = (t >> 2) & 3, col = t & 3;
-					int *p = &R[256 + comp * 64 + ((b >> 1) * 4) * 8 + (b & 1) * 4 + col];
-					int a0 = p[0], a1 = p[8], a2 = p[16], a3 = p[24];
-					d_idct4_1d(a0, a1, a2, a3);
-					p[0] = (a0 + 32) >> 6; p[8] = (a1 + 32) >> 6; p[16] = (a2 + 32) >> 6; p[24] = (a3 + 32) >> 6;
-				}
-				WSYNC();
-				for (int k = t; k < 128; k += 64) {
-					int c = k >> 6, cx = k & 7, cy = (k >> 3) & 7;
-					uint8_t *d = &C[c][1 + cy][1 + cx];
-					*d = (uint8_t)d_clip255(*d + R[256 + c * 64 + cy * 8 + cx]);
-				}
-				WSYNC();
-			}
-		}
-
+		intra_mb_body(m, q, t, do_luma, do_chroma, ctx, tabs);
 		STAMPX(x, 3);
 		/* ---- write back and hand off the bottom rows */
 		if (do_luma)
@@ -1134,6 +1026,283 @@ __device__ void intra_row(const int y, const int t, const int part, IntraLDS *ct
 	signal_progress(&progress[y], Wmb);
 }
 
+/* ======================================================================== inter workers */
+
+/* MB (x, y)'s neighbour record is read by an intra MB: (x + 1, y) left, (x - 1 .. x + 1, y + 1) top */
+__device__ __forceinline__ bool nb_needed(const m2r_mb_t *__restrict__ mbs, int x, int y, int Wmb, int Hmb)
+{
+	bool r = x + 1 < Wmb && mbs[y * Wmb + x + 1].kind != M2R_MB_INTER;
+	if (y + 1 < Hmb)
+		for (int d = -1; d <= 1; ++d)
+			if (x + d >= 0 && x + d < Wmb && mbs[(y + 1) * Wmb + x + d].kind != M2R_MB_INTER) r = true;
+	return r;
+}
+
+/* the neighbour record of MB (x, y) from its LDS output tile (luma [r * 16 + c], chroma [256 + r * 16 +
+ * 2 c + comp]): lanes 0..7, one 8-byte write-through store each */
+__device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int y, const uint8_t *tile, int t)
+{
+	if (t < 8) {
+		unsigned long long v = 0;
+#pragma unroll
+		for (int i = 0; i < 8; ++i) {
+			int b;
+			if (t < 2) b = tile[15 * 16 + 8 * t + i];                                      /* luma bottom row */
+			else if (t < 4) b = tile[256 + 7 * 16 + 8 * (t - 2) + i];                      /* chroma bottom row */
+			else if (t < 6) b = tile[(8 * (t - 4) + i) * 16 + 15];                         /* luma right column */
+			else b = tile[256 + (4 * (t - 6) + (i >> 1)) * 16 + 14 + (i & 1)];            /* chroma right column */
+			v |= (unsigned long long)b << (8 * i);
+		}
+		st_sc1(hbp + ((size_t)y * rs + x) * HBP_BYTES + t * 8, v);
+	}
+}
+
+/*
+ * One intra / PCM MB of a P / B picture, inside an inter worker (all 256 lanes call): the unfiltered
+ * neighbours come from the neighbour records of the MBs around it (sc1 loads; their work items are
+ * done), the MB is reconstructed by intra_mb_body (wave 0 luma, wave 1 chroma) and written to the
+ * frame and to `tile`.
+ */
+__device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, const m2r_mb_t m, const int16_t *__restrict__ pool, uint8_t *cur,
+                            int W, int H, int Wmb, const uint8_t *hbp, int rs, IntraLDS *ctx, const IntraTables *tabs,
+                            uint8_t *tile)
+{
+	const int t = threadIdx.x;
+	const int nq = d_mb_ncoef(m);
+	for (int k = t; k < nq; k += blockDim.x) ctx->Q[0][k] = pool[m.coef + k];
+	if (t < 11) {
+		/* granule: 0,1 (x, y-1) luma bottom; 2 (x+1, y-1) luma bottom 0..7; 3 (x-1, y-1) luma bottom 8..15;
+		 * 4,5 (x-1, y) luma right; 6,7 (x, y-1) chroma bottom; 8 (x-1, y-1) chroma bottom 8..15;
+		 * 9,10 (x-1, y) chroma right */
+		const int nx = (t == 2) ? x + 1 : ((t == 3 || t == 4 || t == 5 || t >= 8) ? x - 1 : x);
+		const int ny = (t == 4 || t == 5 || t >= 9) ? y : y - 1;
+		const int off = (t == 0 || t == 2) ? 0 : (t == 1 || t == 3) ? 8 : (t == 4) ? 32 : (t == 5) ? 40
+		              : (t == 6) ? 16 : (t == 7 || t == 8) ? 24 : (t == 9) ? 48 : 56;
+		if (nx >= 0 && nx < Wmb && ny >= 0) {
+			const unsigned long long v = ld_sc1(hbp + ((size_t)ny * rs + nx) * HBP_BYTES + off);
+#pragma unroll
+			for (int i = 0; i < 8; ++i) {
+				const uint8_t b = (uint8_t)(v >> (8 * i));
+				if (t == 0) ctx->L[0][1 + i] = b;
+				else if (t == 1) ctx->L[0][9 + i] = b;
+				else if (t == 2) ctx->L[0][17 + i] = b;
+				else if (t == 3) { if (i == 7) ctx->L[0][0] = b; }
+				else if (t == 4) ctx->L[1 + i][0] = b;
+				else if (t == 5) ctx->L[9 + i][0] = b;
+				else if (t == 6) ctx->C[i & 1][0][1 + (i >> 1)] = b;
+				else if (t == 7) ctx->C[i & 1][0][5 + (i >> 1)] = b;
+				else if (t == 8) { if (i >= 6) ctx->C[i & 1][0][0] = b; }
+				else if (t == 9) ctx->C[i & 1][1 + (i >> 1)][0] = b;
+				else ctx->C[i & 1][5 + (i >> 1)][0] = b;
+			}
+		}
+	}
+	__syncthreads();
+	const int w = t >> 6;
+	if (w < 2) intra_mb_body(m, ctx->Q[0], t & 63, w == 0, w == 1, ctx, tabs);
+	__syncthreads();
+	{
+		const uint8_t v = ctx->L[1 + (t >> 4)][1 + (t & 15)];
+		tile[t] = v;
+		cur[(size_t)(y * 16 + (t >> 4)) * W + x * 16 + (t & 15)] = v;
+	}
+	if (t < 128) {
+		const int cy = t >> 4, bx = t & 15;
+		const uint8_t v = ctx->C[bx & 1][1 + cy][1 + (bx >> 1)];
+		tile[256 + t] = v;
+		cur[(size_t)W * H + (size_t)(y * 8 + cy) * W + x * 16 + bx] = v;
+	}
+}
+
+/*
+ * Inter MBs (and the intra MBs of P / B pictures) as a bounded persistent grid.  Work items are (MB
+ * row, 8-MB segment) in raster order, dequeued from a per-launch counter.  Before its MBs, an item
+ * waits until
+ *   - every reference picture it reads has its final samples in all the MB rows and columns its
+ *     motion vectors reach (rowflag[picture][row] = ROWFLAG(seq, columns final), raised by the
+ *     deblocking storer as it writes; the columns are rounded up to whole 128-byte lines, so no
+ *     partially final line is ever cached), and
+ *   - if it holds intra MBs, the items holding their left / upper neighbours are done (their
+ *     neighbour records are written; these items are earlier in the queue: no deadlock);
+ * all polled with sc1 loads, then ONE agent acquire.  A picture's MC follows its references'
+ * deblocking wavefront column by column, so consecutive anchor pictures overlap.  A finished item
+ * raises its done flag, which the picture's deblocking loader streams on.  The grid is kept small (a
+ * fraction of the CUs) so that spinning items can never keep the work they wait for off the device.
+ */
+__device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *smem)
+{
+	__shared__ int s_item, s_rmin, s_rmax, s_cmax, s_intra, s_rec;
+	__shared__ unsigned int s_refs[2];
+	const int t = threadIdx.x;
+	const int W = a.W, H = a.H, Wmb = a.Wmb, Hmb = a.Hmb;
+	const int nseg = NSEG(Wmb), nitems = Hmb * nseg, rs = nseg * 8;
+	int *queue = a.scratch + SCR_QUEUE(Hmb), *inter_cnt = a.scratch + SCR_INTER(Hmb), *segdone = a.scratch + SCR_SEG(Hmb);
+	const m2r_mb_t *__restrict__ mbs = a.mbs;
+	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
+	/* intra MBs of this picture: an LDS context, the prediction tables and an output tile */
+	IntraLDS *ictx = (IntraLDS *)smem;
+	IntraTables *tabs = (IntraTables *)(ictx + 1);
+	uint8_t *tile = (uint8_t *)(tabs + 1);
+	const bool recs = a.n_intra != 0;
+	if (recs) {
+		for (int i = t; i < 9 * 16; i += blockDim.x) tabs->p4[i >> 4][i & 15] = c_ipred4[i >> 4][i & 15];
+		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
+	}
+	/* Single-lane work in this loop is done by the whole of wave 0 under a SCALAR branch, the one
+	 * lane picked by value (atomic operand 0 on lanes 1..63).  An `if (t == 0)` here lets the
+	 * compiler thread lanes 1..63 of wave 0 straight back to the next barrier while lane 0 is still
+	 * dequeueing, which deadlocks the workgroup (seen on gfx950 with ROCm 7.2). */
+	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
+	int nst_dbg = 0;
+	for (;;) {
+		if (wave0) {
+			const int v = __hip_atomic_fetch_add((gi32 *)queue, t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			s_item = __builtin_amdgcn_readfirstlane(v);
+			s_rmin = 1 << 30;
+			s_rmax = -1;
+			s_cmax = 0;
+			s_intra = 0;
+			s_rec = 0;
+			s_refs[0] = s_refs[1] = 0;
+		}
+		__syncthreads();
+		const int item = __builtin_amdgcn_readfirstlane(s_item);
+		if (item >= nitems) break;
+		const int y = item / nseg, seg = item % nseg, x0 = seg * 8, x1 = min(x0 + 8, Wmb);
+		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
+		/* ---- vertical and rightward reach of this segment's motion into the references (8 lanes per MB;
+		 * luma 6-tap window; the chroma window never reaches further), and its intra MBs */
+		if (t < 64) {
+			const int mbi = x0 + (t >> 3);
+			int rmin = 1 << 30, rmax = -1, cmax = 0;
+			unsigned int r0 = 0, r1 = 0;
+			if (mbi < x1) {
+				const m2r_mb_t m = mbs[y * Wmb + mbi];
+				if (m.kind == M2R_MB_INTER) {
+					const m2r_inter_t &it = a.inters[m.inter];
+					for (int k = (t & 7) * 4; k < (t & 7) * 4 + 4; ++k) {
+						const int l = k >> 4, blk = k & 15;
+						const int sl = it.slot[l][(blk >> 3) * 2 + ((blk & 3) >> 1)];
+						if (sl < 0) continue;
+						const int py = y * 16 + (blk >> 2) * 4 + (it.mv[l][blk][1] >> 2);
+						const int top = py - 2, bot = py + 3 + 3;
+						rmin = min(rmin, top < 0 ? 0 : min(top >> 4, Hmb - 1));
+						rmax = max(rmax, bot < 0 ? 0 : min(bot >> 4, Hmb - 1));
+						const int right = mbi * 16 + (blk & 3) * 4 + (it.mv[l][blk][0] >> 2) + 3 + 3;
+						cmax = max(cmax, right < 0 ? 0 : min(right >> 4, Wmb - 1));
+						if (sl < 32) r0 |= 1u << sl;
+						else r1 |= 1u << (sl - 32);
+					}
+				} else if ((t & 7) == 0) {
+					/* bit 0: an intra MB; 1: one at x0 (left / top-left in the previous items); 2: one at
+					 * x1 - 1 (top-right in the next item of the row above) */
+					atomicOr(&s_intra, 1 | (mbi == x0 ? 2 : 0) | (mbi == x1 - 1 ? 4 : 0));
+				}
+				/* this MB's neighbour record is read by an intra MB (lane 1 of the MB) */
+				if (recs && (t & 7) == 1 && nb_needed(mbs, mbi, y, Wmb, Hmb)) atomicOr(&s_rec, 1 << (mbi - x0));
+			}
+			if (rmax >= 0) {
+				atomicMin(&s_rmin, rmin);
+				atomicMax(&s_rmax, rmax);
+				atomicMax(&s_cmax, cmax);
+				atomicOr(&s_refs[0], r0);
+				atomicOr(&s_refs[1], r1);
+			}
+		}
+		__syncthreads();
+		const int rmin_u = __builtin_amdgcn_readfirstlane(s_rmin), rmax_u = __builtin_amdgcn_readfirstlane(s_rmax);
+		const int intra_bits = __builtin_amdgcn_readfirstlane(s_intra);
+		const bool has_intra = intra_bits != 0;
+		const int rec_bits = __builtin_amdgcn_readfirstlane(s_rec);
+		if (rmax_u >= 0 && wave0) {
+			unsigned spins = 0;
+#ifndef M2DEC_NO_REFWAIT
+			if (rmax_u >= 0) {
+				/* rows rmin .. rmax final up to the reach: their own stores and the next row's (rows 13..15)
+				 * done.  Columns are whole 128-byte lines (8 MBs) when the stride allows, else whole rows:
+				 * a line cached while partly unfinal could outlive the acquire below */
+				const int rlast = min(rmax_u + 1, Hmb - 1);
+				const int cmax_u = __builtin_amdgcn_readfirstlane(s_cmax);
+				const int need = (W & 127) ? Wmb : min(Wmb, (cmax_u + 8) & ~7);
+				for (int k = 0; k < 2; ++k) {
+					unsigned int bits = __builtin_amdgcn_readfirstlane(s_refs[k]);
+					while (bits) {
+						const int sl = k * 32 + __builtin_ctz(bits);
+						bits &= bits - 1;
+						const int want = ss.s[sl];
+						if (want <= 0) continue;
+						/* entry (seq & 63) only ever grows: a later picture's value also means "final" */
+						const unsigned long long *fl = a.rowflag + (size_t)((want - 1) & 63) * Hmb;
+						const unsigned long long wv = ROWFLAG(want - 1, need);
+						for (int r0 = rmin_u; r0 <= rlast; r0 += 64) {
+							const int r = r0 + t;
+							for (;;) {
+								const bool ok = (r > rlast) ||
+								                __hip_atomic_load((gu64 *)&fl[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= wv;
+								if (__all(ok)) break;
+								if (!spin_ok(spins, a.err, 32)) break;
+							}
+						}
+					}
+				}
+			}
+#endif
+			/* ALWAYS acquire, even when every flag was already set: this XCD's L2 may hold lines of
+			 * rows 13..15 that the row's own deblock workgroup loaded before the row below filtered
+			 * and rewrote them from another XCD */
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		}
+		__syncthreads();
+		STAMPI(96 + (blockIdx.x & 63), 1, nst_dbg & 255, item);
+		/* inter MBs first (they never read this picture), then the intra MBs once the items holding their
+		 * left / top-left / top / top-right neighbours are done (neighbour records, sc1 loads: no acquire) */
+		for (int pass = 0; pass < (has_intra ? 2 : 1); ++pass) {
+			if (pass == 1 && wave0) {
+				unsigned spins = 0;
+				int dep = -1;
+				const bool want = (t == 1) || (t == 0 && (intra_bits & 2)) || (t == 2 && (intra_bits & 4));
+				if (t < 3 && want && y > 0 && seg - 1 + t >= 0 && seg - 1 + t < nseg) dep = (y - 1) * nseg + seg - 1 + t;
+				if (t == 3 && (intra_bits & 2) && seg > 0) dep = y * nseg + seg - 1;
+				for (;;) {
+					const bool ok = dep < 0 || __hip_atomic_load((gi32 *)&segdone[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+					if (__all(ok)) break;
+					if (!spin_ok(spins, a.err, 64)) break;
+				}
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the record loads below the poll */
+			}
+			if (pass == 1) __syncthreads();
+			for (int x = x0; x < x1; ++x) {
+				const m2r_mb_t m = mbs[y * Wmb + x];
+				const bool inter = __builtin_amdgcn_readfirstlane(m.kind) == M2R_MB_INTER;
+				if (inter != (pass == 0)) continue;
+				const bool rec = (rec_bits >> (x - x0)) & 1;
+				if (inter)
+					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr);
+				else
+					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, ictx, tabs, tile);
+				if (rec) {
+					__syncthreads();
+					write_nb_record(a.hbp, rs, x, y, tile, t);
+					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				}
+				__syncthreads();
+			}
+		}
+		/* segment done: every wave drained, then ONE agent release, the row's counter and the item's flag */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+		if (wave0) {
+			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__hip_atomic_fetch_add((gi32 *)&inter_cnt[y], t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_fetch_or((gi32 *)&segdone[item], t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+		STAMPI(96 + (blockIdx.x & 63), 2, nst_dbg & 255, item);
+		nst_dbg++;
+	}
+}
+
 /* ======================================================================== k_deblock */
 
 /*
@@ -1160,7 +1329,7 @@ __device__ __forceinline__ int dbk_done012(int c, int Wmb) { return c >= Wmb ? W
 
 __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur,
                              int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err,
-                             unsigned long long *rowflag, int seq)
+                             unsigned long long *rowflag, int seq, const int *segdone)
 {
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
 	const int nthr = blockDim.x;
@@ -1203,12 +1372,34 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		/* ---------------- loader: own samples run ahead as far as the ring allows (prep); only the
 		 * hand-off record of the row above A waits for that row (got) */
 		const int per = hasB ? 48 : 24; /* granules per MB: 16 luma + 8 chroma rows per row */
-		int prep = 0, got = 0, nld = 0;
+		int prep = 0, got = 0, nld = 0, ready = segdone ? 0 : Wmb;
 		unsigned spins = 0;
 		while (got < Wmb) {
 			const int ring = min(Wmb, __hip_atomic_load(&flags[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + DBK_RING);
-			if (prep < ring) {
-				const int ng = (ring - prep) * per;
+			if (prep < ring && ready < ring) {
+				/* P / B pictures: the MB columns of both rows whose work items are done (a prefix), then
+				 * one agent acquire before their samples are read */
+				const int nseg = NSEG(Wmb);
+				int nr = Wmb;
+				for (int r = 0; r < (hasB ? 2 : 1); ++r)
+					for (int s0 = ready >> 3; s0 < nseg; s0 += 64) {
+						const int sg = s0 + t;
+						const bool done = sg >= nseg || __hip_atomic_load((gi32 *)&segdone[(yA + r) * nseg + sg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+						const unsigned long long nd = __ballot(!done);
+						if (nd) {
+							nr = min(nr, (s0 + __builtin_ctzll(nd)) * 8);
+							break;
+						}
+					}
+				if (nr > ready) {
+					ready = nr;
+					__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				}
+			}
+			const int target = min(ring, ready);
+			if (prep < target) {
+				const int ng = (target - prep) * per;
 				for (int g0 = 0; g0 < ng; g0 += 64) {
 					const int g = g0 + t;
 					if (g < ng) {
@@ -1220,7 +1411,7 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 						else *(uint4 *)(RC + (2 + 8 * r + kk - 16) * S + col) = *(const uint4 *)(chroma + (size_t)(yc0 + kk - 16) * W + mb * 16);
 					}
 				}
-				prep = ring;
+				prep = target;
 				if (yA == 0) {
 					got = prep;
 					if (t == 0) __hip_atomic_store(&flags[0], got, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1554,8 +1745,7 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
 	if (b < a.inter_workers) {
 		if (a.n_inter)
-			inter_worker(a.mbs, a.inters, a.slices, a.pool, a.frames, a.fsz, a.W, a.H, a.Wmb, a.Hmb, a.slot, a.ss, a.rowflag,
-			             a.scratch + SCR_QUEUE(a.Hmb), a.scratch + SCR_INTER(a.Hmb), a.err);
+			inter_worker(a, a.ss, smem);
 		if (a.fin) {
 			/* every reference read of this worker has returned (its values were consumed) */
 			__syncthreads();
@@ -1568,44 +1758,16 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	const int yA = 2 * (b - a.inter_workers);
 	const bool hasB = yA + 1 < a.Hmb;
 	const int nrows = hasB ? 2 : 1;
-	const int Wmb = a.Wmb, nseg = (Wmb + 7) >> 3;
+	const int Wmb = a.Wmb;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
-	uint8_t *chroma = cur + (size_t)a.W * a.H;
-	int *inter_cnt = a.scratch + SCR_INTER(a.Hmb);
 	int *hbi_ready = a.scratch + SCR_HBIRDY(a.Hmb);
 	STAMP(yA, 3, 0, 1);
-	/* ---- phase A.1: these rows' inter MBs are all stored (inter workers of this launch) */
-	if (a.n_inter) {
-		if (t == 0) {
-			unsigned spins = 0;
-			for (int r = 0; r < nrows; ++r)
-				while (__hip_atomic_load((gi32 *)&inter_cnt[yA + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nseg)
-					if (!spin_ok(spins, a.err, 64)) break;
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-		}
-		__syncthreads();
-	}
-	STAMP(yA, 3, 1, 2);
-	/* ---- phase A.2: unfiltered bottom rows of the inter MBs -> hand-off records (intra neighbours) */
-	for (int r = 0; r < nrows; ++r) {
-		const int y = yA + r;
-		if (y + 1 >= a.Hmb) break;
-		for (int k = t; k < Wmb * 4; k += blockDim.x) {
-			const int x = k >> 2, g = k & 3;
-			if (a.mbs[y * Wmb + x].kind != M2R_MB_INTER) continue;
-			const uint8_t *src = (g < 2) ? cur + (size_t)(y * 16 + 15) * a.W + x * 16 + (g & 1) * 8
-			                             : chroma + (size_t)(y * 8 + 7) * a.W + x * 16 + (g & 1) * 8;
-			st_sc1(a.hbi + ((size_t)y * Wmb + x) * HBI_BYTES + g * 8, *(const unsigned long long *)src);
-		}
-	}
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-	__syncthreads();
-	if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-	STAMP(yA, 3, 2, 3);
-	/* ---- phase A.3: intra / PCM MBs: luma of rows A / B on waves 0 / 1, their chroma on waves 2 / 3,
-	 * each wave with its own LDS context */
-	if (a.n_intra) {
+	if (!a.n_inter) {
+		/* ---- I picture, phase A: intra / PCM MBs as a wavefront over the row workgroups: luma of rows A / B
+		 * on waves 0 / 1, their chroma on waves 2 / 3, each wave with its own LDS context.  (P / B pictures:
+		 * the inter workers reconstruct every MB, intra ones included, and the deblocking below streams
+		 * on their per-item done flags.) */
+		if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		IntraTables *tabs = (IntraTables *)((IntraLDS *)smem + 4);
 		for (int i = t; i < 9 * 16; i += blockDim.x) tabs->p4[i >> 4][i & 15] = c_ipred4[i >> 4][i & 15];
 		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
@@ -1627,7 +1789,8 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 	STAMP(yA, 3, 3, 4);
 	/* ---- phase B: deblocking (always: it also publishes the row flags) */
-	deblock_pair(yA, hasB, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq);
+	deblock_pair(yA, hasB, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq,
+	             a.n_inter ? a.scratch + SCR_SEG(a.Hmb) : nullptr);
 	STAMP(yA, 3, 4, 5);
 	if (a.fin) {
 		/* the storer drained and released every frame store before its row flags */
@@ -1672,7 +1835,8 @@ size_t m2r_deblock_lds_bytes(int W, int Wmb)
 	(void)W;
 	const size_t dbk = (size_t)54 * DBK_RW + 3 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
 	const size_t intra = 4 * sizeof(IntraLDS) + sizeof(IntraTables);
-	return dbk > intra ? dbk : intra;
+	const size_t worker = sizeof(IntraLDS) + sizeof(IntraTables) + 384;
+	return std::max(dbk, std::max(intra, worker));
 }
 
 extern "C" int m2dec_amd_debug_stamps(unsigned long long *out, size_t n)

@@ -33,7 +33,14 @@ struct SlotSeq {
 #define SCR_INTER(Hmb) (3 * (Hmb))
 #define SCR_HBIRDY(Hmb) (4 * (Hmb))
 #define SCR_QUEUE(Hmb) (5 * (Hmb))
-#define SCR_WORDS(Hmb) ((5 * (Hmb) + 4 + 3) & ~3)
+/* then one done flag per inter work item (MB row y, 8-MB segment s) at SCR_SEG + y * nseg + s */
+#define SCR_SEG(Hmb) (5 * (Hmb) + 4)
+#define NSEG(Wmb) (((Wmb) + 7) >> 3)
+#define SCR_WORDS(Hmb, Wmb) ((5 * (Hmb) + 4 + (Hmb) * NSEG(Wmb) + 3) & ~3)
+/* P/B pictures: neighbour records of the MBs an intra MB reads (written by the inter workers):
+ * bottom luma row, bottom chroma row (CbCr), right luma column, right chroma column (CbCr pairs);
+ * row stride NSEG * 8 MBs so that no 128-byte line holds records of two work items */
+#define HBP_BYTES 64
 
 struct PictureArgs {
 	const m2r_mb_t *mbs;
@@ -48,6 +55,7 @@ struct PictureArgs {
 	int inter_workers;
 	int *scratch;     /* SCR_* words of this launch */
 	uint8_t *hbi, *hbd; /* hand-off records of this launch's stream */
+	uint8_t *hbp;       /* [Hmb][NSEG * 8] HBP_BYTES neighbour records (P/B pictures) */
 	unsigned long long *rowflag; /* [64][Hmb] column progress of picture rows: ROWFLAG(seq, c) once MB
 	                               columns 0 .. c-1 of the row are final (entry seq & 63) */
 	int *err;

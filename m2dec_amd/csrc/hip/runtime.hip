@@ -58,7 +58,7 @@ struct Sched {
 	size_t fsz = 0;
 	uint8_t *frames = nullptr; /* device frame pool [nslots] x fsz */
 	hipStream_t st[NSTREAMS] = {}; /* per in-flight index: uploads, k_picture, downloads */
-	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb)] per-launch scratch words */
+	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb, Wmb)] per-launch scratch words */
 	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
 	int *err = nullptr;
 	unsigned long long *rowflag = nullptr; /* [64][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
@@ -121,7 +121,7 @@ struct Sched {
 		Hmb = height / 16;
 		fsz = nfsz;
 		if (!prog) {
-			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb) * NSTREAMS));
+			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS));
 			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
 			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * 64 * (size_t)Hmb));
 		}
@@ -140,7 +140,7 @@ struct Sched {
 		return 0;
 	}
 
-	size_t hand_bytes() const { return (size_t)Hmb * Wmb * (HBI_BYTES + HBD_BYTES); }
+	size_t hand_bytes() const { return (size_t)Hmb * Wmb * (HBI_BYTES + HBD_BYTES) + (size_t)Hmb * NSEG(Wmb) * 8 * HBP_BYTES; }
 
 	hipEvent_t next_event()
 	{
@@ -190,13 +190,14 @@ struct Sched {
 		a.n_inter = j.n_inter;
 		a.n_intra = j.n_intra;
 		a.inter_workers = inter_grid;
-		a.scratch = prog + (size_t)k * SCR_WORDS(Hmb);
+		a.scratch = prog + (size_t)k * SCR_WORDS(Hmb, Wmb);
 		a.hbi = hand + (size_t)k * hand_bytes();
 		a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+		a.hbp = a.hbd + (size_t)Hmb * Wmb * HBD_BYTES;
 		a.rowflag = rowflag;
 		a.err = err;
 		a.ss = slot_seq;
-		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb), s));
+		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb, Wmb), s));
 		hipLaunchKernelGGL(k_picture, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, a);
 		CHECK(hipGetLastError());
 		tm.inter_launches += j.n_inter ? 1 : 0;
@@ -225,7 +226,7 @@ struct Sched {
 	{
 		if (cap <= bt.cap) return 0;
 		batch_free();
-		CHECK(hipMalloc(&bt.words, sizeof(int) * ((size_t)2 * cap + (size_t)cap * SCR_WORDS(Hmb))));
+		CHECK(hipMalloc(&bt.words, sizeof(int) * ((size_t)2 * cap + (size_t)cap * SCR_WORDS(Hmb, Wmb))));
 		CHECK(hipMalloc(&bt.hand, hand_bytes() * (size_t)cap));
 		for (int i = 0; i < Batch::NB; ++i) {
 			CHECK(hipMalloc(&bt.d_args[i], sizeof(PictureArgs) * cap));
@@ -321,9 +322,10 @@ struct Sched {
 			a.n_inter = j.n_inter;
 			a.n_intra = j.n_intra;
 			a.inter_workers = inter_grid;
-			a.scratch = bt.words + 2 * (size_t)bt.cap + (size_t)p * SCR_WORDS(Hmb);
+			a.scratch = bt.words + 2 * (size_t)bt.cap + (size_t)p * SCR_WORDS(Hmb, Wmb);
 			a.hbi = bt.hand + (size_t)p * hand_bytes();
 			a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+			a.hbp = a.hbd + (size_t)Hmb * Wmb * HBD_BYTES;
 			a.rowflag = rowflag;
 			a.err = err;
 			a.ss = slot_seq;
@@ -347,7 +349,7 @@ struct Sched {
 		if (!taken) return -1;
 		hoist_intra(ha, taken);
 		CHECK(hipMemcpyAsync(bt.d_args[idx], ha, sizeof(PictureArgs) * taken, hipMemcpyHostToDevice, s));
-		CHECK(hipMemsetAsync(bt.words, 0, sizeof(int) * (2 * (size_t)bt.cap + (size_t)taken * SCR_WORDS(Hmb)), s));
+		CHECK(hipMemsetAsync(bt.words, 0, sizeof(int) * (2 * (size_t)bt.cap + (size_t)taken * SCR_WORDS(Hmb, Wmb)), s));
 		const int bpp = picture_blocks(inter_grid, Hmb);
 		hipLaunchKernelGGL(k_batch, dim3(bpp * taken), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, (const PictureArgs *)bt.d_args[idx], bpp);
 		CHECK(hipGetLastError());
@@ -923,11 +925,11 @@ extern "C" int m2dec_amd_hip_replay_debug_scratch(m2dec_amd_hip_replay_t *r, int
 {
 	if (!r) return -1;
 	Sched &sc = r->sc;
-	int need = SCR_WORDS(sc.Hmb) * NSTREAMS + 1;
+	int need = SCR_WORDS(sc.Hmb, sc.Wmb) * NSTREAMS + 1;
 	if (n < need) return -1;
 	hipStream_t s;
 	CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-	CHECK(hipMemcpyAsync(out, sc.prog, sizeof(int) * SCR_WORDS(sc.Hmb) * NSTREAMS, hipMemcpyDeviceToHost, s));
+	CHECK(hipMemcpyAsync(out, sc.prog, sizeof(int) * SCR_WORDS(sc.Hmb, sc.Wmb) * NSTREAMS, hipMemcpyDeviceToHost, s));
 	CHECK(hipMemcpyAsync(out + need - 1, sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
 	CHECK(hipStreamSynchronize(s));
 	CHECK(hipStreamDestroy(s));

@@ -1738,24 +1738,13 @@ __device__ void war_wait(const PictureArgs &a)
 	__syncthreads();
 }
 
-/* block b of one picture (k_picture: b = blockIdx.x; k_batch: the picture's own block index) */
-__device__ __forceinline__ void picture_block(const PictureArgs &a, const int b, uint8_t *smem)
+/* one pair of MB rows (yA, yA + 1) by the whole workgroup: the I-picture intra wavefront (phase A),
+ * then deblocking (phase B), then the picture's row-pair counter (and the verification copy-out) */
+__device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict__ ap, const int yA, uint8_t *smem)
 {
-	if (b == 0 && threadIdx.x == 0) STAMPP(a.didx, 0);
-	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
-	if (b < a.inter_workers) {
-		if (a.n_inter)
-			inter_worker(a, a.ss, smem);
-		if (a.fin) {
-			/* every reference read of this worker has returned (its values were consumed) */
-			__syncthreads();
-			if (threadIdx.x == 0 && __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.inter_workers - 1)
-				STAMPP(a.didx, 1);
-		}
-		return;
-	}
+	const PictureArgs &a = *ap;
 	const int t = threadIdx.x;
-	const int yA = 2 * (b - a.inter_workers);
+	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
 	const bool hasB = yA + 1 < a.Hmb;
 	const int nrows = hasB ? 2 : 1;
 	const int Wmb = a.Wmb;
@@ -1796,10 +1785,11 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 		/* the storer drained and released every frame store before its row flags */
 		__shared__ int s_last;
 		__syncthreads();
-		if (t == 0) {
-			const int prev = __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+		if (wave0) { /* scalar branch, the lane picked by value (this may run inside a loop) */
+			const int prev = __builtin_amdgcn_readfirstlane(
+			    __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], t == 0 ? 1 : 0, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT));
 			s_last = a.capture && prev == (a.Hmb + 1) / 2 - 1;
-			if (prev == (a.Hmb + 1) / 2 - 1) STAMPP(a.didx, 2);
+			if (t == 0 && prev == (a.Hmb + 1) / 2 - 1) STAMPP(a.didx, 2);
 		}
 		__syncthreads();
 		if (s_last) {
@@ -1812,15 +1802,51 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 			for (size_t i = t; i < n16; i += blockDim.x) dst[i] = src[i];
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 			__syncthreads();
-			if (t == 0) __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+			if (wave0) __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx + 1], t == 0 ? 1 : 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 }
 
-__global__ __launch_bounds__(256, 3) void k_picture(PictureArgs a)
+/* block b of one picture (the picture's own block index in k_batch) */
+__device__ __forceinline__ void picture_block(const PictureArgs &a, const int b, uint8_t *smem)
 {
-	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-	picture_block(a, blockIdx.x, smem);
+	if (b == 0 && threadIdx.x == 0) STAMPP(a.didx, 0);
+	if (a.fin && (a.n_war || a.war_writer >= 0)) war_wait(a);
+	if (b < a.inter_workers) {
+		if (a.n_inter)
+			inter_worker(a, a.ss, smem);
+		if (a.fin) {
+			/* every reference read of this worker has returned (its values were consumed) */
+			__syncthreads();
+			if (threadIdx.x == 0 && __hip_atomic_fetch_add((gi32 *)&a.fin[2 * a.pidx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.inter_workers - 1)
+				STAMPP(a.didx, 1);
+		}
+		return;
+	}
+	/* I picture: one workgroup per pair of rows (the intra wavefront needs them all resident).
+	 * P / B picture: a.row_wgs workgroups take the row pairs in order from a queue (a pair's deblocking
+	 * waits only for the pair above, taken earlier: no deadlock); the other row blocks leave at once.
+	 * (One call site of row_pair: it is large.) */
+	const int r = b - a.inter_workers;
+	const bool queued = a.n_inter != 0;
+	if (queued && r >= a.row_wgs) return;
+	__shared__ int s_pair;
+	const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
+	int *pq = a.scratch + SCR_QUEUE(a.Hmb) + 1;
+	for (int k = 0;; ++k) {
+		int pair = r;
+		if (queued) {
+			__syncthreads();
+			if (wave0) s_pair = __builtin_amdgcn_readfirstlane(
+			               __hip_atomic_fetch_add((gi32 *)pq, threadIdx.x == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+			__syncthreads();
+			pair = __builtin_amdgcn_readfirstlane(s_pair);
+		} else if (k) {
+			break;
+		}
+		if (pair >= (a.Hmb + 1) / 2) break;
+		row_pair(&a, 2 * pair, smem);
+	}
 }
 
 __global__ __launch_bounds__(256, 3) void k_batch(const PictureArgs *pics, int bpp)

@@ -53,6 +53,7 @@ struct PictureArgs {
 	int W, H, Wmb, Hmb;
 	int slot, seq, n_inter, n_intra;
 	int inter_workers;
+	int row_wgs;      /* P / B pictures: row-pair workgroups (taking pairs from a queue) */
 	int *scratch;     /* SCR_* words of this launch */
 	uint8_t *hbi, *hbd; /* hand-off records of this launch's stream */
 	uint8_t *hbp;       /* [Hmb][NSEG * 8] HBP_BYTES neighbour records (P/B pictures) */
@@ -70,7 +71,6 @@ struct PictureArgs {
 	uint8_t *capture; /* verification only: the finished frame is copied here before the slot is released */
 };
 
-__global__ void k_picture(PictureArgs a); /* grid: picture_blocks(Hmb), dynamic LDS m2r_deblock_lds_bytes */
 /* a batch of pictures in decode order, picture p owning blocks [p * bpp, (p + 1) * bpp) */
 __global__ void k_batch(const PictureArgs *pics, int bpp);
 

@@ -59,12 +59,14 @@ struct Sched {
 	uint8_t *frames = nullptr; /* device frame pool [nslots] x fsz */
 	hipStream_t st[NSTREAMS] = {}; /* per in-flight index: uploads, k_picture, downloads */
 	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb, Wmb)] per-launch scratch words */
+	PictureArgs *pargs = nullptr; /* [NSTREAMS] kernel arguments of the per-picture launches */
 	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
 	int *err = nullptr;
 	unsigned long long *rowflag = nullptr; /* [64][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
 	int seq = 0;               /* pictures launched */
 	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
 	int inter_grid = 64;       /* persistent inter workers per picture (a quarter of the CUs) */
+	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
@@ -88,6 +90,8 @@ struct Sched {
 			inter_grid = cus / 4;
 		if (const char *g = getenv("M2DEC_AMD_INTER_WG")) /* tuning knob: inter workers per picture */
 			if (atoi(g) > 0) inter_grid = atoi(g);
+		if (const char *g = getenv("M2DEC_AMD_ROW_WG")) /* tuning knob: row-pair workgroups of a P / B picture */
+			if (atoi(g) > 0) row_wgs = atoi(g);
 		return 0;
 	}
 
@@ -122,6 +126,7 @@ struct Sched {
 		fsz = nfsz;
 		if (!prog) {
 			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS));
+			if (!pargs) CHECK(hipMalloc(&pargs, sizeof(PictureArgs) * NSTREAMS));
 			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
 			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * 64 * (size_t)Hmb));
 		}
@@ -134,7 +139,7 @@ struct Sched {
 		}
 		size_t lds = m2r_deblock_lds_bytes(W, Wmb);
 		if (lds > 65536 && lds > lds_set) {
-			CHECK(hipFuncSetAttribute((const void *)k_picture, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+			CHECK(hipFuncSetAttribute((const void *)k_batch, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 			lds_set = lds;
 		}
 		return 0;
@@ -167,7 +172,7 @@ struct Sched {
 		return k;
 	}
 
-	/* one k_picture launch on stream k; tev (optional): [0] recorded after it; inter_done: the event
+	/* one picture = one k_batch launch of one picture on stream k; tev (optional): [0] recorded after it; inter_done: the event
 	 * after which the picture's reference reads are over */
 	int launch(int k, const PicJob &j, hipEvent_t *tev, hipEvent_t *inter_done)
 	{
@@ -190,6 +195,7 @@ struct Sched {
 		a.n_inter = j.n_inter;
 		a.n_intra = j.n_intra;
 		a.inter_workers = inter_grid;
+		a.row_wgs = row_wgs;
 		a.scratch = prog + (size_t)k * SCR_WORDS(Hmb, Wmb);
 		a.hbi = hand + (size_t)k * hand_bytes();
 		a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
@@ -198,7 +204,11 @@ struct Sched {
 		a.err = err;
 		a.ss = slot_seq;
 		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb, Wmb), s));
-		hipLaunchKernelGGL(k_picture, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s, a);
+		/* the arguments go to device memory (pageable source: staged by the copy call) so that the kernel
+		 * reads them through a pointer, as in batch launches */
+		CHECK(hipMemcpyAsync(pargs + k, &a, sizeof(a), hipMemcpyHostToDevice, s));
+		hipLaunchKernelGGL(k_batch, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
+		                   (const PictureArgs *)(pargs + k), picture_blocks(inter_grid, Hmb));
 		CHECK(hipGetLastError());
 		tm.inter_launches += j.n_inter ? 1 : 0;
 		tm.intra_launches += j.n_intra ? 1 : 0;
@@ -322,6 +332,8 @@ struct Sched {
 			a.n_inter = j.n_inter;
 			a.n_intra = j.n_intra;
 			a.inter_workers = inter_grid;
+			a.row_wgs = row_wgs;
+		a.row_wgs = row_wgs;
 			a.scratch = bt.words + 2 * (size_t)bt.cap + (size_t)p * SCR_WORDS(Hmb, Wmb);
 			a.hbi = bt.hand + (size_t)p * hand_bytes();
 			a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
@@ -399,6 +411,7 @@ struct Sched {
 			if (e) (void)hipEventDestroy(e);
 		if (frames) (void)hipFree(frames);
 		if (prog) (void)hipFree(prog);
+		if (pargs) (void)hipFree(pargs);
 		if (hand) (void)hipFree(hand);
 		if (err) (void)hipFree(err);
 		if (rowflag) (void)hipFree(rowflag);

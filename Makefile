@@ -36,7 +36,7 @@ build/hip/%.o: m2dec_amd/csrc/hip/%.hip $(HIP_HDR) $(wildcard include/*.h)
 
 $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libm2dec_amd.so -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libm2dec_amd.so -Wl,--no-undefined -lpthread
 
 $(ORACLE): oracle/recon_oracle.c include/m2d_recon.h include/m2d.h
 	@mkdir -p $(dir $@)

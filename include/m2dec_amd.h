@@ -69,6 +69,16 @@ int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t
 /* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
 
+/* Throughput drivers over the same decode loop as m2dec_amd_decode_stream (h264dec -O): the HIP back
+ * end on `device`, one MD5 line (35 bytes) per output frame into md5s (at most `max`), the MD5s on a
+ * helper thread.  Returns the number of frames delivered or < 0. */
+int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max,
+                                m2dec_amd_stats_t *stats);
+/* n independent streams decoded concurrently on one device, one host thread and decoder context per
+ * stream; frames[i] = frames delivered by stream i (or < 0).  Returns 0 if every stream succeeded. */
+int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_t *lens, int device,
+                                 char *const *md5s, const int *max, int *frames);
+
 /* ---- record traces (m2dec_amd/csrc/host/trace.c): a stream parsed once, records kept in memory */
 typedef struct m2dec_amd_trace m2dec_amd_trace_t;
 typedef struct {

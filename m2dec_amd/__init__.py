@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("M2DEC_AMD_LIB") or os.path.join(_HERE, "lib", "libm2d
 
 __all__ = [
     "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",
-    "decode_stream", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
+    "decode_stream", "decode_stream_md5", "decode_streams", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
 ]
 
 
@@ -94,6 +94,14 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
         L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
         L.m2dec_amd_frame_md5.restype = None
+        L.m2dec_amd_decode_stream_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_char_p,
+                                                  ctypes.c_int, ctypes.POINTER(Stats)]
+        L.m2dec_amd_decode_stream_md5.restype = ctypes.c_int
+        L.m2dec_amd_decode_streams_md5.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                                   ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                                   ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
+                                                   ctypes.POINTER(ctypes.c_int)]
+        L.m2dec_amd_decode_streams_md5.restype = ctypes.c_int
         vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
         L.m2dec_amd_trace_capture.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]
         L.m2dec_amd_trace_capture.restype = ctypes.c_int
@@ -211,6 +219,51 @@ def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 
     if n < 0:
         raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
     return md5s
+
+
+def _max_frames(data: bytes) -> int:
+    """Upper bound on output frames: one per slice NAL start code (never fewer than pictures)."""
+    return max(1, data.count(b"\x00\x00\x01"))
+
+
+def decode_stream_md5(data: bytes, device: int = 0) -> List[str]:
+    """The HIP decode path exactly like ``h264dec -O`` with the MD5s computed in C on a helper thread
+    (m2dec_amd_decode_stream_md5): the throughput form of ``decode_stream``."""
+    L = lib()
+    if not L.m2dec_amd_hip_available():
+        raise RuntimeError("m2dec_amd: no usable gfx950 device for the HIP back end")
+    cap = _max_frames(data)
+    buf = ctypes.create_string_buffer(35 * cap)
+    st = Stats()
+    n = L.m2dec_amd_decode_stream_md5(data, len(data), device, buf, cap, ctypes.byref(st))
+    if n < 0:
+        raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
+    raw = buf.raw
+    return [raw[35 * i:35 * i + 32].decode() for i in range(min(n, cap))]
+
+
+def decode_streams(datas: List[bytes], device: int = 0) -> List[List[str]]:
+    """Independent streams decoded concurrently on one device, one host thread and decoder context
+    each (m2dec_amd_decode_streams_md5); per-stream MD5 lists."""
+    L = lib()
+    if not L.m2dec_amd_hip_available():
+        raise RuntimeError("m2dec_amd: no usable gfx950 device for the HIP back end")
+    n = len(datas)
+    caps = [_max_frames(d) for d in datas]
+    bufs = [ctypes.create_string_buffer(35 * c) for c in caps]
+    arr_d = (ctypes.c_char_p * n)(*datas)
+    arr_l = (ctypes.c_size_t * n)(*[len(d) for d in datas])
+    arr_m = (ctypes.c_char_p * n)(*[ctypes.cast(b, ctypes.c_char_p) for b in bufs])
+    arr_c = (ctypes.c_int * n)(*caps)
+    frames = (ctypes.c_int * n)()
+    r = L.m2dec_amd_decode_streams_md5(n, arr_d, arr_l, device, arr_m, arr_c, frames)
+    if r < 0:
+        raise RuntimeError(f"m2dec_amd: multi-stream decode failed (frames {list(frames)})")
+    out = []
+    for i in range(n):
+        raw = bufs[i].raw
+        out.append([raw[35 * k:35 * k + 32].decode() for k in range(min(frames[i], caps[i]))])
+    return out
 
 
 class H264Decoder:

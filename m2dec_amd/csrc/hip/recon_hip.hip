@@ -1549,7 +1549,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 						const int a1 = (p2 + p1 + p0 + q0 + 2) >> 2, a2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
 						const int c0_ = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, e0_ = (2 * q1 + q0 + p1 + 2) >> 2;
 						const int c1 = (p0 + q0 + q1 + q2 + 2) >> 2, c2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-						const bool strong = bs == 4;
+						/* bS 4 only on the MB edge (e == 0, unrolled): the inner edges skip the strong filter */
+						const bool strong = (e == 0) && bs == 4;
 						const int np0 = d_sel(strong, d_sel(sp, a0, b0), w0), nq0 = d_sel(strong, d_sel(sq, c0_, e0_), w1);
 						const int np1 = d_sel(strong, d_sel(sp, a1, p1), d_sel(luma & ap, wp1, p1));
 						const int nq1 = d_sel(strong, d_sel(sq, c1, q1), d_sel(luma & aq, wq1, q1));

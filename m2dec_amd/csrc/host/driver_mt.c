@@ -1,0 +1,175 @@
+/*
+ * Throughput drivers over the unchanged h264d_func decode path (the same loop as h264dec -O,
+ * h264dec.cpp:251-257 + m2decoder.h:132-157, see m2dec_amd_decode_stream2):
+ *
+ *   m2dec_amd_decode_stream_md5   one stream; every output frame is copied out of the caller's frame
+ *                                 buffer and its FileWriterMd5 line (filewrite.h:99-124) computed on a
+ *                                 helper thread, so MD5 overlaps the parse of the next pictures;
+ *   m2dec_amd_decode_streams_md5  n independent streams, one host thread (and one decoder context)
+ *                                 each, sharing one GPU — the within-GPU form of SURVEY.md §8e's
+ *                                 stream sharding.
+ *
+ * Decoder contexts are independent (all state in the context, const global tables), as in the
+ * reference (h264.h:435-446), so the threads share nothing but the device.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include "h264_dec.h"
+#include "m2dec_amd.h"
+
+#define MD5_RING 4
+
+typedef struct {
+	pthread_mutex_t mu;
+	pthread_cond_t cv_job, cv_free;
+	uint8_t *buf[MD5_RING];
+	size_t cap;
+	m2d_frame_t frm[MD5_RING];
+	int idx[MD5_RING];       /* output frame number of the job in slot k */
+	int head, tail;          /* jobs [tail, head) pending, modulo MD5_RING */
+	int quit;
+	char *md5s;
+	int max;
+	int n;                   /* frames delivered */
+	int failed;
+} md5_pipe_t;
+
+static void *md5_worker(void *arg)
+{
+	md5_pipe_t *p = (md5_pipe_t *)arg;
+	pthread_mutex_lock(&p->mu);
+	for (;;) {
+		while (p->tail == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
+		if (p->tail == p->head && p->quit) break;
+		const int k = p->tail % MD5_RING;
+		m2d_frame_t f = p->frm[k];
+		const int i = p->idx[k];
+		pthread_mutex_unlock(&p->mu);
+		char line[35];
+		m2dec_amd_frame_md5(&f, line);
+		if (i < p->max) memcpy(p->md5s + (size_t)i * 35, line, 35);
+		pthread_mutex_lock(&p->mu);
+		p->tail++;
+		pthread_cond_signal(&p->cv_free);
+	}
+	pthread_mutex_unlock(&p->mu);
+	return NULL;
+}
+
+/* on_frame of the stream driver: copy the frame into the next free ring slot, queue its MD5 */
+static void md5_on_frame(void *arg, const m2d_frame_t *f)
+{
+	md5_pipe_t *p = (md5_pipe_t *)arg;
+	const size_t luma = (size_t)f->width * (size_t)f->height, bytes = luma * 3 / 2;
+	pthread_mutex_lock(&p->mu);
+	while (p->head - p->tail >= MD5_RING) pthread_cond_wait(&p->cv_free, &p->mu);
+	const int k = p->head % MD5_RING;
+	pthread_mutex_unlock(&p->mu);
+	if (bytes > p->cap) {
+		/* (re)size the ring once no job holds a buffer; only this thread allocates */
+		pthread_mutex_lock(&p->mu);
+		while (p->head != p->tail) pthread_cond_wait(&p->cv_free, &p->mu);
+		pthread_mutex_unlock(&p->mu);
+		for (int j = 0; j < MD5_RING; ++j) {
+			free(p->buf[j]);
+			p->buf[j] = (uint8_t *)malloc(bytes);
+			if (!p->buf[j]) {
+				p->failed = 1;
+				p->cap = 0;
+				return;
+			}
+		}
+		p->cap = bytes;
+	}
+	memcpy(p->buf[k], f->luma, luma);
+	memcpy(p->buf[k] + luma, f->chroma, luma / 2);
+	m2d_frame_t c = *f;
+	c.luma = p->buf[k];
+	c.chroma = p->buf[k] + luma;
+	pthread_mutex_lock(&p->mu);
+	p->frm[k] = c;
+	p->idx[k] = p->n++;
+	p->head++;
+	pthread_cond_signal(&p->cv_job);
+	pthread_mutex_unlock(&p->mu);
+}
+
+int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max, m2dec_amd_stats_t *stats)
+{
+	md5_pipe_t p;
+	pthread_t th;
+	int r;
+	memset(&p, 0, sizeof(p));
+	pthread_mutex_init(&p.mu, NULL);
+	pthread_cond_init(&p.cv_job, NULL);
+	pthread_cond_init(&p.cv_free, NULL);
+	p.md5s = md5s;
+	p.max = max;
+	if (pthread_create(&th, NULL, md5_worker, &p) != 0) return -1;
+	r = m2dec_amd_decode_stream2(data, len, NULL, device, -1, md5_on_frame, &p, stats);
+	pthread_mutex_lock(&p.mu);
+	p.quit = 1;
+	pthread_cond_signal(&p.cv_job);
+	pthread_mutex_unlock(&p.mu);
+	pthread_join(th, NULL);
+	for (int j = 0; j < MD5_RING; ++j) free(p.buf[j]);
+	pthread_mutex_destroy(&p.mu);
+	pthread_cond_destroy(&p.cv_job);
+	pthread_cond_destroy(&p.cv_free);
+	if (p.failed) return -1;
+	return r < 0 ? r : p.n;
+}
+
+typedef struct {
+	const uint8_t *data;
+	size_t len;
+	int device;
+	char *md5s;
+	int max;
+	int result;
+} stream_job_t;
+
+static void *stream_worker(void *arg)
+{
+	stream_job_t *j = (stream_job_t *)arg;
+	j->result = m2dec_amd_decode_stream_md5(j->data, j->len, j->device, j->md5s, j->max, NULL);
+	return NULL;
+}
+
+int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_t *lens, int device, char *const *md5s,
+                                 const int *max, int *frames)
+{
+	stream_job_t *jobs;
+	pthread_t *th;
+	int ok = 0;
+	if (n <= 0) return -1;
+	jobs = (stream_job_t *)calloc((size_t)n, sizeof(*jobs));
+	th = (pthread_t *)calloc((size_t)n, sizeof(*th));
+	if (!jobs || !th) {
+		free(jobs);
+		free(th);
+		return -1;
+	}
+	for (int i = 0; i < n; ++i) {
+		jobs[i].data = datas[i];
+		jobs[i].len = lens[i];
+		jobs[i].device = device;
+		jobs[i].md5s = md5s[i];
+		jobs[i].max = max[i];
+		jobs[i].result = -1;
+		if (pthread_create(&th[i], NULL, stream_worker, &jobs[i]) != 0) {
+			n = i;
+			ok = -1;
+			break;
+		}
+	}
+	for (int i = 0; i < n; ++i) {
+		pthread_join(th[i], NULL);
+		if (frames) frames[i] = jobs[i].result;
+		if (jobs[i].result < 0) ok = -1;
+	}
+	free(jobs);
+	free(th);
+	return ok;
+}

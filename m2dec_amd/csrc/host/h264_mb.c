@@ -9,6 +9,7 @@
  * operation is deferred to the back end through the records.
  */
 #include <stdio.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include "h264_dec.h"
 
@@ -140,7 +141,7 @@ typedef struct {
 } vlc_lut_t;
 
 static vlc_lut_t ct_lut[5], tz_lut[16], rb_lut[8];
-static int vlc_ready;
+static pthread_once_t vlc_once = PTHREAD_ONCE_INIT; /* decoder contexts may run on several threads */
 
 static void build_lut(vlc_lut_t *t, const h264_vlc_code_t *codes, int bits)
 {
@@ -154,13 +155,16 @@ static void build_lut(vlc_lut_t *t, const h264_vlc_code_t *codes, int bits)
 	}
 }
 
-static void vlc_init(void)
+static void vlc_build(void)
 {
-	if (vlc_ready) return;
 	for (int i = 0; i < 5; ++i) build_lut(&ct_lut[i], h264_coeff_token_tab[i], 16);
 	for (int i = 1; i < 16; ++i) build_lut(&tz_lut[i], h264_total_zeros_tab[i], 9);
 	for (int i = 1; i < 8; ++i) build_lut(&rb_lut[i], h264_run_before_tab[i], 11);
-	vlc_ready = 1;
+}
+
+static void vlc_init(void)
+{
+	pthread_once(&vlc_once, vlc_build);
 }
 
 static inline int vlc_read(h264_bits_t *b, const vlc_lut_t *t)

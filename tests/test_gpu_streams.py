@@ -32,3 +32,23 @@ def test_hip_batch_replay_matches_golden(built, name):
     want = GOLDEN[name]["md5"]
     bad = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert len(got) == len(want) and not bad, f"{name}: frames {bad[:10]} differ (of {len(want)})"
+
+
+@pytest.mark.gpu
+def test_hip_md5_driver_matches_golden(built):
+    """m2dec_amd_decode_stream_md5: the same decode loop with the MD5s on a helper thread."""
+    for name in ("cov_tools_s1", "c3_1080p_s1"):
+        got = m2dec_amd.decode_stream_md5(stream(name))
+        assert got == GOLDEN[name]["md5"], name
+
+
+@pytest.mark.gpu
+def test_hip_concurrent_streams_match_golden(built):
+    """Eight independent streams (the C4 set: c3 seeds 1..8) decoded at once on one GPU, one host
+    thread and decoder context each (m2dec_amd_decode_streams_md5); every frame bit-exact."""
+    names = ["c3_1080p_s1"] + [f"c4_1080p_s{s}" for s in range(2, 9)]
+    got = m2dec_amd.decode_streams([stream(n) for n in names])
+    for n, g in zip(names, got):
+        want = GOLDEN[n]["md5"]
+        bad = [i for i, (a, b) in enumerate(zip(g, want)) if a != b]
+        assert len(g) == len(want) and not bad, f"{n}: frames {bad[:10]} differ (of {len(want)})"

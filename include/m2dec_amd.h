@@ -32,6 +32,10 @@ typedef struct {
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
 /* GPU ordinal used by the default back end (call after init, before the first SPS). */
 int m2dec_amd_h264_set_device(void *ctx, int device);
+/* Slice data of up to `threads` pictures parsed ahead on worker threads (0: on the caller's thread).
+ * Default with the built-in HIP back end: $M2DEC_AMD_PARSE_THREADS or 8; with a back end installed by
+ * m2dec_amd_h264_set_backend: 0.  Call before the first set_frames. */
+int m2dec_amd_h264_set_parse_threads(void *ctx, int threads);
 /* Free heap and GPU resources owned by a context. */
 void m2dec_amd_h264_release(void *ctx);
 
@@ -74,6 +78,13 @@ void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
  * helper thread.  Returns the number of frames delivered or < 0. */
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max,
                                 m2dec_amd_stats_t *stats);
+/* A back end that reconstructs nothing (acquire: one record arena; submit / sync: no-ops): decoding
+ * through it times the host parse alone. */
+int m2dec_amd_null_backend_create(m2r_backend_t *out);
+/* the same with an explicit back end (NULL: HIP) and parse-ahead worker count (-1: default) */
+int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                             int parse_threads, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                             m2dec_amd_stats_t *stats);
 /* n independent streams decoded concurrently on one device, one host thread and decoder context per
  * stream; frames[i] = frames delivered by stream i (or < 0).  Returns 0 if every stream succeeded. */
 int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_t *lens, int device,

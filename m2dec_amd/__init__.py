@@ -86,6 +86,10 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_decode_stream.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend), ctypes.c_int,
                                               ON_FRAME, ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.m2dec_amd_decode_stream.restype = ctypes.c_int
+        L.m2dec_amd_decode_stream3.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend), ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_int, ON_FRAME, ctypes.c_void_p,
+                                               ctypes.POINTER(Stats)]
+        L.m2dec_amd_decode_stream3.restype = ctypes.c_int
         L.m2dec_amd_hip_backend_create.argtypes = [ctypes.POINTER(Backend), ctypes.c_int]
         L.m2dec_amd_hip_backend_create.restype = ctypes.c_int
         L.m2dec_amd_hip_available.argtypes = []
@@ -188,11 +192,13 @@ def frame_nv12(f: Frame) -> bytes:
 
 
 def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 0,
-                  on_frame: Optional[Callable[[Frame], None]] = None, md5: bool = True) -> List[str]:
+                  on_frame: Optional[Callable[[Frame], None]] = None, md5: bool = True,
+                  parse_threads: int = -1) -> List[str]:
     """Decode an Annex-B H.264 stream exactly like ``h264dec -O`` and return the per-frame MD5 list.
 
     ``backend`` None -> the HIP back end on ``device`` (raises if absent).  Any other m2r_backend_t
-    (e.g. the oracle's, in tests) is borrowed.
+    (e.g. the oracle's, in tests) is borrowed.  ``parse_threads``: parse-ahead workers (-1: the
+    default — 8 with the HIP back end, none with a borrowed one).
     """
     L = lib()
     if backend is None and not L.m2dec_amd_hip_available():
@@ -212,8 +218,8 @@ def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 
 
     cb = ON_FRAME(_cb)
     st = Stats()
-    n = L.m2dec_amd_decode_stream(data, len(data), ctypes.byref(backend) if backend is not None else None, device, cb,
-                                  None, ctypes.byref(st))
+    n = L.m2dec_amd_decode_stream3(data, len(data), ctypes.byref(backend) if backend is not None else None, device, -1,
+                                   parse_threads, cb, None, ctypes.byref(st))
     if errs:
         raise errs[0]
     if n < 0:

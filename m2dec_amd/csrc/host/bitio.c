@@ -125,6 +125,10 @@ int h264_nal_next(h264_dec_t *d)
 {
 	dec_bits *st = d->stream;
 	int zeros = 0, c;
+	if (d->nal_replay) { /* the parse-ahead pipeline closed a picture on this NAL: hand it out again */
+		d->nal_replay = 0;
+		return 0;
+	}
 	/* find a start code */
 	if (!d->nal_pending) {
 		for (;;) {

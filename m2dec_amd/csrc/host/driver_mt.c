@@ -3,8 +3,8 @@
  * h264dec.cpp:251-257 + m2decoder.h:132-157, see m2dec_amd_decode_stream2):
  *
  *   m2dec_amd_decode_stream_md5   one stream; every output frame is copied out of the caller's frame
- *                                 buffer and its FileWriterMd5 line (filewrite.h:99-124) computed on a
- *                                 helper thread, so MD5 overlaps the parse of the next pictures;
+ *                                 buffer and its FileWriterMd5 line (filewrite.h:99-124) computed on
+ *                                 helper threads, so MD5 overlaps the parse of the next pictures;
  *   m2dec_amd_decode_streams_md5  n independent streams, one host thread (and one decoder context)
  *                                 each, sharing one GPU — the within-GPU form of SURVEY.md §8e's
  *                                 stream sharding.
@@ -18,7 +18,8 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 4
+#define MD5_RING 6
+#define MD5_THREADS 2
 
 typedef struct {
 	pthread_mutex_t mu;
@@ -27,7 +28,8 @@ typedef struct {
 	size_t cap;
 	m2d_frame_t frm[MD5_RING];
 	int idx[MD5_RING];       /* output frame number of the job in slot k */
-	int head, tail;          /* jobs [tail, head) pending, modulo MD5_RING */
+	int state[MD5_RING];     /* 0 free, 1 queued, 2 being hashed */
+	int head, next;          /* slots filled / taken by a hashing thread, in order */
 	int quit;
 	char *md5s;
 	int max;
@@ -40,9 +42,11 @@ static void *md5_worker(void *arg)
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	pthread_mutex_lock(&p->mu);
 	for (;;) {
-		while (p->tail == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
-		if (p->tail == p->head && p->quit) break;
-		const int k = p->tail % MD5_RING;
+		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
+		if (p->next == p->head) break;
+		const int k = p->next % MD5_RING;
+		p->next++;
+		p->state[k] = 2;
 		m2d_frame_t f = p->frm[k];
 		const int i = p->idx[k];
 		pthread_mutex_unlock(&p->mu);
@@ -50,11 +54,18 @@ static void *md5_worker(void *arg)
 		m2dec_amd_frame_md5(&f, line);
 		if (i < p->max) memcpy(p->md5s + (size_t)i * 35, line, 35);
 		pthread_mutex_lock(&p->mu);
-		p->tail++;
-		pthread_cond_signal(&p->cv_free);
+		p->state[k] = 0;
+		pthread_cond_broadcast(&p->cv_free);
 	}
 	pthread_mutex_unlock(&p->mu);
 	return NULL;
+}
+
+static int ring_idle(const md5_pipe_t *p)
+{
+	for (int k = 0; k < MD5_RING; ++k)
+		if (p->state[k]) return 0;
+	return 1;
 }
 
 /* on_frame of the stream driver: copy the frame into the next free ring slot, queue its MD5 */
@@ -62,15 +73,11 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 {
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	const size_t luma = (size_t)f->width * (size_t)f->height, bytes = luma * 3 / 2;
-	pthread_mutex_lock(&p->mu);
-	while (p->head - p->tail >= MD5_RING) pthread_cond_wait(&p->cv_free, &p->mu);
 	const int k = p->head % MD5_RING;
+	pthread_mutex_lock(&p->mu);
+	while (p->state[k] || (bytes > p->cap && !ring_idle(p))) pthread_cond_wait(&p->cv_free, &p->mu);
 	pthread_mutex_unlock(&p->mu);
-	if (bytes > p->cap) {
-		/* (re)size the ring once no job holds a buffer; only this thread allocates */
-		pthread_mutex_lock(&p->mu);
-		while (p->head != p->tail) pthread_cond_wait(&p->cv_free, &p->mu);
-		pthread_mutex_unlock(&p->mu);
+	if (bytes > p->cap) { /* (re)size the ring while no job holds a buffer; only this thread allocates */
 		for (int j = 0; j < MD5_RING; ++j) {
 			free(p->buf[j]);
 			p->buf[j] = (uint8_t *)malloc(bytes);
@@ -90,15 +97,25 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_lock(&p->mu);
 	p->frm[k] = c;
 	p->idx[k] = p->n++;
+	p->state[k] = 1;
 	p->head++;
 	pthread_cond_signal(&p->cv_job);
 	pthread_mutex_unlock(&p->mu);
 }
 
+static int decode_md5(const uint8_t *data, size_t len, int device, int parse_threads, char *md5s, int max,
+                      m2dec_amd_stats_t *stats);
+
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max, m2dec_amd_stats_t *stats)
 {
+	return decode_md5(data, len, device, -1, md5s, max, stats);
+}
+
+static int decode_md5(const uint8_t *data, size_t len, int device, int parse_threads, char *md5s, int max,
+                      m2dec_amd_stats_t *stats)
+{
 	md5_pipe_t p;
-	pthread_t th;
+	pthread_t th[MD5_THREADS];
 	int r;
 	memset(&p, 0, sizeof(p));
 	pthread_mutex_init(&p.mu, NULL);
@@ -106,13 +123,16 @@ int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, cha
 	pthread_cond_init(&p.cv_free, NULL);
 	p.md5s = md5s;
 	p.max = max;
-	if (pthread_create(&th, NULL, md5_worker, &p) != 0) return -1;
-	r = m2dec_amd_decode_stream2(data, len, NULL, device, -1, md5_on_frame, &p, stats);
+	int nth = 0;
+	for (; nth < MD5_THREADS; ++nth)
+		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
+	if (!nth) return -1;
+	r = m2dec_amd_decode_stream3(data, len, NULL, device, -1, parse_threads, md5_on_frame, &p, stats);
 	pthread_mutex_lock(&p.mu);
 	p.quit = 1;
-	pthread_cond_signal(&p.cv_job);
+	pthread_cond_broadcast(&p.cv_job);
 	pthread_mutex_unlock(&p.mu);
-	pthread_join(th, NULL);
+	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
 	for (int j = 0; j < MD5_RING; ++j) free(p.buf[j]);
 	pthread_mutex_destroy(&p.mu);
 	pthread_cond_destroy(&p.cv_job);
@@ -133,7 +153,8 @@ typedef struct {
 static void *stream_worker(void *arg)
 {
 	stream_job_t *j = (stream_job_t *)arg;
-	j->result = m2dec_amd_decode_stream_md5(j->data, j->len, j->device, j->md5s, j->max, NULL);
+	/* one parse-ahead worker per stream: the streams themselves fill the host cores */
+	j->result = decode_md5(j->data, j->len, j->device, 1, j->md5s, j->max, NULL);
 	return NULL;
 }
 
@@ -172,4 +193,81 @@ int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_
 	free(jobs);
 	free(th);
 	return ok;
+}
+
+/* ---------------------------------------------------------------- host-parse measurement back end */
+/* A back end that keeps no pixels: acquire hands out one record arena, submit / sync do nothing.
+ * Decoding through it times the host side alone (parse, or the parse-ahead pipeline). */
+typedef struct {
+	m2r_picture_t pic;
+	uint8_t *mem;
+	size_t size;
+} null_be_t;
+
+static int null_set_frames(void *self, int n, const m2d_frame_t *frames, int w, int h)
+{
+	(void)self; (void)n; (void)frames; (void)w; (void)h;
+	return 0;
+}
+
+static m2r_picture_t *null_acquire(void *self, int wm, int hm)
+{
+	null_be_t *b = (null_be_t *)self;
+	const int n = wm * hm;
+	const size_t need = (size_t)n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t) + sizeof(m2r_inter_t) + 416 * sizeof(int16_t)) +
+	                    256 * sizeof(m2r_slice_t) + 64;
+	if (need > b->size) {
+		free(b->mem);
+		b->mem = (uint8_t *)malloc(need);
+		b->size = b->mem ? need : 0;
+		if (!b->mem) return NULL;
+	}
+	uint8_t *p = b->mem;
+	memset(&b->pic, 0, sizeof(b->pic));
+	b->pic.width_mbs = wm;
+	b->pic.height_mbs = hm;
+	b->pic.mb = (m2r_mb_t *)p; p += (size_t)n * sizeof(m2r_mb_t);
+	b->pic.dbk = (m2r_deblock_t *)p; p += (size_t)n * sizeof(m2r_deblock_t);
+	b->pic.slice = (m2r_slice_t *)p; p += 256 * sizeof(m2r_slice_t);
+	b->pic.inter = (m2r_inter_t *)p; p += (size_t)n * sizeof(m2r_inter_t);
+	b->pic.coef = (int16_t *)p;
+	b->pic.cap_slices = 256;
+	b->pic.cap_inter = n;
+	b->pic.cap_coef = n * 416;
+	return &b->pic;
+}
+
+static int null_submit(void *self, m2r_picture_t *pic)
+{
+	(void)self; (void)pic;
+	return 0;
+}
+
+static int null_sync(void *self, int slot)
+{
+	(void)self; (void)slot;
+	return 0;
+}
+
+static void null_destroy(void *self)
+{
+	null_be_t *b = (null_be_t *)self;
+	free(b->mem);
+	free(b);
+}
+
+int m2dec_amd_null_backend_create(m2r_backend_t *out)
+{
+	null_be_t *b = (null_be_t *)calloc(1, sizeof(null_be_t));
+	if (!b || !out) {
+		free(b);
+		return -1;
+	}
+	out->self = b;
+	out->set_frames = null_set_frames;
+	out->acquire = null_acquire;
+	out->submit = null_submit;
+	out->sync_frame = null_sync;
+	out->destroy = null_destroy;
+	return 0;
 }

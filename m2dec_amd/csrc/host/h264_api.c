@@ -42,6 +42,7 @@ static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg
 	for (int i = 0; i < 16; ++i) d->refs[1][i].col = (int16_t)i;
 	d->curr_col = 16;
 	d->sh.first_mb = -1;
+	d->parse_threads = -1; /* default: decided when the back end is created */
 	return 0;
 }
 
@@ -70,13 +71,19 @@ static int api_get_info(void *ctx, m2d_info_t *info)
 
 static int ensure_backend(h264_dec_t *d)
 {
-	if (d->have_backend) return 0;
-	if (m2dec_amd_hip_backend_create(&d->backend, d->device) < 0) {
-		fprintf(stderr, "m2dec_amd: HIP reconstruction back end unavailable (no gfx950 device / HIP runtime); "
-		                "install an explicit back end with m2dec_amd_h264_set_backend() for CPU checking\n");
-		return -1;
+	if (!d->have_backend) {
+		if (m2dec_amd_hip_backend_create(&d->backend, d->device) < 0) {
+			fprintf(stderr, "m2dec_amd: HIP reconstruction back end unavailable (no gfx950 device / HIP runtime); "
+			                "install an explicit back end with m2dec_amd_h264_set_backend() for CPU checking\n");
+			return -1;
+		}
+		d->have_backend = 1;
+		if (d->parse_threads < 0) { /* default for the product path: parse ahead on worker threads */
+			const char *e = getenv("M2DEC_AMD_PARSE_THREADS");
+			d->parse_threads = e ? atoi(e) : 8;
+		}
 	}
-	d->have_backend = 1;
+	if (d->parse_threads > 0 && !d->as && h264_async_start(d, d->parse_threads) < 0) return -1;
 	return 0;
 }
 
@@ -123,6 +130,16 @@ static int read_slice(h264_dec_t *d, int nal_unit_type, int nal_ref_idc)
 	const h264_sps_t *s;
 	int prev_first = d->in_picture ? d->sh.first_mb : -1;
 	int err;
+	if (d->as && d->in_picture) {
+		/* parse-ahead: a slice whose first_mb is not above the previous one starts the next picture
+		 * (h264.cpp:1427-1430): close the current one, and read this NAL again next time */
+		h264_bits_t b;
+		hb_init(&b, d->nal + 1, d->nal_len - 1);
+		if ((int)hb_ue(&b) <= prev_first) {
+			d->nal_replay = 1;
+			return h264_async_close(d);
+		}
+	}
 	hb_init(&d->bs, d->nal + 1, d->nal_len - 1);
 	d->slice_rbsp = d->nal + 1;
 	d->slice_rbsp_end = d->nal + d->nal_len;
@@ -141,6 +158,7 @@ static int read_slice(h264_dec_t *d, int nal_unit_type, int nal_ref_idc)
 	if (!d->in_picture) {
 		if (h264_picture_begin(d) < 0) return -1;
 	}
+	if (d->as) return h264_async_add_slice(d) < 0 ? -1 : 0;
 	err = h264_slice_data(d);
 	if (err < 0) return err;
 	if (err == 1) return h264_picture_finish(d);
@@ -153,10 +171,19 @@ static int api_decode_picture(void *ctx)
 	if (!d) return -1;
 	for (;;) {
 		int type, ref_idc, err = 0;
-		if (h264_nal_next(d) < 0) return -2;
+		if (h264_nal_next(d) < 0) {
+			if (d->as && d->in_picture) return h264_async_close(d); /* the last picture */
+			return -2;
+		}
 		if (d->nal_len == 0) continue;
 		type = d->nal[0] & 31;
 		ref_idc = (d->nal[0] >> 5) & 3;
+		if (d->as && d->in_picture && type >= 6 && type <= 9) {
+			/* SEI / SPS / PPS / AUD after a picture's slices start the next access unit (7.4.1.2.3) */
+			d->nal_replay = 1;
+			return h264_async_close(d);
+		}
+		if (d->as && type == 7 && h264_async_drain(d, -1) < 0) return -1; /* set_frames may follow */
 		switch (type) {
 		case 1:
 		case 5:
@@ -189,6 +216,7 @@ static int api_decode_picture(void *ctx)
 static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
 {
 	if (idx < 0) return 0;
+	if (d->as && h264_async_drain(d, idx) < 0) return -1; /* the picture in that slot is parsed and submitted */
 	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) return -1;
 	*frame = d->frames[idx];
 	return 1;
@@ -232,6 +260,14 @@ int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
 	return 0;
 }
 
+int m2dec_amd_h264_set_parse_threads(void *ctx, int threads)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d || d->as) return -1; /* before the first set_frames */
+	d->parse_threads = threads < 0 ? 0 : threads;
+	return 0;
+}
+
 int m2dec_amd_h264_set_device(void *ctx, int device)
 {
 	CTX(ctx)->device = device;
@@ -242,6 +278,7 @@ void m2dec_amd_h264_release(void *ctx)
 {
 	h264_dec_t *d = CTX(ctx);
 	if (!d) return;
+	h264_async_stop(d);
 	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
 	d->have_backend = 0;
 	free(d->mbi);
@@ -324,8 +361,20 @@ int m2dec_amd_decode_stream(const uint8_t *data, size_t len, const m2r_backend_t
 	return m2dec_amd_decode_stream2(data, len, backend, device, -1, on_frame, arg, stats);
 }
 
+int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                             int parse_threads, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                             m2dec_amd_stats_t *stats);
+
 int m2dec_amd_decode_stream2(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
                              void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
+{
+	return m2dec_amd_decode_stream3(data, len, backend, device, dpb, -1, on_frame, arg, stats);
+}
+
+/* parse_threads: -1 the context's default, else m2dec_amd_h264_set_parse_threads(threads) */
+int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                             int parse_threads, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                             m2dec_amd_stats_t *stats)
 {
 	driver_t v;
 	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
@@ -339,6 +388,7 @@ int m2dec_amd_decode_stream2(const uint8_t *data, size_t len, const m2r_backend_
 	h264d_func->init(d, dpb, drv_header, &v);
 	d->device = device;
 	if (backend) m2dec_amd_h264_set_backend(d, backend);
+	if (parse_threads >= 0) m2dec_amd_h264_set_parse_threads(d, parse_threads);
 	dec_bits_set_callback(d->stream, drv_reread, &v);
 	/* h264dec.cpp:251-257 + M2Decoder::decode / decode_residual (m2decoder.h:132-157) */
 	for (;;) {

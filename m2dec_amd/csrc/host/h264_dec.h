@@ -265,6 +265,7 @@ struct h264_dec {
 	uint8_t *nal;            /* current NAL as RBSP (emulation prevention removed) */
 	size_t nal_len, nal_cap;
 	int nal_pending;         /* a NAL was read but not consumed (new picture detected) */
+	int nal_replay;          /* the current NAL is handed out again by the next h264_nal_next */
 	int eos;
 
 	h264_sps_t sps[32];
@@ -317,6 +318,10 @@ struct h264_dec {
 
 	/* statistics */
 	uint64_t pictures;
+
+	/* parse-ahead pipeline (h264_async.c); NULL: slice data parsed on the caller's thread */
+	struct h264_async *as;
+	int parse_threads;       /* requested workers (m2dec_amd_h264_set_parse_threads / env) */
 };
 
 /* h264_syntax.c */
@@ -325,12 +330,21 @@ int h264_parse_pps(h264_dec_t *d, h264_bits_t *b, size_t rbsp_len);
 int h264_slice_header(h264_dec_t *d, h264_bits_t *b, int nal_unit_type, int nal_ref_idc);
 int h264_picture_begin(h264_dec_t *d);
 int h264_picture_finish(h264_dec_t *d);
+void h264_picture_resolve_deblock(h264_dec_t *d);
+int h264_picture_mark(h264_dec_t *d);
 void h264_dpb_init(h264_dpb_t *dpb, int maxsize);
 int h264_dpb_peek(h264_dpb_t *dpb, int bypass);
 int h264_dpb_pop(h264_dpb_t *dpb, int bypass);
 
 /* h264_mb.c */
 int h264_slice_data(h264_dec_t *d);
+
+/* h264_async.c */
+int h264_async_start(h264_dec_t *d, int threads);
+int h264_async_add_slice(h264_dec_t *d);
+int h264_async_close(h264_dec_t *d);
+int h264_async_drain(h264_dec_t *d, int slot);
+void h264_async_stop(h264_dec_t *d);
 
 #ifdef __cplusplus
 }

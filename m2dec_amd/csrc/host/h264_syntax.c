@@ -864,6 +864,10 @@ int h264_picture_begin(h264_dec_t *d)
 	d->mbs_decoded = 0;
 	d->slice_num = 0;
 	d->in_picture = 1;
+	if (d->as) { /* parse-ahead: the job owns MB info and records (h264_async.c) */
+		d->pic = NULL;
+		return 0;
+	}
 	for (int i = 0; i < d->n_mbs; ++i) {
 		d->mbi[i].type = -1;
 		d->mbi[i].slice = -1;
@@ -879,16 +883,11 @@ int h264_picture_begin(h264_dec_t *d)
 	return 0;
 }
 
-/* post_process, h264.cpp:11022-11050 (deblocking happens inside the back end) */
-int h264_picture_finish(h264_dec_t *d)
+/* post_process, h264.cpp:11022-11050, in three parts (deblocking happens inside the back end):
+ * the deblock edge enables that deblock_pb derives from the picture-final firstline (needs the
+ * picture's parsed MB info) ... */
+void h264_picture_resolve_deblock(h264_dec_t *d)
 {
-	h264_slice_t *h = &d->sh;
-	const h264_sps_t *s = &d->sps[d->active_sps];
-	int max_frame_num = 1 << s->log2_max_frame_num;
-	int num_ref_frames = s->num_ref_frames;
-	int err;
-
-	/* resolve the deblock edge enables that deblock_pb derives from the picture-final firstline */
 	{
 		m2r_deblock_t *dbk = d->pic->dbk;
 		int any = 0;
@@ -912,10 +911,16 @@ int h264_picture_finish(h264_dec_t *d)
 		}
 		d->pic->deblock = any;
 	}
-	err = d->backend.submit(d->backend.self, d->pic);
-	d->pic = NULL;
-	if (err < 0) return -1;
+}
 
+/* ... the reference marking, the co-located store swap and the DPB insertion (need only the slice
+ * headers: the parse-ahead pipeline runs this before the picture's slice data is parsed) ... */
+int h264_picture_mark(h264_dec_t *d)
+{
+	h264_slice_t *h = &d->sh;
+	const h264_sps_t *s = &d->sps[d->active_sps];
+	int max_frame_num = 1 << s->log2_max_frame_num;
+	int num_ref_frames = s->num_ref_frames;
 	if (h->nal_ref_idc) {
 		h264_ref_t *r = NULL;
 		int target;
@@ -951,4 +956,15 @@ int h264_picture_finish(h264_dec_t *d)
 	d->in_picture = 0;
 	d->pictures++;
 	return 1;
+}
+
+/* ... all three in order (synchronous parse) */
+int h264_picture_finish(h264_dec_t *d)
+{
+	int err;
+	h264_picture_resolve_deblock(d);
+	err = d->backend.submit(d->backend.self, d->pic);
+	d->pic = NULL;
+	if (err < 0) return -1;
+	return h264_picture_mark(d);
 }

@@ -1,0 +1,36 @@
+"""The parse-ahead pipeline (m2dec_amd/csrc/host/h264_async.c: slice data of several pictures parsed on
+worker threads, marking / DPB / back-end calls on the caller's thread) through the CPU oracle back end:
+every frame must equal the synchronous parser's golden, for single- and multi-slice, CAVLC and CABAC,
+P and B (co-located store dependencies of direct prediction), deblocking idc 2 and constrained intra."""
+import os
+
+import pytest
+
+import m2dec_amd
+from tests._oracle import OracleBackend, golden_md5s
+from tests._streams import GOLDEN, stream
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = ["cov_cabac_s1", "cov_cabac_s2", "cov_cabac4x4_s1", "cov_cavlc_s1", "cov_wp_s1", "cov_slices_s1",
+         "cov_tools_s1", "cov_tools_cavlc_s1", "c2_720p_s1"]
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+@pytest.mark.parametrize("name", NAMES)
+def test_parse_ahead_matches_golden(built, name, threads):
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=threads)
+    assert got == GOLDEN[name]["md5"]
+
+
+def test_parse_ahead_f1_matches_reference(built):
+    data = open(os.path.join(ROOT, "tests", "golden", "f1_realshort.264"), "rb").read()
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream(data, backend=ob.be, parse_threads=3)
+    assert got == golden_md5s(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"))
+
+
+def test_parse_ahead_4k_multislice(built):
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream(stream("c5_4k_s1"), backend=ob.be, parse_threads=6)
+    assert got == GOLDEN["c5_4k_s1"]["md5"]

@@ -74,9 +74,9 @@ int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
 
 /* Throughput drivers over the same decode loop as m2dec_amd_decode_stream (h264dec -O): the HIP back
- * end on `device`, one MD5 line (35 bytes) per output frame into md5s (at most `max`), the MD5s on a
- * helper thread.  Returns the number of frames delivered or < 0. */
-int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max,
+ * end on `device`, DPB size `dpb` (h264dec -d; -1 auto), one MD5 line (35 bytes) per output frame into
+ * md5s (at most `max`), the MD5s on helper threads.  Returns the number of frames delivered or < 0. */
+int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
                                 m2dec_amd_stats_t *stats);
 /* A back end that reconstructs nothing (acquire: one record arena; submit / sync: no-ops): decoding
  * through it times the host parse alone. */

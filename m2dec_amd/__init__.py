@@ -98,8 +98,8 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
         L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
         L.m2dec_amd_frame_md5.restype = None
-        L.m2dec_amd_decode_stream_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_char_p,
-                                                  ctypes.c_int, ctypes.POINTER(Stats)]
+        L.m2dec_amd_decode_stream_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(Stats)]
         L.m2dec_amd_decode_stream_md5.restype = ctypes.c_int
         L.m2dec_amd_decode_streams_md5.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
@@ -232,16 +232,16 @@ def _max_frames(data: bytes) -> int:
     return max(1, data.count(b"\x00\x00\x01"))
 
 
-def decode_stream_md5(data: bytes, device: int = 0) -> List[str]:
-    """The HIP decode path exactly like ``h264dec -O`` with the MD5s computed in C on a helper thread
-    (m2dec_amd_decode_stream_md5): the throughput form of ``decode_stream``."""
+def decode_stream_md5(data: bytes, device: int = 0, dpb: int = -1) -> List[str]:
+    """The HIP decode path exactly like ``h264dec -O`` (``-d dpb``) with the MD5s computed in C on helper
+    threads (m2dec_amd_decode_stream_md5): the throughput form of ``decode_stream``."""
     L = lib()
     if not L.m2dec_amd_hip_available():
         raise RuntimeError("m2dec_amd: no usable gfx950 device for the HIP back end")
     cap = _max_frames(data)
     buf = ctypes.create_string_buffer(35 * cap)
     st = Stats()
-    n = L.m2dec_amd_decode_stream_md5(data, len(data), device, buf, cap, ctypes.byref(st))
+    n = L.m2dec_amd_decode_stream_md5(data, len(data), device, dpb, buf, cap, ctypes.byref(st))
     if n < 0:
         raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
     raw = buf.raw

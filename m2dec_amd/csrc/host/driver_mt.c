@@ -103,15 +103,16 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_unlock(&p->mu);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int parse_threads, char *md5s, int max,
+static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, char *md5s, int max,
                       m2dec_amd_stats_t *stats);
 
-int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, char *md5s, int max, m2dec_amd_stats_t *stats)
+int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
+                                m2dec_amd_stats_t *stats)
 {
-	return decode_md5(data, len, device, -1, md5s, max, stats);
+	return decode_md5(data, len, device, dpb, -1, md5s, max, stats);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int parse_threads, char *md5s, int max,
+static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, char *md5s, int max,
                       m2dec_amd_stats_t *stats)
 {
 	md5_pipe_t p;
@@ -127,7 +128,7 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int parse_thr
 	for (; nth < MD5_THREADS; ++nth)
 		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
 	if (!nth) return -1;
-	r = m2dec_amd_decode_stream3(data, len, NULL, device, -1, parse_threads, md5_on_frame, &p, stats);
+	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, stats);
 	pthread_mutex_lock(&p.mu);
 	p.quit = 1;
 	pthread_cond_broadcast(&p.cv_job);
@@ -154,7 +155,7 @@ static void *stream_worker(void *arg)
 {
 	stream_job_t *j = (stream_job_t *)arg;
 	/* one parse-ahead worker per stream: the streams themselves fill the host cores */
-	j->result = decode_md5(j->data, j->len, j->device, 1, j->md5s, j->max, NULL);
+	j->result = decode_md5(j->data, j->len, j->device, -1, 1, j->md5s, j->max, NULL);
 	return NULL;
 }
 

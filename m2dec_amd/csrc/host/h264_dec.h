@@ -103,6 +103,10 @@ typedef struct {
 	uint32_t range;     /* codIRange, 9 bits */
 	int bits;
 	const uint8_t *p, *end;
+} h264_cabac_eng_t;
+
+typedef struct {
+	h264_cabac_eng_t e;        /* kept apart from ctx so hot loops can hold it in registers */
 	uint8_t ctx[H264_NUM_CTX]; /* (pStateIdx << 1) | valMPS */
 } h264_cabac_t;
 

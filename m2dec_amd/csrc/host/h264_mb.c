@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <pthread.h>
 #include <stdlib.h>
+#include <string.h>
 #include "h264_dec.h"
 
 /* blkIdx -> 4x4 position (spec 6.4.3) and inverse */
@@ -31,8 +32,12 @@ static inline int iabs(int a) { return a < 0 ? -a : a; }
 static inline int median3(int a, int b, int c) { return imax(imin(a, b), imin(imax(a, b), c)); }
 
 /* ================================================================== CABAC engine (9.3.1.2, 9.3.3.2) */
+static void cab_build(void);
+static pthread_once_t cab_once;
+
 static void cabac_init_ctx(h264_cabac_t *c, int qp, int idc)
 {
+	pthread_once(&cab_once, cab_build);
 	const int8_t (*mn)[2] = h264_cabac_init_mn[idc];
 	for (int i = 0; i < H264_NUM_CTX; ++i) {
 		int pre = ((mn[i][0] * qp) >> 4) + mn[i][1];
@@ -42,94 +47,123 @@ static void cabac_init_ctx(h264_cabac_t *c, int qp, int idc)
 	}
 }
 
-static inline void cabac_refill(h264_cabac_t *c)
+/* Engine state lives in h264_cabac_eng_t; the eng_* primitives take it apart from the context
+ * bytes so that a caller holding a local copy keeps value/range/bits in registers (a store to a
+ * uint8_t context may alias anything reachable through a pointer). */
+static inline void eng_refill(h264_cabac_eng_t *e)
 {
-	while (c->bits < 24) {
-		uint32_t byte = (c->p < c->end) ? *c->p : 0;
-		c->p++;
-		c->value = (c->value << 8) | byte;
-		c->bits += 8;
+	if (e->bits >= 16) return;
+	if (__builtin_expect(e->p + 4 <= e->end, 1)) {
+		/* value < range << bits < 2^25 here: a 32-bit look-ahead keeps it under 2^57 */
+		uint32_t w = ((uint32_t)e->p[0] << 24) | ((uint32_t)e->p[1] << 16) | ((uint32_t)e->p[2] << 8) | e->p[3];
+		e->p += 4;
+		e->value = (e->value << 32) | w;
+		e->bits += 32;
+		return;
+	}
+	while (e->bits < 24) {
+		uint32_t byte = (e->p < e->end) ? *e->p : 0;
+		e->p++;
+		e->value = (e->value << 8) | byte;
+		e->bits += 8;
 	}
 }
 
 static void cabac_start(h264_cabac_t *c, const uint8_t *p, const uint8_t *end)
 {
-	c->p = p;
-	c->end = end;
-	c->value = 0;
-	c->bits = -9;
-	c->range = 510;
-	cabac_refill(c);
+	h264_cabac_eng_t *e = &c->e;
+	e->p = p;
+	e->end = end;
+	e->value = 0;
+	e->bits = -9;
+	e->range = 510;
+	while (e->bits < 16) { /* the 9-bit codIOffset plus look-ahead */
+		uint32_t byte = (e->p < e->end) ? *e->p : 0;
+		e->p++;
+		e->value = (e->value << 8) | byte;
+		e->bits += 8;
+	}
 }
 
 /* bit position (spec bitstream pointer) relative to the start of the engine's data */
 static inline size_t cabac_bitpos(const h264_cabac_t *c, const uint8_t *start)
 {
-	return (size_t)(c->p - start) * 8 - (size_t)c->bits;
+	return (size_t)(c->e.p - start) * 8 - (size_t)c->e.bits;
+}
+
+/* next context byte after a bin: cab_next[(lps << 7) | ctx] (9.3.3.2.1.1 transitions) */
+static uint8_t cab_next[256];
+static pthread_once_t cab_once = PTHREAD_ONCE_INIT;
+
+static void cab_build(void)
+{
+	for (int s = 0; s < 128; ++s) {
+		const int state = s >> 1, mps = s & 1;
+		cab_next[s] = (uint8_t)(((state + (state < 62)) << 1) | mps);
+		cab_next[128 | s] = (uint8_t)((h264_trans_idx_lps[state] << 1) | (mps ^ (state == 0)));
+	}
+}
+
+/* branch-free on the MPS/LPS outcome, which is unpredictable for residual bins */
+static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
+{
+	const uint32_t s = ctx[ctxidx];
+	const uint32_t lps = h264_range_lps[s >> 1][(e->range >> 6) & 3];
+	uint32_t range = e->range - lps;
+	const uint64_t scaled = (uint64_t)range << e->bits;
+	const uint32_t is_lps = e->value >= scaled;
+	const uint64_t m = (uint64_t)0 - is_lps;
+	e->value -= scaled & m;
+	range ^= (range ^ lps) & (uint32_t)m;
+	ctx[ctxidx] = cab_next[(is_lps << 7) | s];
+	{
+		const int n = __builtin_clz(range) - 23;
+		e->range = range << n;
+		e->bits -= n;
+		eng_refill(e);
+	}
+	return (int)((s & 1) ^ is_lps);
+}
+
+static inline int eng_bypass(h264_cabac_eng_t *e)
+{
+	uint64_t scaled;
+	int ret = 0;
+	e->bits -= 1;
+	scaled = (uint64_t)e->range << e->bits;
+	if (e->value >= scaled) {
+		e->value -= scaled;
+		ret = 1;
+	}
+	eng_refill(e); /* keeps the invariant value < range << bits */
+	return ret;
 }
 
 static inline int cabac_decision(h264_cabac_t *c, int ctxidx)
 {
-	uint32_t s = c->ctx[ctxidx];
-	uint32_t state = s >> 1;
-	uint32_t bin = s & 1;
-	uint32_t lps = h264_range_lps[state][(c->range >> 6) & 3];
-	uint32_t range = c->range - lps;
-	uint64_t scaled = (uint64_t)range << c->bits;
-	if (c->value < scaled) {
-		c->ctx[ctxidx] = (uint8_t)(((state + (state < 62)) << 1) | bin);
-		if (range >= 256) {
-			c->range = range;
-			return (int)bin;
-		}
-	} else {
-		c->value -= scaled;
-		range = lps;
-		c->ctx[ctxidx] = (uint8_t)((h264_trans_idx_lps[state] << 1) | (bin ^ (state == 0)));
-		bin ^= 1;
-	}
-	{
-		int n = __builtin_clz(range) - 23;
-		c->range = range << n;
-		c->bits -= n;
-		if (c->bits < 16) cabac_refill(c);
-	}
-	return (int)bin;
+	return eng_decision(&c->e, c->ctx, ctxidx);
 }
 
 static inline int cabac_bypass(h264_cabac_t *c)
 {
-	uint64_t scaled;
-	c->bits -= 1;
-	scaled = (uint64_t)c->range << c->bits;
-	if (c->bits < 16) {
-		/* keep the invariant value < range << bits while refilling */
-		int ret;
-		if (c->value >= scaled) { c->value -= scaled; ret = 1; } else ret = 0;
-		cabac_refill(c);
-		return ret;
-	}
-	if (c->value >= scaled) {
-		c->value -= scaled;
-		return 1;
-	}
-	return 0;
+	return eng_bypass(&c->e);
 }
 
 static inline int cabac_terminate(h264_cabac_t *c)
 {
-	uint32_t range = c->range - 2;
-	uint64_t scaled = (uint64_t)range << c->bits;
-	if (c->value >= scaled) {
-		c->range = range;
+	h264_cabac_eng_t *e = &c->e;
+	uint32_t range = e->range - 2;
+	uint64_t scaled = (uint64_t)range << e->bits;
+	if (e->value >= scaled) {
+		e->range = range;
 		return 1;
 	}
 	if (range < 256) {
-		c->range = range << 1;
-		c->bits -= 1;
-		if (c->bits < 16) cabac_refill(c);
+		e->range = range << 1;
+		e->bits -= 1;
+		eng_refill(e);
 	} else {
-		c->range = range;
+		e->range = range;
 	}
 	return 0;
 }
@@ -261,6 +295,8 @@ static const int16_t abs_base[5] = {227 + 0, 227 + 10, 227 + 20, 227 + 30, 227 +
 /* decode one block; writes levels at raster positions out[scan[i]]; returns number of nonzero */
 static int cabac_block(h264_cabac_t *c, int cat, int16_t *out)
 {
+	h264_cabac_eng_t e = c->e;
+	uint8_t *ctx = c->ctx;
 	int map[64];
 	int n = 0, i, num;
 	const uint8_t *scan;
@@ -271,9 +307,9 @@ static int cabac_block(h264_cabac_t *c, int cat, int16_t *out)
 	if (cat == 5) {
 		num = 64;
 		for (i = 0; i < 63; ++i) {
-			if (cabac_decision(c, 402 + h264_sig8x8_frame[i])) {
+			if (eng_decision(&e, ctx, 402 + h264_sig8x8_frame[i])) {
 				map[n++] = i;
-				if (cabac_decision(c, 417 + h264_last8x8[i])) goto done;
+				if (eng_decision(&e, ctx, 417 + h264_last8x8[i])) goto done;
 			}
 		}
 		map[n++] = 63;
@@ -283,9 +319,9 @@ static int cabac_block(h264_cabac_t *c, int cat, int16_t *out)
 	sbase = sig_base[cat];
 	lbase = last_base[cat];
 	for (i = 0; i < num - 1; ++i) {
-		if (cabac_decision(c, sbase + i)) {
+		if (eng_decision(&e, ctx, sbase + i)) {
 			map[n++] = i;
-			if (cabac_decision(c, lbase + i)) goto done;
+			if (eng_decision(&e, ctx, lbase + i)) goto done;
 		}
 	}
 	map[n++] = num - 1;
@@ -304,32 +340,33 @@ done:
 	for (int k = n - 1; k >= 0; --k) {
 		int ctxinc = (gt1 != 0) ? 0 : imin(4, 1 + eq1);
 		int lvl;
-		if (!cabac_decision(c, abase + ctxinc)) {
+		if (!eng_decision(&e, ctx, abase + ctxinc)) {
 			lvl = 1;
 			eq1++;
 		} else {
 			int ctx2 = abase + 5 + imin(4 - (cat == 3), gt1);
 			lvl = 2;
-			while (lvl < 15 && cabac_decision(c, ctx2)) lvl++;
+			while (lvl < 15 && eng_decision(&e, ctx, ctx2)) lvl++;
 			if (lvl == 15) {
 				/* UEG0 suffix (9.3.2.3) */
 				int k2 = 0;
-				while (cabac_bypass(c)) {
+				while (eng_bypass(&e)) {
 					lvl += 1 << k2;
 					k2++;
 					if (k2 > 24) break;
 				}
-				while (k2-- > 0) lvl += cabac_bypass(c) << k2;
+				while (k2-- > 0) lvl += eng_bypass(&e) << k2;
 			}
 			gt1++;
 		}
-		if (cabac_bypass(c)) lvl = -lvl;
+		if (eng_bypass(&e)) lvl = -lvl;
 		{
 			int pos = map[k] + first;
 			out[scan ? scan[pos] : pos] = (int16_t)lvl;
 		}
 	}
 	(void)num;
+	c->e = e;
 	return n;
 }
 
@@ -840,26 +877,31 @@ static int read_ref_idx(slice_ctx_t *s, int lx, int b8, int num_active)
 
 static int cabac_mvd(h264_cabac_t *c, int base, int sum)
 {
-	int inc = (sum < 3) ? 0 : (sum <= 32 ? 1 : 2);
-	int mvd, ctx;
+	h264_cabac_eng_t e;
+	uint8_t *ctx = c->ctx;
+	const int inc = (sum < 3) ? 0 : (sum <= 32 ? 1 : 2);
+	int mvd, ci;
 	if (!cabac_decision(c, base + inc)) return 0;
+	e = c->e;
 	mvd = 1;
-	ctx = base + 3;
-	while (cabac_decision(c, ctx)) {
-		if (mvd < 4) ctx++;
+	ci = base + 3;
+	while (eng_decision(&e, ctx, ci)) {
+		if (mvd < 4) ci++;
 		mvd++;
 		if (mvd >= 9) {
 			int k = 3;
-			while (cabac_bypass(c)) {
+			while (eng_bypass(&e)) {
 				mvd += 1 << k;
 				k++;
 				if (k > 24) break;
 			}
-			while (k-- > 0) mvd += cabac_bypass(c) << k;
+			while (k-- > 0) mvd += eng_bypass(&e) << k;
 			break;
 		}
 	}
-	return cabac_bypass(c) ? -mvd : mvd;
+	if (eng_bypass(&e)) mvd = -mvd;
+	c->e = e;
+	return mvd;
 }
 
 static void read_mvd(slice_ctx_t *s, int lx, int x, int y, int out[2])
@@ -1087,6 +1129,20 @@ static int bs_motion(const h264_mbinfo_t *q, int qx, int qy, const h264_mbinfo_t
 
 static inline int is_intra_type(int t) { return t >= 0 && t <= MBT_IPCM; }
 
+/* one motion for the whole MB (both lists): every inner-edge bS-1 test is then 0 */
+static int uniform_motion(const h264_mbinfo_t *q)
+{
+	uint32_t w[2][16];
+	memcpy(w, q->mv, sizeof(w));
+	for (int lx = 0; lx < 2; ++lx) {
+		if (q->fidx[lx][1] != q->fidx[lx][0] || q->fidx[lx][2] != q->fidx[lx][0] || q->fidx[lx][3] != q->fidx[lx][0])
+			return 0;
+		for (int i = 1; i < 16; ++i)
+			if (w[lx][i] != w[lx][0]) return 0;
+	}
+	return 1;
+}
+
 static void compute_bs(slice_ctx_t *s)
 {
 	h264_mbinfo_t *q = s->cur;
@@ -1099,7 +1155,7 @@ static void compute_bs(slice_ctx_t *s)
 		bv = bh = v;
 		flags = M2R_DBK_LEFT_BS4 | M2R_DBK_TOP_BS4;
 	} else {
-		int t8 = q->t8x8;
+		const int t8 = q->t8x8, uni = uniform_motion(q);
 		for (int dir = 0; dir < 2; ++dir) {
 			uint32_t str = 0;
 			for (int e = 0; e < 4; ++e) {
@@ -1130,7 +1186,7 @@ static void compute_bs(slice_ctx_t *s)
 					}
 					if (!v) {
 						if (q->nnz[rast2blk[qy * 4 + qx]] || p->nnz[rast2blk[py * 4 + px]]) v = 2;
-						else if (bs_motion(q, qx, qy, p, px, py)) v = 1;
+						else if ((p != q || !uni) && bs_motion(q, qx, qy, p, px, py)) v = 1;
 					}
 					str |= (uint32_t)v << (e * 8 + sgm * 2);
 				}
@@ -1281,9 +1337,9 @@ static int decode_pcm(slice_ctx_t *s)
 		/* 9.3.1.2: samples start at the byte boundary after the bits the engine consumed */
 		size_t pos = (cabac_bitpos(&d->cabac, d->cabac_start) + 7) >> 3;
 		src = d->cabac_start + pos;
-		if (src + 384 > d->cabac.end) return -1;
+		if (src + 384 > d->cabac.e.end) return -1;
 		memcpy(dst, src, 384);
-		cabac_start(&d->cabac, src + 384, d->cabac.end);
+		cabac_start(&d->cabac, src + 384, d->cabac.e.end);
 	} else {
 		h264_bits_t *b = &d->bs;
 		int mis = b->bits & 7;

@@ -18,8 +18,8 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 6
-#define MD5_THREADS 2
+#define MD5_RING 10
+#define MD5_THREADS 4 /* one stream: MD5 (~5 ms per 1080p frame per core) must keep up with the GPU */
 
 typedef struct {
 	pthread_mutex_t mu;
@@ -103,17 +103,17 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_unlock(&p->mu);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, char *md5s, int max,
-                      m2dec_amd_stats_t *stats);
+static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, int md5_threads,
+                      char *md5s, int max, m2dec_amd_stats_t *stats);
 
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
                                 m2dec_amd_stats_t *stats)
 {
-	return decode_md5(data, len, device, dpb, -1, md5s, max, stats);
+	return decode_md5(data, len, device, dpb, -1, MD5_THREADS, md5s, max, stats);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, char *md5s, int max,
-                      m2dec_amd_stats_t *stats)
+static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, int md5_threads,
+                      char *md5s, int max, m2dec_amd_stats_t *stats)
 {
 	md5_pipe_t p;
 	pthread_t th[MD5_THREADS];
@@ -125,7 +125,7 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	p.md5s = md5s;
 	p.max = max;
 	int nth = 0;
-	for (; nth < MD5_THREADS; ++nth)
+	for (; nth < md5_threads && nth < MD5_THREADS; ++nth)
 		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
 	if (!nth) return -1;
 	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, stats);
@@ -155,7 +155,7 @@ static void *stream_worker(void *arg)
 {
 	stream_job_t *j = (stream_job_t *)arg;
 	/* one parse-ahead worker per stream: the streams themselves fill the host cores */
-	j->result = decode_md5(j->data, j->len, j->device, -1, 1, j->md5s, j->max, NULL);
+	j->result = decode_md5(j->data, j->len, j->device, -1, 1, 2, j->md5s, j->max, NULL);
 	return NULL;
 }
 

@@ -50,7 +50,7 @@ typedef struct h264_job {
 	                             never keep a pointer past its submission) */
 	int ndeps;
 	long seq;
-	int done, err;            /* guarded by the pipeline mutex */
+	int taken, done, err;     /* guarded by the pipeline mutex */
 	h264_dec_t *w;            /* worker context */
 } h264_job_t;
 
@@ -61,7 +61,7 @@ struct h264_async {
 	int nth, quit, depth;
 	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head) */
 	long head, tail;
-	h264_job_t *queue[AS_MAX]; /* dispatched, not yet taken by a worker */
+	h264_job_t *queue[AS_MAX]; /* dispatched; [qtail, qhead) holds every job not yet taken */
 	long qhead, qtail;
 	h264_job_t *cur;          /* the picture being collected */
 	h264_job_t *free_jobs[AS_MAX];
@@ -112,6 +112,7 @@ static void job_clear(h264_job_t *j)
 	}
 	j->nsl = 0;
 	j->ndeps = 0;
+	j->taken = 0;
 	j->done = 0;
 	j->err = 0;
 }
@@ -180,36 +181,48 @@ static void job_run(h264_job_t *j)
 	h264_picture_resolve_deblock(w);
 }
 
+/* 1: every job j waits for has finished parsing (0: not yet); a dependency no longer in the fifo was
+ * submitted, hence finished.  *err collects their errors.  Caller holds the mutex. */
+static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err)
+{
+	for (int i = 0; i < j->ndeps; ++i)
+		for (long k = as->tail; k < as->head; ++k) {
+			const h264_job_t *o = as->fifo[k % AS_MAX];
+			if (o->seq != j->deps[i]) continue;
+			if (!o->done) return 0;
+			*err |= o->err;
+		}
+	return 1;
+}
+
+/* Workers take the oldest queued job whose dependencies have finished, so a B picture waiting for
+ * its co-located P does not hold a worker while later P pictures could be parsed. */
 static void *worker(void *arg)
 {
 	struct h264_async *as = (struct h264_async *)arg;
 	pthread_mutex_lock(&as->mu);
 	for (;;) {
-		while (as->qtail == as->qhead && !as->quit) pthread_cond_wait(&as->cv_work, &as->mu);
-		if (as->qtail == as->qhead) break;
-		h264_job_t *j = as->queue[as->qtail % AS_MAX];
-		as->qtail++;
-		/* the writers of the co-located stores this picture reads (earlier jobs: already taken; a job
-		 * no longer in the fifo was submitted, hence finished) */
+		h264_job_t *j = NULL;
 		int dep_err = 0;
-		for (int i = 0; i < j->ndeps; ++i)
-			for (;;) {
-				const h264_job_t *o = NULL;
-				for (long k = as->tail; k < as->head; ++k)
-					if (as->fifo[k % AS_MAX]->seq == j->deps[i]) o = as->fifo[k % AS_MAX];
-				if (!o) break;
-				if (o->done) {
-					dep_err |= o->err;
-					break;
-				}
-				pthread_cond_wait(&as->cv_done, &as->mu);
+		for (;;) {
+			while (as->qtail < as->qhead && as->queue[as->qtail % AS_MAX]->taken) as->qtail++;
+			for (long k = as->qtail; k < as->qhead && !j; ++k) {
+				h264_job_t *c = as->queue[k % AS_MAX];
+				dep_err = 0;
+				if (!c->taken && deps_ready(as, c, &dep_err)) j = c;
 			}
+			if (j || (as->quit && as->qtail == as->qhead)) break;
+			pthread_cond_wait(&as->cv_work, &as->mu);
+		}
+		if (!j) break;
+		j->taken = 1;
 		pthread_mutex_unlock(&as->mu);
 		if (dep_err) j->err = 1;
 		else job_run(j);
 		pthread_mutex_lock(&as->mu);
 		j->done = 1;
 		pthread_cond_broadcast(&as->cv_done);
+		pthread_cond_broadcast(&as->cv_work); /* jobs waiting on this one may be ready */
 	}
 	pthread_mutex_unlock(&as->mu);
 	return NULL;
@@ -227,6 +240,10 @@ int h264_async_start(h264_dec_t *d, int threads)
 	pthread_cond_init(&as->cv_work, NULL);
 	pthread_cond_init(&as->cv_done, NULL);
 	as->depth = threads + 2;
+	{
+		const char *e = getenv("M2DEC_AMD_PARSE_DEPTH"); /* tuning: pictures in flight past the oldest */
+		if (e && atoi(e) > 0) as->depth = atoi(e) < AS_MAX - 2 ? atoi(e) : AS_MAX - 2;
+	}
 	for (int i = 0; i < 17; ++i) as->col_last[i] = -1;
 	for (int i = 0; i < threads; ++i) {
 		if (pthread_create(&as->th[i], NULL, worker, as) != 0) break;

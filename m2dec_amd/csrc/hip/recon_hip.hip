@@ -486,11 +486,22 @@ __device__ __forceinline__ int avail8(int b, int a)
 /* wave-level sync for the intra wavefront, which runs on ONE wave of its workgroup: lanes talk
  * through LDS only, so an LDS drain + wave barrier suffices (outstanding global prefetches are not
  * waited for) */
+#ifdef M2DEC_WSYNC_WAIT
 #define WSYNC()                                                  \
 	do {                                                         \
 		asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");       \
 		__builtin_amdgcn_wave_barrier();                         \
 	} while (0)
+#else
+/* a wave's LDS operations are performed in issue order, so a later ds_read of this wave sees its
+ * earlier ds_writes without waiting for them: only the compiler must not move memory operations
+ * across the step boundary */
+#define WSYNC()                                                  \
+	do {                                                         \
+		asm volatile("" ::: "memory");                           \
+		__builtin_amdgcn_wave_barrier();                         \
+	} while (0)
+#endif
 
 union MbWords {
 	m2r_mb_t m;
@@ -662,7 +673,7 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 							nv[k] = *a;
 						}
 						v = ipred_taps(w, 4, nv);
-						ok = (av & c_req4[mode]) == c_req4[mode];
+						ok = (av & d_req4(mode)) == d_req4(mode);
 					}
 					const int base = ok ? v : *d; /* the reference leaves the sample as it was */
 					*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
@@ -748,7 +759,7 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 						int nv[3];
 #pragma unroll
 						for (int k = 0; k < 3; ++k) nv[k] = F[(w >> (5 * k)) & 31];
-						v = ((av & c_req8[mode]) == c_req8[mode]) ? ipred_taps(w, 5, nv) : -1;
+						v = ((av & d_req8(mode)) == d_req8(mode)) ? ipred_taps(w, 5, nv) : -1;
 					}
 					uint8_t *d = &L[oy + 1 + (t >> 3)][1 + ox + (t & 7)];
 					const int base = (v >= 0) ? v : *d;

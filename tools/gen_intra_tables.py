@@ -166,14 +166,20 @@ def main():
             for p in range(64):
                 taps, s = taps8(m, p & 7, p >> 3)
                 assert evaluate(t8[m][p], 5, N8) == (sum(w * N8[i] for i, w in taps) + ((1 << s) >> 1)) >> s
+    REQ4 = [2, 1, 0, 0, 3, 3, 3, 0, 1]
+    REQ8 = [2, 1, 0, 2, 11, 11, 11, 2, 1]
     out = ["/* Generated by tools/gen_intra_tables.py -- do not edit.  Table-driven 4x4 / 8x8 intra prediction:",
            " * word = idx0 | idx1 << B | idx2 << 2B | w0 << 3B | w1 << 3B+2 | w2 << 3B+4 | shift << 3B+6",
            " * (B = 4 for 4x4, 5 for 8x8); sample = (w0 N[idx0] + w1 N[idx1] + w2 N[idx2] + rnd) >> shift. */",
            "#pragma once",
            "#include <stdint.h>",
-           "/* neighbour availability a mode needs: 4x4 avail bits (1 left, 2 top); 8x8 (1 left, 2 top, 8 top-left) */",
-           "__constant__ static const uint8_t c_req4[9] = {2, 1, 0, 0, 3, 3, 3, 0, 1};",
-           "__constant__ static const uint8_t c_req8[9] = {2, 1, 0, 2, 11, 11, 11, 2, 1};",
+           "/* neighbour availability a mode needs: 4x4 avail bits (1 left, 2 top), 2 bits per mode; 8x8 (1 left,",
+           " * 2 top, 8 top-left), 4 bits per mode.  Packed immediates: a per-lane index into a __constant__",
+           " * array compiles to a vector memory load on the block chain. */",
+           f"#define M2D_REQ4_PACKED 0x{sum(v << (2 * i) for i, v in enumerate(REQ4)):x}u",
+           f"#define M2D_REQ8_PACKED 0x{sum(v << (4 * i) for i, v in enumerate(REQ8)):x}ull",
+           "__device__ __forceinline__ int d_req4(int mode) { return (int)((M2D_REQ4_PACKED >> (2 * mode)) & 3u); }",
+           "__device__ __forceinline__ int d_req8(int mode) { return (int)((M2D_REQ8_PACKED >> (4 * mode)) & 15u); }",
            "__constant__ static const uint32_t c_ipred4[9][16] = {"]
     for m in range(9):
         out.append("\t{" + ", ".join(f"0x{w:06x}" for w in t4[m]) + "},")

@@ -25,6 +25,11 @@
 #include <algorithm>
 #include "recon_kernels.h"
 #include "intra_tables.h"
+
+/* The workgroup's dynamic LDS.  Out-of-line device functions derive their LDS pointers from this
+ * symbol instead of taking them as arguments: a pointer argument is generic, and every access
+ * through it compiles to a flat_* instruction (vector-memory latency, vmcnt waits) instead of ds_*. */
+extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
 #include "recon_internal.h"
 #include "m2dec_amd.h"
 
@@ -56,7 +61,7 @@ __device__ unsigned long long g_pstamps[256][4];
 #define STAMPI(row, role, idx, val) do { } while (0)
 #endif
 /* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
-#define STAMPX(x, k) do { if ((x) < 16) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
+#define STAMPX(x, k) do { if ((x) < 16 && part == 0) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
 /* ======================================================================== motion compensation */
 struct RefPlane {
@@ -383,6 +388,7 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 
 /* ======================================================================== intra prediction (per sample) */
 #define LW 25 /* intra luma context row: [0] = x0 - 1, [1..24] = x0 .. x0 + 23 */
+static_assert(LW == M2D_IPRED4O_LW, "c_ipred4o offsets assume this luma context stride");
 
 /* 8x8 on filtered neighbours pt[0..15], lf[0..7], tlf (spec 8.3.2.2; h264.cpp:3301-3929); the
  * directional modes go through intra_tables.h, this is used for DC */
@@ -533,7 +539,7 @@ struct IntraLDS {
  * neighbours).  progress: this part's per-row progress words; HBI granules 0,1 luma, 2,3 chroma. */
 /* the prediction tables of intra_tables.h, staged in LDS once per workgroup */
 struct IntraTables {
-	uint32_t p4[9][16];
+	uint32_t p4o[2][9][16];
 	uint32_t p8[9][64];
 };
 
@@ -551,9 +557,13 @@ __device__ __forceinline__ int ipred_taps(uint32_t w, int bits, const int *nv)
  * wave(s) with do_chroma (disjoint LDS: L, R[0..255], DC, F, HV / C, R[256..383]).  q: the MB's pool
  * segment (staged in LDS).  Reference: mb_intra4x4 / intraNxN / intra16x16 / intrapcm
  * (h264.cpp:3121-3254, 4083-4127, 4407-4555, 4708-4761), residual_chroma (2374-2461). */
-__device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *q, const int t, const bool do_luma,
+__device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *q, const int t_in, const bool do_luma,
                                               const bool do_chroma, IntraLDS *ctx, const IntraTables *tabs)
 {
+	/* the lane index laundered per call: inside intra_row's MB loop every lane-dependent address
+	 * below would otherwise be hoisted out of the loop and held in registers (spills) */
+	int t = t_in;
+	asm volatile("" : "+v"(t));
 	uint8_t(&L)[17][LW] = ctx->L;
 	uint8_t(&C)[2][9][9] = ctx->C;
 	int(&R)[256 + 128] = ctx->R;
@@ -611,72 +621,74 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 		if (!do_luma) {
 			/* chroma wave: no luma */
 		} else if (m.kind == M2R_MB_I4x4) {
-			/* residual of all 16 blocks first (independent of the prediction), then the serial
-			 * block chain: predict + add, one wave sync per block */
-			for (int k = t; k < 256; k += 64) {
-				const int blk = k >> 4, pos = k & 15;
-				int v = 0;
-				if ((m.nz >> blk) & 1) v = q[d_luma_off(m, blk) + pos] * d_scale4(qp, pos & 3, pos >> 2);
-				R[k] = v;
-			}
-			WSYNC();
-			{
-				int *p = &R[(t >> 2) * 16 + (t & 3) * 4];
-				int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
-				d_idct4_1d(a0, a1, a2, a3);
-				p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
-			}
-			WSYNC();
-			{
-				int *p = &R[(t >> 2) * 16 + (t & 3)];
-				int a0 = p[0], a1 = p[4], a2 = p[8], a3 = p[12];
-				d_idct4_1d(a0, a1, a2, a3);
-				p[0] = (a0 + 32) >> 6; p[4] = (a1 + 32) >> 6; p[8] = (a2 + 32) >> 6; p[12] = (a3 + 32) >> 6;
-			}
-			WSYNC();
-			/* the serial block chain, table-driven (intra_tables.h): per block one table word
-			 * (fetched a block ahead), three neighbour reads, one sync */
-			uint32_t wn = 0;
+			/* residual first (independent of the prediction): lane t < 16 dequantises and inverse
+			 * transforms block t in registers */
 			if (t < 16) {
-				const int mode0 = (int)(m.ipred[0] & 15);
-				wn = tabs->p4[mode0 == 2 ? 0 : mode0][t];
-			}
-			for (int blk = 0; blk < 16; ++blk) {
-				const int ox = d_blk_x(blk) * 4, oy = d_blk_y(blk) * 4;
-				const int av = avail4(blk, m.avail_luma);
-				const int mode = (int)((((blk >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (blk & 7))) & 15);
-				const uint32_t w = wn;
-				if (t < 16 && blk < 15) {
-					const int nb = blk + 1;
-					const int mn = (int)((((nb >> 3) ? m.ipred[1] : m.ipred[0]) >> (4 * (nb & 7))) & 15);
-					wn = tabs->p4[mn == 2 ? 0 : mn][t];
-				}
-				if (t < 16) {
-					uint8_t *d = &L[oy + 1 + (t >> 2)][1 + ox + (t & 3)];
-					int v;
-					bool ok;
-					if (mode == 2) {
-						/* DC: (avail & 3) picks the sum (pred4x4_dc family) */
-						const uint8_t *tp = &L[oy][1 + ox];
-						int st = tp[0] + tp[1] + tp[2] + tp[3];
-						int sl = L[oy + 1][ox] + L[oy + 2][ox] + L[oy + 3][ox] + L[oy + 4][ox];
-						v = ((av & 3) == 3) ? (st + sl + 4) >> 3 : ((av & 1) ? (sl + 2) >> 2 : ((av & 2) ? (st + 2) >> 2 : 128));
-						ok = true;
-					} else {
-						/* neighbour index -> LDS: 0 top-left, 1..8 top (top-right -> P3 if unavailable), 9..12 left */
-						int nv[3];
+				int c[16];
 #pragma unroll
-						for (int k = 0; k < 3; ++k) {
-							const int i = (int)((w >> (4 * k)) & 15);
-							const int pi = (i - 1 >= 4 && !(av & 4)) ? 3 : i - 1;
-							const uint8_t *a = (i == 0) ? &L[oy][ox] : (i <= 8) ? &L[oy][1 + ox + pi] : &L[oy + 1 + (i - 9)][ox];
-							nv[k] = *a;
-						}
-						v = ipred_taps(w, 4, nv);
-						ok = (av & d_req4(mode)) == d_req4(mode);
-					}
-					const int base = ok ? v : *d; /* the reference leaves the sample as it was */
-					*d = (uint8_t)d_clip255(base + R[blk * 16 + t]);
+				for (int i = 0; i < 16; ++i) c[i] = 0;
+				if ((m.nz >> t) & 1) {
+					const int16_t *src = q + d_luma_off(m, t);
+#pragma unroll
+					for (int i = 0; i < 16; ++i) c[i] = src[i] * d_scale4(qp, i & 3, i >> 2);
+				}
+#pragma unroll
+				for (int r = 0; r < 4; ++r) d_idct4_1d(c[4 * r], c[4 * r + 1], c[4 * r + 2], c[4 * r + 3]);
+#pragma unroll
+				for (int k = 0; k < 4; ++k) {
+					d_idct4_1d(c[k], c[4 + k], c[8 + k], c[12 + k]);
+					c[k] = (c[k] + 32) >> 6;
+					c[4 + k] = (c[4 + k] + 32) >> 6;
+					c[8 + k] = (c[8 + k] + 32) >> 6;
+					c[12 + k] = (c[12 + k] + 32) >> 6;
+				}
+#pragma unroll
+				for (int i = 0; i < 16; ++i) R[t * 16 + i] = c[i];
+			}
+			/* the block chain in anti-diagonal steps: block (bx, by) needs its left, top, top-left and
+			 * top-right blocks, all on earlier steps of s = bx + 2 by, so the 16 blocks take 10 steps of
+			 * at most two blocks (lanes 0-15 / 16-31, one sample each).  Per step: one prediction word
+			 * (LDS offsets of three taps, weights, shift; fetched for all steps up front), the taps, the
+			 * DC sums, one residual read, one write. */
+			const uint64_t modes = (uint64_t)m.ipred[0] | ((uint64_t)m.ipred[1] << 32);
+			uint64_t avs = 0;
+#pragma unroll
+			for (int blk = 0; blk < 16; ++blk) avs |= (uint64_t)avail4(blk, m.avail_luma) << (4 * blk);
+			const int slot = t >> 4, px = t & 15;
+			/* lane's prediction word of step s (0 for an idle lane) */
+			auto word = [&](int s) -> uint32_t {
+				const int by = max(0, (s - 2) >> 1) + slot, bx = s - 2 * by;
+				const int blk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);
+				const int mode = (int)((modes >> (4 * (blk & 15))) & 15);
+				const int av = (int)((avs >> (4 * (blk & 15))) & 15);
+				return (t < 32 && by <= min(3, s >> 1)) ? tabs->p4o[(av & 4) ? 0 : 1][mode][px] : 0u;
+			};
+			uint32_t wn = word(0);
+			WSYNC();
+			uint8_t *const L0 = &L[0][0];
+#pragma unroll
+			for (int s = 0; s < 10; ++s) {
+				const uint32_t w = wn;
+				if (s < 9) wn = word(s + 1); /* a step ahead: off the step's LDS round trip */
+				const int by = max(0, (s - 2) >> 1) + slot, bx = s - 2 * by;
+				if (t < 32 && by <= min(3, s >> 1)) {
+					const int blk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);
+					const int mode = (int)((modes >> (4 * blk)) & 15);
+					const int av = (int)((avs >> (4 * blk)) & 15);
+					const uint8_t *nb = L0 + (by * 4) * LW + bx * 4; /* the block's top-left neighbour */
+					uint8_t *d = L0 + (by * 4 + 1 + (px >> 2)) * LW + bx * 4 + 1 + (px & 3);
+					const int n0 = nb[w & 255], n1 = nb[(w >> 8) & 255], n2 = nb[(w >> 16) & 255];
+					const int st = nb[1] + nb[2] + nb[3] + nb[4];
+					const int sl = nb[LW] + nb[2 * LW] + nb[3 * LW] + nb[4 * LW];
+					const int old = *d, res = R[blk * 16 + px];
+					const int sh = (int)(w >> 30);
+					const int pv = ((int)((w >> 24) & 3) * n0 + (int)((w >> 26) & 3) * n1 + (int)((w >> 28) & 3) * n2 + ((1 << sh) >> 1)) >> sh;
+					/* DC: (avail & 3) picks the sum (pred4x4_dc family) */
+					const int dv = ((av & 3) == 3) ? (st + sl + 4) >> 3 : ((av & 1) ? (sl + 2) >> 2 : ((av & 2) ? (st + 2) >> 2 : 128));
+					const int req = d_req4(mode);
+					/* a mode whose neighbours are missing leaves the sample as it was (the reference) */
+					const int base = (mode == 2) ? dv : (((av & req) == req) ? pv : old);
+					*d = (uint8_t)d_clip255(base + res);
 				}
 				WSYNC();
 			}
@@ -899,10 +911,12 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 	}
 }
 
-__device__ void intra_row(const int y, const int t, const int part, IntraLDS *ctx, const IntraTables *tabs,
+__device__ __attribute__((noinline)) void intra_row(const int y, const int t, const int part, const int wave,
                           const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
                           uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
 {
+	IntraLDS *const ctx = (IntraLDS *)g_lds + wave; /* row blocks: 4 contexts, then the tables */
+	const IntraTables *const tabs = (const IntraTables *)((IntraLDS *)g_lds + 4);
 	const bool do_luma = part == 0, do_chroma = part != 0;
 	uint8_t(&L)[17][LW] = ctx->L;
 	uint8_t(&C)[2][9][9] = ctx->C;
@@ -1074,10 +1088,17 @@ __device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int
  * done), the MB is reconstructed by intra_mb_body (wave 0 luma, wave 1 chroma) and written to the
  * frame and to `tile`.
  */
+/* LDS layout of an inter worker: one intra context, the prediction tables, a 384-byte output tile */
+__device__ __forceinline__ IntraLDS *worker_ictx() { return (IntraLDS *)g_lds; }
+__device__ __forceinline__ IntraTables *worker_tabs() { return (IntraTables *)(worker_ictx() + 1); }
+__device__ __forceinline__ uint8_t *worker_tile() { return (uint8_t *)(worker_tabs() + 1); }
+
 __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, const m2r_mb_t m, const int16_t *__restrict__ pool, uint8_t *cur,
-                            int W, int H, int Wmb, const uint8_t *hbp, int rs, IntraLDS *ctx, const IntraTables *tabs,
-                            uint8_t *tile)
+                            int W, int H, int Wmb, const uint8_t *hbp, int rs)
 {
+	IntraLDS *const ctx = worker_ictx();
+	const IntraTables *const tabs = worker_tabs();
+	uint8_t *const tile = worker_tile();
 	const int t = threadIdx.x;
 	const int nq = d_mb_ncoef(m);
 	for (int k = t; k < nq; k += blockDim.x) ctx->Q[0][k] = pool[m.coef + k];
@@ -1151,12 +1172,11 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 	const m2r_mb_t *__restrict__ mbs = a.mbs;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
 	/* intra MBs of this picture: an LDS context, the prediction tables and an output tile */
-	IntraLDS *ictx = (IntraLDS *)smem;
-	IntraTables *tabs = (IntraTables *)(ictx + 1);
-	uint8_t *tile = (uint8_t *)(tabs + 1);
+	IntraTables *tabs = worker_tabs();
+	uint8_t *tile = worker_tile();
 	const bool recs = a.n_intra != 0;
 	if (recs) {
-		for (int i = t; i < 9 * 16; i += blockDim.x) tabs->p4[i >> 4][i & 15] = c_ipred4[i >> 4][i & 15];
+		for (int i = t; i < 2 * 9 * 16; i += blockDim.x) (&tabs->p4o[0][0][0])[i] = (&c_ipred4o[0][0][0])[i];
 		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
 	}
 	/* Single-lane work in this loop is done by the whole of wave 0 under a SCALAR branch, the one
@@ -1291,7 +1311,7 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 				if (inter)
 					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr);
 				else
-					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, ictx, tabs, tile);
+					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs);
 				if (rec) {
 					__syncthreads();
 					write_nb_record(a.hbp, rs, x, y, tile, t);
@@ -1752,8 +1772,9 @@ __device__ void war_wait(const PictureArgs &a)
 
 /* one pair of MB rows (yA, yA + 1) by the whole workgroup: the I-picture intra wavefront (phase A),
  * then deblocking (phase B), then the picture's row-pair counter (and the verification copy-out) */
-__device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict__ ap, const int yA, uint8_t *smem)
+__device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict__ ap, const int yA)
 {
+	uint8_t *const smem = g_lds;
 	const PictureArgs &a = *ap;
 	const int t = threadIdx.x;
 	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
@@ -1770,14 +1791,14 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 		 * on their per-item done flags.) */
 		if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		IntraTables *tabs = (IntraTables *)((IntraLDS *)smem + 4);
-		for (int i = t; i < 9 * 16; i += blockDim.x) tabs->p4[i >> 4][i & 15] = c_ipred4[i >> 4][i & 15];
+		for (int i = t; i < 2 * 9 * 16; i += blockDim.x) (&tabs->p4o[0][0][0])[i] = (&c_ipred4o[0][0][0])[i];
 		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
 		__syncthreads();
 		const int w = __builtin_amdgcn_readfirstlane(t) >> 6;
 		const int r = w & 1, part = w >> 1;
 		if (r < nrows) {
 			__builtin_amdgcn_s_setprio(3); /* the intra wavefront is an I picture's critical path */
-			intra_row(yA + r, t & 63, part, (IntraLDS *)smem + w, tabs, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
+			intra_row(yA + r, t & 63, part, w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
 			          a.scratch + (part ? SCR_IPROGC(a.Hmb) : SCR_IPROG(a.Hmb)), hbi_ready, a.err);
 			/* write the intra samples back out of this XCD's L2 now: rows 13..15 of an MB row are
 			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
@@ -1857,15 +1878,14 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 			break;
 		}
 		if (pair >= (a.Hmb + 1) / 2) break;
-		row_pair(&a, 2 * pair, smem);
+		row_pair(&a, 2 * pair);
 	}
 }
 
 __global__ __launch_bounds__(256, 3) void k_batch(const PictureArgs *pics, int bpp)
 {
-	extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 	const int p = blockIdx.x / bpp;
-	picture_block(pics[p], blockIdx.x - p * bpp, smem);
+	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
 }
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)

@@ -16,6 +16,7 @@ import random
 import sys
 
 TL4, P4, L4 = 0, 1, 9
+LW = 25  # luma context row stride (recon_hip.hip)
 TL8, PT8, LF8 = 24, 0, 16
 
 
@@ -166,6 +167,37 @@ def main():
             for p in range(64):
                 taps, s = taps8(m, p & 7, p >> 3)
                 assert evaluate(t8[m][p], 5, N8) == (sum(w * N8[i] for i, w in taps) + ((1 << s) >> 1)) >> s
+    # offset form of the 4x4 table over the luma context L[17][LW] (see recon_hip.hip IntraLDS)
+    def off4(i, tr):
+        if i == 0:
+            return 0
+        if i <= 8:
+            return min(i, 4) if tr else i
+        return (i - 8) * LW
+    t4o = [[[0] * 16 for _ in range(9)] for _ in range(2)]
+    for tr in range(2):
+        for m in range(9):
+            if m == 2:
+                continue
+            for p in range(16):
+                idx, wts, sh = unpack(t4[m][p], 4)
+                w = sum(off4(i, tr) << (8 * k) for k, i in enumerate(idx))
+                w |= sum(wt << (24 + 2 * k) for k, wt in enumerate(wts)) | (sh << 30)
+                t4o[tr][m][p] = w
+    for _ in range(200):  # the offset form reads the same samples out of a context array
+        ctx = [rnd.randrange(256) for _ in range(5 * LW)]
+        for tr in range(2):
+            N4 = [ctx[0]] + [ctx[min(i, 4) if tr else i] for i in range(1, 9)] + [ctx[k * LW] for k in range(1, 5)]
+            for m in range(9):
+                if m == 2:
+                    continue
+                for p in range(16):
+                    w = t4o[tr][m][p]
+                    o = [(w >> (8 * k)) & 255 for k in range(3)]
+                    wt = [(w >> (24 + 2 * k)) & 3 for k in range(3)]
+                    sh = w >> 30
+                    got = (sum(a * ctx[b] for a, b in zip(wt, o)) + ((1 << sh) >> 1)) >> sh
+                    assert got == evaluate(t4[m][p], 4, N4)
     REQ4 = [2, 1, 0, 0, 3, 3, 3, 0, 1]
     REQ8 = [2, 1, 0, 2, 11, 11, 11, 2, 1]
     out = ["/* Generated by tools/gen_intra_tables.py -- do not edit.  Table-driven 4x4 / 8x8 intra prediction:",
@@ -180,9 +212,16 @@ def main():
            f"#define M2D_REQ8_PACKED 0x{sum(v << (4 * i) for i, v in enumerate(REQ8)):x}ull",
            "__device__ __forceinline__ int d_req4(int mode) { return (int)((M2D_REQ4_PACKED >> (2 * mode)) & 3u); }",
            "__device__ __forceinline__ int d_req8(int mode) { return (int)((M2D_REQ8_PACKED >> (4 * mode)) & 15u); }",
-           "__constant__ static const uint32_t c_ipred4[9][16] = {"]
-    for m in range(9):
-        out.append("\t{" + ", ".join(f"0x{w:06x}" for w in t4[m]) + "},")
+           "/* 4x4 in LDS-offset form: c_ipred4o[tr][mode][pixel] = off0 | off1 << 8 | off2 << 16 | w0 << 24 |",
+           " * w1 << 26 | w2 << 28 | shift << 30, offsets from the block's top-left neighbour in the luma context",
+           f" * (row stride LW = {LW}); tr = 1: top-right unavailable (P4..P7 read P3). */",
+           f"#define M2D_IPRED4O_LW {LW}",
+           "__constant__ static const uint32_t c_ipred4o[2][9][16] = {"]
+    for tr in range(2):
+        out.append("\t{")
+        for m in range(9):
+            out.append("\t\t{" + ", ".join(f"0x{w:08x}" for w in t4o[tr][m]) + "},")
+        out.append("\t},")
     out.append("};")
     out.append("__constant__ static const uint32_t c_ipred8[9][64] = {")
     for m in range(9):

@@ -30,6 +30,20 @@
  * symbol instead of taking them as arguments: a pointer argument is generic, and every access
  * through it compiles to a flat_* instruction (vector-memory latency, vmcnt waits) instead of ds_*. */
 extern __shared__ __attribute__((aligned(16))) uint8_t g_lds[];
+/* an LDS address as a 32-bit local pointer: out-of-line functions take this (a generic pointer
+ * argument would make every access flat_*, and g_lds named in a non-kernel function is looked up
+ * in a dynamic-LDS offset table with a scalar load at every use) */
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+/* the base, made opaque at the call site (in a kernel it is a constant offset) so that the callee is
+ * not specialised back onto g_lds by interprocedural constant propagation */
+__device__ __forceinline__ lds_u8 *lds_base()
+{
+	uint32_t v = (uint32_t)(uintptr_t)(lds_u8 *)g_lds;
+	asm volatile("" : "+s"(v));
+	return (lds_u8 *)(uintptr_t)v;
+}
+#define LDS_ARG() lds_base()
+template <typename T> __device__ __forceinline__ T *lds_ptr(lds_u8 *p) { return (T *)(uint8_t *)p; }
 #include "recon_internal.h"
 #include "m2dec_amd.h"
 
@@ -203,6 +217,18 @@ __device__ __forceinline__ bool poll_ge(int *flag, int need, int *err)
 	}
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the payload loads below the poll */
 	return true;
+}
+
+/* poll_ge returning the value seen (>= need; need - 1 after a failed spin) */
+__device__ __forceinline__ int poll_get(int *flag, int need, int *err)
+{
+	unsigned spins = 0;
+	int v;
+	while ((v = __hip_atomic_load((gi32 *)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+		if (!spin_ok(spins, err, 2)) return need - 1;
+	}
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the payload loads below the poll */
+	return v;
 }
 
 __device__ __forceinline__ void signal_progress(int *flag, int value)
@@ -911,12 +937,12 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 	}
 }
 
-__device__ __attribute__((noinline)) void intra_row(const int y, const int t, const int part, const int wave,
+__device__ __attribute__((noinline)) void intra_row(const int y, const int t, const int part, lds_u8 *lds, const int wave,
                           const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
-                          uint8_t *hbi, int *progress, const int *hbi_ready, int *err)
+                          uint8_t *hbi, int *progress, int *err)
 {
-	IntraLDS *const ctx = (IntraLDS *)g_lds + wave; /* row blocks: 4 contexts, then the tables */
-	const IntraTables *const tabs = (const IntraTables *)((IntraLDS *)g_lds + 4);
+	IntraLDS *const ctx = lds_ptr<IntraLDS>(lds) + wave; /* row blocks: 4 contexts, then the tables */
+	const IntraTables *const tabs = (const IntraTables *)(lds_ptr<IntraLDS>(lds) + 4);
 	const bool do_luma = part == 0, do_chroma = part != 0;
 	uint8_t(&L)[17][LW] = ctx->L;
 	uint8_t(&C)[2][9][9] = ctx->C;
@@ -928,6 +954,7 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 	uint8_t *chroma = cur + (size_t)W * H;
 	int prev_x = -2;
 	int qb = 0;
+	int seen_up = 0;
 	const int y0 = y * 16;
 
 	for (int xb = 0; xb < Wmb; xb += 64) {
@@ -979,8 +1006,8 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 			int need = 0;
 			for (int d = -1; d <= 1; ++d)
 				if (up_intra(x + d)) need = x + d + 1;
-			if (need) poll_ge(&progress[y - 1], need, err);
-			poll_ge((int *)&hbi_ready[y - 1], 1, err); /* the row above's inter MBs' bottom rows */
+			/* the row above's progress as last seen: poll only when it is not far enough */
+			if (need > seen_up) seen_up = poll_get(&progress[y - 1], need, err);
 		}
 		/* ---- gather the neighbourhood */
 		if (left_in_lds) {
@@ -1089,16 +1116,16 @@ __device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int
  * frame and to `tile`.
  */
 /* LDS layout of an inter worker: one intra context, the prediction tables, a 384-byte output tile */
-__device__ __forceinline__ IntraLDS *worker_ictx() { return (IntraLDS *)g_lds; }
-__device__ __forceinline__ IntraTables *worker_tabs() { return (IntraTables *)(worker_ictx() + 1); }
-__device__ __forceinline__ uint8_t *worker_tile() { return (uint8_t *)(worker_tabs() + 1); }
+__device__ __forceinline__ IntraLDS *worker_ictx(lds_u8 *lds) { return lds_ptr<IntraLDS>(lds); }
+__device__ __forceinline__ IntraTables *worker_tabs(lds_u8 *lds) { return (IntraTables *)(worker_ictx(lds) + 1); }
+__device__ __forceinline__ uint8_t *worker_tile(lds_u8 *lds) { return (uint8_t *)(worker_tabs(lds) + 1); }
 
 __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, const m2r_mb_t m, const int16_t *__restrict__ pool, uint8_t *cur,
-                            int W, int H, int Wmb, const uint8_t *hbp, int rs)
+                            int W, int H, int Wmb, const uint8_t *hbp, int rs, lds_u8 *lds)
 {
-	IntraLDS *const ctx = worker_ictx();
-	const IntraTables *const tabs = worker_tabs();
-	uint8_t *const tile = worker_tile();
+	IntraLDS *const ctx = worker_ictx(lds);
+	const IntraTables *const tabs = worker_tabs(lds);
+	uint8_t *const tile = worker_tile(lds);
 	const int t = threadIdx.x;
 	const int nq = d_mb_ncoef(m);
 	for (int k = t; k < nq; k += blockDim.x) ctx->Q[0][k] = pool[m.coef + k];
@@ -1172,8 +1199,8 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 	const m2r_mb_t *__restrict__ mbs = a.mbs;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
 	/* intra MBs of this picture: an LDS context, the prediction tables and an output tile */
-	IntraTables *tabs = worker_tabs();
-	uint8_t *tile = worker_tile();
+	IntraTables *tabs = worker_tabs(LDS_ARG());
+	uint8_t *tile = worker_tile(LDS_ARG());
 	const bool recs = a.n_intra != 0;
 	if (recs) {
 		for (int i = t; i < 2 * 9 * 16; i += blockDim.x) (&tabs->p4o[0][0][0])[i] = (&c_ipred4o[0][0][0])[i];
@@ -1311,7 +1338,7 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 				if (inter)
 					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr);
 				else
-					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs);
+					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, LDS_ARG());
 				if (rec) {
 					__syncthreads();
 					write_nb_record(a.hbp, rs, x, y, tile, t);
@@ -1772,9 +1799,9 @@ __device__ void war_wait(const PictureArgs &a)
 
 /* one pair of MB rows (yA, yA + 1) by the whole workgroup: the I-picture intra wavefront (phase A),
  * then deblocking (phase B), then the picture's row-pair counter (and the verification copy-out) */
-__device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict__ ap, const int yA)
+__device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict__ ap, const int yA, lds_u8 *lds)
 {
-	uint8_t *const smem = g_lds;
+	uint8_t *const smem = lds_ptr<uint8_t>(lds);
 	const PictureArgs &a = *ap;
 	const int t = threadIdx.x;
 	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
@@ -1782,14 +1809,12 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 	const int nrows = hasB ? 2 : 1;
 	const int Wmb = a.Wmb;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
-	int *hbi_ready = a.scratch + SCR_HBIRDY(a.Hmb);
 	STAMP(yA, 3, 0, 1);
 	if (!a.n_inter) {
 		/* ---- I picture, phase A: intra / PCM MBs as a wavefront over the row workgroups: luma of rows A / B
 		 * on waves 0 / 1, their chroma on waves 2 / 3, each wave with its own LDS context.  (P / B pictures:
 		 * the inter workers reconstruct every MB, intra ones included, and the deblocking below streams
 		 * on their per-item done flags.) */
-		if (t < nrows && yA + t + 1 < a.Hmb) __hip_atomic_store((gi32 *)&hbi_ready[yA + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		IntraTables *tabs = (IntraTables *)((IntraLDS *)smem + 4);
 		for (int i = t; i < 2 * 9 * 16; i += blockDim.x) (&tabs->p4o[0][0][0])[i] = (&c_ipred4o[0][0][0])[i];
 		for (int i = t; i < 9 * 64; i += blockDim.x) tabs->p8[i >> 6][i & 63] = c_ipred8[i >> 6][i & 63];
@@ -1798,8 +1823,8 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 		const int r = w & 1, part = w >> 1;
 		if (r < nrows) {
 			__builtin_amdgcn_s_setprio(3); /* the intra wavefront is an I picture's critical path */
-			intra_row(yA + r, t & 63, part, w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
-			          a.scratch + (part ? SCR_IPROGC(a.Hmb) : SCR_IPROG(a.Hmb)), hbi_ready, a.err);
+			intra_row(yA + r, t & 63, part, lds, w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
+			          a.scratch + (part ? SCR_IPROGC(a.Hmb) : SCR_IPROG(a.Hmb)), a.err);
 			/* write the intra samples back out of this XCD's L2 now: rows 13..15 of an MB row are
 			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
 			 * write-back of our dirty unfiltered bytes would land on top of them */
@@ -1878,7 +1903,7 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 			break;
 		}
 		if (pair >= (a.Hmb + 1) / 2) break;
-		row_pair(&a, 2 * pair);
+		row_pair(&a, 2 * pair, LDS_ARG());
 	}
 }
 

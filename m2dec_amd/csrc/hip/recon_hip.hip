@@ -939,7 +939,7 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 
 __device__ __attribute__((noinline)) void intra_row(const int y, const int t, const int part, lds_u8 *lds, const int wave,
                           const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
-                          uint8_t *hbi, int *progress, int *err)
+                          uint8_t *hbi, const uint32_t tag, int *err)
 {
 	IntraLDS *const ctx = lds_ptr<IntraLDS>(lds) + wave; /* row blocks: 4 contexts, then the tables */
 	const IntraTables *const tabs = (const IntraTables *)(lds_ptr<IntraLDS>(lds) + 4);
@@ -954,7 +954,6 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 	uint8_t *chroma = cur + (size_t)W * H;
 	int prev_x = -2;
 	int qb = 0;
-	int seen_up = 0;
 	const int y0 = y * 16;
 
 	for (int xb = 0; xb < Wmb; xb += 64) {
@@ -1002,35 +1001,47 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 		}
 		const int x0 = x * 16;
 		const int left_in_lds = (prev_x == x - 1);
-		if (y > 0) {
-			int need = 0;
-			for (int d = -1; d <= 1; ++d)
-				if (up_intra(x + d)) need = x + d + 1;
-			/* the row above's progress as last seen: poll only when it is not far enough */
-			if (need > seen_up) seen_up = poll_get(&progress[y - 1], need, err);
-		}
 		/* ---- gather the neighbourhood */
 		if (left_in_lds) {
 			if (do_luma && t < 17) L[t][0] = L[t][16];
 			if (do_chroma && t < 18) { int c = t / 9, r = t % 9; C[c][r][0] = C[c][r][8]; }
 		}
 		WSYNC();
-		if (y > 0 && t < 7 && (do_luma ? t < 4 : t >= 4)) {
-			/* granules of the row above: 0,1 luma MB x; 2 luma MB x+1 (bytes 0..7); 3 luma MB x-1 (bytes 8..15);
-			 * 4,5 chroma MB x; 6 chroma MB x-1 (bytes 8..15) */
-			const int xs = (t == 2) ? x + 1 : ((t == 3 || t == 6) ? x - 1 : x);
-			const int isc = (t >= 4);
-			const int half = (t == 1 || t == 3 || t == 5 || t == 6) ? 1 : 0;
-			if (xs >= 0 && xs < Wmb) {
-				const unsigned long long v = ld_sc1(hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + isc * 16 + half * 8);
-				for (int b = 0; b < 8; ++b) {
-					uint8_t s8 = (uint8_t)(v >> (8 * b));
-					int j = half * 8 + b; /* byte within the 16-byte MB row */
-					if (t == 0 || t == 1) L[0][1 + j] = s8;
-					else if (t == 2) L[0][17 + b] = s8;
-					else if (t == 3) { if (j == 15) L[0][0] = s8; }
-					else if (t == 4 || t == 5) C[j & 1][0][1 + (j >> 1)] = s8;
-					else if (j >= 14) C[j & 1][0][0] = s8;
+		if (y > 0) {
+			/* the row above's hand-off words (self-validating: a word is this picture's once its tag is):
+			 * luma wave lanes 0-2 MB x words 0-2, lanes 3-4 MB x+1 words 0-1, lane 5 MB x-1 word 2;
+			 * chroma wave lanes 0-2 MB x words 3-5, lane 3 MB x-1 word 5 */
+			const int nw = do_luma ? 6 : 4;
+			const int xs = (t < 3) ? x : ((do_luma && t < 5) ? x + 1 : x - 1);
+			const int wi = (t < 3) ? t : ((do_luma && t < 5) ? t - 3 : 2);
+			const bool mine_w = t < nw && xs >= 0 && xs < Wmb && up_intra(xs);
+			const uint8_t *src = hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + (do_luma ? 0 : 24) + wi * 8;
+			unsigned long long v = 0;
+			unsigned spins = 0;
+			for (;;) {
+				bool ok = true;
+				if (mine_w) {
+					v = ld_sc1(src);
+					ok = (uint32_t)(v >> 48) == tag;
+				}
+				if (__all(ok)) break;
+				if (!spin_ok(spins, err, 2)) break;
+			}
+			if (mine_w) {
+#pragma unroll
+				for (int b = 0; b < 6; ++b) {
+					const uint8_t s8 = (uint8_t)(v >> (8 * b));
+					const int j = wi * 6 + b; /* byte within the 16-byte bottom row */
+					if (j < 16) {
+						if (do_luma) {
+							if (t < 3) L[0][1 + j] = s8;
+							else if (t < 5) { if (j < 8) L[0][17 + j] = s8; }
+							else if (j == 15) L[0][0] = s8;
+						} else {
+							if (t < 3) C[j & 1][0][1 + (j >> 1)] = s8;
+							else if (j >= 14) C[j & 1][0][0] = s8;
+						}
+					}
 				}
 			}
 		}
@@ -1051,17 +1062,17 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 				int cy = k >> 4, bx = k & 15;
 				chroma[(size_t)(y0 / 2 + cy) * W + x0 + bx] = C[bx & 1][1 + cy][1 + (bx >> 1)];
 			}
-		if (t < 4 && (do_luma ? t < 2 : t >= 2)) {
-			unsigned long long v = 0;
-			for (int b = 0; b < 8; ++b) {
-				int j = (t & 1) * 8 + b;
-				uint8_t s8 = (t < 2) ? L[16][1 + j] : C[j & 1][8][1 + (j >> 1)];
-				v |= (unsigned long long)s8 << (8 * b);
+		if (t < 3) {
+			/* hand-off words: 6 bottom-row bytes + the picture's 16-bit tag (no progress word, no drain) */
+			unsigned long long v = (unsigned long long)tag << 48;
+#pragma unroll
+			for (int b = 0; b < 6; ++b) {
+				const int j = t * 6 + b;
+				if (j < 16) v |= (unsigned long long)(do_luma ? L[16][1 + j] : C[j & 1][8][1 + (j >> 1)]) << (8 * b);
 			}
-			st_sc1(hbi + ((size_t)y * Wmb + x) * HBI_BYTES + t * 8, v);
+			st_sc1(hbi + ((size_t)y * Wmb + x) * HBI_BYTES + (do_luma ? 0 : 24) + t * 8, v);
 		}
 		STAMPX(x, 4);
-		signal_progress(&progress[y], x + 1);
 		STAMP(y, 3, 16 + x, x);
 		STAMPX(x, 5);
 		/* the prefetched coefficients of the next intra MB */
@@ -1075,7 +1086,6 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 		WSYNC();
 		}
 	}
-	signal_progress(&progress[y], Wmb);
 }
 
 /* ======================================================================== inter workers */
@@ -1824,7 +1834,7 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 		if (r < nrows) {
 			__builtin_amdgcn_s_setprio(3); /* the intra wavefront is an I picture's critical path */
 			intra_row(yA + r, t & 63, part, lds, w, a.mbs, a.pool, cur, a.W, a.H, Wmb, a.hbi,
-			          a.scratch + (part ? SCR_IPROGC(a.Hmb) : SCR_IPROG(a.Hmb)), a.err);
+			          (uint32_t)(a.seq % 65535) + 1, a.err);
 			/* write the intra samples back out of this XCD's L2 now: rows 13..15 of an MB row are
 			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
 			 * write-back of our dirty unfiltered bytes would land on top of them */

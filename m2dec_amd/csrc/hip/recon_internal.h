@@ -8,7 +8,8 @@
 #include <stdint.h>
 #include "m2d_recon.h"
 
-#define HBI_BYTES 32 /* intra hand-off per MB: bottom luma row (16 B) + bottom chroma row (16 B) */
+#define HBI_BYTES 48 /* I-picture intra hand-off per MB: bottom luma row (16 B) + bottom chroma row (16 B) in six
+                        * u64 words of 6 bytes + a 16-bit picture tag each */
 #define HBD_BYTES 96 /* deblock hand-off per MB: luma rows 12..15 (4 x 16 B) + chroma rows 6..7 (2 x 16 B) */
 #define DBK_WAVES 4  /* deblocking workgroup: loader, filter A, storer, filter B waves */
 #define DBK_RING 16  /* deblocking: MB slots of the LDS ring (power of two) */

@@ -131,6 +131,10 @@ struct Sched {
 			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * 64 * (size_t)Hmb));
 		}
 		CHECK(hipMemset(rowflag, 0, sizeof(unsigned long long) * 64 * (size_t)Hmb));
+		/* the I-picture hand-off words carry a tag derived from seq, which restarts here: no word of an
+		 * earlier picture (or decoder) may be left holding a tag a new picture will use */
+		CHECK(hipMemset(hand, 0, hand_bytes() * NSTREAMS));
+		if (bt.hand) CHECK(hipMemset(bt.hand, 0, hand_bytes() * (size_t)bt.cap));
 		seq = 0;
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		for (int i = 0; i < 64; ++i) {
@@ -238,6 +242,7 @@ struct Sched {
 		batch_free();
 		CHECK(hipMalloc(&bt.words, sizeof(int) * ((size_t)2 * cap + (size_t)cap * SCR_WORDS(Hmb, Wmb))));
 		CHECK(hipMalloc(&bt.hand, hand_bytes() * (size_t)cap));
+		CHECK(hipMemset(bt.hand, 0, hand_bytes() * (size_t)cap)); /* tags: see the geometry setup */
 		for (int i = 0; i < Batch::NB; ++i) {
 			CHECK(hipMalloc(&bt.d_args[i], sizeof(PictureArgs) * cap));
 			CHECK(hipHostMalloc((void **)&bt.h_args[i], sizeof(PictureArgs) * cap, hipHostMallocDefault));

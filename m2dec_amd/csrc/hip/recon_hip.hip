@@ -1641,7 +1641,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 						*(ok ? DBK_ADDR(luma ? i : ci) : sink) = (uint8_t)v[i];
 					}
 #undef DBK_ADDR
-					__builtin_amdgcn_s_waitcnt(0xc07f); /* lgkmcnt(0): this direction's LDS writes landed */
+					/* the next direction's reads are this wave's later LDS operations: performed in order */
+					asm volatile("" ::: "memory");
 					__builtin_amdgcn_wave_barrier();
 				}
 			}

@@ -1918,7 +1918,13 @@ __device__ __forceinline__ void picture_block(const PictureArgs &a, const int b,
 	}
 }
 
-__global__ __launch_bounds__(256, 3) void k_batch(const PictureArgs *pics, int bpp)
+#ifndef M2DEC_MIN_BLOCKS
+/* workgroups per CU = waves per SIMD: the VGPR budget (3: 168, 4: 128, 5: 96).  The pictures in flight
+ * are bounded by the workgroup slots their waiting workers hold: 4 gives 1024 slots for +5-8 % (the extra
+ * call-stack spills cost less); 5 spills the filter and intra chains (-25 %).  profiles/r25_occupancy.txt */
+#define M2DEC_MIN_BLOCKS 4
+#endif
+__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_batch(const PictureArgs *pics, int bpp)
 {
 	const int p = blockIdx.x / bpp;
 	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);

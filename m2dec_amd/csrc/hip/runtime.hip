@@ -65,7 +65,7 @@ struct Sched {
 	unsigned long long *rowflag = nullptr; /* [64][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
 	int seq = 0;               /* pictures launched */
 	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
-	int inter_grid = 64;       /* persistent inter workers per picture (a quarter of the CUs) */
+	int inter_grid = 80;       /* persistent inter workers per picture (5/16 of the CUs) */
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	hipEvent_t ev[NEVENTS] = {};
@@ -87,7 +87,7 @@ struct Sched {
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		int cus = 0;
 		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-			inter_grid = cus / 4;
+			inter_grid = cus * 5 / 16; /* 80 on MI355X (sweep at 4 waves per SIMD: 64 -> 80 +3 %, 96+ slower) */
 		if (const char *g = getenv("M2DEC_AMD_INTER_WG")) /* tuning knob: inter workers per picture */
 			if (atoi(g) > 0) inter_grid = atoi(g);
 		if (const char *g = getenv("M2DEC_AMD_ROW_WG")) /* tuning knob: row-pair workgroups of a P / B picture */

@@ -190,6 +190,15 @@ __device__ __forceinline__ void st32_sc1(void *p, uint32_t v)
 	__hip_atomic_store((gi32 *)p, (int)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* 16-byte write-through store (global_store_dwordx4 … sc1): the deblocking storer writes whole 64-byte
+ * row pieces of 4 MBs with it, where 4-byte stores left a partial-line memory write per 16 bytes */
+__device__ __forceinline__ void st128_sc1(void *p, uint4 v)
+{
+	typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+	const u32x4 d = {v.x, v.y, v.z, v.w};
+	asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(d) : "memory");
+}
+
 __device__ __forceinline__ unsigned long long ld_sc1(const void *p)
 {
 	return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1654,16 +1663,27 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 
 	/* ---------------- storer (wave 2) */
 	{
-		int dA = 0, dA13 = 0, dB = 0, nst = 0, pubA = 0, pubB = 0;
+		int dA = 0, dA13 = 0, dB = 0, dH = 0, nst = 0, pubA = 0, pubB = 0;
 		unsigned spins = 0;
 		const int y0A = yA * 16, yc0A = yA * 8, y0B = yB * 16, yc0B = yB * 8;
+		/* frame stores go out in groups of 4 MBs (one 64-byte piece of each sample row, 16 bytes per lane,
+		 * write-through): a final-MB count is rounded down to 4 except at the row end */
+		auto g4 = [Wmb](int v) { return v >= Wmb ? Wmb : (v & ~3); };
+		/* n MBs from m0 of `rows` sample rows: frame row fy0 + r <- ring line rl0 + r of plane `ring` */
+		auto store_rows = [&](uint8_t *plane, int fy0, const uint8_t *ring, int rl0, int m0, int n, int rows) {
+			for (int k = t; k < n * rows; k += 64) {
+				const int r = k / n, mb = m0 + k - r * n;
+				st128_sc1(plane + (size_t)(fy0 + r) * W + mb * 16, *(const uint4 *)(ring + (rl0 + r) * S + (mb & (DBK_RING - 1)) * 16));
+			}
+		};
 		for (;;) {
 			const int cA = __hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 			const int cB = hasB ? __hip_atomic_load(&flags[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
-			const int tA = dbk_done012(cA, Wmb);
-			const int tA13 = cB;                 /* row B filtered MB m (so row A had MB m + 1 done) */
-			const int tB = hasB ? dbk_done012(cB, Wmb) : 0;
-			if (tA <= dA && tA13 <= dA13 && tB <= dB) {
+			const int tA = g4(dbk_done012(cA, Wmb));
+			const int tA13 = g4(cB);             /* row B filtered MB m (so row A had MB m + 1 done) */
+			const int tH = hasB ? dbk_done012(cB, Wmb) : 0;
+			const int tB = g4(tH);
+			if (tA <= dA && tA13 <= dA13 && tB <= dB && (lastB || tH <= dH)) {
 				if ((hasB ? dB : dA) >= Wmb) break;
 				if (!spin_ok(spins, err, 8)) {
 					if (hasB && !lastB) signal_progress(&progress[yB], Wmb); /* release the next workgroup */
@@ -1671,13 +1691,13 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 				}
 				continue;
 			}
-			/* the next workgroup waits on row B's hand-off records: write them first, drain, publish */
-			if (tB > dB && !lastB) {
-				const int n = tB - dB;
+			/* the next workgroup waits on row B's hand-off records (MB by MB): write them first, drain, publish */
+			if (tH > dH && !lastB) {
+				const int n = tH - dH;
 				for (int g0 = 0; g0 < n * 12; g0 += 64) {
 					const int g = g0 + t;
 					if (g < n * 12) {
-						const int mb = dB + g / 12, k = g % 12;
+						const int mb = dH + g / 12, k = g % 12;
 						const int col = (mb & (DBK_RING - 1)) * 16;
 						const uint8_t *sp = (k < 8) ? RL + (32 + (k >> 1)) * S + col + (k & 1) * 8
 						                            : RC + (16 + ((k - 8) >> 1)) * S + col + (k & 1) * 8;
@@ -1685,54 +1705,32 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 						st_sc1(hbd + ((size_t)yB * Wmb + mb) * HBD_BYTES + k * 8, ((unsigned long long)v.y << 32) | v.x);
 					}
 				}
-				signal_progress(&progress[yB], tB);
+				signal_progress(&progress[yB], tH);
+				dH = tH;
 			}
 			/* row A: rows 0..12 (all 16 if A is the last row) and the row above's rows 13..15 */
 			if (tA > dA) {
 				const int n = tA - dA;
-				for (int k = t; k < n * 64; k += 64) {
-					const int mb = dA + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
-					if (lastA || r <= 12)
-						st32_sc1(cur + (size_t)(y0A + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (4 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
+				store_rows(cur, y0A, RL, 4, dA, n, lastA ? 16 : 13);
+				store_rows(chroma, yc0A, RC, 2, dA, n, lastA ? 8 : 7);
+				if (yA > 0) {
+					store_rows(cur, y0A - 3, RL, 1, dA, n, 3);
+					store_rows(chroma, yc0A - 1, RC, 1, dA, n, 1);
 				}
-				for (int k = t; k < n * 32; k += 64) {
-					const int mb = dA + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
-					if (lastA || r <= 6)
-						st32_sc1(chroma + (size_t)(yc0A + r) * W + mb * 16 + cc, *(const uint32_t *)(RC + (2 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
-				}
-				if (yA > 0)
-					for (int k = t; k < n * 16; k += 64) {
-						const int mb = dA + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
-						const int col = (mb & (DBK_RING - 1)) * 16 + cc;
-						if (r < 3) st32_sc1(cur + (size_t)(y0A - 3 + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (1 + r) * S + col));
-						else st32_sc1(chroma + (size_t)(yc0A - 1) * W + mb * 16 + cc, *(const uint32_t *)(RC + 1 * S + col));
-					}
 				dA = tA;
 			}
 			/* row A's rows 13..15 (chroma 7), final once row B filtered its top edge */
 			if (tA13 > dA13) {
 				const int n = tA13 - dA13;
-				for (int k = t; k < n * 16; k += 64) {
-					const int mb = dA13 + (k >> 4), r = (k >> 2) & 3, cc = (k & 3) * 4;
-					const int col = (mb & (DBK_RING - 1)) * 16 + cc;
-					if (r < 3) st32_sc1(cur + (size_t)(y0A + 13 + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (17 + r) * S + col));
-					else st32_sc1(chroma + (size_t)(yc0A + 7) * W + mb * 16 + cc, *(const uint32_t *)(RC + 9 * S + col));
-				}
+				store_rows(cur, y0A + 13, RL, 17, dA13, n, 3);
+				store_rows(chroma, yc0A + 7, RC, 9, dA13, n, 1);
 				dA13 = tA13;
 			}
 			/* row B: rows 0..12 (all 16 if B is the last row) */
 			if (tB > dB) {
 				const int n = tB - dB;
-				for (int k = t; k < n * 64; k += 64) {
-					const int mb = dB + (k >> 6), r = (k >> 2) & 15, cc = (k & 3) * 4;
-					if (lastB || r <= 12)
-						st32_sc1(cur + (size_t)(y0B + r) * W + mb * 16 + cc, *(const uint32_t *)(RL + (20 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
-				}
-				for (int k = t; k < n * 32; k += 64) {
-					const int mb = dB + (k >> 5), r = (k >> 2) & 7, cc = (k & 3) * 4;
-					if (lastB || r <= 6)
-						st32_sc1(chroma + (size_t)(yc0B + r) * W + mb * 16 + cc, *(const uint32_t *)(RC + (10 + r) * S + (mb & (DBK_RING - 1)) * 16 + cc));
-				}
+				store_rows(cur, y0B, RL, 20, dB, n, lastB ? 16 : 13);
+				store_rows(chroma, yc0B, RC, 10, dB, n, lastB ? 8 : 7);
 				dB = tB;
 			}
 			/* the slots' LDS reads are done (their values fed the stores above): hand them back */

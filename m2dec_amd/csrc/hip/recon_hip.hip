@@ -255,7 +255,7 @@ __device__ __forceinline__ void signal_progress(int *flag, int value)
 /* one inter macroblock, all 256 lanes of the workgroup (uniform call) */
 __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t *__restrict__ inters,
                          const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                         size_t fsz, int W, int H, int Wmb, int slot, uint8_t *tile)
+                         size_t fsz, int W, int H, int Wmb, int slot, uint8_t *tile, uint8_t *seg)
 {
 	__shared__ int s_res[256 + 128];
 	__shared__ int s_cnt[4];
@@ -302,8 +302,9 @@ __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, c
 		predc = combine(sl, it, cb8, 1 + cc, use[0], use[1], v[0], v[1]);
 	}
 
-	uint8_t *dl = cur + (size_t)(mby * 16 + ly) * W + mbx * 16 + lx;
-	uint8_t *dc = cur + (size_t)W * H + (size_t)(mby * 8 + cy) * W + mbx * 16 + cx * 2 + cc;
+	/* output: the item's LDS segment buffer (luma rows 0..15, chroma rows 16..23, SEG_ROW bytes each) */
+	uint8_t *dl = seg + ly * SEG_ROW + (mbx & 7) * 16 + lx;
+	uint8_t *dc = seg + (16 + cy) * SEG_ROW + (mbx & 7) * 16 + cx * 2 + cc;
 #ifndef M2DEC_NO_EARLYRET
 	if (__builtin_amdgcn_readfirstlane(m.cbp) == 0) {
 		*dl = (uint8_t)predl;
@@ -1138,6 +1139,8 @@ __device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int
 __device__ __forceinline__ IntraLDS *worker_ictx(lds_u8 *lds) { return lds_ptr<IntraLDS>(lds); }
 __device__ __forceinline__ IntraTables *worker_tabs(lds_u8 *lds) { return (IntraTables *)(worker_ictx(lds) + 1); }
 __device__ __forceinline__ uint8_t *worker_tile(lds_u8 *lds) { return (uint8_t *)(worker_tabs(lds) + 1); }
+/* the item's reconstructed samples before they go out: 24 rows (16 luma, 8 interleaved chroma) of 8 MBs */
+__device__ __forceinline__ uint8_t *worker_seg(lds_u8 *lds) { return worker_tile(lds) + 384; }
 
 __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, const m2r_mb_t m, const int16_t *__restrict__ pool, uint8_t *cur,
                             int W, int H, int Wmb, const uint8_t *hbp, int rs, lds_u8 *lds)
@@ -1145,6 +1148,7 @@ __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, 
 	IntraLDS *const ctx = worker_ictx(lds);
 	const IntraTables *const tabs = worker_tabs(lds);
 	uint8_t *const tile = worker_tile(lds);
+	uint8_t *const seg = worker_seg(lds);
 	const int t = threadIdx.x;
 	const int nq = d_mb_ncoef(m);
 	for (int k = t; k < nq; k += blockDim.x) ctx->Q[0][k] = pool[m.coef + k];
@@ -1182,13 +1186,13 @@ __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, 
 	{
 		const uint8_t v = ctx->L[1 + (t >> 4)][1 + (t & 15)];
 		tile[t] = v;
-		cur[(size_t)(y * 16 + (t >> 4)) * W + x * 16 + (t & 15)] = v;
+		seg[(t >> 4) * SEG_ROW + (x & 7) * 16 + (t & 15)] = v;
 	}
 	if (t < 128) {
 		const int cy = t >> 4, bx = t & 15;
 		const uint8_t v = ctx->C[bx & 1][1 + cy][1 + (bx >> 1)];
 		tile[256 + t] = v;
-		cur[(size_t)W * H + (size_t)(y * 8 + cy) * W + x * 16 + bx] = v;
+		seg[(16 + cy) * SEG_ROW + (x & 7) * 16 + bx] = v;
 	}
 }
 
@@ -1355,7 +1359,7 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 				if (inter != (pass == 0)) continue;
 				const bool rec = (rec_bits >> (x - x0)) & 1;
 				if (inter)
-					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr);
+					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr, worker_seg(LDS_ARG()));
 				else
 					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, LDS_ARG());
 				if (rec) {
@@ -1364,6 +1368,20 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				}
 				__syncthreads();
+			}
+		}
+		/* the item's samples out of LDS as whole 128-byte row pieces (8 MBs x 16 bytes, 16 bytes per lane; the
+		 * byte stores of the MBs left one partially dirty line per MB row in whichever L2 they went to) */
+		{
+			const uint8_t *sg = worker_seg(LDS_ARG());
+			const int nmb = x1 - x0;
+			for (int k = t; k < 24 * 8; k += blockDim.x) {
+				const int r = k >> 3, c = k & 7;
+				if (c < nmb) {
+					uint8_t *dst = r < 16 ? cur + (size_t)(y * 16 + r) * W + (x0 + c) * 16
+					                      : cur + (size_t)W * H + (size_t)(y * 8 + r - 16) * W + (x0 + c) * 16;
+					*(uint4 *)dst = *(const uint4 *)(sg + r * SEG_ROW + c * 16);
+				}
 			}
 		}
 		/* segment done: every wave drained, then ONE agent release, the row's counter and the item's flag */
@@ -1668,7 +1686,7 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		const int y0A = yA * 16, yc0A = yA * 8, y0B = yB * 16, yc0B = yB * 8;
 		/* frame stores go out in groups of 4 MBs (one 64-byte piece of each sample row, 16 bytes per lane,
 		 * write-through): a final-MB count is rounded down to 4 except at the row end */
-		auto g4 = [Wmb](int v) { return v >= Wmb ? Wmb : (v & ~3); };
+		auto g4 = [Wmb](int v) { return v >= Wmb ? Wmb : (v & ~(DBK_SG - 1)); };
 		/* n MBs from m0 of `rows` sample rows: frame row fy0 + r <- ring line rl0 + r of plane `ring` */
 		auto store_rows = [&](uint8_t *plane, int fy0, const uint8_t *ring, int rl0, int m0, int n, int rows) {
 			for (int k = t; k < n * rows; k += 64) {
@@ -1933,7 +1951,7 @@ size_t m2r_deblock_lds_bytes(int W, int Wmb)
 	(void)W;
 	const size_t dbk = (size_t)54 * DBK_RW + 3 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
 	const size_t intra = 4 * sizeof(IntraLDS) + sizeof(IntraTables);
-	const size_t worker = sizeof(IntraLDS) + sizeof(IntraTables) + 384;
+	const size_t worker = sizeof(IntraLDS) + sizeof(IntraTables) + 384 + 24 * SEG_ROW;
 	return std::max(dbk, std::max(intra, worker));
 }
 

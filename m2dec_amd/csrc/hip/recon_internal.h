@@ -12,7 +12,12 @@
                         * u64 words of 6 bytes + a 16-bit picture tag each */
 #define HBD_BYTES 96 /* deblock hand-off per MB: luma rows 12..15 (4 x 16 B) + chroma rows 6..7 (2 x 16 B) */
 #define DBK_WAVES 4  /* deblocking workgroup: loader, filter A, storer, filter B waves */
+#ifndef DBK_RING
 #define DBK_RING 16  /* deblocking: MB slots of the LDS ring (power of two) */
+#endif
+#ifndef DBK_SG
+#define DBK_SG 4     /* deblocking storer: frame stores in groups of DBK_SG MBs (power of two, <= DBK_RING / 2) */
+#endif
 #define DBK_RW (DBK_RING * 16) /* ring line width in bytes */
 
 /* row progress word: picture seq's MB row has its first `cols` MB columns final (all 16 luma / 8 chroma
@@ -42,6 +47,8 @@ struct SlotSeq {
  * bottom luma row, bottom chroma row (CbCr), right luma column, right chroma column (CbCr pairs);
  * row stride NSEG * 8 MBs so that no 128-byte line holds records of two work items */
 #define HBP_BYTES 64
+/* inter worker: LDS row stride of a work item's staged output (8 MBs x 16 bytes) */
+#define SEG_ROW 128
 
 struct PictureArgs {
 	const m2r_mb_t *mbs;

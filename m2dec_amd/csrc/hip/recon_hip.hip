@@ -1564,12 +1564,16 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		const int seg = luma ? seg_l : seg_c;
 		uint8_t *const sink = dummy + t;
 		unsigned spins = 0;
+		/* the last values seen of the loader's and row A's words: a word is polled again only when the value
+		 * seen does not cover this MB (the acquire that returned it still orders the reads below) */
+		int seen0 = 0, seen1 = 0;
 		for (int x = 0; x < Wmb; ++x) {
-			while (__hip_atomic_load(&flags[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= x) {
-				if (!spin_ok(spins, err, 16)) break;
-			}
-			if (rowB) /* row A's MB x is final for us once A filtered MB x + 1 */
-				while (__hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < min(x + 2, Wmb)) {
+			if (seen0 <= x)
+				while ((seen0 = __hip_atomic_load(&flags[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) <= x) {
+					if (!spin_ok(spins, err, 16)) break;
+				}
+			if (rowB && seen1 < min(x + 2, Wmb)) /* row A's MB x is final for us once A filtered MB x + 1 */
+				while ((seen1 = __hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < min(x + 2, Wmb)) {
 					if (!spin_ok(spins, err, 16)) break;
 				}
 			STAMP(yA + rowB, 1, x, x);

@@ -1461,8 +1461,18 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 
 	/* the deblocking chain is the picture's critical path: let its waves win the SIMD arbitration
 	 * over co-resident inter workers (filters highest) */
-	if (wave == 1 || wave == 3) __builtin_amdgcn_s_setprio(3);
-	else __builtin_amdgcn_s_setprio(2);
+#ifndef M2DEC_DBK_PRIO_FILTER
+#define M2DEC_DBK_PRIO_FILTER 3
+#endif
+#ifndef M2DEC_DBK_PRIO_OTHER
+#define M2DEC_DBK_PRIO_OTHER 2
+#endif
+#ifndef M2DEC_DBK_PRIO_STORER
+#define M2DEC_DBK_PRIO_STORER M2DEC_DBK_PRIO_OTHER
+#endif
+	if (wave == 1 || wave == 3) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_FILTER);
+	else if (wave == 2) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_STORER);
+	else __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_OTHER);
 	if (wave == 0) {
 		/* ---------------- loader: own samples run ahead as far as the ring allows (prep); only the
 		 * hand-off record of the row above A waits for that row (got) */

@@ -1470,8 +1470,11 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 #ifndef M2DEC_DBK_PRIO_STORER
 #define M2DEC_DBK_PRIO_STORER M2DEC_DBK_PRIO_OTHER
 #endif
-	if (wave == 1 || wave == 3) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_FILTER);
-	else if (wave == 2) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_STORER);
+	/* s_setprio is a scalar instruction: the role must be a scalar (readfirstlane) value so that each
+	 * s_setprio sits behind a scalar branch, not in an exec-masked block every wave executes */
+	const int swave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+	if (swave == 1 || swave == 3) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_FILTER);
+	else if (swave == 2) __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_STORER);
 	else __builtin_amdgcn_s_setprio(M2DEC_DBK_PRIO_OTHER);
 	if (wave == 0) {
 		/* ---------------- loader: own samples run ahead as far as the ring allows (prep); only the
@@ -1800,6 +1803,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 			if (hasB) __hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
+	/* the raised priority covers the deblocking chain only, not the caller's copy-out / next row pair */
+	__builtin_amdgcn_s_setprio(0);
 }
 
 
@@ -1870,6 +1875,7 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 			 * rewritten (filtered) by the row below's deblocking, possibly from another XCD, and a later
 			 * write-back of our dirty unfiltered bytes would land on top of them */
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+			__builtin_amdgcn_s_setprio(0);
 		}
 	}
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

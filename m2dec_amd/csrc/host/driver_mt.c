@@ -18,8 +18,10 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 10
-#define MD5_THREADS 4 /* one stream: MD5 (~5 ms per 1080p frame per core) must keep up with the GPU */
+#define MD5_RING 24
+#define MD5_THREADS_MAX 16
+#define MD5_THREADS 8 /* one stream: MD5 (~4 ms per 1080p frame per core) must keep up with the decoder;
+                         M2DEC_AMD_MD5_THREADS overrides */
 
 typedef struct {
 	pthread_mutex_t mu;
@@ -109,14 +111,15 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
                                 m2dec_amd_stats_t *stats)
 {
-	return decode_md5(data, len, device, dpb, -1, MD5_THREADS, md5s, max, stats);
+	const char *e = getenv("M2DEC_AMD_MD5_THREADS");
+	return decode_md5(data, len, device, dpb, -1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS, md5s, max, stats);
 }
 
 static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, int md5_threads,
                       char *md5s, int max, m2dec_amd_stats_t *stats)
 {
 	md5_pipe_t p;
-	pthread_t th[MD5_THREADS];
+	pthread_t th[MD5_THREADS_MAX];
 	int r;
 	memset(&p, 0, sizeof(p));
 	pthread_mutex_init(&p.mu, NULL);
@@ -125,7 +128,7 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	p.md5s = md5s;
 	p.max = max;
 	int nth = 0;
-	for (; nth < md5_threads && nth < MD5_THREADS; ++nth)
+	for (; nth < md5_threads && nth < MD5_THREADS_MAX; ++nth)
 		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
 	if (!nth) return -1;
 	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, stats);

@@ -17,8 +17,6 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-int h264_nal_next(h264_dec_t *d);
-
 static int hdr_dummy(void *a, void *b)
 {
 	(void)a;
@@ -153,25 +151,35 @@ static int read_slice(h264_dec_t *d, int nal_unit_type, int nal_ref_idc)
 	if (err < 0) return err;
 	if (d->in_picture && d->sh.first_mb <= prev_first) return -2; /* h264.cpp:1427-1430 */
 	s = &d->sps[d->active_sps];
-	if (!d->frames_ready) return -1;
+	if (!d->lookahead && !d->frames_ready) return -1;
+	if (d->lookahead && ((s->width >> 4) != d->mb_w || (s->height >> 4) != d->mb_h) && h264_async_sps(d) < 0)
+		return -1; /* new geometry: the co-located stores are reallocated, no job may still use them */
 	if (alloc_geometry(d, s->width, s->height) < 0) return -1;
 	if (!d->in_picture) {
 		if (h264_picture_begin(d) < 0) return -1;
 	}
-	if (d->as) return h264_async_add_slice(d) < 0 ? -1 : 0;
+	if (d->lookahead) return h264_async_add_slice(d) < 0 ? -1 : 0;
+	if (d->as) return 0; /* API context of the pipeline: the lookahead context parses the slice data */
 	err = h264_slice_data(d);
 	if (err < 0) return err;
 	if (err == 1) return h264_picture_finish(d);
 	return 0;
 }
 
-static int api_decode_picture(void *ctx)
+/* The NAL loop of decode_picture (h264.cpp:663-693): returns 1 per picture, -1 on error, -2 at the
+ * end of the data.  Run on the API context (headers, DPB, frame slots, back-end submission) and, in
+ * the parse-ahead pipeline, on the lookahead context (headers, slice-data jobs), which stays up to
+ * a few dozen pictures ahead and hands every NAL it finished over to the API context. */
+int h264_decode_loop(h264_dec_t *d)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d) return -1;
 	for (;;) {
-		int type, ref_idc, err = 0;
-		if (h264_nal_next(d) < 0) {
+		/* NALs come from the lookahead context (re-evaluated per NAL: the pipeline starts inside the
+		 * header callback of an SPS) */
+		const int queued = d->as && !d->lookahead;
+		int type, ref_idc, err = 0, r;
+		r = queued ? h264_async_nal_next(d) : h264_nal_next(d);
+		if (r < 0) {
+			if (r == -3) return -1; /* the lookahead context failed before this point */
 			if (d->as && d->in_picture) return h264_async_close(d); /* the last picture */
 			return -2;
 		}
@@ -183,7 +191,7 @@ static int api_decode_picture(void *ctx)
 			d->nal_replay = 1;
 			return h264_async_close(d);
 		}
-		if (d->as && type == 7 && h264_async_drain(d, -1) < 0) return -1; /* set_frames may follow */
+		if (queued && type == 7 && h264_async_drain(d, -1) < 0) return -1; /* set_frames may follow */
 		switch (type) {
 		case 1:
 		case 5:
@@ -197,7 +205,7 @@ static int api_decode_picture(void *ctx)
 			id = h264_parse_sps(d, &b);
 			if (id < 0) return id;
 			if (!d->in_picture) d->active_sps = id;
-			d->header_callback(d->header_callback_arg, d->stream->id);
+			if (!d->lookahead) d->header_callback(d->header_callback_arg, d->stream->id);
 			break;
 		}
 		case 8: {
@@ -210,7 +218,15 @@ static int api_decode_picture(void *ctx)
 		default:
 			break;
 		}
+		if (d->lookahead && h264_async_push_nal(d) < 0) return -1;
 	}
+}
+
+static int api_decode_picture(void *ctx)
+{
+	h264_dec_t *d = CTX(ctx);
+	if (!d) return -1;
+	return h264_decode_loop(d);
 }
 
 static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)

@@ -1,17 +1,34 @@
 /*
- * Parse-ahead pipeline: the slice data of several pictures parsed at once on worker threads, behind
+ * Parse-ahead pipeline: the slice data of many pictures parsed at once on worker threads, behind
  * the unchanged h264d_func API ("pipelining parse n+1 with GPU recon n").
  *
- * What stays on the caller's thread, in stream order: NAL scanning, SPS/PPS, every slice header
- * (POC, reference lists, weights, marking syntax), the reference marking / co-located store swap /
- * DPB insertion of a finished picture (they need only the headers), and every call into the back
- * end (acquire / submit / sync_frame), in decode order.
+ * Two decoder contexts run the same NAL loop (h264_decode_loop) on the caller's thread:
  *
- * What moves to the workers: h264_slice_data (CABAC/CAVLC, MV prediction, direct, bS -> records)
- * and the deblock edge resolution of a whole picture.  A job is one picture: for each of its slices
- * a copy of the decoder context right after that slice's header (60 KB) and a copy of its RBSP;
- * the worker runs the slices in order on a private context, carrying the few fields the slice
- * parser accumulates across slices, into a private MB-info array and a private record arena.
+ *   the lookahead context L   reads the stream, parses SPS / PPS / slice headers, does the reference
+ *                             marking and the co-located store swap, and turns every picture into a
+ *                             job (its slice data to be parsed on a worker).  It names pictures by
+ *                             virtual frame ids, not frame slots, so it does not depend on the
+ *                             caller's output calls and can run up to `depth` pictures ahead of the
+ *                             API.  Every NAL it has finished goes into a queue for A.
+ *   the API context A         consumes that NAL queue: headers again, the header callback
+ *                             (set_frames), frame-slot LRU (find_empty_frame, h264.cpp:924-962),
+ *                             marking, DPB insertion and output bumping — exactly the state the
+ *                             reference's synchronous decoder has at each decode_picture / peek / get
+ *                             call, whatever order the caller uses them in.  At each picture it
+ *                             closes, A records the virtual-id -> slot translation of that picture's
+ *                             job; the job's records are translated when they are submitted.
+ *
+ * Before this split the API context also created the jobs, so parse-ahead could never get further
+ * ahead than the DPB output lag (peek/get must wait for the bumped picture): 3-4 pictures in flight.
+ *
+ * The parser compares frame_idx values only for equality (bS motion tests, the co-located reference
+ * map of temporal direct, the record ref slots), so virtual ids (unique among live pictures, reused
+ * as late as possible) give the same records as frame slots.
+ *
+ * A job is one picture: for each of its slices a copy of L right after that slice's header (60 KB)
+ * and a copy of its RBSP; the worker runs the slices in order on a private context, carrying the
+ * few fields the slice parser accumulates across slices, into a private MB-info array and a private
+ * record arena.
  *
  * Cross-picture dependencies of the slice data: a B slice reads the co-located store of its
  * refs[1][0] (spatial and temporal direct, h264.cpp:9777 / 9848), written by an earlier picture's
@@ -20,29 +37,46 @@
  * read or wrote it has finished.
  *
  * Picture boundaries: the synchronous parser knows a picture is complete when its last MB is
- * parsed; here the caller's thread sees only headers, so a picture is closed when the next
+ * parsed; here the header-level loop sees only headers, so a picture is closed when the next
  * picture's first slice arrives (first_mb not above the previous slice's, the reference's own
- * test, h264.cpp:1427-1430) or at the end of the data.  decode_picture still returns 1 once per
- * picture and the DPB output order is unchanged; a frame is handed out (peek / get) only after its
- * picture was parsed and submitted, and sync_frame has waited for its reconstruction.
+ * test, h264.cpp:1427-1430), at a SEI / SPS / PPS / AUD NAL, or at the end of the data.
+ * decode_picture still returns 1 once per picture and the DPB output order is unchanged; a frame
+ * is handed out (peek / get) only after its picture was parsed and submitted, and sync_frame has
+ * waited for its reconstruction.
+ *
+ * The stream is read ahead of decode_picture by up to `depth` pictures, so stream_pos() points
+ * past the picture decode_picture last returned.
  */
 #include <pthread.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include "h264_dec.h"
 
-#define AS_MAX 32 /* jobs alive (collecting + dispatched + free) */
+#define AS_MAX 64 /* jobs dispatched and not yet submitted */
+
+static double now_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 typedef struct h264_job {
 	int nsl, capsl;
-	h264_dec_t **snap;        /* [nsl] decoder context right after each slice header */
-	uint8_t **rbsp;           /* [nsl] slice RBSP copies (16 zero bytes of padding) */
+	h264_dec_t **snap;        /* [nsl] lookahead context right after each slice header */
+	uint8_t **rbsp;           /* [nsl] slice RBSP copies (32 zero bytes of padding) */
 	h264_mbinfo_t *mbi;       /* private neighbour state */
 	size_t mbi_n;
-	m2r_picture_t pic;        /* private record arena */
+	m2r_picture_t pic;        /* private record arena (frame ids are virtual until submission) */
 	uint8_t *arena;
 	size_t arena_size;
-	int slot, col_store;
+	int vid;                  /* virtual frame id of the picture (lookahead context) */
+	int slot;                 /* frame slot (API context; -1 until A closed the picture) */
+	int poc;                  /* consistency check between the two contexts */
+	int8_t map[64];           /* virtual id -> frame slot, as of the API context's close */
+	int col_store;
 	int nonref;               /* no slice has nal_ref_idc: its co-located store is never read ... */
 	h264_colmb_t *priv_col;   /* ... so it writes this private one (no ordering against other jobs) */
 	size_t priv_n;
@@ -54,21 +88,44 @@ typedef struct h264_job {
 	h264_dec_t *w;            /* worker context */
 } h264_job_t;
 
+typedef struct {
+	uint8_t *buf;
+	size_t cap, len;
+} nal_ent_t;
+
 struct h264_async {
 	pthread_mutex_t mu;
 	pthread_cond_t cv_work, cv_done;
 	pthread_t th[16];
 	int nth, quit, depth;
-	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head) */
+	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head); job seq s at fifo[s % AS_MAX] */
 	long head, tail;
 	h264_job_t *queue[AS_MAX]; /* dispatched; [qtail, qhead) holds every job not yet taken */
 	long qhead, qtail;
-	h264_job_t *cur;          /* the picture being collected */
+	h264_job_t *cur;          /* the picture the lookahead context is collecting */
 	h264_job_t *free_jobs[AS_MAX];
 	int nfree;
-	long seq;
+	long seq;                 /* jobs dispatched by the lookahead context */
+	long a_seq;               /* pictures closed by the API context: jobs [tail, a_seq) may be submitted */
 	long col_last[17];        /* seq of the last dispatched job that reads or writes store i */
 	h264_job_t *col_writer[17]; /* dispatched, unsubmitted job writing store i */
+	/* lookahead context and its NAL hand-over queue (ring, [nq_tail, nq_head)) */
+	h264_dec_t *la;
+	int la_done, la_err;
+	nal_ent_t *nq;
+	long nq_head, nq_tail, nq_cap;
+	int8_t vmap[64];          /* API context: virtual id -> frame slot */
+	/* co-located store buffers taken out of the lookahead's stores (h264_colpic_t.mb) while jobs
+	 * still used them: free once every job dispatched before `unmap_seq` was submitted */
+	struct {
+		h264_colmb_t *mb;
+		long unmap_seq;
+	} spare[64];
+	int nspare;
+	size_t col_n;             /* MBs per store buffer */
+	/* M2DEC_AMD_ASYNC_STATS: where the caller's thread spends its time (seconds) */
+	int stats;
+	double t0, t_col_wait, t_done_wait, t_copy, t_submit, t_slice, t_parse, t_la;
 };
 
 static int job_arena(h264_job_t *j, int wm, int hm)
@@ -115,6 +172,7 @@ static void job_clear(h264_job_t *j)
 	j->taken = 0;
 	j->done = 0;
 	j->err = 0;
+	j->slot = -1;
 }
 
 static void job_free(h264_job_t *j)
@@ -156,7 +214,7 @@ static void job_run(h264_job_t *j)
 		memcpy(w->slice_idc, idc, (size_t)slice_num);
 		memcpy(w->slice_alpha, alpha, (size_t)slice_num);
 		memcpy(w->slice_beta, beta, (size_t)slice_num);
-		/* the bit reader and RBSP bounds pointed into the caller's NAL buffer: rebase onto the copy */
+		/* the bit reader and RBSP bounds pointed into the lookahead's NAL buffer: rebase onto the copy */
 		w->bs.p += off;
 		w->bs.end += off;
 		w->slice_rbsp += off;
@@ -185,13 +243,13 @@ static void job_run(h264_job_t *j)
  * submitted, hence finished.  *err collects their errors.  Caller holds the mutex. */
 static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err)
 {
-	for (int i = 0; i < j->ndeps; ++i)
-		for (long k = as->tail; k < as->head; ++k) {
-			const h264_job_t *o = as->fifo[k % AS_MAX];
-			if (o->seq != j->deps[i]) continue;
-			if (!o->done) return 0;
-			*err |= o->err;
-		}
+	for (int i = 0; i < j->ndeps; ++i) {
+		const long s = j->deps[i];
+		if (s < as->tail || s >= as->head) continue;
+		const h264_job_t *o = as->fifo[s % AS_MAX];
+		if (!o->done) return 0;
+		*err |= o->err;
+	}
 	return 1;
 }
 
@@ -217,9 +275,17 @@ static void *worker(void *arg)
 		if (!j) break;
 		j->taken = 1;
 		pthread_mutex_unlock(&as->mu);
+		const double tp = as->stats ? now_s() : 0;
 		if (dep_err) j->err = 1;
 		else job_run(j);
 		pthread_mutex_lock(&as->mu);
+		if (as->stats) {
+			const double te = now_s();
+			as->t_parse += te - tp;
+			if (as->stats > 1)
+				fprintf(stderr, "job %ld type %d slices %d: start %.1f ms, parse %.2f ms\n", j->seq,
+				        j->snap[0]->sh.slice_type, j->nsl, 1e3 * (tp - as->t0), 1e3 * (te - tp));
+		}
 		j->done = 1;
 		pthread_cond_broadcast(&as->cv_done);
 		pthread_cond_broadcast(&as->cv_work); /* jobs waiting on this one may be ready */
@@ -228,33 +294,104 @@ static void *worker(void *arg)
 	return NULL;
 }
 
-/* ---------------------------------------------------------------- caller's thread */
+/* ---------------------------------------------------------------- start / stop */
+static void la_free(h264_dec_t *la)
+{
+	if (!la) return;
+	free(la->mbi);
+	for (int i = 0; i < 17; ++i) free(la->colpic[i].mb);
+	free(la->nal);
+	free(la);
+}
+
+/* Called from the first set_frames (inside the SPS header callback, on the API context's NAL loop):
+ * the lookahead context starts as a copy of the API context at this stream position; from the next
+ * NAL on, the API context reads NALs only from the lookahead's queue. */
 int h264_async_start(h264_dec_t *d, int threads)
 {
 	struct h264_async *as;
+	h264_dec_t *la;
 	if (threads <= 0) return 0;
 	if (threads > 16) threads = 16;
 	as = (struct h264_async *)calloc(1, sizeof(*as));
-	if (!as) return -1;
+	la = (h264_dec_t *)malloc(sizeof(h264_dec_t));
+	if (!as || !la) {
+		free(as);
+		free(la);
+		return -1;
+	}
+	memcpy(la, d, sizeof(*la));
+	la->mbi = NULL;
+	la->mbi_cap = 0;
+	la->mb_w = la->mb_h = la->n_mbs = 0; /* alloc_geometry: own MB info and co-located stores */
+	for (int i = 0; i < 17; ++i) la->colpic[i].mb = NULL;
+	la->nal = NULL;
+	la->nal_cap = 0;
+	la->nal_len = 0;
+	la->nal_replay = 0;
+	la->have_backend = 0;
+	la->pic = NULL;
+	la->lookahead = 1;
+	la->vid_next = 0;
+	la->as = as;
+	as->la = la;
+	as->nq_cap = 256;
+	as->nq = (nal_ent_t *)calloc((size_t)as->nq_cap, sizeof(nal_ent_t));
+	if (!as->nq) goto fail;
+	for (int i = 0; i < 64; ++i) as->vmap[i] = -1;
 	pthread_mutex_init(&as->mu, NULL);
 	pthread_cond_init(&as->cv_work, NULL);
 	pthread_cond_init(&as->cv_done, NULL);
-	as->depth = threads + 2;
+	as->depth = 2 * threads + 8;
 	{
-		const char *e = getenv("M2DEC_AMD_PARSE_DEPTH"); /* tuning: pictures in flight past the oldest */
-		if (e && atoi(e) > 0) as->depth = atoi(e) < AS_MAX - 2 ? atoi(e) : AS_MAX - 2;
+		const char *e = getenv("M2DEC_AMD_PARSE_DEPTH"); /* tuning: pictures the lookahead runs ahead */
+		if (e && atoi(e) > 0) as->depth = atoi(e);
 	}
+	if (as->depth > AS_MAX - 4) as->depth = AS_MAX - 4;
 	for (int i = 0; i < 17; ++i) as->col_last[i] = -1;
+	as->stats = getenv("M2DEC_AMD_ASYNC_STATS") ? atoi(getenv("M2DEC_AMD_ASYNC_STATS")) : 0;
+	as->t0 = now_s();
 	for (int i = 0; i < threads; ++i) {
 		if (pthread_create(&as->th[i], NULL, worker, as) != 0) break;
 		as->nth++;
 	}
-	if (!as->nth) {
-		free(as);
-		return -1;
-	}
+	if (!as->nth) goto fail;
 	d->as = as;
 	return 0;
+fail:
+	free(as->nq);
+	free(as);
+	free(la);
+	return -1;
+}
+
+void h264_async_stop(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	if (!as) return;
+	if (as->stats)
+		fprintf(stderr, "async: %ld jobs, depth %d; caller: lookahead %.3f s (col-store waits %.3f s, slice copies "
+		                "%.3f s), oldest-done waits %.3f s, record copies %.3f s, back-end submit %.3f s; workers "
+		                "parse %.3f s\n",
+		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
+		        as->t_parse);
+	pthread_mutex_lock(&as->mu);
+	as->quit = 1;
+	pthread_cond_broadcast(&as->cv_work);
+	pthread_mutex_unlock(&as->mu);
+	for (int i = 0; i < as->nth; ++i) pthread_join(as->th[i], NULL);
+	for (long i = as->tail; i < as->head; ++i) job_free(as->fifo[i % AS_MAX]);
+	job_free(as->cur);
+	for (int i = 0; i < as->nfree; ++i) job_free(as->free_jobs[i]);
+	for (long i = 0; i < as->nq_cap; ++i) free(as->nq[i].buf);
+	for (int i = 0; i < as->nspare; ++i) free(as->spare[i].mb);
+	free(as->nq);
+	la_free(as->la);
+	pthread_mutex_destroy(&as->mu);
+	pthread_cond_destroy(&as->cv_work);
+	pthread_cond_destroy(&as->cv_done);
+	free(as);
+	d->as = NULL;
 }
 
 static h264_job_t *job_get(struct h264_async *as)
@@ -263,6 +400,7 @@ static h264_job_t *job_get(struct h264_async *as)
 	if (as->nfree) return as->free_jobs[--as->nfree];
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
+	j->slot = -1;
 	j->w = (h264_dec_t *)malloc(sizeof(h264_dec_t));
 	if (!j->w) {
 		free(j);
@@ -278,7 +416,9 @@ static void job_put(struct h264_async *as, h264_job_t *j)
 	else job_free(j);
 }
 
-/* copy a finished job's records into the back end's arena and submit it (decode order) */
+/* ---------------------------------------------------------------- API context: submission */
+/* copy the oldest closed job's records into the back end's arena, frame ids translated to the API
+ * context's slots, and submit it (decode order) */
 static int submit_oldest(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
@@ -286,10 +426,15 @@ static int submit_oldest(h264_dec_t *d)
 	m2r_picture_t *dst;
 	const m2r_picture_t *src = &j->pic;
 	int n, err;
+	double t0 = as->stats ? now_s() : 0, t1 = 0;
 	pthread_mutex_lock(&as->mu);
 	while (!j->done) pthread_cond_wait(&as->cv_done, &as->mu);
 	as->tail++; /* workers scan [tail, head) under the mutex */
 	pthread_mutex_unlock(&as->mu);
+	if (as->stats) {
+		t1 = now_s();
+		as->t_done_wait += t1 - t0;
+	}
 	for (int i = 0; i < 17; ++i)
 		if (as->col_writer[i] == j) as->col_writer[i] = NULL;
 	err = j->err;
@@ -299,7 +444,7 @@ static int submit_oldest(h264_dec_t *d)
 		if (!dst || dst->cap_slices < src->n_slices || dst->cap_inter < src->n_inter || dst->cap_coef < src->n_coef) {
 			err = 1;
 		} else {
-			dst->slot = src->slot;
+			dst->slot = j->slot;
 			dst->n_inter = src->n_inter;
 			dst->n_coef = src->n_coef;
 			dst->n_slices = src->n_slices;
@@ -308,39 +453,159 @@ static int submit_oldest(h264_dec_t *d)
 			memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
 			memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);
 			memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
-			memcpy(dst->inter, src->inter, sizeof(m2r_inter_t) * (size_t)src->n_inter);
+			for (int i = 0; i < src->n_inter; ++i) {
+				const m2r_inter_t *si = &src->inter[i];
+				m2r_inter_t *di = &dst->inter[i];
+				memcpy(di->mv, si->mv, sizeof(di->mv));
+				memcpy(di->refidx, si->refidx, sizeof(di->refidx));
+				for (int k = 0; k < 8; ++k) {
+					const int v = (&si->slot[0][0])[k];
+					(&di->slot[0][0])[k] = (int8_t)(v < 0 ? -1 : j->map[v & 63]);
+				}
+			}
 			memcpy(dst->coef, src->coef, sizeof(int16_t) * (size_t)src->n_coef);
+			if (as->stats) {
+				const double t2 = now_s();
+				as->t_copy += t2 - t1;
+				t1 = t2;
+			}
 			err = d->backend.submit(d->backend.self, dst) < 0;
+			if (as->stats) as->t_submit += now_s() - t1;
 		}
 	}
 	job_put(as, j);
 	return err ? -1 : 0;
 }
 
-/* submit every dispatched job up to and including the newest one that writes `slot` (-1: all) */
+/* submit every closed job up to and including the newest one that writes `slot` (-1: all) */
 int h264_async_drain(h264_dec_t *d, int slot)
 {
 	struct h264_async *as = d->as;
 	long upto = -1;
 	if (!as) return 0;
-	for (long i = as->tail; i < as->head; ++i)
+	for (long i = as->tail; i < as->a_seq; ++i)
 		if (slot < 0 || as->fifo[i % AS_MAX]->slot == slot) upto = i;
 	while (as->tail <= upto)
 		if (submit_oldest(d) < 0) return -1;
 	return 0;
 }
 
-/* a slice header was parsed into d: open the picture's job if needed, append the slice */
-int h264_async_add_slice(h264_dec_t *d)
+/* submit closed jobs whose parse already finished, in order, without waiting */
+static int submit_ready(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
+	for (;;) {
+		int ready;
+		if (as->tail >= as->a_seq) return 0;
+		pthread_mutex_lock(&as->mu);
+		ready = as->fifo[as->tail % AS_MAX]->done;
+		pthread_mutex_unlock(&as->mu);
+		if (!ready) return 0;
+		if (submit_oldest(d) < 0) return -1;
+	}
+}
+
+/* ---------------------------------------------------------------- lookahead context */
+/* run the lookahead until `until_nal` (the queue holds a NAL) or, else, until it is `depth` pictures
+ * ahead of the API context / out of job slots / at the end of the data */
+static void pump(h264_dec_t *d, int until_nal)
+{
+	struct h264_async *as = d->as;
+	const double t0 = as->stats ? now_s() : 0;
+	while (!as->la_done) {
+		if (until_nal) {
+			if (as->nq_head > as->nq_tail) break;
+		} else if (as->seq - as->a_seq >= as->depth) {
+			break;
+		}
+		/* job slots: submit what the API context closed before dispatching more */
+		while (as->head - as->tail >= AS_MAX - 2 && as->tail < as->a_seq)
+			if (submit_oldest(d) < 0) {
+				as->la_done = as->la_err = 1;
+				break;
+			}
+		if (as->head - as->tail >= AS_MAX - 2) break;
+		const int r = h264_decode_loop(as->la);
+		if (r == -2) as->la_done = 1;
+		else if (r < 0) as->la_done = as->la_err = 1;
+	}
+	if (as->stats) as->t_la += now_s() - t0;
+}
+
+/* the lookahead context finished a NAL: hand it to the API context (buffers are swapped, not copied) */
+int h264_async_push_nal(h264_dec_t *la)
+{
+	struct h264_async *as = la->as;
+	if (as->nq_head - as->nq_tail == as->nq_cap) {
+		const long cap = 2 * as->nq_cap;
+		nal_ent_t *q = (nal_ent_t *)calloc((size_t)cap, sizeof(nal_ent_t));
+		if (!q) return -1;
+		for (long i = 0; i < as->nq_cap; ++i) q[(as->nq_tail + i) % cap] = as->nq[(as->nq_tail + i) % as->nq_cap];
+		free(as->nq);
+		as->nq = q;
+		as->nq_cap = cap;
+	}
+	nal_ent_t *e = &as->nq[as->nq_head % as->nq_cap];
+	uint8_t *b = e->buf;
+	const size_t c = e->cap;
+	e->buf = la->nal;
+	e->cap = la->nal_cap;
+	e->len = la->nal_len;
+	la->nal = b;
+	la->nal_cap = c;
+	la->nal_len = 0;
+	as->nq_head++;
+	return 0;
+}
+
+/* API context: the next NAL (0), end of data (-1), or the lookahead failed before this point (-3) */
+int h264_async_nal_next(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	if (d->nal_replay) {
+		d->nal_replay = 0;
+		return 0;
+	}
+	if (as->nq_head == as->nq_tail) pump(d, 1);
+	if (as->nq_head == as->nq_tail) return as->la_err ? -3 : -1;
+	nal_ent_t *e = &as->nq[as->nq_tail % as->nq_cap];
+	uint8_t *b = d->nal;
+	const size_t c = d->nal_cap;
+	d->nal = e->buf;
+	d->nal_cap = e->cap;
+	d->nal_len = e->len;
+	e->buf = b;
+	e->cap = c;
+	e->len = 0;
+	as->nq_tail++;
+	return 0;
+}
+
+/* lookahead: wait until every dispatched job has finished (before its co-located stores are
+ * reallocated for a new picture size) */
+int h264_async_sps(h264_dec_t *la)
+{
+	struct h264_async *as = la->as;
+	pthread_mutex_lock(&as->mu);
+	for (long i = as->tail; i < as->head; ++i)
+		while (!as->fifo[i % AS_MAX]->done) pthread_cond_wait(&as->cv_done, &as->mu);
+	pthread_mutex_unlock(&as->mu);
+	return 0;
+}
+
+/* lookahead: a slice header was parsed into la: open the picture's job if needed, append the slice */
+int h264_async_add_slice(h264_dec_t *la)
+{
+	struct h264_async *as = la->as;
 	h264_job_t *j = as->cur;
+	const double ts = as->stats ? now_s() : 0;
 	if (!j) {
 		j = job_get(as);
-		if (!j || job_arena(j, d->mb_w, d->mb_h) < 0) return -1;
-		j->slot = d->curr_idx;
-		j->pic.slot = d->curr_idx;
-		j->col_store = d->curr_col;
+		if (!j || job_arena(j, la->mb_w, la->mb_h) < 0) return -1;
+		j->vid = la->curr_idx;
+		j->slot = -1;
+		j->pic.slot = la->curr_idx;
+		j->col_store = la->curr_col;
 		as->cur = j;
 	}
 	if (j->nsl == j->capsl) {
@@ -355,32 +620,52 @@ int h264_async_add_slice(h264_dec_t *d)
 		j->capsl = cap;
 	}
 	{
-		const size_t len = (size_t)(d->slice_rbsp_end - d->slice_rbsp);
+		const size_t len = (size_t)(la->slice_rbsp_end - la->slice_rbsp);
 		h264_dec_t *snap = (h264_dec_t *)malloc(sizeof(h264_dec_t));
-		uint8_t *rb = (uint8_t *)calloc(1, len + 32);
+		uint8_t *rb = (uint8_t *)malloc(len + 32);
 		if (!snap || !rb) {
 			free(snap);
 			free(rb);
 			return -1;
 		}
-		memcpy(snap, d, sizeof(*snap));
-		memcpy(rb, d->slice_rbsp, len);
+		memcpy(snap, la, sizeof(*snap));
+		memcpy(rb, la->slice_rbsp, len);
+		memset(rb + len, 0, 32);
 		j->snap[j->nsl] = snap;
 		j->rbsp[j->nsl] = rb;
 		j->nsl++;
 	}
+	if (as->stats) as->t_slice += now_s() - ts;
 	return 0;
 }
 
-/* the picture being collected is complete (the next picture started, or end of data): marking /
- * DPB on this thread, slice data to the workers */
-int h264_async_close(h264_dec_t *d)
+/* a store buffer no job can still use (a spare unmapped before every unsubmitted job), or a new one */
+static h264_colmb_t *col_spare_get(struct h264_async *as, int n_mbs)
 {
-	struct h264_async *as = d->as;
+	if (as->col_n != (size_t)n_mbs) { /* new geometry (no job in flight, h264_async_sps) */
+		for (int i = 0; i < as->nspare; ++i) free(as->spare[i].mb);
+		as->nspare = 0;
+		as->col_n = (size_t)n_mbs;
+	}
+	for (int i = 0; i < as->nspare; ++i)
+		if (as->spare[i].unmap_seq <= as->tail) {
+			h264_colmb_t *b = as->spare[i].mb;
+			as->spare[i] = as->spare[--as->nspare];
+			return b;
+		}
+	return (h264_colmb_t *)calloc((size_t)n_mbs, sizeof(h264_colmb_t));
+}
+
+/* lookahead: the picture being collected is complete: marking in the lookahead context, slice
+ * data to the workers */
+static int la_close(h264_dec_t *la)
+{
+	struct h264_async *as = la->as;
 	h264_job_t *j = as->cur;
 	if (!j) return -1;
 	as->cur = NULL;
-	j->seq = as->seq++;
+	j->seq = as->seq;
+	j->poc = j->snap[0]->sh.poc;
 	/* a non-reference picture is never anyone's refs[1][0]: its co-located store is dead data */
 	j->nonref = 1;
 	for (int k = 0; k < j->nsl; ++k) j->nonref &= (j->snap[k]->sh.nal_ref_idc == 0);
@@ -402,60 +687,82 @@ int h264_async_close(h264_dec_t *d)
 		if (wj && !seen && j->ndeps < 8) j->deps[j->ndeps++] = wj->seq;
 		if (as->col_last[c] < j->seq) as->col_last[c] = j->seq;
 	}
-	/* the store this picture writes: every earlier job that read or wrote it must have finished */
+	/* the store this picture writes: if an earlier job that reads or writes its buffer is still
+	 * unsubmitted, the picture writes a fresh buffer instead (its snapshots are re-pointed) and the
+	 * old one waits in the spare list until those jobs are submitted */
 	if (!j->nonref) {
-		const long last = as->col_last[j->col_store];
-		pthread_mutex_lock(&as->mu);
-		for (long i = as->tail; i < as->head; ++i) {
-			h264_job_t *o = as->fifo[i % AS_MAX];
-			if (o->seq <= last)
-				while (!o->done) pthread_cond_wait(&as->cv_done, &as->mu);
+		const int c = j->col_store;
+		const long last = as->col_last[c];
+		if (last >= as->tail) {
+			const double tw = as->stats ? now_s() : 0;
+			h264_colmb_t *nb = col_spare_get(as, la->n_mbs);
+			if (nb) {
+				if (as->nspare < 64) {
+					as->spare[as->nspare].mb = la->colpic[c].mb;
+					as->spare[as->nspare].unmap_seq = j->seq;
+					as->nspare++;
+				} else {
+					free(nb); /* spare list full: wait as before */
+					nb = NULL;
+				}
+			}
+			if (nb) {
+				la->colpic[c].mb = nb;
+				for (int k = 0; k < j->nsl; ++k) j->snap[k]->colpic[c].mb = nb;
+			} else {
+				pthread_mutex_lock(&as->mu);
+				for (long i = as->tail; i < as->head; ++i) {
+					h264_job_t *o = as->fifo[i % AS_MAX];
+					if (o->seq <= last)
+						while (!o->done) pthread_cond_wait(&as->cv_done, &as->mu);
+				}
+				pthread_mutex_unlock(&as->mu);
+			}
+			if (as->stats) as->t_col_wait += now_s() - tw;
 		}
-		pthread_mutex_unlock(&as->mu);
-		as->col_last[j->col_store] = j->seq;
-		as->col_writer[j->col_store] = j;
+		as->col_last[c] = j->seq;
+		as->col_writer[c] = j;
 	}
-	/* marking, store swap, DPB insertion (headers only) */
-	d->pic = NULL;
-	if (h264_picture_mark(d) < 0) return -1;
+	/* marking, store swap (headers only) */
+	la->pic = NULL;
+	if (h264_picture_mark(la) < 0) return -1;
 	/* dispatch */
 	pthread_mutex_lock(&as->mu);
 	as->fifo[as->head % AS_MAX] = j;
 	as->head++;
+	as->seq++;
 	as->queue[as->qhead % AS_MAX] = j;
 	as->qhead++;
 	pthread_cond_signal(&as->cv_work);
 	pthread_mutex_unlock(&as->mu);
-	/* bounded depth; then hand over whatever is already finished, in order */
-	while (as->head - as->tail > as->depth)
-		if (submit_oldest(d) < 0) return -1;
-	for (;;) {
-		int ready;
-		if (as->tail == as->head) break;
-		pthread_mutex_lock(&as->mu);
-		ready = as->fifo[as->tail % AS_MAX]->done;
-		pthread_mutex_unlock(&as->mu);
-		if (!ready) break;
-		if (submit_oldest(d) < 0) return -1;
-	}
 	return 1;
 }
 
-void h264_async_stop(h264_dec_t *d)
+/* API context: the picture is complete (the same boundary the lookahead saw): marking, DPB, the
+ * job's frame-id translation; keep the lookahead ahead and hand over whatever is already parsed */
+static int api_close(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
-	if (!as) return;
-	pthread_mutex_lock(&as->mu);
-	as->quit = 1;
-	pthread_cond_broadcast(&as->cv_work);
-	pthread_mutex_unlock(&as->mu);
-	for (int i = 0; i < as->nth; ++i) pthread_join(as->th[i], NULL);
-	for (long i = as->tail; i < as->head; ++i) job_free(as->fifo[i % AS_MAX]);
-	job_free(as->cur);
-	for (int i = 0; i < as->nfree; ++i) job_free(as->free_jobs[i]);
-	pthread_mutex_destroy(&as->mu);
-	pthread_cond_destroy(&as->cv_work);
-	pthread_cond_destroy(&as->cv_done);
-	free(as);
-	d->as = NULL;
+	h264_job_t *j;
+	while (as->a_seq >= as->head && !as->la_done) pump(d, 0); /* (never: the lookahead closed it first) */
+	if (as->a_seq >= as->head) return -1;
+	j = as->fifo[as->a_seq % AS_MAX];
+	if (j->poc != d->sh.poc) {
+		fprintf(stderr, "m2dec_amd: parse-ahead lost step (picture %ld: poc %d vs %d)\n", as->a_seq, j->poc, d->sh.poc);
+		return -1;
+	}
+	d->pic = NULL;
+	if (h264_picture_mark(d) < 0) return -1;
+	as->vmap[j->vid & 63] = (int8_t)d->curr_idx;
+	memcpy(j->map, as->vmap, sizeof(j->map));
+	j->slot = d->curr_idx;
+	as->a_seq++;
+	pump(d, 0);
+	if (submit_ready(d) < 0) return -1;
+	return 1;
+}
+
+int h264_async_close(h264_dec_t *d)
+{
+	return d->lookahead ? la_close(d) : api_close(d);
 }

@@ -326,6 +326,11 @@ struct h264_dec {
 	/* parse-ahead pipeline (h264_async.c); NULL: slice data parsed on the caller's thread */
 	struct h264_async *as;
 	int parse_threads;       /* requested workers (m2dec_amd_h264_set_parse_threads / env) */
+	/* 1: this is the pipeline's lookahead context: it runs the header-level state machine ahead of
+	 * the API-visible context, names pictures by virtual frame ids instead of frame slots (no DPB
+	 * output, no caller frames, no header callback) and creates the slice-data jobs */
+	int lookahead;
+	int vid_next;            /* lookahead: round-robin cursor of the virtual frame id allocator */
 };
 
 /* h264_syntax.c */
@@ -349,6 +354,15 @@ int h264_async_add_slice(h264_dec_t *d);
 int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 void h264_async_stop(h264_dec_t *d);
+int h264_async_nal_next(h264_dec_t *d);
+int h264_async_sps(h264_dec_t *d);
+int h264_async_push_nal(h264_dec_t *la);
+
+/* bitio.c */
+int h264_nal_next(h264_dec_t *d);
+
+/* h264_api.c: the NAL loop of decode_picture, shared by the API context and the lookahead context */
+int h264_decode_loop(h264_dec_t *d);
 
 #ifdef __cplusplus
 }

@@ -285,9 +285,36 @@ static int dpb_exist(const h264_dpb_t *dpb, int frame_idx)
 }
 
 /* ------------------------------------------------------------------ frame LRU (h264.cpp:924-962) */
+/* lookahead context: a virtual frame id per picture, unique among the live pictures (the reference
+ * lists and the current one), reused as late as possible (round robin over 64 ids).  The parser
+ * compares frame_idx values only for equality (bS motion tests, the co-located ref map, the record
+ * ref slots), so the API-visible context can translate ids to its real LRU slots picture by
+ * picture (h264_async.c). */
+static void alloc_virtual_frame(h264_dec_t *d)
+{
+	uint64_t live = 0;
+	for (int i = 0; i < 16; ++i) {
+		if (d->refs[0][i].in_use) live |= 1ull << (d->refs[0][i].frame_idx & 63);
+		if (d->refs[1][i].in_use) live |= 1ull << (d->refs[1][i].frame_idx & 63);
+	}
+	for (int k = 0; k < 64; ++k) {
+		const int v = (d->vid_next + k) & 63;
+		if (!(live >> v & 1)) {
+			d->curr_idx = v;
+			d->vid_next = (v + 1) & 63;
+			return;
+		}
+	}
+	d->curr_idx = 0; /* 64 live pictures: impossible (<= 32 reference entries) */
+}
+
 static void find_empty_frame(h264_dec_t *d)
 {
 	int max_idx = 0, max_val = -1;
+	if (d->lookahead) {
+		alloc_virtual_frame(d);
+		return;
+	}
 	for (int i = 0; i < d->num_frames; ++i) {
 		if (dpb_exist(&d->dpb, i)) d->lru[i] = 0;
 		else d->lru[i] += 1;

@@ -15,39 +15,85 @@ typedef struct {
 
 #define ROTL(x, n) (((x) << (n)) | ((x) >> (32 - (n))))
 
-static const uint32_t K[64] = {
-	0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
-	0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
-	0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
-	0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
-	0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
-	0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
-	0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
-	0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
-static const uint8_t R[64] = {
-	7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
-	5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20,
-	4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
-	6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+/* unrolled rounds (the register roles rotate instead of moving values: a <- d, d <- c, c <- b) */
+#define F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
+#define G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
+#define H(x, y, z) ((x) ^ (y) ^ (z))
+#define I(x, y, z) ((y) ^ ((x) | ~(z)))
+#define STEP(f, a, b, c, d, x, k, s) \
+	do { \
+		a += f(b, c, d) + (x) + (k); \
+		a = ROTL(a, s) + b; \
+	} while (0)
 
 static void md5_block(md5_t *m, const uint8_t *p)
 {
 	uint32_t w[16], a = m->h[0], b = m->h[1], c = m->h[2], d = m->h[3];
-	for (int i = 0; i < 16; ++i)
-		w[i] = (uint32_t)p[i * 4] | ((uint32_t)p[i * 4 + 1] << 8) | ((uint32_t)p[i * 4 + 2] << 16) | ((uint32_t)p[i * 4 + 3] << 24);
-	for (int i = 0; i < 64; ++i) {
-		uint32_t f;
-		int g;
-		if (i < 16) { f = (b & c) | (~b & d); g = i; }
-		else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) & 15; }
-		else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
-		else { f = c ^ (b | ~d); g = (7 * i) & 15; }
-		f = f + a + K[i] + w[g];
-		a = d;
-		d = c;
-		c = b;
-		b = b + ROTL(f, R[i]);
-	}
+	memcpy(w, p, 64); /* little-endian host (x86-64) */
+	STEP(F, a, b, c, d, w[0], 0xd76aa478u, 7);
+	STEP(F, d, a, b, c, w[1], 0xe8c7b756u, 12);
+	STEP(F, c, d, a, b, w[2], 0x242070dbu, 17);
+	STEP(F, b, c, d, a, w[3], 0xc1bdceeeu, 22);
+	STEP(F, a, b, c, d, w[4], 0xf57c0fafu, 7);
+	STEP(F, d, a, b, c, w[5], 0x4787c62au, 12);
+	STEP(F, c, d, a, b, w[6], 0xa8304613u, 17);
+	STEP(F, b, c, d, a, w[7], 0xfd469501u, 22);
+	STEP(F, a, b, c, d, w[8], 0x698098d8u, 7);
+	STEP(F, d, a, b, c, w[9], 0x8b44f7afu, 12);
+	STEP(F, c, d, a, b, w[10], 0xffff5bb1u, 17);
+	STEP(F, b, c, d, a, w[11], 0x895cd7beu, 22);
+	STEP(F, a, b, c, d, w[12], 0x6b901122u, 7);
+	STEP(F, d, a, b, c, w[13], 0xfd987193u, 12);
+	STEP(F, c, d, a, b, w[14], 0xa679438eu, 17);
+	STEP(F, b, c, d, a, w[15], 0x49b40821u, 22);
+	STEP(G, a, b, c, d, w[1], 0xf61e2562u, 5);
+	STEP(G, d, a, b, c, w[6], 0xc040b340u, 9);
+	STEP(G, c, d, a, b, w[11], 0x265e5a51u, 14);
+	STEP(G, b, c, d, a, w[0], 0xe9b6c7aau, 20);
+	STEP(G, a, b, c, d, w[5], 0xd62f105du, 5);
+	STEP(G, d, a, b, c, w[10], 0x02441453u, 9);
+	STEP(G, c, d, a, b, w[15], 0xd8a1e681u, 14);
+	STEP(G, b, c, d, a, w[4], 0xe7d3fbc8u, 20);
+	STEP(G, a, b, c, d, w[9], 0x21e1cde6u, 5);
+	STEP(G, d, a, b, c, w[14], 0xc33707d6u, 9);
+	STEP(G, c, d, a, b, w[3], 0xf4d50d87u, 14);
+	STEP(G, b, c, d, a, w[8], 0x455a14edu, 20);
+	STEP(G, a, b, c, d, w[13], 0xa9e3e905u, 5);
+	STEP(G, d, a, b, c, w[2], 0xfcefa3f8u, 9);
+	STEP(G, c, d, a, b, w[7], 0x676f02d9u, 14);
+	STEP(G, b, c, d, a, w[12], 0x8d2a4c8au, 20);
+	STEP(H, a, b, c, d, w[5], 0xfffa3942u, 4);
+	STEP(H, d, a, b, c, w[8], 0x8771f681u, 11);
+	STEP(H, c, d, a, b, w[11], 0x6d9d6122u, 16);
+	STEP(H, b, c, d, a, w[14], 0xfde5380cu, 23);
+	STEP(H, a, b, c, d, w[1], 0xa4beea44u, 4);
+	STEP(H, d, a, b, c, w[4], 0x4bdecfa9u, 11);
+	STEP(H, c, d, a, b, w[7], 0xf6bb4b60u, 16);
+	STEP(H, b, c, d, a, w[10], 0xbebfbc70u, 23);
+	STEP(H, a, b, c, d, w[13], 0x289b7ec6u, 4);
+	STEP(H, d, a, b, c, w[0], 0xeaa127fau, 11);
+	STEP(H, c, d, a, b, w[3], 0xd4ef3085u, 16);
+	STEP(H, b, c, d, a, w[6], 0x04881d05u, 23);
+	STEP(H, a, b, c, d, w[9], 0xd9d4d039u, 4);
+	STEP(H, d, a, b, c, w[12], 0xe6db99e5u, 11);
+	STEP(H, c, d, a, b, w[15], 0x1fa27cf8u, 16);
+	STEP(H, b, c, d, a, w[2], 0xc4ac5665u, 23);
+	STEP(I, a, b, c, d, w[0], 0xf4292244u, 6);
+	STEP(I, d, a, b, c, w[7], 0x432aff97u, 10);
+	STEP(I, c, d, a, b, w[14], 0xab9423a7u, 15);
+	STEP(I, b, c, d, a, w[5], 0xfc93a039u, 21);
+	STEP(I, a, b, c, d, w[12], 0x655b59c3u, 6);
+	STEP(I, d, a, b, c, w[3], 0x8f0ccc92u, 10);
+	STEP(I, c, d, a, b, w[10], 0xffeff47du, 15);
+	STEP(I, b, c, d, a, w[1], 0x85845dd1u, 21);
+	STEP(I, a, b, c, d, w[8], 0x6fa87e4fu, 6);
+	STEP(I, d, a, b, c, w[15], 0xfe2ce6e0u, 10);
+	STEP(I, c, d, a, b, w[6], 0xa3014314u, 15);
+	STEP(I, b, c, d, a, w[13], 0x4e0811a1u, 21);
+	STEP(I, a, b, c, d, w[4], 0xf7537e82u, 6);
+	STEP(I, d, a, b, c, w[11], 0xbd3af235u, 10);
+	STEP(I, c, d, a, b, w[2], 0x2ad7d2bbu, 15);
+	STEP(I, b, c, d, a, w[9], 0xeb86d391u, 21);
 	m->h[0] += a;
 	m->h[1] += b;
 	m->h[2] += c;

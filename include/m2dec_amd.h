@@ -25,6 +25,15 @@ typedef struct {
 	int pictures;
 	int last_error;
 	int pad;
+	/* CLOCK_MONOTONIC seconds: the first decode_picture call, and the last frame delivered to the
+	 * writer (on_frame returned; for the MD5 drivers: its MD5 line written) — the fps interval of
+	 * SURVEY.md §8d.  setup_s: time inside the first set_frames (back-end creation, frame pinning). */
+	double t_start, t_end, setup_s;
+	/* the built-in HIP back end only (m2dec_amd_hip_timing_t of the decode): k_picture launches, their
+	 * HIP-event time, and their algorithmic bytes (F_write + sum_PU 1.5 w h + R_pic) */
+	double kernel_us;
+	int64_t kernel_launches;
+	int64_t alg_bytes;
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).

@@ -45,8 +45,11 @@ class Backend(ctypes.Structure):
 
 
 class Stats(ctypes.Structure):
+    """m2dec_amd_stats_t (include/m2dec_amd.h)."""
     _fields_ = [("frames_out", ctypes.c_int), ("pictures", ctypes.c_int), ("last_error", ctypes.c_int),
-                ("pad", ctypes.c_int)]
+                ("pad", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
+                ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
+                ("alg_bytes", ctypes.c_int64)]
 
 
 class HipTiming(ctypes.Structure):
@@ -232,15 +235,16 @@ def _max_frames(data: bytes) -> int:
     return max(1, data.count(b"\x00\x00\x01"))
 
 
-def decode_stream_md5(data: bytes, device: int = 0, dpb: int = -1) -> List[str]:
+def decode_stream_md5(data: bytes, device: int = 0, dpb: int = -1, stats: Optional[Stats] = None) -> List[str]:
     """The HIP decode path exactly like ``h264dec -O`` (``-d dpb``) with the MD5s computed in C on helper
-    threads (m2dec_amd_decode_stream_md5): the throughput form of ``decode_stream``."""
+    threads (m2dec_amd_decode_stream_md5): the throughput form of ``decode_stream``.  ``stats`` (a
+    Stats) receives the §8d interval: first decode_picture -> last MD5 line written (t_start, t_end)."""
     L = lib()
     if not L.m2dec_amd_hip_available():
         raise RuntimeError("m2dec_amd: no usable gfx950 device for the HIP back end")
     cap = _max_frames(data)
     buf = ctypes.create_string_buffer(35 * cap)
-    st = Stats()
+    st = stats if stats is not None else Stats()
     n = L.m2dec_amd_decode_stream_md5(data, len(data), device, dpb, buf, cap, ctypes.byref(st))
     if n < 0:
         raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")

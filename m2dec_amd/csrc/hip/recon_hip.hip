@@ -1966,6 +1966,13 @@ __global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_batch(const PictureAr
 	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
 }
 
+/* the decode path's launch (one picture per launch, h264d_func): the same blocks as k_batch under
+ * its own name, so that rocprofv3 reports the decode path and the trace replay separately */
+__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_picture(const PictureArgs *pic)
+{
+	picture_block(*pic, blockIdx.x, g_lds);
+}
+
 size_t m2r_deblock_lds_bytes(int W, int Wmb)
 {
 	(void)W;

@@ -211,8 +211,8 @@ struct Sched {
 		/* the arguments go to device memory (pageable source: staged by the copy call) so that the kernel
 		 * reads them through a pointer, as in batch launches */
 		CHECK(hipMemcpyAsync(pargs + k, &a, sizeof(a), hipMemcpyHostToDevice, s));
-		hipLaunchKernelGGL(k_batch, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
-		                   (const PictureArgs *)(pargs + k), picture_blocks(inter_grid, Hmb));
+		hipLaunchKernelGGL(k_picture, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
+		                   (const PictureArgs *)(pargs + k));
 		CHECK(hipGetLastError());
 		tm.inter_launches += j.n_inter ? 1 : 0;
 		tm.intra_launches += j.n_intra ? 1 : 0;

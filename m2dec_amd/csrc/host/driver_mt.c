@@ -14,7 +14,9 @@
  */
 #include <pthread.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
+#include <time.h>
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
@@ -37,7 +39,17 @@ typedef struct {
 	int max;
 	int n;                   /* frames delivered */
 	int failed;
+	int stats;
+	double t_wait, t_copy;   /* caller: waiting for a free ring slot, copying frames */
+	double t_done;           /* the last MD5 line written */
 } md5_pipe_t;
+
+static double now_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static void *md5_worker(void *arg)
 {
@@ -55,7 +67,9 @@ static void *md5_worker(void *arg)
 		char line[35];
 		m2dec_amd_frame_md5(&f, line);
 		if (i < p->max) memcpy(p->md5s + (size_t)i * 35, line, 35);
+		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
+		if (t > p->t_done) p->t_done = t;
 		p->state[k] = 0;
 		pthread_cond_broadcast(&p->cv_free);
 	}
@@ -76,9 +90,11 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	const size_t luma = (size_t)f->width * (size_t)f->height, bytes = luma * 3 / 2;
 	const int k = p->head % MD5_RING;
+	const double t0 = p->stats ? now_s() : 0;
 	pthread_mutex_lock(&p->mu);
 	while (p->state[k] || (bytes > p->cap && !ring_idle(p))) pthread_cond_wait(&p->cv_free, &p->mu);
 	pthread_mutex_unlock(&p->mu);
+	const double t1 = p->stats ? now_s() : 0;
 	if (bytes > p->cap) { /* (re)size the ring while no job holds a buffer; only this thread allocates */
 		for (int j = 0; j < MD5_RING; ++j) {
 			free(p->buf[j]);
@@ -93,6 +109,10 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	}
 	memcpy(p->buf[k], f->luma, luma);
 	memcpy(p->buf[k] + luma, f->chroma, luma / 2);
+	if (p->stats) {
+		p->t_wait += t1 - t0;
+		p->t_copy += now_s() - t1;
+	}
 	m2d_frame_t c = *f;
 	c.luma = p->buf[k];
 	c.chroma = p->buf[k] + luma;
@@ -127,17 +147,23 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	pthread_cond_init(&p.cv_free, NULL);
 	p.md5s = md5s;
 	p.max = max;
+	p.stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	int nth = 0;
 	for (; nth < md5_threads && nth < MD5_THREADS_MAX; ++nth)
 		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
 	if (!nth) return -1;
-	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, stats);
+	m2dec_amd_stats_t st;
+	memset(&st, 0, sizeof(st));
+	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, &st);
 	pthread_mutex_lock(&p.mu);
 	p.quit = 1;
 	pthread_cond_broadcast(&p.cv_job);
 	pthread_mutex_unlock(&p.mu);
 	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
+	if (p.stats) fprintf(stderr, "md5 ring: caller waits %.3f s, frame copies %.3f s (%d threads)\n", p.t_wait, p.t_copy, nth);
 	for (int j = 0; j < MD5_RING; ++j) free(p.buf[j]);
+	if (p.t_done > st.t_end) st.t_end = p.t_done; /* delivered = its MD5 line written */
+	if (stats) *stats = st;
 	pthread_mutex_destroy(&p.mu);
 	pthread_cond_destroy(&p.cv_job);
 	pthread_cond_destroy(&p.cv_free);

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
@@ -41,6 +42,7 @@ static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg
 	d->curr_col = 16;
 	d->sh.first_mb = -1;
 	d->parse_threads = -1; /* default: decided when the back end is created */
+	d->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	return 0;
 }
 
@@ -229,11 +231,25 @@ static int api_decode_picture(void *ctx)
 	return h264_decode_loop(d);
 }
 
+static double mono_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
 {
+	double t0 = 0, t1 = 0;
 	if (idx < 0) return 0;
+	if (d->stats) t0 = mono_s();
 	if (d->as && h264_async_drain(d, idx) < 0) return -1; /* the picture in that slot is parsed and submitted */
+	if (d->stats) t1 = mono_s();
 	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) return -1;
+	if (d->stats) {
+		d->t_drain += t1 - t0;
+		d->t_sync += mono_s() - t1;
+	}
 	*frame = d->frames[idx];
 	return 1;
 }
@@ -294,6 +310,7 @@ void m2dec_amd_h264_release(void *ctx)
 {
 	h264_dec_t *d = CTX(ctx);
 	if (!d) return;
+	if (d->stats) fprintf(stderr, "deliver: drain %.3f s, sync_frame %.3f s\n", d->t_drain, d->t_sync);
 	h264_async_stop(d);
 	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
 	d->have_backend = 0;
@@ -320,7 +337,17 @@ typedef struct {
 	size_t luma_len;
 	uint8_t work[64];
 	int failed;
+	double setup_s;
+	double t_last;           /* on_frame of the last frame returned */
+	void (*on_frame)(void *arg, const m2d_frame_t *f);
+	void *arg;
 } driver_t;
+
+static void emit(driver_t *v, const m2d_frame_t *f)
+{
+	if (v->on_frame) v->on_frame(v->arg, f);
+	v->t_last = mono_s();
+}
 
 static int drv_reread(void *arg)
 {
@@ -367,7 +394,12 @@ static int drv_header(void *arg, void *id)
 	}
 	v->nframes = bufnum;
 	v->luma_len = luma_len;
-	if (h264d_func->set_frames(v->d, bufnum, v->frames, v->work, info.additional_size) < 0) v->failed = 1;
+	{
+		const double t0 = mono_s();
+		if (h264d_func->set_frames(v->d, bufnum, v->frames, v->work, info.additional_size) < 0) v->failed = 1;
+		v->setup_s += mono_s() - t0;
+		if (v->d->stats) fprintf(stderr, "set_frames: %d frames, %.3f s\n", bufnum, mono_s() - t0);
+	}
 	return 0;
 }
 
@@ -401,11 +433,15 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 	v.d = d;
 	v.data = data;
 	v.len = len;
+	v.on_frame = on_frame;
+	v.arg = arg;
 	h264d_func->init(d, dpb, drv_header, &v);
 	d->device = device;
 	if (backend) m2dec_amd_h264_set_backend(d, backend);
 	if (parse_threads >= 0) m2dec_amd_h264_set_parse_threads(d, parse_threads);
 	dec_bits_set_callback(d->stream, drv_reread, &v);
+	const double t_start = mono_s();
+	v.t_last = t_start;
 	/* h264dec.cpp:251-257 + M2Decoder::decode / decode_residual (m2decoder.h:132-157) */
 	for (;;) {
 		err = 0;
@@ -414,7 +450,7 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 			if (v.failed) { err = -1; break; }
 			if (err < 0) {
 				while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
-					if (on_frame) on_frame(arg, &frm);
+					emit(&v, &frm);
 					n++;
 					h264d_func->get_decoded_frame(d, &frm, 1);
 				}
@@ -422,12 +458,13 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 			}
 		}
 		h264d_func->get_decoded_frame(d, &frm, 0);
-		if (on_frame) on_frame(arg, &frm);
+		if (d->stats && n == 0) fprintf(stderr, "first frame out: %.3f s\n", mono_s() - t_start);
+		emit(&v, &frm);
 		n++;
 		err = h264d_func->decode_picture(d);
 		if (err < 0) {
 			while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
-				if (on_frame) on_frame(arg, &frm);
+				emit(&v, &frm);
 				n++;
 				h264d_func->get_decoded_frame(d, &frm, 1);
 			}
@@ -435,10 +472,22 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 		}
 	}
 done:
+	if (d->stats) fprintf(stderr, "stream: %d frames, %.3f s\n", n, mono_s() - t_start);
+	if (stats && !backend && d->have_backend) {
+		m2dec_amd_hip_timing_t t;
+		if (m2dec_amd_hip_backend_timing(&d->backend, &t) == 0) {
+			stats->kernel_us = t.picture_us;
+			stats->kernel_launches = t.kernel_launches;
+			stats->alg_bytes = t.frame_bytes + t.ref_bytes + t.record_bytes;
+		}
+	}
 	if (stats) {
 		stats->frames_out = n;
 		stats->pictures = (int)d->pictures;
 		stats->last_error = err;
+		stats->t_start = t_start;
+		stats->t_end = v.t_last;
+		stats->setup_s = v.setup_s;
 	}
 	if (backend) d->have_backend = 0; /* borrowed: the caller destroys it */
 	m2dec_amd_h264_release(d);

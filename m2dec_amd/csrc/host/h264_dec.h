@@ -331,6 +331,8 @@ struct h264_dec {
 	 * output, no caller frames, no header callback) and creates the slice-data jobs */
 	int lookahead;
 	int vid_next;            /* lookahead: round-robin cursor of the virtual frame id allocator */
+	int stats;               /* M2DEC_AMD_ASYNC_STATS: time spent delivering frames */
+	double t_drain, t_sync;
 };
 
 /* h264_syntax.c */

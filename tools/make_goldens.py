@@ -31,7 +31,8 @@ STREAMS = [
     ("cov_tools_s1", "cov_tools", 1, 16),
     ("cov_tools_s2", "cov_tools", 2, 16),
     ("cov_tools_cavlc_s1", "cov_tools_cavlc", 1, 16),
-] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)]  # C4: one c3 stream per GPU, seed 1 + rank
+] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)] \
+  + [(f"c5_4k_s{s}", "c5", s, 16) for s in range(2, 9)]  # C4 / C5: one stream per GPU, seed 1 + rank
 
 
 def gen(preset, seed, frames, out):

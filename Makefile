@@ -18,10 +18,11 @@ HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o
 LIB := m2dec_amd/lib/libm2dec_amd.so
 ORACLE := oracle/_build/liboracle.so
 GEN := tools/_build/h264gen
+M2VGEN := tools/_build/m2vgen
 
 APP := m2dec_amd/lib/h264dec
 
-all: $(LIB) $(ORACLE) $(GEN) $(APP)
+all: $(LIB) $(ORACLE) $(GEN) $(M2VGEN) $(APP)
 
 $(APP): m2dec_amd/csrc/app/h264dec.c $(LIB) include/m2dec_amd.h
 	$(CC) -O2 -Wall -std=gnu11 -Iinclude -o $@ $< -Lm2dec_amd/lib -lm2dec_amd -Wl,-rpath,'$$ORIGIN'
@@ -45,6 +46,10 @@ $(ORACLE): oracle/recon_oracle.c include/m2d_recon.h include/m2d.h
 $(GEN): $(wildcard tools/h264gen/*.c) $(wildcard tools/h264gen/*.h) m2dec_amd/csrc/host/h264_spec_tables.c
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ $(wildcard tools/h264gen/*.c) m2dec_amd/csrc/host/h264_spec_tables.c -lm
+
+$(M2VGEN): tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c m2dec_amd/csrc/host/mpeg2_dec.h tools/h264gen/bitwriter.h
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c -lm
 
 DBG_LIB := build/dbg/libm2dec_amd_stamps.so
 $(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o

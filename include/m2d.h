@@ -105,6 +105,9 @@ enum {
 
 /* The H.264 decoder: GPU reconstruction behind the reference's function table. */
 extern const m2d_func_table_t * const h264d_func;
+/* The MPEG-1/2 video decoder (mpeg2.cpp:1800-1811; mpeg2.h): intra pictures on the CPU
+ * (BASELINE.json configs[0]); P / B pictures are reported as errors. */
+extern const m2d_func_table_t * const m2d_func;
 
 #ifdef __cplusplus
 }

@@ -99,6 +99,33 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_t *lens, int device,
                                  char *const *md5s, const int *max, int *frames);
 
+/* M2Decoder (m2decoder.h:33-223) over any function table (h264d_func: h264 = 1, m2d_func: 0): the
+ * header callback sizes a Frames pool, the output loop delivers every frame to on_frame in output
+ * order; emptify = h264dec -e, skip = h264dec -f n.  Returns the last decode_picture result (-2: end
+ * of the data; -1: error) also in *last_error. */
+int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
+                           int emptify, int skip, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
+                           int *last_error);
+
+/* ---- MPEG-1/2 (m2d_func, m2dec_amd/csrc/host/mpeg2_dec.c) */
+/* Free the heap an m2d_func context owns (its start-code unit buffer). */
+void m2dec_amd_m2v_release(void *ctx);
+/* CLIP255C arguments outside the reference table's domain [-256, 767] seen by a context. */
+uint64_t m2dec_amd_m2v_clip_violations(const void *ctx);
+/* VLC probes for the table tests: one codeword at the MSB end of bits32.  DCT (table 0 = B.14,
+ * 1 = B.15): length incl. the sign bit, run (-1: EOB / escape), sign-folded level (2|l| + s).
+ * Plain tables (0: macroblock_address_increment after its leading 0, 1 / 2: dct_dc_size luma /
+ * chroma, 3: motion_code after its leading 0, signed): length and value.  0 = invalid code. */
+int m2dec_amd_m2v_dct_code(int table, uint32_t bits32, int *run, int *level);
+int m2dec_amd_m2v_vlc_code(int table, uint32_t bits32, int *value);
+/* Block-level probes (fresh decoder state): the intra DC of component cc (0 luma) with predictor
+ * `pred` -> *value (dequantised, << (3 - precision)); the AC coefficients of an intra block (DC in
+ * coef[0]) dequantised with q_scale and qmat (NULL: flat 16), mismatch control / oddification
+ * applied -> coef[64] raster.  Both return the bits consumed, or -1 on an undefined code. */
+int m2dec_amd_m2v_intra_dc(const uint8_t *bits, size_t n, int cc, int dc_precision, int pred, int *value);
+int m2dec_amd_m2v_intra_ac(const uint8_t *bits, size_t n, int mpeg2, int intra_vlc_format, int alternate_scan,
+                           int q_scale, const uint8_t *qmat, int dc, int16_t coef[64]);
+
 /* ---- record traces (m2dec_amd/csrc/host/trace.c): a stream parsed once, records kept in memory */
 typedef struct m2dec_amd_trace m2dec_amd_trace_t;
 typedef struct {

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("M2DEC_AMD_LIB") or os.path.join(_HERE, "lib", "libm2d
 
 __all__ = [
     "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",
-    "decode_stream", "decode_stream_md5", "decode_streams", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
+    "decode_stream", "decode_stream_md5", "decode_streams", "decode_m2v", "decode_table_frames", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
 ]
 
 
@@ -134,6 +134,15 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_replay_timing.restype = ctypes.c_int
         L.m2dec_amd_hip_replay_md5.argtypes = [vp, ctypes.c_char_p]
         L.m2dec_amd_hip_replay_md5.restype = ctypes.c_int
+        L.m2dec_amd_decode_table.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ON_FRAME, vp, ctypes.POINTER(ctypes.c_int)]
+        L.m2dec_amd_decode_table.restype = ctypes.c_int
+        L.m2dec_amd_m2v_dct_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip, ip]
+        L.m2dec_amd_m2v_vlc_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip]
+        L.m2dec_amd_m2v_intra_dc.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
+        L.m2dec_amd_m2v_intra_ac.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int16)]
         L.m2dec_amd_hip_replay_destroy.argtypes = [vp]
         L.m2dec_amd_hip_replay_destroy.restype = None
         _lib = L
@@ -274,6 +283,33 @@ def decode_streams(datas: List[bytes], device: int = 0) -> List[List[str]]:
         raw = bufs[i].raw
         out.append([raw[35 * k:35 * k + 32].decode() for k in range(min(frames[i], caps[i]))])
     return out
+
+
+def decode_table_frames(table: str, data: bytes, dpb: int = -1, emptify: bool = False, skip: int = 0,
+                        on_frame: Optional[Callable[[Frame], None]] = None) -> tuple:
+    """M2Decoder over the reference-shaped function table ``table`` ("m2d_func" MPEG-1/2 on the CPU, or
+    "h264d_func") exactly like the ``h264dec`` CLI (m2dec_amd_decode_table): returns (MD5 lines,
+    last decode_picture result: -2 end of data / -1 error)."""
+    L = lib()
+    md5s: List[str] = []
+
+    def _cb(_arg, fp):
+        md5s.append(frame_md5(fp.contents))
+        if on_frame is not None:
+            on_frame(fp.contents)
+
+    cb = ON_FRAME(_cb)
+    err = ctypes.c_int()
+    tab = ctypes.c_void_p.in_dll(L, table)
+    L.m2dec_amd_decode_table(tab, 1 if table == "h264d_func" else 0, data, len(data), dpb, int(emptify), skip, cb,
+                             None, ctypes.byref(err))
+    return md5s, err.value
+
+
+def decode_m2v(data: bytes) -> List[str]:
+    """An MPEG-1/2 video elementary stream through m2d_func (CPU, BASELINE.json configs[0]) like
+    ``h264dec -O x.m2v``: the MD5 line of every output frame."""
+    return decode_table_frames("m2d_func", data)[0]
 
 
 class H264Decoder:

@@ -56,6 +56,12 @@ static int next_byte(dec_bits *ths)
 	return *ths->buf_++;
 }
 
+/* the byte-level feeder for the start-code scanners of the codecs (H.264 NALs, MPEG-2 units) */
+int m2d_stream_next_byte(dec_bits *ths)
+{
+	return next_byte(ths);
+}
+
 uint32_t show_bits(dec_bits *ths, int bit_len)
 {
 	while (ths->cache_len_ < bit_len) {

@@ -30,6 +30,7 @@ def test_all_declared_symbols_exported(built):
     assert not missing, missing
     # the reference's decoder table (h264.h:457) is an exported data symbol
     assert ctypes.c_void_p.in_dll(lib, "h264d_func").value
+    assert ctypes.c_void_p.in_dll(lib, "m2d_func").value  # mpeg2.cpp:1811
 
 
 def test_declared_symbol_scan_is_not_empty():

@@ -23,3 +23,28 @@ def test_cli_md5_matches_golden(built, tmp_path, name):
     subprocess.run([APP, "-O", src], cwd=tmp_path, check=True, timeout=300)
     got = open(tmp_path / f"{os.path.splitext(os.path.basename(src))[0]}.out", "rb").read()
     assert got == want
+
+
+@pytest.mark.gpu
+def test_cli_skip_to_idr(built, tmp_path):
+    """`h264dec -f 20` (M2Decoder::skip_frames, m2decoder.h:96-131): F1's SPS / PPS are replayed, decoding
+    starts at the IDR before frame 20, and the output equals the tail of the full decode."""
+    src = os.path.join(ROOT, "tests", "golden", "f1_realshort.264")
+    want = open(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"), "rb").read()
+    r = subprocess.run([APP, "-f", "20", "-O", src], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Skip " in r.stderr
+    got = open(tmp_path / "f1_realshort.out", "rb").read()
+    assert 0 < len(got) < len(want) and len(got) % 34 == 0
+    assert want.endswith(got)
+
+
+@pytest.mark.gpu
+def test_cli_mpeg2_c1(built, tmp_path):
+    """BASELINE.json configs[0] in the GPU pass too: `h264dec -O c1.m2v` (MPEG-2 on the CPU path)."""
+    from tests.test_mpeg2_cpu import GOLD, m2v_stream
+    src = tmp_path / "c1.m2v"
+    src.write_bytes(m2v_stream("c1_480p_s1"))
+    r = subprocess.run([APP, "-O", str(src)], cwd=tmp_path, capture_output=True, timeout=300)
+    assert r.returncode == 255, r.stderr  # MPEG-2 decode_picture ends with -1 (mpeg2.cpp:1583-1604)
+    assert (tmp_path / "c1.out").read_bytes() == b"".join(m.encode() + b"\r\n" for m in GOLD["c1_480p_s1"]["md5"])

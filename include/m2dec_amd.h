@@ -37,7 +37,8 @@ typedef struct {
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).
- * The context takes ownership: m2dec_amd_h264_release() calls be->destroy. */
+ * The context takes ownership: m2dec_amd_h264_release() calls be->destroy.  be == NULL detaches the
+ * current back end without destroying it (a borrowed one). */
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
 /* GPU ordinal used by the default back end (call after init, before the first SPS). */
 int m2dec_amd_h264_set_device(void *ctx, int device);
@@ -106,6 +107,10 @@ int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_
 int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
                            int emptify, int skip, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
                            int *last_error);
+/* The same with an H.264 back end to borrow (NULL: the HIP back end) and parse-ahead workers (-1 default). */
+int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
+                            int emptify, int skip, const m2r_backend_t *backend, int parse_threads,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
 
 /* ---- MPEG-1/2 (m2d_func, m2dec_amd/csrc/host/mpeg2_dec.c) */
 /* Free the heap an m2d_func context owns (its start-code unit buffer). */

@@ -137,6 +137,10 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_decode_table.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ON_FRAME, vp, ctypes.POINTER(ctypes.c_int)]
         L.m2dec_amd_decode_table.restype = ctypes.c_int
+        L.m2dec_amd_decode_table2.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.POINTER(Backend), ctypes.c_int, ON_FRAME,
+                                              vp, ctypes.POINTER(ctypes.c_int)]
+        L.m2dec_amd_decode_table2.restype = ctypes.c_int
         L.m2dec_amd_m2v_dct_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip, ip]
         L.m2dec_amd_m2v_vlc_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip]
         L.m2dec_amd_m2v_intra_dc.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
@@ -286,7 +290,8 @@ def decode_streams(datas: List[bytes], device: int = 0) -> List[List[str]]:
 
 
 def decode_table_frames(table: str, data: bytes, dpb: int = -1, emptify: bool = False, skip: int = 0,
-                        on_frame: Optional[Callable[[Frame], None]] = None) -> tuple:
+                        on_frame: Optional[Callable[[Frame], None]] = None, backend: Optional[Backend] = None,
+                        parse_threads: int = -1) -> tuple:
     """M2Decoder over the reference-shaped function table ``table`` ("m2d_func" MPEG-1/2 on the CPU, or
     "h264d_func") exactly like the ``h264dec`` CLI (m2dec_amd_decode_table): returns (MD5 lines,
     last decode_picture result: -2 end of data / -1 error)."""
@@ -301,8 +306,9 @@ def decode_table_frames(table: str, data: bytes, dpb: int = -1, emptify: bool = 
     cb = ON_FRAME(_cb)
     err = ctypes.c_int()
     tab = ctypes.c_void_p.in_dll(L, table)
-    L.m2dec_amd_decode_table(tab, 1 if table == "h264d_func" else 0, data, len(data), dpb, int(emptify), skip, cb,
-                             None, ctypes.byref(err))
+    L.m2dec_amd_decode_table2(tab, 1 if table == "h264d_func" else 0, data, len(data), dpb, int(emptify), skip,
+                              ctypes.byref(backend) if backend is not None else None, parse_threads, cb, None,
+                              ctypes.byref(err))
     return md5s, err.value
 
 

@@ -135,11 +135,18 @@ int h264_nal_next(h264_dec_t *d)
 		d->nal_replay = 0;
 		return 0;
 	}
+	/* the refill callback reported the end of the data: like the reference's error exit (longjmp out of
+	 * decode_picture, bitio.c / h264.cpp:673-685), nothing more is read in this decode_picture call;
+	 * the next call asks the callback again (h264dec -f feeds the stream after its header replay) */
+	if (d->eos) return -1;
 	/* find a start code */
 	if (!d->nal_pending) {
 		for (;;) {
 			c = next_byte(st);
-			if (c < 0) return -1;
+			if (c < 0) {
+				d->eos = 1;
+				return -1;
+			}
 			if (c == 0) {
 				zeros++;
 			} else {
@@ -153,7 +160,10 @@ int h264_nal_next(h264_dec_t *d)
 	zeros = 0;
 	for (;;) {
 		c = next_byte(st);
-		if (c < 0) break;
+		if (c < 0) {
+			d->eos = 1;
+			break;
+		}
 		if (zeros >= 2 && c == 1) {
 			/* next start code: drop the zero bytes that belong to it */
 			d->nal_len -= (size_t)((zeros > 3) ? 3 : zeros);

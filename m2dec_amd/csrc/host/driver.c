@@ -157,6 +157,13 @@ int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t
                            int emptify, int skip, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
                            int *last_error)
 {
+	return m2dec_amd_decode_table2(func, h264, data, len, dpb, emptify, skip, NULL, -1, on_frame, arg, last_error);
+}
+
+int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
+                            int emptify, int skip, const m2r_backend_t *backend, int parse_threads,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+{
 	drv_t v;
 	m2d_frame_t frm;
 	int err = -1;
@@ -168,6 +175,8 @@ int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t
 	v.ctx = calloc(1, func->context_size);
 	if (!v.ctx) return -1;
 	func->init(v.ctx, dpb, header_cb, &v);
+	if (h264 && backend) m2dec_amd_h264_set_backend(v.ctx, backend);
+	if (h264 && parse_threads >= 0) m2dec_amd_h264_set_parse_threads(v.ctx, parse_threads);
 	dec_bits_set_callback(func->stream_pos(v.ctx), reread, &v);
 	if (skip) {
 		long skipped_bytes = 0;
@@ -204,6 +213,7 @@ int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t
 	}
 done:
 	if (last_error) *last_error = err;
+	if (h264 && backend) m2dec_amd_h264_set_backend(v.ctx, NULL); /* borrowed: the caller destroys it */
 	if (h264) m2dec_amd_h264_release(v.ctx);
 	else m2dec_amd_m2v_release(v.ctx);
 	free(v.ctx);

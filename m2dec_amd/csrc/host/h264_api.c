@@ -228,6 +228,8 @@ static int api_decode_picture(void *ctx)
 {
 	h264_dec_t *d = CTX(ctx);
 	if (!d) return -1;
+	d->eos = 0;
+	if (d->as) h264_async_resume(d);
 	return h264_decode_loop(d);
 }
 
@@ -285,7 +287,11 @@ const m2d_func_table_t * const h264d_func = &h264d_func_;
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
 {
 	h264_dec_t *d = CTX(ctx);
-	if (!d || !be) return -1;
+	if (!d) return -1;
+	if (!be) { /* detach a borrowed back end without destroying it */
+		d->have_backend = 0;
+		return 0;
+	}
 	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
 	d->backend = *be;
 	d->have_backend = 1;

@@ -558,6 +558,17 @@ int h264_async_push_nal(h264_dec_t *la)
 	return 0;
 }
 
+/* a new decode_picture call: a lookahead that stopped at the end of the data may read again (the
+ * caller's refill callback can have more data now); one that failed stays stopped */
+void h264_async_resume(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	if (as->la_done && !as->la_err) {
+		as->la_done = 0;
+		as->la->eos = 0;
+	}
+}
+
 /* API context: the next NAL (0), end of data (-1), or the lookahead failed before this point (-3) */
 int h264_async_nal_next(h264_dec_t *d)
 {

@@ -270,7 +270,7 @@ struct h264_dec {
 	size_t nal_len, nal_cap;
 	int nal_pending;         /* a NAL was read but not consumed (new picture detected) */
 	int nal_replay;          /* the current NAL is handed out again by the next h264_nal_next */
-	int eos;
+	int eos;                 /* the refill callback reported the end of the data in this decode_picture call */
 
 	h264_sps_t sps[32];
 	h264_pps_t pps[256];
@@ -357,6 +357,7 @@ int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 void h264_async_stop(h264_dec_t *d);
 int h264_async_nal_next(h264_dec_t *d);
+void h264_async_resume(h264_dec_t *d);
 int h264_async_sps(h264_dec_t *d);
 int h264_async_push_nal(h264_dec_t *la);
 

@@ -27,11 +27,11 @@ def test_cli_md5_matches_golden(built, tmp_path, name):
 
 @pytest.mark.gpu
 def test_cli_skip_to_idr(built, tmp_path):
-    """`h264dec -f 20` (M2Decoder::skip_frames, m2decoder.h:96-131): F1's SPS / PPS are replayed, decoding
-    starts at the IDR before frame 20, and the output equals the tail of the full decode."""
+    """`h264dec -f 33` (M2Decoder::skip_frames, m2decoder.h:96-131): F1's SPS / PPS are replayed, decoding
+    starts at the IDR before frame 33 (frame 30), and the output equals the tail of the full decode."""
     src = os.path.join(ROOT, "tests", "golden", "f1_realshort.264")
     want = open(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"), "rb").read()
-    r = subprocess.run([APP, "-f", "20", "-O", src], cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([APP, "-f", "33", "-O", src], cwd=tmp_path, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Skip " in r.stderr
     got = open(tmp_path / "f1_realshort.out", "rb").read()

@@ -34,3 +34,36 @@ def test_parse_ahead_4k_multislice(built):
     with OracleBackend() as ob:
         got = m2dec_amd.decode_stream(stream("c5_4k_s1"), backend=ob.be, parse_threads=6)
     assert got == GOLDEN["c5_4k_s1"]["md5"]
+
+
+@pytest.mark.parametrize("threads", [0, 4])
+def test_skip_to_idr_cpu(built, threads):
+    """h264dec -f (M2Decoder::skip_frames): the headers before the key frame are replayed, decoding
+    starts at F1's IDR at frame 30 (the last key frame before frame 33), through the oracle back end;
+    end of data inside one decode_picture call ends that call (the header replay's sentinel)."""
+    data = open(os.path.join(ROOT, "tests", "golden", "f1_realshort.264"), "rb").read()
+    gold = golden_md5s(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"))
+    with OracleBackend() as ob:
+        got, err = m2dec_amd.decode_table_frames("h264d_func", data, skip=33, backend=ob.be, parse_threads=threads)
+    assert err == -2 and got == gold[30:]
+    with OracleBackend() as ob:
+        got, err = m2dec_amd.decode_table_frames("h264d_func", data, skip=20, backend=ob.be, parse_threads=threads)
+    assert got == gold
+
+
+@pytest.mark.parametrize("threads", [0, 4])
+@pytest.mark.parametrize("dpb,emptify", [(-1, True), (16, False), (1, False)])
+def test_output_calls_match_any_caller_pattern(built, threads, dpb, emptify):
+    """The DPB options of h264dec (-d, -b, -e: M2Decoder::decode's emptify loop) change when frames are
+    popped, never what they are: with the lookahead the API context still answers every peek / get
+    exactly as the synchronous decoder."""
+    name = "cov_cabac_s1"
+    with OracleBackend() as ob:
+        got, err = m2dec_amd.decode_table_frames("h264d_func", stream(name), dpb=dpb, emptify=emptify, backend=ob.be,
+                                                 parse_threads=threads)
+    with OracleBackend() as ob:
+        ref, _ = m2dec_amd.decode_table_frames("h264d_func", stream(name), dpb=dpb, emptify=emptify, backend=ob.be,
+                                               parse_threads=0)
+    assert err == -2 and got == ref
+    if dpb != 1:
+        assert sorted(got) == sorted(GOLDEN[name]["md5"])

@@ -45,6 +45,28 @@ static inline int clip255c(int v)
 	return clip255(v);
 }
 
+/* Hit counters of the reference quirks the GPU kernels reproduce, so that a
+ * test can prove each one is executed by some golden stream (oracle_quirk_hits):
+ *   0 Q_SAT16      explicit bi-weighting where the SSE2 int16 saturation changes the result (A#1)
+ *   1 Q_W128_EXP   explicit weight -128 used (int8 store of 1 << 7, A#16)
+ *   2 Q_W128_IMP   implicit weight -128 used (int8 wrap of w = 128, A#16)
+ *   3 Q_SWAR_BIG   DC-only SWAR add with |adj| >= 200 that saturates a byte (A#17 path at large DC)
+ *   4 Q_DEQ8_TRUNC 8x8 dequant below QP 12 whose truncated scale differs from the rounded one (A#3)
+ *   5 Q_UMV        motion compensation reading outside the reference frame (A#13)
+ *   6 Q_PCM        I_PCM macroblocks (deblock QP quirk A#5)
+ *   7 Q_SWAR_CALLS DC-only SWAR adds */
+enum { Q_SAT16, Q_W128_EXP, Q_W128_IMP, Q_SWAR_BIG, Q_DEQ8_TRUNC, Q_UMV, Q_PCM, Q_SWAR_CALLS, Q_N };
+static unsigned long g_quirk[Q_N];
+
+unsigned long oracle_quirk_hits(int which, int reset)
+{
+	unsigned long v;
+	if (which < 0 || which >= Q_N) return 0;
+	v = g_quirk[which];
+	if (reset) g_quirk[which] = 0;
+	return v;
+}
+
 unsigned long oracle_domain_violations(int reset)
 {
 	unsigned long v = g_domain_violations;
@@ -75,6 +97,7 @@ static int scale8(int qp, int x, int y)
 	else if (((x & 3) == 0 && (y & 3) == 2) || ((x & 3) == 2 && (y & 3) == 0)) cls = 4;
 	else cls = 5;
 	v = norm8[qp % 6][cls];
+	if (sh < 0 && ((v >> (-sh)) << (-sh)) != v) g_quirk[Q_DEQ8_TRUNC]++;
 	return sh >= 0 ? v << sh : v >> (-sh); /* truncation below qp 12: Appendix A #3 */
 }
 
@@ -137,15 +160,18 @@ static void idct8(const int *c, int *r)
 /* m2d.h:286-341: DC-only add through byte replication + per-byte saturation */
 static void dconly_swar(uint8_t *dst, int gap, int stride, int n, int dc)
 {
-	int adj = (dc + 32) >> 6;
+	int adj = (dc + 32) >> 6, sat = 0;
 	uint64_t v = (uint64_t)(adj < 0 ? -(int64_t)adj : adj);
 	uint64_t w = (n == 4) ? (uint64_t)(uint32_t)(v * 0x01010101u) : v * 0x0101010101010101ull;
 	for (int y = 0; y < n; ++y)
 		for (int x = 0; x < n; ++x) {
 			int b = (int)((w >> (8 * x)) & 255);
 			uint8_t *p = dst + y * stride + x * gap;
+			sat |= adj < 0 ? (*p - b < 0) : (*p + b > 255);
 			*p = (uint8_t)(adj < 0 ? (*p - b < 0 ? 0 : *p - b) : (*p + b > 255 ? 255 : *p + b));
 		}
+	g_quirk[Q_SWAR_CALLS]++;
+	if (sat && (adj >= 200 || adj <= -200)) g_quirk[Q_SWAR_BIG]++;
 }
 
 /* ======================================================================== frame access */
@@ -734,6 +760,7 @@ static void mc_block(const plane_t *ref, int bx, int by, const int16_t *mv, int 
 	int mx = mv[0], my = mv[1];
 	int fx = mx & 3, fy = my & 3;
 	int ix = bx + (mx >> 2), iy = by + (my >> 2);
+	if (ix - 2 < 0 || iy - 2 < 0 || ix + 4 + 3 > w || iy + 4 + 3 > h) g_quirk[Q_UMV]++;
 	for (int y = 0; y < 4; ++y)
 		for (int x = 0; x < 4; ++x) l[y * 4 + x] = luma_sample(ref->luma, stride, w, h, ix + x, iy + y, fx, fy);
 	{
@@ -768,6 +795,11 @@ static int wp_bi_explicit(int p0, int p1, int w0, int w1, int o0, int o1, int sh
 	t = sat16(t + p1 * w1);
 	t >>= shift + 1;
 	t = sat16(t + ((o0 + o1 + 1) >> 1));
+	{
+		const int exact = ((p0 * w0 + p1 * w1 + (1 << shift)) >> (shift + 1)) + ((o0 + o1 + 1) >> 1);
+		if (clip255(exact) != clip255(t)) g_quirk[Q_SAT16]++;
+	}
+	if (w0 == -128 || w1 == -128) g_quirk[Q_W128_EXP]++;
 	return clip255(t);
 }
 
@@ -808,6 +840,7 @@ static void inter_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, co
 			} else {
 				int lx = use[0] ? 0 : 1;
 				int r = it->refidx[lx][b8];
+				if (sl->w[lx][r][0] == -128 || sl->w[lx][r][1] == -128 || sl->w[lx][r][2] == -128) g_quirk[Q_W128_EXP]++;
 				for (int k = 0; k < 16; ++k)
 					dl[(k >> 2) * stride + (k & 3)] = (uint8_t)wp_uni(L[lx][k], sl->w[lx][r][0], sl->o[lx][r][0], sl->log2wd[0]);
 				for (int k = 0; k < 4; ++k) {
@@ -819,6 +852,7 @@ static void inter_mb(const m2r_picture_t *pic, const m2r_mb_t *m, plane_t *f, co
 			if (sl->wp_mode == M2R_WP_IMPLICIT) {
 				int r0 = it->refidx[0][b8], r1 = it->refidx[1][b8];
 				int w0 = sl->iw[r0][r1][0], w1 = sl->iw[r0][r1][1];
+				if (w0 == -128 || w1 == -128) g_quirk[Q_W128_IMP]++;
 				for (int k = 0; k < 16; ++k) dl[(k >> 2) * stride + (k & 3)] = (uint8_t)wp_bi_implicit(L[0][k], L[1][k], w0, w1);
 				for (int k = 0; k < 4; ++k) {
 					dc[(k >> 1) * stride + (k & 1) * 2] = (uint8_t)wp_bi_implicit(CB[0][k], CB[1][k], w0, w1);
@@ -1014,7 +1048,10 @@ void oracle_recon_picture(const m2r_picture_t *pic, const m2d_frame_t *frames, i
 		for (int mbx = 0; mbx < W; ++mbx) {
 			const m2r_mb_t *m = &pic->mb[mby * W + mbx];
 			if (m->kind == M2R_MB_INTER) inter_mb(pic, m, cur, fr, mbx, mby);
-			else if (m->kind == M2R_MB_PCM) pcm_mb(pic, m, cur, mbx, mby);
+			else if (m->kind == M2R_MB_PCM) {
+				g_quirk[Q_PCM]++;
+				pcm_mb(pic, m, cur, mbx, mby);
+			}
 			else intra_mb(pic, m, cur, mbx, mby);
 		}
 	if (pic->deblock) deblock_picture(pic, cur);

@@ -19,6 +19,8 @@ def oracle_lib():
         _orc.oracle_backend_create.restype = ctypes.c_int
         _orc.oracle_domain_violations.argtypes = [ctypes.c_int]
         _orc.oracle_domain_violations.restype = ctypes.c_ulong
+        _orc.oracle_quirk_hits.argtypes = [ctypes.c_int, ctypes.c_int]
+        _orc.oracle_quirk_hits.restype = ctypes.c_ulong
     return _orc
 
 
@@ -48,3 +50,11 @@ def golden_md5s(path):
     data = open(path, "rb").read()
     assert len(data) % 34 == 0
     return [data[i:i + 32].decode() for i in range(0, len(data), 34)]
+
+
+QUIRKS = ["sat16", "w128_explicit", "w128_implicit", "swar_big", "deq8_trunc", "umv", "pcm", "swar_calls"]
+
+
+def quirk_hits(reset=True):
+    """Counts of the Appendix A quirk paths the oracle executed since the last reset (recon_oracle.c)."""
+    return {q: int(oracle_lib().oracle_quirk_hits(i, 1 if reset else 0)) for i, q in enumerate(QUIRKS)}

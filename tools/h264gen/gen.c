@@ -560,7 +560,20 @@ static void choose_residual(gctx_t *g, mbsyn_t *s, gmb_t *m, int qp)
 	} else {
 		for (int b8 = 0; b8 < 4; ++b8) {
 			if (!((m->cbp >> b8) & 1)) continue;
-			if (s->t8x8) {
+			if (s->t8x8 && g->p->quirks && pct(15)) {
+				/* one DC coefficient: the reference's SWAR DC-only add (h264.cpp:4072-4080, m2d.h:306-336)
+				 * adjusting by 200..255 */
+				static const int n0[6] = {20, 22, 26, 28, 32, 36};
+				const int sc = qp >= 12 ? n0[qp % 6] << (qp / 6 - 2) : n0[qp % 6] >> (2 - qp / 6), t = rr(200, 255);
+				int level = imax(1, (t * 64 + sc / 2) / sc);
+				while (level > 1 && ((level * sc + 32) >> 6) > 255) level--;
+				memset(s->luma8[b8], 0, sizeof(s->luma8[b8]));
+				s->luma8[b8][0] = (int16_t)(pct(50) ? -level : level);
+				for (int k = 0; k < 4; ++k) {
+					int b = b8 * 4 + k;
+					m->nnz[blk_y[b] * 4 + blk_x[b]] = 1;
+				}
+			} else if (s->t8x8) {
 				gen_levels(s->luma8[b8], 0, 64, scale8max(qp), RES_BUDGET * 64 / 144, dens + 2);
 				for (int k = 0; k < 4; ++k) {
 					int b = b8 * 4 + k;
@@ -570,7 +583,16 @@ static void choose_residual(gctx_t *g, mbsyn_t *s, gmb_t *m, int qp)
 				int any = 0;
 				for (int k = 0; k < 4; ++k) {
 					int b = b8 * 4 + k;
-					if (pct(g->p->coef_pct) || (k == 3 && !any)) {
+					if (g->p->quirks && pct(12)) {
+						/* DC-only block whose DC-only add (m2d.h:306-336) adjusts by 200..255 */
+						static const int n0[6] = {10, 11, 13, 14, 16, 18};
+						const int sc = n0[qp % 6] << (qp / 6), t = rr(200, 255);
+						int level = imax(1, (t * 64 + sc / 2) / sc);
+						while (level > 1 && ((level * sc + 32) >> 6) > 255) level--;
+						memset(s->luma[b], 0, sizeof(s->luma[b]));
+						s->luma[b][0] = (int16_t)(pct(50) ? -level : level);
+						any = 1;
+					} else if (pct(g->p->coef_pct) || (k == 3 && !any)) {
 						gen_levels(s->luma[b], 0, 16, scale4max(qp), RES_BUDGET, dens);
 						any = 1;
 					} else {
@@ -1328,23 +1350,29 @@ typedef struct {
 static void write_pred_weight_table(gctx_t *g, bw_t *r, int nl)
 {
 	int ld = rr(4, 5), cd = rr(4, 5); /* weights <= 48: bi sums stay inside int16 (Appendix A #1) */
+	const int q = g->p->quirks;
+	if (q) { /* denominator 7: absent weights default to 128, stored as int8 -128 (A#16) */
+		ld = pct(50) ? 7 : 6;
+		cd = pct(50) ? 7 : 6;
+	}
 	bw_ue(r, (uint32_t)ld);
 	bw_ue(r, (uint32_t)cd);
 	for (int lx = 0; lx < nl; ++lx) {
 		int n = lx ? g->l1n : g->l0n;
 		for (int i = 0; i < n; ++i) {
-			int f = pct(70);
+			int f = pct(q ? 60 : 70);
 			bw_bit(r, f);
 			if (f) {
-				bw_se(r, rr((1 << ld) / 2, (1 << ld) * 3 / 2));
-				bw_se(r, rr(-20, 20));
+				/* quirks: weights near 127 overflow the SSE2 int16 sum of a bright bi-pair (A#1) */
+				bw_se(r, q ? rr(96, 127) : rr((1 << ld) / 2, (1 << ld) * 3 / 2));
+				bw_se(r, q ? rr(0, 40) : rr(-20, 20));
 			}
 			f = pct(50);
 			bw_bit(r, f);
 			if (f)
 				for (int c = 0; c < 2; ++c) {
-					bw_se(r, rr((1 << cd) / 2, (1 << cd) * 3 / 2));
-					bw_se(r, rr(-12, 12));
+					bw_se(r, q ? rr(96, 127) : rr((1 << cd) / 2, (1 << cd) * 3 / 2));
+					bw_se(r, q ? rr(0, 20) : rr(-12, 12));
 				}
 		}
 	}

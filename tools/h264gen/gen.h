@@ -40,6 +40,9 @@ typedef struct {
 	int cip;                /* constrained_intra_pred_flag (reference quirk A#8 reproduced by the decoder) */
 	int idc2;               /* allow disable_deblocking_filter_idc 2 (reference quirk A#6) */
 	int scaling;            /* SPS seq_scaling_matrix_present_flag with random lists (parsed, ignored: A#4) */
+	int quirks;             /* reach the reference quirks the kernels reproduce: explicit weights up to 127
+	                           (SSE2 int16 saturation, A#1), log2 denominator 7 with default weights (the
+	                           int8 store of 128, A#16), DC-only 4x4 blocks with |adj| 200..255 (SWAR, A#17) */
 	uint64_t seed;
 } params_t;
 

@@ -1,6 +1,6 @@
 /* h264gen command line: deterministic synthetic H.264 streams for tests and bench.py.
  *
- *   h264gen --preset c2|c3|c5|cov_cabac|cov_cavlc|cov_wp|cov_slices|cov_tools|cov_tools_cavlc
+ *   h264gen --preset c2|c3|c5|cov_cabac|cov_cavlc|cov_wp|cov_wp_quirks|cov_slices|cov_tools|cov_tools_cavlc
  *           [--seed N] [--frames N]
  *           [--size WxH] [--set key=value ...] -o out.264
  *
@@ -55,6 +55,13 @@ static void preset(params_t *p, const char *name)
 		p->gop = 0;
 		return;
 	}
+	if (!strcmp(name, "cov_wp_quirks")) {
+		/* explicit weighting at the edges the reference's SSE2 path handles its own way (int16
+		 * saturation, int8 weight 128) and DC-only blocks at large adjustments: oracle_quirk_hits > 0 */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 16; p->wp_p = 1; p->wp_b = 1;
+		p->gop = 8; p->t8x8 = 1; p->quirks = 1; p->qp_min = 24; p->qp_max = 36;
+		return;
+	}
 	if (!strcmp(name, "cov_tools")) {
 		/* the reference paths no other preset reaches: plane prediction (luma 16x16 and chroma),
 		 * constrained intra prediction, deblocking idc 2 across 3 slices, SPS scaling lists */
@@ -90,7 +97,7 @@ static void set_kv(params_t *p, const char *kv)
 	F(width) F(height) F(crop_bottom) F(frames) F(cabac) F(bframes) F(t8x8) F(gop) F(idr_period) F(slices)
 	F(profile) F(level) F(wp_p) F(wp_b) F(direct) F(qp_min) F(qp_max) F(deblock) F(pcm_permille) F(mv_px)
 	F(num_ref_frames) F(l0_active) F(l1_active) F(p_skip_pct) F(p_intra_pct) F(i4_pct) F(i8_pct)
-	F(sub8x8_pct) F(coef_pct) F(planar) F(cip) F(idc2) F(scaling)
+	F(sub8x8_pct) F(coef_pct) F(planar) F(cip) F(idc2) F(scaling) F(quirks)
 #undef F
 	fprintf(stderr, "h264gen: unknown key %s\n", key);
 	exit(2);

@@ -31,6 +31,9 @@ STREAMS = [
     ("cov_tools_s1", "cov_tools", 1, 16),
     ("cov_tools_s2", "cov_tools", 2, 16),
     ("cov_tools_cavlc_s1", "cov_tools_cavlc", 1, 16),
+    # explicit weights at the SSE2 int16 saturation and the int8 weight 128 (A#1, A#16), SWAR DC-only
+    # adds of 200..255 (A#17): tests/test_quirks.py asserts the oracle's hit counters
+    ("cov_wp_quirks_s1", "cov_wp_quirks", 1, 16),
 ] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)] \
   + [(f"c5_4k_s{s}", "c5", s, 16) for s in range(2, 9)]  # C4 / C5: one stream per GPU, seed 1 + rank
 

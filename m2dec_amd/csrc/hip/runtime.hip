@@ -19,7 +19,12 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <algorithm>
+#include <atomic>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <vector>
 #include "recon_internal.h"
 #include "m2dec_amd.h"
@@ -28,6 +33,13 @@
 
 namespace {
 
+static double wall_s()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 static int dbg_knob(const char *name)
 {
 	const char *v = getenv(name);
@@ -35,6 +47,132 @@ static int dbg_knob(const char *name)
 }
 
 const int NSTREAMS = 3; /* pictures in flight: all of their k_inter + k_rows workgroups fit on the device */
+
+/* Forward-progress invariant of the decode path.  A picture's workgroups spin on its references' row
+ * flags, written by EARLIER launches that may sit on other HIP streams (hardware queues), and the
+ * hardware may dispatch a later launch first.  If the spinning workgroups of later launches could fill
+ * every workgroup slot of the device, an earlier launch would never get its workgroups dispatched.
+ * So every decode-path launch in this process (all decoder contexts, all their streams) first
+ * reserves its workgroup count from a device-wide budget equal to the resident-workgroup capacity of
+ * k_picture (occupancy x CUs); the reservation is returned when the launch completes.  All reserved
+ * launches fit on the device together, and every wait points at an earlier launch, which holds a
+ * reservation too — so the oldest unfinished launch always runs.  (A replay k_batch launch is one
+ * kernel whose waits point at lower block indices: in-order dispatch inside a launch.) */
+struct SlotBudget {
+	std::mutex mu;
+	int cap = 0, used = 0;
+	std::deque<std::pair<hipEvent_t, int>> pend; /* completion event of a launch, its workgroups */
+	std::vector<hipEvent_t> pool;
+
+	/* returns the workgroups reserved (the launch's, or the whole capacity for a bigger launch) */
+	int reserve(int blocks)
+	{
+		std::unique_lock<std::mutex> lk(mu);
+		const int want = std::min(blocks, cap);
+		for (;;) {
+			for (size_t i = 0; i < pend.size();) {
+				if (hipEventQuery(pend[i].first) == hipSuccess) {
+					used -= pend[i].second;
+					pool.push_back(pend[i].first);
+					pend.erase(pend.begin() + (long)i);
+				} else {
+					++i;
+				}
+			}
+			if (used + want <= cap) break;
+			if (pend.empty()) { /* in flight but not registered yet (another thread between launch and
+			                     * register): let it finish registering */
+				lk.unlock();
+				std::this_thread::yield();
+				lk.lock();
+				continue;
+			}
+			hipEvent_t e = pend.front().first;
+			lk.unlock();
+			(void)hipEventSynchronize(e);
+			lk.lock();
+		}
+		used += want;
+		return want;
+	}
+
+	hipEvent_t event()
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		hipEvent_t e = nullptr;
+		if (!pool.empty()) {
+			e = pool.back();
+			pool.pop_back();
+		} else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+			e = nullptr;
+		}
+		return e;
+	}
+
+	/* the launch's completion event is recorded: it returns `n` workgroups once it fires */
+	void registered(hipEvent_t e, int n)
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		pend.emplace_back(e, n);
+	}
+
+	void cancel(int n)
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		used -= n;
+	}
+};
+
+SlotBudget g_budget[16]; /* per device ordinal */
+
+/* Streams and events outlive a decoder context too (creating a stream and the ~160 events of a back
+ * end costs ~10 ms): released ones are kept per device and handed to the next context. */
+struct HipPool {
+	std::mutex mu;
+	std::vector<hipStream_t> streams[16];
+	std::vector<hipEvent_t> events[16][2]; /* [dev][timing] */
+
+	hipError_t stream(int dev, hipStream_t *s)
+	{
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if (!streams[dev & 15].empty()) {
+				*s = streams[dev & 15].back();
+				streams[dev & 15].pop_back();
+				return hipSuccess;
+			}
+		}
+		return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+	}
+	void put_stream(int dev, hipStream_t s)
+	{
+		if (!s) return;
+		(void)hipStreamSynchronize(s);
+		std::lock_guard<std::mutex> lk(mu);
+		streams[dev & 15].push_back(s);
+	}
+	hipError_t event(int dev, bool timing, hipEvent_t *e)
+	{
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			auto &v = events[dev & 15][timing];
+			if (!v.empty()) {
+				*e = v.back();
+				v.pop_back();
+				return hipSuccess;
+			}
+		}
+		return timing ? hipEventCreate(e) : hipEventCreateWithFlags(e, hipEventDisableTiming);
+	}
+	void put_event(int dev, bool timing, hipEvent_t e)
+	{
+		if (!e) return;
+		(void)hipEventSynchronize(e);
+		std::lock_guard<std::mutex> lk(mu);
+		events[dev & 15][timing].push_back(e);
+	}
+};
+HipPool g_pool;
 const int NEVENTS = 4096; /* recycled sync events: far more than the pictures a dependency can span */
 
 struct RecPtrs {
@@ -80,9 +218,8 @@ struct Sched {
 		dev = device;
 		memset(&tm, 0, sizeof(tm));
 		CHECK(hipSetDevice(dev));
-		for (auto &s : st) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-		for (auto &e : ev) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-		CHECK(hipMalloc(&err, 16));
+		for (auto &s : st) CHECK(g_pool.stream(dev, &s));
+		CHECK(hipMalloc(&err, 16)); /* (the sync events are created on first use: next_event) */
 		CHECK(hipMemset(err, 0, 16));
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		int cus = 0;
@@ -144,7 +281,19 @@ struct Sched {
 		size_t lds = m2r_deblock_lds_bytes(W, Wmb);
 		if (lds > 65536 && lds > lds_set) {
 			CHECK(hipFuncSetAttribute((const void *)k_batch, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+			CHECK(hipFuncSetAttribute((const void *)k_picture, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 			lds_set = lds;
+		}
+		{
+			/* resident-workgroup capacity of k_picture at this picture size: the decode path's budget */
+			int per_cu = 0, cus = 0;
+			CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_picture, 256, lds));
+			CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+			SlotBudget &bg = g_budget[dev & 15];
+			std::lock_guard<std::mutex> lk(bg.mu);
+			const int cap = std::max(1, per_cu * cus);
+			if (!bg.cap || cap < bg.cap) bg.cap = cap; /* contexts of several picture sizes: the smallest */
+			if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "k_picture: %d workgroups resident (%d per CU)\n", bg.cap, per_cu);
 		}
 		return 0;
 	}
@@ -153,6 +302,7 @@ struct Sched {
 
 	hipEvent_t next_event()
 	{
+		if (!ev[ev_next] && g_pool.event(dev, false, &ev[ev_next]) != hipSuccess) return nullptr;
 		hipEvent_t e = ev[ev_next];
 		ev_next = (ev_next + 1) % NEVENTS;
 		return e;
@@ -211,9 +361,22 @@ struct Sched {
 		/* the arguments go to device memory (pageable source: staged by the copy call) so that the kernel
 		 * reads them through a pointer, as in batch launches */
 		CHECK(hipMemcpyAsync(pargs + k, &a, sizeof(a), hipMemcpyHostToDevice, s));
-		hipLaunchKernelGGL(k_picture, dim3(picture_blocks(inter_grid, Hmb)), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
-		                   (const PictureArgs *)(pargs + k));
-		CHECK(hipGetLastError());
+		{
+			/* the device-wide workgroup budget (SlotBudget): reserve, launch, register the release */
+			SlotBudget &bg = g_budget[dev & 15];
+			const int nb = picture_blocks(inter_grid, Hmb);
+			hipEvent_t done = bg.event();
+			if (!done) return -1;
+			const int held = bg.reserve(nb);
+			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
+			                   (const PictureArgs *)(pargs + k));
+			if (hipGetLastError() != hipSuccess || hipEventRecord(done, s) != hipSuccess) {
+				bg.cancel(held);
+				fprintf(stderr, "m2dec_amd: k_picture launch failed\n");
+				return -1;
+			}
+			bg.registered(done, held);
+		}
 		tm.inter_launches += j.n_inter ? 1 : 0;
 		tm.intra_launches += j.n_intra ? 1 : 0;
 		tm.deblock_launches++;
@@ -412,16 +575,20 @@ struct Sched {
 		batch_free();
 		for (auto &s : st)
 			if (s) (void)hipStreamSynchronize(s);
-		for (auto &e : ev)
-			if (e) (void)hipEventDestroy(e);
+		for (auto &e : ev) {
+			g_pool.put_event(dev, false, e);
+			e = nullptr;
+		}
 		if (frames) (void)hipFree(frames);
 		if (prog) (void)hipFree(prog);
 		if (pargs) (void)hipFree(pargs);
 		if (hand) (void)hipFree(hand);
 		if (err) (void)hipFree(err);
 		if (rowflag) (void)hipFree(rowflag);
-		for (auto &s : st)
-			if (s) (void)hipStreamDestroy(s);
+		for (auto &s : st) {
+			g_pool.put_stream(dev, s);
+			s = nullptr;
+		}
 	}
 };
 
@@ -458,6 +625,52 @@ struct Arena {
 	bool pending = false;
 };
 
+/* Pinned record arenas (+ their device twins) outlive a decoder context: a process decoding stream
+ * after stream (a transcoding service, bench.py's steps) reuses them instead of pinning 8 MB per
+ * arena per stream (~2 ms each on the MI355X host). */
+struct ArenaPool {
+	struct Block {
+		int dev;
+		uint8_t *host, *dev_ptr;
+		size_t size;
+	};
+	std::mutex mu;
+	std::vector<Block> free_blocks;
+
+	bool take(int dev, size_t need, Arena &a)
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		for (size_t i = 0; i < free_blocks.size(); ++i)
+			if (free_blocks[i].dev == dev && free_blocks[i].size >= need) {
+				a.host = free_blocks[i].host;
+				a.dev = free_blocks[i].dev_ptr;
+				a.size = free_blocks[i].size;
+				free_blocks.erase(free_blocks.begin() + (long)i);
+				return true;
+			}
+		return false;
+	}
+
+	void give(int dev, Arena &a)
+	{
+		if (!a.host) return;
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if (free_blocks.size() < 32) {
+				free_blocks.push_back({dev, a.host, a.dev, a.size});
+				a.host = a.dev = nullptr;
+				a.size = 0;
+				return;
+			}
+		}
+		(void)hipHostFree(a.host);
+		(void)hipFree(a.dev);
+		a.host = a.dev = nullptr;
+		a.size = 0;
+	}
+};
+ArenaPool g_arenas;
+
 struct TimingSlot {
 	hipEvent_t e[6]; /* start, uploaded, after inter, after intra, after deblock, after D2H */
 	bool pending = false;
@@ -469,6 +682,11 @@ struct HipBackend {
 	void *reg[64][2];
 	hipEvent_t slot_ev[64];
 	bool slot_pending[64];
+	/* the caller's frames are page-locked (hipHostRegister, ~0.15 ms per 1080p frame) on a helper
+	 * thread while the first pictures are parsed; a picture's download waits for its frame's turn */
+	std::thread reg_thread;
+	std::atomic<int> reg_done{0}; /* frames [0, reg_done) registered */
+	int reg_n = 0;
 	Arena ar[kArenas];
 	int next = 0;
 	TimingSlot tr[16];
@@ -493,6 +711,9 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 
 void unregister_frames(HipBackend *b)
 {
+	if (b->reg_thread.joinable()) b->reg_thread.join();
+	b->reg_done = 0;
+	b->reg_n = 0;
 	for (int i = 0; i < 64; ++i)
 		for (int k = 0; k < 2; ++k)
 			if (b->reg[i][k]) {
@@ -504,22 +725,32 @@ void unregister_frames(HipBackend *b)
 int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
 {
 	HipBackend *b = (HipBackend *)self;
+	const double t0 = wall_s();
 	if (b->sc.sync_all() < 0) return -1;
 	unregister_frames(b);
 	if (n > 64) n = 64;
 	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
 	if (b->sc.configure(width, height, n) < 0) return -1;
+	const double t1 = wall_s();
 	size_t ls = (size_t)width * height, cs = ls / 2;
-	for (int i = 0; i < n; ++i) {
-		b->slot_pending[i] = false;
-		if (b->frames[i].chroma == b->frames[i].luma + ls) {
-			if (hipHostRegister(b->frames[i].luma, ls + cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-		} else {
-			if (hipHostRegister(b->frames[i].luma, ls, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-			if (hipHostRegister(b->frames[i].chroma, cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][1] = b->frames[i].chroma;
+	for (int i = 0; i < n; ++i) b->slot_pending[i] = false;
+	b->reg_n = n;
+	const int dev = b->sc.dev;
+	b->reg_thread = std::thread([b, n, ls, cs, dev]() {
+		(void)hipSetDevice(dev);
+		for (int i = 0; i < n; ++i) {
+			if (b->frames[i].chroma == b->frames[i].luma + ls) {
+				if (hipHostRegister(b->frames[i].luma, ls + cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
+			} else {
+				if (hipHostRegister(b->frames[i].luma, ls, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
+				if (hipHostRegister(b->frames[i].chroma, cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][1] = b->frames[i].chroma;
+			}
+			b->reg_done.store(i + 1, std::memory_order_release);
 		}
-		(void)hipGetLastError();
-	}
+	});
+	if (dbg_knob("M2DEC_AMD_ASYNC_STATS"))
+		fprintf(stderr, "be_set_frames: configure %.2f ms, register %d frames %.2f ms\n", 1e3 * (t1 - t0), n,
+		        1e3 * (wall_s() - t1));
 	return 0;
 }
 
@@ -534,15 +765,22 @@ int arena_alloc(Arena &a, int wm, int hm)
 	a.off_inter = off; off = al(off + n * sizeof(m2r_inter_t));
 	a.off_coef = off; off = al(off + n * 416 * sizeof(int16_t));
 	if (a.size < off) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
-		a.host = nullptr;
-		a.dev = nullptr;
-		CHECK(hipHostMalloc(&a.host, off, hipHostMallocDefault));
-		CHECK(hipMalloc(&a.dev, off));
-		a.size = off;
+		int dev = 0;
+		CHECK(hipGetDevice(&dev));
+		g_arenas.give(dev, a);
+		if (!g_arenas.take(dev, off, a)) {
+			const double t0 = wall_s();
+			CHECK(hipHostMalloc(&a.host, off, hipHostMallocDefault));
+			CHECK(hipMalloc(&a.dev, off));
+			if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "arena_alloc: %zu bytes %.2f ms\n", off, 1e3 * (wall_s() - t0));
+			a.size = off;
+		}
 	}
-	if (!a.consumed) CHECK(hipEventCreateWithFlags(&a.consumed, hipEventDisableTiming));
+	if (!a.consumed) {
+		int dev = 0;
+		CHECK(hipGetDevice(&dev));
+		CHECK(g_pool.event(dev, false, &a.consumed));
+	}
 	m2r_picture_t &p = a.pic;
 	memset(&p, 0, sizeof(p));
 	p.width_mbs = wm;
@@ -619,6 +857,7 @@ int be_submit(void *self, m2r_picture_t *pic)
 	a->pending = true;
 	const m2d_frame_t &f = b->frames[pic->slot];
 	uint8_t *cur = sc.frames + (size_t)pic->slot * sc.fsz;
+	while (b->reg_done.load(std::memory_order_acquire) <= pic->slot && pic->slot < b->reg_n) std::this_thread::yield();
 	size_t ls = (size_t)sc.W * sc.H;
 	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
 	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
@@ -654,13 +893,12 @@ void be_destroy(void *self)
 	b->sc.sync_all();
 	unregister_frames(b);
 	for (auto &a : b->ar) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
-		if (a.consumed) (void)hipEventDestroy(a.consumed);
+		g_arenas.give(b->sc.dev, a); /* (every kernel reading it finished: sync_all above) */
+		g_pool.put_event(b->sc.dev, false, a.consumed);
 	}
-	for (int i = 0; i < 64; ++i) (void)hipEventDestroy(b->slot_ev[i]);
+	for (int i = 0; i < 64; ++i) g_pool.put_event(b->sc.dev, false, b->slot_ev[i]);
 	for (auto &t : b->tr)
-		for (auto &e : t.e) (void)hipEventDestroy(e);
+		for (auto &e : t.e) g_pool.put_event(b->sc.dev, true, e);
 	b->sc.destroy();
 	delete b;
 }
@@ -677,6 +915,7 @@ extern "C" int m2dec_amd_hip_available(void)
 extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 {
 	if (!out || !m2dec_amd_hip_available()) return -1;
+	const double t0 = wall_s();
 	HipBackend *b = new HipBackend();
 	memset(b->reg, 0, sizeof(b->reg));
 	memset(b->slot_pending, 0, sizeof(b->slot_pending));
@@ -684,9 +923,9 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 		delete b;
 		return -1;
 	}
-	for (int i = 0; i < 64; ++i) CHECK(hipEventCreateWithFlags(&b->slot_ev[i], hipEventDisableTiming));
+	for (int i = 0; i < 64; ++i) CHECK(g_pool.event(device, false, &b->slot_ev[i]));
 	for (auto &t : b->tr)
-		for (auto &e : t.e) CHECK(hipEventCreate(&e));
+		for (auto &e : t.e) CHECK(g_pool.event(device, true, &e));
 	const char *tm = getenv("M2DEC_AMD_TIMING");
 	b->timing = tm ? atoi(tm) != 0 : true;
 	out->self = b;
@@ -695,6 +934,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->submit = be_submit;
 	out->sync_frame = be_sync;
 	out->destroy = be_destroy;
+	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
 }
 

@@ -109,12 +109,24 @@ typedef struct m2r_picture {
 	m2r_inter_t *inter;    /* [cap_inter] */
 	int16_t *coef;         /* [cap_coef] */
 	int32_t cap_slices, cap_inter, cap_coef;
-	int32_t pad;
+	int32_t flags;         /* M2R_PIC_* */
 } m2r_picture_t;
+
+/* m2r_picture_t.flags: `slot` and every m2r_inter_t.slot are the back end's picture buffers (virtual
+ * frame ids 0..63 of the parse-ahead pipeline), not caller frame slots; the picture reaches a caller
+ * frame only through bind().  Set only for back ends that provide bind. */
+#define M2R_PIC_VIRTUAL 1
 
 /* A reconstruction back end.  The parser acquires an arena, fills it, and submits it; frames are
  * caller-owned NV12 buffers (set_frames), synchronised on demand (sync_frame) before the caller
- * reads them through peek/get_decoded_frame. */
+ * reads them through peek/get_decoded_frame.
+ *
+ * bind (optional, NULL if absent): decode ahead of the caller.  Pictures are submitted with
+ * M2R_PIC_VIRTUAL as soon as they are parsed, into the back end's own buffers named by virtual
+ * frame ids, before the API context has given them a caller frame; bind(vid, slot) later says that
+ * buffer `vid` holds the picture of caller frame `slot` (copied out by the time sync_frame(slot)
+ * returns).  The caller guarantees: a virtual id is bound before any later picture that writes
+ * the same id is submitted, and a picture is submitted before it is bound. */
 typedef struct m2r_backend {
 	void *self;
 	int (*set_frames)(void *self, int n, const m2d_frame_t *frames, int width, int height);
@@ -122,6 +134,7 @@ typedef struct m2r_backend {
 	int (*submit)(void *self, m2r_picture_t *pic);
 	int (*sync_frame)(void *self, int slot);
 	void (*destroy)(void *self);
+	int (*bind)(void *self, int vid, int slot);
 } m2r_backend_t;
 
 #ifdef __cplusplus

@@ -24,7 +24,7 @@ typedef struct {
 	int frames_out;
 	int pictures;
 	int last_error;
-	int pad;
+	int ahead; /* pictures submitted before the API context reached them (decode ahead, m2d_recon.h bind) */
 	/* CLOCK_MONOTONIC seconds: the first decode_picture call, and the last frame delivered to the
 	 * writer (on_frame returned; for the MD5 drivers: its MD5 line written) — the fps interval of
 	 * SURVEY.md §8d.  setup_s: time inside the first set_frames (back-end creation, frame pinning). */
@@ -82,6 +82,9 @@ int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t
 
 /* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
+/* MD5 lines of n <= 16 frames at once (16-lane AVX-512 multi-buffer MD5 when the CPU has it and the
+ * frames share one geometry without horizontal crop; else one by one); 0, or -1 for a bad n */
+int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35]);
 
 /* Throughput drivers over the same decode loop as m2dec_amd_decode_stream (h264dec -O): the HIP back
  * end on `device`, DPB size `dpb` (h264dec -d; -1 auto), one MD5 line (35 bytes) per output frame into

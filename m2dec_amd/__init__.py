@@ -39,15 +39,16 @@ class Info(ctypes.Structure):
 
 
 class Backend(ctypes.Structure):
-    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy."""
+    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind."""
     _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("acquire", ctypes.c_void_p),
-                ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p)]
+                ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p),
+                ("bind", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
     """m2dec_amd_stats_t (include/m2dec_amd.h)."""
     _fields_ = [("frames_out", ctypes.c_int), ("pictures", ctypes.c_int), ("last_error", ctypes.c_int),
-                ("pad", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
+                ("ahead", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
                 ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64)]
 
@@ -101,6 +102,8 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
         L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
         L.m2dec_amd_frame_md5.restype = None
+        L.m2dec_amd_frames_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_int, ctypes.c_char_p]
+        L.m2dec_amd_frames_md5.restype = ctypes.c_int
         L.m2dec_amd_decode_stream_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(Stats)]
         L.m2dec_amd_decode_stream_md5.restype = ctypes.c_int
@@ -209,12 +212,13 @@ def frame_nv12(f: Frame) -> bytes:
 
 def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 0,
                   on_frame: Optional[Callable[[Frame], None]] = None, md5: bool = True,
-                  parse_threads: int = -1) -> List[str]:
+                  parse_threads: int = -1, stats: Optional[Stats] = None) -> List[str]:
     """Decode an Annex-B H.264 stream exactly like ``h264dec -O`` and return the per-frame MD5 list.
 
     ``backend`` None -> the HIP back end on ``device`` (raises if absent).  Any other m2r_backend_t
     (e.g. the oracle's, in tests) is borrowed.  ``parse_threads``: parse-ahead workers (-1: the
-    default — 8 with the HIP back end, none with a borrowed one).
+    default — 8 with the HIP back end, none with a borrowed one).  ``stats`` (a Stats) receives the
+    decoder's counters.
     """
     L = lib()
     if backend is None and not L.m2dec_amd_hip_available():
@@ -233,7 +237,7 @@ def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 
             errs.append(e)
 
     cb = ON_FRAME(_cb)
-    st = Stats()
+    st = stats if stats is not None else Stats()
     n = L.m2dec_amd_decode_stream3(data, len(data), ctypes.byref(backend) if backend is not None else None, device, -1,
                                    parse_threads, cb, None, ctypes.byref(st))
     if errs:

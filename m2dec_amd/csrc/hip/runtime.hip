@@ -678,6 +678,7 @@ struct TimingSlot {
 
 struct HipBackend {
 	Sched sc;
+	hipStream_t copy = nullptr; /* decode ahead: bind's copies out of the picture buffers */
 	m2d_frame_t frames[64];
 	void *reg[64][2];
 	hipEvent_t slot_ev[64];
@@ -727,10 +728,12 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	HipBackend *b = (HipBackend *)self;
 	const double t0 = wall_s();
 	if (b->sc.sync_all() < 0) return -1;
+	if (b->copy) CHECK(hipStreamSynchronize(b->copy)); /* copies into the frames about to be released */
 	unregister_frames(b);
 	if (n > 64) n = 64;
 	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
-	if (b->sc.configure(width, height, n) < 0) return -1;
+	/* one device picture buffer per virtual id (decode ahead) — a caller slot also names one */
+	if (b->sc.configure(width, height, 64) < 0) return -1;
 	const double t1 = wall_s();
 	size_t ls = (size_t)width * height, cs = ls / 2;
 	for (int i = 0; i < n; ++i) b->slot_pending[i] = false;
@@ -819,7 +822,9 @@ int be_submit(void *self, m2r_picture_t *pic)
 		if (&x.pic == pic) a = &x;
 	if (!a) return -1;
 	const int n = pic->width_mbs * pic->height_mbs;
+	const bool virt = (pic->flags & M2R_PIC_VIRTUAL) != 0;
 	if (pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots) return -1;
+	if (!virt && pic->slot >= b->reg_n) return -1;
 	if (pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) return -1;
 	CHECK(hipSetDevice(sc.dev));
 	PicJob j;
@@ -855,14 +860,17 @@ int be_submit(void *self, m2r_picture_t *pic)
 	if (sc.launch(k, j, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
 	CHECK(hipEventRecord(a->consumed, s));
 	a->pending = true;
-	const m2d_frame_t &f = b->frames[pic->slot];
-	uint8_t *cur = sc.frames + (size_t)pic->slot * sc.fsz;
-	while (b->reg_done.load(std::memory_order_acquire) <= pic->slot && pic->slot < b->reg_n) std::this_thread::yield();
-	size_t ls = (size_t)sc.W * sc.H;
-	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
-	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
-	CHECK(hipEventRecord(b->slot_ev[pic->slot], s));
-	b->slot_pending[pic->slot] = true;
+	const size_t ls = (size_t)sc.W * sc.H;
+	if (!virt) {
+		/* the caller's slot is the picture buffer: copy out right behind the kernel */
+		const m2d_frame_t &f = b->frames[pic->slot];
+		uint8_t *cur = sc.frames + (size_t)pic->slot * sc.fsz;
+		while (b->reg_done.load(std::memory_order_acquire) <= pic->slot) std::this_thread::yield();
+		CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
+		CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
+		CHECK(hipEventRecord(b->slot_ev[pic->slot], s));
+		b->slot_pending[pic->slot] = true;
+	}
 	if (ts) {
 		CHECK(hipEventRecord(ts->e[5], s));
 		ts->pending = true;
@@ -872,6 +880,32 @@ int be_submit(void *self, m2r_picture_t *pic)
 	sc.tm.record_bytes += (int64_t)rec_bytes;
 	sc.tm.ref_bytes += ref_bytes_of(pic->inter, pic->n_inter);
 	sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
+	return 0;
+}
+
+/* decode ahead: picture buffer `vid` (its last writer is submitted) is caller frame `slot`.  The copy
+ * runs on its own stream behind the writer's completion event; it is a reader of the buffer, so the
+ * next picture writing `vid` waits for it (Sched::begin) */
+int be_bind(void *self, int vid, int slot)
+{
+	HipBackend *b = (HipBackend *)self;
+	Sched &sc = b->sc;
+	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->reg_n || !sc.slot_write[vid]) return -1;
+	CHECK(hipSetDevice(sc.dev));
+	if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
+	CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[vid], 0));
+	const m2d_frame_t &f = b->frames[slot];
+	const uint8_t *cur = sc.frames + (size_t)vid * sc.fsz;
+	const size_t ls = (size_t)sc.W * sc.H;
+	while (b->reg_done.load(std::memory_order_acquire) <= slot) std::this_thread::yield();
+	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, b->copy));
+	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, b->copy));
+	CHECK(hipEventRecord(b->slot_ev[slot], b->copy));
+	b->slot_pending[slot] = true;
+	hipEvent_t r = sc.next_event();
+	if (!r) return -1;
+	CHECK(hipEventRecord(r, b->copy));
+	sc.readers[vid].push_back(r);
 	return 0;
 }
 
@@ -891,6 +925,8 @@ void be_destroy(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
 	b->sc.sync_all();
+	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: no copy into a caller frame is left) */
+	b->copy = nullptr;
 	unregister_frames(b);
 	for (auto &a : b->ar) {
 		g_arenas.give(b->sc.dev, a); /* (every kernel reading it finished: sync_all above) */
@@ -934,6 +970,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->submit = be_submit;
 	out->sync_frame = be_sync;
 	out->destroy = be_destroy;
+	out->bind = be_bind;
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
 }

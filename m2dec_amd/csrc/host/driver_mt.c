@@ -20,16 +20,59 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 24
+#define MD5_RING 48
+#define MD5_BATCH 16       /* frames one thread hashes together (m2dec_amd_frames_md5 lanes) */
 #define MD5_THREADS_MAX 16
-#define MD5_THREADS 8 /* one stream: MD5 (~4 ms per 1080p frame per core) must keep up with the decoder;
-                         M2DEC_AMD_MD5_THREADS overrides */
+#define MD5_THREADS 3      /* one stream: a 16-frame batch of 1080p takes one core ~5 ms, so a few threads
+                              keep up with the decoder; M2DEC_AMD_MD5_THREADS overrides */
+
+/* Ring memory outlives a call (a service decoding stream after stream, bench.py's steps): touching
+ * 150 MB of fresh pages per stream costs more than the hashing.  One contiguous block per ring, so
+ * the multi-buffer MD5 addresses every slot with 32-bit offsets. */
+static pthread_mutex_t ring_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+	uint8_t *mem;
+	size_t size;
+} ring_cache[4];
+
+static uint8_t *ring_take(size_t need, size_t *got)
+{
+	uint8_t *m = NULL;
+	pthread_mutex_lock(&ring_mu);
+	for (int i = 0; i < 4 && !m; ++i)
+		if (ring_cache[i].mem && ring_cache[i].size >= need) {
+			m = ring_cache[i].mem;
+			*got = ring_cache[i].size;
+			ring_cache[i].mem = NULL;
+		}
+	pthread_mutex_unlock(&ring_mu);
+	if (!m) {
+		m = (uint8_t *)malloc(need);
+		*got = m ? need : 0;
+	}
+	return m;
+}
+
+static void ring_give(uint8_t *m, size_t size)
+{
+	if (!m) return;
+	pthread_mutex_lock(&ring_mu);
+	for (int i = 0; i < 4; ++i)
+		if (!ring_cache[i].mem) {
+			ring_cache[i].mem = m;
+			ring_cache[i].size = size;
+			m = NULL;
+			break;
+		}
+	pthread_mutex_unlock(&ring_mu);
+	free(m);
+}
 
 typedef struct {
 	pthread_mutex_t mu;
 	pthread_cond_t cv_job, cv_free;
-	uint8_t *buf[MD5_RING];
-	size_t cap;
+	uint8_t *mem;            /* MD5_RING slots of `cap` bytes (ring_take) */
+	size_t mem_size, cap;
 	m2d_frame_t frm[MD5_RING];
 	int idx[MD5_RING];       /* output frame number of the job in slot k */
 	int state[MD5_RING];     /* 0 free, 1 queued, 2 being hashed */
@@ -51,6 +94,7 @@ static double now_s(void)
 	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+/* a free thread takes every queued frame (up to MD5_BATCH) and hashes them side by side */
 static void *md5_worker(void *arg)
 {
 	md5_pipe_t *p = (md5_pipe_t *)arg;
@@ -58,19 +102,25 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
-		const int k = p->next % MD5_RING;
-		p->next++;
-		p->state[k] = 2;
-		m2d_frame_t f = p->frm[k];
-		const int i = p->idx[k];
+		m2d_frame_t f[MD5_BATCH];
+		int ks[MD5_BATCH], ix[MD5_BATCH], n = 0;
+		while (n < MD5_BATCH && p->next < p->head) {
+			const int k = p->next % MD5_RING;
+			p->next++;
+			p->state[k] = 2;
+			f[n] = p->frm[k];
+			ix[n] = p->idx[k];
+			ks[n++] = k;
+		}
 		pthread_mutex_unlock(&p->mu);
-		char line[35];
-		m2dec_amd_frame_md5(&f, line);
-		if (i < p->max) memcpy(p->md5s + (size_t)i * 35, line, 35);
+		char lines[MD5_BATCH][35];
+		m2dec_amd_frames_md5(f, n, lines);
+		for (int j = 0; j < n; ++j)
+			if (ix[j] < p->max) memcpy(p->md5s + (size_t)ix[j] * 35, lines[j], 35);
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
 		if (t > p->t_done) p->t_done = t;
-		p->state[k] = 0;
+		for (int j = 0; j < n; ++j) p->state[ks[j]] = 0;
 		pthread_cond_broadcast(&p->cv_free);
 	}
 	pthread_mutex_unlock(&p->mu);
@@ -96,26 +146,26 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_unlock(&p->mu);
 	const double t1 = p->stats ? now_s() : 0;
 	if (bytes > p->cap) { /* (re)size the ring while no job holds a buffer; only this thread allocates */
-		for (int j = 0; j < MD5_RING; ++j) {
-			free(p->buf[j]);
-			p->buf[j] = (uint8_t *)malloc(bytes);
-			if (!p->buf[j]) {
-				p->failed = 1;
-				p->cap = 0;
-				return;
-			}
+		const size_t slot = (bytes + 63) & ~(size_t)63;
+		ring_give(p->mem, p->mem_size);
+		p->mem = ring_take(slot * MD5_RING, &p->mem_size);
+		if (!p->mem) {
+			p->failed = 1;
+			p->cap = 0;
+			return;
 		}
-		p->cap = bytes;
+		p->cap = p->mem_size / MD5_RING;
 	}
-	memcpy(p->buf[k], f->luma, luma);
-	memcpy(p->buf[k] + luma, f->chroma, luma / 2);
+	uint8_t *buf = p->mem + (size_t)k * p->cap;
+	memcpy(buf, f->luma, luma);
+	memcpy(buf + luma, f->chroma, luma / 2);
 	if (p->stats) {
 		p->t_wait += t1 - t0;
 		p->t_copy += now_s() - t1;
 	}
 	m2d_frame_t c = *f;
-	c.luma = p->buf[k];
-	c.chroma = p->buf[k] + luma;
+	c.luma = buf;
+	c.chroma = buf + luma;
 	pthread_mutex_lock(&p->mu);
 	p->frm[k] = c;
 	p->idx[k] = p->n++;
@@ -161,7 +211,7 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	pthread_mutex_unlock(&p.mu);
 	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
 	if (p.stats) fprintf(stderr, "md5 ring: caller waits %.3f s, frame copies %.3f s (%d threads)\n", p.t_wait, p.t_copy, nth);
-	for (int j = 0; j < MD5_RING; ++j) free(p.buf[j]);
+	ring_give(p.mem, p.mem_size);
 	if (p.t_done > st.t_end) st.t_end = p.t_done; /* delivered = its MD5 line written */
 	if (stats) *stats = st;
 	pthread_mutex_destroy(&p.mu);
@@ -299,5 +349,6 @@ int m2dec_amd_null_backend_create(m2r_backend_t *out)
 	out->submit = null_submit;
 	out->sync_frame = null_sync;
 	out->destroy = null_destroy;
+	out->bind = NULL;
 	return 0;
 }

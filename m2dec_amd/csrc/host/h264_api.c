@@ -208,6 +208,7 @@ int h264_decode_loop(h264_dec_t *d)
 			if (id < 0) return id;
 			if (!d->in_picture) d->active_sps = id;
 			if (!d->lookahead) d->header_callback(d->header_callback_arg, d->stream->id);
+			else h264_async_la_sps(d); /* pictures after it wait for the API context's callback */
 			break;
 		}
 		case 8: {
@@ -491,6 +492,7 @@ done:
 		stats->frames_out = n;
 		stats->pictures = (int)d->pictures;
 		stats->last_error = err;
+		stats->ahead = (int)d->ahead_submits;
 		stats->t_start = t_start;
 		stats->t_end = v.t_last;
 		stats->setup_s = v.setup_s;

@@ -46,6 +46,15 @@
  *
  * The stream is read ahead of decode_picture by up to `depth` pictures, so stream_pos() points
  * past the picture decode_picture last returned.
+ *
+ * Decode ahead (back ends with bind, m2d_recon.h): a parsed picture is submitted at once, named by
+ * its virtual id (the back end keeps one picture buffer per id), instead of waiting for the API
+ * context to give it a frame slot.  Without it the GPU could never run ahead of the caller's output
+ * calls: a B picture is bumped out right after it is decoded, and sync_frame on it drained the
+ * device before the next picture was even submitted (one picture in flight).  The API context's
+ * close binds the buffer to the slot; a picture waits (is submitted in API order) when the previous
+ * picture of its virtual id is not bound yet, or when an SPS the API context has not run the header
+ * callback for lies before it.
  */
 #include <pthread.h>
 #include <stdio.h>
@@ -76,6 +85,8 @@ typedef struct h264_job {
 	int slot;                 /* frame slot (API context; -1 until A closed the picture) */
 	int poc;                  /* consistency check between the two contexts */
 	int8_t map[64];           /* virtual id -> frame slot, as of the API context's close */
+	long sps_nal;             /* NAL index of the last SPS the lookahead read before this picture */
+	int submitted, bound;     /* records handed to the back end / its buffer bound to `slot` */
 	int col_store;
 	int nonref;               /* no slice has nal_ref_idc: its co-located store is never read ... */
 	h264_colmb_t *priv_col;   /* ... so it writes this private one (no ordering against other jobs) */
@@ -99,7 +110,10 @@ struct h264_async {
 	pthread_t th[16];
 	int nth, quit, depth;
 	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head); job seq s at fifo[s % AS_MAX] */
-	long head, tail;
+	long head, tail;          /* tail: oldest job not retired (submitted, and bound when decoding ahead) */
+	long sub;                 /* next job to submit: [tail, sub) submitted */
+	int ahead;                /* decode ahead: the back end has bind (M2R_PIC_VIRTUAL submissions) */
+	long la_sps_nal;          /* NAL index of the last SPS the lookahead context read (-1: none) */
 	h264_job_t *queue[AS_MAX]; /* dispatched; [qtail, qhead) holds every job not yet taken */
 	long qhead, qtail;
 	h264_job_t *cur;          /* the picture the lookahead context is collecting */
@@ -108,7 +122,7 @@ struct h264_async {
 	long seq;                 /* jobs dispatched by the lookahead context */
 	long a_seq;               /* pictures closed by the API context: jobs [tail, a_seq) may be submitted */
 	long col_last[17];        /* seq of the last dispatched job that reads or writes store i */
-	h264_job_t *col_writer[17]; /* dispatched, unsubmitted job writing store i */
+	long col_writer[17];      /* seq of the last dispatched job writing store i (-1: none) */
 	/* lookahead context and its NAL hand-over queue (ring, [nq_tail, nq_head)) */
 	h264_dec_t *la;
 	int la_done, la_err;
@@ -173,6 +187,8 @@ static void job_clear(h264_job_t *j)
 	j->done = 0;
 	j->err = 0;
 	j->slot = -1;
+	j->submitted = 0;
+	j->bound = 0;
 }
 
 static void job_free(h264_job_t *j)
@@ -348,7 +364,9 @@ int h264_async_start(h264_dec_t *d, int threads)
 		if (e && atoi(e) > 0) as->depth = atoi(e);
 	}
 	if (as->depth > AS_MAX - 4) as->depth = AS_MAX - 4;
-	for (int i = 0; i < 17; ++i) as->col_last[i] = -1;
+	for (int i = 0; i < 17; ++i) as->col_last[i] = as->col_writer[i] = -1;
+	as->la_sps_nal = -1;
+	as->ahead = d->have_backend && d->backend.bind && !getenv("M2DEC_AMD_NO_AHEAD");
 	as->stats = getenv("M2DEC_AMD_ASYNC_STATS") ? atoi(getenv("M2DEC_AMD_ASYNC_STATS")) : 0;
 	as->t0 = now_s();
 	for (int i = 0; i < threads; ++i) {
@@ -417,26 +435,62 @@ static void job_put(struct h264_async *as, h264_job_t *j)
 }
 
 /* ---------------------------------------------------------------- API context: submission */
-/* copy the oldest closed job's records into the back end's arena, frame ids translated to the API
- * context's slots, and submit it (decode order) */
-static int submit_oldest(h264_dec_t *d)
+/* Submission runs on the caller's thread, in decode order ([tail, sub) submitted).  Without bind a
+ * job is submitted once the API context closed it: its virtual ids are translated to the frame slots
+ * of that moment (j->map) and it retires at once.  With bind (decode ahead) a parsed job is submitted
+ * as it is, virtual ids naming the back end's buffers, possibly before the API context reached it;
+ * the API context's close binds its buffer to the frame slot it chose, and the job retires then. */
+
+static int bind_job(h264_dec_t *d, h264_job_t *j)
+{
+	j->bound = 1;
+	return d->backend.bind(d->backend.self, j->vid & 63, j->slot) < 0 ? -1 : 0;
+}
+
+/* recycle submitted jobs from the tail, in order, once the pipeline no longer needs them */
+static void retire(struct h264_async *as)
+{
+	while (as->tail < as->sub) {
+		h264_job_t *j = as->fifo[as->tail % AS_MAX];
+		if (as->ahead && !j->bound) return;
+		pthread_mutex_lock(&as->mu);
+		as->tail++; /* workers scan [tail, head) under the mutex */
+		pthread_mutex_unlock(&as->mu);
+		job_put(as, j);
+	}
+}
+
+/* a parsed job the API context has not closed yet may go to the back end now: no header callback
+ * (set_frames) the API context has not run yet lies before it, and the previous picture in its
+ * virtual buffer was bound already (so the back end orders the overwrite after that copy-out) */
+static int ahead_ok(const struct h264_async *as, const h264_job_t *j)
+{
+	if (j->err || j->sps_nal >= as->nq_tail) return 0;
+	for (long i = as->tail; i < j->seq; ++i) {
+		const h264_job_t *o = as->fifo[i % AS_MAX];
+		if (o->vid == j->vid && !o->bound) return 0;
+	}
+	return 1;
+}
+
+/* copy the next job's records into the back end's arena and submit it (waits for its parse) */
+static int submit_next(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
-	h264_job_t *j = as->fifo[as->tail % AS_MAX];
+	h264_job_t *j = as->fifo[as->sub % AS_MAX];
 	m2r_picture_t *dst;
 	const m2r_picture_t *src = &j->pic;
+	const int virt = as->ahead;
 	int n, err;
 	double t0 = as->stats ? now_s() : 0, t1 = 0;
 	pthread_mutex_lock(&as->mu);
 	while (!j->done) pthread_cond_wait(&as->cv_done, &as->mu);
-	as->tail++; /* workers scan [tail, head) under the mutex */
 	pthread_mutex_unlock(&as->mu);
+	as->sub++;
 	if (as->stats) {
 		t1 = now_s();
 		as->t_done_wait += t1 - t0;
 	}
-	for (int i = 0; i < 17; ++i)
-		if (as->col_writer[i] == j) as->col_writer[i] = NULL;
 	err = j->err;
 	if (!err) {
 		n = src->width_mbs * src->height_mbs;
@@ -444,7 +498,8 @@ static int submit_oldest(h264_dec_t *d)
 		if (!dst || dst->cap_slices < src->n_slices || dst->cap_inter < src->n_inter || dst->cap_coef < src->n_coef) {
 			err = 1;
 		} else {
-			dst->slot = j->slot;
+			dst->slot = virt ? (j->vid & 63) : j->slot;
+			dst->flags = virt ? M2R_PIC_VIRTUAL : 0;
 			dst->n_inter = src->n_inter;
 			dst->n_coef = src->n_coef;
 			dst->n_slices = src->n_slices;
@@ -453,14 +508,18 @@ static int submit_oldest(h264_dec_t *d)
 			memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
 			memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);
 			memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
-			for (int i = 0; i < src->n_inter; ++i) {
-				const m2r_inter_t *si = &src->inter[i];
-				m2r_inter_t *di = &dst->inter[i];
-				memcpy(di->mv, si->mv, sizeof(di->mv));
-				memcpy(di->refidx, si->refidx, sizeof(di->refidx));
-				for (int k = 0; k < 8; ++k) {
-					const int v = (&si->slot[0][0])[k];
-					(&di->slot[0][0])[k] = (int8_t)(v < 0 ? -1 : j->map[v & 63]);
+			if (virt) {
+				memcpy(dst->inter, src->inter, sizeof(m2r_inter_t) * (size_t)src->n_inter);
+			} else {
+				for (int i = 0; i < src->n_inter; ++i) {
+					const m2r_inter_t *si = &src->inter[i];
+					m2r_inter_t *di = &dst->inter[i];
+					memcpy(di->mv, si->mv, sizeof(di->mv));
+					memcpy(di->refidx, si->refidx, sizeof(di->refidx));
+					for (int k = 0; k < 8; ++k) {
+						const int v = (&si->slot[0][0])[k];
+						(&di->slot[0][0])[k] = (int8_t)(v < 0 ? -1 : j->map[v & 63]);
+					}
 				}
 			}
 			memcpy(dst->coef, src->coef, sizeof(int16_t) * (size_t)src->n_coef);
@@ -469,11 +528,15 @@ static int submit_oldest(h264_dec_t *d)
 				as->t_copy += t2 - t1;
 				t1 = t2;
 			}
+			if (virt && j->slot < 0) d->ahead_submits++;
 			err = d->backend.submit(d->backend.self, dst) < 0;
 			if (as->stats) as->t_submit += now_s() - t1;
 		}
 	}
-	job_put(as, j);
+	j->submitted = 1;
+	if (!err && virt && j->slot >= 0) err = bind_job(d, j) < 0;
+	if (err) j->bound = 1; /* nothing to bind: the error is reported now */
+	retire(as);
 	return err ? -1 : 0;
 }
 
@@ -485,23 +548,26 @@ int h264_async_drain(h264_dec_t *d, int slot)
 	if (!as) return 0;
 	for (long i = as->tail; i < as->a_seq; ++i)
 		if (slot < 0 || as->fifo[i % AS_MAX]->slot == slot) upto = i;
-	while (as->tail <= upto)
-		if (submit_oldest(d) < 0) return -1;
+	while (as->sub <= upto)
+		if (submit_next(d) < 0) return -1;
 	return 0;
 }
 
-/* submit closed jobs whose parse already finished, in order, without waiting */
+/* submit, in order and without waiting, parsed jobs that are closed (or may go ahead) */
 static int submit_ready(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
 	for (;;) {
+		h264_job_t *j;
 		int ready;
-		if (as->tail >= as->a_seq) return 0;
+		if (as->sub >= as->head) return 0;
+		j = as->fifo[as->sub % AS_MAX];
 		pthread_mutex_lock(&as->mu);
-		ready = as->fifo[as->tail % AS_MAX]->done;
+		ready = j->done;
 		pthread_mutex_unlock(&as->mu);
 		if (!ready) return 0;
-		if (submit_oldest(d) < 0) return -1;
+		if (as->sub >= as->a_seq && (!as->ahead || !ahead_ok(as, j))) return 0;
+		if (submit_next(d) < 0) return -1;
 	}
 }
 
@@ -519,8 +585,9 @@ static void pump(h264_dec_t *d, int until_nal)
 			break;
 		}
 		/* job slots: submit what the API context closed before dispatching more */
-		while (as->head - as->tail >= AS_MAX - 2 && as->tail < as->a_seq)
-			if (submit_oldest(d) < 0) {
+		retire(as);
+		while (as->head - as->tail >= AS_MAX - 2 && as->sub < as->a_seq)
+			if (submit_next(d) < 0) {
 				as->la_done = as->la_err = 1;
 				break;
 			}
@@ -592,6 +659,12 @@ int h264_async_nal_next(h264_dec_t *d)
 	return 0;
 }
 
+/* lookahead: it read an SPS (the API context runs the header callback there: set_frames) */
+void h264_async_la_sps(h264_dec_t *la)
+{
+	la->as->la_sps_nal = la->as->nq_head;
+}
+
 /* lookahead: wait until every dispatched job has finished (before its co-located stores are
  * reallocated for a new picture size) */
 int h264_async_sps(h264_dec_t *la)
@@ -615,6 +688,7 @@ int h264_async_add_slice(h264_dec_t *la)
 		if (!j || job_arena(j, la->mb_w, la->mb_h) < 0) return -1;
 		j->vid = la->curr_idx;
 		j->slot = -1;
+		j->sps_nal = as->la_sps_nal;
 		j->pic.slot = la->curr_idx;
 		j->col_store = la->curr_col;
 		as->cur = j;
@@ -692,10 +766,10 @@ static int la_close(h264_dec_t *la)
 		if (s->sh.slice_type != 1) continue;
 		const int c = s->refs[1][0].col;
 		if (c < 0 || c >= 17) continue;
-		h264_job_t *wj = as->col_writer[c];
+		const long ws = as->col_writer[c];
 		int seen = 0;
-		for (int i = 0; i < j->ndeps; ++i) seen |= wj && (j->deps[i] == wj->seq);
-		if (wj && !seen && j->ndeps < 8) j->deps[j->ndeps++] = wj->seq;
+		for (int i = 0; i < j->ndeps; ++i) seen |= (j->deps[i] == ws);
+		if (ws >= 0 && !seen && j->ndeps < 8) j->deps[j->ndeps++] = ws; /* (finished or retired: no wait) */
 		if (as->col_last[c] < j->seq) as->col_last[c] = j->seq;
 	}
 	/* the store this picture writes: if an earlier job that reads or writes its buffer is still
@@ -732,7 +806,7 @@ static int la_close(h264_dec_t *la)
 			if (as->stats) as->t_col_wait += now_s() - tw;
 		}
 		as->col_last[c] = j->seq;
-		as->col_writer[c] = j;
+		as->col_writer[c] = j->seq;
 	}
 	/* marking, store swap (headers only) */
 	la->pic = NULL;
@@ -768,6 +842,8 @@ static int api_close(h264_dec_t *d)
 	memcpy(j->map, as->vmap, sizeof(j->map));
 	j->slot = d->curr_idx;
 	as->a_seq++;
+	if (j->submitted && !j->bound && bind_job(d, j) < 0) return -1; /* decoded ahead: now it has a slot */
+	retire(as);
 	pump(d, 0);
 	if (submit_ready(d) < 0) return -1;
 	return 1;

@@ -330,6 +330,7 @@ struct h264_dec {
 	 * the API-visible context, names pictures by virtual frame ids instead of frame slots (no DPB
 	 * output, no caller frames, no header callback) and creates the slice-data jobs */
 	int lookahead;
+	long ahead_submits;       /* pictures submitted before this (API) context closed them (decode ahead) */
 	int vid_next;            /* lookahead: round-robin cursor of the virtual frame id allocator */
 	int stats;               /* M2DEC_AMD_ASYNC_STATS: time spent delivering frames */
 	double t_drain, t_sync;
@@ -358,6 +359,7 @@ int h264_async_drain(h264_dec_t *d, int slot);
 void h264_async_stop(h264_dec_t *d);
 int h264_async_nal_next(h264_dec_t *d);
 void h264_async_resume(h264_dec_t *d);
+void h264_async_la_sps(h264_dec_t *la);
 int h264_async_sps(h264_dec_t *d);
 int h264_async_push_nal(h264_dec_t *la);
 

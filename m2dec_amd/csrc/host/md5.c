@@ -3,6 +3,7 @@
  * (src/app/filewrite.h:11-29 cropped NV12 rows, :99-105 "%02x" x16 + "\r\n").
  */
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include "m2dec_amd.h"
 
@@ -155,9 +156,20 @@ static void md5_final(md5_t *m, uint8_t out[16])
 	}
 }
 
-void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
+static void md5_line(const uint8_t dg[16], char out[35])
 {
 	static const char hex[] = "0123456789abcdef";
+	for (int i = 0; i < 16; ++i) {
+		out[i * 2] = hex[dg[i] >> 4];
+		out[i * 2 + 1] = hex[dg[i] & 15];
+	}
+	out[32] = '\r';
+	out[33] = '\n';
+	out[34] = 0;
+}
+
+void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
+{
 	md5_t m;
 	uint8_t dg[16];
 	int stride = f->width;
@@ -176,11 +188,180 @@ void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
 		src += stride;
 	}
 	md5_final(&m, dg);
-	for (int i = 0; i < 16; ++i) {
-		out[i * 2] = hex[dg[i] >> 4];
-		out[i * 2 + 1] = hex[dg[i] & 15];
+	md5_line(dg, out);
+}
+
+/* ---------------------------------------------------------------- 16 frames at once (AVX-512F)
+ * Multi-buffer MD5: lane l of every 512-bit register carries frame l's chain, so one core runs 16
+ * independent MD5s at about the latency of one (the per-frame MD5 of FileWriterMd5 is a sequential
+ * chain; frames are what can go side by side).  A frame's message is its cropped luma rows then its
+ * cropped chroma rows; without horizontal crop each is one contiguous run, and every full 64-byte
+ * block of a run is hashed in the lanes; the last partial block and the padding go through the
+ * scalar code from the lane's chaining value. */
+#if defined(__x86_64__)
+#include <immintrin.h>
+
+#define VSTEP(imm, a, b, c, d, wi, k, s) \
+	do { \
+		a = _mm512_add_epi32(a, _mm512_add_epi32(_mm512_ternarylogic_epi32(b, c, d, imm), \
+		                                         _mm512_add_epi32(w[wi], _mm512_set1_epi32((int)(k))))); \
+		a = _mm512_add_epi32(_mm512_rol_epi32(a, s), b); \
+	} while (0)
+/* ternary-logic truth tables over (b, c, d): F = b ? c : d, G = d ? b : c, H = b ^ c ^ d, I = c ^ (b | ~d) */
+#define TF 0xca
+#define TG 0xe4
+#define TH 0x96
+#define TI 0x39
+
+__attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16], const uint8_t *base,
+                                                              const int32_t off[16], size_t nblocks)
+{
+	__m512i va = _mm512_loadu_si512(st[0]), vb = _mm512_loadu_si512(st[1]);
+	__m512i vc = _mm512_loadu_si512(st[2]), vd = _mm512_loadu_si512(st[3]);
+	__m512i vo = _mm512_loadu_si512(off);
+	const __m512i step = _mm512_set1_epi32(64);
+	for (size_t n = 0; n < nblocks; ++n) {
+		__m512i w[16];
+		__m512i a = va, b = vb, c = vc, d = vd;
+		for (int i = 0; i < 16; ++i) w[i] = _mm512_i32gather_epi32(_mm512_add_epi32(vo, _mm512_set1_epi32(4 * i)), base, 1);
+		vo = _mm512_add_epi32(vo, step);
+		VSTEP(TF, a, b, c, d, 0, 0xd76aa478u, 7);
+		VSTEP(TF, d, a, b, c, 1, 0xe8c7b756u, 12);
+		VSTEP(TF, c, d, a, b, 2, 0x242070dbu, 17);
+		VSTEP(TF, b, c, d, a, 3, 0xc1bdceeeu, 22);
+		VSTEP(TF, a, b, c, d, 4, 0xf57c0fafu, 7);
+		VSTEP(TF, d, a, b, c, 5, 0x4787c62au, 12);
+		VSTEP(TF, c, d, a, b, 6, 0xa8304613u, 17);
+		VSTEP(TF, b, c, d, a, 7, 0xfd469501u, 22);
+		VSTEP(TF, a, b, c, d, 8, 0x698098d8u, 7);
+		VSTEP(TF, d, a, b, c, 9, 0x8b44f7afu, 12);
+		VSTEP(TF, c, d, a, b, 10, 0xffff5bb1u, 17);
+		VSTEP(TF, b, c, d, a, 11, 0x895cd7beu, 22);
+		VSTEP(TF, a, b, c, d, 12, 0x6b901122u, 7);
+		VSTEP(TF, d, a, b, c, 13, 0xfd987193u, 12);
+		VSTEP(TF, c, d, a, b, 14, 0xa679438eu, 17);
+		VSTEP(TF, b, c, d, a, 15, 0x49b40821u, 22);
+		VSTEP(TG, a, b, c, d, 1, 0xf61e2562u, 5);
+		VSTEP(TG, d, a, b, c, 6, 0xc040b340u, 9);
+		VSTEP(TG, c, d, a, b, 11, 0x265e5a51u, 14);
+		VSTEP(TG, b, c, d, a, 0, 0xe9b6c7aau, 20);
+		VSTEP(TG, a, b, c, d, 5, 0xd62f105du, 5);
+		VSTEP(TG, d, a, b, c, 10, 0x02441453u, 9);
+		VSTEP(TG, c, d, a, b, 15, 0xd8a1e681u, 14);
+		VSTEP(TG, b, c, d, a, 4, 0xe7d3fbc8u, 20);
+		VSTEP(TG, a, b, c, d, 9, 0x21e1cde6u, 5);
+		VSTEP(TG, d, a, b, c, 14, 0xc33707d6u, 9);
+		VSTEP(TG, c, d, a, b, 3, 0xf4d50d87u, 14);
+		VSTEP(TG, b, c, d, a, 8, 0x455a14edu, 20);
+		VSTEP(TG, a, b, c, d, 13, 0xa9e3e905u, 5);
+		VSTEP(TG, d, a, b, c, 2, 0xfcefa3f8u, 9);
+		VSTEP(TG, c, d, a, b, 7, 0x676f02d9u, 14);
+		VSTEP(TG, b, c, d, a, 12, 0x8d2a4c8au, 20);
+		VSTEP(TH, a, b, c, d, 5, 0xfffa3942u, 4);
+		VSTEP(TH, d, a, b, c, 8, 0x8771f681u, 11);
+		VSTEP(TH, c, d, a, b, 11, 0x6d9d6122u, 16);
+		VSTEP(TH, b, c, d, a, 14, 0xfde5380cu, 23);
+		VSTEP(TH, a, b, c, d, 1, 0xa4beea44u, 4);
+		VSTEP(TH, d, a, b, c, 4, 0x4bdecfa9u, 11);
+		VSTEP(TH, c, d, a, b, 7, 0xf6bb4b60u, 16);
+		VSTEP(TH, b, c, d, a, 10, 0xbebfbc70u, 23);
+		VSTEP(TH, a, b, c, d, 13, 0x289b7ec6u, 4);
+		VSTEP(TH, d, a, b, c, 0, 0xeaa127fau, 11);
+		VSTEP(TH, c, d, a, b, 3, 0xd4ef3085u, 16);
+		VSTEP(TH, b, c, d, a, 6, 0x04881d05u, 23);
+		VSTEP(TH, a, b, c, d, 9, 0xd9d4d039u, 4);
+		VSTEP(TH, d, a, b, c, 12, 0xe6db99e5u, 11);
+		VSTEP(TH, c, d, a, b, 15, 0x1fa27cf8u, 16);
+		VSTEP(TH, b, c, d, a, 2, 0xc4ac5665u, 23);
+		VSTEP(TI, a, b, c, d, 0, 0xf4292244u, 6);
+		VSTEP(TI, d, a, b, c, 7, 0x432aff97u, 10);
+		VSTEP(TI, c, d, a, b, 14, 0xab9423a7u, 15);
+		VSTEP(TI, b, c, d, a, 5, 0xfc93a039u, 21);
+		VSTEP(TI, a, b, c, d, 12, 0x655b59c3u, 6);
+		VSTEP(TI, d, a, b, c, 3, 0x8f0ccc92u, 10);
+		VSTEP(TI, c, d, a, b, 10, 0xffeff47du, 15);
+		VSTEP(TI, b, c, d, a, 1, 0x85845dd1u, 21);
+		VSTEP(TI, a, b, c, d, 8, 0x6fa87e4fu, 6);
+		VSTEP(TI, d, a, b, c, 15, 0xfe2ce6e0u, 10);
+		VSTEP(TI, c, d, a, b, 6, 0xa3014314u, 15);
+		VSTEP(TI, b, c, d, a, 13, 0x4e0811a1u, 21);
+		VSTEP(TI, a, b, c, d, 4, 0xf7537e82u, 6);
+		VSTEP(TI, d, a, b, c, 11, 0xbd3af235u, 10);
+		VSTEP(TI, c, d, a, b, 2, 0x2ad7d2bbu, 15);
+		VSTEP(TI, b, c, d, a, 9, 0xeb86d391u, 21);
+		va = _mm512_add_epi32(va, a);
+		vb = _mm512_add_epi32(vb, b);
+		vc = _mm512_add_epi32(vc, c);
+		vd = _mm512_add_epi32(vd, d);
 	}
-	out[32] = '\r';
-	out[33] = '\n';
-	out[34] = 0;
+	_mm512_storeu_si512(st[0], va);
+	_mm512_storeu_si512(st[1], vb);
+	_mm512_storeu_si512(st[2], vc);
+	_mm512_storeu_si512(st[3], vd);
+}
+
+static int have_avx512(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("M2DEC_AMD_MD5_SCALAR"); /* (tests: force the scalar path) */
+		__builtin_cpu_init();
+		v = __builtin_cpu_supports("avx512f") && !(e && atoi(e));
+	}
+	return v;
+}
+#endif
+
+int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
+{
+	if (n <= 0 || n > 16) return -1;
+#if defined(__x86_64__)
+	int lanes_ok = n >= 2 && have_avx512();
+	const int stride = f[0].width, h = f[0].height - f[0].crop[2] - f[0].crop[3];
+	const uint8_t *lo = NULL, *hi = NULL;
+	for (int i = 0; i < n && lanes_ok; ++i) {
+		const m2d_frame_t *g = &f[i];
+		/* one geometry; rows contiguous (no horizontal crop) */
+		lanes_ok = g->width == stride && g->height == f[0].height && g->crop[2] == f[0].crop[2] &&
+		           g->crop[3] == f[0].crop[3] && g->crop[0] == 0 && g->crop[1] == 0;
+		for (int k = 0; k < 2 && lanes_ok; ++k) {
+			const uint8_t *p = k ? g->chroma : g->luma;
+			if (!lo || p < lo) lo = p;
+			if (!hi || p > hi) hi = p;
+		}
+	}
+	if (lanes_ok && h > 0 && (size_t)(hi - lo) + (size_t)stride * (size_t)h < ((size_t)1 << 31)) {
+		const size_t la = (size_t)stride * (size_t)h, lb = (size_t)stride * (size_t)(h >> 1);
+		const size_t na = la / 64, nb = (la % 64) ? 0 : lb / 64;
+		uint32_t st[4][16];
+		int32_t offa[16], offb[16];
+		static const uint32_t iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+		for (int l = 0; l < 16; ++l) {
+			const m2d_frame_t *g = &f[l < n ? l : 0]; /* idle lanes repeat lane 0 */
+			offa[l] = (int32_t)(g->luma + (size_t)stride * f[0].crop[2] - lo);
+			offb[l] = (int32_t)(g->chroma + (size_t)stride * (f[0].crop[2] >> 1) - lo);
+			for (int k = 0; k < 4; ++k) st[k][l] = iv[k];
+		}
+		md5x16_blocks(st, lo, offa, na);
+		md5x16_blocks(st, lo, offb, nb);
+		for (int l = 0; l < n; ++l) {
+			md5_t m;
+			uint8_t dg[16];
+			for (int k = 0; k < 4; ++k) m.h[k] = st[k][l];
+			m.len = (uint64_t)(na + nb) * 64;
+			m.fill = 0;
+			if (nb) {
+				md5_update(&m, lo + offb[l] + nb * 64, lb - nb * 64);
+			} else {
+				md5_update(&m, lo + offa[l] + na * 64, la - na * 64);
+				md5_update(&m, lo + offb[l], lb);
+			}
+			md5_final(&m, dg);
+			md5_line(dg, out[l]);
+		}
+		return 0;
+	}
+#endif
+	for (int i = 0; i < n; ++i) m2dec_amd_frame_md5(&f[i], out[i]);
+	return 0;
 }

@@ -25,6 +25,7 @@
  *   deblocking       h264.cpp:10253-10663 (deblock_pb), tables h264vld.h:932-4627 (spec 8.7)
  */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include "m2d_recon.h"
@@ -1063,15 +1064,30 @@ typedef struct {
 	m2r_picture_t pic;
 	void *mem;
 	size_t mem_size;
+	/* decode ahead (M2R_PIC_VIRTUAL): one picture buffer per virtual id, copied to a frame by bind */
+	m2d_frame_t vfr[64];
+	size_t luma_size;
 } oracle_be_t;
+
+/* the recon reads unavailable neighbours' bytes (unused) around the frame, as it may in the caller's
+ * frames: each buffer keeps a margin on both sides */
+#define VMARGIN 32768
+
+static void vfree(oracle_be_t *b)
+{
+	for (int i = 0; i < 64; ++i) {
+		if (b->vfr[i].luma) free(b->vfr[i].luma - VMARGIN);
+		b->vfr[i].luma = b->vfr[i].chroma = NULL;
+	}
+}
 
 static int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
 {
 	oracle_be_t *b = (oracle_be_t *)self;
-	(void)width;
-	(void)height;
 	b->n = n > 64 ? 64 : n;
 	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)b->n);
+	if (b->luma_size != (size_t)width * (size_t)height) vfree(b);
+	b->luma_size = (size_t)width * (size_t)height;
 	return 0;
 }
 
@@ -1108,7 +1124,35 @@ static m2r_picture_t *be_acquire(void *self, int wm, int hm)
 static int be_submit(void *self, m2r_picture_t *pic)
 {
 	oracle_be_t *b = (oracle_be_t *)self;
+	if (pic->flags & M2R_PIC_VIRTUAL) {
+		if (pic->slot < 0 || pic->slot >= 64) return -1;
+		if (!b->vfr[pic->slot].luma) {
+			uint8_t *m = (uint8_t *)calloc(1, b->luma_size * 3 / 2 + 2 * VMARGIN);
+			if (!m) return -1;
+			b->vfr[pic->slot].luma = m + VMARGIN;
+			b->vfr[pic->slot].chroma = b->vfr[pic->slot].luma + b->luma_size;
+		}
+		for (int i = 0; i < pic->n_inter; ++i)
+			for (int k = 0; k < 8; ++k) {
+				const int v = (&pic->inter[i].slot[0][0])[k];
+				if (v >= 64 || (v >= 0 && !b->vfr[v].luma)) {
+					fprintf(stderr, "oracle: picture into %d reads unwritten buffer %d (inter %d)\n", pic->slot, v, i);
+					return -1;
+				}
+			}
+		oracle_recon_picture(pic, b->vfr, 64);
+		return 0;
+	}
 	oracle_recon_picture(pic, b->frames, b->n);
+	return 0;
+}
+
+static int be_bind(void *self, int vid, int slot)
+{
+	oracle_be_t *b = (oracle_be_t *)self;
+	if (vid < 0 || vid >= 64 || slot < 0 || slot >= b->n || !b->vfr[vid].luma) return -1;
+	memcpy(b->frames[slot].luma, b->vfr[vid].luma, b->luma_size);
+	memcpy(b->frames[slot].chroma, b->vfr[vid].chroma, b->luma_size / 2);
 	return 0;
 }
 
@@ -1122,6 +1166,7 @@ static int be_sync(void *self, int slot)
 static void be_destroy(void *self)
 {
 	oracle_be_t *b = (oracle_be_t *)self;
+	vfree(b);
 	free(b->mem);
 	free(b);
 }
@@ -1136,5 +1181,6 @@ int oracle_backend_create(m2r_backend_t *out)
 	out->submit = be_submit;
 	out->sync_frame = be_sync;
 	out->destroy = be_destroy;
+	out->bind = be_bind;
 	return 0;
 }

@@ -34,7 +34,7 @@ class Picture(ctypes.Structure):
                 ("n_intra", ctypes.c_int32), ("deblock", ctypes.c_int32), ("mb", ctypes.POINTER(MB)),
                 ("dbk", ctypes.c_void_p), ("slice", ctypes.c_void_p), ("inter", ctypes.c_void_p),
                 ("coef", ctypes.c_void_p), ("cap_slices", ctypes.c_int32), ("cap_inter", ctypes.c_int32),
-                ("cap_coef", ctypes.c_int32), ("pad", ctypes.c_int32)]
+                ("cap_coef", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
 
 SET_FRAMES = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Frame), ctypes.c_int,

@@ -67,3 +67,19 @@ def test_output_calls_match_any_caller_pattern(built, threads, dpb, emptify):
     assert err == -2 and got == ref
     if dpb != 1:
         assert sorted(got) == sorted(GOLDEN[name]["md5"])
+
+
+def test_decode_ahead(built, monkeypatch):
+    """Back ends with bind (the oracle's, like the HIP one) get pictures as soon as they are parsed,
+    named by virtual ids, before the API context reaches them (Stats.ahead counts those); the frames
+    are the same with decode-ahead off (M2DEC_AMD_NO_AHEAD: submission in API order, slots translated)."""
+    name = "c2_720p_s1"
+    st = m2dec_amd.Stats()
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=4, stats=st)
+    assert got == GOLDEN[name]["md5"] and st.ahead > 0
+    monkeypatch.setenv("M2DEC_AMD_NO_AHEAD", "1")
+    st = m2dec_amd.Stats()
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=4, stats=st)
+    assert got == GOLDEN[name]["md5"] and st.ahead == 0

@@ -34,6 +34,7 @@ typedef struct {
 	double kernel_us;
 	int64_t kernel_launches;
 	int64_t alg_bytes;
+	int64_t hold_waits; /* MD5 drivers: times the frame LRU waited for a frame the MD5 threads held */
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).
@@ -66,6 +67,10 @@ int m2dec_amd_decode_stream2(const uint8_t *data, size_t len, const m2r_backend_
 int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device);
 /* Non-zero if a gfx950 device is usable by this process. */
 int m2dec_amd_hip_available(void);
+/* page-lock host memory for the life of the process (or until unpin); HIP back ends then skip
+ * registering caller frames that lie inside it */
+int m2dec_amd_hip_pin(void *p, size_t n);
+void m2dec_amd_hip_unpin(void *p);
 
 /* Per-kernel timing of the HIP back end since creation (microseconds, HIP events). */
 typedef struct {
@@ -91,6 +96,9 @@ int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35]);
  * md5s (at most `max`), the MD5s on helper threads.  Returns the number of frames delivered or < 0. */
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
                                 m2dec_amd_stats_t *stats);
+/* the same driver over a borrowed back end (tests: the CPU oracle), with explicit parse / MD5 threads */
+int m2dec_amd_decode_stream_md5_backend(const uint8_t *data, size_t len, const m2r_backend_t *backend, int parse_threads,
+                                        int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats);
 /* A back end that reconstructs nothing (acquire: one record arena; submit / sync: no-ops): decoding
  * through it times the host parse alone. */
 int m2dec_amd_null_backend_create(m2r_backend_t *out);

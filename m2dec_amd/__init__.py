@@ -50,7 +50,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("frames_out", ctypes.c_int), ("pictures", ctypes.c_int), ("last_error", ctypes.c_int),
                 ("ahead", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
                 ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
-                ("alg_bytes", ctypes.c_int64)]
+                ("alg_bytes", ctypes.c_int64), ("hold_waits", ctypes.c_int64)]
 
 
 class HipTiming(ctypes.Structure):
@@ -107,6 +107,10 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_decode_stream_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(Stats)]
         L.m2dec_amd_decode_stream_md5.restype = ctypes.c_int
+        L.m2dec_amd_decode_stream_md5_backend.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend),
+                                                          ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                                          ctypes.POINTER(Stats)]
+        L.m2dec_amd_decode_stream_md5_backend.restype = ctypes.c_int
         L.m2dec_amd_decode_streams_md5.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
                                                    ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
@@ -217,7 +221,7 @@ def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 
 
     ``backend`` None -> the HIP back end on ``device`` (raises if absent).  Any other m2r_backend_t
     (e.g. the oracle's, in tests) is borrowed.  ``parse_threads``: parse-ahead workers (-1: the
-    default — 8 with the HIP back end, none with a borrowed one).  ``stats`` (a Stats) receives the
+    default — 12 with the HIP back end, none with a borrowed one).  ``stats`` (a Stats) receives the
     decoder's counters.
     """
     L = lib()
@@ -263,6 +267,21 @@ def decode_stream_md5(data: bytes, device: int = 0, dpb: int = -1, stats: Option
     buf = ctypes.create_string_buffer(35 * cap)
     st = stats if stats is not None else Stats()
     n = L.m2dec_amd_decode_stream_md5(data, len(data), device, dpb, buf, cap, ctypes.byref(st))
+    if n < 0:
+        raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
+    raw = buf.raw
+    return [raw[35 * i:35 * i + 32].decode() for i in range(min(n, cap))]
+
+
+def decode_stream_md5_backend(data: bytes, backend: Backend, parse_threads: int = 4, md5_threads: int = 2,
+                              stats: Optional[Stats] = None) -> List[str]:
+    """``decode_stream_md5``'s driver (frames held while helper threads hash them in place, 16 at a
+    time) over a borrowed back end — the CPU oracle in tests."""
+    cap = _max_frames(data)
+    buf = ctypes.create_string_buffer(35 * cap)
+    st = stats if stats is not None else Stats()
+    n = lib().m2dec_amd_decode_stream_md5_backend(data, len(data), ctypes.byref(backend), parse_threads, md5_threads,
+                                                  buf, cap, ctypes.byref(st))
     if n < 0:
         raise RuntimeError(f"m2dec_amd: decode failed (last_error={st.last_error}, frames={st.frames_out})")
     raw = buf.raw

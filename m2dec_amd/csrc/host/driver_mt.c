@@ -17,62 +17,24 @@
 #include <stdio.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 48
+#define MD5_RING 32        /* frames queued or being hashed; the decoder gets as many extra frames */
 #define MD5_BATCH 16       /* frames one thread hashes together (m2dec_amd_frames_md5 lanes) */
 #define MD5_THREADS_MAX 16
-#define MD5_THREADS 3      /* one stream: a 16-frame batch of 1080p takes one core ~5 ms, so a few threads
+#define MD5_THREADS 2      /* one stream: a 16-frame batch of 1080p takes one core ~4 ms, so two threads
                               keep up with the decoder; M2DEC_AMD_MD5_THREADS overrides */
 
-/* Ring memory outlives a call (a service decoding stream after stream, bench.py's steps): touching
- * 150 MB of fresh pages per stream costs more than the hashing.  One contiguous block per ring, so
- * the multi-buffer MD5 addresses every slot with 32-bit offsets. */
-static pthread_mutex_t ring_mu = PTHREAD_MUTEX_INITIALIZER;
-static struct {
-	uint8_t *mem;
-	size_t size;
-} ring_cache[4];
-
-static uint8_t *ring_take(size_t need, size_t *got)
-{
-	uint8_t *m = NULL;
-	pthread_mutex_lock(&ring_mu);
-	for (int i = 0; i < 4 && !m; ++i)
-		if (ring_cache[i].mem && ring_cache[i].size >= need) {
-			m = ring_cache[i].mem;
-			*got = ring_cache[i].size;
-			ring_cache[i].mem = NULL;
-		}
-	pthread_mutex_unlock(&ring_mu);
-	if (!m) {
-		m = (uint8_t *)malloc(need);
-		*got = m ? need : 0;
-	}
-	return m;
-}
-
-static void ring_give(uint8_t *m, size_t size)
-{
-	if (!m) return;
-	pthread_mutex_lock(&ring_mu);
-	for (int i = 0; i < 4; ++i)
-		if (!ring_cache[i].mem) {
-			ring_cache[i].mem = m;
-			ring_cache[i].size = size;
-			m = NULL;
-			break;
-		}
-	pthread_mutex_unlock(&ring_mu);
-	free(m);
-}
-
+/* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
+ * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
+ * caller's thread.  The driver's frames are one allocation, so the multi-buffer MD5 addresses
+ * every frame with 32-bit offsets. */
 typedef struct {
 	pthread_mutex_t mu;
 	pthread_cond_t cv_job, cv_free;
-	uint8_t *mem;            /* MD5_RING slots of `cap` bytes (ring_take) */
-	size_t mem_size, cap;
+	m2dec_hold_t hold;
 	m2d_frame_t frm[MD5_RING];
 	int idx[MD5_RING];       /* output frame number of the job in slot k */
 	int state[MD5_RING];     /* 0 free, 1 queued, 2 being hashed */
@@ -81,9 +43,9 @@ typedef struct {
 	char *md5s;
 	int max;
 	int n;                   /* frames delivered */
-	int failed;
 	int stats;
-	double t_wait, t_copy;   /* caller: waiting for a free ring slot, copying frames */
+	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
+	double t_wait;           /* caller: waiting for a free queue slot */
 	double t_done;           /* the last MD5 line written */
 } md5_pipe_t;
 
@@ -113,10 +75,13 @@ static void *md5_worker(void *arg)
 			ks[n++] = k;
 		}
 		pthread_mutex_unlock(&p->mu);
+		if (p->delay_us) usleep((useconds_t)p->delay_us); /* (tests: MD5 slower than the decoder) */
 		char lines[MD5_BATCH][35];
 		m2dec_amd_frames_md5(f, n, lines);
-		for (int j = 0; j < n; ++j)
+		for (int j = 0; j < n; ++j) {
 			if (ix[j] < p->max) memcpy(p->md5s + (size_t)ix[j] * 35, lines[j], 35);
+			m2dec_hold_release(&p->hold, f[j].luma);
+		}
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
 		if (t > p->t_done) p->t_done = t;
@@ -127,47 +92,17 @@ static void *md5_worker(void *arg)
 	return NULL;
 }
 
-static int ring_idle(const md5_pipe_t *p)
-{
-	for (int k = 0; k < MD5_RING; ++k)
-		if (p->state[k]) return 0;
-	return 1;
-}
-
-/* on_frame of the stream driver: copy the frame into the next free ring slot, queue its MD5 */
+/* on_frame of the stream driver: hold the frame, queue its MD5 */
 static void md5_on_frame(void *arg, const m2d_frame_t *f)
 {
 	md5_pipe_t *p = (md5_pipe_t *)arg;
-	const size_t luma = (size_t)f->width * (size_t)f->height, bytes = luma * 3 / 2;
 	const int k = p->head % MD5_RING;
 	const double t0 = p->stats ? now_s() : 0;
+	m2dec_hold_add(&p->hold, f->luma);
 	pthread_mutex_lock(&p->mu);
-	while (p->state[k] || (bytes > p->cap && !ring_idle(p))) pthread_cond_wait(&p->cv_free, &p->mu);
-	pthread_mutex_unlock(&p->mu);
-	const double t1 = p->stats ? now_s() : 0;
-	if (bytes > p->cap) { /* (re)size the ring while no job holds a buffer; only this thread allocates */
-		const size_t slot = (bytes + 63) & ~(size_t)63;
-		ring_give(p->mem, p->mem_size);
-		p->mem = ring_take(slot * MD5_RING, &p->mem_size);
-		if (!p->mem) {
-			p->failed = 1;
-			p->cap = 0;
-			return;
-		}
-		p->cap = p->mem_size / MD5_RING;
-	}
-	uint8_t *buf = p->mem + (size_t)k * p->cap;
-	memcpy(buf, f->luma, luma);
-	memcpy(buf + luma, f->chroma, luma / 2);
-	if (p->stats) {
-		p->t_wait += t1 - t0;
-		p->t_copy += now_s() - t1;
-	}
-	m2d_frame_t c = *f;
-	c.luma = buf;
-	c.chroma = buf + luma;
-	pthread_mutex_lock(&p->mu);
-	p->frm[k] = c;
+	while (p->state[k]) pthread_cond_wait(&p->cv_free, &p->mu);
+	if (p->stats) p->t_wait += now_s() - t0;
+	p->frm[k] = *f;
 	p->idx[k] = p->n++;
 	p->state[k] = 1;
 	p->head++;
@@ -175,18 +110,24 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_unlock(&p->mu);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, int md5_threads,
-                      char *md5s, int max, m2dec_amd_stats_t *stats);
+static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                      int parse_threads, int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats);
 
 int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int dpb, char *md5s, int max,
                                 m2dec_amd_stats_t *stats)
 {
 	const char *e = getenv("M2DEC_AMD_MD5_THREADS");
-	return decode_md5(data, len, device, dpb, -1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS, md5s, max, stats);
+	return decode_md5(data, len, NULL, device, dpb, -1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS, md5s, max, stats);
 }
 
-static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int parse_threads, int md5_threads,
-                      char *md5s, int max, m2dec_amd_stats_t *stats)
+int m2dec_amd_decode_stream_md5_backend(const uint8_t *data, size_t len, const m2r_backend_t *backend, int parse_threads,
+                                        int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats)
+{
+	return decode_md5(data, len, backend, 0, -1, parse_threads, md5_threads, md5s, max, stats);
+}
+
+static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                      int parse_threads, int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats)
 {
 	md5_pipe_t p;
 	pthread_t th[MD5_THREADS_MAX];
@@ -195,6 +136,8 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	pthread_mutex_init(&p.mu, NULL);
 	pthread_cond_init(&p.cv_job, NULL);
 	pthread_cond_init(&p.cv_free, NULL);
+	m2dec_hold_init(&p.hold);
+	if (getenv("M2DEC_AMD_MD5_DELAY_US")) p.delay_us = atoi(getenv("M2DEC_AMD_MD5_DELAY_US"));
 	p.md5s = md5s;
 	p.max = max;
 	p.stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
@@ -204,20 +147,22 @@ static int decode_md5(const uint8_t *data, size_t len, int device, int dpb, int 
 	if (!nth) return -1;
 	m2dec_amd_stats_t st;
 	memset(&st, 0, sizeof(st));
-	r = m2dec_amd_decode_stream3(data, len, NULL, device, dpb, parse_threads, md5_on_frame, &p, &st);
+	const char *ex = getenv("M2DEC_AMD_MD5_EXTRA"); /* (tests: fewer spare frames -> the decoder waits on holds) */
+	r = h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, ex ? atoi(ex) : MD5_RING, &p.hold,
+	                            md5_on_frame, &p, &st);
 	pthread_mutex_lock(&p.mu);
 	p.quit = 1;
 	pthread_cond_broadcast(&p.cv_job);
 	pthread_mutex_unlock(&p.mu);
 	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
-	if (p.stats) fprintf(stderr, "md5 ring: caller waits %.3f s, frame copies %.3f s (%d threads)\n", p.t_wait, p.t_copy, nth);
-	ring_give(p.mem, p.mem_size);
+	if (p.stats) fprintf(stderr, "md5: caller waits %.3f s, frame LRU waits %ld (%d threads)\n", p.t_wait, p.hold.waits, nth);
+	m2dec_hold_destroy(&p.hold);
 	if (p.t_done > st.t_end) st.t_end = p.t_done; /* delivered = its MD5 line written */
+	st.hold_waits = p.hold.waits;
 	if (stats) *stats = st;
 	pthread_mutex_destroy(&p.mu);
 	pthread_cond_destroy(&p.cv_job);
 	pthread_cond_destroy(&p.cv_free);
-	if (p.failed) return -1;
 	return r < 0 ? r : p.n;
 }
 
@@ -234,7 +179,7 @@ static void *stream_worker(void *arg)
 {
 	stream_job_t *j = (stream_job_t *)arg;
 	/* one parse-ahead worker per stream: the streams themselves fill the host cores */
-	j->result = decode_md5(j->data, j->len, j->device, -1, 1, 2, j->md5s, j->max, NULL);
+	j->result = decode_md5(j->data, j->len, NULL, j->device, -1, 1, 2, j->md5s, j->max, NULL);
 	return NULL;
 }
 

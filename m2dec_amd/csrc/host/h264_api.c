@@ -80,7 +80,7 @@ static int ensure_backend(h264_dec_t *d)
 		d->have_backend = 1;
 		if (d->parse_threads < 0) { /* default for the product path: parse ahead on worker threads */
 			const char *e = getenv("M2DEC_AMD_PARSE_THREADS");
-			d->parse_threads = e ? atoi(e) : 8;
+			d->parse_threads = e ? atoi(e) : 12;
 		}
 	}
 	if (d->parse_threads > 0 && !d->as && h264_async_start(d, d->parse_threads) < 0) return -1;
@@ -207,8 +207,12 @@ int h264_decode_loop(h264_dec_t *d)
 			id = h264_parse_sps(d, &b);
 			if (id < 0) return id;
 			if (!d->in_picture) d->active_sps = id;
-			if (!d->lookahead) d->header_callback(d->header_callback_arg, d->stream->id);
-			else h264_async_la_sps(d); /* pictures after it wait for the API context's callback */
+			if (d->lookahead) {
+				h264_async_la_sps(d); /* pictures after it wait for the API context's callback */
+			} else {
+				d->header_callback(d->header_callback_arg, d->stream->id);
+				if (d->as) h264_async_api_sps(d);
+			}
 			break;
 		}
 		case 8: {
@@ -343,6 +347,10 @@ typedef struct {
 	int nframes;
 	size_t luma_len;
 	uint8_t work[64];
+	int extra;               /* frames beyond the decoder's need (held by the caller meanwhile) */
+	size_t frame_size;       /* frame_mem: a block of the frame pool (fpool_take) */
+	int frame_pinned, pin;   /* page-locked / to be page-locked (the built-in HIP back end) */
+	m2dec_hold_t *hold;
 	int failed;
 	double setup_s;
 	double t_last;           /* on_frame of the last frame returned */
@@ -367,6 +375,55 @@ static int drv_reread(void *arg)
 	return -1;
 }
 
+/* Frame memory of the stream driver outlives a stream (bench steps, a service decoding stream after
+ * stream): fresh memory costs page faults, and the HIP back end would page-lock it again (~0.15 ms
+ * per 1080p frame).  Blocks used with the built-in HIP back end are page-locked once, for good. */
+static pthread_mutex_t fpool_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+	uint8_t *mem;
+	size_t size;
+	int pinned;
+} fpool[16];
+
+static uint8_t *fpool_take(size_t need, size_t *size, int *pinned)
+{
+	uint8_t *m = NULL;
+	pthread_mutex_lock(&fpool_mu);
+	for (int i = 0; i < 16 && !m; ++i)
+		if (fpool[i].mem && fpool[i].size >= need) {
+			m = fpool[i].mem;
+			*size = fpool[i].size;
+			*pinned = fpool[i].pinned;
+			fpool[i].mem = NULL;
+		}
+	pthread_mutex_unlock(&fpool_mu);
+	if (!m) {
+		m = (uint8_t *)aligned_alloc(4096, need);
+		*size = need;
+		*pinned = 0;
+	}
+	return m;
+}
+
+static void fpool_give(uint8_t *m, size_t size, int pinned)
+{
+	if (!m) return;
+	pthread_mutex_lock(&fpool_mu);
+	for (int i = 0; i < 16; ++i)
+		if (!fpool[i].mem) {
+			fpool[i].mem = m;
+			fpool[i].size = size;
+			fpool[i].pinned = pinned;
+			m = NULL;
+			break;
+		}
+	pthread_mutex_unlock(&fpool_mu);
+	if (m) {
+		if (pinned) m2dec_amd_hip_unpin(m);
+		free(m);
+	}
+}
+
 /* M2Decoder::SetFrames, m2decoder.h:54-80 */
 static int drv_header(void *arg, void *id)
 {
@@ -382,15 +439,17 @@ static int drv_header(void *arg, void *id)
 	w = (info.src_width + 15) & ~15;
 	h = (info.src_height + 15) & ~15;
 	luma_len = (size_t)w * (size_t)h;
-	bufnum = v->outbuf + info.frame_num + 16;
+	bufnum = v->outbuf + info.frame_num + 16 + v->extra;
 	if (bufnum > H264D_MAX_FRAME_NUM) bufnum = H264D_MAX_FRAME_NUM;
 	if (v->frame_mem && bufnum <= v->nframes && luma_len <= v->luma_len) return 0;
-	free(v->frame_mem);
-	v->frame_mem = (uint8_t *)aligned_alloc(4096, ((luma_len * 3 / 2 + 4095) & ~(size_t)4095) * (size_t)bufnum);
+	if (v->hold) m2dec_hold_wait_idle(v->hold); /* nobody reads the old frames any more */
+	fpool_give(v->frame_mem, v->frame_size, v->frame_pinned);
+	v->frame_mem = fpool_take(((luma_len * 3 / 2 + 4095) & ~(size_t)4095) * (size_t)bufnum, &v->frame_size, &v->frame_pinned);
 	if (!v->frame_mem) {
 		v->failed = 1;
 		return -1;
 	}
+	if (v->pin && !v->frame_pinned) v->frame_pinned = m2dec_amd_hip_pin(v->frame_mem, v->frame_size) == 0;
 	{
 		size_t fsz = (luma_len * 3 / 2 + 4095) & ~(size_t)4095;
 		for (int i = 0; i < bufnum; ++i) {
@@ -431,6 +490,15 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
                              int parse_threads, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
                              m2dec_amd_stats_t *stats)
 {
+	return h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, 0, NULL, on_frame, arg, stats);
+}
+
+/* the stream driver; `hold`: on_frame may keep reading a frame after it returns until it releases it
+ * from `hold` (the frame is not reused meanwhile), with `extra` more frames than the decoder needs */
+int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                            int parse_threads, int extra, m2dec_hold_t *hold,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
+{
 	driver_t v;
 	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
 	m2d_frame_t frm;
@@ -442,7 +510,11 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
 	v.len = len;
 	v.on_frame = on_frame;
 	v.arg = arg;
+	v.extra = extra;
+	v.hold = hold;
+	v.pin = backend == NULL;
 	h264d_func->init(d, dpb, drv_header, &v);
+	d->hold = hold;
 	d->device = device;
 	if (backend) m2dec_amd_h264_set_backend(d, backend);
 	if (parse_threads >= 0) m2dec_amd_h264_set_parse_threads(d, parse_threads);
@@ -500,6 +572,67 @@ done:
 	if (backend) d->have_backend = 0; /* borrowed: the caller destroys it */
 	m2dec_amd_h264_release(d);
 	free(d);
-	free(v.frame_mem);
+	if (hold) m2dec_hold_wait_idle(hold);
+	fpool_give(v.frame_mem, v.frame_size, v.frame_pinned);
 	return (err == -2) ? n : -1;
+}
+
+/* ------------------------------------------------------------------ held frames */
+void m2dec_hold_init(m2dec_hold_t *h)
+{
+	memset(h, 0, sizeof(*h));
+	pthread_mutex_init(&h->mu, NULL);
+	pthread_cond_init(&h->cv, NULL);
+}
+
+void m2dec_hold_destroy(m2dec_hold_t *h)
+{
+	pthread_mutex_destroy(&h->mu);
+	pthread_cond_destroy(&h->cv);
+}
+
+int m2dec_hold_busy(const m2dec_hold_t *h, const uint8_t *luma)
+{
+	for (int i = 0; i < h->n; ++i)
+		if (h->luma[i] == luma) return h->cnt[i] > 0;
+	return 0;
+}
+
+void m2dec_hold_add(m2dec_hold_t *h, const uint8_t *luma)
+{
+	pthread_mutex_lock(&h->mu);
+	int i = 0;
+	while (i < h->n && h->luma[i] != luma) ++i;
+	if (i == h->n && h->n < 64) {
+		h->luma[i] = luma;
+		h->cnt[i] = 0;
+		h->n++;
+	}
+	if (i < h->n) h->cnt[i]++;
+	pthread_mutex_unlock(&h->mu);
+}
+
+void m2dec_hold_release(m2dec_hold_t *h, const uint8_t *luma)
+{
+	pthread_mutex_lock(&h->mu);
+	for (int i = 0; i < h->n; ++i)
+		if (h->luma[i] == luma && h->cnt[i] > 0) {
+			h->cnt[i]--;
+			break;
+		}
+	pthread_cond_broadcast(&h->cv);
+	pthread_mutex_unlock(&h->mu);
+}
+
+void m2dec_hold_wait_idle(m2dec_hold_t *h)
+{
+	pthread_mutex_lock(&h->mu);
+	for (;;) {
+		int busy = 0;
+		for (int i = 0; i < h->n; ++i) busy |= h->cnt[i] > 0;
+		if (!busy) break;
+		pthread_cond_wait(&h->cv, &h->mu);
+	}
+	h->n = 0; /* (frame memory may be reallocated: forget the addresses) */
+	pthread_mutex_unlock(&h->mu);
 }

@@ -87,6 +87,7 @@ typedef struct h264_job {
 	int8_t map[64];           /* virtual id -> frame slot, as of the API context's close */
 	long sps_nal;             /* NAL index of the last SPS the lookahead read before this picture */
 	int submitted, bound;     /* records handed to the back end / its buffer bound to `slot` */
+	int sub_err;              /* its submission failed (decode ahead: nothing to bind) */
 	int col_store;
 	int nonref;               /* no slice has nal_ref_idc: its co-located store is never read ... */
 	h264_colmb_t *priv_col;   /* ... so it writes this private one (no ordering against other jobs) */
@@ -112,8 +113,14 @@ struct h264_async {
 	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head); job seq s at fifo[s % AS_MAX] */
 	long head, tail;          /* tail: oldest job not retired (submitted, and bound when decoding ahead) */
 	long sub;                 /* next job to submit: [tail, sub) submitted */
+	long bnd;                 /* decode ahead: next job to bind: [tail, bnd) bound */
 	int ahead;                /* decode ahead: the back end has bind (M2R_PIC_VIRTUAL submissions) */
+	pthread_t sub_th;         /* decode ahead: the submitter thread */
+	int sub_quit, sub_err;
+	int ahead_all;            /* M2DEC_AMD_AHEAD_ALL (tests): the API context closes a picture only after the
+	                             submitter took it, so every picture goes ahead whatever the thread timing */
 	long la_sps_nal;          /* NAL index of the last SPS the lookahead context read (-1: none) */
+	long api_sps_nal;         /* NAL index of the last SPS whose header callback the API context ran */
 	h264_job_t *queue[AS_MAX]; /* dispatched; [qtail, qhead) holds every job not yet taken */
 	long qhead, qtail;
 	h264_job_t *cur;          /* the picture the lookahead context is collecting */
@@ -189,6 +196,7 @@ static void job_clear(h264_job_t *j)
 	j->slot = -1;
 	j->submitted = 0;
 	j->bound = 0;
+	j->sub_err = 0;
 }
 
 static void job_free(h264_job_t *j)
@@ -311,6 +319,8 @@ static void *worker(void *arg)
 }
 
 /* ---------------------------------------------------------------- start / stop */
+static void *submitter(void *arg);
+
 static void la_free(h264_dec_t *la)
 {
 	if (!la) return;
@@ -374,7 +384,10 @@ int h264_async_start(h264_dec_t *d, int threads)
 		as->nth++;
 	}
 	if (!as->nth) goto fail;
+	as->api_sps_nal = -1;
+	as->ahead_all = getenv("M2DEC_AMD_AHEAD_ALL") && atoi(getenv("M2DEC_AMD_AHEAD_ALL"));
 	d->as = as;
+	if (as->ahead && pthread_create(&as->sub_th, NULL, submitter, d) != 0) as->ahead = 0;
 	return 0;
 fail:
 	free(as->nq);
@@ -395,8 +408,11 @@ void h264_async_stop(h264_dec_t *d)
 		        as->t_parse);
 	pthread_mutex_lock(&as->mu);
 	as->quit = 1;
+	as->sub_quit = 1;
 	pthread_cond_broadcast(&as->cv_work);
+	pthread_cond_broadcast(&as->cv_done);
 	pthread_mutex_unlock(&as->mu);
+	if (as->ahead) pthread_join(as->sub_th, NULL);
 	for (int i = 0; i < as->nth; ++i) pthread_join(as->th[i], NULL);
 	for (long i = as->tail; i < as->head; ++i) job_free(as->fifo[i % AS_MAX]);
 	job_free(as->cur);
@@ -435,37 +451,90 @@ static void job_put(struct h264_async *as, h264_job_t *j)
 }
 
 /* ---------------------------------------------------------------- API context: submission */
-/* Submission runs on the caller's thread, in decode order ([tail, sub) submitted).  Without bind a
- * job is submitted once the API context closed it: its virtual ids are translated to the frame slots
- * of that moment (j->map) and it retires at once.  With bind (decode ahead) a parsed job is submitted
- * as it is, virtual ids naming the back end's buffers, possibly before the API context reached it;
- * the API context's close binds its buffer to the frame slot it chose, and the job retires then. */
+/* Submission is in decode order ([tail, sub) submitted, [tail, bnd) bound).
+ *
+ * Without bind (back ends that only take frame slots) it runs on the caller's thread: a job goes to
+ * the back end once the API context closed it, its virtual ids translated to the frame slots of
+ * that moment (j->map), and retires at once.
+ *
+ * With bind (decode ahead) a submitter thread owns every back-end call but sync_frame: it submits
+ * each parsed job as it is, virtual ids naming the back end's picture buffers, as soon as the rules
+ * below allow — possibly long before the API context reaches it — and binds closed jobs' buffers to
+ * the frame slots the API context chose, in order.  The caller's thread only closes pictures and,
+ * to hand a frame out, waits until its job is bound (h264_async_drain) before sync_frame.  The record
+ * copies and the HIP calls leave the caller's thread, the one serial stage of the pipeline. */
 
-static int bind_job(h264_dec_t *d, h264_job_t *j)
+/* records into the back end's arena (virtual ids as they are, or translated to slots) + submit */
+static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 {
-	j->bound = 1;
-	return d->backend.bind(d->backend.self, j->vid & 63, j->slot) < 0 ? -1 : 0;
-}
-
-/* recycle submitted jobs from the tail, in order, once the pipeline no longer needs them */
-static void retire(struct h264_async *as)
-{
-	while (as->tail < as->sub) {
-		h264_job_t *j = as->fifo[as->tail % AS_MAX];
-		if (as->ahead && !j->bound) return;
-		pthread_mutex_lock(&as->mu);
-		as->tail++; /* workers scan [tail, head) under the mutex */
-		pthread_mutex_unlock(&as->mu);
-		job_put(as, j);
+	struct h264_async *as = d->as;
+	const m2r_picture_t *src = &j->pic;
+	const int n = src->width_mbs * src->height_mbs;
+	double t1 = as->stats ? now_s() : 0;
+	m2r_picture_t *dst = d->backend.acquire(d->backend.self, src->width_mbs, src->height_mbs);
+	if (!dst || dst->cap_slices < src->n_slices || dst->cap_inter < src->n_inter || dst->cap_coef < src->n_coef) return 1;
+	dst->slot = virt ? (j->vid & 63) : j->slot;
+	dst->flags = virt ? M2R_PIC_VIRTUAL : 0;
+	dst->n_inter = src->n_inter;
+	dst->n_coef = src->n_coef;
+	dst->n_slices = src->n_slices;
+	dst->n_intra = src->n_intra;
+	dst->deblock = src->deblock;
+	memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
+	memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);
+	memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
+	if (virt) {
+		memcpy(dst->inter, src->inter, sizeof(m2r_inter_t) * (size_t)src->n_inter);
+	} else {
+		for (int i = 0; i < src->n_inter; ++i) {
+			const m2r_inter_t *si = &src->inter[i];
+			m2r_inter_t *di = &dst->inter[i];
+			memcpy(di->mv, si->mv, sizeof(di->mv));
+			memcpy(di->refidx, si->refidx, sizeof(di->refidx));
+			for (int k = 0; k < 8; ++k) {
+				const int v = (&si->slot[0][0])[k];
+				(&di->slot[0][0])[k] = (int8_t)(v < 0 ? -1 : j->map[v & 63]);
+			}
+		}
 	}
+	memcpy(dst->coef, src->coef, sizeof(int16_t) * (size_t)src->n_coef);
+	if (as->stats) {
+		const double t2 = now_s();
+		as->t_copy += t2 - t1;
+		t1 = t2;
+	}
+	const int err = d->backend.submit(d->backend.self, dst) < 0;
+	if (as->stats) as->t_submit += now_s() - t1;
+	return err;
 }
 
+/* ---- without bind: the caller's thread */
+static int submit_next(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	h264_job_t *j = as->fifo[as->sub % AS_MAX];
+	const double t0 = as->stats ? now_s() : 0;
+	int err;
+	pthread_mutex_lock(&as->mu);
+	while (!j->done) pthread_cond_wait(&as->cv_done, &as->mu);
+	pthread_mutex_unlock(&as->mu);
+	if (as->stats) as->t_done_wait += now_s() - t0;
+	err = j->err || copy_submit(d, j, 0);
+	pthread_mutex_lock(&as->mu);
+	as->sub++;
+	as->tail++; /* workers scan [tail, head) under the mutex */
+	job_put(as, j);
+	pthread_mutex_unlock(&as->mu);
+	return err ? -1 : 0;
+}
+
+/* ---- decode ahead: the submitter thread */
 /* a parsed job the API context has not closed yet may go to the back end now: no header callback
- * (set_frames) the API context has not run yet lies before it, and the previous picture in its
- * virtual buffer was bound already (so the back end orders the overwrite after that copy-out) */
+ * (set_frames) the API context has not run yet lies before it, and the previous picture of its
+ * virtual buffer is bound (so the back end orders the overwrite after that copy-out).  Mutex held. */
 static int ahead_ok(const struct h264_async *as, const h264_job_t *j)
 {
-	if (j->err || j->sps_nal >= as->nq_tail) return 0;
+	if (j->err || j->sps_nal > as->api_sps_nal) return 0;
 	for (long i = as->tail; i < j->seq; ++i) {
 		const h264_job_t *o = as->fifo[i % AS_MAX];
 		if (o->vid == j->vid && !o->bound) return 0;
@@ -473,102 +542,116 @@ static int ahead_ok(const struct h264_async *as, const h264_job_t *j)
 	return 1;
 }
 
-/* copy the next job's records into the back end's arena and submit it (waits for its parse) */
-static int submit_next(h264_dec_t *d)
+static void *submitter(void *arg)
 {
+	h264_dec_t *d = (h264_dec_t *)arg;
 	struct h264_async *as = d->as;
-	h264_job_t *j = as->fifo[as->sub % AS_MAX];
-	m2r_picture_t *dst;
-	const m2r_picture_t *src = &j->pic;
-	const int virt = as->ahead;
-	int n, err;
-	double t0 = as->stats ? now_s() : 0, t1 = 0;
 	pthread_mutex_lock(&as->mu);
-	while (!j->done) pthread_cond_wait(&as->cv_done, &as->mu);
-	pthread_mutex_unlock(&as->mu);
-	as->sub++;
-	if (as->stats) {
-		t1 = now_s();
-		as->t_done_wait += t1 - t0;
-	}
-	err = j->err;
-	if (!err) {
-		n = src->width_mbs * src->height_mbs;
-		dst = d->backend.acquire(d->backend.self, src->width_mbs, src->height_mbs);
-		if (!dst || dst->cap_slices < src->n_slices || dst->cap_inter < src->n_inter || dst->cap_coef < src->n_coef) {
-			err = 1;
-		} else {
-			dst->slot = virt ? (j->vid & 63) : j->slot;
-			dst->flags = virt ? M2R_PIC_VIRTUAL : 0;
-			dst->n_inter = src->n_inter;
-			dst->n_coef = src->n_coef;
-			dst->n_slices = src->n_slices;
-			dst->n_intra = src->n_intra;
-			dst->deblock = src->deblock;
-			memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
-			memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);
-			memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
-			if (virt) {
-				memcpy(dst->inter, src->inter, sizeof(m2r_inter_t) * (size_t)src->n_inter);
-			} else {
-				for (int i = 0; i < src->n_inter; ++i) {
-					const m2r_inter_t *si = &src->inter[i];
-					m2r_inter_t *di = &dst->inter[i];
-					memcpy(di->mv, si->mv, sizeof(di->mv));
-					memcpy(di->refidx, si->refidx, sizeof(di->refidx));
-					for (int k = 0; k < 8; ++k) {
-						const int v = (&si->slot[0][0])[k];
-						(&di->slot[0][0])[k] = (int8_t)(v < 0 ? -1 : j->map[v & 63]);
-					}
-				}
+	while (!as->sub_quit) {
+		if (as->bnd < as->sub && as->bnd < as->a_seq) {
+			/* bind the oldest closed, submitted job; retire what is bound */
+			h264_job_t *j = as->fifo[as->bnd % AS_MAX];
+			const int skip = j->sub_err, vid = j->vid & 63, slot = j->slot;
+			pthread_mutex_unlock(&as->mu);
+			const int err = !skip && d->backend.bind(d->backend.self, vid, slot) < 0;
+			pthread_mutex_lock(&as->mu);
+			j->bound = 1;
+			as->sub_err += err;
+			as->bnd++;
+			while (as->tail < as->bnd) {
+				h264_job_t *o = as->fifo[as->tail % AS_MAX];
+				as->tail++;
+				job_put(as, o);
 			}
-			memcpy(dst->coef, src->coef, sizeof(int16_t) * (size_t)src->n_coef);
-			if (as->stats) {
-				const double t2 = now_s();
-				as->t_copy += t2 - t1;
-				t1 = t2;
-			}
-			if (virt && j->slot < 0) d->ahead_submits++;
-			err = d->backend.submit(d->backend.self, dst) < 0;
-			if (as->stats) as->t_submit += now_s() - t1;
+			pthread_cond_broadcast(&as->cv_done);
+			continue;
 		}
+		if (as->sub < as->head) {
+			/* submit the next parsed job: closed, or allowed ahead */
+			h264_job_t *j = as->fifo[as->sub % AS_MAX];
+			if (j->done && (as->sub < as->a_seq || ahead_ok(as, j))) {
+				const int ahead = as->sub >= as->a_seq;
+				pthread_mutex_unlock(&as->mu);
+				const int err = j->err || copy_submit(d, j, 1);
+				pthread_mutex_lock(&as->mu);
+				j->sub_err = err;
+				j->submitted = 1;
+				as->sub_err += err;
+				as->sub++;
+				d->ahead_submits += ahead && !err;
+				pthread_cond_broadcast(&as->cv_done);
+				continue;
+			}
+		}
+		pthread_cond_wait(&as->cv_done, &as->mu);
 	}
-	j->submitted = 1;
-	if (!err && virt && j->slot >= 0) err = bind_job(d, j) < 0;
-	if (err) j->bound = 1; /* nothing to bind: the error is reported now */
-	retire(as);
-	return err ? -1 : 0;
+	pthread_mutex_unlock(&as->mu);
+	return NULL;
 }
 
-/* submit every closed job up to and including the newest one that writes `slot` (-1: all) */
+/* a submission or bind failed since the last call: report it once (mutex held) */
+static int take_error(struct h264_async *as)
+{
+	const int e = as->sub_err;
+	as->sub_err = 0;
+	return e ? -1 : 0;
+}
+
+/* every closed job up to and including the newest one that writes `slot` (-1: all) is submitted —
+ * and, decoding ahead, bound to its slot */
 int h264_async_drain(h264_dec_t *d, int slot)
 {
 	struct h264_async *as = d->as;
 	long upto = -1;
 	if (!as) return 0;
+	if (!as->ahead) {
+		for (long i = as->tail; i < as->a_seq; ++i)
+			if (slot < 0 || as->fifo[i % AS_MAX]->slot == slot) upto = i;
+		while (as->sub <= upto)
+			if (submit_next(d) < 0) return -1;
+		return 0;
+	}
+	const double t0 = as->stats ? now_s() : 0;
+	pthread_mutex_lock(&as->mu);
 	for (long i = as->tail; i < as->a_seq; ++i)
 		if (slot < 0 || as->fifo[i % AS_MAX]->slot == slot) upto = i;
-	while (as->sub <= upto)
-		if (submit_next(d) < 0) return -1;
-	return 0;
+	while (as->bnd <= upto) pthread_cond_wait(&as->cv_done, &as->mu);
+	const int err = take_error(as);
+	pthread_mutex_unlock(&as->mu);
+	if (as->stats) as->t_done_wait += now_s() - t0;
+	return err;
 }
 
-/* submit, in order and without waiting, parsed jobs that are closed (or may go ahead) */
+/* without bind: submit, in order and without waiting, closed jobs whose parse finished.  Decoding
+ * ahead the submitter does that; report its errors */
 static int submit_ready(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
-	for (;;) {
-		h264_job_t *j;
-		int ready;
-		if (as->sub >= as->head) return 0;
-		j = as->fifo[as->sub % AS_MAX];
+	if (as->ahead) {
 		pthread_mutex_lock(&as->mu);
-		ready = j->done;
+		const int err = take_error(as);
+		pthread_mutex_unlock(&as->mu);
+		return err;
+	}
+	for (;;) {
+		int ready;
+		if (as->sub >= as->a_seq) return 0;
+		pthread_mutex_lock(&as->mu);
+		ready = as->fifo[as->sub % AS_MAX]->done;
 		pthread_mutex_unlock(&as->mu);
 		if (!ready) return 0;
-		if (as->sub >= as->a_seq && (!as->ahead || !ahead_ok(as, j))) return 0;
 		if (submit_next(d) < 0) return -1;
 	}
+}
+
+/* the API context ran the header callback of the SPS it just read: pictures after it may go ahead */
+void h264_async_api_sps(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	pthread_mutex_lock(&as->mu);
+	as->api_sps_nal = as->nq_tail - 1;
+	pthread_cond_broadcast(&as->cv_done);
+	pthread_mutex_unlock(&as->mu);
 }
 
 /* ---------------------------------------------------------------- lookahead context */
@@ -585,13 +668,21 @@ static void pump(h264_dec_t *d, int until_nal)
 			break;
 		}
 		/* job slots: submit what the API context closed before dispatching more */
-		retire(as);
-		while (as->head - as->tail >= AS_MAX - 2 && as->sub < as->a_seq)
-			if (submit_next(d) < 0) {
-				as->la_done = as->la_err = 1;
-				break;
-			}
-		if (as->head - as->tail >= AS_MAX - 2) break;
+		if (as->ahead) {
+			int full;
+			pthread_mutex_lock(&as->mu);
+			while (as->head - as->tail >= AS_MAX - 2 && as->tail < as->a_seq) pthread_cond_wait(&as->cv_done, &as->mu);
+			full = as->head - as->tail >= AS_MAX - 2;
+			pthread_mutex_unlock(&as->mu);
+			if (full) break;
+		} else {
+			while (as->head - as->tail >= AS_MAX - 2 && as->sub < as->a_seq)
+				if (submit_next(d) < 0) {
+					as->la_done = as->la_err = 1;
+					break;
+				}
+			if (as->head - as->tail >= AS_MAX - 2) break;
+		}
 		const int r = h264_decode_loop(as->la);
 		if (r == -2) as->la_done = 1;
 		else if (r < 0) as->la_done = as->la_err = 1;
@@ -684,7 +775,9 @@ int h264_async_add_slice(h264_dec_t *la)
 	h264_job_t *j = as->cur;
 	const double ts = as->stats ? now_s() : 0;
 	if (!j) {
+		pthread_mutex_lock(&as->mu); /* (the submitter thread recycles jobs) */
 		j = job_get(as);
+		pthread_mutex_unlock(&as->mu);
 		if (!j || job_arena(j, la->mb_w, la->mb_h) < 0) return -1;
 		j->vid = la->curr_idx;
 		j->slot = -1;
@@ -725,7 +818,7 @@ int h264_async_add_slice(h264_dec_t *la)
 }
 
 /* a store buffer no job can still use (a spare unmapped before every unsubmitted job), or a new one */
-static h264_colmb_t *col_spare_get(struct h264_async *as, int n_mbs)
+static h264_colmb_t *col_spare_get(struct h264_async *as, int n_mbs, long tail)
 {
 	if (as->col_n != (size_t)n_mbs) { /* new geometry (no job in flight, h264_async_sps) */
 		for (int i = 0; i < as->nspare; ++i) free(as->spare[i].mb);
@@ -733,7 +826,7 @@ static h264_colmb_t *col_spare_get(struct h264_async *as, int n_mbs)
 		as->col_n = (size_t)n_mbs;
 	}
 	for (int i = 0; i < as->nspare; ++i)
-		if (as->spare[i].unmap_seq <= as->tail) {
+		if (as->spare[i].unmap_seq <= tail) {
 			h264_colmb_t *b = as->spare[i].mb;
 			as->spare[i] = as->spare[--as->nspare];
 			return b;
@@ -778,9 +871,13 @@ static int la_close(h264_dec_t *la)
 	if (!j->nonref) {
 		const int c = j->col_store;
 		const long last = as->col_last[c];
-		if (last >= as->tail) {
+		long tail;
+		pthread_mutex_lock(&as->mu); /* (the submitter thread moves the tail) */
+		tail = as->tail;
+		pthread_mutex_unlock(&as->mu);
+		if (last >= tail) {
 			const double tw = as->stats ? now_s() : 0;
-			h264_colmb_t *nb = col_spare_get(as, la->n_mbs);
+			h264_colmb_t *nb = col_spare_get(as, la->n_mbs, tail);
 			if (nb) {
 				if (as->nspare < 64) {
 					as->spare[as->nspare].mb = la->colpic[c].mb;
@@ -840,10 +937,13 @@ static int api_close(h264_dec_t *d)
 	if (h264_picture_mark(d) < 0) return -1;
 	as->vmap[j->vid & 63] = (int8_t)d->curr_idx;
 	memcpy(j->map, as->vmap, sizeof(j->map));
+	pthread_mutex_lock(&as->mu);
+	if (as->ahead && as->ahead_all)
+		while (!j->submitted && !(j->done && j->err)) pthread_cond_wait(&as->cv_done, &as->mu);
 	j->slot = d->curr_idx;
 	as->a_seq++;
-	if (j->submitted && !j->bound && bind_job(d, j) < 0) return -1; /* decoded ahead: now it has a slot */
-	retire(as);
+	pthread_cond_broadcast(&as->cv_done); /* (decode ahead: the submitter binds it) */
+	pthread_mutex_unlock(&as->mu);
 	pump(d, 0);
 	if (submit_ready(d) < 0) return -1;
 	return 1;

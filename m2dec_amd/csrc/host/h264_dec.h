@@ -7,10 +7,12 @@
 #ifndef M2DEC_AMD_H264_DEC_H
 #define M2DEC_AMD_H264_DEC_H
 
+#include <pthread.h>
 #include <stdint.h>
 #include <string.h>
 #include "m2d.h"
 #include "m2d_recon.h"
+#include "m2dec_amd.h"
 #include "h264_spec_tables.h"
 
 #ifdef __cplusplus
@@ -259,6 +261,24 @@ typedef struct {
 /* ---------------------------------------------------------------- decoder context */
 typedef struct h264_dec h264_dec_t;
 
+/* Frames the caller still reads after handing them back to the decoder (the MD5 threads of
+ * m2dec_amd_decode_stream_md5 hash the caller's frame buffers in place): the frame LRU skips them
+ * (find_empty_frame) and the driver frees frame memory only once none is held. */
+typedef struct m2dec_hold {
+	pthread_mutex_t mu;
+	pthread_cond_t cv;
+	const uint8_t *luma[64];
+	int cnt[64];
+	int n;
+	long waits;   /* times the frame LRU waited for a release */
+} m2dec_hold_t;
+void m2dec_hold_init(m2dec_hold_t *h);
+void m2dec_hold_destroy(m2dec_hold_t *h);
+void m2dec_hold_add(m2dec_hold_t *h, const uint8_t *luma);
+void m2dec_hold_release(m2dec_hold_t *h, const uint8_t *luma);
+void m2dec_hold_wait_idle(m2dec_hold_t *h);
+int m2dec_hold_busy(const m2dec_hold_t *h, const uint8_t *luma); /* h->mu held */
+
 struct h264_dec {
 	/* input */
 	dec_bits stream_i;
@@ -325,6 +345,7 @@ struct h264_dec {
 
 	/* parse-ahead pipeline (h264_async.c); NULL: slice data parsed on the caller's thread */
 	struct h264_async *as;
+	m2dec_hold_t *hold;      /* frames the caller holds (NULL: none) */
 	int parse_threads;       /* requested workers (m2dec_amd_h264_set_parse_threads / env) */
 	/* 1: this is the pipeline's lookahead context: it runs the header-level state machine ahead of
 	 * the API-visible context, names pictures by virtual frame ids instead of frame slots (no DPB
@@ -360,6 +381,7 @@ void h264_async_stop(h264_dec_t *d);
 int h264_async_nal_next(h264_dec_t *d);
 void h264_async_resume(h264_dec_t *d);
 void h264_async_la_sps(h264_dec_t *la);
+void h264_async_api_sps(h264_dec_t *d);
 int h264_async_sps(h264_dec_t *d);
 int h264_async_push_nal(h264_dec_t *la);
 
@@ -368,6 +390,9 @@ int h264_nal_next(h264_dec_t *d);
 
 /* h264_api.c: the NAL loop of decode_picture, shared by the API context and the lookahead context */
 int h264_decode_loop(h264_dec_t *d);
+int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                            int parse_threads, int extra, m2dec_hold_t *hold,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats);
 
 #ifdef __cplusplus
 }

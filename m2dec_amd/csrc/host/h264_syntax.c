@@ -323,6 +323,34 @@ static void find_empty_frame(h264_dec_t *d)
 		if (d->refs[0][i].in_use) d->lru[d->refs[0][i].frame_idx] = 0;
 		if (d->refs[1][i].in_use) d->lru[d->refs[1][i].frame_idx] = 0;
 	}
+	if (d->hold) {
+		/* frames the caller still holds are skipped; when only frames in use (lru 0) are left, wait for
+		 * a release rather than take one (with none held: the reference's choice below) */
+		m2dec_hold_t *h = d->hold;
+		pthread_mutex_lock(&h->mu);
+		for (;;) {
+			int held = 0;
+			max_idx = 0;
+			max_val = -1;
+			for (int i = 0; i < d->num_frames; ++i) {
+				if (m2dec_hold_busy(h, d->frames[i].luma)) {
+					held = 1;
+					continue;
+				}
+				if (max_val < d->lru[i]) {
+					max_val = d->lru[i];
+					max_idx = i;
+				}
+			}
+			if (!held || max_val > 0) break;
+			h->waits++;
+			pthread_cond_wait(&h->cv, &h->mu);
+		}
+		pthread_mutex_unlock(&h->mu);
+		d->lru[max_idx] = 0;
+		d->curr_idx = max_idx;
+		return;
+	}
 	for (int i = 0; i < d->num_frames; ++i) {
 		if (max_val < d->lru[i]) {
 			max_val = d->lru[i];

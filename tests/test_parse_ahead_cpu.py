@@ -69,17 +69,41 @@ def test_output_calls_match_any_caller_pattern(built, threads, dpb, emptify):
         assert sorted(got) == sorted(GOLDEN[name]["md5"])
 
 
-def test_decode_ahead(built, monkeypatch):
+@pytest.mark.parametrize("name", ["c2_720p_s1", "cov_cabac_s1", "cov_slices_s1", "cov_tools_cavlc_s1"])
+def test_decode_ahead(built, monkeypatch, name):
     """Back ends with bind (the oracle's, like the HIP one) get pictures as soon as they are parsed,
-    named by virtual ids, before the API context reaches them (Stats.ahead counts those); the frames
-    are the same with decode-ahead off (M2DEC_AMD_NO_AHEAD: submission in API order, slots translated)."""
-    name = "c2_720p_s1"
+    named by virtual ids, from a submitter thread, before the API context reaches them (Stats.ahead
+    counts those; M2DEC_AMD_AHEAD_ALL makes every picture go ahead, whatever the thread timing); the
+    frames are the same with decode-ahead off (M2DEC_AMD_NO_AHEAD: submission in API order on the
+    caller's thread, slots translated)."""
+    monkeypatch.setenv("M2DEC_AMD_AHEAD_ALL", "1")
     st = m2dec_amd.Stats()
     with OracleBackend() as ob:
         got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=4, stats=st)
-    assert got == GOLDEN[name]["md5"] and st.ahead > 0
+    assert got == GOLDEN[name]["md5"] and st.ahead == st.pictures
+    monkeypatch.delenv("M2DEC_AMD_AHEAD_ALL")
     monkeypatch.setenv("M2DEC_AMD_NO_AHEAD", "1")
     st = m2dec_amd.Stats()
     with OracleBackend() as ob:
         got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=4, stats=st)
     assert got == GOLDEN[name]["md5"] and st.ahead == 0
+
+
+@pytest.mark.parametrize("extra", [None, "0"])
+@pytest.mark.parametrize("threads", [0, 4])
+@pytest.mark.parametrize("name", ["c2_720p_s1", "cov_slices_s1"])
+def test_md5_driver_holds_frames(built, monkeypatch, name, threads, extra):
+    """The throughput driver (m2dec_amd_decode_stream_md5): frames hashed in place on helper threads,
+    16 side by side, while the decoder keeps going — held frames are not reused until released
+    (m2dec_hold_t), so the MD5 lines equal the goldens, in output order.  With no spare frames
+    (M2DEC_AMD_MD5_EXTRA=0) the frame LRU has to wait for releases."""
+    if extra is not None:  # and slow MD5 threads: frames stay held
+        monkeypatch.setenv("M2DEC_AMD_MD5_EXTRA", extra)
+        monkeypatch.setenv("M2DEC_AMD_MD5_DELAY_US", "1500000")
+    st = m2dec_amd.Stats()
+    with OracleBackend() as ob:
+        got = m2dec_amd.decode_stream_md5_backend(stream(name), ob.be, parse_threads=threads,
+                                                  md5_threads=1 if extra else 2, stats=st)
+    assert got == GOLDEN[name]["md5"]
+    if extra is not None and name == "c2_720p_s1":  # (cov_slices_s1 has fewer pictures than frames)
+        assert st.hold_waits > 0

@@ -6,7 +6,9 @@ ARCH ?= gfx950
 JOBS ?= 8
 
 INC := -Iinclude -Im2dec_amd/csrc/host
-CFLAGS := -O3 -g -fPIC -Wall -Wextra -Wno-unused-parameter -std=gnu11 $(INC)
+# host code: x86-64-v3 (AVX2 / BMI2 / LZCNT: every MI355X host CPU, EPYC Zen 4/5) — ~9 % faster CABAC parse
+HOST_ARCH ?= -march=x86-64-v3
+CFLAGS := -O3 -g -fPIC $(HOST_ARCH) -Wall -Wextra -Wno-unused-parameter -std=gnu11 $(INC)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -g -fPIC -std=c++17 $(INC) -Wno-unused-result
 
 HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)

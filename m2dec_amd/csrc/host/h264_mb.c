@@ -1143,6 +1143,16 @@ static int uniform_motion(const h264_mbinfo_t *q)
 	return 1;
 }
 
+/* luma blocks with coefficients, raster bit y * 4 + x */
+static inline uint32_t nz_raster(const h264_mbinfo_t *m)
+{
+	uint32_t r = 0;
+	for (int b = 0; b < 16; ++b) r |= (uint32_t)(m->nnz[b] != 0) << (blk_y[b] * 4 + blk_x[b]);
+	return r;
+}
+
+static inline int b8_of(int r) { return ((r >> 3) << 1) | ((r & 3) >> 1); }
+
 static void compute_bs(slice_ctx_t *s)
 {
 	h264_mbinfo_t *q = s->cur;
@@ -1156,37 +1166,50 @@ static void compute_bs(slice_ctx_t *s)
 		flags = M2R_DBK_LEFT_BS4 | M2R_DBK_TOP_BS4;
 	} else {
 		const int t8 = q->t8x8, uni = uniform_motion(q);
+		const uint32_t nzq = nz_raster(q);
+		uint32_t mvw[2][16];
+		memcpy(mvw, q->mv, sizeof(mvw));
 		for (int dir = 0; dir < 2; ++dir) {
 			uint32_t str = 0;
-			for (int e = 0; e < 4; ++e) {
-				if (e != 0 && t8 && (e & 1)) continue;
+			/* MB edge: the left / top neighbour */
+			const h264_mbinfo_t *p = NULL;
+			if (dir == 0 && s->mbx != 0) p = &s->d->mbi[s->addr - 1];
+			if (dir == 1 && s->mby != 0) p = &s->d->mbi[s->addr - s->d->mb_w];
+			if (p && is_intra_type(p->type)) {
+				flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
+				str = 0xaa; /* 2 in every segment (the flag makes it 4) */
+			} else if (p) {
 				for (int sgm = 0; sgm < 4; ++sgm) {
-					/* dir 0: vertical edge x = e, row sgm ; dir 1: horizontal edge y = e, column sgm */
-					int qx = dir ? sgm : e, qy = dir ? e : sgm;
-					const h264_mbinfo_t *p;
-					int px, py, v = 0;
-					if (e == 0) {
-						if (dir == 0) {
-							if (s->mbx == 0) continue;
-							p = &s->d->mbi[s->addr - 1];
-							px = 3; py = qy;
-						} else {
-							if (s->mby == 0) continue;
-							p = &s->d->mbi[s->addr - s->d->mb_w];
-							px = qx; py = 3;
-						}
-						if (is_intra_type(p->type)) {
-							flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
-							v = 2;
-						}
+					const int qx = dir ? sgm : 0, qy = dir ? 0 : sgm, px = dir ? qx : 3, py = dir ? 3 : qy;
+					int v;
+					const int qr = qy * 4 + qx, pr = py * 4 + px, bq = b8_of(qr), bp = b8_of(pr);
+					if (((nzq >> qr) & 1) || p->nnz[rast2blk[pr]]) v = 2;
+					else if (q->fidx[0][bq] == p->fidx[0][bp] && q->fidx[1][bq] == p->fidx[1][bp] &&
+					         !memcmp(q->mv[0][qr], p->mv[0][pr], 4) && !memcmp(q->mv[1][qr], p->mv[1][pr], 4))
+						v = 0;
+					else v = bs_motion(q, qx, qy, p, px, py);
+					str |= (uint32_t)v << (sgm * 2);
+				}
+			}
+			/* inner edges: blocks of the same MB; identical motion (the common case inside a partition)
+			 * is bS 0 without the full test */
+			for (int e = 1; e < 4; ++e) {
+				if (t8 && (e & 1)) continue;
+				for (int sgm = 0; sgm < 4; ++sgm) {
+					const int qx = dir ? sgm : e, qy = dir ? e : sgm;
+					const int qr = qy * 4 + qx, pr = dir ? qr - 4 : qr - 1;
+					int v;
+					if (((nzq >> qr) | (nzq >> pr)) & 1) {
+						v = 2;
+					} else if (uni) {
+						v = 0;
 					} else {
-						p = q;
-						px = dir ? qx : qx - 1;
-						py = dir ? qy - 1 : qy;
-					}
-					if (!v) {
-						if (q->nnz[rast2blk[qy * 4 + qx]] || p->nnz[rast2blk[py * 4 + px]]) v = 2;
-						else if ((p != q || !uni) && bs_motion(q, qx, qy, p, px, py)) v = 1;
+						const int bq = b8_of(qr), bp = b8_of(pr);
+						if (q->fidx[0][bq] == q->fidx[0][bp] && q->fidx[1][bq] == q->fidx[1][bp] && mvw[0][qr] == mvw[0][pr] &&
+						    mvw[1][qr] == mvw[1][pr])
+							v = 0;
+						else
+							v = bs_motion(q, qx, qy, q, dir ? qx : qx - 1, dir ? qy - 1 : qy);
 					}
 					str |= (uint32_t)v << (e * 8 + sgm * 2);
 				}

@@ -21,8 +21,11 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 32        /* frames queued or being hashed; the decoder gets as many extra frames */
+#define MD5_RING 40        /* frames queued or being hashed; the decoder gets as many extra frames */
 #define MD5_BATCH 16       /* frames one thread hashes together (m2dec_amd_frames_md5 lanes) */
+#define MD5_MIN_BATCH 8    /* a batch costs about the same CPU time for 2 or 16 frames: a thread waits for
+                              this many (or MD5_WAIT_S after the oldest was queued, or the end) */
+#define MD5_WAIT_S 0.004
 #define MD5_THREADS_MAX 16
 #define MD5_THREADS 2      /* one stream: a 16-frame batch of 1080p takes one core ~4 ms, so two threads
                               keep up with the decoder; M2DEC_AMD_MD5_THREADS overrides */
@@ -37,6 +40,7 @@ typedef struct {
 	m2dec_hold_t hold;
 	m2d_frame_t frm[MD5_RING];
 	int idx[MD5_RING];       /* output frame number of the job in slot k */
+	double t_queued[MD5_RING];
 	int state[MD5_RING];     /* 0 free, 1 queued, 2 being hashed */
 	int head, next;          /* slots filled / taken by a hashing thread, in order */
 	int quit;
@@ -46,6 +50,8 @@ typedef struct {
 	int stats;
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	double t_wait;           /* caller: waiting for a free queue slot */
+	double t_hash;           /* MD5 threads: time hashing */
+	long batches;
 	double t_done;           /* the last MD5 line written */
 } md5_pipe_t;
 
@@ -64,6 +70,17 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
+		while (!p->quit && p->head - p->next < MD5_MIN_BATCH) {
+			const double left = p->t_queued[p->next % MD5_RING] + MD5_WAIT_S - now_s();
+			struct timespec ts;
+			if (left <= 0) break;
+			clock_gettime(CLOCK_REALTIME, &ts);
+			ts.tv_nsec += (long)(left * 1e9);
+			ts.tv_sec += ts.tv_nsec / 1000000000L;
+			ts.tv_nsec %= 1000000000L;
+			pthread_cond_timedwait(&p->cv_job, &p->mu, &ts);
+		}
+		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		int ks[MD5_BATCH], ix[MD5_BATCH], n = 0;
 		while (n < MD5_BATCH && p->next < p->head) {
@@ -77,13 +94,17 @@ static void *md5_worker(void *arg)
 		pthread_mutex_unlock(&p->mu);
 		if (p->delay_us) usleep((useconds_t)p->delay_us); /* (tests: MD5 slower than the decoder) */
 		char lines[MD5_BATCH][35];
+		const double th = now_s();
 		m2dec_amd_frames_md5(f, n, lines);
+		const double th1 = now_s();
 		for (int j = 0; j < n; ++j) {
 			if (ix[j] < p->max) memcpy(p->md5s + (size_t)ix[j] * 35, lines[j], 35);
 			m2dec_hold_release(&p->hold, f[j].luma);
 		}
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
+		p->t_hash += th1 - th;
+		p->batches++;
 		if (t > p->t_done) p->t_done = t;
 		for (int j = 0; j < n; ++j) p->state[ks[j]] = 0;
 		pthread_cond_broadcast(&p->cv_free);
@@ -104,9 +125,20 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	if (p->stats) p->t_wait += now_s() - t0;
 	p->frm[k] = *f;
 	p->idx[k] = p->n++;
+	p->t_queued[k] = now_s();
 	p->state[k] = 1;
 	p->head++;
-	pthread_cond_signal(&p->cv_job);
+	pthread_cond_broadcast(&p->cv_job);
+	pthread_mutex_unlock(&p->mu);
+}
+
+/* the stream's last frame was queued: hash what is left at once */
+static void md5_on_end(void *arg)
+{
+	md5_pipe_t *p = (md5_pipe_t *)arg;
+	pthread_mutex_lock(&p->mu);
+	p->quit = 1;
+	pthread_cond_broadcast(&p->cv_job);
 	pthread_mutex_unlock(&p->mu);
 }
 
@@ -149,13 +181,15 @@ static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *back
 	memset(&st, 0, sizeof(st));
 	const char *ex = getenv("M2DEC_AMD_MD5_EXTRA"); /* (tests: fewer spare frames -> the decoder waits on holds) */
 	r = h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, ex ? atoi(ex) : MD5_RING, &p.hold,
-	                            md5_on_frame, &p, &st);
+	                            md5_on_frame, md5_on_end, &p, &st);
 	pthread_mutex_lock(&p.mu);
-	p.quit = 1;
+	p.quit = 1; /* (already set by md5_on_end unless the decode failed early) */
 	pthread_cond_broadcast(&p.cv_job);
 	pthread_mutex_unlock(&p.mu);
 	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
-	if (p.stats) fprintf(stderr, "md5: caller waits %.3f s, frame LRU waits %ld (%d threads)\n", p.t_wait, p.hold.waits, nth);
+	if (p.stats)
+		fprintf(stderr, "md5: caller waits %.3f s, frame LRU waits %ld, %d frames in %ld batches, hashing %.3f s (%d threads)\n",
+		        p.t_wait, p.hold.waits, p.n, p.batches, p.t_hash, nth);
 	m2dec_hold_destroy(&p.hold);
 	if (p.t_done > st.t_end) st.t_end = p.t_done; /* delivered = its MD5 line written */
 	st.hold_waits = p.hold.waits;

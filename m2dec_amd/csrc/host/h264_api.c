@@ -490,14 +490,16 @@ int m2dec_amd_decode_stream3(const uint8_t *data, size_t len, const m2r_backend_
                              int parse_threads, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg,
                              m2dec_amd_stats_t *stats)
 {
-	return h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, 0, NULL, on_frame, arg, stats);
+	return h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, 0, NULL, on_frame, NULL, arg, stats);
 }
 
 /* the stream driver; `hold`: on_frame may keep reading a frame after it returns until it releases it
- * from `hold` (the frame is not reused meanwhile), with `extra` more frames than the decoder needs */
+ * from `hold` (the frame is not reused meanwhile), with `extra` more frames than the decoder needs;
+ * on_end (optional): called after the last frame, before the held frames are waited for */
 int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
                             int parse_threads, int extra, m2dec_hold_t *hold,
-                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats)
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void (*on_end)(void *arg), void *arg,
+                            m2dec_amd_stats_t *stats)
 {
 	driver_t v;
 	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
@@ -551,6 +553,7 @@ int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t
 		}
 	}
 done:
+	if (on_end) on_end(arg);
 	if (d->stats) fprintf(stderr, "stream: %d frames, %.3f s\n", n, mono_s() - t_start);
 	if (stats && !backend && d->have_backend) {
 		m2dec_amd_hip_timing_t t;

@@ -392,7 +392,8 @@ int h264_nal_next(h264_dec_t *d);
 int h264_decode_loop(h264_dec_t *d);
 int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
                             int parse_threads, int extra, m2dec_hold_t *hold,
-                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_amd_stats_t *stats);
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void (*on_end)(void *arg), void *arg,
+                            m2dec_amd_stats_t *stats);
 
 #ifdef __cplusplus
 }

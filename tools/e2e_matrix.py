@@ -3,6 +3,7 @@ MD5, decode with the MD5 threads — at a few parse-worker counts (M2DEC_AMD_PAR
 decoder).  Usage: python tools/e2e_matrix.py [workers ...]"""
 import ctypes
 import os
+import resource
 import sys
 import time
 
@@ -18,8 +19,24 @@ gold = GOLDEN["c3_1080p_s1"]["md5"]
 m2dec_amd.decode_stream_md5(data)
 
 
+def cpu_s():
+    r = resource.getrusage(resource.RUSAGE_SELF)
+    return r.ru_utime + r.ru_stime
+
+
 def best(fn, reps=4):
-    return max(fn() for _ in range(reps))
+    """best rate of `reps` runs, and the process CPU time per frame (ms) over them"""
+    c0 = cpu_s()
+    rates = [fn() for _ in range(reps)]
+    return max(rates), (cpu_s() - c0) / (60 * reps) * 1e3
+
+
+def throttled():
+    try:
+        st = dict(line.split() for line in open("/sys/fs/cgroup/cpu.stat"))
+        return int(st.get("nr_throttled", 0)), int(st.get("throttled_usec", 0))
+    except OSError:
+        return 0, 0
 
 
 for th in [int(x) for x in sys.argv[1:]] or [8, 12]:
@@ -46,5 +63,10 @@ for th in [int(x) for x in sys.argv[1:]] or [8, 12]:
         assert got == gold
         return len(got) / (st.t_end - st.t_start)
 
-    print(f"workers {th}: parse only {best(parse_only):.0f} fps, decode no MD5 {best(no_md5):.0f} fps, "
-          f"decode + MD5 {best(with_md5):.0f} fps", flush=True)
+    out = []
+    for name, fn in (("parse only", parse_only), ("decode no MD5", no_md5), ("decode + MD5", with_md5)):
+        t0 = throttled()
+        fps, cpu = best(fn)
+        t1 = throttled()
+        out.append(f"{name} {fps:.0f} fps ({cpu:.2f} CPU-ms/frame, throttled {t1[0] - t0[0]}x {(t1[1] - t0[1]) / 1e3:.0f} ms)")
+    print(f"workers {th}: " + ", ".join(out), flush=True)

@@ -2,7 +2,9 @@
 
 The generator (tools/h264gen) writes, next to each stream, a dump of what it encoded per
 macroblock: type, cbp, QP, intra modes, reference indices, motion vectors (exact in I/P pictures)
-and every coefficient level.  Here the stream is parsed by libm2dec_amd's host parser (with the
+and every coefficient level.  Direct-predicted blocks (B_Skip, B_Direct_16x16, direct sub-MBs)
+carry the generator's own spec restatement of spatial / temporal direct (8.4.1.2), so B-picture
+reference indices and vectors are compared like any other.  Here the stream is parsed by libm2dec_amd's host parser (with the
 CPU oracle as the back end so that decoding completes), the per-picture records are captured at
 submit time, and every field is compared with the dump.  This checks CABAC/CAVLC syntax decoding,
 scans, QP tracking, intra-mode and motion-vector prediction independently of reconstruction.
@@ -26,7 +28,7 @@ MB_DT = np.dtype([("kind", "u1"), ("cbp", "u1"), ("avail_luma", "u1"), ("avail_c
                   ("ipred", "<u4", 2), ("coef", "<u4"), ("nz", "<u4"), ("inter", "<u4")])
 INTER_DT = np.dtype([("mv", "<i2", (2, 16, 2)), ("slot", "i1", (2, 4)), ("refidx", "i1", (2, 4))])
 DUMP_DT = np.dtype([("pic", "<i4"), ("mbaddr", "<i4"), ("kind", "u1"), ("cbp", "u1"), ("qp", "i1"), ("t8x8", "u1"),
-                    ("exact_mv", "u1"), ("i16_pred", "u1"), ("cmode", "u1"), ("pad", "u1"), ("ipm", "i1", 16),
+                    ("exact_mv", "u1"), ("i16_pred", "u1"), ("cmode", "u1"), ("dir8", "u1"), ("ipm", "i1", 16),
                     ("ref", "i1", (2, 4)), ("mv", "<i2", (2, 16, 2)), ("ldc", "<i2", 16), ("luma", "<i2", 256),
                     ("cdc", "<i2", (2, 4)), ("cac", "<i2", (2, 4, 16))])
 assert MB_DT.itemsize == 32 and INTER_DT.itemsize == 144 and DUMP_DT.itemsize == 984
@@ -124,8 +126,9 @@ def _pool_blocks(rec, coef):
     return out
 
 
-def compare(pics, dump, max_errors=20):
+def compare(pics, dump, max_errors=20, stats=None):
     errs = []
+    stats = {"direct": 0, "mv": 0} if stats is None else stats
     kind_map = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: 4}
 
     def err(d, msg):
@@ -169,8 +172,8 @@ def compare(pics, dump, max_errors=20):
             for lx in range(2):
                 for b8 in range(4):
                     gref = int(d["ref"][lx][b8])
-                    if gref == -2:
-                        continue  # direct: decoder-derived
+                    if (int(d["dir8"]) >> b8) & 1:
+                        stats["direct"] += 1
                     used = int(I["slot"][lx][b8]) >= 0
                     if (gref >= 0) != used:
                         err(d, f"L{lx} 8x8 {b8}: used {used} vs generator ref {gref}")
@@ -179,6 +182,7 @@ def compare(pics, dump, max_errors=20):
                         if int(I["refidx"][lx][b8]) != gref:
                             err(d, f"L{lx} 8x8 {b8}: refidx {int(I['refidx'][lx][b8])} != {gref}")
                         if d["exact_mv"]:
+                            stats["mv"] += 1
                             for blk in range(4):
                                 x = (b8 & 1) * 2 + (blk & 1)
                                 y = (b8 >> 1) * 2 + (blk >> 1)

@@ -37,6 +37,26 @@ def test_parser_matches_generator_1080p(built, tmp_path):
     assert not errs, "\n".join(errs)
 
 
+@pytest.mark.parametrize("direct", [0, 1])
+def test_b_direct_motion_matches_generator(built, tmp_path, direct):
+    """B-picture motion, direct blocks included, against the generator's spec restatement of
+    temporal (direct=0) and spatial (direct=1) direct prediction (8.4.1.2): every MB exact, and
+    direct blocks and B vectors actually compared."""
+    import numpy as np
+    from tests.gen_check import DUMP_DT, RecordingBackend, compare, generate
+    out = str(tmp_path / f"d{direct}.264")
+    generate("cov_cabac", out, out + ".dump", seed=9, extra=(f"direct={direct}",))
+    dump = np.fromfile(out + ".dump", dtype=DUMP_DT)
+    with OracleBackend() as ob:
+        rec = RecordingBackend(ob.be)
+        m2dec_amd.decode_stream(open(out, "rb").read(), backend=rec.be)
+    st = {"direct": 0, "mv": 0}
+    errs = compare(rec.pics, dump, stats=st)
+    assert not errs, "\n".join(errs)
+    assert int((dump["exact_mv"] == 0).sum()) == 0
+    assert st["direct"] > 1000 and st["mv"] > 5000, st
+
+
 def test_sps_scaling_lists_are_ignored(built, tmp_path):
     """The reference parses SPS scaling lists (6 + 8 lists, h264.cpp:280-296) and discards them:
     dequantisation stays flat.  The same stream with and without lists

@@ -120,7 +120,21 @@ typedef struct {
 	int gv[2];
 	int16_t *region; /* per 4x4-MB region velocity (qpel / frame) */
 	int rw, rh;
+	/* direct prediction of B pictures (8.4.1.2) */
+	const struct gcol *col; /* co-located store of RefPicList1[0] */
+	int l0_all_poc[16];     /* the whole initial RefPicList0 (temporal direct maps into it) */
+	int n0_all;
+	int dsf[16];            /* DistScaleFactor per L0 index */
+	int taint;              /* a direct block's motion is not defined by the spec: later MVs inexact */
 } gctx_t;
+
+/* co-located motion of a reference picture (8.4.1.2.1).  Anchors are I / P pictures, so the
+ * co-located block's motion is its L0 motion (or intra: ref -1). */
+typedef struct gcol {
+	int8_t ref[4];      /* refIdxCol per 8x8 */
+	int ref_poc[4];     /* POC of the picture it names */
+	int16_t mv[16][2];  /* mvCol per raster 4x4 */
+} gcol_t;
 
 static gmb_t *nbmb(gctx_t *g, int x, int y, int *bx, int *by)
 {
@@ -726,18 +740,69 @@ static void set_motion(gctx_t *g, gmb_t *m, mbsyn_t *s, int lx, int x, int y, in
 		}
 }
 
-static void direct_belief(gctx_t *g, gmb_t *m, int b8)
+/* Direct motion of 8x8 block b8 of a B macroblock, restated from the spec (ITU-T H.264 8.4.1.2)
+ * so that the dump's B-picture motion checks the parser's derivation (h264.cpp:8325-8387 spatial,
+ * :1247-1277 + temporal_direct_block temporal).  direct_8x8_inference_flag is 1 in every stream
+ * (write_sps), so the co-located vector is the corner 4x4 of the 8x8 block.
+ *  - spatial (8.4.1.2.2): per list refIdx = MinPositive over the MB neighbours A, B, C (C falling
+ *    back to D), mv = the 16x16 prediction for that refIdx; both refIdx < 0 -> refs 0 / 0, mvs 0;
+ *    a list with refIdx 0 gets a zero mv where colZeroFlag (L1[0] short-term, refIdxCol 0,
+ *    |mvCol| <= 1 in both components) holds;
+ *  - temporal (8.4.1.2.3): refIdxL0 = the lowest L0 index naming refIdxCol's picture (0 for an
+ *    intra co-located block), refIdxL1 = 0, mvL0 = (DistScaleFactor * mvCol + 128) >> 8,
+ *    mvL1 = mvL0 - mvCol.  A co-located picture absent from L0 (not in a conforming stream, and
+ *    never produced by these presets) taints the rest of the picture instead of guessing. */
+static void direct_motion(gctx_t *g, gmb_t *m, int b8)
 {
-	/* spatial-direct style belief (the decoder's exact value is not needed for syntax) */
+	const gcol_t *col = &g->col[g->cur];
+	const int16_t *mc = col->mv[(b8 >> 1) * 12 + (b8 & 1) * 3];
+	int x0 = (b8 & 1) * 2, y0 = (b8 >> 1) * 2;
+	int ref[2], mv[2][2];
+	if (g->direct_spatial) {
+		int colzero = col->ref[b8] == 0 && mc[0] >= -1 && mc[0] <= 1 && mc[1] >= -1 && mc[1] <= 1;
+		for (int lx = 0; lx < 2; ++lx) {
+			nbm_t A, B, C;
+			unsigned r;
+			nb_motion(g, lx, -1, 0, &A);
+			nb_motion(g, lx, 0, -1, &B);
+			nb_c(g, lx, 0, 0, 4, &C);
+			r = (unsigned)A.ref < (unsigned)B.ref ? (unsigned)A.ref : (unsigned)B.ref;
+			r = r < (unsigned)C.ref ? r : (unsigned)C.ref;
+			ref[lx] = (int)r;
+			mv[lx][0] = mv[lx][1] = 0;
+			if (ref[lx] >= 0) mvpred(g, lx, 0, 0, 4, ref[lx], 0, mv[lx]);
+		}
+		if (ref[0] < 0 && ref[1] < 0) {
+			ref[0] = ref[1] = 0;
+		} else {
+			for (int lx = 0; lx < 2; ++lx)
+				if (ref[lx] < 0 || (ref[lx] == 0 && colzero)) mv[lx][0] = mv[lx][1] = 0;
+		}
+	} else {
+		ref[1] = 0;
+		if (col->ref[b8] < 0) {
+			ref[0] = 0;
+			mv[0][0] = mv[0][1] = mv[1][0] = mv[1][1] = 0;
+		} else {
+			int k = 0;
+			while (k < g->n0_all && g->l0_all_poc[k] != col->ref_poc[b8]) ++k;
+			if (k >= g->l0n) {
+				g->taint = 1;
+				k = 0;
+			}
+			ref[0] = k;
+			for (int c = 0; c < 2; ++c) {
+				mv[0][c] = (g->dsf[k] * mc[c] + 128) >> 8;
+				mv[1][c] = mv[0][c] - mc[c];
+			}
+		}
+	}
 	for (int lx = 0; lx < 2; ++lx) {
-		int mvp[2] = {0, 0};
-		int x = (b8 & 1) * 2, y = (b8 >> 1) * 2;
-		if (g->slice_type == 1) mvpred(g, lx, 0, 0, 4, 0, 0, mvp);
-		m->ref[lx][b8] = (g->slice_type == 1) ? 0 : -1;
-		for (int yy = y; yy < y + 2; ++yy)
-			for (int xx = x; xx < x + 2; ++xx) {
-				m->mv[lx][yy * 4 + xx][0] = (int16_t)mvp[0];
-				m->mv[lx][yy * 4 + xx][1] = (int16_t)mvp[1];
+		m->ref[lx][b8] = (int8_t)ref[lx];
+		for (int yy = y0; yy < y0 + 2; ++yy)
+			for (int xx = x0; xx < x0 + 2; ++xx) {
+				m->mv[lx][yy * 4 + xx][0] = (int16_t)mv[lx][0];
+				m->mv[lx][yy * 4 + xx][1] = (int16_t)mv[lx][1];
 				m->mvd[lx][yy * 4 + xx][0] = m->mvd[lx][yy * 4 + xx][1] = 0;
 			}
 	}
@@ -762,7 +827,7 @@ static void choose_inter(gctx_t *g, mbsyn_t *s, gmb_t *m)
 		s->mbtype = 0;
 		m->direct16 = 1;
 		m->dir8 = 15;
-		for (int b8 = 0; b8 < 4; ++b8) direct_belief(g, m, b8);
+		for (int b8 = 0; b8 < 4; ++b8) direct_motion(g, m, b8);
 	} else if (r < 100 - g->p->sub8x8_pct) {
 		int shape = (r < 55) ? 0 : (r < 55 + (45 - g->p->sub8x8_pct) / 2 ? 1 : 2); /* 16x16, 16x8, 8x16 */
 		int np = shape ? 2 : 1;
@@ -829,7 +894,7 @@ static void choose_inter(gctx_t *g, mbsyn_t *s, gmb_t *m)
 			}
 			if (is_b && s->sub[b8] == 0) {
 				m->dir8 |= (uint8_t)(1 << b8);
-				direct_belief(g, m, b8);
+				direct_motion(g, m, b8);
 			}
 		}
 		for (int lx = 0; lx < 2; ++lx)
@@ -1345,7 +1410,17 @@ typedef struct {
 
 typedef struct {
 	int disp, poc, frame_num, long_term;
+	int store; /* its co-located store (gen_stream's pool) */
 } dpbref_t;
+
+/* DistScaleFactor (8.4.1.2.3) */
+static int dist_scale(int poc0, int poc1, int cur)
+{
+	int td = clampi(poc1 - poc0, -128, 127), tb = clampi(cur - poc0, -128, 127), tx;
+	if (td == 0) return 256; /* mvL0 = mvCol, mvL1 = 0 */
+	tx = (16384 + abs(td / 2)) / td;
+	return clampi((tb * tx + 32) >> 6, -1024, 1023);
+}
 
 static void write_pred_weight_table(gctx_t *g, bw_t *r, int nl)
 {
@@ -1384,6 +1459,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 	picdesc_t *order;
 	int n = 0, log2_fn = 8, log2_poc = 10;
 	dpbref_t dpb[16];
+	gcol_t *store[17];
 	int ndpb = 0, last_ref_fn = 0, idr_count = 0, cqp_off;
 	bw_t r;
 	mbsyn_t *syn = (mbsyn_t *)calloc(1, sizeof(mbsyn_t));
@@ -1400,6 +1476,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 	g->rw = (g->mbw + 3) / 4;
 	g->rh = (g->mbh + 3) / 4;
 	g->region = (int16_t *)calloc((size_t)(g->rw * g->rh * 2), sizeof(int16_t));
+	for (int i = 0; i < 17; ++i) store[i] = (gcol_t *)calloc((size_t)g->nmb, sizeof(gcol_t));
 	bw_init(&r);
 
 	/* coding order */
@@ -1498,6 +1575,13 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			}
 			g->l0n = imin(p->l0_active, n0);
 			g->l1n = imin(p->l1_active, n1);
+			g->taint = 0;
+			g->n0_all = n0;
+			for (int i = 0; i < n0; ++i) g->l0_all_poc[i] = l0[i].poc;
+			if (n1) {
+				g->col = store[l1[0].store];
+				for (int i = 0; i < n0; ++i) g->dsf[i] = dist_scale(l0[i].poc, l1[0].poc, poc);
+			}
 			for (int i = 0; i < g->l0n; ++i) g->ref_poc[0][i] = l0[i].poc;
 			for (int i = 0; i < g->l1n; ++i) g->ref_poc[1][i] = l1[i].poc;
 			if (pd.type == 1 && (g->l0n == 0 || g->l1n == 0)) pd.type = 0;
@@ -1588,7 +1672,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 					} else {
 						m->direct16 = 1;
 						m->dir8 = 15;
-						for (int b8 = 0; b8 < 4; ++b8) direct_belief(g, m, b8);
+						for (int b8 = 0; b8 < 4; ++b8) direct_motion(g, m, b8);
 					}
 				} else if (pd.type == 2 || pct(p->p_intra_pct)) {
 					choose_intra(g, s, m);
@@ -1612,7 +1696,8 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 					dd.cbp = m->cbp;
 					dd.qp = (int8_t)g->qp;
 					dd.t8x8 = (uint8_t)(s->kind == K_I8 || (s->kind == K_INTER && s->t8x8));
-					dd.exact_mv = pd.type != 1;
+					dd.exact_mv = !g->taint;
+					dd.dir8 = m->dir8;
 					dd.i16_pred = (uint8_t)s->i16_pred;
 					dd.cmode = m->cmode;
 					if (s->kind == K_I4)
@@ -1620,7 +1705,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 					if (s->kind == K_I8)
 						for (int b8 = 0; b8 < 4; ++b8) dd.ipm[b8] = m->ipm[(b8 >> 1) * 8 + (b8 & 1) * 2];
 					for (int lx = 0; lx < 2; ++lx)
-						for (int k = 0; k < 4; ++k) dd.ref[lx][k] = ((m->dir8 >> k) & 1) ? -2 : m->ref[lx][k];
+						for (int k = 0; k < 4; ++k) dd.ref[lx][k] = m->ref[lx][k];
 					memcpy(dd.mv, m->mv, sizeof(dd.mv));
 					if (!skip && s->kind != K_PCM) {
 						if (s->kind == K_I16) {
@@ -1680,6 +1765,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 		}
 		/* reference marking: sliding window (8.2.5.3) */
 		if (pd.ref) {
+			int used[17] = {0}, st = 0;
 			if (ndpb == p->num_ref_frames) {
 				int oldest = 0;
 				for (int i = 1; i < ndpb; ++i) {
@@ -1689,7 +1775,23 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 				}
 				dpb[oldest] = dpb[--ndpb];
 			}
-			dpb[ndpb++] = (dpbref_t){pd.disp, poc, frame_num, 0};
+			/* the picture's co-located store: L0 motion (anchors are I / P) or intra */
+			for (int i = 0; i < ndpb; ++i) used[dpb[i].store] = 1;
+			while (used[st]) ++st;
+			for (int a = 0; a < g->nmb; ++a) {
+				const gmb_t *m = &g->mb[a];
+				gcol_t *c = &store[st][a];
+				for (int b8 = 0; b8 < 4; ++b8) {
+					c->ref[b8] = m->ref[0][b8];
+					c->ref_poc[b8] = m->ref[0][b8] >= 0 ? g->ref_poc[0][m->ref[0][b8]] : 0;
+				}
+				for (int k = 0; k < 16; ++k) {
+					int on = m->ref[0][(k >> 3) * 2 + ((k & 3) >> 1)] >= 0;
+					c->mv[k][0] = on ? m->mv[0][k][0] : 0;
+					c->mv[k][1] = on ? m->mv[0][k][1] : 0;
+				}
+			}
+			dpb[ndpb++] = (dpbref_t){pd.disp, poc, frame_num, 0, st};
 			last_ref_fn = frame_num;
 		}
 	}
@@ -1697,6 +1799,7 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 	free(order);
 	free(g->mb);
 	free(g->region);
+	for (int i = 0; i < 17; ++i) free(store[i]);
 	free(syn);
 	return n;
 }

@@ -54,10 +54,11 @@ typedef struct {
 	uint8_t cbp;
 	int8_t qp;
 	uint8_t t8x8;
-	uint8_t exact_mv;     /* mv[] below equal the decoder's (P/I pictures) */
-	uint8_t i16_pred, cmode, pad;
+	uint8_t exact_mv;     /* ref[] / mv[] below equal the decoder's (direct blocks included) */
+	uint8_t i16_pred, cmode;
+	uint8_t dir8;         /* direct-predicted 8x8 blocks (B_Skip, B_Direct_16x16, direct sub-MBs) */
 	int8_t ipm[16];       /* intra modes per blkIdx (I4x4) or per 8x8 (I8x8, first 4) */
-	int8_t ref[2][4];     /* per 8x8 raster, -1 unused (direct: -2) */
+	int8_t ref[2][4];     /* per 8x8 raster, -1 unused (direct: the derived refIdx) */
 	int16_t mv[2][16][2]; /* per 4x4 raster */
 	int16_t ldc[16];      /* luma DC levels, raster */
 	int16_t luma[256];    /* 4x4: blkIdx*16 + raster; 8x8: b8*64 + raster */

@@ -7,8 +7,11 @@ TAG=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --no-end-to-end"
-for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --replay-only"
+# the 4th group is the wave-state split of MI355X_MICROARCH.md §PMC (quad-cycles, disjoint:
+# WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) plus VALU issue and the clock
+for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   N=$(echo $C | tr ' ' '_')
   timeout -s KILL 240 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_$TAG/$N -o run --output-format csv -- $CMD \
     > $R/gpurun_out/pmc_${TAG}_$N.log 2>&1

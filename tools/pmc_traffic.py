@@ -51,6 +51,18 @@ def main():
         h = statistics.median(v["TCC_HIT_sum"] for v in hit)
         m = statistics.median(v["TCC_MISS_sum"] for v in hit)
         out["l2_hit_rate"] = round(h / max(1.0, h + m), 4)
+    sq = per_dispatch(os.path.join(root, "SQ_WAVES_SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_"
+                                         "SQ_ACTIVE_INST_VALU_SQ_INSTS_VALU_SQ_BUSY_CYCLES_GRBM_GUI_ACTIVE"))
+    if sq:
+        med = {k: statistics.median(v.get(k, 0.0) for v in sq) for k in sq[0]}
+        wc = max(1.0, med.get("SQ_WAVE_CYCLES", 0.0))
+        out["sq"] = {k: int(v) for k, v in sorted(med.items())}
+        # fractions of wave-resident time (quad-cycles): parked on waitcnt / barrier, stalled at issue,
+        # issuing any instruction, issuing VALU
+        out["sq_frac"] = {"wait_any": round(med.get("SQ_WAIT_ANY", 0) / wc, 4),
+                          "wait_inst_any": round(med.get("SQ_WAIT_INST_ANY", 0) / wc, 4),
+                          "active_inst_any": round(med.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4),
+                          "active_inst_valu": round(med.get("SQ_ACTIVE_INST_VALU", 0) / wc, 4)}
     print(json.dumps(out, indent=1))
 
 

@@ -163,6 +163,12 @@ void m2dec_amd_trace_free(m2dec_amd_trace_t *t);
 /* ---- GPU replay of a trace with the records resident in HBM (recon_hip.hip) */
 typedef struct m2dec_amd_hip_replay m2dec_amd_hip_replay_t;
 int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out);
+/* n independent streams (same frame size) in one replay: pictures interleaved one per stream in turn,
+ * each stream on its own frame slots (at most 64 in all), so one k_batch launch carries all of them.
+ * replay_md5 reports pictures in that interleaved order (m2dec_amd_hip_replay_stream gives each one's
+ * stream; a stream's pictures keep their decoding order). */
+int m2dec_amd_hip_replay_create_multi(const m2dec_amd_trace_t *const *ts, int n, int device, m2dec_amd_hip_replay_t **out);
+int m2dec_amd_hip_replay_stream(const m2dec_amd_hip_replay_t *r, int i);
 /* Enqueue `passes` reconstructions of every picture in decoding order (asynchronous). */
 int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes);
 /* Wait for the enqueued work; returns -1 on a device error or wavefront hand-off timeout. */

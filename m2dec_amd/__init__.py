@@ -133,6 +133,10 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_trace_free.restype = None
         L.m2dec_amd_hip_replay_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
         L.m2dec_amd_hip_replay_create.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_create_multi.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        L.m2dec_amd_hip_replay_create_multi.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_stream.argtypes = [vp, ctypes.c_int]
+        L.m2dec_amd_hip_replay_stream.restype = ctypes.c_int
         L.m2dec_amd_hip_replay_run.argtypes = [vp, ctypes.c_int]
         L.m2dec_amd_hip_replay_run.restype = ctypes.c_int
         L.m2dec_amd_hip_replay_sync.argtypes = [vp]
@@ -394,13 +398,19 @@ class Trace:
 
 
 class HipReplay:
-    """GPU reconstruction of a Trace with its records resident in HBM (m2dec_amd_hip_replay_*)."""
+    """GPU reconstruction of a Trace with its records resident in HBM (m2dec_amd_hip_replay_*).
 
-    def __init__(self, trace: Trace, device: int = 0):
-        self.trace = trace
+    Given a list of Traces (independent streams of one frame size), one replay carries all of them:
+    their pictures interleaved in one k_batch launch, each stream on its own frame slots."""
+
+    def __init__(self, trace, device: int = 0):
+        self.traces = list(trace) if isinstance(trace, (list, tuple)) else [trace]
+        self.trace = self.traces[0]
         self.h = ctypes.c_void_p()
-        if lib().m2dec_amd_hip_replay_create(trace.h, device, ctypes.byref(self.h)) < 0:
+        hs = (ctypes.c_void_p * len(self.traces))(*[t.h.value for t in self.traces])
+        if lib().m2dec_amd_hip_replay_create_multi(hs, len(self.traces), device, ctypes.byref(self.h)) < 0:
             raise RuntimeError(f"m2dec_amd: HIP replay unavailable on device {device}")
+        self.npics = sum(t.npics for t in self.traces)
 
     def run(self, passes: int = 1) -> None:
         if lib().m2dec_amd_hip_replay_run(self.h, passes) < 0:
@@ -416,15 +426,21 @@ class HipReplay:
         return t.as_dict()
 
     def md5_decode_order(self) -> List[str]:
-        buf = ctypes.create_string_buffer(35 * self.trace.npics)
+        """Per picture in replay order (one stream: its decoding order)."""
+        buf = ctypes.create_string_buffer(35 * self.npics)
         if lib().m2dec_amd_hip_replay_md5(self.h, buf) < 0:
             raise RuntimeError("m2dec_amd: replay md5 pass failed")
         raw = buf.raw
-        return [raw[35 * i:35 * i + 32].decode() for i in range(self.trace.npics)]
+        return [raw[35 * i:35 * i + 32].decode() for i in range(self.npics)]
 
-    def md5_output_order(self) -> List[str]:
+    def md5_output_order(self):
+        """One stream: its frames' MD5s in output order; several: one such list per stream."""
         d = self.md5_decode_order()
-        return [d[i] for i in self.trace.output_order]
+        per = [[] for _ in self.traces]
+        for i, m in enumerate(d):
+            per[lib().m2dec_amd_hip_replay_stream(self.h, i)].append(m)
+        out = [[p[i] for i in t.output_order] for p, t in zip(per, self.traces)]
+        return out[0] if len(self.traces) == 1 else out
 
     def close(self):
         if self.h:

@@ -1312,8 +1312,8 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 						bits &= bits - 1;
 						const int want = ss.s[sl];
 						if (want <= 0) continue;
-						/* entry (seq & 63) only ever grows: a later picture's value also means "final" */
-						const unsigned long long *fl = a.rowflag + (size_t)((want - 1) & 63) * Hmb;
+						/* entry (seq % ROWFLAG_N) only ever grows: a later picture's value also means "final" */
+						const unsigned long long *fl = a.rowflag + (size_t)((want - 1) & (ROWFLAG_N - 1)) * Hmb;
 						const unsigned long long wv = ROWFLAG(want - 1, need);
 						for (int r0 = rmin_u; r0 <= rlast; r0 += 64) {
 							const int r = r0 + t;
@@ -1782,9 +1782,9 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 					if (t == 0) {
 						if (cA > pubA)
-							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], ROWFLAG(seq, cA), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & (ROWFLAG_N - 1)) * Hmb + yA], ROWFLAG(seq, cA), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 						if (cB > pubB)
-							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], ROWFLAG(seq, cB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+							__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & (ROWFLAG_N - 1)) * Hmb + yB], ROWFLAG(seq, cB), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					}
 					pubA = max(pubA, cA);
 					pubB = max(pubB, cB);
@@ -1799,8 +1799,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		if (t == 0) {
 			__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yA], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-			if (hasB) __hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & 63) * Hmb + yB], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			__hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & (ROWFLAG_N - 1)) * Hmb + yA], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (hasB) __hip_atomic_store((gu64 *)&rowflag[(size_t)(seq & (ROWFLAG_N - 1)) * Hmb + yB], ROWFLAG(seq, Wmb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 		}
 	}
 	/* the raised priority covers the deblocking chain only, not the caller's copy-out / next row pair */

@@ -21,7 +21,11 @@
 #define DBK_RW (DBK_RING * 16) /* ring line width in bytes */
 
 /* row progress word: picture seq's MB row has its first `cols` MB columns final (all 16 luma / 8 chroma
- * sample rows).  An entry (seq & 63) only ever grows, also across pictures. */
+ * sample rows).  An entry (seq % ROWFLAG_N) only ever grows, also across pictures: a reader of picture
+ * q may see picture q + ROWFLAG_N's value, so ROWFLAG_N must exceed the decode-order distance between
+ * a picture and its last reader plus the pictures in flight (interleaved multi-stream batches: the
+ * streams multiply that distance). */
+#define ROWFLAG_N 256
 #define ROWFLAG(seq, cols) ((((unsigned long long)(seq) + 1) << 16) | (unsigned long long)(cols))
 
 #define WAR_MAX 16 /* readers of one slot's content a batch picture can wait for */

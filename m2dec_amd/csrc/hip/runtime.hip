@@ -215,7 +215,7 @@ struct Sched {
 	PictureArgs *pargs = nullptr; /* [NSTREAMS] kernel arguments of the per-picture launches */
 	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
 	int *err = nullptr;
-	unsigned long long *rowflag = nullptr; /* [64][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
+	unsigned long long *rowflag = nullptr; /* [ROWFLAG_N][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
 	int seq = 0;               /* pictures launched */
 	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
 	int inter_grid = 80;       /* persistent inter workers per picture (5/16 of the CUs) */
@@ -280,9 +280,9 @@ struct Sched {
 			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS));
 			if (!pargs) CHECK(hipMalloc(&pargs, sizeof(PictureArgs) * NSTREAMS));
 			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
-			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * 64 * (size_t)Hmb));
+			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb));
 		}
-		CHECK(hipMemset(rowflag, 0, sizeof(unsigned long long) * 64 * (size_t)Hmb));
+		CHECK(hipMemset(rowflag, 0, sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb));
 		/* the I-picture hand-off words carry a tag derived from seq, which restarts here: no word of an
 		 * earlier picture (or decoder) may be left holding a tag a new picture will use */
 		CHECK(hipMemset(hand, 0, hand_bytes() * NSTREAMS));
@@ -1026,7 +1026,8 @@ struct m2dec_amd_hip_replay {
 	int npics = 0;
 	int crop[4] = {0, 0, 0, 0};
 	uint8_t *d_rec = nullptr;
-	std::vector<m2dec_amd_trace_pic_t> pics;
+	std::vector<m2dec_amd_trace_pic_t> pics; /* replay order (streams interleaved), slots / offsets rebased */
+	std::vector<int> stream;                 /* the stream of each picture */
 	std::vector<uint64_t> refs;
 	std::vector<PicJob> jobs;
 	/* timing: 2 events per launch (before / after its k_batch) */
@@ -1045,27 +1046,125 @@ static void replay_free(m2dec_amd_hip_replay_t *r)
 
 extern "C" int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_amd_hip_replay_t **out)
 {
-	int npics, W, H, nslots, nout;
-	size_t len;
-	if (!t || !out || !m2dec_amd_hip_available()) return -1;
-	if (m2dec_amd_trace_info(t, &npics, &W, &H, &nslots, &nout) < 0 || npics <= 0 || W <= 0 || H <= 0) return -1;
-	const uint8_t *rec = m2dec_amd_trace_records(t, &len);
-	const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(t);
-	for (int i = 0; i < npics; ++i)
-		if (pics[i].slot < 0 || pics[i].slot >= nslots || pics[i].width_mbs != W / 16 || pics[i].height_mbs != H / 16) return -1;
+	return m2dec_amd_hip_replay_create_multi(&t, 1, device, out);
+}
+
+/* Frame slots of one stream packed into k slots: a trace names the decoder's frame slots (the frame
+ * LRU cycles through all of them), but only the pictures still read later are live.  Content c (the
+ * picture written at decode index c) lives until its last reader; picture i takes the slot free the
+ * longest among those whose content has no reader at or after i, and every reference in the inter
+ * records is renamed to where its content went.  Returns the new slot per picture (and rewrites the
+ * records), or an empty vector if k slots are not enough. */
+static std::vector<int> pack_slots(uint8_t *rec, const m2dec_amd_trace_pic_t *pics, int np, int k)
+{
+	std::vector<int> writer(64, -1), last(np, -1), out(np, -1), holder(k, -1), freed(k, -1);
+	std::vector<std::vector<int>> content(np); /* per picture: the writer index of each old slot it reads */
+	for (int i = 0; i < np; ++i) {
+		const uint64_t refs = refs_of((const m2r_inter_t *)(rec + pics[i].off_inter), pics[i].n_inter);
+		for (int r = 0; r < 64; ++r)
+			if (((refs >> r) & 1) && r != pics[i].slot) {
+				if (writer[r] < 0) return {}; /* a reference no picture of the trace wrote */
+				last[writer[r]] = i;
+			}
+		content[i].assign(writer.begin(), writer.end());
+		writer[pics[i].slot & 63] = i;
+	}
+	std::vector<int> where(np, -1); /* new slot of each content */
+	for (int i = 0; i < np; ++i) {
+		int best = -1;
+		for (int p = 0; p < k; ++p) {
+			const int c = holder[p];
+			if (c >= 0 && last[c] >= i) continue; /* still read by picture i or later */
+			if (best < 0 || freed[p] < freed[best]) best = p;
+		}
+		if (best < 0) return {};
+		m2r_inter_t *it = (m2r_inter_t *)(rec + pics[i].off_inter);
+		for (int q = 0; q < pics[i].n_inter; ++q)
+			for (int l = 0; l < 2; ++l)
+				for (int b = 0; b < 4; ++b)
+					if (it[q].slot[l][b] >= 0) it[q].slot[l][b] = (int8_t)where[content[i][it[q].slot[l][b] & 63]];
+		if (holder[best] >= 0) freed[best] = i;
+		holder[best] = i;
+		where[i] = best;
+		out[i] = best;
+	}
+	return out;
+}
+
+/* Several independent streams in one replay: their pictures interleaved one by one (stream 0's
+ * first, stream 1's first, ...; each stream's pictures stay in decode order), every stream on its
+ * own range of frame slots (packed, pack_slots), so one k_batch launch carries pictures of all of
+ * them and the device orders only pictures of the same stream against each other (slot reuse,
+ * reference rows). */
+extern "C" int m2dec_amd_hip_replay_create_multi(const m2dec_amd_trace_t *const *ts, int n, int device,
+                                                m2dec_amd_hip_replay_t **out)
+{
+	int W = 0, H = 0, nslots = 0, total = 0, most = 0;
+	if (!ts || n <= 0 || !out || !m2dec_amd_hip_available()) return -1;
+	std::vector<int> np(n), base(n);
+	std::vector<std::vector<int>> newslot(n);
+	std::vector<size_t> rbase(n);
+	std::vector<uint8_t> rec;
+	for (int s = 0; s < n; ++s) {
+		int w, h, ns, nout;
+		size_t len;
+		if (!ts[s] || m2dec_amd_trace_info(ts[s], &np[s], &w, &h, &ns, &nout) < 0 || np[s] <= 0 || w <= 0 || h <= 0) return -1;
+		if (s && (w != W || h != H)) return -1; /* one frame geometry per replay */
+		W = w;
+		H = h;
+		base[s] = nslots;
+		nslots += ns;
+		total += np[s];
+		most = std::max(most, np[s]);
+		const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(ts[s]);
+		for (int i = 0; i < np[s]; ++i)
+			if (pics[i].slot < 0 || pics[i].slot >= ns || pics[i].width_mbs != W / 16 || pics[i].height_mbs != H / 16) return -1;
+		const uint8_t *src = m2dec_amd_trace_records(ts[s], &len);
+		rbase[s] = rec.size();
+		rec.insert(rec.end(), src, src + len);
+		rec.resize((rec.size() + 255) & ~(size_t)255); /* keep every record array as aligned as it was */
+		if (n > 1) { /* pack the stream into its share of the 64 slots */
+			const int k = 64 / n;
+			newslot[s] = pack_slots(rec.data() + rbase[s], pics, np[s], k);
+			if (newslot[s].empty()) return -1;
+			nslots = base[s] + k;
+		}
+		/* the inter records name reference frame slots: move them into the stream's slot range */
+		for (int i = 0; i < np[s]; ++i) {
+			m2r_inter_t *it = (m2r_inter_t *)(rec.data() + rbase[s] + pics[i].off_inter);
+			for (int k = 0; k < pics[i].n_inter; ++k)
+				for (int l = 0; l < 2; ++l)
+					for (int b = 0; b < 4; ++b)
+						if (it[k].slot[l][b] >= 0) it[k].slot[l][b] = (int8_t)(it[k].slot[l][b] + base[s]);
+		}
+	}
+	if (nslots > 64) return -1; /* slot bit masks (refs, SlotSeq) */
 	m2dec_amd_hip_replay_t *r = new m2dec_amd_hip_replay_t();
-	r->npics = npics;
-	m2dec_amd_trace_crop(t, r->crop);
-	r->pics.assign(pics, pics + npics);
-	for (int i = 0; i < npics; ++i)
-		r->refs.push_back(refs_of((const m2r_inter_t *)(rec + pics[i].off_inter), pics[i].n_inter) & ~(1ull << pics[i].slot));
+	r->npics = total;
+	m2dec_amd_trace_crop(ts[0], r->crop);
+	for (int i = 0; i < most; ++i)
+		for (int s = 0; s < n; ++s) {
+			if (i >= np[s]) continue;
+			m2dec_amd_trace_pic_t p = m2dec_amd_trace_pictures(ts[s])[i];
+			p.slot = (n > 1 ? newslot[s][i] : p.slot) + base[s];
+			p.off_mb += rbase[s];
+			p.off_dbk += rbase[s];
+			p.off_slice += rbase[s];
+			p.off_inter += rbase[s];
+			p.off_coef += rbase[s];
+			r->pics.push_back(p);
+			r->stream.push_back(s);
+			r->refs.push_back(refs_of((const m2r_inter_t *)(rec.data() + p.off_inter), p.n_inter) & ~(1ull << p.slot));
+		}
+	const m2dec_amd_trace_pic_t *pics = r->pics.data();
+	const int npics = total;
 #define RCHECK(x) do { if ((x) != hipSuccess) { fprintf(stderr, "m2dec_amd replay: %s failed\n", #x); replay_free(r); return -1; } } while (0)
 	if (r->sc.init(device) < 0 || r->sc.configure(W, H, nslots) < 0) {
 		replay_free(r);
 		return -1;
 	}
-	RCHECK(hipMalloc(&r->d_rec, len));
-	RCHECK(hipMemcpy(r->d_rec, rec, len, hipMemcpyHostToDevice));
+	RCHECK(hipMalloc(&r->d_rec, rec.size()));
+	RCHECK(hipMemcpy(r->d_rec, rec.data(), rec.size(), hipMemcpyHostToDevice));
 	for (int i = 0; i < npics; ++i) {
 		const m2dec_amd_trace_pic_t &p = pics[i];
 		PicJob j;
@@ -1243,6 +1342,12 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	}
 	if (cap) (void)hipFree(cap);
 	return 0;
+}
+
+extern "C" int m2dec_amd_hip_replay_stream(const m2dec_amd_hip_replay_t *r, int i)
+{
+	if (!r || i < 0 || i >= r->npics) return -1;
+	return r->stream[i];
 }
 
 extern "C" void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r)

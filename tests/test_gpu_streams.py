@@ -52,3 +52,28 @@ def test_hip_concurrent_streams_match_golden(built):
         want = GOLDEN[n]["md5"]
         bad = [i for i, (a, b) in enumerate(zip(g, want)) if a != b]
         assert len(g) == len(want) and not bad, f"{n}: frames {bad[:10]} differ (of {len(want)})"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("names", [
+    # 320x192 coverage streams of different tools (CAVLC, CABAC, explicit weights, slices + cip + idc 2)
+    ["cov_cabac_s1", "cov_cavlc_s1", "cov_wp_s1", "cov_tools_s1", "cov_cabac4x4_s1", "cov_wp_quirks_s1"],
+    # the C4 set: eight 1080p streams in one replay (the gpu_recon_streams bench leg)
+    ["c3_1080p_s1"] + [f"c4_1080p_s{s}" for s in range(2, 9)],
+])
+def test_hip_multistream_batch_replay_matches_golden(built, names):
+    """Several independent streams in ONE replay (m2dec_amd_hip_replay_create_multi): pictures
+    interleaved in one k_batch launch, each stream on its own frame slots; every frame of every
+    stream bit-exact."""
+    trs = [m2dec_amd.Trace(stream(n)) for n in names]
+    rp = m2dec_amd.HipReplay(trs, 0)
+    try:
+        got = rp.md5_output_order()
+    finally:
+        rp.close()
+        for t in trs:
+            t.close()
+    for n, g in zip(names, got):
+        want = GOLDEN[n]["md5"]
+        bad = [i for i, (a, b) in enumerate(zip(g, want)) if a != b]
+        assert len(g) == len(want) and not bad, f"{n}: frames {bad[:10]} differ (of {len(want)})"

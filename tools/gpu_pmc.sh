@@ -1,13 +1,20 @@
 #!/bin/bash
 # HBM traffic of the bench's k_batch launches from rocprofv3 PMC counters, one counter group per pass
 # (MI355X_MICROARCH.md §HBM / §rocprofv3 PMC slots: FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so
-# they cannot share a pass).  Usage: bash tools/gpu_pmc.sh TAG   -> gpurun_out/pmc_TAG.json
+# they cannot share a pass).  Usage: bash tools/gpu_pmc.sh TAG [KERNEL]  -> gpurun_out/pmc_TAG.json
+# KERNEL k_batch (default): the replay leg; k_picture: the decode path of the end-to-end leg (one
+# launch per picture; counter collection serialises the launches, the bytes are per launch).
 set -o pipefail
 TAG=${1:-r01}
+K=${2:-k_batch}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --replay-only"
+if [ "$K" = k_batch ]; then
+  CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --replay-only"
+else
+  CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extras"
+fi
 # the 4th group is the wave-state split of MI355X_MICROARCH.md §PMC (quad-cycles, disjoint:
 # WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) plus VALU issue and the clock
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
@@ -18,4 +25,4 @@ for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
   rc=$?; echo "pmc $C rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $R/gpurun_out/pmc_${TAG}_$N.log; exit $rc; fi
 done
-cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_$TAG > gpurun_out/pmc_$TAG.json && cat gpurun_out/pmc_$TAG.json
+cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_$TAG $K > gpurun_out/pmc_$TAG.json && cat gpurun_out/pmc_$TAG.json

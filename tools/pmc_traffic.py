@@ -16,23 +16,29 @@ import statistics
 import sys
 
 
+KERNEL = "k_batch"
+
+
 def per_dispatch(d):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if not row["Kernel_Name"].startswith("k_batch"):
+            if not row["Kernel_Name"].startswith(KERNEL):
                 continue
             key = int(row["Dispatch_Id"])
             vals.setdefault(key, {})
             name = row["Counter_Name"]
             vals[key][name] = vals[key].get(name, 0.0) + float(row["Counter_Value"])
-    keys = sorted(vals)[1:]  # drop the parity-gate launch
+    keys = sorted(vals)[1:] if KERNEL == "k_batch" else sorted(vals)  # k_batch: drop the parity-gate launch
     return [vals[k] for k in keys]
 
 
 def main():
+    global KERNEL
     root = sys.argv[1]
-    out = {"kernel": "k_batch", "source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh)"}
+    if len(sys.argv) > 2:
+        KERNEL = sys.argv[2]
+    out = {"kernel": KERNEL, "source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh)"}
     fetch = per_dispatch(os.path.join(root, "FETCH_SIZE"))
     write = per_dispatch(os.path.join(root, "WRITE_SIZE"))
     hit = per_dispatch(os.path.join(root, "TCC_HIT_sum_TCC_MISS_sum"))

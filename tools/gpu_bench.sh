@@ -10,7 +10,13 @@ timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/ben
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -5 gpurun_out/bench_$TAG.err
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1
+# two profiles, one per roofline of the bench line, so each kernel's average is over exactly the launches
+# its roofline is quoted on: the value leg (k_picture, one launch per 1080p picture) and the
+# single-stream replay leg (k_batch, one launch per 60-picture pass)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras > $R/gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; tail -2 $R/gpurun_out/prof_$TAG.log
-find $R/gpurun_out/prof_$TAG -name "*stats*"
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_replay -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --replay-only > $R/gpurun_out/prof_${TAG}_replay.log 2>&1
+rc=$?; echo "rocprof replay rc=$rc"; tail -2 $R/gpurun_out/prof_${TAG}_replay.log
+find $R/gpurun_out/prof_$TAG $R/gpurun_out/prof_${TAG}_replay -name "*kernel_stats*"
 exit $rc

@@ -35,6 +35,10 @@ typedef struct {
 	int64_t kernel_launches;
 	int64_t alg_bytes;
 	int64_t hold_waits; /* MD5 drivers: times the frame LRU waited for a frame the MD5 threads held */
+	/* per-stage host view: record uploads and frame downloads (HIP-event time of the
+	 * built-in back end's copies), and the CPU time of the slice-data parse on the parse-ahead workers */
+	double h2d_us, d2h_us;
+	double parse_cpu_s;
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).

@@ -50,7 +50,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("frames_out", ctypes.c_int), ("pictures", ctypes.c_int), ("last_error", ctypes.c_int),
                 ("ahead", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
                 ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
-                ("alg_bytes", ctypes.c_int64), ("hold_waits", ctypes.c_int64)]
+                ("alg_bytes", ctypes.c_int64), ("hold_waits", ctypes.c_int64),
+                ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("parse_cpu_s", ctypes.c_double)]
 
 
 class HipTiming(ctypes.Structure):

@@ -561,8 +561,11 @@ done:
 			stats->kernel_us = t.picture_us;
 			stats->kernel_launches = t.kernel_launches;
 			stats->alg_bytes = t.frame_bytes + t.ref_bytes + t.record_bytes;
+			stats->h2d_us = t.h2d_us;
+			stats->d2h_us = t.d2h_us;
 		}
 	}
+	if (stats) stats->parse_cpu_s = h264_async_parse_seconds(d);
 	if (stats) {
 		stats->frames_out = n;
 		stats->pictures = (int)d->pictures;

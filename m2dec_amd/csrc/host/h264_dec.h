@@ -378,6 +378,7 @@ int h264_async_add_slice(h264_dec_t *d);
 int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 void h264_async_stop(h264_dec_t *d);
+double h264_async_parse_seconds(h264_dec_t *d);
 int h264_async_nal_next(h264_dec_t *d);
 void h264_async_resume(h264_dec_t *d);
 void h264_async_la_sps(h264_dec_t *la);

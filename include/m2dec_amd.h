@@ -39,6 +39,8 @@ typedef struct {
 	 * built-in back end's copies), and the CPU time of the slice-data parse on the parse-ahead workers */
 	double h2d_us, d2h_us;
 	double parse_cpu_s;
+	/* pictures of several slices parsed slice-parallel, and those re-parsed sequentially after a try */
+	int64_t slice_par_pictures, slice_par_fallbacks;
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).

@@ -51,7 +51,8 @@ class Stats(ctypes.Structure):
                 ("ahead", ctypes.c_int), ("t_start", ctypes.c_double), ("t_end", ctypes.c_double),
                 ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64), ("hold_waits", ctypes.c_int64),
-                ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("parse_cpu_s", ctypes.c_double)]
+                ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("parse_cpu_s", ctypes.c_double),
+                ("slice_par_pictures", ctypes.c_int64), ("slice_par_fallbacks", ctypes.c_int64)]
 
 
 class HipTiming(ctypes.Structure):

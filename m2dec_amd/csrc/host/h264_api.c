@@ -565,7 +565,12 @@ done:
 			stats->d2h_us = t.d2h_us;
 		}
 	}
-	if (stats) stats->parse_cpu_s = h264_async_parse_seconds(d);
+	if (stats) {
+		long par, fb;
+		stats->parse_cpu_s = h264_async_parse_seconds(d, &par, &fb);
+		stats->slice_par_pictures = par;
+		stats->slice_par_fallbacks = fb;
+	}
 	if (stats) {
 		stats->frames_out = n;
 		stats->pictures = (int)d->pictures;

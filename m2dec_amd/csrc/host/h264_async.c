@@ -94,6 +94,13 @@ typedef struct h264_job {
 	size_t priv_n;
 	long deps[8];             /* seq of the jobs whose parse must finish first (jobs are recycled:
 	                             never keep a pointer past its submission) */
+	/* slice-parallel parse (job_run_par): per slice a private context and a private view of the
+	 * record arena; slices are taken from sl_next by the job's worker and idle workers */
+	h264_dec_t **sw;
+	m2r_picture_t *spic;
+	int *sret;
+	int capsw;
+	int sl_next, sl_done;     /* guarded by the pipeline mutex */
 	int ndeps;
 	long seq;
 	int taken, done, err;     /* guarded by the pipeline mutex */
@@ -147,6 +154,11 @@ struct h264_async {
 	/* M2DEC_AMD_ASYNC_STATS: where the caller's thread spends its time (seconds) */
 	int stats;
 	double t0, t_col_wait, t_done_wait, t_copy, t_submit, t_slice, t_parse, t_la;
+	/* pictures whose slices are being parsed in parallel (slices left to take: sl_next < nsl) */
+	h264_job_t *par[16];
+	int npar;
+	int slice_par;            /* M2DEC_AMD_SLICE_PAR (default 1): slices of a picture on several workers */
+	long n_par, n_par_fallback; /* pictures parsed slice-parallel / re-parsed sequentially after a try */
 };
 
 static int job_arena(h264_job_t *j, int wm, int hm)
@@ -207,6 +219,10 @@ static void job_free(h264_job_t *j)
 	free(j->rbsp);
 	free(j->mbi);
 	free(j->priv_col);
+	for (int i = 0; i < j->capsw; ++i) free(j->sw[i]);
+	free(j->sw);
+	free(j->spic);
+	free(j->sret);
 	free(j->arena);
 	free(j->w);
 	free(j);
@@ -217,6 +233,7 @@ static void job_run(h264_job_t *j)
 {
 	h264_dec_t *w = j->w;
 	int mbs = 0, slice_num = 0, slice_rec = 0, last_firstline = 0, ret = 0;
+	w->par_first_mb = 0;
 	int8_t idc[1024], alpha[1024], beta[1024];
 	const int n = j->snap[0]->n_mbs;
 	for (int i = 0; i < n; ++i) {
@@ -228,6 +245,7 @@ static void job_run(h264_job_t *j)
 		const h264_dec_t *s = j->snap[k];
 		const ptrdiff_t off = j->rbsp[k] - s->slice_rbsp;
 		memcpy(w, s, sizeof(*w));
+		w->par_first_mb = 0;
 		w->mbi = j->mbi;
 		w->pic = &j->pic;
 		if (j->nonref) w->colpic[w->curr_col].mb = j->priv_col;
@@ -263,6 +281,154 @@ static void job_run(h264_job_t *j)
 	h264_picture_resolve_deblock(w);
 }
 
+/* Slice-parallel parse of one picture.  The slices of a picture are
+ * independent for the slice-data parse: intra / motion prediction and the CABAC / CAVLC contexts never
+ * read an MB of another slice (availability stops at the slice), so slice k runs on its own context
+ * with its own MB range, writing its records into the picture arena from MB first_mb(k) on (coefficients
+ * from first_mb(k) * 416, inter records from first_mb(k): the arena holds the worst case of every MB)
+ * and its slice record at index k.  Afterwards: the records are packed in slice order (offsets in the
+ * MB records moved with them), the MB-edge bS toward an earlier slice (skipped during the parse,
+ * par_first_mb) is computed, and the per-slice deblock parameters are gathered for
+ * h264_picture_resolve_deblock.  The records equal the sequential parse's up to where the
+ * coefficients / inter records sit.  A picture whose slices do not tile it exactly in order (the
+ * sequential parse's picture-complete test) is parsed again sequentially.  Returns 0, or -1 when
+ * job_run must take over. */
+static void slice_run(h264_job_t *j, int k)
+{
+	const h264_dec_t *s = j->snap[k];
+	h264_dec_t *w = j->sw[k];
+	m2r_picture_t *pk = &j->spic[k];
+	const ptrdiff_t off = j->rbsp[k] - s->slice_rbsp;
+	const int first = s->sh.first_mb;
+	*pk = j->pic;
+	pk->n_slices = k;
+	pk->n_inter = first;
+	pk->n_coef = first * 416;
+	pk->n_intra = 0;
+	memcpy(w, s, sizeof(*w));
+	w->par_first_mb = first;
+	w->mbi = j->mbi;
+	w->pic = pk;
+	if (j->nonref) w->colpic[w->curr_col].mb = j->priv_col;
+	w->mbs_decoded = 0;
+	w->slice_num = k;
+	w->bs.p += off;
+	w->bs.end += off;
+	w->slice_rbsp += off;
+	w->slice_rbsp_end += off;
+	j->sret[k] = h264_slice_data(w);
+}
+
+static int job_run_par(struct h264_async *as, h264_job_t *j)
+{
+	const int nsl = j->nsl, n = j->snap[0]->n_mbs;
+	if (j->pic.n_slices || j->pic.n_inter || j->pic.n_coef || j->pic.n_intra || nsl > 16) return -1;
+	for (int k = 1; k < nsl; ++k)
+		if (j->snap[k]->sh.first_mb <= j->snap[k - 1]->sh.first_mb) return -1;
+	if (j->snap[0]->sh.first_mb != 0 || j->snap[nsl - 1]->sh.first_mb >= n) return -1;
+	if (nsl > j->capsw) {
+		h264_dec_t **sw = (h264_dec_t **)realloc(j->sw, sizeof(*sw) * (size_t)nsl);
+		if (!sw) return -1;
+		j->sw = sw;
+		for (int k = j->capsw; k < nsl; ++k) j->sw[k] = NULL;
+		j->capsw = nsl;
+		free(j->spic);
+		free(j->sret);
+		j->spic = (m2r_picture_t *)malloc(sizeof(m2r_picture_t) * (size_t)nsl);
+		j->sret = (int *)malloc(sizeof(int) * (size_t)nsl);
+		if (!j->spic || !j->sret) {
+			j->capsw = 0;
+			return -1;
+		}
+	}
+	for (int k = 0; k < nsl; ++k) {
+		if (!j->sw[k]) j->sw[k] = (h264_dec_t *)malloc(sizeof(h264_dec_t));
+		if (!j->sw[k]) return -1;
+	}
+	for (int i = 0; i < n; ++i) {
+		j->mbi[i].type = -1;
+		j->mbi[i].slice = -1;
+	}
+	/* offer the slices to idle workers; this worker takes them too, and waits for the rest */
+	pthread_mutex_lock(&as->mu);
+	if (as->npar >= 16) {
+		pthread_mutex_unlock(&as->mu);
+		return -1;
+	}
+	j->sl_next = 0;
+	j->sl_done = 0;
+	as->par[as->npar++] = j;
+	pthread_cond_broadcast(&as->cv_work);
+	while (j->sl_next < nsl) {
+		const int k = j->sl_next++;
+		if (j->sl_next == nsl)
+			for (int i = 0; i < as->npar; ++i)
+				if (as->par[i] == j) as->par[i] = as->par[--as->npar];
+		pthread_mutex_unlock(&as->mu);
+		slice_run(j, k);
+		pthread_mutex_lock(&as->mu);
+		j->sl_done++;
+	}
+	{
+		const double tw = now_s();
+		while (j->sl_done < nsl) pthread_cond_wait(&as->cv_done, &as->mu);
+		as->t_parse -= now_s() - tw; /* the worker's job time counts parse work only */
+	}
+	pthread_mutex_unlock(&as->mu);
+
+	/* every slice parsed exactly its MB range, in order, the last one ending the picture */
+	for (int k = 0; k < nsl; ++k) {
+		const int first = j->snap[k]->sh.first_mb, end = k + 1 < nsl ? j->snap[k + 1]->sh.first_mb : n;
+		if (j->sret[k] != (k + 1 == nsl ? 1 : 0) || j->sw[k]->mbs_decoded != end - first) return -1;
+	}
+	/* pack the coefficient pool and the inter records in slice order */
+	{
+		m2r_picture_t *pic = &j->pic;
+		int ncoef = 0, ninter = 0, nintra = 0;
+		for (int k = 0; k < nsl; ++k) {
+			const m2r_picture_t *pk = &j->spic[k];
+			const int first = j->snap[k]->sh.first_mb, end = k + 1 < nsl ? j->snap[k + 1]->sh.first_mb : n;
+			const int cb = first * 416, ib = first;
+			const int nc = pk->n_coef - cb, ni = pk->n_inter - ib;
+			if (ncoef != cb) memmove(pic->coef + ncoef, pic->coef + cb, sizeof(int16_t) * (size_t)nc);
+			if (ninter != ib) memmove(pic->inter + ninter, pic->inter + ib, sizeof(m2r_inter_t) * (size_t)ni);
+			for (int a = first; a < end; ++a) {
+				m2r_mb_t *r = &pic->mb[a];
+				r->coef -= (uint32_t)(cb - ncoef);
+				if (r->kind == M2R_MB_INTER) r->inter -= (uint32_t)(ib - ninter);
+			}
+			ncoef += nc;
+			ninter += ni;
+			nintra += pk->n_intra;
+		}
+		pic->n_coef = ncoef;
+		pic->n_inter = ninter;
+		pic->n_intra = nintra;
+		pic->n_slices = nsl;
+	}
+	/* the picture-level context: the last slice's, with every slice's deblock parameters */
+	{
+		h264_dec_t *w = j->sw[nsl - 1];
+		w->pic = &j->pic;
+		w->par_first_mb = 0;
+		for (int k = 0; k < nsl - 1; ++k) {
+			w->slice_idc[k] = j->sw[k]->slice_idc[k];
+			w->slice_alpha[k] = j->sw[k]->slice_alpha[k];
+			w->slice_beta[k] = j->sw[k]->slice_beta[k];
+		}
+		w->slice_num = nsl;
+		w->mbs_decoded = n;
+		for (int k = 1; k < nsl; ++k) {
+			const int first = j->snap[k]->sh.first_mb, mw = w->mb_w;
+			/* MBs with the left or top neighbour in an earlier slice: the MB row from the slice's first MB */
+			for (int a = first; a < n && a < first + mw; ++a)
+				if (((a % mw) != 0 && a - 1 < first) || (a >= mw && a - mw < first)) h264_fix_bs(w, a);
+		}
+		h264_picture_resolve_deblock(w);
+	}
+	return 0;
+}
+
 /* 1: every job j waits for has finished parsing (0: not yet); a dependency no longer in the fifo was
  * submitted, hence finished.  *err collects their errors.  Caller holds the mutex. */
 static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err)
@@ -287,6 +453,21 @@ static void *worker(void *arg)
 		h264_job_t *j = NULL;
 		int dep_err = 0;
 		for (;;) {
+			/* a slice of a picture parsed slice-parallel first: that picture is already under way */
+			if (as->npar) {
+				h264_job_t *pj = as->par[0];
+				const int k = pj->sl_next++;
+				if (pj->sl_next == pj->nsl) as->par[0] = as->par[--as->npar];
+				pthread_mutex_unlock(&as->mu);
+				const double ts = now_s();
+				slice_run(pj, k);
+				const double te = now_s();
+				pthread_mutex_lock(&as->mu);
+				as->t_parse += te - ts;
+				pj->sl_done++;
+				pthread_cond_broadcast(&as->cv_done);
+				continue;
+			}
 			while (as->qtail < as->qhead && as->queue[as->qtail % AS_MAX]->taken) as->qtail++;
 			for (long k = as->qtail; k < as->qhead && !j; ++k) {
 				h264_job_t *c = as->queue[k % AS_MAX];
@@ -301,7 +482,13 @@ static void *worker(void *arg)
 		pthread_mutex_unlock(&as->mu);
 		const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
 		if (dep_err) j->err = 1;
-		else job_run(j);
+		else if (!(as->slice_par && j->nsl > 1)) job_run(j);
+		else if (job_run_par(as, j) < 0) {
+			job_run(j);
+			__atomic_fetch_add(&as->n_par_fallback, 1, __ATOMIC_RELAXED);
+		} else {
+			__atomic_fetch_add(&as->n_par, 1, __ATOMIC_RELAXED);
+		}
 		pthread_mutex_lock(&as->mu);
 		{
 			const double te = now_s();
@@ -378,6 +565,7 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->la_sps_nal = -1;
 	as->ahead = d->have_backend && d->backend.bind && !getenv("M2DEC_AMD_NO_AHEAD");
 	as->stats = getenv("M2DEC_AMD_ASYNC_STATS") ? atoi(getenv("M2DEC_AMD_ASYNC_STATS")) : 0;
+	as->slice_par = !getenv("M2DEC_AMD_SLICE_PAR") || atoi(getenv("M2DEC_AMD_SLICE_PAR")) != 0;
 	as->t0 = now_s();
 	for (int i = 0; i < threads; ++i) {
 		if (pthread_create(&as->th[i], NULL, worker, as) != 0) break;
@@ -396,14 +584,18 @@ fail:
 	return -1;
 }
 
-/* CPU seconds the workers spent parsing slice data so far (0 without parse-ahead) */
-double h264_async_parse_seconds(h264_dec_t *d)
+/* CPU seconds the workers spent parsing slice data so far (0 without parse-ahead), and the pictures
+ * parsed slice-parallel / re-parsed sequentially after a slice-parallel try */
+double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback)
 {
 	struct h264_async *as = d->as;
 	double t;
+	*par = *par_fallback = 0;
 	if (!as) return 0.0;
 	pthread_mutex_lock(&as->mu);
 	t = as->t_parse;
+	*par = as->n_par;
+	*par_fallback = as->n_par_fallback;
 	pthread_mutex_unlock(&as->mu);
 	return t;
 }

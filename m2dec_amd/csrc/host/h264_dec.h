@@ -347,6 +347,8 @@ struct h264_dec {
 	struct h264_async *as;
 	m2dec_hold_t *hold;      /* frames the caller holds (NULL: none) */
 	int parse_threads;       /* requested workers (m2dec_amd_h264_set_parse_threads / env) */
+	int par_first_mb;        /* slice-parallel parse: this slice's first MB; the MB-edge bS toward an MB
+	                            before it (an earlier slice, parsed concurrently) is left to h264_fix_bs */
 	/* 1: this is the pipeline's lookahead context: it runs the header-level state machine ahead of
 	 * the API-visible context, names pictures by virtual frame ids instead of frame slots (no DPB
 	 * output, no caller frames, no header callback) and creates the slice-data jobs */
@@ -364,6 +366,7 @@ int h264_slice_header(h264_dec_t *d, h264_bits_t *b, int nal_unit_type, int nal_
 int h264_picture_begin(h264_dec_t *d);
 int h264_picture_finish(h264_dec_t *d);
 void h264_picture_resolve_deblock(h264_dec_t *d);
+void h264_fix_bs(h264_dec_t *d, int addr);
 int h264_picture_mark(h264_dec_t *d);
 void h264_dpb_init(h264_dpb_t *dpb, int maxsize);
 int h264_dpb_peek(h264_dpb_t *dpb, int bypass);
@@ -378,7 +381,7 @@ int h264_async_add_slice(h264_dec_t *d);
 int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 void h264_async_stop(h264_dec_t *d);
-double h264_async_parse_seconds(h264_dec_t *d);
+double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback);
 int h264_async_nal_next(h264_dec_t *d);
 void h264_async_resume(h264_dec_t *d);
 void h264_async_la_sps(h264_dec_t *la);

@@ -1153,7 +1153,8 @@ static inline uint32_t nz_raster(const h264_mbinfo_t *m)
 
 static inline int b8_of(int r) { return ((r >> 3) << 1) | ((r & 3) >> 1); }
 
-static void compute_bs(slice_ctx_t *s)
+/* boundary strengths of the current MB's edges (bs_v / bs_h / the BS4 flags of its deblock record) */
+static void bs_strength(slice_ctx_t *s)
 {
 	h264_mbinfo_t *q = s->cur;
 	m2r_deblock_t *db = s->dbk;
@@ -1175,6 +1176,7 @@ static void compute_bs(slice_ctx_t *s)
 			const h264_mbinfo_t *p = NULL;
 			if (dir == 0 && s->mbx != 0) p = &s->d->mbi[s->addr - 1];
 			if (dir == 1 && s->mby != 0) p = &s->d->mbi[s->addr - s->d->mb_w];
+			if (p && (int)(p - s->d->mbi) < s->d->par_first_mb) p = NULL; /* h264_fix_bs, once that slice is parsed */
 			if (p && is_intra_type(p->type)) {
 				flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
 				str = 0xaa; /* 2 in every segment (the flag makes it 4) */
@@ -1221,6 +1223,28 @@ static void compute_bs(slice_ctx_t *s)
 	db->bs_v = bv;
 	db->bs_h = bh;
 	db->flags = flags;
+}
+
+/* slice-parallel parse: an MB whose left or top neighbour lies in an earlier slice gets its bS again
+ * once every slice of the picture is parsed */
+void h264_fix_bs(h264_dec_t *d, int addr)
+{
+	slice_ctx_t s;
+	memset(&s, 0, sizeof(s));
+	s.d = d;
+	s.addr = addr;
+	s.mbx = addr % d->mb_w;
+	s.mby = addr / d->mb_w;
+	s.cur = &d->mbi[addr];
+	s.dbk = &d->pic->dbk[addr];
+	bs_strength(&s);
+}
+
+static void compute_bs(slice_ctx_t *s)
+{
+	const h264_mbinfo_t *q = s->cur;
+	m2r_deblock_t *db = s->dbk;
+	bs_strength(s);
 	if (q->type == MBT_IPCM) {
 		/* I_PCM deblock qp quirk (h264.cpp:4749-4751, Appendix A #5) */
 		db->qpy = 0;

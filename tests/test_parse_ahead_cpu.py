@@ -107,3 +107,23 @@ def test_md5_driver_holds_frames(built, monkeypatch, name, threads, extra):
     assert got == GOLDEN[name]["md5"]
     if extra is not None and name == "c2_720p_s1":  # (cov_slices_s1 has fewer pictures than frames)
         assert st.hold_waits > 0
+
+
+@pytest.mark.parametrize("name", ["cov_slices_s1", "cov_tools_s1", "cov_tools_cavlc_s1", "c5_4k_s1"])
+def test_slice_parallel_parse(built, monkeypatch, name):
+    """Multi-slice pictures parsed slice-parallel (several workers per picture, records packed in slice
+    order, the MB-edge bS toward earlier slices computed after): every frame equals the golden, every
+    multi-slice picture took that path (no sequential re-parse), and M2DEC_AMD_SLICE_PAR=0 (one worker
+    per picture) gives the same frames."""
+    want = GOLDEN[name]["md5"]
+    with OracleBackend() as ob:
+        st = m2dec_amd.Stats()
+        got = m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=6, stats=st)
+    assert got == want
+    assert st.slice_par_pictures == len(want) and st.slice_par_fallbacks == 0, (st.slice_par_pictures,
+                                                                                  st.slice_par_fallbacks)
+    monkeypatch.setenv("M2DEC_AMD_SLICE_PAR", "0")
+    with OracleBackend() as ob:
+        st = m2dec_amd.Stats()
+        assert m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=6, stats=st) == want
+    assert st.slice_par_pictures == 0

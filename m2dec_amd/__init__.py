@@ -227,7 +227,7 @@ def decode_stream(data: bytes, backend: Optional[Backend] = None, device: int = 
 
     ``backend`` None -> the HIP back end on ``device`` (raises if absent).  Any other m2r_backend_t
     (e.g. the oracle's, in tests) is borrowed.  ``parse_threads``: parse-ahead workers (-1: the
-    default — 12 with the HIP back end, none with a borrowed one).  ``stats`` (a Stats) receives the
+    default — 16 with the HIP back end, none with a borrowed one).  ``stats`` (a Stats) receives the
     decoder's counters.
     """
     L = lib()

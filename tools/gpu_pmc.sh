@@ -2,7 +2,7 @@
 # HBM traffic of the bench's k_batch launches from rocprofv3 PMC counters, one counter group per pass
 # (MI355X_MICROARCH.md §HBM / §rocprofv3 PMC slots: FETCH_SIZE costs 3 TCC slots, WRITE_SIZE 2, so
 # they cannot share a pass).  Usage: bash tools/gpu_pmc.sh TAG [KERNEL]  -> gpurun_out/pmc_TAG.json
-# KERNEL k_batch (default): the replay leg; k_picture: the decode path of the end-to-end leg (one
+# KERNEL k_batch (default): the replay leg; k_batch8: the 8-stream replay; k_picture: the decode path of the end-to-end leg (one
 # launch per picture; counter collection serialises the launches, the bytes are per launch).
 set -o pipefail
 TAG=${1:-r01}
@@ -12,6 +12,8 @@ mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 if [ "$K" = k_batch ]; then
   CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --replay-only"
+elif [ "$K" = k_batch8 ]; then  # the 8-stream replay (bench gpu_recon_streams)
+  CMD="python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --replay-only --replay-streams 8"
 else
   CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extras"
 fi

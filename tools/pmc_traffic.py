@@ -36,9 +36,11 @@ def per_dispatch(d):
 def main():
     global KERNEL
     root = sys.argv[1]
-    if len(sys.argv) > 2:
-        KERNEL = sys.argv[2]
+    label = sys.argv[2] if len(sys.argv) > 2 else "k_batch"
+    KERNEL = "k_batch" if label == "k_batch8" else label
     out = {"kernel": KERNEL, "source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh)"}
+    if label == "k_batch8":
+        out["preset"] = "c3x8"  # bench.py gpu_recon_streams: the 8 C4 streams in one replay
     fetch = per_dispatch(os.path.join(root, "FETCH_SIZE"))
     write = per_dispatch(os.path.join(root, "WRITE_SIZE"))
     hit = per_dispatch(os.path.join(root, "TCC_HIT_sum_TCC_MISS_sum"))

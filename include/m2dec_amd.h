@@ -175,6 +175,10 @@ int m2dec_amd_hip_replay_create(const m2dec_amd_trace_t *t, int device, m2dec_am
  * stream; a stream's pictures keep their decoding order). */
 int m2dec_amd_hip_replay_create_multi(const m2dec_amd_trace_t *const *ts, int n, int device, m2dec_amd_hip_replay_t **out);
 int m2dec_amd_hip_replay_stream(const m2dec_amd_hip_replay_t *r, int i);
+/* Host-only check of the multi-stream slot packing on one trace packed into k slots (tests): 0 when
+ * every reference still names the picture it named before, -1 when k slots are too few, 1 + i when
+ * picture i would read other content. */
+int m2dec_amd_replay_pack_check(const m2dec_amd_trace_t *t, int k);
 /* Enqueue `passes` reconstructions of every picture in decoding order (asynchronous). */
 int m2dec_amd_hip_replay_run(m2dec_amd_hip_replay_t *r, int passes);
 /* Wait for the enqueued work; returns -1 on a device error or wavefront hand-off timeout. */

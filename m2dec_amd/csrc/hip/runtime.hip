@@ -1091,6 +1091,36 @@ static std::vector<int> pack_slots(uint8_t *rec, const m2dec_amd_trace_pic_t *pi
 	return out;
 }
 
+/* Host-only check of pack_slots on a trace (tests, no GPU): every reference of every picture must
+ * name, after packing into k slots, the content (writer picture) it named before.  0: preserved,
+ * -1: k slots are not enough, 1 + i: picture i reads other content. */
+extern "C" int m2dec_amd_replay_pack_check(const m2dec_amd_trace_t *t, int k)
+{
+	int np, w, h, ns, nout;
+	size_t len;
+	if (!t || k <= 0 || k > 64 || m2dec_amd_trace_info(t, &np, &w, &h, &ns, &nout) < 0) return -1;
+	const uint8_t *src = m2dec_amd_trace_records(t, &len);
+	const m2dec_amd_trace_pic_t *pics = m2dec_amd_trace_pictures(t);
+	std::vector<uint8_t> rec(src, src + len);
+	const std::vector<int> ns_ = pack_slots(rec.data(), pics, np, k);
+	if (ns_.empty()) return -1;
+	int orig[64], packed[64];
+	for (int i = 0; i < 64; ++i) orig[i] = packed[i] = -1;
+	for (int i = 0; i < np; ++i) {
+		const m2r_inter_t *a = (const m2r_inter_t *)(src + pics[i].off_inter);
+		const m2r_inter_t *b = (const m2r_inter_t *)(rec.data() + pics[i].off_inter);
+		for (int q = 0; q < pics[i].n_inter; ++q)
+			for (int l = 0; l < 2; ++l)
+				for (int s = 0; s < 4; ++s) {
+					if ((a[q].slot[l][s] < 0) != (b[q].slot[l][s] < 0)) return 1 + i;
+					if (a[q].slot[l][s] >= 0 && orig[a[q].slot[l][s] & 63] != packed[b[q].slot[l][s] & 63]) return 1 + i;
+				}
+		orig[pics[i].slot & 63] = i;
+		packed[ns_[i]] = i;
+	}
+	return 0;
+}
+
 /* Several independent streams in one replay: their pictures interleaved one by one (stream 0's
  * first, stream 1's first, ...; each stream's pictures stay in decode order), every stream on its
  * own range of frame slots (packed, pack_slots), so one k_batch launch carries pictures of all of

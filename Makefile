@@ -23,8 +23,14 @@ GEN := tools/_build/h264gen
 M2VGEN := tools/_build/m2vgen
 
 APP := m2dec_amd/lib/h264dec
+HARNESS := tools/_build/m2decoder_like
 
-all: $(LIB) $(ORACLE) $(GEN) $(M2VGEN) $(APP)
+all: $(LIB) $(ORACLE) $(GEN) $(M2VGEN) $(APP) $(HARNESS)
+
+# test harness: drives h264d_func the way src/app/m2decoder.h does (no release call)
+$(HARNESS): tests/harness/m2decoder_like.cpp $(LIB) include/m2dec_amd.h include/m2d.h
+	@mkdir -p $(dir $@)
+	g++ -O2 -g -Wall -std=c++17 -Iinclude -o $@ $< -Lm2dec_amd/lib -lm2dec_amd -ldl -Wl,-rpath,'$$ORIGIN/../../m2dec_amd/lib'
 
 $(APP): m2dec_amd/csrc/app/h264dec.c $(LIB) include/m2dec_amd.h
 	$(CC) -O2 -Wall -std=gnu11 -Iinclude -o $@ $< -Lm2dec_amd/lib -lm2dec_amd -Wl,-rpath,'$$ORIGIN'

@@ -41,11 +41,17 @@ typedef struct {
 	double parse_cpu_s;
 	/* pictures of several slices parsed slice-parallel, and those re-parsed sequentially after a try */
 	int64_t slice_par_pictures, slice_par_fallbacks;
+	/* the drivers: seconds spent releasing the decoder context after the last frame (outside t_end) */
+	double teardown_s;
+	/* the built-in HIP back end: frame bytes downloaded (d2h_us above is their copy time), and the host
+	 * time of the staging -> caller-frame copies inside peek / get */
+	int64_t d2h_bytes;
+	double host_copy_us;
 } m2dec_amd_stats_t;
 
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).
- * The context takes ownership: m2dec_amd_h264_release() calls be->destroy.  be == NULL detaches the
- * current back end without destroying it (a borrowed one). */
+ * The context takes ownership: be->destroy is called when the context is released or reclaimed.
+ * be == NULL detaches the current back end without destroying it (a borrowed one). */
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
 /* GPU ordinal used by the default back end (call after init, before the first SPS). */
 int m2dec_amd_h264_set_device(void *ctx, int device);
@@ -53,8 +59,11 @@ int m2dec_amd_h264_set_device(void *ctx, int device);
  * Default with the built-in HIP back end: $M2DEC_AMD_PARSE_THREADS or 8; with a back end installed by
  * m2dec_amd_h264_set_backend: 0.  Call before the first set_frames. */
 int m2dec_amd_h264_set_parse_threads(void *ctx, int threads);
-/* Free heap and GPU resources owned by a context. */
+/* Free the state behind a context at once (optional: as in the reference, a caller may also just
+ * free the context memory; the library then reclaims the state itself — see h264_api.c). */
 void m2dec_amd_h264_release(void *ctx);
+/* Decoder states alive in the process registry, and how many were reclaimed over the cap. */
+int m2dec_amd_h264_registry(int *contexts, long *evicted);
 
 /* Decode a whole Annex-B stream exactly like `h264dec` (m2decoder.h:132-157 output loop).
  * on_frame receives every output frame in output order.  backend may be NULL (a HIP back end is
@@ -81,13 +90,17 @@ void m2dec_amd_hip_unpin(void *p);
 /* Per-kernel timing of the HIP back end since creation (microseconds, HIP events). */
 typedef struct {
 	double picture_us;      /* kernel time: k_picture launches (decode path) / k_batch launches (replay) */
-	double h2d_us, d2h_us;  /* decode path only: record upload, frame download */
+	double h2d_us, d2h_us;  /* decode path only: record upload, frame download (device -> staging) */
 	int64_t pictures;       /* pictures reconstructed */
 	int64_t inter_launches, intra_launches, deblock_launches; /* pictures with inter MBs / intra MBs / deblocked */
 	int64_t record_bytes;   /* bytes of records uploaded (R_pic summed) */
 	int64_t ref_bytes;      /* algorithmic reference bytes read by MC (sum over PUs and lists) */
 	int64_t frame_bytes;    /* NV12 bytes written (1.5 W H per picture) */
 	int64_t kernel_launches; /* k_picture / k_batch launches timed in picture_us */
+	/* decode path: bytes copied device -> pinned staging (d2h_us is their HIP-event time on the copy
+	 * stream), and the host time of staging -> caller frame copies inside sync_frame */
+	int64_t d2h_bytes;
+	double host_copy_us;
 } m2dec_amd_hip_timing_t;
 int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out);
 

@@ -52,7 +52,8 @@ class Stats(ctypes.Structure):
                 ("setup_s", ctypes.c_double), ("kernel_us", ctypes.c_double), ("kernel_launches", ctypes.c_int64),
                 ("alg_bytes", ctypes.c_int64), ("hold_waits", ctypes.c_int64),
                 ("h2d_us", ctypes.c_double), ("d2h_us", ctypes.c_double), ("parse_cpu_s", ctypes.c_double),
-                ("slice_par_pictures", ctypes.c_int64), ("slice_par_fallbacks", ctypes.c_int64)]
+                ("slice_par_pictures", ctypes.c_int64), ("slice_par_fallbacks", ctypes.c_int64),
+                ("teardown_s", ctypes.c_double), ("d2h_bytes", ctypes.c_int64), ("host_copy_us", ctypes.c_double)]
 
 
 class HipTiming(ctypes.Structure):
@@ -61,7 +62,8 @@ class HipTiming(ctypes.Structure):
                 ("pictures", ctypes.c_int64),
                 ("inter_launches", ctypes.c_int64), ("intra_launches", ctypes.c_int64),
                 ("deblock_launches", ctypes.c_int64), ("record_bytes", ctypes.c_int64),
-                ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64), ("kernel_launches", ctypes.c_int64)]
+                ("ref_bytes", ctypes.c_int64), ("frame_bytes", ctypes.c_int64), ("kernel_launches", ctypes.c_int64),
+                ("d2h_bytes", ctypes.c_int64), ("host_copy_us", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

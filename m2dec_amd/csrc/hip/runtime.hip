@@ -174,6 +174,49 @@ struct HipPool {
 };
 HipPool g_pool;
 
+/* Device buffers outlive a decoder context as well: the picture buffers (64 x 1.5 W H, 200 MB at
+ * 1080p), the hand-off records and the progress words are handed to the next context of the same
+ * geometry instead of hipFree + hipMalloc (several ms per context at 1080p).  Exact-size match; at
+ * most 4 GiB kept per process. */
+struct DevPool {
+	std::mutex mu;
+	struct Block {
+		int dev;
+		void *p;
+		size_t n;
+	};
+	std::vector<Block> blocks;
+	size_t kept = 0;
+
+	hipError_t take(int dev, void **p, size_t n)
+	{
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			for (size_t i = 0; i < blocks.size(); ++i)
+				if (blocks[i].dev == dev && blocks[i].n == n) {
+					*p = blocks[i].p;
+					kept -= n;
+					blocks.erase(blocks.begin() + (long)i);
+					return hipSuccess;
+				}
+		}
+		return hipMalloc(p, n);
+	}
+	void give(int dev, void *p, size_t n)
+	{
+		if (!p) return;
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if (kept + n <= ((size_t)4 << 30)) {
+				blocks.push_back({dev, p, n});
+				kept += n;
+				return;
+			}
+		}
+		(void)hipFree(p);
+	}
+} g_dev;
+
 /* Host ranges page-locked for the life of the process (m2dec_amd_hip_pin: the stream driver's pooled
  * frame memory).  set_frames does not register frames inside them again — a new stream reuses the
  * pool's frames without ~0.15 ms of pinning per frame. */
@@ -254,19 +297,19 @@ struct Sched {
 		for (auto &s : st) CHECK(hipStreamSynchronize(s));
 		size_t nfsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
 		if (frames && (nfsz != fsz || n > nslots)) {
-			(void)hipFree(frames);
+			g_dev.give(dev, frames, fsz * (size_t)nslots);
 			frames = nullptr;
 		}
 		if (!frames) {
-			CHECK(hipMalloc(&frames, nfsz * (size_t)n));
-			CHECK(hipMemset(frames, 0, nfsz * (size_t)n));
+			CHECK(g_dev.take(dev, (void **)&frames, nfsz * (size_t)n));
+			CHECK(hipMemsetAsync(frames, 0, nfsz * (size_t)n, st[0])); /* (a pooled buffer holds another stream's pictures) */
 			nslots = n;
 		}
 		if (prog && (width / 16 != Wmb || height / 16 != Hmb)) {
 			batch_free();
-			(void)hipFree(prog);
-			(void)hipFree(hand);
-			(void)hipFree(rowflag);
+			g_dev.give(dev, prog, prog_bytes());
+			g_dev.give(dev, hand, hand_bytes() * NSTREAMS);
+			g_dev.give(dev, rowflag, rowflag_bytes());
 			prog = nullptr;
 			hand = nullptr;
 			rowflag = nullptr;
@@ -277,16 +320,17 @@ struct Sched {
 		Hmb = height / 16;
 		fsz = nfsz;
 		if (!prog) {
-			CHECK(hipMalloc(&prog, sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS));
+			CHECK(g_dev.take(dev, (void **)&prog, prog_bytes()));
 			if (!pargs) CHECK(hipMalloc(&pargs, sizeof(PictureArgs) * NSTREAMS));
-			CHECK(hipMalloc(&hand, hand_bytes() * NSTREAMS));
-			CHECK(hipMalloc(&rowflag, sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb));
+			CHECK(g_dev.take(dev, (void **)&hand, hand_bytes() * NSTREAMS));
+			CHECK(g_dev.take(dev, (void **)&rowflag, rowflag_bytes()));
 		}
-		CHECK(hipMemset(rowflag, 0, sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb));
+		CHECK(hipMemsetAsync(rowflag, 0, rowflag_bytes(), st[0]));
 		/* the I-picture hand-off words carry a tag derived from seq, which restarts here: no word of an
 		 * earlier picture (or decoder) may be left holding a tag a new picture will use */
-		CHECK(hipMemset(hand, 0, hand_bytes() * NSTREAMS));
-		if (bt.hand) CHECK(hipMemset(bt.hand, 0, hand_bytes() * (size_t)bt.cap));
+		CHECK(hipMemsetAsync(hand, 0, hand_bytes() * NSTREAMS, st[0]));
+		if (bt.hand) CHECK(hipMemsetAsync(bt.hand, 0, hand_bytes() * (size_t)bt.cap, st[0]));
+		CHECK(hipStreamSynchronize(st[0]));
 		seq = 0;
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		for (int i = 0; i < 64; ++i) {
@@ -314,6 +358,8 @@ struct Sched {
 	}
 
 	size_t hand_bytes() const { return (size_t)Hmb * Wmb * (HBI_BYTES + HBD_BYTES) + (size_t)Hmb * NSEG(Wmb) * 8 * HBP_BYTES; }
+	size_t prog_bytes() const { return sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS; }
+	size_t rowflag_bytes() const { return sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb; }
 
 	hipEvent_t next_event()
 	{
@@ -594,12 +640,16 @@ struct Sched {
 			g_pool.put_event(dev, false, e);
 			e = nullptr;
 		}
-		if (frames) (void)hipFree(frames);
-		if (prog) (void)hipFree(prog);
+		g_dev.give(dev, frames, fsz * (size_t)nslots);
+		if (prog) g_dev.give(dev, prog, prog_bytes());
+		if (hand) g_dev.give(dev, hand, hand_bytes() * NSTREAMS);
+		if (rowflag) g_dev.give(dev, rowflag, rowflag_bytes());
 		if (pargs) (void)hipFree(pargs);
-		if (hand) (void)hipFree(hand);
 		if (err) (void)hipFree(err);
-		if (rowflag) (void)hipFree(rowflag);
+		frames = nullptr;
+		prog = nullptr;
+		hand = nullptr;
+		rowflag = nullptr;
 		for (auto &s : st) {
 			g_pool.put_stream(dev, s);
 			s = nullptr;
@@ -687,22 +737,65 @@ struct ArenaPool {
 ArenaPool g_arenas;
 
 struct TimingSlot {
-	hipEvent_t e[6]; /* start, uploaded, after inter, after intra, after deblock, after D2H */
+	hipEvent_t e[6]; /* start, uploaded, after the kernel, (unused), (unused), end */
 	bool pending = false;
 };
 
+/* Pinned staging buffers for the frames on their way to the caller (one NV12 picture each), kept
+ * per process: a decoder context takes them as pictures are bound and gives them back when the
+ * caller has the frame. */
+struct StagePool {
+	std::mutex mu;
+	std::vector<std::pair<uint8_t *, size_t>> free_blocks;
+	size_t kept = 0;
+
+	uint8_t *take(size_t need)
+	{
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			for (size_t i = 0; i < free_blocks.size(); ++i)
+				if (free_blocks[i].second == need) {
+					uint8_t *p = free_blocks[i].first;
+					free_blocks.erase(free_blocks.begin() + (long)i);
+					kept -= need;
+					return p;
+				}
+		}
+		void *p = nullptr;
+		if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return nullptr;
+		return (uint8_t *)p;
+	}
+	void give(uint8_t *p, size_t n)
+	{
+		if (!p) return;
+		{
+			std::lock_guard<std::mutex> lk(mu);
+			if (kept + n <= ((size_t)1 << 30)) { /* keep up to 1 GiB for the next contexts */
+				free_blocks.emplace_back(p, n);
+				kept += n;
+				return;
+			}
+		}
+		(void)hipHostFree(p);
+	}
+} g_stage;
+
+/* The caller's frames are plain caller memory (m2decoder.h:54-80 may free them inside the header
+ * callback; the destructor frees them without telling the decoder, m2decoder.h:39-46).  So the GPU
+ * never writes them: a picture is copied device -> the context's own pinned staging buffer for its
+ * slot (asynchronously, bind / submit), and staging -> the caller's frame on the caller's thread
+ * inside sync_frame, i.e. inside peek / get_decoded_frame.  Between API calls nothing in flight
+ * points into caller memory. */
 struct HipBackend {
 	Sched sc;
 	hipStream_t copy = nullptr; /* decode ahead: bind's copies out of the picture buffers */
 	m2d_frame_t frames[64];
-	void *reg[64][2];
-	hipEvent_t slot_ev[64];
-	bool slot_pending[64];
-	/* the caller's frames are page-locked (hipHostRegister, ~0.15 ms per 1080p frame) on a helper
-	 * thread while the first pictures are parsed; a picture's download waits for its frame's turn */
-	std::thread reg_thread;
-	std::atomic<int> reg_done{0}; /* frames [0, reg_done) registered */
-	int reg_n = 0;
+	int nframes = 0;
+	uint8_t *stg[64];          /* staging buffer holding / receiving slot i's picture (null: none) */
+	size_t stg_size = 0;       /* bytes per staging buffer (1.5 W H) */
+	hipEvent_t slot_ev[64];    /* the copy into stg[i] is complete */
+	hipEvent_t d2h_ev[64][2];  /* timing: start / end of that copy */
+	bool slot_pending[64];     /* stg[i] holds a picture not yet copied to the caller's frame */
 	Arena ar[kArenas];
 	int next = 0;
 	TimingSlot tr[16];
@@ -721,21 +814,15 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 		tm.picture_us += ms * 1e3;
 		tm.kernel_launches++;
 	}
-	if (hipEventElapsedTime(&ms, t.e[2], t.e[5]) == hipSuccess) tm.d2h_us += ms * 1e3;
 	t.pending = false;
 }
 
-void unregister_frames(HipBackend *b)
+/* slot i's staging buffer goes back to the pool (its copy, if any, is complete) */
+void stage_drop(HipBackend *b, int i)
 {
-	if (b->reg_thread.joinable()) b->reg_thread.join();
-	b->reg_done = 0;
-	b->reg_n = 0;
-	for (int i = 0; i < 64; ++i)
-		for (int k = 0; k < 2; ++k)
-			if (b->reg[i][k]) {
-				(void)hipHostUnregister(b->reg[i][k]);
-				b->reg[i][k] = nullptr;
-			}
+	g_stage.give(b->stg[i], b->stg_size);
+	b->stg[i] = nullptr;
+	b->slot_pending[i] = false;
 }
 
 int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int height)
@@ -743,34 +830,35 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	HipBackend *b = (HipBackend *)self;
 	const double t0 = wall_s();
 	if (b->sc.sync_all() < 0) return -1;
-	if (b->copy) CHECK(hipStreamSynchronize(b->copy)); /* copies into the frames about to be released */
-	unregister_frames(b);
+	if (b->copy) CHECK(hipStreamSynchronize(b->copy)); /* every staging copy is complete */
 	if (n > 64) n = 64;
 	memcpy(b->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
+	b->nframes = n;
+	const size_t stg = (size_t)width * height * 3 / 2;
+	/* pictures bound but not yet handed out keep their staging (they reach the new frames) unless the
+	 * picture size changed — the reference would hand out the new, unwritten frames then */
+	for (int i = 0; i < 64; ++i)
+		if (b->stg[i] && (stg != b->stg_size || i >= n)) stage_drop(b, i);
+	b->stg_size = stg;
 	/* one device picture buffer per virtual id (decode ahead) — a caller slot also names one */
 	if (b->sc.configure(width, height, 64) < 0) return -1;
-	const double t1 = wall_s();
-	size_t ls = (size_t)width * height, cs = ls / 2;
-	for (int i = 0; i < n; ++i) b->slot_pending[i] = false;
-	b->reg_n = n;
-	const int dev = b->sc.dev;
-	b->reg_thread = std::thread([b, n, ls, cs, dev]() {
-		(void)hipSetDevice(dev);
-		for (int i = 0; i < n; ++i) {
-			if (g_pins.covers(b->frames[i].luma, ls) && g_pins.covers(b->frames[i].chroma, cs)) {
-				/* already page-locked (pooled frame memory): nothing to register or unregister */
-			} else if (b->frames[i].chroma == b->frames[i].luma + ls) {
-				if (hipHostRegister(b->frames[i].luma, ls + cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-			} else {
-				if (hipHostRegister(b->frames[i].luma, ls, hipHostRegisterDefault) == hipSuccess) b->reg[i][0] = b->frames[i].luma;
-				if (hipHostRegister(b->frames[i].chroma, cs, hipHostRegisterDefault) == hipSuccess) b->reg[i][1] = b->frames[i].chroma;
-			}
-			b->reg_done.store(i + 1, std::memory_order_release);
-		}
-	});
-	if (dbg_knob("M2DEC_AMD_ASYNC_STATS"))
-		fprintf(stderr, "be_set_frames: configure %.2f ms, register %d frames %.2f ms\n", 1e3 * (t1 - t0), n,
-		        1e3 * (wall_s() - t1));
+	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "be_set_frames: configure %.2f ms\n", 1e3 * (wall_s() - t0));
+	return 0;
+}
+
+/* enqueue the copy of picture buffer `cur` into slot's staging buffer on stream s (after what s waits for) */
+int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
+{
+	if (!b->stg[slot] && !(b->stg[slot] = g_stage.take(b->stg_size))) {
+		fprintf(stderr, "m2dec_amd: no pinned staging memory\n");
+		return -1;
+	}
+	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][0], s));
+	CHECK(hipMemcpyAsync(b->stg[slot], cur, b->stg_size, hipMemcpyDeviceToHost, s));
+	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][1], s));
+	CHECK(hipEventRecord(b->slot_ev[slot], s));
+	b->slot_pending[slot] = true;
+	b->sc.tm.d2h_bytes += (int64_t)b->stg_size;
 	return 0;
 }
 
@@ -841,7 +929,7 @@ int be_submit(void *self, m2r_picture_t *pic)
 	const int n = pic->width_mbs * pic->height_mbs;
 	const bool virt = (pic->flags & M2R_PIC_VIRTUAL) != 0;
 	if (pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots) return -1;
-	if (!virt && pic->slot >= b->reg_n) return -1;
+	if (!virt && pic->slot >= b->nframes) return -1;
 	if (pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) return -1;
 	CHECK(hipSetDevice(sc.dev));
 	PicJob j;
@@ -878,16 +966,8 @@ int be_submit(void *self, m2r_picture_t *pic)
 	CHECK(hipEventRecord(a->consumed, s));
 	a->pending = true;
 	const size_t ls = (size_t)sc.W * sc.H;
-	if (!virt) {
-		/* the caller's slot is the picture buffer: copy out right behind the kernel */
-		const m2d_frame_t &f = b->frames[pic->slot];
-		uint8_t *cur = sc.frames + (size_t)pic->slot * sc.fsz;
-		while (b->reg_done.load(std::memory_order_acquire) <= pic->slot) std::this_thread::yield();
-		CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, s));
-		CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, s));
-		CHECK(hipEventRecord(b->slot_ev[pic->slot], s));
-		b->slot_pending[pic->slot] = true;
-	}
+	if (!virt) /* the caller's slot is the picture buffer: copy out right behind the kernel */
+		if (stage_copy(b, sc.frames + (size_t)pic->slot * sc.fsz, pic->slot, s) < 0) return -1;
 	if (ts) {
 		CHECK(hipEventRecord(ts->e[5], s));
 		ts->pending = true;
@@ -907,18 +987,11 @@ int be_bind(void *self, int vid, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	Sched &sc = b->sc;
-	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->reg_n || !sc.slot_write[vid]) return -1;
+	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->nframes || !sc.slot_write[vid]) return -1;
 	CHECK(hipSetDevice(sc.dev));
 	if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
 	CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[vid], 0));
-	const m2d_frame_t &f = b->frames[slot];
-	const uint8_t *cur = sc.frames + (size_t)vid * sc.fsz;
-	const size_t ls = (size_t)sc.W * sc.H;
-	while (b->reg_done.load(std::memory_order_acquire) <= slot) std::this_thread::yield();
-	CHECK(hipMemcpyAsync(f.luma, cur, ls, hipMemcpyDeviceToHost, b->copy));
-	CHECK(hipMemcpyAsync(f.chroma, cur + ls, ls / 2, hipMemcpyDeviceToHost, b->copy));
-	CHECK(hipEventRecord(b->slot_ev[slot], b->copy));
-	b->slot_pending[slot] = true;
+	if (stage_copy(b, sc.frames + (size_t)vid * sc.fsz, slot, b->copy) < 0) return -1;
 	hipEvent_t r = sc.next_event();
 	if (!r) return -1;
 	CHECK(hipEventRecord(r, b->copy));
@@ -926,14 +999,26 @@ int be_bind(void *self, int vid, int slot)
 	return 0;
 }
 
+/* the picture of `slot` into the caller's frame: wait for its staging copy, then copy it on this
+ * (the caller's) thread */
 int be_sync(void *self, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	if (slot < 0 || slot >= 64) return -1;
 	if (b->slot_pending[slot]) {
 		CHECK(hipEventSynchronize(b->slot_ev[slot]));
-		b->slot_pending[slot] = false;
 		if (b->sc.check_err() < 0) return -1;
+		if (b->timing) {
+			float ms;
+			if (hipEventElapsedTime(&ms, b->d2h_ev[slot][0], b->d2h_ev[slot][1]) == hipSuccess) b->sc.tm.d2h_us += ms * 1e3;
+		}
+		const double t0 = wall_s();
+		const m2d_frame_t &f = b->frames[slot];
+		const size_t ls = b->stg_size / 3 * 2;
+		memcpy(f.luma, b->stg[slot], ls);
+		memcpy(f.chroma, b->stg[slot] + ls, ls / 2);
+		b->sc.tm.host_copy_us += (wall_s() - t0) * 1e6;
+		stage_drop(b, slot);
 	}
 	return 0;
 }
@@ -941,18 +1026,28 @@ int be_sync(void *self, int slot)
 void be_destroy(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
+	const double t0 = wall_s();
 	b->sc.sync_all();
-	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: no copy into a caller frame is left) */
+	const double t1 = wall_s();
+	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: every staging copy is complete) */
 	b->copy = nullptr;
-	unregister_frames(b);
+	for (int i = 0; i < 64; ++i) stage_drop(b, i);
 	for (auto &a : b->ar) {
 		g_arenas.give(b->sc.dev, a); /* (every kernel reading it finished: sync_all above) */
 		g_pool.put_event(b->sc.dev, false, a.consumed);
 	}
-	for (int i = 0; i < 64; ++i) g_pool.put_event(b->sc.dev, false, b->slot_ev[i]);
+	for (int i = 0; i < 64; ++i) {
+		g_pool.put_event(b->sc.dev, false, b->slot_ev[i]);
+		g_pool.put_event(b->sc.dev, true, b->d2h_ev[i][0]);
+		g_pool.put_event(b->sc.dev, true, b->d2h_ev[i][1]);
+	}
 	for (auto &t : b->tr)
 		for (auto &e : t.e) g_pool.put_event(b->sc.dev, true, e);
+	const double t2 = wall_s();
 	b->sc.destroy();
+	if (dbg_knob("M2DEC_AMD_ASYNC_STATS"))
+		fprintf(stderr, "be_destroy: sync %.2f ms, staging / arenas / events %.2f ms, scheduler %.2f ms\n",
+		        1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (wall_s() - t2));
 	delete b;
 }
 
@@ -989,13 +1084,17 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	if (!out || !m2dec_amd_hip_available()) return -1;
 	const double t0 = wall_s();
 	HipBackend *b = new HipBackend();
-	memset(b->reg, 0, sizeof(b->reg));
+	memset(b->stg, 0, sizeof(b->stg));
 	memset(b->slot_pending, 0, sizeof(b->slot_pending));
 	if (b->sc.init(device) < 0) {
 		delete b;
 		return -1;
 	}
-	for (int i = 0; i < 64; ++i) CHECK(g_pool.event(device, false, &b->slot_ev[i]));
+	for (int i = 0; i < 64; ++i) {
+		CHECK(g_pool.event(device, false, &b->slot_ev[i]));
+		CHECK(g_pool.event(device, true, &b->d2h_ev[i][0]));
+		CHECK(g_pool.event(device, true, &b->d2h_ev[i][1]));
+	}
 	for (auto &t : b->tr)
 		for (auto &e : t.e) CHECK(g_pool.event(device, true, &e));
 	const char *tm = getenv("M2DEC_AMD_TIMING");

@@ -25,13 +25,143 @@ static int hdr_dummy(void *a, void *b)
 	return 0;
 }
 
-static h264_dec_t *CTX(void *p) { return (h264_dec_t *)p; }
+static double mono_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* ------------------------------------------------------------------ caller context = handle
+ * The reference's context is plain caller memory: M2Decoder allocates context_size bytes
+ * (m2decoder.h:184) and frees them with delete[] (m2decoder.h:43-50) without any release call, and
+ * SetFrames deletes the frames inside the header callback (m2decoder.h:68-77).  This decoder owns
+ * worker threads' work, GPU buffers and pinned memory, so none of it may live in, or point into,
+ * that memory.  The caller's context_size bytes hold only a handle; the state (h264_dec_t) is
+ * library memory kept in a process registry:
+ *   - nothing the library runs between API calls (pool workers, pipe_drive, GPU copies) touches
+ *     caller memory: frames reach the caller's buffers only inside peek / get (sync_frame copies out
+ *     of the back end's own staging), so dropping frames or the context at any time is safe;
+ *   - a state whose context the caller dropped is reclaimed by the registry: when init() is called
+ *     on the same context address again (the caller reuses the memory), or when a new context
+ *     would bring the registry over M2DEC_AMD_MAX_CONTEXTS (default 8) — then the least recently
+ *     used state that finished its stream (decode_picture returned -2) or was not called for
+ *     M2DEC_AMD_IDLE_EVICT_S seconds (default 30) goes first; at twice the cap, one idle for a second.
+ *     A state is never reclaimed during a call on it.  Calls on a reclaimed context fail (-1;
+ *     stream_pos returns an empty reader).
+ *   - m2dec_amd_h264_release() still frees a context at once (optional). */
+typedef struct {
+	uint64_t magic;
+	uint64_t gen;
+	h264_dec_t *st;
+} h264_handle_t;
+
+#define H264_HANDLE_MAGIC 0x6d32646563616d64ull /* "m2decamd" */
+
+static pthread_mutex_t reg_mu = PTHREAD_MUTEX_INITIALIZER;
+static h264_dec_t *reg_head;
+static int reg_count;
+static uint64_t reg_gen;
+static long reg_evicted;
+
+static void state_destroy(h264_dec_t *d);
+
+static int env_int(const char *name, int def)
+{
+	const char *e = getenv(name);
+	return e && *e ? atoi(e) : def;
+}
+
+/* registry lookup of a caller context; counts the call in (leave() counts it out) */
+static h264_dec_t *enter(void *ctx)
+{
+	const h264_handle_t *h = (const h264_handle_t *)ctx;
+	h264_dec_t *d;
+	if (!h || h->magic != H264_HANDLE_MAGIC) return NULL;
+	pthread_mutex_lock(&reg_mu);
+	for (d = reg_head; d; d = d->reg_next)
+		if (d == h->st && d->gen == h->gen && d->owner == ctx) break;
+	if (d) {
+		d->in_call++;
+		d->last_call = mono_s();
+	}
+	pthread_mutex_unlock(&reg_mu);
+	if (!d) {
+		static int warned;
+		if (!__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
+			fprintf(stderr, "m2dec_amd: call on a context that was released or reclaimed (not initialised, "
+			                "dropped, or evicted over M2DEC_AMD_MAX_CONTEXTS)\n");
+	}
+	return d;
+}
+
+static void leave(h264_dec_t *d)
+{
+	pthread_mutex_lock(&reg_mu);
+	d->in_call--;
+	pthread_mutex_unlock(&reg_mu);
+}
+
+h264_dec_t *h264_state(void *ctx)
+{
+	h264_dec_t *d = enter(ctx);
+	if (d) leave(d);
+	return d;
+}
+
+/* States to reclaim before registering a context at `ctx` (registry mutex held): those initialised
+ * on the same address (its memory is being reused: that context is gone), then LRU ones over the
+ * cap.  They are unlinked here and destroyed by the caller outside the mutex. */
+static int reclaim_victims(const void *ctx, h264_dec_t **out, int max)
+{
+	const int cap = env_int("M2DEC_AMD_MAX_CONTEXTS", 8);
+	const double idle = (double)env_int("M2DEC_AMD_IDLE_EVICT_S", 30), now = mono_s();
+	int n = 0;
+	for (h264_dec_t **pp = &reg_head; *pp && n < max;) {
+		h264_dec_t *d = *pp;
+		if (d->owner == ctx && !d->in_call) {
+			*pp = d->reg_next;
+			reg_count--;
+			out[n++] = d;
+		} else {
+			if (d->owner == ctx) d->owner = NULL; /* (in a call on another thread: orphaned, reclaimed later) */
+			pp = &d->reg_next;
+		}
+	}
+	while (reg_count >= cap && n < max) {
+		/* over twice the cap, any state idle for a second goes too (it is most likely dropped) */
+		const double lim = reg_count >= 2 * cap ? (idle < 1.0 ? idle : 1.0) : idle;
+		h264_dec_t **best = NULL;
+		for (h264_dec_t **pp = &reg_head; *pp; pp = &(*pp)->reg_next) {
+			const h264_dec_t *d = *pp;
+			if (d->in_call || !(d->finished || !d->owner || now - d->last_call >= lim)) continue;
+			if (!best || d->last_call < (*best)->last_call) best = pp;
+		}
+		if (!best) break;
+		h264_dec_t *d = *best;
+		*best = d->reg_next;
+		reg_count--;
+		reg_evicted++;
+		out[n++] = d;
+	}
+	return n;
+}
 
 static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d) return -1;
-	memset(d, 0, sizeof(*d));
+	h264_handle_t *h = (h264_handle_t *)ctx;
+	h264_dec_t *victims[64], *d;
+	int nv;
+	if (!ctx) return -1;
+	pthread_mutex_lock(&reg_mu);
+	nv = reclaim_victims(ctx, victims, 64);
+	pthread_mutex_unlock(&reg_mu);
+	for (int i = 0; i < nv; ++i) state_destroy(victims[i]);
+	d = (h264_dec_t *)calloc(1, sizeof(h264_dec_t));
+	if (!d) {
+		memset(h, 0, sizeof(*h));
+		return -1;
+	}
 	d->stream = &d->stream_i;
 	d->header_callback = cb ? cb : hdr_dummy;
 	d->header_callback_arg = arg;
@@ -43,19 +173,36 @@ static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg
 	d->sh.first_mb = -1;
 	d->parse_threads = -1; /* default: decided when the back end is created */
 	d->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
+	d->owner = ctx;
+	d->last_call = mono_s();
+	pthread_mutex_lock(&reg_mu);
+	d->gen = ++reg_gen;
+	d->reg_next = reg_head;
+	reg_head = d;
+	reg_count++;
+	pthread_mutex_unlock(&reg_mu);
+	h->magic = H264_HANDLE_MAGIC;
+	h->gen = d->gen;
+	h->st = d;
 	return 0;
 }
 
 static dec_bits *api_stream_pos(void *ctx)
 {
-	return CTX(ctx)->stream;
+	static dec_bits gone; /* a reclaimed context: a reader with no data */
+	h264_dec_t *d = h264_state(ctx);
+	return d ? d->stream : &gone;
 }
 
 static int api_get_info(void *ctx, m2d_info_t *info)
 {
-	h264_dec_t *d = CTX(ctx);
+	h264_dec_t *d = enter(ctx);
 	const h264_sps_t *s;
-	if (!d || !info) return -1;
+	if (!d) return -1;
+	if (!info) {
+		leave(d);
+		return -1;
+	}
 	/* the reference reads the SPS of the current slice's PPS (h264.cpp:511) */
 	s = &d->sps[d->pps[d->sh.pps_id].sps_id];
 	if (!s->valid) s = &d->sps[d->active_sps];
@@ -65,7 +212,8 @@ static int api_get_info(void *ctx, m2d_info_t *info)
 	info->disp_height = (int16_t)s->height;
 	info->frame_num = (int16_t)(s->num_ref_frames + 1);
 	for (int i = 0; i < 4; ++i) info->crop[i] = (int16_t)s->crop[i];
-	info->additional_size = 16; /* parser state lives in the context / back end, not the caller's work buffer */
+	info->additional_size = 16; /* parser state lives in the library's state / back end, not the caller's work buffer */
+	leave(d);
 	return 0;
 }
 
@@ -78,7 +226,7 @@ static int ensure_backend(h264_dec_t *d)
 			return -1;
 		}
 		d->have_backend = 1;
-		if (d->parse_threads < 0) { /* default for the product path: parse ahead on worker threads */
+		if (d->parse_threads < 0) { /* default for the product path: parse ahead on the pool */
 			const char *e = getenv("M2DEC_AMD_PARSE_THREADS");
 			d->parse_threads = e ? atoi(e) : 16; /* profiles/r48*_threads.txt: 14-20 within noise of each other, 12 ~8 % lower */
 		}
@@ -107,12 +255,10 @@ static int alloc_geometry(h264_dec_t *d, int w, int h)
 	return 0;
 }
 
-static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, int work_len)
+static int set_frames_st(h264_dec_t *d, int n, m2d_frame_t *frames, uint8_t *work)
 {
-	h264_dec_t *d = CTX(ctx);
 	const h264_sps_t *s;
-	(void)work_len;
-	if (!d || n < 3 || n > H264D_MAX_FRAME_NUM || !frames || !work) return -1;
+	if (n < 3 || n > H264D_MAX_FRAME_NUM || !frames || !work) return -1;
 	d->num_frames = n;
 	memcpy(d->frames, frames, sizeof(m2d_frame_t) * (size_t)n);
 	memset(d->lru, 0, sizeof(d->lru));
@@ -122,6 +268,17 @@ static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, 
 	if (d->backend.set_frames(d->backend.self, n, d->frames, s->width, s->height) < 0) return -1;
 	d->frames_ready = 1;
 	return 0;
+}
+
+static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, int work_len)
+{
+	h264_dec_t *d = enter(ctx);
+	int r;
+	(void)work_len;
+	if (!d) return -1;
+	r = set_frames_st(d, n, frames, work);
+	leave(d);
+	return r;
 }
 
 /* one slice NAL */
@@ -193,7 +350,9 @@ int h264_decode_loop(h264_dec_t *d)
 			d->nal_replay = 1;
 			return h264_async_close(d);
 		}
-		if (queued && type == 7 && h264_async_drain(d, -1) < 0) return -1; /* set_frames may follow */
+		/* the header callback may free the caller's frames (m2decoder.h:68-77): every closed picture is
+		 * bound first, so that sync_frame can still deliver it from the back end's own staging */
+		if (queued && type == 7 && h264_async_drain(d, -1) < 0) return -1;
 		switch (type) {
 		case 1:
 		case 5:
@@ -231,18 +390,16 @@ int h264_decode_loop(h264_dec_t *d)
 
 static int api_decode_picture(void *ctx)
 {
-	h264_dec_t *d = CTX(ctx);
+	h264_dec_t *d = enter(ctx);
+	int r;
 	if (!d) return -1;
 	d->eos = 0;
 	if (d->as) h264_async_resume(d);
-	return h264_decode_loop(d);
-}
-
-static double mono_s(void)
-{
-	struct timespec ts;
-	clock_gettime(CLOCK_MONOTONIC, &ts);
-	return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+	r = h264_decode_loop(d);
+	d->finished = r == -2;
+	if (d->finished) h264_async_trim(d);
+	leave(d);
+	return r;
 }
 
 static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
@@ -252,6 +409,7 @@ static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
 	if (d->stats) t0 = mono_s();
 	if (d->as && h264_async_drain(d, idx) < 0) return -1; /* the picture in that slot is parsed and submitted */
 	if (d->stats) t1 = mono_s();
+	/* (sync_frame copies the picture into the caller's frame, on this thread, inside this call) */
 	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) return -1;
 	if (d->stats) {
 		d->t_drain += t1 - t0;
@@ -263,20 +421,26 @@ static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
 
 static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d || !frame) return -1;
-	return deliver(d, h264_dpb_peek(&d->dpb, bypass), frame);
+	h264_dec_t *d = enter(ctx);
+	int r;
+	if (!d) return -1;
+	r = frame ? deliver(d, h264_dpb_peek(&d->dpb, bypass), frame) : -1;
+	leave(d);
+	return r;
 }
 
 static int api_get(void *ctx, m2d_frame_t *frame, int bypass)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d || !frame) return -1;
-	return deliver(d, h264_dpb_pop(&d->dpb, bypass), frame);
+	h264_dec_t *d = enter(ctx);
+	int r;
+	if (!d) return -1;
+	r = frame ? deliver(d, h264_dpb_pop(&d->dpb, bypass), frame) : -1;
+	leave(d);
+	return r;
 }
 
 static const m2d_func_table_t h264d_func_ = {
-	sizeof(h264_dec_t),
+	sizeof(h264_handle_t),
 	api_init,
 	api_stream_pos,
 	api_get_info,
@@ -291,53 +455,91 @@ const m2d_func_table_t * const h264d_func = &h264d_func_;
 /* ------------------------------------------------------------------ extra C ABI */
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
 {
-	h264_dec_t *d = CTX(ctx);
+	h264_dec_t *d = enter(ctx);
 	if (!d) return -1;
 	if (!be) { /* detach a borrowed back end without destroying it */
 		d->have_backend = 0;
-		return 0;
+	} else {
+		if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
+		d->backend = *be;
+		d->have_backend = 1;
 	}
-	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
-	d->backend = *be;
-	d->have_backend = 1;
+	leave(d);
 	return 0;
 }
 
 int m2dec_amd_h264_set_parse_threads(void *ctx, int threads)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d || d->as) return -1; /* before the first set_frames */
-	d->parse_threads = threads < 0 ? 0 : threads;
-	return 0;
+	h264_dec_t *d = enter(ctx);
+	int r = -1;
+	if (!d) return -1;
+	if (!d->as) { /* before the first set_frames */
+		d->parse_threads = threads < 0 ? 0 : threads;
+		r = 0;
+	}
+	leave(d);
+	return r;
 }
 
 int m2dec_amd_h264_set_device(void *ctx, int device)
 {
-	CTX(ctx)->device = device;
+	h264_dec_t *d = enter(ctx);
+	if (!d) return -1;
+	d->device = device;
+	leave(d);
 	return 0;
+}
+
+static void state_destroy(h264_dec_t *d)
+{
+	const int stats = d->stats;
+	const double t0 = mono_s();
+	if (stats) fprintf(stderr, "deliver: drain %.3f s, sync_frame %.3f s\n", d->t_drain, d->t_sync);
+	h264_async_stop(d);
+	const double t1 = mono_s();
+	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
+	d->have_backend = 0;
+	const double t2 = mono_s();
+	free(d->mbi);
+	for (int i = 0; i < 17; ++i) free(d->colpic[i].mb);
+	free(d->nal);
+	free(d);
+	if (stats)
+		fprintf(stderr, "state_destroy: pipeline %.2f ms, back end %.2f ms, heap %.2f ms\n", 1e3 * (t1 - t0),
+		        1e3 * (t2 - t1), 1e3 * (mono_s() - t2));
 }
 
 void m2dec_amd_h264_release(void *ctx)
 {
-	h264_dec_t *d = CTX(ctx);
-	if (!d) return;
-	if (d->stats) fprintf(stderr, "deliver: drain %.3f s, sync_frame %.3f s\n", d->t_drain, d->t_sync);
-	h264_async_stop(d);
-	if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
-	d->have_backend = 0;
-	free(d->mbi);
-	d->mbi = NULL;
-	for (int i = 0; i < 17; ++i) {
-		free(d->colpic[i].mb);
-		d->colpic[i].mb = NULL;
-	}
-	free(d->nal);
-	d->nal = NULL;
+	h264_handle_t *h = (h264_handle_t *)ctx;
+	h264_dec_t *d = NULL;
+	if (!h || h->magic != H264_HANDLE_MAGIC) return;
+	pthread_mutex_lock(&reg_mu);
+	for (h264_dec_t **pp = &reg_head; *pp; pp = &(*pp)->reg_next)
+		if (*pp == h->st && (*pp)->gen == h->gen && !(*pp)->in_call) {
+			d = *pp;
+			*pp = d->reg_next;
+			reg_count--;
+			break;
+		}
+	pthread_mutex_unlock(&reg_mu);
+	h->magic = 0;
+	if (d) state_destroy(d);
+}
+
+int m2dec_amd_h264_registry(int *contexts, long *evicted)
+{
+	pthread_mutex_lock(&reg_mu);
+	if (contexts) *contexts = reg_count;
+	if (evicted) *evicted = reg_evicted;
+	pthread_mutex_unlock(&reg_mu);
+	return 0;
 }
 
 /* ------------------------------------------------------------------ stream driver (h264dec.cpp + m2decoder.h) */
 typedef struct {
-	h264_dec_t *d;
+	void *ctx;               /* the caller-side context (a handle, h264d_func->context_size bytes) */
+	h264_dec_t *d;           /* its state, for the driver's statistics */
 	const uint8_t *data;
 	size_t len;
 	size_t pos;
@@ -349,7 +551,6 @@ typedef struct {
 	uint8_t work[64];
 	int extra;               /* frames beyond the decoder's need (held by the caller meanwhile) */
 	size_t frame_size;       /* frame_mem: a block of the frame pool (fpool_take) */
-	int frame_pinned, pin;   /* page-locked / to be page-locked (the built-in HIP back end) */
 	m2dec_hold_t *hold;
 	int failed;
 	double setup_s;
@@ -368,7 +569,7 @@ static int drv_reread(void *arg)
 {
 	driver_t *v = (driver_t *)arg;
 	if (v->pos < v->len) {
-		dec_bits_set_data(v->d->stream, v->data + v->pos, v->len - v->pos, 0);
+		dec_bits_set_data(h264d_func->stream_pos(v->ctx), v->data + v->pos, v->len - v->pos, 0);
 		v->pos = v->len;
 		return 0;
 	}
@@ -376,16 +577,16 @@ static int drv_reread(void *arg)
 }
 
 /* Frame memory of the stream driver outlives a stream (bench steps, a service decoding stream after
- * stream): fresh memory costs page faults, and the HIP back end would page-lock it again (~0.15 ms
- * per 1080p frame).  Blocks used with the built-in HIP back end are page-locked once, for good. */
+ * stream): fresh memory costs page faults.  The frames are plain caller memory — the back end never
+ * writes them asynchronously (sync_frame copies into them inside peek / get), so a block can go back
+ * to the pool as soon as no MD5 thread reads it. */
 static pthread_mutex_t fpool_mu = PTHREAD_MUTEX_INITIALIZER;
 static struct {
 	uint8_t *mem;
 	size_t size;
-	int pinned;
 } fpool[16];
 
-static uint8_t *fpool_take(size_t need, size_t *size, int *pinned)
+static uint8_t *fpool_take(size_t need, size_t *size)
 {
 	uint8_t *m = NULL;
 	pthread_mutex_lock(&fpool_mu);
@@ -393,19 +594,17 @@ static uint8_t *fpool_take(size_t need, size_t *size, int *pinned)
 		if (fpool[i].mem && fpool[i].size >= need) {
 			m = fpool[i].mem;
 			*size = fpool[i].size;
-			*pinned = fpool[i].pinned;
 			fpool[i].mem = NULL;
 		}
 	pthread_mutex_unlock(&fpool_mu);
 	if (!m) {
 		m = (uint8_t *)aligned_alloc(4096, need);
 		*size = need;
-		*pinned = 0;
 	}
 	return m;
 }
 
-static void fpool_give(uint8_t *m, size_t size, int pinned)
+static void fpool_give(uint8_t *m, size_t size)
 {
 	if (!m) return;
 	pthread_mutex_lock(&fpool_mu);
@@ -413,15 +612,11 @@ static void fpool_give(uint8_t *m, size_t size, int pinned)
 		if (!fpool[i].mem) {
 			fpool[i].mem = m;
 			fpool[i].size = size;
-			fpool[i].pinned = pinned;
 			m = NULL;
 			break;
 		}
 	pthread_mutex_unlock(&fpool_mu);
-	if (m) {
-		if (pinned) m2dec_amd_hip_unpin(m);
-		free(m);
-	}
+	free(m);
 }
 
 /* M2Decoder::SetFrames, m2decoder.h:54-80 */
@@ -432,7 +627,7 @@ static int drv_header(void *arg, void *id)
 	int w, h, bufnum;
 	size_t luma_len;
 	(void)id;
-	if (h264d_func->get_info(v->d, &info) < 0) {
+	if (h264d_func->get_info(v->ctx, &info) < 0) {
 		v->failed = 1;
 		return -1;
 	}
@@ -443,13 +638,12 @@ static int drv_header(void *arg, void *id)
 	if (bufnum > H264D_MAX_FRAME_NUM) bufnum = H264D_MAX_FRAME_NUM;
 	if (v->frame_mem && bufnum <= v->nframes && luma_len <= v->luma_len) return 0;
 	if (v->hold) m2dec_hold_wait_idle(v->hold); /* nobody reads the old frames any more */
-	fpool_give(v->frame_mem, v->frame_size, v->frame_pinned);
-	v->frame_mem = fpool_take(((luma_len * 3 / 2 + 4095) & ~(size_t)4095) * (size_t)bufnum, &v->frame_size, &v->frame_pinned);
+	fpool_give(v->frame_mem, v->frame_size);
+	v->frame_mem = fpool_take(((luma_len * 3 / 2 + 4095) & ~(size_t)4095) * (size_t)bufnum, &v->frame_size);
 	if (!v->frame_mem) {
 		v->failed = 1;
 		return -1;
 	}
-	if (v->pin && !v->frame_pinned) v->frame_pinned = m2dec_amd_hip_pin(v->frame_mem, v->frame_size) == 0;
 	{
 		size_t fsz = (luma_len * 3 / 2 + 4095) & ~(size_t)4095;
 		for (int i = 0; i < bufnum; ++i) {
@@ -462,7 +656,7 @@ static int drv_header(void *arg, void *id)
 	v->luma_len = luma_len;
 	{
 		const double t0 = mono_s();
-		if (h264d_func->set_frames(v->d, bufnum, v->frames, v->work, info.additional_size) < 0) v->failed = 1;
+		if (h264d_func->set_frames(v->ctx, bufnum, v->frames, v->work, info.additional_size) < 0) v->failed = 1;
 		v->setup_s += mono_s() - t0;
 		if (v->d->stats) fprintf(stderr, "set_frames: %d frames, %.3f s\n", bufnum, mono_s() - t0);
 	}
@@ -502,52 +696,56 @@ int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t
                             m2dec_amd_stats_t *stats)
 {
 	driver_t v;
-	h264_dec_t *d = (h264_dec_t *)calloc(1, h264d_func->context_size);
+	void *ctx = calloc(1, h264d_func->context_size);
+	h264_dec_t *d;
 	m2d_frame_t frm;
 	int err = 0, n = 0;
-	if (!d) return -1;
+	if (!ctx) return -1;
 	memset(&v, 0, sizeof(v));
-	v.d = d;
+	v.ctx = ctx;
 	v.data = data;
 	v.len = len;
 	v.on_frame = on_frame;
 	v.arg = arg;
 	v.extra = extra;
 	v.hold = hold;
-	v.pin = backend == NULL;
-	h264d_func->init(d, dpb, drv_header, &v);
+	if (h264d_func->init(ctx, dpb, drv_header, &v) < 0 || !(d = h264_state(ctx))) {
+		free(ctx);
+		return -1;
+	}
+	v.d = d;
 	d->hold = hold;
 	d->device = device;
-	if (backend) m2dec_amd_h264_set_backend(d, backend);
-	if (parse_threads >= 0) m2dec_amd_h264_set_parse_threads(d, parse_threads);
-	dec_bits_set_callback(d->stream, drv_reread, &v);
+	if (backend) m2dec_amd_h264_set_backend(ctx, backend);
+	if (parse_threads >= 0) m2dec_amd_h264_set_parse_threads(ctx, parse_threads);
+	dec_bits_set_callback(h264d_func->stream_pos(ctx), drv_reread, &v);
 	const double t_start = mono_s();
 	v.t_last = t_start;
 	/* h264dec.cpp:251-257 + M2Decoder::decode / decode_residual (m2decoder.h:132-157) */
 	for (;;) {
 		err = 0;
-		while (h264d_func->peek_decoded_frame(d, &frm, 0) <= 0) {
-			err = h264d_func->decode_picture(d);
+		while (h264d_func->peek_decoded_frame(ctx, &frm, 0) <= 0) {
+			err = h264d_func->decode_picture(ctx);
 			if (v.failed) { err = -1; break; }
 			if (err < 0) {
-				while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
+				while (h264d_func->peek_decoded_frame(ctx, &frm, 1) > 0) {
 					emit(&v, &frm);
 					n++;
-					h264d_func->get_decoded_frame(d, &frm, 1);
+					h264d_func->get_decoded_frame(ctx, &frm, 1);
 				}
 				goto done;
 			}
 		}
-		h264d_func->get_decoded_frame(d, &frm, 0);
+		h264d_func->get_decoded_frame(ctx, &frm, 0);
 		if (d->stats && n == 0) fprintf(stderr, "first frame out: %.3f s\n", mono_s() - t_start);
 		emit(&v, &frm);
 		n++;
-		err = h264d_func->decode_picture(d);
+		err = h264d_func->decode_picture(ctx);
 		if (err < 0) {
-			while (h264d_func->peek_decoded_frame(d, &frm, 1) > 0) {
+			while (h264d_func->peek_decoded_frame(ctx, &frm, 1) > 0) {
 				emit(&v, &frm);
 				n++;
-				h264d_func->get_decoded_frame(d, &frm, 1);
+				h264d_func->get_decoded_frame(ctx, &frm, 1);
 			}
 			break;
 		}
@@ -563,6 +761,8 @@ done:
 			stats->alg_bytes = t.frame_bytes + t.ref_bytes + t.record_bytes;
 			stats->h2d_us = t.h2d_us;
 			stats->d2h_us = t.d2h_us;
+			stats->d2h_bytes = t.d2h_bytes;
+			stats->host_copy_us = t.host_copy_us;
 		}
 	}
 	if (stats) {
@@ -580,11 +780,15 @@ done:
 		stats->t_end = v.t_last;
 		stats->setup_s = v.setup_s;
 	}
-	if (backend) d->have_backend = 0; /* borrowed: the caller destroys it */
-	m2dec_amd_h264_release(d);
-	free(d);
+	if (backend) m2dec_amd_h264_set_backend(ctx, NULL); /* borrowed: the caller destroys it */
+	{
+		const double t0 = mono_s();
+		m2dec_amd_h264_release(ctx);
+		if (stats) stats->teardown_s = mono_s() - t0;
+	}
+	free(ctx);
 	if (hold) m2dec_hold_wait_idle(hold);
-	fpool_give(v.frame_mem, v.frame_size, v.frame_pinned);
+	fpool_give(v.frame_mem, v.frame_size);
 	return (err == -2) ? n : -1;
 }
 

@@ -113,19 +113,22 @@ typedef struct {
 } nal_ent_t;
 
 struct h264_async {
-	pthread_mutex_t mu;
-	pthread_cond_t cv_work, cv_done;
-	pthread_t th[16];
-	int nth, quit, depth;
+	pthread_mutex_t *mu;      /* the parse pool's mutex (g_parse.mu): it guards every pipeline's job state */
+	pthread_cond_t cv_done;
+	struct h264_async *pnext; /* the pool's list of pipelines */
+	h264_dec_t *api;          /* the API context (library memory: the caller's context is only a handle) */
+	int nth;                  /* pool workers this pipeline may occupy at once */
+	int running;              /* pool workers inside one of its jobs or slices */
+	int quit, depth;
 	h264_job_t *fifo[AS_MAX]; /* dispatched, not yet submitted: [tail, head); job seq s at fifo[s % AS_MAX] */
 	long head, tail;          /* tail: oldest job not retired (submitted, and bound when decoding ahead) */
 	long sub;                 /* next job to submit: [tail, sub) submitted */
 	long bnd;                 /* decode ahead: next job to bind: [tail, bnd) bound */
 	int ahead;                /* decode ahead: the back end has bind (M2R_PIC_VIRTUAL submissions) */
-	pthread_t sub_th;         /* decode ahead: the submitter thread */
-	int sub_quit, sub_err;
+	int driving;              /* decode ahead: a thread is inside pipe_drive (back-end calls are serial) */
+	int sub_err;
 	int ahead_all;            /* M2DEC_AMD_AHEAD_ALL (tests): the API context closes a picture only after the
-	                             submitter took it, so every picture goes ahead whatever the thread timing */
+	                             pipe_drive submitted it, so every picture goes ahead whatever the thread timing */
 	long la_sps_nal;          /* NAL index of the last SPS the lookahead context read (-1: none) */
 	long api_sps_nal;         /* NAL index of the last SPS whose header callback the API context ran */
 	h264_job_t *queue[AS_MAX]; /* dispatched; [qtail, qhead) holds every job not yet taken */
@@ -160,6 +163,24 @@ struct h264_async {
 	int slice_par;            /* M2DEC_AMD_SLICE_PAR (default 1): slices of a picture on several workers */
 	long n_par, n_par_fallback; /* pictures parsed slice-parallel / re-parsed sequentially after a try */
 };
+
+/* The parse pool: one set of worker threads per process, shared by every decoder's pipeline (a
+ * decoder context owns no thread, so a context the caller drops leaves none behind, and N streams
+ * decoded at once do not oversubscribe the host with N private pools).  Workers take the oldest
+ * ready job (or a slice of a picture parsed slice-parallel) of any pipeline, round robin over the
+ * pipelines, each pipeline capped at its own `nth` workers at a time.  Threads are created on
+ * demand (up to the largest `nth` asked for) and live for the process. */
+#define POOL_MAX 64
+static struct {
+	pthread_mutex_t mu;
+	pthread_cond_t cv_work;
+	pthread_t th[POOL_MAX];
+	int nth;
+	struct h264_async *pipes; /* registered pipelines */
+	struct h264_async *rr;    /* the pipeline to look at first next time */
+} g_parse = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, {0}, 0, NULL, NULL};
+
+static void pipe_drive(struct h264_async *as);
 
 static int job_arena(h264_job_t *j, int wm, int hm)
 {
@@ -226,6 +247,21 @@ static void job_free(h264_job_t *j)
 	free(j->arena);
 	free(j->w);
 	free(j);
+}
+
+/* Jobs (each with a record arena of ~1 KB per MB) outlive a pipeline: a context's jobs go back to a
+ * process-wide pool when it stops or reaches the end of its stream, and the next context takes them —
+ * no allocation or page faults while decoding, no frees when a context goes.  Mutex: g_parse.mu. */
+#define JOB_POOL_MAX 96
+static h264_job_t *g_jobs[JOB_POOL_MAX];
+static int g_njobs;
+
+static void job_release(h264_job_t *j) /* (mutex held) */
+{
+	if (!j) return;
+	job_clear(j);
+	if (g_njobs < JOB_POOL_MAX) g_jobs[g_njobs++] = j;
+	else job_free(j);
 }
 
 /* ---------------------------------------------------------------- worker */
@@ -336,7 +372,14 @@ static int job_run_par(struct h264_async *as, h264_job_t *j)
 		free(j->sret);
 		j->spic = (m2r_picture_t *)malloc(sizeof(m2r_picture_t) * (size_t)nsl);
 		j->sret = (int *)malloc(sizeof(int) * (size_t)nsl);
-		if (!j->spic || !j->sret) {
+		if (!j->spic || !j->sret) { /* (keep sw[] and capsw consistent for job_free) */
+			free(j->spic);
+			free(j->sret);
+			j->spic = NULL;
+			j->sret = NULL;
+			for (int k = 0; k < j->capsw; ++k) free(j->sw[k]);
+			free(j->sw);
+			j->sw = NULL;
 			j->capsw = 0;
 			return -1;
 		}
@@ -350,31 +393,31 @@ static int job_run_par(struct h264_async *as, h264_job_t *j)
 		j->mbi[i].slice = -1;
 	}
 	/* offer the slices to idle workers; this worker takes them too, and waits for the rest */
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	if (as->npar >= 16) {
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		return -1;
 	}
 	j->sl_next = 0;
 	j->sl_done = 0;
 	as->par[as->npar++] = j;
-	pthread_cond_broadcast(&as->cv_work);
+	pthread_cond_broadcast(&g_parse.cv_work);
 	while (j->sl_next < nsl) {
 		const int k = j->sl_next++;
 		if (j->sl_next == nsl)
 			for (int i = 0; i < as->npar; ++i)
 				if (as->par[i] == j) as->par[i] = as->par[--as->npar];
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		slice_run(j, k);
-		pthread_mutex_lock(&as->mu);
+		pthread_mutex_lock(as->mu);
 		j->sl_done++;
 	}
 	{
 		const double tw = now_s();
-		while (j->sl_done < nsl) pthread_cond_wait(&as->cv_done, &as->mu);
+		while (j->sl_done < nsl) pthread_cond_wait(&as->cv_done, as->mu);
 		as->t_parse -= now_s() - tw; /* the worker's job time counts parse work only */
 	}
-	pthread_mutex_unlock(&as->mu);
+	pthread_mutex_unlock(as->mu);
 
 	/* every slice parsed exactly its MB range, in order, the last one ending the picture */
 	for (int k = 0; k < nsl; ++k) {
@@ -443,70 +486,109 @@ static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err
 	return 1;
 }
 
-/* Workers take the oldest queued job whose dependencies have finished, so a B picture waiting for
- * its co-located P does not hold a worker while later P pictures could be parsed. */
-static void *worker(void *arg)
+/* A ready job (or a slice to help with) of pipeline `as`, marked taken; NULL if none.  Mutex held. */
+static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *slice_k, int *dep_err)
 {
-	struct h264_async *as = (struct h264_async *)arg;
-	pthread_mutex_lock(&as->mu);
+	*slice_of = NULL;
+	/* a slice of a picture parsed slice-parallel first: that picture is already under way */
+	if (as->npar) {
+		h264_job_t *pj = as->par[0];
+		*slice_k = pj->sl_next++;
+		if (pj->sl_next == pj->nsl) as->par[0] = as->par[--as->npar];
+		*slice_of = pj;
+		return NULL;
+	}
+	/* a taken job leaves the queue at once (its entry is cleared): once finished and retired it is
+	 * recycled for a later picture, and a stale entry would hand that one out half built */
+	while (as->qtail < as->qhead && !as->queue[as->qtail % AS_MAX]) as->qtail++;
+	for (long k = as->qtail; k < as->qhead; ++k) {
+		h264_job_t *c = as->queue[k % AS_MAX];
+		*dep_err = 0;
+		if (c && deps_ready(as, c, dep_err)) {
+			c->taken = 1;
+			as->queue[k % AS_MAX] = NULL;
+			return c;
+		}
+	}
+	return NULL;
+}
+
+/* Pool workers take the oldest queued job whose dependencies have finished, so a B picture waiting
+ * for its co-located P does not hold a worker while later P pictures could be parsed; pipelines are
+ * served round robin.  A finished job may let its pipeline submit: the worker drives it. */
+static void *pool_worker(void *arg)
+{
+	(void)arg;
+	pthread_mutex_lock(&g_parse.mu);
 	for (;;) {
-		h264_job_t *j = NULL;
-		int dep_err = 0;
-		for (;;) {
-			/* a slice of a picture parsed slice-parallel first: that picture is already under way */
-			if (as->npar) {
-				h264_job_t *pj = as->par[0];
-				const int k = pj->sl_next++;
-				if (pj->sl_next == pj->nsl) as->par[0] = as->par[--as->npar];
-				pthread_mutex_unlock(&as->mu);
-				const double ts = now_s();
-				slice_run(pj, k);
-				const double te = now_s();
-				pthread_mutex_lock(&as->mu);
-				as->t_parse += te - ts;
-				pj->sl_done++;
-				pthread_cond_broadcast(&as->cv_done);
-				continue;
+		struct h264_async *as = NULL, *first = g_parse.rr ? g_parse.rr : g_parse.pipes;
+		h264_job_t *j = NULL, *pj = NULL;
+		int k = 0, dep_err = 0;
+		for (struct h264_async *p = first; p && !j && !pj;) {
+			if (!p->quit && p->running < p->nth) {
+				j = pick_job(p, &pj, &k, &dep_err);
+				if (j || pj) as = p;
 			}
-			while (as->qtail < as->qhead && as->queue[as->qtail % AS_MAX]->taken) as->qtail++;
-			for (long k = as->qtail; k < as->qhead && !j; ++k) {
-				h264_job_t *c = as->queue[k % AS_MAX];
-				dep_err = 0;
-				if (!c->taken && deps_ready(as, c, &dep_err)) j = c;
-			}
-			if (j || (as->quit && as->qtail == as->qhead)) break;
-			pthread_cond_wait(&as->cv_work, &as->mu);
+			p = p->pnext ? p->pnext : g_parse.pipes;
+			if (p == first) break;
 		}
-		if (!j) break;
-		j->taken = 1;
-		pthread_mutex_unlock(&as->mu);
-		const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
-		if (dep_err) j->err = 1;
-		else if (!(as->slice_par && j->nsl > 1)) job_run(j);
-		else if (job_run_par(as, j) < 0) {
-			job_run(j);
-			__atomic_fetch_add(&as->n_par_fallback, 1, __ATOMIC_RELAXED);
+		if (!as) {
+			pthread_cond_wait(&g_parse.cv_work, &g_parse.mu);
+			continue;
+		}
+		g_parse.rr = as->pnext;
+		as->running++;
+		pthread_mutex_unlock(&g_parse.mu);
+		if (pj) {
+			const double ts = now_s();
+			slice_run(pj, k);
+			const double te = now_s();
+			pthread_mutex_lock(&g_parse.mu);
+			as->t_parse += te - ts;
+			pj->sl_done++;
 		} else {
-			__atomic_fetch_add(&as->n_par, 1, __ATOMIC_RELAXED);
-		}
-		pthread_mutex_lock(&as->mu);
-		{
+			const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
+			if (dep_err) j->err = 1;
+			else if (!(as->slice_par && j->nsl > 1)) job_run(j);
+			else if (job_run_par(as, j) < 0) {
+				job_run(j);
+				__atomic_fetch_add(&as->n_par_fallback, 1, __ATOMIC_RELAXED);
+			} else {
+				__atomic_fetch_add(&as->n_par, 1, __ATOMIC_RELAXED);
+			}
+			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
 			as->t_parse += te - tp;
 			if (as->stats > 1)
 				fprintf(stderr, "job %ld type %d slices %d: start %.1f ms, parse %.2f ms\n", j->seq,
 				        j->snap[0]->sh.slice_type, j->nsl, 1e3 * (tp - as->t0), 1e3 * (te - tp));
+			j->done = 1;
+			pthread_cond_broadcast(&g_parse.cv_work); /* jobs waiting on this one may be ready */
 		}
-		j->done = 1;
+		as->running--;
 		pthread_cond_broadcast(&as->cv_done);
-		pthread_cond_broadcast(&as->cv_work); /* jobs waiting on this one may be ready */
+		if (j) pipe_drive(as);
 	}
-	pthread_mutex_unlock(&as->mu);
 	return NULL;
 }
 
+/* at least n pool workers (mutex held) */
+static int pool_grow(int n)
+{
+	if (n > POOL_MAX) n = POOL_MAX;
+	while (g_parse.nth < n) {
+		pthread_attr_t at;
+		pthread_attr_init(&at);
+		pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+		const int e = pthread_create(&g_parse.th[g_parse.nth], &at, pool_worker, NULL);
+		pthread_attr_destroy(&at);
+		if (e != 0) break;
+		g_parse.nth++;
+	}
+	return g_parse.nth;
+}
+
 /* ---------------------------------------------------------------- start / stop */
-static void *submitter(void *arg);
 
 static void la_free(h264_dec_t *la)
 {
@@ -525,7 +607,7 @@ int h264_async_start(h264_dec_t *d, int threads)
 	struct h264_async *as;
 	h264_dec_t *la;
 	if (threads <= 0) return 0;
-	if (threads > 16) threads = 16;
+	if (threads > POOL_MAX) threads = POOL_MAX;
 	as = (struct h264_async *)calloc(1, sizeof(*as));
 	la = (h264_dec_t *)malloc(sizeof(h264_dec_t));
 	if (!as || !la) {
@@ -552,8 +634,8 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->nq = (nal_ent_t *)calloc((size_t)as->nq_cap, sizeof(nal_ent_t));
 	if (!as->nq) goto fail;
 	for (int i = 0; i < 64; ++i) as->vmap[i] = -1;
-	pthread_mutex_init(&as->mu, NULL);
-	pthread_cond_init(&as->cv_work, NULL);
+	as->mu = &g_parse.mu;
+	as->api = d;
 	pthread_cond_init(&as->cv_done, NULL);
 	as->depth = 2 * threads + 8;
 	{
@@ -567,15 +649,19 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->stats = getenv("M2DEC_AMD_ASYNC_STATS") ? atoi(getenv("M2DEC_AMD_ASYNC_STATS")) : 0;
 	as->slice_par = !getenv("M2DEC_AMD_SLICE_PAR") || atoi(getenv("M2DEC_AMD_SLICE_PAR")) != 0;
 	as->t0 = now_s();
-	for (int i = 0; i < threads; ++i) {
-		if (pthread_create(&as->th[i], NULL, worker, as) != 0) break;
-		as->nth++;
-	}
-	if (!as->nth) goto fail;
 	as->api_sps_nal = -1;
 	as->ahead_all = getenv("M2DEC_AMD_AHEAD_ALL") && atoi(getenv("M2DEC_AMD_AHEAD_ALL"));
+	pthread_mutex_lock(&g_parse.mu);
+	as->nth = pool_grow(threads) < threads ? g_parse.nth : threads;
+	if (as->nth <= 0) {
+		pthread_mutex_unlock(&g_parse.mu);
+		pthread_cond_destroy(&as->cv_done);
+		goto fail;
+	}
+	as->pnext = g_parse.pipes;
+	g_parse.pipes = as;
+	pthread_mutex_unlock(&g_parse.mu);
 	d->as = as;
-	if (as->ahead && pthread_create(&as->sub_th, NULL, submitter, d) != 0) as->ahead = 0;
 	return 0;
 fail:
 	free(as->nq);
@@ -592,11 +678,11 @@ double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback)
 	double t;
 	*par = *par_fallback = 0;
 	if (!as) return 0.0;
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	t = as->t_parse;
 	*par = as->n_par;
 	*par_fallback = as->n_par_fallback;
-	pthread_mutex_unlock(&as->mu);
+	pthread_mutex_unlock(as->mu);
 	return t;
 }
 
@@ -610,32 +696,54 @@ void h264_async_stop(h264_dec_t *d)
 		                "parse %.3f s\n",
 		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
 		        as->t_parse);
-	pthread_mutex_lock(&as->mu);
+	/* no pool worker starts anything of this pipeline any more; wait for the ones inside it */
+	pthread_mutex_lock(as->mu);
 	as->quit = 1;
-	as->sub_quit = 1;
-	pthread_cond_broadcast(&as->cv_work);
-	pthread_cond_broadcast(&as->cv_done);
-	pthread_mutex_unlock(&as->mu);
-	if (as->ahead) pthread_join(as->sub_th, NULL);
-	for (int i = 0; i < as->nth; ++i) pthread_join(as->th[i], NULL);
-	for (long i = as->tail; i < as->head; ++i) job_free(as->fifo[i % AS_MAX]);
-	job_free(as->cur);
-	for (int i = 0; i < as->nfree; ++i) job_free(as->free_jobs[i]);
+	while (as->running || as->driving) pthread_cond_wait(&as->cv_done, as->mu);
+	for (struct h264_async **pp = &g_parse.pipes; *pp; pp = &(*pp)->pnext)
+		if (*pp == as) {
+			*pp = as->pnext;
+			break;
+		}
+	if (g_parse.rr == as) g_parse.rr = NULL;
+	for (long i = as->tail; i < as->head; ++i) job_release(as->fifo[i % AS_MAX]);
+	job_release(as->cur);
+	for (int i = 0; i < as->nfree; ++i) job_release(as->free_jobs[i]);
+	pthread_mutex_unlock(as->mu);
 	for (long i = 0; i < as->nq_cap; ++i) free(as->nq[i].buf);
 	for (int i = 0; i < as->nspare; ++i) free(as->spare[i].mb);
 	free(as->nq);
 	la_free(as->la);
-	pthread_mutex_destroy(&as->mu);
-	pthread_cond_destroy(&as->cv_work);
 	pthread_cond_destroy(&as->cv_done);
 	free(as);
 	d->as = NULL;
+}
+
+/* The stream ended (decode_picture returned -2): the retired jobs (record arenas of about 1 KB per MB
+ * each) go back to the process pool, the co-located spares are freed.  A context the caller drops at
+ * the end of its stream then holds little host memory until the registry reclaims it.  (The lookahead context's co-located stores stay: temporal / spatial
+ * direct of a continuation reads them.) */
+void h264_async_trim(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	int idle;
+	if (!as) return;
+	pthread_mutex_lock(as->mu);
+	for (int i = 0; i < as->nfree; ++i) job_release(as->free_jobs[i]);
+	as->nfree = 0;
+	idle = as->head == as->tail;
+	pthread_mutex_unlock(as->mu);
+	if (idle) { /* no job may still read a spare (the lookahead runs on this thread) */
+		for (int i = 0; i < as->nspare; ++i) free(as->spare[i].mb);
+		as->nspare = 0;
+	}
 }
 
 static h264_job_t *job_get(struct h264_async *as)
 {
 	h264_job_t *j;
 	if (as->nfree) return as->free_jobs[--as->nfree];
+	if (g_njobs) return g_jobs[--g_njobs];
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
 	j->slot = -1;
@@ -661,12 +769,13 @@ static void job_put(struct h264_async *as, h264_job_t *j)
  * the back end once the API context closed it, its virtual ids translated to the frame slots of
  * that moment (j->map), and retires at once.
  *
- * With bind (decode ahead) a submitter thread owns every back-end call but sync_frame: it submits
- * each parsed job as it is, virtual ids naming the back end's picture buffers, as soon as the rules
- * below allow — possibly long before the API context reaches it — and binds closed jobs' buffers to
- * the frame slots the API context chose, in order.  The caller's thread only closes pictures and,
- * to hand a frame out, waits until its job is bound (h264_async_drain) before sync_frame.  The record
- * copies and the HIP calls leave the caller's thread, the one serial stage of the pipeline. */
+ * With bind (decode ahead) pipe_drive makes every back-end call but sync_frame: it submits each
+ * parsed job as it is, virtual ids naming the back end's picture buffers, as soon as the rules below
+ * allow — possibly long before the API context reaches it — and binds closed jobs' buffers to the
+ * frame slots the API context chose, in order.  It runs mostly on the pool worker that finished a
+ * job, so the record copies and the HIP calls stay off the caller's thread; the caller's thread
+ * closes pictures and, to hand a frame out, waits until its job is bound (h264_async_drain) before
+ * sync_frame. */
 
 /* records into the back end's arena (virtual ids as they are, or translated to slots) + submit */
 static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
@@ -719,20 +828,20 @@ static int submit_next(h264_dec_t *d)
 	h264_job_t *j = as->fifo[as->sub % AS_MAX];
 	const double t0 = as->stats ? now_s() : 0;
 	int err;
-	pthread_mutex_lock(&as->mu);
-	while (!j->done) pthread_cond_wait(&as->cv_done, &as->mu);
-	pthread_mutex_unlock(&as->mu);
+	pthread_mutex_lock(as->mu);
+	while (!j->done) pthread_cond_wait(&as->cv_done, as->mu);
+	pthread_mutex_unlock(as->mu);
 	if (as->stats) as->t_done_wait += now_s() - t0;
 	err = j->err || copy_submit(d, j, 0);
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	as->sub++;
 	as->tail++; /* workers scan [tail, head) under the mutex */
 	job_put(as, j);
-	pthread_mutex_unlock(&as->mu);
+	pthread_mutex_unlock(as->mu);
 	return err ? -1 : 0;
 }
 
-/* ---- decode ahead: the submitter thread */
+/* ---- decode ahead */
 /* a parsed job the API context has not closed yet may go to the back end now: no header callback
  * (set_frames) the API context has not run yet lies before it, and the previous picture of its
  * virtual buffer is bound (so the back end orders the overwrite after that copy-out).  Mutex held. */
@@ -746,19 +855,25 @@ static int ahead_ok(const struct h264_async *as, const h264_job_t *j)
 	return 1;
 }
 
-static void *submitter(void *arg)
+/* Decode ahead: make every step the state allows — bind the oldest closed, submitted job (and retire
+ * what is bound), or submit the next parsed job that is closed or allowed ahead.  There is no
+ * submitter thread: whoever changes what is possible (a pool worker that finished a job, the API
+ * context closing a picture or running a header callback, a thread about to wait for a bind) calls
+ * this, and the first one in does the back-end calls (serially) until nothing is left; the others
+ * return at once — the state is re-checked under the mutex before the driver leaves, so no step is
+ * lost.  Mutex held on entry and on return. */
+static void pipe_drive(struct h264_async *as)
 {
-	h264_dec_t *d = (h264_dec_t *)arg;
-	struct h264_async *as = d->as;
-	pthread_mutex_lock(&as->mu);
-	while (!as->sub_quit) {
+	h264_dec_t *d = as->api;
+	if (!as->ahead || as->driving || as->quit) return;
+	as->driving = 1;
+	while (!as->quit) { /* (a context being released stops after the back-end call under way) */
 		if (as->bnd < as->sub && as->bnd < as->a_seq) {
-			/* bind the oldest closed, submitted job; retire what is bound */
 			h264_job_t *j = as->fifo[as->bnd % AS_MAX];
 			const int skip = j->sub_err, vid = j->vid & 63, slot = j->slot;
-			pthread_mutex_unlock(&as->mu);
+			pthread_mutex_unlock(as->mu);
 			const int err = !skip && d->backend.bind(d->backend.self, vid, slot) < 0;
-			pthread_mutex_lock(&as->mu);
+			pthread_mutex_lock(as->mu);
 			j->bound = 1;
 			as->sub_err += err;
 			as->bnd++;
@@ -771,13 +886,13 @@ static void *submitter(void *arg)
 			continue;
 		}
 		if (as->sub < as->head) {
-			/* submit the next parsed job: closed, or allowed ahead */
 			h264_job_t *j = as->fifo[as->sub % AS_MAX];
 			if (j->done && (as->sub < as->a_seq || ahead_ok(as, j))) {
 				const int ahead = as->sub >= as->a_seq;
-				pthread_mutex_unlock(&as->mu);
+				pthread_mutex_unlock(as->mu);
+				if (as->stats > 1 && j->err) fprintf(stderr, "job %ld: parse error, not submitted\n", j->seq);
 				const int err = j->err || copy_submit(d, j, 1);
-				pthread_mutex_lock(&as->mu);
+				pthread_mutex_lock(as->mu);
 				j->sub_err = err;
 				j->submitted = 1;
 				as->sub_err += err;
@@ -787,10 +902,10 @@ static void *submitter(void *arg)
 				continue;
 			}
 		}
-		pthread_cond_wait(&as->cv_done, &as->mu);
+		break;
 	}
-	pthread_mutex_unlock(&as->mu);
-	return NULL;
+	as->driving = 0;
+	pthread_cond_broadcast(&as->cv_done);
 }
 
 /* a submission or bind failed since the last call: report it once (mutex held) */
@@ -816,33 +931,37 @@ int h264_async_drain(h264_dec_t *d, int slot)
 		return 0;
 	}
 	const double t0 = as->stats ? now_s() : 0;
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	for (long i = as->tail; i < as->a_seq; ++i)
 		if (slot < 0 || as->fifo[i % AS_MAX]->slot == slot) upto = i;
-	while (as->bnd <= upto) pthread_cond_wait(&as->cv_done, &as->mu);
+	while (as->bnd <= upto) {
+		pipe_drive(as);
+		if (as->bnd > upto) break;
+		pthread_cond_wait(&as->cv_done, as->mu);
+	}
 	const int err = take_error(as);
-	pthread_mutex_unlock(&as->mu);
+	pthread_mutex_unlock(as->mu);
 	if (as->stats) as->t_done_wait += now_s() - t0;
 	return err;
 }
 
 /* without bind: submit, in order and without waiting, closed jobs whose parse finished.  Decoding
- * ahead the submitter does that; report its errors */
+ * ahead pipe_drive does that; report its errors */
 static int submit_ready(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
 	if (as->ahead) {
-		pthread_mutex_lock(&as->mu);
+		pthread_mutex_lock(as->mu);
 		const int err = take_error(as);
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		return err;
 	}
 	for (;;) {
 		int ready;
 		if (as->sub >= as->a_seq) return 0;
-		pthread_mutex_lock(&as->mu);
+		pthread_mutex_lock(as->mu);
 		ready = as->fifo[as->sub % AS_MAX]->done;
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		if (!ready) return 0;
 		if (submit_next(d) < 0) return -1;
 	}
@@ -852,10 +971,10 @@ static int submit_ready(h264_dec_t *d)
 void h264_async_api_sps(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	as->api_sps_nal = as->nq_tail - 1;
-	pthread_cond_broadcast(&as->cv_done);
-	pthread_mutex_unlock(&as->mu);
+	pipe_drive(as);
+	pthread_mutex_unlock(as->mu);
 }
 
 /* ---------------------------------------------------------------- lookahead context */
@@ -874,10 +993,14 @@ static void pump(h264_dec_t *d, int until_nal)
 		/* job slots: submit what the API context closed before dispatching more */
 		if (as->ahead) {
 			int full;
-			pthread_mutex_lock(&as->mu);
-			while (as->head - as->tail >= AS_MAX - 2 && as->tail < as->a_seq) pthread_cond_wait(&as->cv_done, &as->mu);
+			pthread_mutex_lock(as->mu);
+			while (as->head - as->tail >= AS_MAX - 2 && as->tail < as->a_seq) {
+				pipe_drive(as);
+				if (as->head - as->tail < AS_MAX - 2) break;
+				pthread_cond_wait(&as->cv_done, as->mu);
+			}
 			full = as->head - as->tail >= AS_MAX - 2;
-			pthread_mutex_unlock(&as->mu);
+			pthread_mutex_unlock(as->mu);
 			if (full) break;
 		} else {
 			while (as->head - as->tail >= AS_MAX - 2 && as->sub < as->a_seq)
@@ -965,10 +1088,11 @@ void h264_async_la_sps(h264_dec_t *la)
 int h264_async_sps(h264_dec_t *la)
 {
 	struct h264_async *as = la->as;
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
+	/* (a job below the tail is retired — and its object maybe recycled: do not look at it again) */
 	for (long i = as->tail; i < as->head; ++i)
-		while (!as->fifo[i % AS_MAX]->done) pthread_cond_wait(&as->cv_done, &as->mu);
-	pthread_mutex_unlock(&as->mu);
+		while (i >= as->tail && !as->fifo[i % AS_MAX]->done) pthread_cond_wait(&as->cv_done, as->mu);
+	pthread_mutex_unlock(as->mu);
 	return 0;
 }
 
@@ -979,9 +1103,9 @@ int h264_async_add_slice(h264_dec_t *la)
 	h264_job_t *j = as->cur;
 	const double ts = as->stats ? now_s() : 0;
 	if (!j) {
-		pthread_mutex_lock(&as->mu); /* (the submitter thread recycles jobs) */
+		pthread_mutex_lock(as->mu); /* (pipe_drive recycles jobs) */
 		j = job_get(as);
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		if (!j || job_arena(j, la->mb_w, la->mb_h) < 0) return -1;
 		j->vid = la->curr_idx;
 		j->slot = -1;
@@ -1076,9 +1200,9 @@ static int la_close(h264_dec_t *la)
 		const int c = j->col_store;
 		const long last = as->col_last[c];
 		long tail;
-		pthread_mutex_lock(&as->mu); /* (the submitter thread moves the tail) */
+		pthread_mutex_lock(as->mu); /* (pipe_drive moves the tail) */
 		tail = as->tail;
-		pthread_mutex_unlock(&as->mu);
+		pthread_mutex_unlock(as->mu);
 		if (last >= tail) {
 			const double tw = as->stats ? now_s() : 0;
 			h264_colmb_t *nb = col_spare_get(as, la->n_mbs, tail);
@@ -1096,13 +1220,10 @@ static int la_close(h264_dec_t *la)
 				la->colpic[c].mb = nb;
 				for (int k = 0; k < j->nsl; ++k) j->snap[k]->colpic[c].mb = nb;
 			} else {
-				pthread_mutex_lock(&as->mu);
-				for (long i = as->tail; i < as->head; ++i) {
-					h264_job_t *o = as->fifo[i % AS_MAX];
-					if (o->seq <= last)
-						while (!o->done) pthread_cond_wait(&as->cv_done, &as->mu);
-				}
-				pthread_mutex_unlock(&as->mu);
+				pthread_mutex_lock(as->mu);
+				for (long i = as->tail; i < as->head && i <= last; ++i) /* (jobs seq = fifo index) */
+					while (i >= as->tail && !as->fifo[i % AS_MAX]->done) pthread_cond_wait(&as->cv_done, as->mu);
+				pthread_mutex_unlock(as->mu);
 			}
 			if (as->stats) as->t_col_wait += now_s() - tw;
 		}
@@ -1113,14 +1234,14 @@ static int la_close(h264_dec_t *la)
 	la->pic = NULL;
 	if (h264_picture_mark(la) < 0) return -1;
 	/* dispatch */
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	as->fifo[as->head % AS_MAX] = j;
 	as->head++;
 	as->seq++;
 	as->queue[as->qhead % AS_MAX] = j;
 	as->qhead++;
-	pthread_cond_signal(&as->cv_work);
-	pthread_mutex_unlock(&as->mu);
+	pthread_cond_broadcast(&g_parse.cv_work);
+	pthread_mutex_unlock(as->mu);
 	return 1;
 }
 
@@ -1141,13 +1262,17 @@ static int api_close(h264_dec_t *d)
 	if (h264_picture_mark(d) < 0) return -1;
 	as->vmap[j->vid & 63] = (int8_t)d->curr_idx;
 	memcpy(j->map, as->vmap, sizeof(j->map));
-	pthread_mutex_lock(&as->mu);
+	pthread_mutex_lock(as->mu);
 	if (as->ahead && as->ahead_all)
-		while (!j->submitted && !(j->done && j->err)) pthread_cond_wait(&as->cv_done, &as->mu);
+		while (!j->submitted && !(j->done && j->err)) {
+			pipe_drive(as);
+			if (j->submitted) break;
+			pthread_cond_wait(&as->cv_done, as->mu);
+		}
 	j->slot = d->curr_idx;
 	as->a_seq++;
-	pthread_cond_broadcast(&as->cv_done); /* (decode ahead: the submitter binds it) */
-	pthread_mutex_unlock(&as->mu);
+	pipe_drive(as); /* (decode ahead: bind it, and submit what that allows) */
+	pthread_mutex_unlock(as->mu);
 	pump(d, 0);
 	if (submit_ready(d) < 0) return -1;
 	return 1;

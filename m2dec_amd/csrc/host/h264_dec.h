@@ -357,6 +357,14 @@ struct h264_dec {
 	int vid_next;            /* lookahead: round-robin cursor of the virtual frame id allocator */
 	int stats;               /* M2DEC_AMD_ASYNC_STATS: time spent delivering frames */
 	double t_drain, t_sync;
+
+	/* process registry (h264_api.c): the caller's context memory holds only a handle naming this state */
+	const void *owner;       /* the caller's context address this state was initialised on */
+	uint64_t gen;            /* handle generation */
+	struct h264_dec *reg_next;
+	int in_call;             /* API calls in progress (registry mutex) */
+	double last_call;        /* CLOCK_MONOTONIC seconds of the last API call */
+	int finished;            /* the last decode_picture returned -2 (end of the data) */
 };
 
 /* h264_syntax.c */
@@ -388,12 +396,15 @@ void h264_async_la_sps(h264_dec_t *la);
 void h264_async_api_sps(h264_dec_t *d);
 int h264_async_sps(h264_dec_t *d);
 int h264_async_push_nal(h264_dec_t *la);
+void h264_async_trim(h264_dec_t *d);
 
 /* bitio.c */
 int h264_nal_next(h264_dec_t *d);
 
 /* h264_api.c: the NAL loop of decode_picture, shared by the API context and the lookahead context */
 int h264_decode_loop(h264_dec_t *d);
+/* the decoder state behind a caller context initialised by h264d_func->init (NULL: none / evicted) */
+h264_dec_t *h264_state(void *ctx);
 int h264_decode_stream_held(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
                             int parse_threads, int extra, m2dec_hold_t *hold,
                             void (*on_frame)(void *arg, const m2d_frame_t *f), void (*on_end)(void *arg), void *arg,

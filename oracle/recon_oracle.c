@@ -1064,8 +1064,12 @@ typedef struct {
 	m2r_picture_t pic;
 	void *mem;
 	size_t mem_size;
-	/* decode ahead (M2R_PIC_VIRTUAL): one picture buffer per virtual id, copied to a frame by bind */
+	/* decode ahead (M2R_PIC_VIRTUAL): one picture buffer per virtual id; bind copies it into the
+	 * slot's staging buffer, sync_frame copies that into the caller's frame (the HIP back end's
+	 * contract: caller frames are written only inside peek / get) */
 	m2d_frame_t vfr[64];
+	uint8_t *stg[64];
+	int stg_pending[64];
 	size_t luma_size;
 } oracle_be_t;
 
@@ -1078,6 +1082,9 @@ static void vfree(oracle_be_t *b)
 	for (int i = 0; i < 64; ++i) {
 		if (b->vfr[i].luma) free(b->vfr[i].luma - VMARGIN);
 		b->vfr[i].luma = b->vfr[i].chroma = NULL;
+		free(b->stg[i]);
+		b->stg[i] = NULL;
+		b->stg_pending[i] = 0;
 	}
 }
 
@@ -1151,15 +1158,21 @@ static int be_bind(void *self, int vid, int slot)
 {
 	oracle_be_t *b = (oracle_be_t *)self;
 	if (vid < 0 || vid >= 64 || slot < 0 || slot >= b->n || !b->vfr[vid].luma) return -1;
-	memcpy(b->frames[slot].luma, b->vfr[vid].luma, b->luma_size);
-	memcpy(b->frames[slot].chroma, b->vfr[vid].chroma, b->luma_size / 2);
+	if (!b->stg[slot] && !(b->stg[slot] = (uint8_t *)malloc(b->luma_size * 3 / 2))) return -1;
+	memcpy(b->stg[slot], b->vfr[vid].luma, b->luma_size * 3 / 2); /* (chroma follows luma in vfr) */
+	b->stg_pending[slot] = 1;
 	return 0;
 }
 
 static int be_sync(void *self, int slot)
 {
-	(void)self;
-	(void)slot;
+	oracle_be_t *b = (oracle_be_t *)self;
+	if (slot < 0 || slot >= 64) return -1;
+	if (b->stg_pending[slot]) {
+		memcpy(b->frames[slot].luma, b->stg[slot], b->luma_size);
+		memcpy(b->frames[slot].chroma, b->stg[slot] + b->luma_size, b->luma_size / 2);
+		b->stg_pending[slot] = 0;
+	}
 	return 0;
 }
 

@@ -214,9 +214,10 @@ static void *stream_worker(void *arg)
 	stream_job_t *j = (stream_job_t *)arg;
 	/* few parse-ahead workers per stream: the streams themselves fill the host cores
 	 * (M2DEC_AMD_STREAM_PARSE_THREADS, tuning) */
-	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS");
+	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS"), *m = getenv("M2DEC_AMD_STREAM_MD5_THREADS");
 	const int pt = e && atoi(e) > 0 ? atoi(e) : 3; /* profiles/r54_stream_threads.txt: 8 streams, 1 -> ~1070 fps, 3 -> ~1250 */
-	j->result = decode_md5(j->data, j->len, NULL, j->device, -1, pt, 2, j->md5s, j->max, NULL);
+	const int mt = m && atoi(m) > 0 ? atoi(m) : 2;
+	j->result = decode_md5(j->data, j->len, NULL, j->device, -1, pt, mt, j->md5s, j->max, NULL);
 	return NULL;
 }
 

@@ -652,7 +652,14 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->api_sps_nal = -1;
 	as->ahead_all = getenv("M2DEC_AMD_AHEAD_ALL") && atoi(getenv("M2DEC_AMD_AHEAD_ALL"));
 	pthread_mutex_lock(&g_parse.mu);
-	as->nth = pool_grow(threads) < threads ? g_parse.nth : threads;
+	{
+		/* the pool is sized for the host share, not per pipeline: M2DEC_AMD_POOL_THREADS, default 16 (the
+		 * GPU box's CPU share per job; profiles/r48*_threads.txt), at least what a pipeline asks for */
+		const char *e = getenv("M2DEC_AMD_POOL_THREADS");
+		const int want = e && atoi(e) > 0 ? atoi(e) : 16;
+		pool_grow(want > threads ? want : threads);
+	}
+	as->nth = g_parse.nth < threads ? g_parse.nth : threads;
 	if (as->nth <= 0) {
 		pthread_mutex_unlock(&g_parse.mu);
 		pthread_cond_destroy(&as->cv_done);

@@ -21,38 +21,49 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
-#define MD5_RING 40        /* frames queued or being hashed; the decoder gets as many extra frames */
+#define MD5_RING 64        /* frames queued or being hashed (all streams of a pipe) */
+#define MD5_EXTRA 40       /* frames a stream's decoder gets beyond its need (held by queued MD5s meanwhile) */
 #define MD5_BATCH 16       /* frames one thread hashes together (m2dec_amd_frames_md5 lanes) */
 #define MD5_MIN_BATCH 8    /* a batch costs about the same CPU time for 2 or 16 frames: a thread waits for
                               this many (or MD5_WAIT_S after the oldest was queued, or the end) */
 #define MD5_WAIT_S 0.004
 #define MD5_THREADS_MAX 16
-#define MD5_THREADS 2      /* one stream: a 16-frame batch of 1080p takes one core ~4 ms, so two threads
-                              keep up with the decoder; M2DEC_AMD_MD5_THREADS overrides */
+#define MD5_THREADS 3      /* one stream: a 16-frame batch of 1080p takes one core ~4 ms; the third thread
+                              shortens the stream's tail (profiles/r59_knobs.txt); M2DEC_AMD_MD5_THREADS */
 
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
  * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
- * caller's thread.  The driver's frames are one allocation, so the multi-buffer MD5 addresses
- * every frame with 32-bit offsets. */
+ * caller's thread.  One pipe may serve several streams (m2dec_amd_decode_streams_md5): their frames
+ * share the 16 lanes of a batch, which a single stream fills only at its end. */
+struct md5_pipe;
 typedef struct {
+	struct md5_pipe *pipe;
+	m2dec_hold_t hold;
+	char *md5s;
+	int max;
+	int n;                   /* frames delivered */
+	int ended;               /* md5_on_end ran */
+	double t_done;           /* the last MD5 line written */
+} md5_stream_t;
+
+typedef struct md5_pipe {
 	pthread_mutex_t mu;
 	pthread_cond_t cv_job, cv_free;
-	m2dec_hold_t hold;
 	m2d_frame_t frm[MD5_RING];
+	md5_stream_t *of[MD5_RING];
 	int idx[MD5_RING];       /* output frame number of the job in slot k */
 	double t_queued[MD5_RING];
 	int state[MD5_RING];     /* 0 free, 1 queued, 2 being hashed */
 	int head, next;          /* slots filled / taken by a hashing thread, in order */
-	int quit;
-	char *md5s;
-	int max;
-	int n;                   /* frames delivered */
+	int quit;                /* no more frames (every stream ended) */
+	int streams, ended;      /* streams using the pipe / past their last frame: hash at once */
 	int stats;
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
-	double t_wait;           /* caller: waiting for a free queue slot */
+	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
 	long batches;
-	double t_done;           /* the last MD5 line written */
+	pthread_t th[MD5_THREADS_MAX];
+	int nth;
 } md5_pipe_t;
 
 static double now_s(void)
@@ -70,7 +81,7 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
-		while (!p->quit && p->head - p->next < MD5_MIN_BATCH) {
+		while (!p->quit && p->ended == 0 && p->head - p->next < MD5_MIN_BATCH) {
 			const double left = p->t_queued[p->next % MD5_RING] + MD5_WAIT_S - now_s();
 			struct timespec ts;
 			if (left <= 0) break;
@@ -82,12 +93,14 @@ static void *md5_worker(void *arg)
 		}
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
+		md5_stream_t *sof[MD5_BATCH];
 		int ks[MD5_BATCH], ix[MD5_BATCH], n = 0;
 		while (n < MD5_BATCH && p->next < p->head) {
 			const int k = p->next % MD5_RING;
 			p->next++;
 			p->state[k] = 2;
 			f[n] = p->frm[k];
+			sof[n] = p->of[k];
 			ix[n] = p->idx[k];
 			ks[n++] = k;
 		}
@@ -97,16 +110,17 @@ static void *md5_worker(void *arg)
 		const double th = now_s();
 		m2dec_amd_frames_md5(f, n, lines);
 		const double th1 = now_s();
-		for (int j = 0; j < n; ++j) {
-			if (ix[j] < p->max) memcpy(p->md5s + (size_t)ix[j] * 35, lines[j], 35);
-			m2dec_hold_release(&p->hold, f[j].luma);
-		}
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
 		p->t_hash += th1 - th;
 		p->batches++;
-		if (t > p->t_done) p->t_done = t;
-		for (int j = 0; j < n; ++j) p->state[ks[j]] = 0;
+		for (int j = 0; j < n; ++j) {
+			if (ix[j] < sof[j]->max) memcpy(sof[j]->md5s + (size_t)ix[j] * 35, lines[j], 35);
+			if (t > sof[j]->t_done) sof[j]->t_done = t;
+			p->state[ks[j]] = 0;
+		}
+		/* (last: once its holds are released a stream may return and its md5_stream_t is gone) */
+		for (int j = 0; j < n; ++j) m2dec_hold_release(&sof[j]->hold, f[j].luma);
 		pthread_cond_broadcast(&p->cv_free);
 	}
 	pthread_mutex_unlock(&p->mu);
@@ -116,15 +130,17 @@ static void *md5_worker(void *arg)
 /* on_frame of the stream driver: hold the frame, queue its MD5 */
 static void md5_on_frame(void *arg, const m2d_frame_t *f)
 {
-	md5_pipe_t *p = (md5_pipe_t *)arg;
-	const int k = p->head % MD5_RING;
+	md5_stream_t *s = (md5_stream_t *)arg;
+	md5_pipe_t *p = s->pipe;
 	const double t0 = p->stats ? now_s() : 0;
-	m2dec_hold_add(&p->hold, f->luma);
+	m2dec_hold_add(&s->hold, f->luma);
 	pthread_mutex_lock(&p->mu);
-	while (p->state[k]) pthread_cond_wait(&p->cv_free, &p->mu);
+	while (p->state[p->head % MD5_RING]) pthread_cond_wait(&p->cv_free, &p->mu);
+	const int k = p->head % MD5_RING;
 	if (p->stats) p->t_wait += now_s() - t0;
 	p->frm[k] = *f;
-	p->idx[k] = p->n++;
+	p->of[k] = s;
+	p->idx[k] = s->n++;
 	p->t_queued[k] = now_s();
 	p->state[k] = 1;
 	p->head++;
@@ -132,14 +148,81 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_unlock(&p->mu);
 }
 
-/* the stream's last frame was queued: hash what is left at once */
+/* a stream's last frame was queued: hash what is left at once */
 static void md5_on_end(void *arg)
 {
-	md5_pipe_t *p = (md5_pipe_t *)arg;
+	md5_stream_t *s = (md5_stream_t *)arg;
+	md5_pipe_t *p = s->pipe;
 	pthread_mutex_lock(&p->mu);
-	p->quit = 1;
+	if (!s->ended) {
+		s->ended = 1;
+		p->ended++;
+		if (p->ended >= p->streams) p->quit = 1;
+	}
 	pthread_cond_broadcast(&p->cv_job);
 	pthread_mutex_unlock(&p->mu);
+}
+
+static int pipe_open(md5_pipe_t *p, int streams, int threads)
+{
+	memset(p, 0, sizeof(*p));
+	pthread_mutex_init(&p->mu, NULL);
+	pthread_cond_init(&p->cv_job, NULL);
+	pthread_cond_init(&p->cv_free, NULL);
+	if (getenv("M2DEC_AMD_MD5_DELAY_US")) p->delay_us = atoi(getenv("M2DEC_AMD_MD5_DELAY_US"));
+	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
+	p->streams = streams;
+	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)
+		if (pthread_create(&p->th[p->nth], NULL, md5_worker, p) != 0) break;
+	if (!p->nth) {
+		pthread_mutex_destroy(&p->mu);
+		pthread_cond_destroy(&p->cv_job);
+		pthread_cond_destroy(&p->cv_free);
+		return -1;
+	}
+	return 0;
+}
+
+static void pipe_close(md5_pipe_t *p)
+{
+	pthread_mutex_lock(&p->mu);
+	p->quit = 1; /* (already set by the last md5_on_end unless a decode failed early) */
+	pthread_cond_broadcast(&p->cv_job);
+	pthread_mutex_unlock(&p->mu);
+	for (int i = 0; i < p->nth; ++i) pthread_join(p->th[i], NULL);
+	if (p->stats)
+		fprintf(stderr, "md5: caller waits %.3f s, %d frames in %ld batches, hashing %.3f s (%d threads)\n", p->t_wait,
+		        p->head, p->batches, p->t_hash, p->nth);
+	pthread_mutex_destroy(&p->mu);
+	pthread_cond_destroy(&p->cv_job);
+	pthread_cond_destroy(&p->cv_free);
+}
+
+/* one stream through the shared pipe p: decode, MD5 lines into md5s; returns frames or < 0 */
+static int stream_md5(md5_pipe_t *p, const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
+                      int parse_threads, char *md5s, int max, m2dec_amd_stats_t *stats)
+{
+	md5_stream_t s;
+	m2dec_amd_stats_t st;
+	int r;
+	memset(&s, 0, sizeof(s));
+	s.pipe = p;
+	s.md5s = md5s;
+	s.max = max;
+	m2dec_hold_init(&s.hold);
+	memset(&st, 0, sizeof(st));
+	const char *ex = getenv("M2DEC_AMD_MD5_EXTRA"); /* (tests: fewer spare frames -> the decoder waits on holds) */
+	r = h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, ex ? atoi(ex) : MD5_EXTRA, &s.hold,
+	                            md5_on_frame, md5_on_end, &s, &st);
+	md5_on_end(&s); /* (a decode that failed early did not reach on_end: do not hold the pipe up) */
+	m2dec_hold_wait_idle(&s.hold); /* every queued MD5 of this stream is written */
+	m2dec_hold_destroy(&s.hold);
+	pthread_mutex_lock(&p->mu);
+	if (s.t_done > st.t_end) st.t_end = s.t_done; /* delivered = its MD5 line written */
+	pthread_mutex_unlock(&p->mu);
+	st.hold_waits = s.hold.waits;
+	if (stats) *stats = st;
+	return r < 0 ? r : s.n;
 }
 
 static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
@@ -162,45 +245,15 @@ static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *back
                       int parse_threads, int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats)
 {
 	md5_pipe_t p;
-	pthread_t th[MD5_THREADS_MAX];
 	int r;
-	memset(&p, 0, sizeof(p));
-	pthread_mutex_init(&p.mu, NULL);
-	pthread_cond_init(&p.cv_job, NULL);
-	pthread_cond_init(&p.cv_free, NULL);
-	m2dec_hold_init(&p.hold);
-	if (getenv("M2DEC_AMD_MD5_DELAY_US")) p.delay_us = atoi(getenv("M2DEC_AMD_MD5_DELAY_US"));
-	p.md5s = md5s;
-	p.max = max;
-	p.stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
-	int nth = 0;
-	for (; nth < md5_threads && nth < MD5_THREADS_MAX; ++nth)
-		if (pthread_create(&th[nth], NULL, md5_worker, &p) != 0) break;
-	if (!nth) return -1;
-	m2dec_amd_stats_t st;
-	memset(&st, 0, sizeof(st));
-	const char *ex = getenv("M2DEC_AMD_MD5_EXTRA"); /* (tests: fewer spare frames -> the decoder waits on holds) */
-	r = h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, ex ? atoi(ex) : MD5_RING, &p.hold,
-	                            md5_on_frame, md5_on_end, &p, &st);
-	pthread_mutex_lock(&p.mu);
-	p.quit = 1; /* (already set by md5_on_end unless the decode failed early) */
-	pthread_cond_broadcast(&p.cv_job);
-	pthread_mutex_unlock(&p.mu);
-	for (int i = 0; i < nth; ++i) pthread_join(th[i], NULL);
-	if (p.stats)
-		fprintf(stderr, "md5: caller waits %.3f s, frame LRU waits %ld, %d frames in %ld batches, hashing %.3f s (%d threads)\n",
-		        p.t_wait, p.hold.waits, p.n, p.batches, p.t_hash, nth);
-	m2dec_hold_destroy(&p.hold);
-	if (p.t_done > st.t_end) st.t_end = p.t_done; /* delivered = its MD5 line written */
-	st.hold_waits = p.hold.waits;
-	if (stats) *stats = st;
-	pthread_mutex_destroy(&p.mu);
-	pthread_cond_destroy(&p.cv_job);
-	pthread_cond_destroy(&p.cv_free);
-	return r < 0 ? r : p.n;
+	if (pipe_open(&p, 1, md5_threads) < 0) return -1;
+	r = stream_md5(&p, data, len, backend, device, dpb, parse_threads, md5s, max, stats);
+	pipe_close(&p);
+	return r;
 }
 
 typedef struct {
+	md5_pipe_t *pipe;
 	const uint8_t *data;
 	size_t len;
 	int device;
@@ -212,30 +265,37 @@ typedef struct {
 static void *stream_worker(void *arg)
 {
 	stream_job_t *j = (stream_job_t *)arg;
-	/* few parse-ahead workers per stream: the streams themselves fill the host cores
-	 * (M2DEC_AMD_STREAM_PARSE_THREADS, tuning) */
-	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS"), *m = getenv("M2DEC_AMD_STREAM_MD5_THREADS");
-	const int pt = e && atoi(e) > 0 ? atoi(e) : 3; /* profiles/r54_stream_threads.txt: 8 streams, 1 -> ~1070 fps, 3 -> ~1250 */
-	const int mt = m && atoi(m) > 0 ? atoi(m) : 2;
-	j->result = decode_md5(j->data, j->len, NULL, j->device, -1, pt, mt, j->md5s, j->max, NULL);
+	/* parse-ahead workers a stream may occupy in the shared pool (M2DEC_AMD_STREAM_PARSE_THREADS) */
+	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS");
+	const int pt = e && atoi(e) > 0 ? atoi(e) : 8; /* profiles/r59_sweep_e2e.txt: 8 streams, 3 -> ~1440, 8 -> ~1490 fps */
+	j->result = stream_md5(j->pipe, j->data, j->len, NULL, j->device, -1, pt, j->md5s, j->max, NULL);
 	return NULL;
 }
 
+/* n streams, one host thread and decoder context each, one MD5 pipe for all of them */
 int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_t *lens, int device, char *const *md5s,
                                  const int *max, int *frames)
 {
 	stream_job_t *jobs;
 	pthread_t *th;
+	md5_pipe_t pipe;
 	int ok = 0;
 	if (n <= 0) return -1;
+	{
+		const char *m = getenv("M2DEC_AMD_STREAM_MD5_THREADS"); /* MD5 threads of the shared pipe */
+		const int mt = m && atoi(m) > 0 ? atoi(m) : (n + 1) / 2 + 1;
+		if (pipe_open(&pipe, n, mt) < 0) return -1;
+	}
 	jobs = (stream_job_t *)calloc((size_t)n, sizeof(*jobs));
 	th = (pthread_t *)calloc((size_t)n, sizeof(*th));
 	if (!jobs || !th) {
 		free(jobs);
 		free(th);
+		pipe_close(&pipe);
 		return -1;
 	}
 	for (int i = 0; i < n; ++i) {
+		jobs[i].pipe = &pipe;
 		jobs[i].data = datas[i];
 		jobs[i].len = lens[i];
 		jobs[i].device = device;
@@ -243,6 +303,13 @@ int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_
 		jobs[i].max = max[i];
 		jobs[i].result = -1;
 		if (pthread_create(&th[i], NULL, stream_worker, &jobs[i]) != 0) {
+			for (int k = i; k < n; ++k) { /* (streams never started end now) */
+				pthread_mutex_lock(&pipe.mu);
+				pipe.ended++;
+				if (pipe.ended >= pipe.streams) pipe.quit = 1;
+				pthread_cond_broadcast(&pipe.cv_job);
+				pthread_mutex_unlock(&pipe.mu);
+			}
 			n = i;
 			ok = -1;
 			break;
@@ -253,6 +320,7 @@ int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_
 		if (frames) frames[i] = jobs[i].result;
 		if (jobs[i].result < 0) ok = -1;
 	}
+	pipe_close(&pipe);
 	free(jobs);
 	free(th);
 	return ok;

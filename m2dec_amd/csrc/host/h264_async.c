@@ -637,7 +637,7 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->mu = &g_parse.mu;
 	as->api = d;
 	pthread_cond_init(&as->cv_done, NULL);
-	as->depth = 2 * threads + 8;
+	as->depth = 3 * threads + 12; /* (16 workers: the cap, 60 pictures; profiles/r59_knobs.txt) */
 	{
 		const char *e = getenv("M2DEC_AMD_PARSE_DEPTH"); /* tuning: pictures the lookahead runs ahead */
 		if (e && atoi(e) > 0) as->depth = atoi(e);

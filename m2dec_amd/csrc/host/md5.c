@@ -241,13 +241,11 @@ __attribute__((target("avx512f"))) static inline void transpose16(__m512i r[16])
 
 /* lane l hashes nblocks 64-byte blocks at base + off[l]: each block step loads one 64-byte block per
  * lane and transposes them (gathers measured 2.5x slower on the EPYC host) */
-__attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16], const uint8_t *base,
-                                                              const int32_t off[16], size_t nblocks)
+__attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16], const uint8_t *const lp[16],
+                                                              size_t nblocks)
 {
 	__m512i va = _mm512_loadu_si512(st[0]), vb = _mm512_loadu_si512(st[1]);
 	__m512i vc = _mm512_loadu_si512(st[2]), vd = _mm512_loadu_si512(st[3]);
-	const uint8_t *lp[16];
-	for (int l = 0; l < 16; ++l) lp[l] = base + off[l];
 	for (size_t n = 0; n < nblocks; ++n) {
 		__m512i w[16];
 		__m512i a = va, b = vb, c = vc, d = vd;
@@ -346,32 +344,26 @@ int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
 #if defined(__x86_64__)
 	int lanes_ok = n >= 2 && have_avx512();
 	const int stride = f[0].width, h = f[0].height - f[0].crop[2] - f[0].crop[3];
-	const uint8_t *lo = NULL, *hi = NULL;
 	for (int i = 0; i < n && lanes_ok; ++i) {
 		const m2d_frame_t *g = &f[i];
 		/* one geometry; rows contiguous (no horizontal crop) */
 		lanes_ok = g->width == stride && g->height == f[0].height && g->crop[2] == f[0].crop[2] &&
 		           g->crop[3] == f[0].crop[3] && g->crop[0] == 0 && g->crop[1] == 0;
-		for (int k = 0; k < 2 && lanes_ok; ++k) {
-			const uint8_t *p = k ? g->chroma : g->luma;
-			if (!lo || p < lo) lo = p;
-			if (!hi || p > hi) hi = p;
-		}
 	}
-	if (lanes_ok && h > 0 && (size_t)(hi - lo) + (size_t)stride * (size_t)h < ((size_t)1 << 31)) {
+	if (lanes_ok && h > 0) {
 		const size_t la = (size_t)stride * (size_t)h, lb = (size_t)stride * (size_t)(h >> 1);
 		const size_t na = la / 64, nb = (la % 64) ? 0 : lb / 64;
 		uint32_t st[4][16];
-		int32_t offa[16], offb[16];
+		const uint8_t *pa[16], *pb[16];
 		static const uint32_t iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
 		for (int l = 0; l < 16; ++l) {
 			const m2d_frame_t *g = &f[l < n ? l : 0]; /* idle lanes repeat lane 0 */
-			offa[l] = (int32_t)(g->luma + (size_t)stride * f[0].crop[2] - lo);
-			offb[l] = (int32_t)(g->chroma + (size_t)stride * (f[0].crop[2] >> 1) - lo);
+			pa[l] = g->luma + (size_t)stride * f[0].crop[2];
+			pb[l] = g->chroma + (size_t)stride * (f[0].crop[2] >> 1);
 			for (int k = 0; k < 4; ++k) st[k][l] = iv[k];
 		}
-		md5x16_blocks(st, lo, offa, na);
-		md5x16_blocks(st, lo, offb, nb);
+		md5x16_blocks(st, pa, na);
+		md5x16_blocks(st, pb, nb);
 		for (int l = 0; l < n; ++l) {
 			md5_t m;
 			uint8_t dg[16];
@@ -379,10 +371,10 @@ int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
 			m.len = (uint64_t)(na + nb) * 64;
 			m.fill = 0;
 			if (nb) {
-				md5_update(&m, lo + offb[l] + nb * 64, lb - nb * 64);
+				md5_update(&m, pb[l] + nb * 64, lb - nb * 64);
 			} else {
-				md5_update(&m, lo + offa[l] + na * 64, la - na * 64);
-				md5_update(&m, lo + offb[l], lb);
+				md5_update(&m, pa[l] + na * 64, la - na * 64);
+				md5_update(&m, pb[l], lb);
 			}
 			md5_final(&m, dg);
 			md5_line(dg, out[l]);

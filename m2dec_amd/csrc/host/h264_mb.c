@@ -12,7 +12,6 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
-#include <immintrin.h>
 #include "h264_dec.h"
 
 /* blkIdx -> 4x4 position (spec 6.4.3) and inverse */
@@ -1109,6 +1108,25 @@ static inline int mv_far(const int16_t *a, const int16_t *b)
 	return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4;
 }
 
+/* bS 1 test between two inter 4x4 blocks (str_mv_calc*, h264.cpp:7119-7270) */
+static int bs_motion(const h264_mbinfo_t *q, int qx, int qy, const h264_mbinfo_t *p, int px, int py)
+{
+	int q0 = blk_fidx(q, 0, qx, qy), q1 = blk_fidx(q, 1, qx, qy);
+	int p0 = blk_fidx(p, 0, px, py), p1 = blk_fidx(p, 1, px, py);
+	const int16_t *qm0 = q->mv[0][qy * 4 + qx], *qm1 = q->mv[1][qy * 4 + qx];
+	const int16_t *pm0 = p->mv[0][py * 4 + px], *pm1 = p->mv[1][py * 4 + px];
+	if (((p0 != q0) || (p1 != q1)) && ((p1 != q0) || (p0 != q1))) return 1;
+	if (q0 >= 0 && q1 >= 0) {
+		if (q0 == q1) {
+			return (mv_far(qm0, pm0) || mv_far(qm1, pm1)) && (mv_far(qm0, pm1) || mv_far(qm1, pm0));
+		}
+		if (q0 == p0) return mv_far(qm0, pm0) || mv_far(qm1, pm1);
+		return mv_far(qm0, pm1) || mv_far(qm1, pm0);
+	}
+	if (q0 >= 0) return (q0 == p0) ? mv_far(qm0, pm0) : mv_far(qm0, pm1);
+	return (q1 == p0) ? mv_far(qm1, pm0) : mv_far(qm1, pm1);
+}
+
 static inline int is_intra_type(int t) { return t >= 0 && t <= MBT_IPCM; }
 
 /* one motion for the whole MB (both lists): every inner-edge bS-1 test is then 0 */
@@ -1125,100 +1143,17 @@ static int uniform_motion(const h264_mbinfo_t *q)
 	return 1;
 }
 
-/* luma blocks with coefficients, raster bit y * 4 + x (nnz[] is in blkIdx order: 8x8 quadrants of
- * 2x2 blocks) */
+/* luma blocks with coefficients, raster bit y * 4 + x */
 static inline uint32_t nz_raster(const h264_mbinfo_t *m)
 {
-	const __m128i v = _mm_loadu_si128((const __m128i *)m->nnz);
-	const uint32_t b = ~(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_setzero_si128())) & 0xffffu;
-	return _pdep_u32(b & 15, 0x0033) | _pdep_u32((b >> 4) & 15, 0x00cc) | _pdep_u32((b >> 8) & 15, 0x3300) |
-	       _pdep_u32(b >> 12, 0xcc00);
+	uint32_t r = 0;
+	for (int b = 0; b < 16; ++b) r |= (uint32_t)(m->nnz[b] != 0) << (blk_y[b] * 4 + blk_x[b]);
+	return r;
 }
 
 static inline int b8_of(int r) { return ((r >> 3) << 1) | ((r & 3) >> 1); }
 
-/* bS 2 ("2" in the high bit of each 2-bit segment) of the four edges of one direction from the
- * per-edge nz bits: vertical edges have their segments (rows) at bits y * 4 + e, horizontal ones
- * (columns) at e * 4 + x */
-static inline uint32_t bs2_vert(uint32_t e)
-{
-	uint32_t r = 0;
-	for (int k = 0; k < 4; ++k) r |= _pdep_u32(_pext_u32(e, 0x1111u << k), 0xaa) << (8 * k);
-	return r;
-}
-
-static inline uint32_t bs2_horiz(uint32_t e)
-{
-	uint32_t r = 0;
-	for (int k = 0; k < 4; ++k) r |= _pdep_u32((e >> (4 * k)) & 15, 0xaa) << (8 * k);
-	return r;
-}
-
-/* the bS 0 / 1 motion test (bs_motion) of 8 segments at once: lanes are q blocks, with their
- * references (frame ids) and vectors and those of the blocks across the edge */
-static inline uint32_t bs_motion8(__m256i qf0, __m256i qf1, __m256i pf0, __m256i pf1, __m256i qm0, __m256i qm1,
-                                  __m256i pm0, __m256i pm1)
-{
-	const __m256i z = _mm256_setzero_si256(), three = _mm256_set1_epi16(3), m1 = _mm256_set1_epi32(-1);
-#define FAR(a, b) _mm256_xor_si256(_mm256_cmpeq_epi32(_mm256_cmpgt_epi16(_mm256_abs_epi16(_mm256_sub_epi16(a, b)), three), z), m1)
-	const __m256i f00 = FAR(qm0, pm0), f11 = FAR(qm1, pm1), f01 = FAR(qm0, pm1), f10 = FAR(qm1, pm0);
-#undef FAR
-	const __m256i e00 = _mm256_cmpeq_epi32(qf0, pf0), e11 = _mm256_cmpeq_epi32(qf1, pf1);
-	const __m256i e01 = _mm256_cmpeq_epi32(qf0, pf1), e10 = _mm256_cmpeq_epi32(qf1, pf0);
-	/* different reference sets: bS 1 */
-	const __m256i diff = _mm256_andnot_si256(_mm256_and_si256(e00, e11), _mm256_andnot_si256(_mm256_and_si256(e01, e10), m1));
-	const __m256i q0ok = _mm256_cmpgt_epi32(qf0, m1), q1ok = _mm256_cmpgt_epi32(qf1, m1);
-	const __m256i same = _mm256_or_si256(f00, f11), cross = _mm256_or_si256(f01, f10);
-	/* both lists: one reference twice -> both pairings far; else the pairing of equal references */
-	const __m256i bi = _mm256_blendv_epi8(_mm256_blendv_epi8(cross, same, e00), _mm256_and_si256(same, cross),
-	                                      _mm256_cmpeq_epi32(qf0, qf1));
-	const __m256i one0 = _mm256_blendv_epi8(f01, f00, e00);                         /* list 0 only */
-	const __m256i one1 = _mm256_blendv_epi8(f11, f10, _mm256_cmpeq_epi32(qf1, pf0)); /* list 1 only */
-	const __m256i r = _mm256_blendv_epi8(_mm256_blendv_epi8(one1, one0, q0ok), bi, _mm256_and_si256(q0ok, q1ok));
-	return (uint32_t)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_or_si256(diff, r)));
-}
-
-/* bS 1 (motion) of the 16 segments of one direction, lane = the q block's raster index: its
- * neighbour across the edge is the block to the left (dir 0) / above (dir 1), in p for the MB edge
- * (str_mv_calc*, h264.cpp:7119-7270) */
-static uint32_t bs_motion16(const h264_mbinfo_t *q, const h264_mbinfo_t *p, int dir)
-{
-	int32_t qf[2][16], pf[2][16];
-	uint32_t qm[2][16], pm[2][16];
-	uint32_t r = 0;
-	memcpy(qm, q->mv, sizeof(qm));
-	for (int k = 0; k < 16; ++k) {
-		const int b = b8_of(k);
-		qf[0][k] = q->fidx[0][b];
-		qf[1][k] = q->fidx[1][b];
-	}
-	for (int k = 0; k < 16; ++k) {
-		const int edge = dir ? (k < 4) : ((k & 3) == 0);
-		const h264_mbinfo_t *m = edge ? p : q;
-		const int pr = dir ? (edge ? k + 12 : k - 4) : (edge ? k + 3 : k - 1);
-		if (!m) { /* (no MB across: the lane is never used) */
-			pf[0][k] = qf[0][k];
-			pf[1][k] = qf[1][k];
-			pm[0][k] = qm[0][k];
-			pm[1][k] = qm[1][k];
-			continue;
-		}
-		const int b = b8_of(pr);
-		pf[0][k] = m->fidx[0][b];
-		pf[1][k] = m->fidx[1][b];
-		memcpy(&pm[0][k], m->mv[0][pr], 4);
-		memcpy(&pm[1][k], m->mv[1][pr], 4);
-	}
-	for (int h = 0; h < 2; ++h) {
-#define L(a) _mm256_loadu_si256((const __m256i *)((const int32_t *)(a) + 8 * h))
-		r |= bs_motion8(L(qf[0]), L(qf[1]), L(pf[0]), L(pf[1]), L(qm[0]), L(qm[1]), L(pm[0]), L(pm[1])) << (8 * h);
-#undef L
-	}
-	return r;
-}
-
-/* boundary strengths of the current MB's edges (bs_v / bs_h / the BS4 flags of its deblock record):
- * bS 2 where either side has coefficients (bit-parallel from the nz masks), else the motion test */
+/* boundary strengths of the current MB's edges (bs_v / bs_h / the BS4 flags of its deblock record) */
 static void bs_strength(slice_ctx_t *s)
 {
 	h264_mbinfo_t *q = s->cur;
@@ -1231,42 +1166,54 @@ static void bs_strength(slice_ctx_t *s)
 		bv = bh = v;
 		flags = M2R_DBK_LEFT_BS4 | M2R_DBK_TOP_BS4;
 	} else {
-		const int uni = uniform_motion(q);
+		const int t8 = q->t8x8, uni = uniform_motion(q);
 		const uint32_t nzq = nz_raster(q);
-		/* edges skipped with the 8x8 transform (inner edges 1 and 3) */
-		const uint32_t emask = q->t8x8 ? 0x00ff00ffu : 0xffffffffu;
+		uint32_t mvw[2][16];
+		memcpy(mvw, q->mv, sizeof(mvw));
 		for (int dir = 0; dir < 2; ++dir) {
+			uint32_t str = 0;
+			/* MB edge: the left / top neighbour */
 			const h264_mbinfo_t *p = NULL;
-			uint32_t enz, str, todo;
 			if (dir == 0 && s->mbx != 0) p = &s->d->mbi[s->addr - 1];
 			if (dir == 1 && s->mby != 0) p = &s->d->mbi[s->addr - s->d->mb_w];
 			if (p && (int)(p - s->d->mbi) < s->d->par_first_mb) p = NULL; /* h264_fix_bs, once that slice is parsed */
-			/* per-segment "coefficients on either side" of the inner edges */
-			enz = dir ? ((nzq | (nzq << 4)) & 0xfff0u) : ((nzq | (nzq << 1)) & 0xeeeeu);
-			if (p && !is_intra_type(p->type)) {
-				const uint32_t nzp = nz_raster(p);
-				enz |= dir ? ((nzq | (nzp >> 12)) & 0xfu) : ((nzq | (nzp >> 3)) & 0x1111u);
-			}
-			str = (dir ? bs2_horiz(enz) : bs2_vert(enz)) & emask;
-			/* segments without coefficients: bit = segment index in the nz layout */
-			todo = ~enz & 0xffffu;
-			if (!p) todo &= dir ? 0xfff0u : 0xeeeeu;
 			if (p && is_intra_type(p->type)) {
 				flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
-				str |= 0xaa; /* 2 in every segment (the flag makes it 4) */
-				todo &= dir ? 0xfff0u : 0xeeeeu;
+				str = 0xaa; /* 2 in every segment (the flag makes it 4) */
+			} else if (p) {
+				for (int sgm = 0; sgm < 4; ++sgm) {
+					const int qx = dir ? sgm : 0, qy = dir ? 0 : sgm, px = dir ? qx : 3, py = dir ? 3 : qy;
+					int v;
+					const int qr = qy * 4 + qx, pr = py * 4 + px, bq = b8_of(qr), bp = b8_of(pr);
+					if (((nzq >> qr) & 1) || p->nnz[rast2blk[pr]]) v = 2;
+					else if (q->fidx[0][bq] == p->fidx[0][bp] && q->fidx[1][bq] == p->fidx[1][bp] &&
+					         !memcmp(q->mv[0][qr], p->mv[0][pr], 4) && !memcmp(q->mv[1][qr], p->mv[1][pr], 4))
+						v = 0;
+					else v = bs_motion(q, qx, qy, p, px, py);
+					str |= (uint32_t)v << (sgm * 2);
+				}
 			}
-			if (uni) todo &= dir ? 0x000fu : 0x1111u; /* inner edges of one motion: bS 0 */
-			if (q->t8x8) todo &= dir ? 0x0f0fu : 0x5555u; /* (edges 1 and 3 are not filtered) */
-			if (todo) {
-				/* lanes (bits) in the nz layout: vertical y * 4 + e is block raster y * 4 + x with x = e,
-				 * horizontal e * 4 + x is raster e * 4 + x: both are the q block's raster index */
-				uint32_t mv1 = bs_motion16(q, p, dir) & todo;
-				while (mv1) {
-					const int bit = __builtin_ctz(mv1);
-					mv1 &= mv1 - 1;
-					const int e = dir ? bit >> 2 : bit & 3, sg = dir ? bit & 3 : bit >> 2;
-					str |= 1u << (e * 8 + sg * 2);
+			/* inner edges: blocks of the same MB; identical motion (the common case inside a partition)
+			 * is bS 0 without the full test */
+			for (int e = 1; e < 4; ++e) {
+				if (t8 && (e & 1)) continue;
+				for (int sgm = 0; sgm < 4; ++sgm) {
+					const int qx = dir ? sgm : e, qy = dir ? e : sgm;
+					const int qr = qy * 4 + qx, pr = dir ? qr - 4 : qr - 1;
+					int v;
+					if (((nzq >> qr) | (nzq >> pr)) & 1) {
+						v = 2;
+					} else if (uni) {
+						v = 0;
+					} else {
+						const int bq = b8_of(qr), bp = b8_of(pr);
+						if (q->fidx[0][bq] == q->fidx[0][bp] && q->fidx[1][bq] == q->fidx[1][bp] && mvw[0][qr] == mvw[0][pr] &&
+						    mvw[1][qr] == mvw[1][pr])
+							v = 0;
+						else
+							v = bs_motion(q, qx, qy, q, dir ? qx : qx - 1, dir ? qy - 1 : qy);
+					}
+					str |= (uint32_t)v << (e * 8 + sgm * 2);
 				}
 			}
 			if (dir == 0) bv = str;

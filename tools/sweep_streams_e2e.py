@@ -2,6 +2,7 @@
 parse-pool / per-stream settings; prints fps per configuration (bit-exact checked)."""
 import os
 import sys
+import resource
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -25,10 +26,14 @@ for pt, mt in configs:
     os.environ["M2DEC_AMD_STREAM_MD5_THREADS"] = mt
     res = []
     for _ in range(3):
+        r0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         got = m2dec_amd.decode_streams(datas)
         dt = time.perf_counter() - t0
+        r1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
         ok = all(g == GOLDEN[n]["md5"] for g, n in zip(got, names))
-        res.append((sum(len(g) for g in got) / dt, ok))
+        res.append((sum(len(g) for g in got) / dt, ok, cpu / dt, (r1.ru_stime - r0.ru_stime) / dt))
     print(f"8 streams, {pt} parse threads / stream, {mt} md5 threads / stream: "
-          + " ".join("%.0f%s" % (f, "" if ok else "(BAD)") for f, ok in res) + " fps", flush=True)
+          + " ".join("%.0f%s (%.1f cores, sys %.1f)" % (f, "" if ok else "(BAD)", c, sy) for f, ok, c, sy in res) + " fps",
+          flush=True)

@@ -15,7 +15,7 @@ HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)
 HOST_OBJ := $(patsubst m2dec_amd/csrc/host/%.c,build/host/%.o,$(HOST_SRC))
 HIP_SRC := m2dec_amd/csrc/hip/recon_hip.hip
 HIP_HDR := m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h
-HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o
+HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o
 
 LIB := m2dec_amd/lib/libm2dec_amd.so
 ORACLE := oracle/_build/liboracle.so
@@ -60,18 +60,18 @@ $(M2VGEN): tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c m2dec_amd/cs
 	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c -lm
 
 DBG_LIB := build/dbg/libm2dec_amd_stamps.so
-$(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o
+$(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -c $(HIP_SRC) -o build/dbg/recon_hip_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stamps.o build/hip/runtime.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stamps.o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
 
 stamps: $(DBG_LIB)
 
 # diagnostic variants: make variant V=NAME FLAGS="-DX"
-variant: $(HOST_OBJ) build/hip/runtime.o
+variant: $(HOST_OBJ) build/hip/runtime.o build/hip/m2v_hip.o
 	@mkdir -p build/var
 	$(HIPCC) $(HIPFLAGS) $(FLAGS) -c $(HIP_SRC) -o build/var/recon_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/var/lib_$(V).so $(HOST_OBJ) build/var/recon_$(V).o build/hip/runtime.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/var/lib_$(V).so $(HOST_OBJ) build/var/recon_$(V).o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
 
 clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build

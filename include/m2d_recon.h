@@ -137,6 +137,42 @@ typedef struct m2r_backend {
 	int (*bind)(void *self, int vid, int slot);
 } m2r_backend_t;
 
+/* ---------------------------------------------------------------- MPEG-1/2 (m2d_func)
+ * The MPEG-2 parser (m2dec_amd/csrc/host/mpeg2_dec.c) turns each picture into one record per macroblock
+ * in raster order; a reconstruction back end (the CPU one in mpeg2_dec.c, the gfx950 one in
+ * m2dec_amd/csrc/hip/m2v_hip.hip) builds the picture: the prediction of m2d_parse_inter_macroblock /
+ * m2d_skip_mb_P / _B (mpeg2.cpp:715-810, 1355-1395, motioncomp.cpp), then the IDCT of each coded block
+ * stored (intra) or added (inter) with CLIP255C (idct.cpp:286-422).  Nothing of a picture depends on
+ * another macroblock of the same picture. */
+#define M2V_REC_INTRA 1u      /* blocks are stored, not added */
+#define M2V_REC_FWD 2u        /* prediction from the forward reference (fwd) */
+#define M2V_REC_BWD 4u        /* prediction from the backward reference (bwd), averaged if FWD too */
+#define M2V_REC_FIELD 8u      /* field prediction: vectors [dir][0] / [dir][1] for the top / bottom field lines */
+#define M2V_REC_DCT_FIELD 16u /* field DCT: luma blocks 0/1 on even lines, 2/3 on odd lines */
+#define M2V_REC_COPY 32u      /* skipped / lost MB: a copy of the `copy` picture (vector 0) */
+
+/* One macroblock, 32 bytes. */
+typedef struct m2v_mb {
+	uint8_t flags;        /* M2V_REC_*; 0: the MB keeps what the frame holds */
+	uint8_t cbp;          /* bit 5 - i: luma block i, bit 1 - i: chroma block i coded (64 coefficients each in the pool, in block order) */
+	uint8_t field_sel;    /* field prediction: bit 2 * dir + i = the reference field (0 top, 1 bottom) of vector i */
+	uint8_t pad0;
+	uint16_t mbx, mby;
+	int16_t mv[2][2][2];  /* [dir 0 fwd / 1 bwd][vector][x, y] in half samples (field lines for field vectors) */
+	uint32_t coef;        /* offset in int16 units into the coefficient pool (dequantised, mismatch-controlled) */
+	uint32_t pad1[2];
+} m2v_mb_t;
+
+/* One picture's records. */
+typedef struct m2v_picture {
+	int32_t width, height;   /* coded size (MB multiples); NV12, stride = width */
+	int32_t cur, fwd, bwd, copy; /* frame slots: the picture, its forward / backward reference, the copy source (-1: none) */
+	int32_t n_mbs;           /* records (width / 16 * height / 16) */
+	int32_t n_coef;          /* int16 coefficients used in coef[] */
+	m2v_mb_t *mb;
+	int16_t *coef;
+} m2v_picture_t;
+
 #ifdef __cplusplus
 }
 #endif

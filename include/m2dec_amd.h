@@ -143,10 +143,25 @@ int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_
                             void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
 
 /* ---- MPEG-1/2 (m2d_func, m2dec_amd/csrc/host/mpeg2_dec.c) */
+/* M2Decoder over m2d_func (as m2dec_amd_decode_table) with the pictures reconstructed on gfx950
+ * device `device` (m2dec_amd_m2v_use_gpu), or on the host for device < 0.  Returns the last
+ * decode_picture result, or -3 if the device is unusable (no host fallback). */
+int m2dec_amd_decode_m2v(const uint8_t *data, size_t len, int device, int emptify,
+                         void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
 /* Free the heap an m2d_func context owns (its start-code unit buffer). */
 void m2dec_amd_m2v_release(void *ctx);
 /* CLIP255C arguments outside the reference table's domain [-256, 767] seen by a context. */
 uint64_t m2dec_amd_m2v_clip_violations(const void *ctx);
+/* Reconstruct this context's pictures on gfx950 device `device` (m2dec_amd/csrc/hip/m2v_hip.hip)
+ * instead of the host: call after init, before set_frames.  Frames are written into the caller's
+ * memory only inside peek / get.  -1 if no device (the context keeps the host reconstruction).
+ * m2dec_amd_m2v_release frees the device state.  Host reconstruction only: motion-compensated reads
+ * outside the reference frame seen (clamped; the reference reads out of bounds there), and the
+ * CLIP255C count above. */
+int m2dec_amd_m2v_use_gpu(void *ctx, int device);
+uint64_t m2dec_amd_m2v_mc_out_of_frame(const void *ctx);
+/* the two counters of the calling thread's last whole-stream m2d_func decode (decode_table* / decode_m2v) */
+void m2dec_amd_m2v_last_checks(uint64_t *clip_violations, uint64_t *mc_out_of_frame);
 /* VLC probes for the table tests: one codeword at the MSB end of bits32.  DCT (table 0 = B.14,
  * 1 = B.15): length incl. the sign bit, run (-1: EOB / escape), sign-folded level (2|l| + s).
  * Plain tables (0: macroblock_address_increment after its leading 0, 1 / 2: dct_dc_size luma /

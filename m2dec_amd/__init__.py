@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("M2DEC_AMD_LIB") or os.path.join(_HERE, "lib", "libm2d
 
 __all__ = [
     "LIB_PATH", "Frame", "Backend", "Stats", "HipTiming", "lib", "hip_available", "HipBackend",
-    "decode_stream", "decode_stream_md5", "decode_streams", "decode_m2v", "decode_table_frames", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
+    "decode_stream", "decode_stream_md5", "decode_streams", "decode_m2v", "m2v_last_checks", "decode_table_frames", "frame_md5", "frame_nv12", "H264Decoder", "Trace", "HipReplay", "TracePic",
 ]
 
 
@@ -156,6 +156,9 @@ def lib() -> ctypes.CDLL:
                                               ctypes.c_int, ctypes.c_int, ctypes.POINTER(Backend), ctypes.c_int, ON_FRAME,
                                               vp, ctypes.POINTER(ctypes.c_int)]
         L.m2dec_amd_decode_table2.restype = ctypes.c_int
+        L.m2dec_amd_decode_m2v.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ON_FRAME, vp,
+                                           ctypes.POINTER(ctypes.c_int)]
+        L.m2dec_amd_decode_m2v.restype = ctypes.c_int
         L.m2dec_amd_m2v_dct_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip, ip]
         L.m2dec_amd_m2v_vlc_code.argtypes = [ctypes.c_int, ctypes.c_uint32, ip]
         L.m2dec_amd_m2v_intra_dc.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ip]
@@ -343,10 +346,35 @@ def decode_table_frames(table: str, data: bytes, dpb: int = -1, emptify: bool = 
     return md5s, err.value
 
 
-def decode_m2v(data: bytes) -> List[str]:
-    """An MPEG-1/2 video elementary stream through m2d_func (CPU, BASELINE.json configs[0]) like
-    ``h264dec -O x.m2v``: the MD5 line of every output frame."""
-    return decode_table_frames("m2d_func", data)[0]
+def m2v_last_checks() -> tuple:
+    """(CLIP255C arguments outside the reference table's domain, motion-compensated reads outside the
+    reference frame) of this thread's last MPEG-2 decode — both 0 for a stream whose output does not
+    depend on reference undefined behaviour (host reconstruction only)."""
+    L = lib()
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    L.m2dec_amd_m2v_last_checks(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def decode_m2v(data: bytes, device: Optional[int] = None, emptify: bool = False) -> List[str]:
+    """An MPEG-1/2 video elementary stream through m2d_func like ``h264dec -O x.m2v``: the MD5 line of
+    every output frame.  device None: host reconstruction (BASELINE.json configs[0]); else the pictures
+    are reconstructed on that gfx950 device (m2dec_amd/csrc/hip/m2v_hip.hip) — an error, not a host
+    fallback, when it is unusable."""
+    if device is None:
+        return decode_table_frames("m2d_func", data, emptify=emptify)[0]
+    L = lib()
+    md5s: List[str] = []
+
+    def _cb(_arg, fp):
+        md5s.append(frame_md5(fp.contents))
+
+    cb = ON_FRAME(_cb)
+    err = ctypes.c_int()
+    r = L.m2dec_amd_decode_m2v(data, len(data), device, int(emptify), cb, None, ctypes.byref(err))
+    if r == -3:
+        raise RuntimeError(f"m2dec_amd: MPEG-2 decode on device {device} failed")
+    return md5s
 
 
 class H264Decoder:

@@ -160,9 +160,18 @@ int m2dec_amd_decode_table(const m2d_func_table_t *func, int h264, const uint8_t
 	return m2dec_amd_decode_table2(func, h264, data, len, dpb, emptify, skip, NULL, -1, on_frame, arg, last_error);
 }
 
-int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
-                            int emptify, int skip, const m2r_backend_t *backend, int parse_threads,
-                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+/* the checks of the calling thread's last m2d_func decode (m2dec_amd_m2v_last_checks) */
+static __thread uint64_t t_m2v_clip, t_m2v_mc;
+
+void m2dec_amd_m2v_last_checks(uint64_t *clip_violations, uint64_t *mc_out_of_frame)
+{
+	if (clip_violations) *clip_violations = t_m2v_clip;
+	if (mc_out_of_frame) *mc_out_of_frame = t_m2v_mc;
+}
+
+static int decode_core(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb, int emptify,
+                       int skip, const m2r_backend_t *backend, int parse_threads, int m2v_device,
+                       void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
 {
 	drv_t v;
 	m2d_frame_t frm;
@@ -177,6 +186,11 @@ int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_
 	func->init(v.ctx, dpb, header_cb, &v);
 	if (h264 && backend) m2dec_amd_h264_set_backend(v.ctx, backend);
 	if (h264 && parse_threads >= 0) m2dec_amd_h264_set_parse_threads(v.ctx, parse_threads);
+	if (!h264 && m2v_device >= 0 && m2dec_amd_m2v_use_gpu(v.ctx, m2v_device) < 0) { /* (asked for: no host fallback) */
+		free(v.ctx);
+		if (last_error) *last_error = -1;
+		return -3;
+	}
 	dec_bits_set_callback(func->stream_pos(v.ctx), reread, &v);
 	if (skip) {
 		long skipped_bytes = 0;
@@ -214,9 +228,27 @@ int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_
 done:
 	if (last_error) *last_error = err;
 	if (h264 && backend) m2dec_amd_h264_set_backend(v.ctx, NULL); /* borrowed: the caller destroys it */
-	if (h264) m2dec_amd_h264_release(v.ctx);
-	else m2dec_amd_m2v_release(v.ctx);
+	if (h264) {
+		m2dec_amd_h264_release(v.ctx);
+	} else {
+		t_m2v_clip = m2dec_amd_m2v_clip_violations(v.ctx);
+		t_m2v_mc = m2dec_amd_m2v_mc_out_of_frame(v.ctx);
+		m2dec_amd_m2v_release(v.ctx);
+	}
 	free(v.ctx);
 	frames_free(&v);
 	return err;
+}
+
+int m2dec_amd_decode_table2(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb,
+                            int emptify, int skip, const m2r_backend_t *backend, int parse_threads,
+                            void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+{
+	return decode_core(func, h264, data, len, dpb, emptify, skip, backend, parse_threads, -1, on_frame, arg, last_error);
+}
+
+int m2dec_amd_decode_m2v(const uint8_t *data, size_t len, int device, int emptify,
+                         void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+{
+	return decode_core(m2d_func, 0, data, len, -1, emptify, 0, NULL, -1, device, on_frame, arg, last_error);
 }

@@ -3,8 +3,8 @@
  * .m2v on reference CPU path (plumbing, no GPU)", behind the reference's m2d_func table
  * (mpeg2.cpp:1800-1811).  Intra pictures are decoded completely (intra DC / AC VLC, dequant,
  * mismatch control / MPEG-1 oddification, the reference's integer Chen-Wang IDCT, frame / field DCT
- * placement, concealment motion vectors parsed); P and B pictures (motion compensation,
- * motioncomp.cpp) are reported as an error.
+ * placement, concealment motion vectors parsed); P and B frame pictures with frame and field
+ * prediction (motioncomp.cpp), reconstructed from per-MB records on the CPU or the GPU.
  */
 #ifndef M2DEC_AMD_MPEG2_DEC_H
 #define M2DEC_AMD_MPEG2_DEC_H
@@ -12,6 +12,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include "m2d.h"
+#include "m2d_recon.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -28,6 +29,7 @@ typedef struct {
 } m2v_dct_code_t;
 
 extern const m2v_code_t m2v_mb_inc[], m2v_dc_luma[], m2v_dc_chroma[], m2v_motion_code[];
+extern const m2v_code_t m2v_mb_type_p[], m2v_mb_type_b[], m2v_cbp[];
 extern const m2v_dct_code_t m2v_dct0[], m2v_dct1[];
 extern const int m2v_q_scale[2][32];
 extern const uint8_t m2v_scan[2][64];
@@ -74,10 +76,36 @@ typedef struct {
 	int index;
 	int out_state;
 	int copy_src;            /* frame skipped / lost MBs are copied from (diff_to_ref[0]); -1: in place */
+	/* P / B (reference m2d_mb_current: type, motion_type) */
+	int prev_type;           /* macroblock_type flags of the last coded MB (M2V_MBF_*) */
+	int mv_count, mv_field, mv_dmv; /* motion type of the current MB (m2d_motion_type) */
+	/* the picture being parsed as records (m2d_recon.h), reconstructed when it is complete */
+	m2v_picture_t pic;
+	size_t coef_cap;
+	int pic_open;
+	/* reconstruction back end: NULL = this file's CPU reconstruction (the C1 path); else the GPU one
+	 * (m2dec_amd_m2v_use_gpu) */
+	void *gpu;
+	int gpu_device;
 	/* statistics / checks */
 	uint64_t clip_out_of_domain; /* CLIP255C arguments outside [-256, 767] (reference UB) */
+	uint64_t mc_out_of_frame;    /* prediction reads outside the frame (the reference reads outside its buffers) */
 	uint64_t pictures;
 } mpeg2_dec_t;
+
+/* macroblock_type flags (the reference's MB_* values, mpeg2.h:175-182) */
+enum { M2V_MBF_FWD = 1, M2V_MBF_BWD = 2, M2V_MBF_INTRA = 4, M2V_MBF_PATTERN = 8, M2V_MBF_QUANT = 16 };
+
+/* CPU reconstruction of one picture's records into frames[] (mpeg2_dec.c); returns CLIP255C
+ * out-of-domain arguments and prediction reads outside the frame via the counters */
+void m2v_recon_picture_cpu(const m2v_picture_t *pic, const m2d_frame_t *frames, uint64_t *clip_bad, uint64_t *mc_bad);
+
+/* GPU back end (m2dec_amd/csrc/hip/m2v_hip.hip) */
+void *m2v_hip_create(int device);
+int m2v_hip_set_frames(void *g, int n, const m2d_frame_t *frames, int width, int height);
+int m2v_hip_submit(void *g, const m2v_picture_t *pic);
+int m2v_hip_sync(void *g, int slot);
+void m2v_hip_destroy(void *g);
 
 #ifdef __cplusplus
 }

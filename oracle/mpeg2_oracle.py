@@ -1,9 +1,11 @@
-"""CPU restatement of the reference's MPEG-1/2 intra decode path — TEST INFRASTRUCTURE ONLY.
+"""CPU restatement of the reference's MPEG-1/2 decode path — TEST INFRASTRUCTURE ONLY.
 
 Only tests/ (and tools/make_m2v_goldens.py) use this module: it is the checker of the product's
 MPEG-2 decoder (m2dec_amd/csrc/host/mpeg2_dec.c, behind m2d_func), never part of it.
 
-It follows /root/reference/src/lib/mpeg2.cpp + idct.cpp + src/app/m2decoder.h step by step, written
+It follows /root/reference/src/lib/mpeg2.cpp + idct.cpp + motioncomp.cpp + src/app/m2decoder.h step by
+step (intra, P and B frame pictures: macroblock types, skipped macroblocks, frame / field / dual-prime
+motion vectors and their predictors, half-sample prediction, non-intra blocks), written
 independently of the product's C and reading its variable-length codes from
 tests/golden/mpeg2_vlc.json — the codewords of the REFERENCE's own tables (vld.h) as its decoder walks
 them (tools/gen_mpeg2_vlc_golden.py) — so a transcription error in the product's Annex-B tables
@@ -83,7 +85,19 @@ def units(data):
 
 
 def idct_block(coef):
-    """idct.cpp:69-236 (rows, stored as int16) + 286-358 (columns, (x + 8192) >> 14)."""
+    """intra: idct_raw clipped (ClipStore, idct.cpp:364-370)"""
+    out = idct_raw(coef)
+    for r in range(8):
+        for k in range(8):
+            v = out[r][k]
+            assert -256 <= v <= 767, "CLIP255C argument outside the reference table (UB)"
+            out[r][k] = 0 if v < 0 else 255 if v > 255 else v
+    return out
+
+
+def idct_raw(coef):
+    """idct.cpp:69-236 (rows, stored as int16) + 286-358 (columns, (x + 8192) >> 14); rows without
+    AC coefficients take the DC-only branch there (idct.cpp:147-159), which gives the same values."""
     def s16(v):
         v &= 0xffff
         return v - 0x10000 if v & 0x8000 else v
@@ -125,14 +139,12 @@ def idct_block(coef):
         col = [(x7 + x1) >> 14, (x3 + x2) >> 14, (x0 + x4) >> 14, (x8 + x6) >> 14,
                (x8 - x6) >> 14, (x0 - x4) >> 14, (x3 - x2) >> 14, (x7 - x1) >> 14]
         for r in range(8):
-            v = col[r]
-            assert -256 <= v <= 767, "CLIP255C argument outside the reference table (UB)"
-            out[r][k] = 0 if v < 0 else 255 if v > 255 else v
+            out[r][k] = col[r]
     return out
 
 
 class Decoder:
-    """m2d_context + M2Decoder (outbuf 0: 3 frames) for intra pictures."""
+    """m2d_context + M2Decoder (outbuf 0: 3 frames) for intra, P and B frame pictures."""
 
     def __init__(self):
         self.c = _codes()
@@ -154,7 +166,10 @@ class Decoder:
         self.copy_src = -1
         self.coding_type = 0
         self.mb_x, self.mb_y = -1, 0
-        self.prev_intra = 0
+        self.mb_type = 0
+        self.dif = [None, None]
+        self.r_size = [[0, 0], [0, 0]]
+        self.pmv = [[[0, 0], [0, 0]], [[0, 0], [0, 0]]]
         self.out = []
 
     # ---- frames / output (mpeg2.cpp:130-194, 1543-1573; m2decoder.h:54-80, 132-157)
@@ -189,6 +204,7 @@ class Decoder:
             self.out_state |= 1
         self.index = mi
         self.copy_src = self.ref[0]
+        self.dif = [self.ref[0], self.ref[1]]
 
     def peek(self, is_end):
         if self.coding_type == 3:
@@ -257,7 +273,7 @@ class Decoder:
                         self.qm[i] = q
         elif eid == 8:
             f = b.get(16)
-            self.r_size = [(f >> 12) - 1, ((f >> 8) & 15) - 1]
+            self.r_size = [[(f >> 12) - 1, ((f >> 8) & 15) - 1], [((f >> 4) & 15) - 1, (f & 15) - 1]]
             if not self.coding_type:
                 self.coding_type = (1 if (f & 0xff00) == 0xff00 else 2) if (f & 0xff) == 0xff else 3
             bits = b.get(14)
@@ -285,11 +301,14 @@ class Decoder:
             d = max(0, min(self.dc_max, d))
         return d << self.dc_scale
 
-    def block(self, b, dcv):
-        coef = [0] * 64
-        coef[0] = dcv
-        tab = self.c["dct1" if self.intra_vlc else "dct0"]
-        mismatch, idx = dcv, 1
+    def coefs(self, b, coef, idx, inter):
+        """parse_coef (mpeg2.cpp:1021-1097): coefficients from scan index idx (coef[0] kept when idx > 0),
+        dequantised, saturated, then mismatch control (MPEG-2) or oddification (MPEG-1)"""
+        tab = self.c["dct1" if (self.intra_vlc and not inter) else "dct0"]
+        qm = self.qm[1 if inter else 0]
+        mismatch = coef[0] if idx else 0
+        for k in range(idx, 64):
+            coef[k] = 0
         while True:
             run, level = b.vlc(tab)
             if run >= 0:
@@ -312,7 +331,8 @@ class Decoder:
             if idx >= 64:
                 break
             z = self.scan[idx]
-            t = ((level >> 1) * (self.qm[0][z] * self.qs)) >> 4
+            q = qm[z] * self.qs
+            t = (((level | 1) * q) >> 5) if inter else (((level >> 1) * q) >> 4)
             v = -t if level & 1 else t
             v = max(-2048, min(2047, v))
             mismatch += v
@@ -322,17 +342,49 @@ class Decoder:
             if not mismatch & 1:
                 coef[63] ^= 1
         else:
-            coef = [(c - 1 if c > 0 else c + 1) if c and not c & 1 else c for c in coef]
-        return idct_block(coef)
+            for k in range(64):
+                c = coef[k]
+                if c and not c & 1:
+                    coef[k] = c - 1 if c > 0 else c + 1
+        return coef
+
+    def block(self, b, dcv):
+        """an intra block: DC + AC (m2d_parse_intra_block_*), reconstructed samples (ClipStore)"""
+        coef = [0] * 64
+        coef[0] = dcv
+        return idct_block(self.coefs(b, coef, 1, False))
+
+    def inter_block(self, b):
+        """m2d_parse_inter_block (mpeg2.cpp:1317-1341): a first coefficient "1s" is level 1 at scan 0,
+        dequantised without saturation; the residual (AddStore adds it)"""
+        coef = [0] * 64
+        idx = 0
+        bits = b.show(2)
+        if bits & 2:
+            b.get(2)
+            t = ((bits | 1) * (self.qs * self.qm[1][0])) >> 5
+            coef[0] = -t if bits & 1 else t
+            idx = 1
+        return idct_raw(self.coefs(b, coef, idx, True))
 
     def cur(self):
         return self.frames[self.index if self.index >= 0 else 0]
 
+    def refframe(self, s):
+        """diff_to_ref[s] (set_ptrdiff): the frame of idx_of_ref[s] at the last update; before any, the
+        current frame itself (diff 0)"""
+        return self.cur() if self.dif[s] is None else self.frames[self.dif[s]]
+
+    def mb_reset(self):
+        """m2d_mb_reset: intra DC and motion vector predictors"""
+        r = (self.dc_max + 1) >> 1
+        self.pred = [r] * 3
+        self.pmv = [[[0, 0], [0, 0]], [[0, 0], [0, 0]]]
+
     def copy_mb(self):
-        if self.copy_src < 0:
-            return
+        """m2d_skip_mb_P's copy of the co-located MB of diff_to_ref[0] (in place before any update)"""
         fw = self.fsize[0]
-        src, dst = self.frames[self.copy_src], self.cur()
+        src, dst = self.refframe(0), self.cur()
         if src is dst:
             return
         for r in range(16):
@@ -368,13 +420,205 @@ class Decoder:
             if b.get(1):
                 return val + 1
 
-    def one_mv(self, b, r):
+    # ---- prediction (motioncomp.cpp:28-546; mpeg2.cpp:1277-1308, 740-808)
+    def predict(self, ref, cur, src, dst, stride, mvx, mvy, h, chroma, avg):
+        """m2d_motion_compensation_{luma,chroma}[_add]: 16 bytes x h rows at byte offset dst of plane cur
+        (row stride `stride`) from plane ref at byte offset src moved by the vector (half samples; chroma:
+        the vector halved toward zero, Cb / Cr interleaved); avg: AveStore (the second direction)"""
+        W = self.fsize[0]
+        if chroma:
+            mvx, mvy = int(mvx / 2), int(mvy / 2)
+            dx, gap = mvx & ~1, 2
+        else:
+            dx, gap = mvx >> 1, 1
+        hx, hy = mvx & 1, mvy & 1
+        s0 = src + stride * (mvy >> 1) + dx
+        col = src % W + dx
+        assert 0 <= col and col + 15 + gap * hx < W and s0 >= 0 and s0 + (h - 1 + hy) * stride + 15 + gap * hx < len(ref), \
+            "prediction outside the reference frame (the reference reads outside its buffers: UB)"
+        for r in range(h):
+            a0 = s0 + r * stride
+            b0 = a0 + stride
+            d0 = dst + r * stride
+            for c in range(16):
+                a = ref[a0 + c]
+                if hx and hy:
+                    v = (a + ref[a0 + c + gap] + ref[b0 + c] + ref[b0 + c + gap] + 2) >> 2
+                elif hx:
+                    v = (a + ref[a0 + c + gap] + 1) >> 1
+                elif hy:
+                    v = (a + ref[b0 + c] + 1) >> 1
+                else:
+                    v = a
+                cur[d0 + c] = (cur[d0 + c] + v + 1) >> 1 if avg else v
+
+    def motion_comp(self, s, avg, mvxy, ref_field):
+        """m2d_motion_comp: one direction of the current MB (frame: one vector; field: one per parity,
+        from the selected reference field, into the lines of that parity)"""
+        W = self.fsize[0]
+        ref, cur = self.refframe(s), self.cur()
+        lo = self.mb_y * 16 * W + self.mb_x * 16
+        co = self.mb_y * 8 * W + self.mb_x * 16
+        if self.mt[0] == 1:
+            self.predict(ref[0], cur[0], lo, lo, W, mvxy[0], mvxy[1], 16, False, avg)
+            self.predict(ref[1], cur[1], co, co, W, mvxy[0], mvxy[1], 8, True, avg)
+        else:
+            for i in range(2):
+                so = W if ref_field[i] else 0
+                mx, my = mvxy[2 * i], mvxy[2 * i + 1]
+                self.predict(ref[0], cur[0], lo + so, lo + i * W, 2 * W, mx, my, 8, False, avg)
+                self.predict(ref[1], cur[1], co + so, co + i * W, 2 * W, mx, my, 4, True, avg)
+
+    def skip_b(self, inc):
+        """m2d_skip_mb_B: the skipped MBs predicted like the last coded one — its directions, frame
+        prediction with the first vector predictor of each"""
+        d = self.mb_type & 3
+        bi = d == 3
+        one = 0 if bi else d >> 1
+        W = self.fsize[0]
+        for _ in range(inc - 1):
+            self.inc_pos()
+            lo = self.mb_y * 16 * W + self.mb_x * 16
+            co = self.mb_y * 8 * W + self.mb_x * 16
+            cur = self.cur()
+            dirs = [(0, False), (1, True)] if bi else [(one, False)]
+            for s, avg in dirs:
+                ref = self.refframe(s)
+                mx, my = self.pmv[s][0]
+                self.predict(ref[0], cur[0], lo, lo, W, mx, my, 16, False, avg)
+                self.predict(ref[1], cur[1], co, co, W, mx, my, 8, True, avg)
+
+    # ---- motion vectors (mpeg2.cpp:1189-1275)
+    def one_mv(self, b, pm, comp, r, is_field):
+        p = pm[comp]
         if b.get(1) == 0:
-            b.vlc(self.c["motion_code"])
-            if r > 0:
-                b.get(r)
+            code = b.vlc(self.c["motion_code"])[0]
+            res = 1 + b.get(r) if r > 0 else 1
+            mv = ((code - 1) << r) + res if code >= 0 else ((code + 1) << r) - res
+            mv += p >> is_field
+            lim = 16 << r
+            if mv < -lim:
+                mv += 2 * lim
+            elif mv >= lim:
+                mv -= 2 * lim
+        else:
+            mv = p >> is_field
+        pm[comp] = mv << is_field
+        return mv
+
+    def motion_vectors(self, b, s):
+        count, fmt_field, dmv = self.mt
+        pm = self.pmv[s]
+        rs = self.r_size[s]
+        if count == 1:
+            if fmt_field and not dmv:
+                b.get(1)  # motion_vertical_field_select (not used)
+            mx = self.one_mv(b, pm[0], 0, rs[0], 0)
+            if dmv and b.get(1):
+                b.get(1)
+            my = self.one_mv(b, pm[0], 1, rs[1], 1 if fmt_field else 0)
+            if dmv and b.get(1):
+                b.get(1)
+            pm[1][0], pm[1][1] = pm[0][0], pm[0][1]
+            return [mx, my], None
+        out, rf = [], []
+        for i in range(2):
+            rf.append(b.get(1))
+            out.append(self.one_mv(b, pm[i], 0, rs[0], 0))
+            out.append(self.one_mv(b, pm[i], 1, rs[1], 1))
+        return out, rf
+
+    # ---- macroblocks (mpeg2.cpp:834-872, 1136-1187, 1343-1417)
+    MT = [[(2, 1, 0), (2, 1, 0), (1, 0, 0), (1, 1, 1)], [(1, 1, 0), (1, 1, 0), (2, 1, 0), (1, 1, 1)]]
+
+    def mb_modes(self, b):
+        ct = self.coding_type
+        if ct == 2:
+            t = b.vlc(self.c["mb_type_p"])[0]
+        elif ct == 3:
+            t = b.vlc(self.c["mb_type_b"])[0]
+        elif b.show(1):
+            b.get(1)
+            t = 4
+        else:
+            b.get(2)
+            t = 20
+        fm = self.frame_mode
+        if t & 3:
+            if fm & 1:
+                self.mt = self.MT[0][b.get(2) if fm == 1 else 2]
+            else:
+                self.mt = self.MT[1][b.get(2)]
+        else:
+            k = 1 if fm == 0 else 0
+            self.mt = self.MT[k][2 - k]
+        if fm == 1 and t & 12:
+            self.dct_type = b.get(1)
+        else:
+            self.dct_type = 0 if fm else 1
+        return t
+
+    def put_block(self, px, i, add):
+        """m2d_idct_{intra,inter}_{luma,chroma}: block i of the current MB (LUMA_BLOCK_OFFSET, stride
+        W << dct_type; chroma interleaved), ClipStore / AddStore"""
+        f = self.cur()
+        fw = self.fsize[0]
+        if i < 4:
+            plane = f[0]
+            bx = self.mb_x * 16 + (i & 1) * 8
+            rows = [self.mb_y * 16 + ((i >> 1) + 2 * r if self.dct_type else (i >> 1) * 8 + r) for r in range(8)]
+            offs = [[y * fw + bx + k for k in range(8)] for y in rows]
+        else:
+            plane = f[1]
+            offs = [[(self.mb_y * 8 + r) * fw + self.mb_x * 16 + 2 * k + (i - 4) for k in range(8)] for r in range(8)]
+        for r in range(8):
+            for k in range(8):
+                o = offs[r][k]
+                v = plane[o] + px[r][k] if add else px[r][k]
+                assert -256 <= v <= 767, "CLIP255C argument outside the reference table (UB)"
+                plane[o] = 0 if v < 0 else 255 if v > 255 else v
+
+    def macroblock(self, b):
+        """m2d_parse_macroblock"""
+        prev_intra = self.mb_type & 4
+        t = self.mb_modes(b)
+        self.mb_type = t
+        if t & 4:
+            if not prev_intra:
+                self.pred = [(self.dc_max + 1) >> 1] * 3
+            if t & 16:
+                self.qs = Q_SCALE[self.qst][b.get(5)]
+            if self.conceal:
+                self.motion_vectors(b, 0)
+                b.get(1)
+            for i in range(4):
+                self.put_block(self.block(b, self.dc(b, 0)), i, False)
+            for cc in range(2):
+                self.put_block(self.block(b, self.dc(b, 1 + cc)), 4 + cc, False)
+            return
+        if prev_intra:
+            self.pmv = [[[0, 0], [0, 0]], [[0, 0], [0, 0]]]
+        if t & 16:
+            self.qs = Q_SCALE[self.qst][b.get(5)]
+        if t & 3:
+            fwd = t & 1
+            if fwd:
+                mvxy, rf = self.motion_vectors(b, 0)
+                self.motion_comp(0, False, mvxy, rf)
+            if t & 2:
+                mvxy, rf = self.motion_vectors(b, 1)
+                self.motion_comp(1, fwd != 0, mvxy, rf)
+        else:  # m2d_skip_mb_P(mb, 0)
+            self.copy_mb()
+            self.mb_reset()
+        if t & 8:
+            cbp = b.vlc(self.c["cbp"])[0]
+            for i in range(6):
+                if cbp & (1 << (5 - i)):
+                    self.put_block(self.inter_block(b), i, True)
 
     def slice(self, b, code):
+        """m2d_read_slice + m2d_decode_macroblocks (mpeg2.cpp:625-660, 1502-1524)"""
         vpos = code - 1
         self.qs = Q_SCALE[self.qst][b.get(5)]
         if vpos == 0:
@@ -383,8 +627,8 @@ class Decoder:
         fw = self.fsize[0]
         if mbh <= vpos:
             return 0
-        if 1 < vpos - self.mb_y and self.copy_src >= 0:
-            src, dst = self.frames[self.copy_src], self.cur()
+        if 1 < vpos - self.mb_y:  # m2d_copy_slice
+            src, dst = self.refframe(0), self.cur()
             if src is not dst:
                 lo, n = (self.mb_y + 1) * 16 * fw, fw * (vpos - self.mb_y - 1) * 16
                 dst[0][lo:lo + n] = src[0][lo:lo + n]
@@ -394,50 +638,19 @@ class Decoder:
             b.get(8)
             while b.get(1):
                 b.get(8)
-        reset = (self.dc_max + 1) >> 1
-        self.pred = [reset] * 3
+        self.mb_reset()
         while True:
             inc = self.mb_inc(b)
             if inc > 1:
-                for _ in range(inc - 1):
-                    self.inc_pos()
-                    self.copy_mb()
-                self.pred = [reset] * 3
+                if self.coding_type == 3:
+                    self.skip_b(inc)
+                else:  # m2d_skip_mb_P (also the I table's entry)
+                    for _ in range(inc - 1):
+                        self.inc_pos()
+                        self.copy_mb()
+                    self.mb_reset()
             self.inc_pos()
-            quant = 0
-            if b.show(1):
-                b.get(1)
-            else:
-                b.get(2)
-                quant = 1
-            if not self.prev_intra:
-                self.pred = [reset] * 3
-            self.prev_intra = 1
-            if self.frame_mode == 1:
-                dct_type = b.get(1)
-            else:
-                dct_type = 0 if self.frame_mode else 1
-            if quant:
-                self.qs = Q_SCALE[self.qst][b.get(5)]
-            if self.conceal:
-                if self.frame_mode == 0:
-                    b.get(1)
-                self.one_mv(b, self.r_size[0])
-                self.one_mv(b, self.r_size[1])
-                b.get(1)
-            f = self.cur()
-            for i in range(4):
-                px = self.block(b, self.dc(b, 0))
-                bx = self.mb_x * 16 + (i & 1) * 8
-                for r in range(8):
-                    y = self.mb_y * 16 + ((i >> 1) + 2 * r if dct_type else (i >> 1) * 8 + r)
-                    f[0][y * fw + bx:y * fw + bx + 8] = bytes(px[r])
-            for cc in range(2):
-                px = self.block(b, self.dc(b, 1 + cc))
-                for r in range(8):
-                    y = self.mb_y * 8 + r
-                    for k in range(8):
-                        f[1][y * fw + self.mb_x * 16 + 2 * k + cc] = px[r][k]
+            self.macroblock(b)
             if (self.mb_y == mbh - 1 and fw // 16 - 1 <= self.mb_x) or mbh <= self.mb_y:
                 self.mb_x, self.mb_y = -1, 0
                 return 1
@@ -452,9 +665,16 @@ class Decoder:
             if code == 0:
                 b.get(10)
                 self.coding_type = b.get(3)
-                if self.coding_type != 1:
-                    raise ValueError("only intra pictures")
+                b.get(16)
+                if self.coding_type not in (1, 2, 3):
+                    raise ValueError("D pictures")
                 self.mb_x, self.mb_y = -1, 0
+                if self.coding_type in (2, 3):  # full_pel + f_code as one value - 1 (mpeg2.cpp:608-618)
+                    r = b.get(4) - 1
+                    self.r_size[0] = [r, r]
+                    if self.coding_type == 3:
+                        r = b.get(4) - 1
+                        self.r_size[1] = [r, r]
             elif code < 0xb0:
                 try:
                     if self.slice(b, code) == 1:

@@ -1,5 +1,6 @@
 """MPEG-1/2 video, BASELINE.json configs[0] (C1: MPEG-2 MP@ML 720x480 I-frame-only .m2v on the CPU path),
-through the reference-shaped m2d_func table (m2dec_amd/csrc/host/mpeg2_dec.c).
+and P / B frame pictures, through the reference-shaped m2d_func table (m2dec_amd/csrc/host/mpeg2_dec.c)
+with the host reconstruction (the gfx950 one: tests/test_gpu_mpeg2.py).
 
 Pinned by the reference itself:
   * every VLC table against the codewords of the reference's own tables (tests/golden/mpeg2_vlc.json,
@@ -145,10 +146,50 @@ def test_c1_cli_md5(built, tmp_path):
     assert r.returncode == 0 and (tmp_path / "c1.out").read_bytes() == out
 
 
-def test_p_pictures_are_reported(built):
-    """P / B pictures (motion compensation) are not decoded: decode_picture returns -1 at their header."""
+PB_SMALL = ["cov_m2v_pb_s1", "cov_m2v_pb_s2", "cov_m2v_pb_field_s1", "cov_m2v_pb_field_s2", "cov_mpeg1_pb_s1"]
+
+
+@pytest.mark.parametrize("name", PB_SMALL)
+def test_m2v_pb_matches_oracle_and_golden(built, name):
+    """P / B frame pictures (every macroblock type, skips, frame / field / dual-prime MC, field DCT,
+    f_codes 1-4, lost slices) on the host reconstruction: the golden, and the oracle's restatement of
+    mpeg2.cpp + motioncomp.cpp; no output depends on reference UB (CLIP255C domain, reads outside the
+    reference frame)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mpeg2_oracle
+    data = m2v_stream(name)
+    got = m2dec_amd.decode_m2v(data)
+    assert m2dec_amd.m2v_last_checks() == (0, 0)
+    assert got == GOLD[name]["md5"]
+    assert mpeg2_oracle.decode(data) == GOLD[name]["md5"]
+
+
+def test_c1_pb_matches_golden(built):
+    """C1's geometry (720x480) with P / B pictures; its golden was checked against the oracle on every
+    frame when it was made (tools/make_m2v_goldens.py)."""
+    got, err = m2dec_amd.decode_table_frames("m2d_func", m2v_stream("c1_pb_480p_s1"))
+    assert err == -1
+    assert got == GOLD["c1_pb_480p_s1"]["md5"]
+    assert m2dec_amd.m2v_last_checks() == (0, 0)
+
+
+def test_m2v_pb_emptify_same_frames(built):
+    """h264dec -e (emptify the output queue after each picture) delivers the same frames in the same order."""
+    data = m2v_stream("cov_m2v_pb_s1")
+    assert m2dec_amd.decode_m2v(data, emptify=True) == GOLD["cov_m2v_pb_s1"]["md5"]
+
+
+def test_d_pictures_are_reported(built):
+    """D pictures (picture_coding_type 4) are not decoded: decode_picture returns -1 at their header."""
     data = bytearray(m2v_stream("cov_m2v_s1"))
     k = data.find(b"\x00\x00\x01\x00", 100)  # the second picture header
-    data[k + 5] = (data[k + 5] & 0xc7) | (2 << 3)  # picture_coding_type = P
+    data[k + 5] = (data[k + 5] & 0xc7) | (4 << 3)  # picture_coding_type = D
     got, err = m2dec_amd.decode_table_frames("m2d_func", bytes(data))
     assert err == -1 and len(got) < GOLD["cov_m2v_s1"]["frames"]
+
+
+def test_gpu_reconstruction_has_no_host_fallback(built):
+    """decode_m2v(device=n) on a device that does not exist (or with no GPU at all) is an error, never a
+    silent host decode."""
+    with pytest.raises(RuntimeError):
+        m2dec_amd.decode_m2v(m2v_stream("cov_m2v_pb_s1"), device=64)

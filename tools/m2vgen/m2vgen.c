@@ -7,7 +7,14 @@
  * matrices (sequence header and quant matrix extension), escape codes, slices starting mid-row,
  * missing slices, MPEG-1 syntax (8/16-bit escapes, oddification).
  *
- *   m2vgen --preset c1|cov_m2v|cov_m2v_slices|cov_mpeg1 [--seed N] [--frames N] [--size WxH] -o out.m2v
+ * P / B coverage (presets *_pb): coded order I P B B P B B ..., every macroblock type of Tables B.3 /
+ * B.4 (with / without MC, coded / not coded, quantiser changes, intra), skipped macroblocks (P: copies,
+ * B: the last vectors repeated), frame / field / dual-prime motion types, field DCT, f_codes 1-4, motion
+ * vectors against the decoder's predictors (kept inside the reference frames: the reference does not
+ * bound its reads), non-intra quantiser matrices, lost slices.
+ *
+ *   m2vgen --preset c1|c1_pb|cov_m2v|cov_m2v_slices|cov_mpeg1|cov_m2v_pb|cov_m2v_pb_field|cov_mpeg1_pb
+ *          [--seed N] [--frames N] [--size WxH] -o out.m2v
  *
  * Encoding: floating-point forward DCT of procedural 8x8 blocks, quantised to the levels the
  * decoder's dequantiser expects; codes from the VLC lists of m2dec_amd/csrc/host/mpeg2_tables.c.
@@ -27,6 +34,8 @@ typedef struct {
 	int drop_slice;           /* leave out one slice row now and then (lost-slice copy) */
 	int intra_vlc_format, dc_precision;
 	uint64_t seed;
+	int pb;                   /* I P B B P B B ... (coded order) */
+	int field_mc;             /* P / B pictures with frame_pred_frame_dct 0 (field / dual-prime MC, field DCT) */
 } params_t;
 
 static uint64_t rng_s;
@@ -194,9 +203,262 @@ static void put_qmat(bw_t *w, const uint8_t *q, const uint8_t *scan)
 	for (int i = 0; i < 64; ++i) bw_bits(w, q[scan[i]], 8);
 }
 
+/* ---------------------------------------------------------------- P / B pictures */
+/* the decoder state the syntax depends on (mpeg2.cpp m2d_mb_current: mv predictors, type of the last
+ * coded MB, intra DC predictors), mirrored so that every vector lands where the generator wants it */
+typedef struct {
+	int16_t pmv[2][2][2];
+	int prev_type;            /* M2V_MBF_* of the last coded MB (persists over slices and pictures) */
+	int ctype;                /* 2 P, 3 B */
+	int r_size[2][2];
+	int frame_mode;           /* 3: frame_pred_frame_dct, 1: frame picture with field MC / DCT choices */
+	int w, h;                 /* frame (multiple of 16) */
+	int vary;
+} pbstate_t;
+
+static pbstate_t g_pb;
+
+static void pb_reset_mv(void) { memset(g_pb.pmv, 0, sizeof(g_pb.pmv)); }
+
+static void enc_reset_dc(enc_t *e)
+{
+	e->dc_pred[0] = e->dc_pred[1] = e->dc_pred[2] = (int16_t)(1 << (7 + e->dc_precision));
+}
+
+/* is a 16 x 16 prediction with vector (mvx, mvy) (half samples) of the MB at (mbx, mby) inside the
+ * frame?  field: one field's 16 x 8 lines (vertical vector in field lines) */
+static int mv_inside(int mbx, int mby, int mvx, int mvy, int field)
+{
+	const int W = g_pb.w, H = field ? g_pb.h / 2 : g_pb.h, lh = field ? 8 : 16, ch = field ? 4 : 8;
+	const int x = mbx * 16 + (mvx >> 1), y = mby * lh + (mvy >> 1);
+	const int cx = mvx / 2, cy = mvy / 2;
+	const int xc = mbx * 16 + 2 * (cx >> 1), yc = mby * ch + (cy >> 1);
+	if (x < 0 || y < 0 || x + 16 + (mvx & 1) > W || y + lh + (mvy & 1) > H) return 0;
+	if (xc < 0 || yc < 0 || xc + 16 + 2 * (cx & 1) > W || yc + ch + (cy & 1) > H / 2) return 0;
+	return 1;
+}
+
+/* one vector component: `mv` against the predictor *pmv (stored << is_field), as m2d_one_mv decodes */
+static void put_one_mv(bw_t *w, int16_t *pmv, int mv, int r_size, int is_field)
+{
+	const int limit = 16 << r_size;
+	int delta = mv - (*pmv >> is_field);
+	if (delta < -limit) delta += 2 * limit;
+	if (delta >= limit) delta -= 2 * limit;
+	if (!delta) {
+		bw_bit(w, 1);
+	} else {
+		const int a = abs(delta) - 1;
+		put_code(w, find_code(m2v_motion_code, (a >> r_size) + 1));
+		bw_bit(w, delta < 0);
+		if (r_size) bw_bits(w, (uint32_t)(a & ((1 << r_size) - 1)), r_size);
+	}
+	*pmv = (int16_t)(mv << is_field);
+}
+
+/* a random vector component in [-limit, limit) biased to small values */
+static int rnd_mv(int r_size)
+{
+	const int limit = 16 << r_size;
+	const int k = rnd_n(4);
+	int v = k == 0 ? 0 : k == 1 ? rnd_n(9) - 4 : rnd_n(2 * limit) - limit;
+	return v;
+}
+
+/* motion vectors of direction s for motion type mt (2 frame, 1 field, 3 dual prime) of the MB at
+ * (mbx, mby), chosen inside the frame */
+static void put_mvs(bw_t *w, int s, int mt, int mbx, int mby)
+{
+	const int *rs = g_pb.r_size[s];
+	if (mt == 1) {
+		for (int i = 0; i < 2; ++i) {
+			int vx = 0, vy = 0;
+			for (int tries = 0; tries < 16; ++tries) {
+				vx = rnd_mv(rs[0]);
+				vy = rnd_mv(rs[1]);
+				if (mv_inside(mbx, mby, vx, vy, 1)) break;
+				vx = vy = 0;
+			}
+			bw_bit(w, rnd_n(2)); /* motion_vertical_field_select */
+			put_one_mv(w, &g_pb.pmv[s][i][0], vx, rs[0], 0);
+			put_one_mv(w, &g_pb.pmv[s][i][1], vy, rs[1], 1);
+		}
+		return;
+	}
+	{
+		int vx = 0, vy = 0;
+		for (int tries = 0; tries < 16; ++tries) {
+			vx = rnd_mv(rs[0]);
+			vy = rnd_mv(rs[1]);
+			if (mv_inside(mbx, mby, vx, vy, 0)) break;
+			vx = vy = 0;
+		}
+		put_one_mv(w, &g_pb.pmv[s][0][0], vx, rs[0], 0);
+		if (mt == 3) { /* dmvector: 0, or 1 s */
+			const int d = rnd_n(3);
+			bw_bit(w, d != 0);
+			if (d) bw_bit(w, d == 2);
+		}
+		/* dual prime: the vertical component is parsed as a field vector (the reference then predicts
+		 * a frame with it) */
+		put_one_mv(w, &g_pb.pmv[s][0][1], vy, rs[1], mt == 3);
+		if (mt == 3) {
+			const int d = rnd_n(3);
+			bw_bit(w, d != 0);
+			if (d) bw_bit(w, d == 2);
+		}
+		g_pb.pmv[s][1][0] = g_pb.pmv[s][0][0];
+		g_pb.pmv[s][1][1] = g_pb.pmv[s][0][1];
+	}
+}
+
+/* a non-intra block: a few small coefficients (table B.14; a first coefficient of run 0 / level 1 as
+ * "1s"), sometimes escaped, then end of block */
+static void put_inter_block(bw_t *w, enc_t *e, int force_escape)
+{
+	const int n = 1 + rnd_n(3);
+	int idx = -1;
+	for (int k = 0; k < n; ++k) {
+		const int run = rnd_n(k ? 8 : 4);
+		const int level = 1 + (rnd_n(4) == 0);
+		const int neg = rnd_n(2);
+		if (idx + 1 + run >= 64) break;
+		idx += 1 + run;
+		if (k == 0 && run == 0 && level == 1) {
+			bw_bit(w, 1);
+			bw_bit(w, neg);
+			continue;
+		}
+		{
+			const char *c = (force_escape && rnd_n(2)) ? NULL : dct_code(0, run, level);
+			const int l = neg ? -level : level;
+			if (c) {
+				put_code(w, c);
+				bw_bit(w, neg);
+			} else {
+				put_code(w, "000001");
+				bw_bits(w, (uint32_t)run, 6);
+				if (e->mpeg2) bw_bits(w, (uint32_t)l & 0xfff, 12);
+				else bw_bits(w, (uint32_t)l & 0xff, 8);
+			}
+		}
+	}
+	put_code(w, "10");
+}
+
+/* the B-skip prediction of the MB at (mbx, mby) (m2d_skip_mb_B: the last MB's directions, frame MC with
+ * the first predictor of each) stays inside the frame */
+static int b_skip_ok(int mbx, int mby)
+{
+	const int dir = g_pb.prev_type & (M2V_MBF_FWD | M2V_MBF_BWD);
+	const int bi = dir == (M2V_MBF_FWD | M2V_MBF_BWD);
+	const int one = bi ? 0 : (dir >> 1);
+	for (int s = 0; s < 2; ++s) {
+		if (!bi && s != one) continue;
+		if (!mv_inside(mbx, mby, g_pb.pmv[s][0][0], g_pb.pmv[s][0][1], 0)) return 0;
+	}
+	return 1;
+}
+
+/* one coded macroblock of a P / B picture (6.2.5 order: type, motion type, dct_type, quantiser,
+ * vectors, coded_block_pattern, blocks) */
+static void put_pb_mb(bw_t *w, enc_t *e, int mbx, int mby, int t, int seed, int mpeg2)
+{
+	int type;
+	if (g_pb.ctype == 2) {
+		static const int tp[] = {9, 9, 9, 8, 1, 1, 4, 25, 24, 20};
+		type = tp[rnd_n(10)];
+	} else {
+		static const int tb[] = {3, 11, 11, 2, 10, 10, 1, 9, 9, 4, 27, 25, 26, 20};
+		type = tb[rnd_n(14)];
+	}
+	put_code(w, find_code(g_pb.ctype == 2 ? m2v_mb_type_p : m2v_mb_type_b, type));
+	{
+		const int prev_intra = (g_pb.prev_type & M2V_MBF_INTRA) != 0;
+		const int mc = type & (M2V_MBF_FWD | M2V_MBF_BWD);
+		int mt = 2;
+		g_pb.prev_type = type;
+		if (mc && g_pb.frame_mode == 1) {
+			const int k = rnd_n(g_pb.ctype == 2 ? 7 : 5);
+			mt = k < 3 ? 2 : k < 5 ? 1 : 3; /* (dual prime in P pictures only) */
+			bw_bits(w, (uint32_t)mt, 2);
+		}
+		if (g_pb.frame_mode == 1 && (type & (M2V_MBF_INTRA | M2V_MBF_PATTERN))) bw_bit(w, rnd_n(2)); /* dct_type */
+		if (type & M2V_MBF_QUANT) {
+			e->qcode = 1 + rnd_n(20);
+			bw_bits(w, (uint32_t)e->qcode, 5);
+		}
+		if (type & M2V_MBF_INTRA) {
+			double blk[64];
+			if (!prev_intra) enc_reset_dc(e);
+			for (int b = 0; b < 4; ++b) {
+				for (int y = 0; y < 8; ++y)
+					for (int x = 0; x < 8; ++x) blk[y * 8 + x] = sample(0, mbx * 16 + (b & 1) * 8 + x, mby * 16 + (b >> 1) * 8 + y, t, seed);
+				put_block(w, e, blk, 0, rnd_n(16) == 0);
+			}
+			for (int c = 0; c < 2; ++c) {
+				for (int y = 0; y < 8; ++y)
+					for (int x = 0; x < 8; ++x) blk[y * 8 + x] = sample(1 + c, mbx * 8 + x, mby * 8 + y, t, seed);
+				put_block(w, e, blk, 1 + c, rnd_n(16) == 0);
+			}
+			return;
+		}
+		if (prev_intra) pb_reset_mv();
+		if (mc) {
+			if (type & M2V_MBF_FWD) put_mvs(w, 0, mt, mbx, mby);
+			if (type & M2V_MBF_BWD) put_mvs(w, 1, mt, mbx, mby);
+		} else { /* P "no MC": the co-located MB, predictors reset */
+			pb_reset_mv();
+			enc_reset_dc(e);
+		}
+		if (type & M2V_MBF_PATTERN) {
+			const int cbp = 1 + rnd_n(63);
+			put_code(w, find_code(m2v_cbp, cbp));
+			for (int i = 0; i < 6; ++i)
+				if (cbp & (1 << (5 - i))) put_inter_block(w, e, rnd_n(12) == 0);
+		}
+		(void)mpeg2;
+	}
+}
+
+/* the slices of a P / B picture: one per MB row (a row left out now and then); macroblocks inside a
+ * slice skipped at random where the syntax and the in-frame rule allow */
+static void put_pb_slices(bw_t *w, enc_t *e, int mbw, int mbh, int t, int seed, int drop_row)
+{
+	for (int y = 0; y < mbh; ++y) {
+		int skip = 0;
+		if (y == drop_row) continue;
+		start_code(w, y + 1);
+		bw_bits(w, (uint32_t)e->qcode, 5);
+		bw_bit(w, 0);
+		enc_reset_dc(e);
+		pb_reset_mv();
+		for (int x = 0; x < mbw; ++x) {
+			if (x > 0 && x < mbw - 1 && rnd_n(5) == 0 && (g_pb.ctype == 2 || b_skip_ok(x, y))) {
+				skip++;
+				continue;
+			}
+			if (skip && g_pb.ctype == 2) { /* m2d_skip_mb_P: predictors reset after the copies */
+				pb_reset_mv();
+				enc_reset_dc(e);
+			}
+			{
+				int inc = skip + 1;
+				while (inc > 33) {
+					put_code(w, "00000001000");
+					inc -= 33;
+				}
+				put_code(w, find_code(m2v_mb_inc, inc));
+			}
+			skip = 0;
+			put_pb_mb(w, e, x, y, t, seed, e->mpeg2);
+		}
+	}
+}
+
 int main(int argc, char **argv)
 {
-	params_t p = {720, 480, 30, 1, 8, 0, 0, 0, 1, 0, 1};
+	params_t p = {720, 480, 30, 1, 8, 0, 0, 0, 1, 0, 1, 0, 0};
 	const char *out = NULL, *preset = "c1";
 	for (int i = 1; i < argc; ++i) {
 		if (!strcmp(argv[i], "--preset") && i + 1 < argc) preset = argv[++i];
@@ -207,7 +469,7 @@ int main(int argc, char **argv)
 			p.w = -p.w;
 		} else if (!strcmp(argv[i], "-o") && i + 1 < argc) out = argv[++i];
 		else {
-			fprintf(stderr, "usage: m2vgen --preset c1|cov_m2v|cov_m2v_slices|cov_mpeg1 [--seed N] [--frames N] [--size WxH] -o out.m2v\n");
+			fprintf(stderr, "usage: m2vgen --preset c1|c1_pb|cov_m2v|cov_m2v_slices|cov_mpeg1|cov_m2v_pb|cov_m2v_pb_field|cov_mpeg1_pb [--seed N] [--frames N] [--size WxH] -o out.m2v\n");
 			return 2;
 		}
 	}
@@ -221,6 +483,14 @@ int main(int argc, char **argv)
 			p.slices_midrow = p.drop_slice = !strcmp(preset, "cov_m2v_slices");
 		} else if (!strcmp(preset, "cov_mpeg1")) {
 			p.w = 176, p.h = 144, p.frames = 6, p.mpeg2 = 0, p.vary = 1;
+		} else if (!strcmp(preset, "c1_pb")) { /* C1's geometry with P / B pictures (GPU reconstruction bench) */
+			p.w = 720, p.h = 480, p.frames = 30, p.mpeg2 = 1, p.qscale_code = 8, p.vary = 0, p.pb = 1;
+			p.intra_vlc_format = 1, p.dc_precision = 0;
+		} else if (!strcmp(preset, "cov_m2v_pb") || !strcmp(preset, "cov_m2v_pb_field")) {
+			p.w = 176, p.h = 144, p.frames = 10, p.mpeg2 = 1, p.vary = 1, p.pb = 1, p.drop_slice = 1;
+			p.field_mc = !strcmp(preset, "cov_m2v_pb_field");
+		} else if (!strcmp(preset, "cov_mpeg1_pb")) {
+			p.w = 176, p.h = 144, p.frames = 10, p.mpeg2 = 0, p.vary = 1, p.pb = 1;
 		} else {
 			fprintf(stderr, "m2vgen: unknown preset %s\n", preset);
 			return 2;
@@ -240,8 +510,13 @@ int main(int argc, char **argv)
 	 * the next sequence header (mpeg2.cpp:258-266, 381-403) */
 	static uint8_t ext_intra[64];
 	const uint8_t *cur_qmat = m2v_default_intra_qmat;
+	g_pb.w = p.w;
+	g_pb.h = p.h;
+	g_pb.vary = p.vary;
 	for (int t = 0; t < p.frames; ++t) {
 		enc_t e;
+		/* coded order I P B B P B B ... (an I picture every 9 in the coverage streams) */
+		const int ctype = !p.pb || t == 0 || (p.vary && t % 9 == 0) ? 1 : (t % 3 == 1 ? 2 : 3);
 		memset(&e, 0, sizeof(e));
 		e.mpeg2 = p.mpeg2;
 		if (t == 0 || (p.vary && t % 3 == 0)) {
@@ -258,7 +533,14 @@ int main(int argc, char **argv)
 			bw_bit(&w, seq_loaded);
 			if (seq_loaded) put_qmat(&w, seq_intra, m2v_scan[0]);
 			cur_qmat = seq_loaded ? seq_intra : m2v_default_intra_qmat;
-			bw_bit(&w, 0);          /* default non-intra matrix */
+			if (p.pb && p.vary && rnd_n(2)) { /* a non-intra matrix */
+				uint8_t ni[64];
+				for (int i = 0; i < 64; ++i) ni[i] = (uint8_t)(8 + rnd_n(33));
+				bw_bit(&w, 1);
+				put_qmat(&w, ni, m2v_scan[0]);
+			} else {
+				bw_bit(&w, 0);          /* default non-intra matrix */
+			}
 			if (p.mpeg2) {
 				start_code(&w, 0xb5);
 				bw_bits(&w, 1, 4);      /* sequence extension */
@@ -291,21 +573,45 @@ int main(int argc, char **argv)
 		}
 		/* picture header, 6.2.3 */
 		start_code(&w, 0x00);
-		bw_bits(&w, (uint32_t)t & 1023, 10);
-		bw_bits(&w, 1, 3); /* I */
+		{
+			/* temporal_reference: display order of I0 P3 B1 B2 P6 B4 B5 ... */
+			const int tr = ctype == 2 ? t + 2 : ctype == 3 ? t - 1 : t;
+			bw_bits(&w, (uint32_t)tr & 1023, 10);
+		}
+		bw_bits(&w, (uint32_t)ctype, 3);
 		bw_bits(&w, 0xffff, 16);
+		g_pb.ctype = ctype;
+		if (ctype != 1) {
+			/* f_codes 1-4 (r_size 0-3); MPEG-2 sends them in the picture coding extension and 0111 here */
+			for (int s2 = 0; s2 < 2; ++s2)
+				for (int c = 0; c < 2; ++c) g_pb.r_size[s2][c] = p.vary ? rnd_n(4) : 1;
+			if (!p.mpeg2) { /* one f_code per direction */
+				g_pb.r_size[0][1] = g_pb.r_size[0][0];
+				g_pb.r_size[1][1] = g_pb.r_size[1][0];
+			}
+			bw_bits(&w, p.mpeg2 ? 7 : (uint32_t)(g_pb.r_size[0][0] + 1), 4); /* full_pel 0 + f_code */
+			if (ctype == 3) bw_bits(&w, p.mpeg2 ? 7 : (uint32_t)(g_pb.r_size[1][0] + 1), 4);
+		}
 		bw_bit(&w, 0);
 		e.qmat = cur_qmat;
-		e.qcode = p.vary ? 1 + rnd_n(31) : p.qscale_code;
+		e.qcode = p.vary ? 1 + rnd_n(ctype == 1 ? 31 : 20) : p.qscale_code;
 		if (p.mpeg2) {
 			e.intra_vlc_format = p.vary ? rnd_n(2) : p.intra_vlc_format;
 			e.alternate_scan = p.vary ? rnd_n(2) : 0;
 			e.q_scale_type = p.vary ? rnd_n(2) : 0;
 			e.dc_precision = p.vary ? rnd_n(4) : p.dc_precision;
 			e.frame_pred_frame_dct = p.vary ? rnd_n(2) : 1;
+			if (ctype != 1 && p.field_mc) e.frame_pred_frame_dct = 0;
 			start_code(&w, 0xb5); /* picture coding extension, 6.2.3.1 */
 			bw_bits(&w, 8, 4);
-			bw_bits(&w, 0xffff, 16); /* f_codes (I picture) */
+			if (ctype == 1) {
+				bw_bits(&w, 0xffff, 16); /* f_codes (I picture) */
+			} else {
+				bw_bits(&w, (uint32_t)(g_pb.r_size[0][0] + 1), 4);
+				bw_bits(&w, (uint32_t)(g_pb.r_size[0][1] + 1), 4);
+				bw_bits(&w, ctype == 3 ? (uint32_t)(g_pb.r_size[1][0] + 1) : 15, 4);
+				bw_bits(&w, ctype == 3 ? (uint32_t)(g_pb.r_size[1][1] + 1) : 15, 4);
+			}
 			bw_bits(&w, (uint32_t)e.dc_precision, 2);
 			bw_bits(&w, 3, 2);       /* frame picture */
 			bw_bit(&w, 0);           /* top_field_first */
@@ -332,6 +638,12 @@ int main(int argc, char **argv)
 		} else {
 			e.dc_precision = 0;
 			e.frame_pred_frame_dct = 1;
+		}
+		g_pb.frame_mode = (p.mpeg2 && !e.frame_pred_frame_dct) ? 1 : 3;
+		if (ctype != 1) {
+			const int drop_row = (p.drop_slice && rnd_n(3) == 0) ? 1 + rnd_n(mbh - 2) : -1;
+			put_pb_slices(&w, &e, mbw, mbh, t, (int)p.seed, drop_row);
+			continue;
 		}
 		/* slices: one per MB row; coverage: some rows split inside the row, a row left out */
 		const int drop_row = (p.drop_slice && t > 0 && t % 2 == 0) ? 1 + rnd_n(mbh - 2) : -1;
@@ -369,6 +681,7 @@ int main(int argc, char **argv)
 				}
 			}
 		}
+		g_pb.prev_type = M2V_MBF_INTRA;
 	}
 	start_code(&w, 0xb7); /* sequence end */
 	{

@@ -18,7 +18,11 @@ import mpeg2_oracle  # noqa: E402
 
 GEN = os.path.join(ROOT, "tools", "_build", "m2vgen")
 STREAMS = [("c1_480p_s1", "c1", 1, 30), ("cov_m2v_s1", "cov_m2v", 1, 8), ("cov_m2v_s2", "cov_m2v", 2, 8),
-           ("cov_m2v_slices_s1", "cov_m2v_slices", 1, 8), ("cov_mpeg1_s1", "cov_mpeg1", 1, 6)]
+           ("cov_m2v_slices_s1", "cov_m2v_slices", 1, 8), ("cov_mpeg1_s1", "cov_mpeg1", 1, 6),
+           # P / B pictures (coded order I P B B ...): frame / field / dual-prime MC, skips, lost slices
+           ("c1_pb_480p_s1", "c1_pb", 1, 30), ("cov_m2v_pb_s1", "cov_m2v_pb", 1, 10),
+           ("cov_m2v_pb_s2", "cov_m2v_pb", 2, 10), ("cov_m2v_pb_field_s1", "cov_m2v_pb_field", 1, 10),
+           ("cov_m2v_pb_field_s2", "cov_m2v_pb_field", 2, 10), ("cov_mpeg1_pb_s1", "cov_mpeg1_pb", 1, 10)]
 
 
 def gen(preset, seed, frames):
@@ -35,6 +39,7 @@ def main():
     for name, preset, seed, frames in STREAMS:
         data = gen(preset, seed, frames)
         got = m2dec_amd.decode_m2v(data)
+        assert m2dec_amd.m2v_last_checks() == (0, 0), f"{name}: output depends on reference UB"
         ref = mpeg2_oracle.decode(data)
         assert got == ref, f"{name}: product and oracle differ on frames " \
                            f"{[i for i, (a, b) in enumerate(zip(got, ref)) if a != b][:8]} ({len(got)} vs {len(ref)})"

@@ -77,3 +77,12 @@ clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build
 
 .PHONY: all clean stamps variant
+
+# inter MB phase stamps (tools/stamps_interw.py)
+STW_LIB := build/dbg/libm2dec_amd_stampw.so
+$(STW_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -DM2DEC_STAMPW -DM2DEC_NO_STAMPI -c $(HIP_SRC) -o build/dbg/recon_hip_stampw.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stampw.o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
+
+stampw: $(STW_LIB)

@@ -74,6 +74,12 @@ __device__ unsigned long long g_pstamps[256][4];
 #else
 #define STAMPI(row, role, idx, val) do { } while (0)
 #endif
+/* inter MB phase stamps (-DM2DEC_STAMPW): rows 72..87 = workgroup & 15, role = wave, idx = (MB count * 8 + event) */
+#if defined(M2DEC_STAMPS) && defined(M2DEC_STAMPW)
+#define STAMPW(cnt, ev) do { if ((threadIdx.x & 63) == 0) g_stamps[72 + (blockIdx.x & 15)][threadIdx.x >> 6][((cnt) * 8 + (ev)) & 255] = (__builtin_amdgcn_s_memrealtime() << 16) | (unsigned long long)(ev); } while (0)
+#else
+#define STAMPW(cnt, ev) do { } while (0)
+#endif
 /* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
 #define STAMPX(x, k) do { if ((x) < 16 && part == 0) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
@@ -121,6 +127,46 @@ __device__ int luma_mc(const RefPlane &r, int x, int y, int fx, int fy)
 		if (c == 10) return j;
 		if (fx == 2) o = d_clip255((((fy == 1) ? t2 : t3) + 16) >> 5);         /* f: b, q: s */
 		else o = d_clip255((TAPV(fx == 1 ? 0 : 1) + 16) >> 5);                /* i: h, k: m */
+		return (j + o + 1) >> 1;
+	}
+#undef P
+#undef TAPH
+#undef TAPV
+}
+
+/* the same on a reference window staged in LDS: 9 rows of 12 bytes around one 4x4 block (rows from 2
+ * above the block's integer position, columns from the 4-aligned byte at or left of 2 before it; `off`
+ * = that distance), edge samples already clamped when it was loaded; (cx, ry) = the sample inside the
+ * block */
+__device__ __forceinline__ int luma_mc_win(const uint8_t *w, int off, int cx, int ry, int fx, int fy)
+{
+#define P(dx, dy) ((int)w[(ry + 2 + (dy)) * 12 + off + 2 + cx + (dx)])
+#define TAPH(dy) (P(-2, dy) - 5 * P(-1, dy) + 20 * P(0, dy) + 20 * P(1, dy) - 5 * P(2, dy) + P(3, dy))
+#define TAPV(dx) (P(dx, -2) - 5 * P(dx, -1) + 20 * P(dx, 0) + 20 * P(dx, 1) - 5 * P(dx, 2) + P(dx, 3))
+	const int c = fy * 4 + fx;
+	if (c == 0) return P(0, 0);
+	if (fy == 0) {
+		const int b = d_clip255((TAPH(0) + 16) >> 5);
+		if (fx == 2) return b;
+		return (b + P(fx == 1 ? 0 : 1, 0) + 1) >> 1;
+	}
+	if (fx == 0) {
+		const int h = d_clip255((TAPV(0) + 16) >> 5);
+		if (fy == 2) return h;
+		return (h + P(0, fy == 1 ? 0 : 1) + 1) >> 1;
+	}
+	if (fx != 2 && fy != 2) {
+		const int bh = d_clip255((TAPH(fy == 1 ? 0 : 1) + 16) >> 5);
+		const int vv = d_clip255((TAPV(fx == 1 ? 0 : 1) + 16) >> 5);
+		return (bh + vv + 1) >> 1;
+	}
+	{
+		const int t0 = TAPH(-2), t1 = TAPH(-1), t2 = TAPH(0), t3 = TAPH(1), t4 = TAPH(2), t5 = TAPH(3);
+		const int j = d_clip255((t0 - 5 * t1 + 20 * t2 + 20 * t3 - 5 * t4 + t5 + 512) >> 10);
+		int o;
+		if (c == 10) return j;
+		if (fx == 2) o = d_clip255((((fy == 1) ? t2 : t3) + 16) >> 5);
+		else o = d_clip255((TAPV(fx == 1 ? 0 : 1) + 16) >> 5);
 		return (j + o + 1) >> 1;
 	}
 #undef P
@@ -252,174 +298,307 @@ __device__ __forceinline__ void signal_progress(int *flag, int value)
 #else
 #define M2DEC_INTER_MB_ATTR
 #endif
-/* one inter macroblock, all 256 lanes of the workgroup (uniform call) */
-__device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t *__restrict__ inters,
-                         const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                         size_t fsz, int W, int H, int Wmb, int slot, uint8_t *tile, uint8_t *seg)
-{
-	__shared__ int s_res[256 + 128];
-	__shared__ int s_cnt[4];
-	const int t = threadIdx.x;
-	const int mbx = addr % Wmb, mby = addr / Wmb;
-	const m2r_inter_t &it = inters[m.inter];
-	const m2r_slice_t *sl = &slices[m.slice];
-	uint8_t *cur = frames + (size_t)slot * fsz;
-	const int CH = H >> 1;
+/* wave-private residual buffers of the inter MBs in flight in a workgroup (one MB per wave) */
+struct InterRes {
+	int r[256 + 128]; /* luma raster 16x16, then Cb / Cr 8x8 */
+	uint32_t win[2][16][9][3]; /* luma reference windows per list and raster 4x4 block (luma_mc_win) */
+	uint32_t cwin[2][16][3][2]; /* chroma windows per list and 2x2 chroma block: 3 rows x 8 bytes */
+};
 
-	/* ---- luma prediction: one sample per thread */
-	const int lx = t & 15, ly = t >> 4;
-	const int lb = (ly >> 2) * 4 + (lx >> 2), lb8 = (ly >> 3) * 2 + (lx >> 3);
-	int predl;
-	{
+/* wave-level step boundary for the inter MB: its lanes talk through LDS only (see WSYNC below) */
+#define ISYNC()                                                  \
+	do {                                                         \
+		asm volatile("" ::: "memory");                           \
+		__builtin_amdgcn_wave_barrier();                         \
+	} while (0)
+
+/* one inter macroblock on ONE wave (lane = 0..63; the call is wave-uniform): luma 4 samples and chroma
+ * 2 samples per lane, the residual in the wave's own LDS buffer, no workgroup barrier — the four waves
+ * of a worker each take a different MB of the item.  `it` is the MB's motion record staged in LDS.
+ * Every global load of the MB (the luma and chroma reference windows, the coefficients) is issued
+ * before the first of them is waited for: one memory round trip per MB.  The samples go to the item's
+ * LDS segment. */
+__device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t &it,
+                         const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
+                         size_t fsz, int W, int H, int Wmb, uint8_t *seg, InterRes *res, const int lane, const int scnt = 0)
+{
+	STAMPW(scnt, 0);
+	const int mbx = addr % Wmb, mby = addr / Wmb;
+	const m2r_slice_t *sl = &slices[m.slice];
+	const int CH = H >> 1;
+	int *const R = res->r;
+	const int lx = lane & 15;
+	const int cx = lane & 7, cy = lane >> 3;
+	const int t8 = (m.flags & M2R_FLAG_T8x8) != 0;
+	const bool coded = __builtin_amdgcn_readfirstlane(m.cbp) != 0;
+
+	/* ---- phase 1: loads.  Luma windows: (list, 4x4 block, row) p = lane + 64 j, 12 bytes each (three
+	 * dwords, or clamped bytes where the span leaves the picture) */
+	uint32_t lw[5][3];
+#pragma unroll
+	for (int j = 0; j < 5; ++j) {
+		const int p = lane + 64 * j;
+		lw[j][0] = lw[j][1] = lw[j][2] = 0;
+		if (p < 288) {
+			const int l = p >= 144, rem = p - 144 * l, b = rem / 9, row = rem - 9 * b;
+			const int s = it.slot[l][(b >> 3) * 2 + ((b & 3) >> 1)];
+			if (s >= 0) {
+				const int X = mbx * 16 + (b & 3) * 4 + (it.mv[l][b][0] >> 2), Y = mby * 16 + (b >> 2) * 4 + (it.mv[l][b][1] >> 2);
+				const int xa = (X - 2) & ~3, y = min(max(Y - 2 + row, 0), H - 1);
+				const uint8_t *src = frames + (size_t)s * fsz + (size_t)y * W;
+				if (xa >= 0 && xa + 12 <= W) {
+					const uint32_t *s32 = (const uint32_t *)(src + xa);
+					lw[j][0] = s32[0];
+					lw[j][1] = s32[1];
+					lw[j][2] = s32[2];
+				} else {
+#pragma unroll
+					for (int k = 0; k < 3; ++k) {
+						uint32_t v = 0;
+#pragma unroll
+						for (int i = 0; i < 4; ++i) v |= (uint32_t)src[min(max(xa + 4 * k + i, 0), W - 1)] << (8 * i);
+						lw[j][k] = v;
+					}
+				}
+			}
+		}
+	}
+	/* chroma windows: (list, 2x2 chroma block, row) p = lane + 64 j < 96: 3 rows of the interleaved
+	 * Cb / Cr bytes of component samples X .. X + 2 (8 bytes from the 4-aligned byte at or left of 2 X) */
+	uint32_t cw[2][2];
+#pragma unroll
+	for (int j = 0; j < 2; ++j) {
+		const int p = lane + 64 * j;
+		cw[j][0] = cw[j][1] = 0;
+		if (p < 96) {
+			const int l = p >= 48, rem = p - 48 * l, b = rem / 3, row = rem - 3 * b;
+			const int s = it.slot[l][(b >> 3) * 2 + ((b & 3) >> 1)];
+			if (s >= 0) {
+				const int X = mbx * 8 + (b & 3) * 2 + (it.mv[l][b][0] >> 3), Y = mby * 8 + (b >> 2) * 2 + (it.mv[l][b][1] >> 3);
+				const int xa = (2 * X) & ~3, y = min(max(Y + row, 0), CH - 1);
+				const uint8_t *src = frames + (size_t)s * fsz + (size_t)W * H + (size_t)y * W;
+				if (xa >= 0 && xa + 8 <= W) {
+					const uint32_t *s32 = (const uint32_t *)(src + xa);
+					cw[j][0] = s32[0];
+					cw[j][1] = s32[1];
+				} else {
+#pragma unroll
+					for (int k = 0; k < 2; ++k) {
+						uint32_t v = 0;
+#pragma unroll
+						for (int i = 0; i < 4; ++i) {
+							const int bx = xa + 4 * k + i;
+							const int pos = min(max(bx >> 1, 0), (W >> 1) - 1); /* clamped component sample */
+							v |= (uint32_t)src[2 * pos + (bx & 1)] << (8 * i);
+						}
+						cw[j][k] = v;
+					}
+				}
+			}
+		}
+	}
+	/* the residual's coefficients (dequantised), luma sample (lx, (lane >> 4) + 4 k), chroma (cx, cy) */
+	int rl[4] = {0, 0, 0, 0}, rc[2] = {0, 0}, lv0[2] = {0, 0};
+	uint64_t nzl[4] = {0, 0, 0, 0};
+	if (coded) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const int ly = (lane >> 4) + 4 * k;
+			const int lb = (ly >> 2) * 4 + (lx >> 2), lb8 = (ly >> 3) * 2 + (lx >> 3);
+			if (t8) {
+				const int bit = 4 * lb8;
+				if (m.nz & (1u << bit)) {
+					const int lv = pool[m.coef + d_luma_off(m, bit) + (ly & 7) * 8 + (lx & 7)];
+					rl[k] = lv * d_scale8(m.qpy, lx & 7, ly & 7);
+					nzl[k] = __ballot(lv != 0);
+				}
+			} else {
+				const int blk = d_rast2blk(lb);
+				if (m.nz & (1u << blk)) rl[k] = pool[m.coef + d_luma_off(m, blk) + (ly & 3) * 4 + (lx & 3)] * d_scale4(m.qpy, lx & 3, ly & 3);
+			}
+		}
+		if (t8) {
+			/* the DC level of this lane's two 8x8 blocks (the DC-only add below) */
+#pragma unroll
+			for (int h = 0; h < 2; ++h) {
+				const int lb8 = h * 2 + (lx >> 3);
+				if (m.nz & (1u << (4 * lb8))) lv0[h] = pool[m.coef + d_luma_off(m, 4 * lb8)];
+			}
+		}
+		const int ccbp = m.cbp >> 4;
+		const int cblk = (cy >> 2) * 2 + (cx >> 2);
+		const int pos = (cy & 3) * 4 + (cx & 3);
+#pragma unroll
+		for (int cc = 0; cc < 2; ++cc) {
+			if (ccbp) {
+				if (pos == 0) {
+					rc[cc] = d_chroma_dc(m, pool + m.coef, cc, cblk);
+				} else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(cc, cblk))) {
+					const int bit = 19 + 4 * cc + cblk;
+					rc[cc] = pool[m.coef + d_chroma_off(m, bit) + pos] * d_scale4(cc ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
+				}
+			}
+		}
+	}
+	/* ---- phase 2: windows and residual into the wave's LDS */
+#pragma unroll
+	for (int j = 0; j < 5; ++j) {
+		const int p = lane + 64 * j;
+		if (p < 288) {
+			const int l = p >= 144, rem = p - 144 * l, b = rem / 9, row = rem - 9 * b;
+			uint32_t *dst = res->win[l][b][row];
+			dst[0] = lw[j][0];
+			dst[1] = lw[j][1];
+			dst[2] = lw[j][2];
+		}
+	}
+#pragma unroll
+	for (int j = 0; j < 2; ++j) {
+		const int p = lane + 64 * j;
+		if (p < 96) {
+			const int l = p >= 48, rem = p - 48 * l, b = rem / 3, row = rem - 3 * b;
+			uint32_t *dst = res->cwin[l][b][row];
+			dst[0] = cw[j][0];
+			dst[1] = cw[j][1];
+		}
+	}
+	if (coded) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) R[((lane >> 4) + 4 * k) * 16 + lx] = rl[k];
+#pragma unroll
+		for (int cc = 0; cc < 2; ++cc) R[256 + cc * 64 + cy * 8 + cx] = rc[cc];
+	}
+	ISYNC();
+	STAMPW(scnt, 1);
+	/* ---- luma prediction: samples lane + 64 k (row (lane >> 4) + 4 k, column lane & 15) */
+	int predl[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const int ly = (lane >> 4) + 4 * k;
+		const int lb = (ly >> 2) * 4 + (lx >> 2), lb8 = (ly >> 3) * 2 + (lx >> 3);
 		int v[2] = {0, 0};
 		int use[2];
 		for (int l = 0; l < 2; ++l) {
-			int s = it.slot[l][lb8];
+			const int s = it.slot[l][lb8];
 			use[l] = s >= 0;
 			if (use[l]) {
-				RefPlane r = {frames + (size_t)s * fsz, W, H};
-				int mx = it.mv[l][lb][0], my = it.mv[l][lb][1];
-				v[l] = luma_mc(r, mbx * 16 + lx + (mx >> 2), mby * 16 + ly + (my >> 2), mx & 3, my & 3);
+				const int mx = it.mv[l][lb][0], my = it.mv[l][lb][1];
+				const int X = mbx * 16 + (lb & 3) * 4 + (mx >> 2);
+				v[l] = luma_mc_win((const uint8_t *)res->win[l][lb], (X - 2) & 3, lx & 3, ly & 3, mx & 3, my & 3);
 			}
 		}
-		predl = combine(sl, it, lb8, 0, use[0], use[1], v[0], v[1]);
+		predl[k] = combine(sl, it, lb8, 0, use[0], use[1], v[0], v[1]);
 	}
-	/* ---- chroma prediction: threads 0..127, one sample each */
-	const int cc = (t >> 6) & 1, cx = t & 7, cy = (t >> 3) & 7;
+	/* ---- chroma prediction: component cc, sample (cx, cy), from the chroma windows (filter_chroma_*) */
 	const int cb = (cy >> 1) * 4 + (cx >> 1), cb8 = (cy >> 2) * 2 + (cx >> 2);
-	int predc = 0;
-	if (t < 128) {
+	int predc[2];
+#pragma unroll
+	for (int cc = 0; cc < 2; ++cc) {
 		int v[2] = {0, 0};
 		int use[2];
 		for (int l = 0; l < 2; ++l) {
-			int s = it.slot[l][cb8];
+			const int s = it.slot[l][cb8];
 			use[l] = s >= 0;
 			if (use[l]) {
-				int mx = it.mv[l][cb][0], my = it.mv[l][cb][1];
-				v[l] = chroma_mc(frames + (size_t)s * fsz + (size_t)W * H, W, CH, cc, mbx * 8 + cx + (mx >> 3), mby * 8 + cy + (my >> 3), mx & 7, my & 7);
+				const int mx = it.mv[l][cb][0], my = it.mv[l][cb][1];
+				const int dx = mx & 7, dy = my & 7;
+				const int X = mbx * 8 + (cb & 3) * 2 + (mx >> 3);
+				/* sample (cx, cy) sits at window row (cy & 1), component column (cx & 1) from X */
+				const uint8_t *w = (const uint8_t *)res->cwin[l][cb][cy & 1];
+				const int o = 2 * X - ((2 * X) & ~3) + 2 * (cx & 1) + cc;
+				const int A = w[o], B = w[o + 2], C = w[o + 8], D = w[o + 10];
+				v[l] = ((8 - dx) * (8 - dy) * A + dx * (8 - dy) * B + (8 - dx) * dy * C + dx * dy * D + 32) >> 6;
 			}
 		}
-		predc = combine(sl, it, cb8, 1 + cc, use[0], use[1], v[0], v[1]);
+		predc[cc] = combine(sl, it, cb8, 1 + cc, use[0], use[1], v[0], v[1]);
 	}
+	STAMPW(scnt, 2);
 
 	/* output: the item's LDS segment buffer (luma rows 0..15, chroma rows 16..23, SEG_ROW bytes each) */
-	uint8_t *dl = seg + ly * SEG_ROW + (mbx & 7) * 16 + lx;
-	uint8_t *dc = seg + (16 + cy) * SEG_ROW + (mbx & 7) * 16 + cx * 2 + cc;
-#ifndef M2DEC_NO_EARLYRET
-	if (__builtin_amdgcn_readfirstlane(m.cbp) == 0) {
-		*dl = (uint8_t)predl;
-		if (t < 128) *dc = (uint8_t)predc;
-		if (tile) {
-			tile[t] = (uint8_t)predl;
-			if (t < 128) tile[256 + cy * 16 + cx * 2 + cc] = (uint8_t)predc;
-		}
+	uint8_t *const dl = seg + (lane >> 4) * SEG_ROW + (mbx & 7) * 16 + lx;
+	uint8_t *const dc = seg + (16 + cy) * SEG_ROW + (mbx & 7) * 16 + cx * 2;
+	if (!coded) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) dl[4 * k * SEG_ROW] = (uint8_t)predl[k];
+		dc[0] = (uint8_t)predc[0];
+		dc[1] = (uint8_t)predc[1];
+		STAMPW(scnt, 6);
 		return; /* uniform: m is the same in every lane */
 	}
-#endif
-
-	/* ---- residual: dequantise into LDS */
-	const int t8 = (m.flags & M2R_FLAG_T8x8) != 0;
-	if (t < 4) s_cnt[t] = 0;
-	__syncthreads();
-	{
-		int r = 0;
-		if (t8) {
-			int bit = 4 * lb8;
-			if (m.nz & (1u << bit)) {
-				int lv = pool[m.coef + d_luma_off(m, bit) + (ly & 7) * 8 + (lx & 7)];
-				r = lv * d_scale8(m.qpy, lx & 7, ly & 7);
-				if (lv) atomicAdd(&s_cnt[lb8], 1);
-			}
-		} else {
-			int blk = d_rast2blk(lb);
-			if (m.nz & (1u << blk)) r = pool[m.coef + d_luma_off(m, blk) + (ly & 3) * 4 + (lx & 3)] * d_scale4(m.qpy, lx & 3, ly & 3);
-		}
-		s_res[t] = r;
-	}
-	if (t < 128) {
-		int ccbp = m.cbp >> 4;
-		int cblk = (cy >> 2) * 2 + (cx >> 2);
-		int pos = (cy & 3) * 4 + (cx & 3);
-		int r = 0;
-		if (ccbp) {
-			if (pos == 0) {
-				r = d_chroma_dc(m, pool + m.coef, cc, cblk);
-			} else if (ccbp == 2 && (m.nz & M2R_NZ_CAC(cc, cblk))) {
-				int bit = 19 + 4 * cc + cblk;
-				r = pool[m.coef + d_chroma_off(m, bit) + pos] * d_scale4(cc ? m.qpc[1] : m.qpc[0], cx & 3, cy & 3);
-			}
-		}
-		s_res[256 + cc * 64 + cy * 8 + cx] = r;
-	}
-	__syncthreads();
-	/* ---- row pass */
+	STAMPW(scnt, 3);
+	/* ---- row pass: 8x8 luma rows on lanes 0..31 beside the chroma rows on 32..63; 4x4: luma rows on all
+	 * lanes, then chroma rows */
 	if (t8) {
-		if (t < 32) {
-			int b8 = t >> 3, row = t & 7;
-			int *p = &s_res[((b8 >> 1) * 8 + row) * 16 + (b8 & 1) * 8];
+		if (lane < 32) {
+			const int b8 = lane >> 3, row = lane & 7;
+			int *p = &R[((b8 >> 1) * 8 + row) * 16 + (b8 & 1) * 8];
 			int v[8];
 			for (int k = 0; k < 8; ++k) v[k] = p[k];
 			d_idct8_1d(v);
 			for (int k = 0; k < 8; ++k) p[k] = v[k];
 		}
-	} else if (t < 64) {
-		int b = t >> 2, row = t & 3;
-		int *p = &s_res[((b >> 2) * 4 + row) * 16 + (b & 3) * 4];
+	} else {
+		const int b = lane >> 2, row = lane & 3;
+		int *p = &R[((b >> 2) * 4 + row) * 16 + (b & 3) * 4];
 		int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
 		d_idct4_1d(a0, a1, a2, a3);
 		p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
 	}
-	if (t >= 128 && t < 160) {
-		int k = t - 128, comp = k >> 4, b = (k >> 2) & 3, row = k & 3;
-		int *p = &s_res[256 + comp * 64 + ((b >> 1) * 4 + row) * 8 + (b & 1) * 4];
+	if (t8 ? lane >= 32 : lane < 32) {
+		const int k = lane & 31, comp = k >> 4, b = (k >> 2) & 3, row = k & 3;
+		int *p = &R[256 + comp * 64 + ((b >> 1) * 4 + row) * 8 + (b & 1) * 4];
 		int a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
 		d_idct4_1d(a0, a1, a2, a3);
 		p[0] = a0; p[1] = a1; p[2] = a2; p[3] = a3;
 	}
-	__syncthreads();
+	ISYNC();
 	/* ---- column pass (+32 >> 6) */
 	if (t8) {
-		if (t < 32) {
-			int b8 = t >> 3, col = t & 7;
-			int *p = &s_res[((b8 >> 1) * 8) * 16 + (b8 & 1) * 8 + col];
+		if (lane < 32) {
+			const int b8 = lane >> 3, col = lane & 7;
+			int *p = &R[((b8 >> 1) * 8) * 16 + (b8 & 1) * 8 + col];
 			int v[8];
 			for (int k = 0; k < 8; ++k) v[k] = p[k * 16];
 			d_idct8_1d(v);
 			for (int k = 0; k < 8; ++k) p[k * 16] = (v[k] + 32) >> 6;
 		}
-	} else if (t < 64) {
-		int b = t >> 2, col = t & 3;
-		int *p = &s_res[((b >> 2) * 4) * 16 + (b & 3) * 4 + col];
+	} else {
+		const int b = lane >> 2, col = lane & 3;
+		int *p = &R[((b >> 2) * 4) * 16 + (b & 3) * 4 + col];
 		int a0 = p[0], a1 = p[16], a2 = p[32], a3 = p[48];
 		d_idct4_1d(a0, a1, a2, a3);
 		p[0] = (a0 + 32) >> 6; p[16] = (a1 + 32) >> 6; p[32] = (a2 + 32) >> 6; p[48] = (a3 + 32) >> 6;
 	}
-	if (t >= 128 && t < 160) {
-		int k = t - 128, comp = k >> 4, b = (k >> 2) & 3, col = k & 3;
-		int *p = &s_res[256 + comp * 64 + ((b >> 1) * 4) * 8 + (b & 1) * 4 + col];
+	if (t8 ? lane >= 32 : lane < 32) {
+		const int k = lane & 31, comp = k >> 4, b = (k >> 2) & 3, col = k & 3;
+		int *p = &R[256 + comp * 64 + ((b >> 1) * 4) * 8 + (b & 1) * 4 + col];
 		int a0 = p[0], a1 = p[8], a2 = p[16], a3 = p[24];
 		d_idct4_1d(a0, a1, a2, a3);
 		p[0] = (a0 + 32) >> 6; p[8] = (a1 + 32) >> 6; p[16] = (a2 + 32) >> 6; p[24] = (a3 + 32) >> 6;
 	}
-	__syncthreads();
-	/* ---- add */
-	{
+	ISYNC();
+	STAMPW(scnt, 4);
+	/* ---- add.  8x8 blocks with only their DC level take the reference's DC-only path (d_swar): the
+	 * non-zero levels per 8x8 block from the ballots of the dequantisation (samples k = 0, 1 cover the top
+	 * blocks, 2, 3 the bottom ones; lanes with (lane & 15) < 8 the left ones) */
+	const uint64_t LEFT = 0x00ff00ff00ff00ffull;
+	const int n8[4] = {(int)(__popcll(nzl[0] & LEFT) + __popcll(nzl[1] & LEFT)), (int)(__popcll(nzl[0] & ~LEFT) + __popcll(nzl[1] & ~LEFT)),
+	                   (int)(__popcll(nzl[2] & LEFT) + __popcll(nzl[3] & LEFT)), (int)(__popcll(nzl[2] & ~LEFT) + __popcll(nzl[3] & ~LEFT))};
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const int ly = (lane >> 4) + 4 * k;
+		const int lb8 = (ly >> 3) * 2 + (lx >> 3);
+		const int cnt = (lx >> 3) ? ((k >> 1) ? n8[3] : n8[1]) : ((k >> 1) ? n8[2] : n8[0]);
 		int out;
-		if (t8 && s_cnt[lb8] == 1 && (m.nz & (1u << (4 * lb8)))) {
-			int lv0 = pool[m.coef + d_luma_off(m, 4 * lb8)];
-			if (lv0 != 0) out = d_swar(predl, lv0 * d_scale8(m.qpy, 0, 0), lx & 7, 8);
-			else out = d_clip255(predl + s_res[t]);
-		} else {
-			out = d_clip255(predl + s_res[t]);
-		}
-		*dl = (uint8_t)out;
-		if (tile) tile[t] = (uint8_t)out;
+		if (t8 && cnt == 1 && (m.nz & (1u << (4 * lb8))) && lv0[k >> 1] != 0)
+			out = d_swar(predl[k], lv0[k >> 1] * d_scale8(m.qpy, 0, 0), lx & 7, 8);
+		else
+			out = d_clip255(predl[k] + R[ly * 16 + lx]);
+		dl[4 * k * SEG_ROW] = (uint8_t)out;
 	}
-	if (t < 128) {
-		const uint8_t v = (uint8_t)d_clip255(predc + s_res[256 + cc * 64 + cy * 8 + cx]);
-		*dc = v;
-		if (tile) tile[256 + cy * 16 + cx * 2 + cc] = v;
-	}
+#pragma unroll
+	for (int cc = 0; cc < 2; ++cc) dc[cc] = (uint8_t)d_clip255(predc[cc] + R[256 + cc * 64 + cy * 8 + cx]);
+	STAMPW(scnt, 5);
 }
 
 /* ======================================================================== intra prediction (per sample) */
@@ -1110,19 +1289,20 @@ __device__ __forceinline__ bool nb_needed(const m2r_mb_t *__restrict__ mbs, int 
 	return r;
 }
 
-/* the neighbour record of MB (x, y) from its LDS output tile (luma [r * 16 + c], chroma [256 + r * 16 +
- * 2 c + comp]): lanes 0..7, one 8-byte write-through store each */
-__device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int y, const uint8_t *tile, int t)
+/* the neighbour record of MB (x, y) from the item's LDS segment (luma rows 0..15, interleaved chroma rows
+ * 16..23, the MB at column (x & 7) * 16): lanes 0..7, one 8-byte write-through store each */
+__device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int y, const uint8_t *seg, int t)
 {
 	if (t < 8) {
+		const uint8_t *mb = seg + (x & 7) * 16;
 		unsigned long long v = 0;
 #pragma unroll
 		for (int i = 0; i < 8; ++i) {
 			int b;
-			if (t < 2) b = tile[15 * 16 + 8 * t + i];                                      /* luma bottom row */
-			else if (t < 4) b = tile[256 + 7 * 16 + 8 * (t - 2) + i];                      /* chroma bottom row */
-			else if (t < 6) b = tile[(8 * (t - 4) + i) * 16 + 15];                         /* luma right column */
-			else b = tile[256 + (4 * (t - 6) + (i >> 1)) * 16 + 14 + (i & 1)];            /* chroma right column */
+			if (t < 2) b = mb[15 * SEG_ROW + 8 * t + i];                                   /* luma bottom row */
+			else if (t < 4) b = mb[23 * SEG_ROW + 8 * (t - 2) + i];                        /* chroma bottom row */
+			else if (t < 6) b = mb[(8 * (t - 4) + i) * SEG_ROW + 15];                      /* luma right column */
+			else b = mb[(16 + 4 * (t - 6) + (i >> 1)) * SEG_ROW + 14 + (i & 1)];           /* chroma right column */
 			v |= (unsigned long long)b << (8 * i);
 		}
 		st_sc1(hbp + ((size_t)y * rs + x) * HBP_BYTES + t * 8, v);
@@ -1132,22 +1312,21 @@ __device__ __forceinline__ void write_nb_record(uint8_t *hbp, int rs, int x, int
 /*
  * One intra / PCM MB of a P / B picture, inside an inter worker (all 256 lanes call): the unfiltered
  * neighbours come from the neighbour records of the MBs around it (sc1 loads; their work items are
- * done), the MB is reconstructed by intra_mb_body (wave 0 luma, wave 1 chroma) and written to the
- * frame and to `tile`.
+ * done), the MB is reconstructed by intra_mb_body (wave 0 luma, wave 1 chroma) into the item's segment.
  */
-/* LDS layout of an inter worker: one intra context, the prediction tables, a 384-byte output tile */
+/* LDS layout of an inter worker: one intra context, the prediction tables, the item's segment, and the
+ * residual buffers of the four inter MBs in flight (one per wave) */
 __device__ __forceinline__ IntraLDS *worker_ictx(lds_u8 *lds) { return lds_ptr<IntraLDS>(lds); }
 __device__ __forceinline__ IntraTables *worker_tabs(lds_u8 *lds) { return (IntraTables *)(worker_ictx(lds) + 1); }
-__device__ __forceinline__ uint8_t *worker_tile(lds_u8 *lds) { return (uint8_t *)(worker_tabs(lds) + 1); }
 /* the item's reconstructed samples before they go out: 24 rows (16 luma, 8 interleaved chroma) of 8 MBs */
-__device__ __forceinline__ uint8_t *worker_seg(lds_u8 *lds) { return worker_tile(lds) + 384; }
+__device__ __forceinline__ uint8_t *worker_seg(lds_u8 *lds) { return (uint8_t *)(worker_tabs(lds) + 1); }
+__device__ __forceinline__ InterRes *worker_res(lds_u8 *lds, int wave) { return (InterRes *)(worker_seg(lds) + 24 * SEG_ROW) + wave; }
 
 __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, const m2r_mb_t m, const int16_t *__restrict__ pool, uint8_t *cur,
                             int W, int H, int Wmb, const uint8_t *hbp, int rs, lds_u8 *lds)
 {
 	IntraLDS *const ctx = worker_ictx(lds);
 	const IntraTables *const tabs = worker_tabs(lds);
-	uint8_t *const tile = worker_tile(lds);
 	uint8_t *const seg = worker_seg(lds);
 	const int t = threadIdx.x;
 	const int nq = d_mb_ncoef(m);
@@ -1184,15 +1363,11 @@ __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, 
 	if (w < 2) intra_mb_body(m, ctx->Q[0], t & 63, w == 0, w == 1, ctx, tabs);
 	__syncthreads();
 	{
-		const uint8_t v = ctx->L[1 + (t >> 4)][1 + (t & 15)];
-		tile[t] = v;
-		seg[(t >> 4) * SEG_ROW + (x & 7) * 16 + (t & 15)] = v;
+		seg[(t >> 4) * SEG_ROW + (x & 7) * 16 + (t & 15)] = ctx->L[1 + (t >> 4)][1 + (t & 15)];
 	}
 	if (t < 128) {
 		const int cy = t >> 4, bx = t & 15;
-		const uint8_t v = ctx->C[bx & 1][1 + cy][1 + (bx >> 1)];
-		tile[256 + t] = v;
-		seg[(16 + cy) * SEG_ROW + (x & 7) * 16 + bx] = v;
+		seg[(16 + cy) * SEG_ROW + (x & 7) * 16 + bx] = ctx->C[bx & 1][1 + cy][1 + (bx >> 1)];
 	}
 }
 
@@ -1214,6 +1389,9 @@ __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, 
 __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *smem)
 {
 	__shared__ int s_item, s_rmin, s_rmax, s_cmax, s_intra, s_rec;
+	/* the item's MB records and the motion records of its inter MBs, staged once per item */
+	__shared__ uint32_t s_mbw[8][sizeof(m2r_mb_t) / 4];
+	__shared__ uint32_t s_itw[8][sizeof(m2r_inter_t) / 4];
 	__shared__ unsigned int s_refs[2];
 	const int t = threadIdx.x;
 	const int W = a.W, H = a.H, Wmb = a.Wmb, Hmb = a.Hmb;
@@ -1221,9 +1399,8 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 	int *queue = a.scratch + SCR_QUEUE(Hmb), *inter_cnt = a.scratch + SCR_INTER(Hmb), *segdone = a.scratch + SCR_SEG(Hmb);
 	const m2r_mb_t *__restrict__ mbs = a.mbs;
 	uint8_t *cur = a.frames + (size_t)a.slot * a.fsz;
-	/* intra MBs of this picture: an LDS context, the prediction tables and an output tile */
+	/* intra MBs of this picture: an LDS context and the prediction tables */
 	IntraTables *tabs = worker_tabs(LDS_ARG());
-	uint8_t *tile = worker_tile(LDS_ARG());
 	const bool recs = a.n_intra != 0;
 	if (recs) {
 		for (int i = t; i < 2 * 9 * 16; i += blockDim.x) (&tabs->p4o[0][0][0])[i] = (&c_ipred4o[0][0][0])[i];
@@ -1234,7 +1411,7 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 	 * compiler thread lanes 1..63 of wave 0 straight back to the next barrier while lane 0 is still
 	 * dequeueing, which deadlocks the workgroup (seen on gfx950 with ROCm 7.2). */
 	const bool wave0 = __builtin_amdgcn_readfirstlane(t) < 64;
-	int nst_dbg = 0;
+	int nst_dbg = 0, nmb_dbg = 0;
 	for (;;) {
 		if (wave0) {
 			const int v = __hip_atomic_fetch_add((gi32 *)queue, t == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1251,6 +1428,18 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 		if (item >= nitems) break;
 		const int y = item / nseg, seg = item % nseg, x0 = seg * 8, x1 = min(x0 + 8, Wmb);
 		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
+		/* ---- the item's records into LDS: MB records, then the motion records they point at */
+		if (t < 8 * (int)(sizeof(m2r_mb_t) / 4)) {
+			const int mb = t / (sizeof(m2r_mb_t) / 4), wd = t % (sizeof(m2r_mb_t) / 4);
+			if (x0 + mb < x1) s_mbw[mb][wd] = ((const uint32_t *)&mbs[y * Wmb + x0 + mb])[wd];
+		}
+		__syncthreads();
+		for (int k = t; k < 8 * (int)(sizeof(m2r_inter_t) / 4); k += blockDim.x) {
+			const int mb = k / (sizeof(m2r_inter_t) / 4), wd = k % (sizeof(m2r_inter_t) / 4);
+			const m2r_mb_t &mm = *(const m2r_mb_t *)s_mbw[mb];
+			if (x0 + mb < x1 && mm.kind == M2R_MB_INTER) s_itw[mb][wd] = ((const uint32_t *)&a.inters[mm.inter])[wd];
+		}
+		__syncthreads();
 		/* ---- vertical and rightward reach of this segment's motion into the references (8 lanes per MB;
 		 * luma 6-tap window; the chroma window never reaches further), and its intra MBs */
 		if (t < 64) {
@@ -1258,9 +1447,9 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 			int rmin = 1 << 30, rmax = -1, cmax = 0;
 			unsigned int r0 = 0, r1 = 0;
 			if (mbi < x1) {
-				const m2r_mb_t m = mbs[y * Wmb + mbi];
+				const m2r_mb_t &m = *(const m2r_mb_t *)s_mbw[mbi - x0];
 				if (m.kind == M2R_MB_INTER) {
-					const m2r_inter_t &it = a.inters[m.inter];
+					const m2r_inter_t &it = *(const m2r_inter_t *)s_itw[mbi - x0];
 					for (int k = (t & 7) * 4; k < (t & 7) * 4 + 4; ++k) {
 						const int l = k >> 4, blk = k & 15;
 						const int sl = it.slot[l][(blk >> 3) * 2 + ((blk & 3) >> 1)];
@@ -1353,18 +1542,31 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the record loads below the poll */
 			}
 			if (pass == 1) __syncthreads();
+			if (pass == 0) {
+				/* the inter MBs, one per wave: wave w takes x0 + w, x0 + w + 4 (no workgroup barrier per MB) */
+				const int w = __builtin_amdgcn_readfirstlane(t) >> 6;
+				for (int x = x0 + w; x < x1; x += 4) {
+					const m2r_mb_t m = *(const m2r_mb_t *)s_mbw[x - x0];
+					if (__builtin_amdgcn_readfirstlane(m.kind) != M2R_MB_INTER) continue;
+					inter_mb(y * Wmb + x, m, *(const m2r_inter_t *)s_itw[x - x0], a.slices, a.pool, a.frames, a.fsz, W, H, Wmb,
+					         worker_seg(LDS_ARG()), worker_res(LDS_ARG(), w), t & 63, nmb_dbg++);
+					if ((rec_bits >> (x - x0)) & 1) {
+						ISYNC();
+						write_nb_record(a.hbp, rs, x, y, worker_seg(LDS_ARG()), t & 63);
+					}
+				}
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the records are out before the barrier */
+				__syncthreads();
+				STAMPI(96 + (blockIdx.x & 63), 3, nst_dbg & 255, item);
+				continue;
+			}
 			for (int x = x0; x < x1; ++x) {
 				const m2r_mb_t m = mbs[y * Wmb + x];
-				const bool inter = __builtin_amdgcn_readfirstlane(m.kind) == M2R_MB_INTER;
-				if (inter != (pass == 0)) continue;
-				const bool rec = (rec_bits >> (x - x0)) & 1;
-				if (inter)
-					inter_mb(y * Wmb + x, m, a.inters, a.slices, a.pool, a.frames, a.fsz, W, H, Wmb, a.slot, rec ? tile : nullptr, worker_seg(LDS_ARG()));
-				else
-					intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, LDS_ARG());
-				if (rec) {
+				if (__builtin_amdgcn_readfirstlane(m.kind) == M2R_MB_INTER) continue;
+				intra_mb_wg(x, y, m, a.pool, cur, W, H, Wmb, a.hbp, rs, LDS_ARG());
+				if ((rec_bits >> (x - x0)) & 1) {
 					__syncthreads();
-					write_nb_record(a.hbp, rs, x, y, tile, t);
+					write_nb_record(a.hbp, rs, x, y, worker_seg(LDS_ARG()), t);
 					asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 				}
 				__syncthreads();
@@ -1978,7 +2180,7 @@ size_t m2r_deblock_lds_bytes(int W, int Wmb)
 	(void)W;
 	const size_t dbk = (size_t)54 * DBK_RW + 3 * (size_t)Wmb * sizeof(m2r_deblock_t) + 16 + 64;
 	const size_t intra = 4 * sizeof(IntraLDS) + sizeof(IntraTables);
-	const size_t worker = sizeof(IntraLDS) + sizeof(IntraTables) + 384 + 24 * SEG_ROW;
+	const size_t worker = sizeof(IntraLDS) + sizeof(IntraTables) + 24 * SEG_ROW + 4 * sizeof(InterRes);
 	return std::max(dbk, std::max(intra, worker));
 }
 

@@ -139,6 +139,38 @@ static inline int eng_bypass(h264_cabac_eng_t *e)
 	return ret;
 }
 
+/* k <= 16 bypass bins at once, MSB first: k steps of the bypass compare-subtract are one long division
+ * of value by range << (bits - k) (value < range << bits bounds the quotient by 2^k) */
+static inline uint32_t eng_bypass_bits(h264_cabac_eng_t *e, int k)
+{
+	e->bits -= k;
+	{
+		const uint64_t scaled = (uint64_t)e->range << e->bits;
+		const uint64_t q = e->value / scaled;
+		e->value -= q * scaled;
+		eng_refill(e);
+		return (uint32_t)q;
+	}
+}
+
+/* a unary run of bypass 1s ended by a 0 (Exp-Golomb prefix), at most 16 bins: the number of 1s, the 0
+ * consumed; -1 (nothing consumed) if no 0 within 16 bins */
+static inline int eng_bypass_ones(h264_cabac_eng_t *e)
+{
+	const uint64_t scaled = (uint64_t)e->range << (e->bits - 16);
+	const uint32_t q = (uint32_t)(e->value / scaled); /* the next 16 bins, not consumed yet */
+	const int ones = __builtin_clz(~(q << 16) | 1u);  /* leading 1s of the 16-bit window */
+	if (ones >= 16) return -1;
+	{
+		/* consume ones + 1 bins: the quotient's top (ones + 1) bits */
+		const int n = ones + 1;
+		e->bits -= n;
+		e->value -= (uint64_t)(q >> (16 - n)) * ((uint64_t)e->range << e->bits);
+		eng_refill(e);
+	}
+	return ones;
+}
+
 static inline int cabac_decision(h264_cabac_t *c, int ctxidx)
 {
 	return eng_decision(&c->e, c->ctx, ctxidx);
@@ -889,13 +921,21 @@ static int cabac_mvd(h264_cabac_t *c, int base, int sum)
 		if (mvd < 4) ci++;
 		mvd++;
 		if (mvd >= 9) {
+			/* UEG3 suffix: unary prefix of bypass 1s, then k fixed bits, in batches (9.3.2.3) */
 			int k = 3;
-			while (eng_bypass(&e)) {
-				mvd += 1 << k;
-				k++;
-				if (k > 24) break;
+			const int ones = eng_bypass_ones(&e);
+			if (ones >= 0 && ones <= 13) {
+				mvd += ((1 << ones) - 1) << 3; /* sum of 1 << (3 + i), i < ones */
+				k = 3 + ones;
+				mvd += (int)eng_bypass_bits(&e, k);
+			} else {
+				while (eng_bypass(&e)) {
+					mvd += 1 << k;
+					k++;
+					if (k > 24) break;
+				}
+				while (k-- > 0) mvd += eng_bypass(&e) << k;
 			}
-			while (k-- > 0) mvd += eng_bypass(&e) << k;
 			break;
 		}
 	}

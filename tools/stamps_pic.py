@@ -32,6 +32,7 @@ ends = [t[y, 3, 4] for y in range(Hmb) if t[y, 3, 4] > 0]
 print("picture span us", us(max(ends)))
 # inter workers: rows 96..159, role 0 = dequeued item, 1 = after ref wait, 2 = segment done
 wait_tot, work_tot, items = 0.0, 0.0, 0
+p0_tot, n_p0 = 0.0, 0
 first = []
 for w in range(64):
     r = 96 + w
@@ -41,9 +42,14 @@ for w in range(64):
         items += 1
         wait_tot += (t[r, 1, i] - t[r, 0, i]) / 100.0
         work_tot += (t[r, 2, i] - t[r, 1, i]) / 100.0
+        if t[r, 3, i] > 0:
+            p0_tot += (t[r, 3, i] - t[r, 1, i]) / 100.0
+            n_p0 += 1
         first.append((us(t[r, 0, i]), int(v[r, 0, i]), round((t[r, 1, i] - t[r, 0, i]) / 100.0, 1), round((t[r, 2, i] - t[r, 1, i]) / 100.0, 1)))
 if items:
     print(f"inter items {items}: ref-wait {wait_tot / items:.1f} us/item, work {work_tot / items:.1f} us/item (8 MBs)")
+    if n_p0:
+        print(f"  of which inter MBs (pass 0, 4 waves): {p0_tot / n_p0:.1f} us/item")
     first.sort()
     print("first items (t, item, wait, work):", first[:8])
     print("last items:", first[-5:])

@@ -84,7 +84,9 @@ typedef struct m2r_slice {
 
 /* Deblocking input of one macroblock, 16 bytes. */
 typedef struct m2r_deblock {
-	uint32_t bs_v;        /* vertical edges x = 0,4,8,12: byte e = edge, 2 bits per 4-row segment (LSB = top), bS 0..3 */
+	/* bS 0..3 of the MB's edges, derived by the back end from the MB and motion records (the parser
+	 * writes 0; recon_hip.hip bs_of, oracle/recon_oracle.c orc_bs): */
+	uint32_t bs_v;        /* vertical edges x = 0,4,8,12: byte e = edge, 2 bits per 4-row segment (LSB = top) */
 	uint32_t bs_h;        /* horizontal edges y = 0,4,8,12: byte e = edge, 2 bits per 4-column segment (LSB = left) */
 	int8_t qpy;
 	int8_t qpc[2];

@@ -80,6 +80,14 @@ __device__ unsigned long long g_pstamps[256][4];
 #else
 #define STAMPW(cnt, ev) do { } while (0)
 #endif
+/* deblocking filter sub-step stamps (-DM2DEC_STAMPD): [MB row][event][MB x]: 0 inputs ready, 1 vertical
+ * edges done, 2 horizontal edges done */
+#if defined(M2DEC_STAMPS) && defined(M2DEC_STAMPD)
+__device__ unsigned long long g_dstamps[160][3][128];
+#define STAMPD(row, ev, x) do { if ((threadIdx.x & 63) == 0 && (row) < 160 && (x) < 128) g_dstamps[row][ev][x] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define STAMPD(row, ev, x) do { } while (0)
+#endif
 /* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
 #define STAMPX(x, k) do { if ((x) < 16 && part == 0) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
@@ -1624,9 +1632,75 @@ __device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *s
  */
 __device__ __forceinline__ int dbk_done012(int c, int Wmb) { return c >= Wmb ? Wmb : max(c - 1, 0); }
 
+/* ---- boundary strengths, derived here from the MB and motion records (the host parser leaves
+ * m2r_deblock_t.bs_v / bs_h at 0; bS is ~17 % of its cycles otherwise): store_strength_intra*
+ * (h264.cpp:3086-3106, 4749-4755) for intra MBs; else per 4-sample segment 2 when either 4x4 block has
+ * coefficients, else str_mv_calc* (h264.cpp:7119-7270) on the blocks' reference pictures (record slots,
+ * one per picture) and vectors.  Same derivation as oracle/recon_oracle.c orc_bs. */
+__device__ __forceinline__ int bs_nz(const m2r_mb_t &m, int bx, int by)
+{
+	const int r = by * 4 + bx;
+	const int blk = ((r >> 3) << 3) | (((r >> 1) & 1) << 2) | ((r & 4) >> 1) | (r & 1); /* raster -> blkIdx */
+	return (m.flags & M2R_FLAG_T8x8) ? (int)((m.nz >> (4 * (blk >> 2))) & 1) : (int)((m.nz >> blk) & 1);
+}
+
+__device__ __forceinline__ int bs_far(uint32_t a, uint32_t b)
+{
+	const int dx = (int)(int16_t)(a & 0xffff) - (int)(int16_t)(b & 0xffff);
+	const int dy = (int)(int16_t)(a >> 16) - (int)(int16_t)(b >> 16);
+	return (abs(dx) >= 4) | (abs(dy) >= 4);
+}
+
+__device__ int bs_motion(const m2r_inter_t *q, int qx, int qy, const m2r_inter_t *p, int px, int py)
+{
+	const int bq = (qy >> 1) * 2 + (qx >> 1), bp = (py >> 1) * 2 + (px >> 1);
+	const int q0 = q->slot[0][bq], q1 = q->slot[1][bq], p0 = p->slot[0][bp], p1 = p->slot[1][bp];
+	const uint32_t *qmv = (const uint32_t *)q->mv, *pmv = (const uint32_t *)p->mv;
+	const uint32_t qm0 = qmv[qy * 4 + qx], qm1 = qmv[16 + qy * 4 + qx], pm0 = pmv[py * 4 + px], pm1 = pmv[16 + py * 4 + px];
+	if ((p0 != q0 || p1 != q1) && (p1 != q0 || p0 != q1)) return 1;
+	if (q0 >= 0 && q1 >= 0) {
+		if (q0 == q1) return (bs_far(qm0, pm0) | bs_far(qm1, pm1)) & (bs_far(qm0, pm1) | bs_far(qm1, pm0));
+		return q0 == p0 ? (bs_far(qm0, pm0) | bs_far(qm1, pm1)) : (bs_far(qm0, pm1) | bs_far(qm1, pm0));
+	}
+	if (q0 >= 0) return q0 == p0 ? bs_far(qm0, pm0) : bs_far(qm0, pm1);
+	return q1 == p0 ? bs_far(qm1, pm0) : bs_far(qm1, pm1);
+}
+
+/* bS of MB (x, y), direction dir (0: vertical edges, 1: horizontal): byte e = edge, 2 bits per segment */
+__device__ uint32_t bs_of(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters, int x, int y, int Wmb, int dir)
+{
+	const m2r_mb_t q = mbs[y * Wmb + x];
+	if (q.kind != M2R_MB_INTER) return (q.kind == M2R_MB_PCM || q.kind == M2R_MB_I8x8) ? 0x00ff00ffu : 0xffffffffu;
+	const m2r_inter_t *qi = &inters[q.inter];
+	uint32_t str = 0;
+	if (dir ? y > 0 : x > 0) {
+		const m2r_mb_t p = mbs[dir ? (y - 1) * Wmb + x : y * Wmb + x - 1];
+		if (p.kind != M2R_MB_INTER) {
+			str = 0xaa; /* bS 2 on every segment; the BS4 flag makes it 4 */
+		} else {
+			const m2r_inter_t *pi = &inters[p.inter];
+			for (int g = 0; g < 4; ++g) {
+				const int qx = dir ? g : 0, qy = dir ? 0 : g, px = dir ? g : 3, py = dir ? 3 : g;
+				const int v = (bs_nz(q, qx, qy) | bs_nz(p, px, py)) ? 2 : bs_motion(qi, qx, qy, pi, px, py);
+				str |= (uint32_t)v << (2 * g);
+			}
+		}
+	}
+	for (int e = 1; e < 4; ++e) {
+		if ((q.flags & M2R_FLAG_T8x8) && (e & 1)) continue;
+		for (int g = 0; g < 4; ++g) {
+			const int qx = dir ? g : e, qy = dir ? e : g, px = dir ? qx : qx - 1, py = dir ? qy - 1 : qy;
+			const int v = (bs_nz(q, qx, qy) | bs_nz(q, px, py)) ? 2 : bs_motion(qi, qx, qy, qi, px, py);
+			str |= (uint32_t)v << (8 * e + 2 * g);
+		}
+	}
+	return str;
+}
+
 __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur,
                              int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err,
-                             unsigned long long *rowflag, int seq, const int *segdone)
+                             unsigned long long *rowflag, int seq, const int *segdone,
+                             const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *__restrict__ inters)
 {
 	const int wave = threadIdx.x >> 6, t = threadIdx.x & 63;
 	const int nthr = blockDim.x;
@@ -1659,6 +1733,15 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		if (hasB) rB[k] = dbk[yB * Wmb + k];
 	}
 	if (threadIdx.x < 4) flags[threadIdx.x] = 0;
+	__syncthreads();
+	/* the rows' boundary strengths from the records: one (row, MB, direction) per lane */
+	for (int k = threadIdx.x; k < (hasB ? 4 : 2) * Wmb; k += nthr) {
+		const int r = k / (2 * Wmb), rem = k - r * 2 * Wmb, x = rem >> 1, dir = rem & 1;
+		const uint32_t v = bs_of(mbs, inters, x, yA + r, Wmb, dir);
+		m2r_deblock_t *rec = (r ? rB : rA) + x;
+		if (dir) rec->bs_h = v;
+		else rec->bs_v = v;
+	}
 	__syncthreads();
 
 	/* the deblocking chain is the picture's critical path: let its waves win the SIMD arbitration
@@ -1792,6 +1875,7 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 					if (!spin_ok(spins, err, 16)) break;
 				}
 			STAMP(yA + rowB, 1, x, x);
+			STAMPD(yA + rowB, 0, x);
 			const m2r_deblock_t q = rq[x];
 			if (!(q.flags & M2R_DBK_OFF)) {
 				const m2r_deblock_t pl = x > 0 ? rq[x - 1] : q, pt = rt[x];
@@ -1890,6 +1974,7 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 					/* the next direction's reads are this wave's later LDS operations: performed in order */
 					asm volatile("" ::: "memory");
 					__builtin_amdgcn_wave_barrier();
+					STAMPD(yA + rowB, 1 + dir, x);
 				}
 			}
 			if (t == 0) __hip_atomic_store(done, x + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2086,7 +2171,7 @@ __device__ __attribute__((noinline)) void row_pair(const PictureArgs *__restrict
 	STAMP(yA, 3, 3, 4);
 	/* ---- phase B: deblocking (always: it also publishes the row flags) */
 	deblock_pair(yA, hasB, smem, a.dbk, cur, a.W, a.H, Wmb, a.Hmb, a.hbd, a.scratch + SCR_DPROG(a.Hmb), a.err, a.rowflag, a.seq,
-	             a.n_inter ? a.scratch + SCR_SEG(a.Hmb) : nullptr);
+	             a.n_inter ? a.scratch + SCR_SEG(a.Hmb) : nullptr, a.mbs, a.inters);
 	STAMP(yA, 3, 4, 5);
 	if (a.fin) {
 		/* the storer drained and released every frame store before its row flags */
@@ -2204,6 +2289,19 @@ extern "C" int m2dec_amd_debug_pstamps(unsigned long long *out, size_t n)
 	if (n < 256 * 4) return -1;
 	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 256 * 4, 0, hipMemcpyDeviceToHost));
 	return 256 * 4;
+#else
+	(void)out;
+	(void)n;
+	return -1;
+#endif
+}
+
+extern "C" int m2dec_amd_debug_dstamps(unsigned long long *out, size_t n)
+{
+#if defined(M2DEC_STAMPS) && defined(M2DEC_STAMPD)
+	if (n < 160 * 3 * 128) return -1;
+	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dstamps), sizeof(unsigned long long) * 160 * 3 * 128, 0, hipMemcpyDeviceToHost));
+	return 160 * 3 * 128;
 #else
 	(void)out;
 	(void)n;

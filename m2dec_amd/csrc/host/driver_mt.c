@@ -12,6 +12,7 @@
  * Decoder contexts are independent (all state in the context, const global tables), as in the
  * reference (h264.h:435-446), so the threads share nothing but the device.
  */
+#define _GNU_SOURCE /* pthread_setname_np */
 #include <pthread.h>
 #include <stdlib.h>
 #include <stdio.h>
@@ -76,6 +77,7 @@ static double now_s(void)
 /* a free thread takes every queued frame (up to MD5_BATCH) and hashes them side by side */
 static void *md5_worker(void *arg)
 {
+	pthread_setname_np(pthread_self(), "m2d-md5");
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	pthread_mutex_lock(&p->mu);
 	for (;;) {
@@ -264,6 +266,7 @@ typedef struct {
 
 static void *stream_worker(void *arg)
 {
+	pthread_setname_np(pthread_self(), "m2d-stream");
 	stream_job_t *j = (stream_job_t *)arg;
 	/* parse-ahead workers a stream may occupy in the shared pool (M2DEC_AMD_STREAM_PARSE_THREADS) */
 	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS");

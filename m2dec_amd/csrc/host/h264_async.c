@@ -56,6 +56,7 @@
  * picture of its virtual id is not bound yet, or when an SPS the API context has not run the header
  * callback for lies before it.
  */
+#define _GNU_SOURCE /* pthread_setname_np */
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -518,6 +519,7 @@ static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *s
  * served round robin.  A finished job may let its pipeline submit: the worker drives it. */
 static void *pool_worker(void *arg)
 {
+	pthread_setname_np(pthread_self(), "m2d-parse");
 	(void)arg;
 	pthread_mutex_lock(&g_parse.mu);
 	for (;;) {

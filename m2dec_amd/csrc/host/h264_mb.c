@@ -125,18 +125,24 @@ static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
 	return (int)((s & 1) ^ is_lps);
 }
 
+/* branch-free: bypass bins (signs, suffixes) are coin flips to a branch predictor */
 static inline int eng_bypass(h264_cabac_eng_t *e)
 {
-	uint64_t scaled;
-	int ret = 0;
 	e->bits -= 1;
-	scaled = (uint64_t)e->range << e->bits;
-	if (e->value >= scaled) {
-		e->value -= scaled;
-		ret = 1;
+	{
+		const uint64_t scaled = (uint64_t)e->range << e->bits;
+		const uint64_t ge = e->value >= scaled;
+		e->value -= scaled & ((uint64_t)0 - ge);
+		eng_refill(e); /* keeps the invariant value < range << bits */
+		return (int)ge;
 	}
-	eng_refill(e); /* keeps the invariant value < range << bits */
-	return ret;
+}
+
+/* v negated when the next bypass bin (a sign) is 1, without a branch */
+static inline int eng_bypass_sign(h264_cabac_eng_t *e, int v)
+{
+	const int s = eng_bypass(e);
+	return (v ^ -s) + s;
 }
 
 /* k <= 16 bypass bins at once, MSB first: k steps of the bypass compare-subtract are one long division
@@ -380,18 +386,24 @@ done:
 			lvl = 2;
 			while (lvl < 15 && eng_decision(&e, ctx, ctx2)) lvl++;
 			if (lvl == 15) {
-				/* UEG0 suffix (9.3.2.3) */
+				/* UEG0 suffix (9.3.2.3): unary prefix and k fixed bits in batches */
 				int k2 = 0;
-				while (eng_bypass(&e)) {
-					lvl += 1 << k2;
-					k2++;
-					if (k2 > 24) break;
+				const int ones = eng_bypass_ones(&e);
+				if (ones >= 0) {
+					lvl += (1 << ones) - 1;
+					if (ones) lvl += (int)eng_bypass_bits(&e, ones);
+				} else {
+					while (eng_bypass(&e)) {
+						lvl += 1 << k2;
+						k2++;
+						if (k2 > 24) break;
+					}
+					while (k2-- > 0) lvl += eng_bypass(&e) << k2;
 				}
-				while (k2-- > 0) lvl += eng_bypass(&e) << k2;
 			}
 			gt1++;
 		}
-		if (eng_bypass(&e)) lvl = -lvl;
+		lvl = eng_bypass_sign(&e, lvl);
 		{
 			int pos = map[k] + first;
 			out[scan ? scan[pos] : pos] = (int16_t)lvl;
@@ -939,7 +951,7 @@ static int cabac_mvd(h264_cabac_t *c, int base, int sum)
 			break;
 		}
 	}
-	if (eng_bypass(&e)) mvd = -mvd;
+	mvd = eng_bypass_sign(&e, mvd);
 	c->e = e;
 	return mvd;
 }
@@ -1137,131 +1149,30 @@ static int residual_chroma(slice_ctx_t *s, int cbp, uint32_t *nz)
 }
 
 /* ================================================================== deblocking strengths */
-/* frame identity of the reference of 4x4 block (bx,by) of m in list lx, -1 unused */
-static inline int blk_fidx(const h264_mbinfo_t *m, int lx, int bx, int by)
-{
-	return m->fidx[lx][(by >> 1) * 2 + (bx >> 1)];
-}
-
-static inline int mv_far(const int16_t *a, const int16_t *b)
-{
-	return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4;
-}
-
-/* bS 1 test between two inter 4x4 blocks (str_mv_calc*, h264.cpp:7119-7270) */
-static int bs_motion(const h264_mbinfo_t *q, int qx, int qy, const h264_mbinfo_t *p, int px, int py)
-{
-	int q0 = blk_fidx(q, 0, qx, qy), q1 = blk_fidx(q, 1, qx, qy);
-	int p0 = blk_fidx(p, 0, px, py), p1 = blk_fidx(p, 1, px, py);
-	const int16_t *qm0 = q->mv[0][qy * 4 + qx], *qm1 = q->mv[1][qy * 4 + qx];
-	const int16_t *pm0 = p->mv[0][py * 4 + px], *pm1 = p->mv[1][py * 4 + px];
-	if (((p0 != q0) || (p1 != q1)) && ((p1 != q0) || (p0 != q1))) return 1;
-	if (q0 >= 0 && q1 >= 0) {
-		if (q0 == q1) {
-			return (mv_far(qm0, pm0) || mv_far(qm1, pm1)) && (mv_far(qm0, pm1) || mv_far(qm1, pm0));
-		}
-		if (q0 == p0) return mv_far(qm0, pm0) || mv_far(qm1, pm1);
-		return mv_far(qm0, pm1) || mv_far(qm1, pm0);
-	}
-	if (q0 >= 0) return (q0 == p0) ? mv_far(qm0, pm0) : mv_far(qm0, pm1);
-	return (q1 == p0) ? mv_far(qm1, pm0) : mv_far(qm1, pm1);
-}
-
 static inline int is_intra_type(int t) { return t >= 0 && t <= MBT_IPCM; }
 
-/* one motion for the whole MB (both lists): every inner-edge bS-1 test is then 0 */
-static int uniform_motion(const h264_mbinfo_t *q)
-{
-	uint32_t w[2][16];
-	memcpy(w, q->mv, sizeof(w));
-	for (int lx = 0; lx < 2; ++lx) {
-		if (q->fidx[lx][1] != q->fidx[lx][0] || q->fidx[lx][2] != q->fidx[lx][0] || q->fidx[lx][3] != q->fidx[lx][0])
-			return 0;
-		for (int i = 1; i < 16; ++i)
-			if (w[lx][i] != w[lx][0]) return 0;
-	}
-	return 1;
-}
-
-/* luma blocks with coefficients, raster bit y * 4 + x */
-static inline uint32_t nz_raster(const h264_mbinfo_t *m)
-{
-	uint32_t r = 0;
-	for (int b = 0; b < 16; ++b) r |= (uint32_t)(m->nnz[b] != 0) << (blk_y[b] * 4 + blk_x[b]);
-	return r;
-}
-
-static inline int b8_of(int r) { return ((r >> 3) << 1) | ((r & 3) >> 1); }
-
-/* boundary strengths of the current MB's edges (bs_v / bs_h / the BS4 flags of its deblock record) */
+/* the BS4 flags of the current MB's deblock record: bS 4 on an MB edge with an intra MB on either side
+ * (store_strength_intra*, h264.cpp:3086-3106, 4749-4755).  The strengths themselves (bs_v / bs_h) are
+ * derived by the back end from the MB and motion records (recon_hip.hip bs_of, the oracle's orc_bs):
+ * the parser leaves them 0. */
 static void bs_strength(slice_ctx_t *s)
 {
 	h264_mbinfo_t *q = s->cur;
 	m2r_deblock_t *db = s->dbk;
-	uint32_t bv = 0, bh = 0;
 	uint8_t flags = 0;
 	if (is_intra_type(q->type)) {
-		/* store_strength_intra / _intra8x8 / mb_intrapcm (h264.cpp:3086-3106, 4749-4755) */
-		uint32_t v = (q->type == MBT_IPCM || (q->type == MBT_INxN && q->t8x8)) ? 0x00ff00ffu : 0xffffffffu;
-		bv = bh = v;
 		flags = M2R_DBK_LEFT_BS4 | M2R_DBK_TOP_BS4;
 	} else {
-		const int t8 = q->t8x8, uni = uniform_motion(q);
-		const uint32_t nzq = nz_raster(q);
-		uint32_t mvw[2][16];
-		memcpy(mvw, q->mv, sizeof(mvw));
 		for (int dir = 0; dir < 2; ++dir) {
-			uint32_t str = 0;
-			/* MB edge: the left / top neighbour */
 			const h264_mbinfo_t *p = NULL;
 			if (dir == 0 && s->mbx != 0) p = &s->d->mbi[s->addr - 1];
 			if (dir == 1 && s->mby != 0) p = &s->d->mbi[s->addr - s->d->mb_w];
 			if (p && (int)(p - s->d->mbi) < s->d->par_first_mb) p = NULL; /* h264_fix_bs, once that slice is parsed */
-			if (p && is_intra_type(p->type)) {
-				flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
-				str = 0xaa; /* 2 in every segment (the flag makes it 4) */
-			} else if (p) {
-				for (int sgm = 0; sgm < 4; ++sgm) {
-					const int qx = dir ? sgm : 0, qy = dir ? 0 : sgm, px = dir ? qx : 3, py = dir ? 3 : qy;
-					int v;
-					const int qr = qy * 4 + qx, pr = py * 4 + px, bq = b8_of(qr), bp = b8_of(pr);
-					if (((nzq >> qr) & 1) || p->nnz[rast2blk[pr]]) v = 2;
-					else if (q->fidx[0][bq] == p->fidx[0][bp] && q->fidx[1][bq] == p->fidx[1][bp] &&
-					         !memcmp(q->mv[0][qr], p->mv[0][pr], 4) && !memcmp(q->mv[1][qr], p->mv[1][pr], 4))
-						v = 0;
-					else v = bs_motion(q, qx, qy, p, px, py);
-					str |= (uint32_t)v << (sgm * 2);
-				}
-			}
-			/* inner edges: blocks of the same MB; identical motion (the common case inside a partition)
-			 * is bS 0 without the full test */
-			for (int e = 1; e < 4; ++e) {
-				if (t8 && (e & 1)) continue;
-				for (int sgm = 0; sgm < 4; ++sgm) {
-					const int qx = dir ? sgm : e, qy = dir ? e : sgm;
-					const int qr = qy * 4 + qx, pr = dir ? qr - 4 : qr - 1;
-					int v;
-					if (((nzq >> qr) | (nzq >> pr)) & 1) {
-						v = 2;
-					} else if (uni) {
-						v = 0;
-					} else {
-						const int bq = b8_of(qr), bp = b8_of(pr);
-						if (q->fidx[0][bq] == q->fidx[0][bp] && q->fidx[1][bq] == q->fidx[1][bp] && mvw[0][qr] == mvw[0][pr] &&
-						    mvw[1][qr] == mvw[1][pr])
-							v = 0;
-						else
-							v = bs_motion(q, qx, qy, q, dir ? qx : qx - 1, dir ? qy - 1 : qy);
-					}
-					str |= (uint32_t)v << (e * 8 + sgm * 2);
-				}
-			}
-			if (dir == 0) bv = str;
-			else bh = str;
+			if (p && is_intra_type(p->type)) flags |= dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
 		}
 	}
-	db->bs_v = bv;
-	db->bs_h = bh;
+	db->bs_v = 0;
+	db->bs_h = 0;
 	db->flags = flags;
 }
 

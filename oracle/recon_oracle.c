@@ -999,6 +999,70 @@ static void filter_edge(plane_t *f, int mbx, int mby, int dir, int e, uint32_t s
 	}
 }
 
+/* ---- boundary strengths from the MB and motion records (the parser leaves m2r_deblock_t.bs_v / bs_h
+ * to the back end): store_strength_intra* (h264.cpp:3086-3106, 4749-4755) for intra MBs, else per
+ * 4-sample edge segment 2 when either 4x4 block has coefficients, else str_mv_calc* (h264.cpp:7119-7270)
+ * on the blocks' reference pictures (the records' slots: one per picture) and vectors */
+static int orc_nz(const m2r_mb_t *m, int bx, int by)
+{
+	static const uint8_t r2b[16] = {0, 1, 4, 5, 2, 3, 6, 7, 8, 9, 12, 13, 10, 11, 14, 15};
+	const int blk = r2b[by * 4 + bx];
+	return (m->flags & M2R_FLAG_T8x8) ? (int)((m->nz >> (4 * (blk >> 2))) & 1) : (int)((m->nz >> blk) & 1);
+}
+
+static int orc_far(const int16_t *a, const int16_t *b)
+{
+	return abs(a[0] - b[0]) >= 4 || abs(a[1] - b[1]) >= 4;
+}
+
+static int orc_mv_bs(const m2r_inter_t *q, int qx, int qy, const m2r_inter_t *p, int px, int py)
+{
+	const int bq = (qy >> 1) * 2 + (qx >> 1), bp = (py >> 1) * 2 + (px >> 1);
+	const int q0 = q->slot[0][bq], q1 = q->slot[1][bq], p0 = p->slot[0][bp], p1 = p->slot[1][bp];
+	const int16_t *qm0 = q->mv[0][qy * 4 + qx], *qm1 = q->mv[1][qy * 4 + qx];
+	const int16_t *pm0 = p->mv[0][py * 4 + px], *pm1 = p->mv[1][py * 4 + px];
+	if ((p0 != q0 || p1 != q1) && (p1 != q0 || p0 != q1)) return 1; /* different reference pictures */
+	if (q0 >= 0 && q1 >= 0) {
+		if (q0 == q1) return (orc_far(qm0, pm0) || orc_far(qm1, pm1)) && (orc_far(qm0, pm1) || orc_far(qm1, pm0));
+		return q0 == p0 ? (orc_far(qm0, pm0) || orc_far(qm1, pm1)) : (orc_far(qm0, pm1) || orc_far(qm1, pm0));
+	}
+	if (q0 >= 0) return q0 == p0 ? orc_far(qm0, pm0) : orc_far(qm0, pm1);
+	return q1 == p0 ? orc_far(qm1, pm0) : orc_far(qm1, pm1);
+}
+
+/* bS of MB (mbx, mby) in direction dir (0 vertical edges, 1 horizontal): byte e = edge, 2 bits per segment */
+static uint32_t orc_bs(const m2r_picture_t *pic, int mbx, int mby, int dir)
+{
+	const int W = pic->width_mbs;
+	const m2r_mb_t *q = &pic->mb[mby * W + mbx];
+	const m2r_inter_t *qi;
+	uint32_t str = 0;
+	if (q->kind != M2R_MB_INTER) return (q->kind == M2R_MB_PCM || q->kind == M2R_MB_I8x8) ? 0x00ff00ffu : 0xffffffffu;
+	qi = &pic->inter[q->inter];
+	if (dir ? mby > 0 : mbx > 0) {
+		const m2r_mb_t *p = dir ? q - W : q - 1;
+		if (p->kind != M2R_MB_INTER) {
+			str = 0xaa; /* bS 2 on every segment; the BS4 flag makes it 4 */
+		} else {
+			const m2r_inter_t *pi = &pic->inter[p->inter];
+			for (int g = 0; g < 4; ++g) {
+				const int qx = dir ? g : 0, qy = dir ? 0 : g, px = dir ? g : 3, py = dir ? 3 : g;
+				const int v = (orc_nz(q, qx, qy) || orc_nz(p, px, py)) ? 2 : orc_mv_bs(qi, qx, qy, pi, px, py);
+				str |= (uint32_t)v << (2 * g);
+			}
+		}
+	}
+	for (int e = 1; e < 4; ++e) {
+		if ((q->flags & M2R_FLAG_T8x8) && (e & 1)) continue; /* no 4x4 edges inside an 8x8 transform */
+		for (int g = 0; g < 4; ++g) {
+			const int qx = dir ? g : e, qy = dir ? e : g, px = dir ? qx : qx - 1, py = dir ? qy - 1 : qy;
+			const int v = (orc_nz(q, qx, qy) || orc_nz(q, px, py)) ? 2 : orc_mv_bs(qi, qx, qy, qi, px, py);
+			str |= (uint32_t)v << (8 * e + 2 * g);
+		}
+	}
+	return str;
+}
+
 /* deblock_pb (h264.cpp:10540-10663): MB raster order; per MB left edge, inner vertical, top edge,
  * inner horizontal; chroma inner edge uses luma edge 2 strengths */
 static void deblock_picture(const m2r_picture_t *pic, plane_t *f)
@@ -1010,7 +1074,7 @@ static void deblock_picture(const m2r_picture_t *pic, plane_t *f)
 			int qpc[2];
 			if (q->flags & M2R_DBK_OFF) continue;
 			for (int dir = 0; dir < 2; ++dir) {
-				uint32_t str = dir ? q->bs_h : q->bs_v;
+				uint32_t str = orc_bs(pic, mbx, mby, dir);
 				int edge_flag = dir ? M2R_DBK_TOP : M2R_DBK_LEFT;
 				int bs4_flag = dir ? M2R_DBK_TOP_BS4 : M2R_DBK_LEFT_BS4;
 				if ((q->flags & edge_flag) && (str & 255)) {

@@ -35,6 +35,11 @@ $(HARNESS): tests/harness/m2decoder_like.cpp $(LIB) include/m2dec_amd.h include/
 $(APP): m2dec_amd/csrc/app/h264dec.c $(LIB) include/m2dec_amd.h
 	$(CC) -O2 -Wall -std=gnu11 -Iinclude -o $@ $< -Lm2dec_amd/lib -lm2dec_amd -Wl,-rpath,'$$ORIGIN'
 
+# the CPU guard itself must run on any x86-64: no HOST_ARCH
+build/host/cpucheck.o: m2dec_amd/csrc/host/cpucheck.c
+	@mkdir -p $(dir $@)
+	$(CC) $(filter-out $(HOST_ARCH),$(CFLAGS)) -c $< -o $@
+
 build/host/%.o: m2dec_amd/csrc/host/%.c $(wildcard m2dec_amd/csrc/host/*.h) $(wildcard include/*.h)
 	@mkdir -p $(dir $@)
 	$(CC) $(CFLAGS) -c $< -o $@

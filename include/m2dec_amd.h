@@ -49,10 +49,24 @@ typedef struct {
 	double host_copy_us;
 } m2dec_amd_stats_t;
 
+/* ABI revision of the structs in this header and m2d_recon.h.  3: m2r_backend_t gained `bind` (decode
+ * ahead) and m2dec_amd_stats_t grew to its current size.  A caller compiled against another revision
+ * checks m2dec_amd_abi_version() before passing either struct; m2dec_amd_h264_set_backend2 accepts an
+ * older (smaller) m2r_backend_t by size, and m2dec_amd_stats_size() is the size every stats pointer
+ * must have room for. */
+#define M2DEC_AMD_ABI_VERSION 3
+int m2dec_amd_abi_version(void);
+size_t m2dec_amd_stats_size(void);
+/* 0 if the host CPU lacks the x86-64-v3 features the host library is built for (decoder inits then
+ * fail with a message, cpucheck.c) */
+int m2dec_amd_host_cpu_ok(void);
+
 /* Use `be` instead of the default HIP back end for this decoder context (call after init).
  * The context takes ownership: be->destroy is called when the context is released or reclaimed.
  * be == NULL detaches the current back end without destroying it (a borrowed one). */
 int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be);
+/* the same with the caller's sizeof(m2r_backend_t): members past be_size are taken as NULL */
+int m2dec_amd_h264_set_backend2(void *ctx, const m2r_backend_t *be, size_t be_size);
 /* GPU ordinal used by the default back end (call after init, before the first SPS). */
 int m2dec_amd_h264_set_device(void *ctx, int device);
 /* Slice data of up to `threads` pictures parsed ahead on worker threads (0: on the caller's thread).

@@ -1,3 +1,4 @@
+#include <stddef.h>
 /*
  * h264d_func — the reference's m2d_func_table_t for H.264 (h264.cpp:12057-12068), backed by the
  * m2dec_amd host parser + a reconstruction back end (the gfx950 HIP back end by default).
@@ -147,12 +148,14 @@ static int reclaim_victims(const void *ctx, h264_dec_t **out, int max)
 	return n;
 }
 
+extern int m2dec_host_cpu_ok; /* cpucheck.c */
+
 static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg)
 {
 	h264_handle_t *h = (h264_handle_t *)ctx;
 	h264_dec_t *victims[64], *d;
 	int nv;
-	if (!ctx) return -1;
+	if (!ctx || !m2dec_host_cpu_ok) return -1;
 	pthread_mutex_lock(&reg_mu);
 	nv = reclaim_victims(ctx, victims, 64);
 	pthread_mutex_unlock(&reg_mu);
@@ -453,20 +456,33 @@ static const m2d_func_table_t h264d_func_ = {
 const m2d_func_table_t * const h264d_func = &h264d_func_;
 
 /* ------------------------------------------------------------------ extra C ABI */
-int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
+int m2dec_amd_h264_set_backend2(void *ctx, const m2r_backend_t *be, size_t be_size)
 {
-	h264_dec_t *d = enter(ctx);
+	h264_dec_t *d;
+	if (be && (be_size < offsetof(m2r_backend_t, bind) || be_size > sizeof(m2r_backend_t))) return -1;
+	d = enter(ctx);
 	if (!d) return -1;
 	if (!be) { /* detach a borrowed back end without destroying it */
 		d->have_backend = 0;
 	} else {
 		if (d->have_backend && d->backend.destroy) d->backend.destroy(d->backend.self);
-		d->backend = *be;
+		/* a caller built against an older m2r_backend_t passes its smaller size: the members it does
+		 * not know (bind) stay NULL, so its back end gets pictures in API order */
+		memset(&d->backend, 0, sizeof(d->backend));
+		memcpy(&d->backend, be, be_size);
 		d->have_backend = 1;
 	}
 	leave(d);
 	return 0;
 }
+
+int m2dec_amd_h264_set_backend(void *ctx, const m2r_backend_t *be)
+{
+	return m2dec_amd_h264_set_backend2(ctx, be, sizeof(m2r_backend_t));
+}
+
+int m2dec_amd_abi_version(void) { return M2DEC_AMD_ABI_VERSION; }
+size_t m2dec_amd_stats_size(void) { return sizeof(m2dec_amd_stats_t); }
 
 int m2dec_amd_h264_set_parse_threads(void *ctx, int threads)
 {

@@ -1023,11 +1023,13 @@ static int hdr_dummy(void *a, void *b)
 	return 0;
 }
 
+extern int m2dec_host_cpu_ok; /* cpucheck.c */
+
 static int api_init(void *ctx, int dummy, int (*cb)(void *, void *), void *arg)
 {
 	mpeg2_dec_t *m = CTX(ctx);
 	(void)dummy;
-	if (!m) return -1;
+	if (!m || !m2dec_host_cpu_ok) return -1;
 	memset(m, 0, sizeof(*m));
 	pthread_once(&lut_once, build_luts);
 	m->header_callback = cb ? cb : hdr_dummy;

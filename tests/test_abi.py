@@ -62,3 +62,29 @@ def test_product_path_fails_loudly_without_gpu(built):
         pass
     else:
         raise AssertionError("HIP product path must not fall back to a CPU reconstruction")
+
+
+def test_abi_revision_and_sized_backend(built):
+    """the structs changed size in revision 3; the library says which revision it is and
+    accepts an older, smaller m2r_backend_t by size (its unknown `bind` taken as NULL)."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "m2dec_amd", "lib", "libm2dec_amd.so"))
+    hdr = open(os.path.join(ROOT, "include", "m2dec_amd.h")).read()
+    rev = int(re.search(r"#define M2DEC_AMD_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.m2dec_amd_abi_version() == rev
+    lib.m2dec_amd_stats_size.restype = ctypes.c_size_t
+    assert lib.m2dec_amd_stats_size() >= 112
+    assert lib.m2dec_amd_host_cpu_ok() == 1
+    import m2dec_amd
+
+    t = m2dec_amd.H264Decoder.table()
+    ctx = ctypes.create_string_buffer(t.context_size)
+    init = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)(t.init)
+    assert init(ctx, -1, None, None) == 0
+    be = (ctypes.c_void_p * 7)()  # self + 6 function pointers (revision 3)
+    lib.m2dec_amd_h264_set_backend2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    ptr = ctypes.sizeof(ctypes.c_void_p)
+    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 3 * ptr) == -1   # shorter than any revision
+    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 8 * ptr) == -1   # longer than this revision
+    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 6 * ptr) == 0    # revision 2: no bind
+    assert lib.m2dec_amd_h264_set_backend2(ctx, None, 0) == 0        # detach (borrowed, not destroyed)
+    lib.m2dec_amd_h264_release(ctx)

@@ -14,18 +14,19 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -g -fPIC -std=c++17 $(INC) -Wno-unused-re
 HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)
 HOST_OBJ := $(patsubst m2dec_amd/csrc/host/%.c,build/host/%.o,$(HOST_SRC))
 HIP_SRC := m2dec_amd/csrc/hip/recon_hip.hip
-HIP_HDR := m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h
-HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o
+HIP_HDR := m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h m2dec_amd/csrc/host/h265_dec.h
+HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 
 LIB := m2dec_amd/lib/libm2dec_amd.so
 ORACLE := oracle/_build/liboracle.so
 GEN := tools/_build/h264gen
+GEN265 := tools/_build/h265gen
 M2VGEN := tools/_build/m2vgen
 
 APP := m2dec_amd/lib/h264dec
 HARNESS := tools/_build/m2decoder_like
 
-all: $(LIB) $(ORACLE) $(GEN) $(M2VGEN) $(APP) $(HARNESS)
+all: $(LIB) $(ORACLE) $(GEN) $(GEN265) $(M2VGEN) $(APP) $(HARNESS)
 
 # test harness: drives h264d_func the way src/app/m2decoder.h does (no release call)
 $(HARNESS): tests/harness/m2decoder_like.cpp $(LIB) include/m2dec_amd.h include/m2d.h
@@ -52,9 +53,13 @@ $(LIB): $(HOST_OBJ) $(HIP_OBJ)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libm2dec_amd.so -Wl,--no-undefined -lpthread
 
-$(ORACLE): oracle/recon_oracle.c include/m2d_recon.h include/m2d.h
+$(ORACLE): oracle/recon_oracle.c oracle/h265_oracle.c include/m2d_recon.h include/m2d.h
 	@mkdir -p $(dir $@)
-	$(CC) -O2 -g -fPIC -Wall -std=gnu11 -Iinclude -shared -o $@ oracle/recon_oracle.c
+	$(CC) -O2 -g -fPIC -Wall -std=gnu11 -Iinclude -shared -o $@ oracle/recon_oracle.c oracle/h265_oracle.c
+
+$(GEN265): tools/h265gen/h265gen.c tools/h264gen/cabac_enc.c tools/h264gen/bitwriter.h m2dec_amd/csrc/host/h264_spec_tables.c m2dec_amd/csrc/host/h265_tables.c m2dec_amd/csrc/host/h265_dec.h
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ tools/h265gen/h265gen.c tools/h264gen/cabac_enc.c m2dec_amd/csrc/host/h264_spec_tables.c m2dec_amd/csrc/host/h265_tables.c -lm
 
 $(GEN): $(wildcard tools/h264gen/*.c) $(wildcard tools/h264gen/*.h) m2dec_amd/csrc/host/h264_spec_tables.c
 	@mkdir -p $(dir $@)
@@ -65,18 +70,18 @@ $(M2VGEN): tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c m2dec_amd/cs
 	$(CC) -O2 -g -Wall -std=gnu11 $(INC) -o $@ tools/m2vgen/m2vgen.c m2dec_amd/csrc/host/mpeg2_tables.c -lm
 
 DBG_LIB := build/dbg/libm2dec_amd_stamps.so
-$(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o
+$(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -c $(HIP_SRC) -o build/dbg/recon_hip_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stamps.o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stamps.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o -Wl,--no-undefined
 
 stamps: $(DBG_LIB)
 
 # diagnostic variants: make variant V=NAME FLAGS="-DX"
-variant: $(HOST_OBJ) build/hip/runtime.o build/hip/m2v_hip.o
+variant: $(HOST_OBJ) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 	@mkdir -p build/var
 	$(HIPCC) $(HIPFLAGS) $(FLAGS) -c $(HIP_SRC) -o build/var/recon_$(V).o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/var/lib_$(V).so $(HOST_OBJ) build/var/recon_$(V).o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o build/var/lib_$(V).so $(HOST_OBJ) build/var/recon_$(V).o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o -Wl,--no-undefined
 
 clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build

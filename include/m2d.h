@@ -6,6 +6,7 @@
  *   m2d_info_t        /root/reference/src/lib/m2d.h:58-65
  *   m2d_func_table_t  /root/reference/src/lib/m2d.h:66-75
  *   h264d_func        /root/reference/src/lib/h264.h:457, h264.cpp:12057-12068
+ *   h265d_func        /root/reference/src/lib/h265.h:37, h265.cpp:5010-5025
  *   bitio API         /root/reference/src/lib/bitio.h:57-75 (+ m2d_next_start_code, m2d.h:77-80)
  * Same names, argument meaning and return conventions (decode_picture: 1 picture done,
  * -1 syntax error, -2 end of data; peek/get: 1 frame, 0 none, -1 bad args).
@@ -108,6 +109,8 @@ extern const m2d_func_table_t * const h264d_func;
 /* The MPEG-1/2 video decoder (mpeg2.cpp:1800-1811; mpeg2.h): intra pictures on the CPU
  * (BASELINE.json configs[0]); P / B pictures are reported as errors. */
 extern const m2d_func_table_t * const m2d_func;
+/* h265.h:37, h265.cpp:5010-5025 (m2dec_amd/csrc/host/h265_dec.c) */
+extern const m2d_func_table_t * const h265d_func;
 
 #ifdef __cplusplus
 }

@@ -175,6 +175,70 @@ typedef struct m2v_picture {
 	int16_t *coef;
 } m2v_picture_t;
 
+/* ---------------------------------------------------------------- H.265 (h265d_func) records
+ * The host parser (m2dec_amd/csrc/host/h265_dec.c) turns each picture into:
+ *   - transform blocks in decoding order, each predicted (intra) then given its residual: the
+ *     reference's transform_tree leaves (h265.cpp:3026-3075), luma and chroma (Cb + Cr together)
+ *     as separate records;
+ *   - a map from every 4x4 unit of each plane to the record that writes it (the GPU waits on the
+ *     records that own a block's neighbour samples);
+ *   - deblocking edge records (bS and edge QP per 4-sample segment on the 8x8 grid, h265modules.h
+ *     h265d_deblocking_strength_t) and one SAO record per CTU (h265modules.h:338-351). */
+#define H265R_MAX_FRAMES 8 /* H265D_MAX_FRAME_NUM (h265modules.h:40) */
+enum { H265R_RES_NONE = 0, H265R_RES_DC = 1, H265R_RES_FULL = 2, H265R_RES_DST = 3, H265R_RES_SKIP = 4 };
+#define H265R_TU_PRED 1u /* intra-predict the block before its residual (else: residual only) */
+
+typedef struct {
+	uint16_t x, y;        /* top-left sample in its plane (chroma: in chroma samples) */
+	uint8_t log2;         /* 2..5 */
+	uint8_t plane;        /* 0 luma, 1 chroma (Cb and Cr, interleaved NV12) */
+	uint8_t mode;         /* intra prediction mode 0..34 */
+	uint8_t flags;        /* H265R_TU_PRED */
+	int16_t avail_top;    /* samples of the row above available from x on (top + top-right), -1: none */
+	int16_t avail_left;   /* samples of the column left available from y on (left + bottom-left), -1: none */
+	uint8_t res[2];       /* residual kind H265R_RES_*: luma [0]; chroma Cb [0], Cr [1] */
+	uint8_t strong;       /* luma: strong intra smoothing enabled (sps) */
+	uint8_t pad;
+	uint32_t coef[2];     /* coefficient-pool offsets (dequantised int16, (1 << log2)^2 raster) */
+} h265r_tu_t;
+
+typedef struct {
+	uint8_t type[3];      /* per component: 0 off, 1 band offset, 2 edge offset */
+	uint8_t band[3];      /* band position */
+	uint8_t eo[3];        /* edge class 0..3 (Cr shares Cb's) */
+	uint8_t pad[3];
+	int8_t off[3][4];     /* offsets, signs applied (edge: categories 1, 2 >= 0; 3, 4 <= 0) */
+} h265r_sao_t;
+
+#define H265R_PIC_DEBLOCK 1
+#define H265R_PIC_SAO_LUMA 2
+#define H265R_PIC_SAO_CHROMA 4
+
+typedef struct {
+	int32_t width, height;       /* frame: CTB-aligned, luma stride = width */
+	int32_t pic_w, pic_h;        /* pic_width / height_in_luma_samples */
+	int32_t ctb_log2, slot;      /* CTB size, caller frame written */
+	int32_t n_tu, n_coef;
+	int32_t flags;               /* H265R_PIC_* */
+	int32_t beta_offset, tc_offset;    /* slice_beta_offset_div2 * 2, slice_tc_offset_div2 * 2 */
+	int32_t cb_qp_offset, cr_qp_offset; /* pps_cb / cr_qp_offset (chroma deblocking) */
+	h265r_tu_t *tu;
+	int16_t *coef;
+	int32_t *map;                /* luma (width/4 x height/4) then chroma (width/8 x height/8) 4x4 units: record index */
+	uint8_t *bs_v;               /* vertical edges [height/4][width/8]: (qp << 2) | bS, edge x = 8 i, rows 4 j.. */
+	uint8_t *bs_h;               /* horizontal edges [height/8][width/4]: edge y = 8 j, columns 4 i.. */
+	h265r_sao_t *sao;            /* per CTU, raster */
+} h265r_picture_t;
+
+/* An H.265 reconstruction back end (default: the gfx950 one, m2dec_amd/csrc/hip/h265_hip.hip). */
+typedef struct h265r_backend {
+	void *self;
+	int (*set_frames)(void *self, int n, const m2d_frame_t *frames, int width, int height);
+	int (*submit)(void *self, const h265r_picture_t *pic);
+	int (*sync_frame)(void *self, int slot); /* the picture last submitted into `slot` is in the caller's frame */
+	void (*destroy)(void *self);
+} h265r_backend_t;
+
 #ifdef __cplusplus
 }
 #endif

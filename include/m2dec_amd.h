@@ -190,6 +190,26 @@ int m2dec_amd_m2v_intra_dc(const uint8_t *bits, size_t n, int cc, int dc_precisi
 int m2dec_amd_m2v_intra_ac(const uint8_t *bits, size_t n, int mpeg2, int intra_vlc_format, int alternate_scan,
                            int q_scale, const uint8_t *qmat, int dc, int16_t coef[64]);
 
+/* ---- H.265 (h265d_func, m2dec_amd/csrc/host/h265_dec.c) */
+/* M2Decoder over h265d_func (m2decoder.h MODE_H265): every output frame to on_frame in output order;
+ * `be` is a borrowed reconstruction back end (NULL: the gfx950 one on `device`, no host fallback).
+ * Returns the last decode_picture result (-2: end of the data). */
+int m2dec_amd_decode_h265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
+/* Reconstruct an h265d_func context's pictures with `be` instead of the gfx950 back end (call after init,
+ * before the first SPS; NULL detaches a borrowed one), or on GPU `device`. */
+int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be);
+int m2dec_amd_h265_set_device(void *ctx, int device);
+/* Free the heap and device state an h265d_func context owns. */
+void m2dec_amd_h265_release(void *ctx);
+/* Test hook: the parsed syntax (CU modes, residual levels) of later H.265 decodes into `path`, in
+ * tools/h265gen --dump's format (NULL: stop). */
+int m2dec_amd_h265_set_dump(const char *path);
+/* CABAC bins decoded by a context (host-parse measurement). */
+uint64_t m2dec_amd_h265_cabac_bins(const void *ctx);
+/* The gfx950 H.265 reconstruction back end (m2dec_amd/csrc/hip/h265_hip.hip). */
+int m2dec_amd_h265_hip_backend_create(h265r_backend_t *out, int device);
+
 /* ---- record traces (m2dec_amd/csrc/host/trace.c): a stream parsed once, records kept in memory */
 typedef struct m2dec_amd_trace m2dec_amd_trace_t;
 typedef struct {

@@ -484,3 +484,41 @@ class HipReplay:
 
     def __exit__(self, *a):
         self.close()
+
+
+class Backend265(ctypes.Structure):
+    """h265r_backend_t (include/m2d_recon.h)."""
+    _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("submit", ctypes.c_void_p),
+                ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p)]
+
+
+def decode_h265(data: bytes, backend: Optional[Backend265] = None, device: int = 0, emptify: bool = False,
+                on_frame: Optional[Callable[[Frame], None]] = None) -> tuple:
+    """An H.265 elementary stream through h265d_func like ``h264dec -O x.265`` (M2Decoder, MODE_H265):
+    returns (MD5 line of every output frame, last decode_picture result: -2 at the end of the data).
+    ``backend`` None -> the gfx950 reconstruction on ``device`` (an error, not a host fallback, when it
+    is unusable); a borrowed h265r_backend_t otherwise (the CPU oracle in tests)."""
+    L = lib()
+    md5s: List[str] = []
+    errs: List[BaseException] = []
+
+    def _cb(_arg, fp):
+        try:
+            md5s.append(frame_md5(fp.contents))
+            if on_frame is not None:
+                on_frame(fp.contents)
+        except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
+            errs.append(e)
+
+    cb = ON_FRAME(_cb)
+    err = ctypes.c_int()
+    L.m2dec_amd_decode_h265.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend265), ctypes.c_int,
+                                        ctypes.c_int, ON_FRAME, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    L.m2dec_amd_decode_h265.restype = ctypes.c_int
+    if backend is None and not L.m2dec_amd_hip_available():
+        raise RuntimeError("m2dec_amd: no usable gfx950 device for the H.265 reconstruction")
+    L.m2dec_amd_decode_h265(data, len(data), ctypes.byref(backend) if backend is not None else None, device,
+                            int(emptify), cb, None, ctypes.byref(err))
+    if errs:
+        raise errs[0]
+    return md5s, err.value

@@ -17,6 +17,7 @@ typedef struct {
 	const m2d_func_table_t *func;
 	void *ctx;
 	int h264;
+	int h265;
 	const uint8_t *data;
 	size_t len, pos;
 	/* -f: headers replayed before the key frame (header_data_list_t), then a null sentinel */
@@ -76,7 +77,8 @@ static int header_cb(void *arg, void *id)
 	width = (info.src_width + 15) & ~15;
 	height = (info.src_height + 15) & ~15;
 	luma_len = (size_t)width * (size_t)height;
-	bufnum = info.frame_num + (v->h264 ? 16 : 0);
+	/* m2decoder.h:59-66: +16 for H.264 / H.265; at most 64 (H.264) or MAX_FRAME_NUM 16 */
+	bufnum = info.frame_num + ((v->h264 || v->h265) ? 16 : 0);
 	if (bufnum > (v->h264 ? 64 : 16)) bufnum = v->h264 ? 64 : 16;
 	if (v->nframes && bufnum <= v->nframes && luma_len <= v->luma_len &&
 	    (size_t)(info.additional_size ? info.additional_size : 1) <= v->second_len) {
@@ -167,6 +169,82 @@ void m2dec_amd_m2v_last_checks(uint64_t *clip_violations, uint64_t *mc_out_of_fr
 {
 	if (clip_violations) *clip_violations = t_m2v_clip;
 	if (mc_out_of_frame) *mc_out_of_frame = t_m2v_mc;
+}
+
+static int decode_core(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb, int emptify,
+                       int skip, const m2r_backend_t *backend, int parse_threads, int m2v_device,
+                       void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
+
+static int decode_core265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
+
+/* H.265 through h265d_func (M2Decoder with MODE_H265, m2decoder.h:180-182): the back end `be` (borrowed;
+ * NULL: the gfx950 one on `device`) */
+int m2dec_amd_decode_h265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+{
+	return decode_core265(data, len, be, device, emptify, on_frame, arg, last_error);
+}
+
+static int decode_loop(drv_t *v, int emptify, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg);
+
+static int decode_core265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+{
+	drv_t v;
+	int err;
+	memset(&v, 0, sizeof(v));
+	v.func = h265d_func;
+	v.h265 = 1;
+	v.data = data;
+	v.len = len;
+	v.ctx = calloc(1, h265d_func->context_size);
+	if (!v.ctx) return -1;
+	h265d_func->init(v.ctx, -1, header_cb, &v);
+	if (be) m2dec_amd_h265_set_backend(v.ctx, be);
+	else m2dec_amd_h265_set_device(v.ctx, device);
+	dec_bits_set_callback(h265d_func->stream_pos(v.ctx), reread, &v);
+	err = decode_loop(&v, emptify, on_frame, arg);
+	if (last_error) *last_error = err;
+	if (be) m2dec_amd_h265_set_backend(v.ctx, NULL); /* borrowed */
+	m2dec_amd_h265_release(v.ctx);
+	free(v.ctx);
+	frames_free(&v);
+	return err;
+}
+
+/* h264dec.cpp:251-257 over M2Decoder::decode / decode_residual (m2decoder.h:132-157) */
+static int decode_loop(drv_t *v, int emptify, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg)
+{
+	const m2d_func_table_t *func = v->func;
+	m2d_frame_t frm;
+	int err = -1;
+	for (;;) {
+		while (func->peek_decoded_frame(v->ctx, &frm, 0) <= 0) {
+			err = func->decode_picture(v->ctx);
+			if (v->failed) err = -1;
+			if (err < 0) {
+				while (func->peek_decoded_frame(v->ctx, &frm, 1) > 0) {
+					if (on_frame) on_frame(arg, &frm);
+					func->get_decoded_frame(v->ctx, &frm, 1);
+				}
+				return err;
+			}
+		}
+		do {
+			func->get_decoded_frame(v->ctx, &frm, 0);
+			if (on_frame) on_frame(arg, &frm);
+		} while (emptify && 0 < func->peek_decoded_frame(v->ctx, &frm, 0));
+		err = func->decode_picture(v->ctx);
+		if (v->failed) err = -1;
+		if (err < 0) {
+			while (0 < func->peek_decoded_frame(v->ctx, &frm, 1)) {
+				if (on_frame) on_frame(arg, &frm);
+				func->get_decoded_frame(v->ctx, &frm, 1);
+			}
+			return err;
+		}
+	}
 }
 
 static int decode_core(const m2d_func_table_t *func, int h264, const uint8_t *data, size_t len, int dpb, int emptify,

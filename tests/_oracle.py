@@ -58,3 +58,38 @@ QUIRKS = ["sat16", "w128_explicit", "w128_implicit", "swar_big", "deq8_trunc", "
 def quirk_hits(reset=True):
     """Counts of the Appendix A quirk paths the oracle executed since the last reset (recon_oracle.c)."""
     return {q: int(oracle_lib().oracle_quirk_hits(i, 1 if reset else 0)) for i, q in enumerate(QUIRKS)}
+
+
+# ---- H.265: oracle/h265_oracle.c as an h265r_backend_t
+def _h265_lib():
+    L = oracle_lib()
+    from m2dec_amd import Backend265
+    L.h265_oracle_backend_create.argtypes = [ctypes.POINTER(Backend265)]
+    L.h265_oracle_backend_create.restype = ctypes.c_int
+    L.h265_oracle_violations.argtypes = [ctypes.c_int]
+    L.h265_oracle_violations.restype = ctypes.c_uint64
+    return L
+
+
+def h265_violations(reset=True):
+    """CLIP255C arguments outside [-256, 767] and DC-only terms beyond the SWAR byte range seen by the H.265
+    oracle since the last reset."""
+    return int(_h265_lib().h265_oracle_violations(1 if reset else 0))
+
+
+class Oracle265Backend:
+    def __init__(self):
+        from m2dec_amd import Backend265
+        self.be = Backend265()
+        assert _h265_lib().h265_oracle_backend_create(ctypes.byref(self.be)) == 0
+
+    def close(self):
+        if self.be.destroy:
+            ctypes.CFUNCTYPE(None, ctypes.c_void_p)(self.be.destroy)(self.be.self)
+            self.be.destroy = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -1,6 +1,707 @@
-/* placeholder: replaced by the gfx950 H.265 reconstruction */
+/*
+ * gfx950 reconstruction of H.265 intra pictures (h265d_func): the records of one picture (include/m2d_recon.h
+ * h265r_*, made by m2dec_amd/csrc/host/h265_dec.c) in, the picture's NV12 samples in its device frame out.
+ * It restates the reference decoder's reconstruction (h265.cpp:1693-2913 intra prediction and residual,
+ * :4125-4384 deblocking, :4386-4729 SAO), exactly as oracle/h265_oracle.c does on the CPU.
+ *
+ * k_h265_intra — the transform blocks in decoding order, one 64-lane wave (= one workgroup) at a time,
+ *   persistent: a wave takes the next block from a counter, waits until the blocks that own its
+ *   neighbour samples are done (the 4x4-unit owner map: one lane per neighbour unit, at most 33), then
+ *   predicts (reference samples gathered straight from the frame with the substitution folded into a
+ *   clamp — the available samples of a block always form one run of the substitution order —, [1 2 1] /
+ *   strong smoothing in LDS, planar / DC / angular per sample), inverse-transforms the residual in LDS
+ *   (DCT 4..32 / DST 4 as two matrix passes with the int16 clip between, the reference's DC-only and
+ *   transform-skip shortcuts), adds, stores, releases and raises the block's done flag.  Luma and chroma
+ *   blocks are independent chains and run side by side; the dependency graph, not the CTU raster, bounds
+ *   the picture (a block starts as soon as its left / top / top-right / bottom-left owners are done).
+ * k_h265_deblock — one thread per 4-sample edge segment on the 8x8 grid, vertical edges of the whole
+ *   picture, then (second launch) horizontal edges: HEVC's edges 8 samples apart never touch the same
+ *   sample, so every segment of a direction is independent.  Chroma rides on the luma segment (bS 2,
+ *   16-sample grid).
+ * k_h265_sao — one thread per sample, from a copy of the deblocked frame.
+ * Bounds: the intra kernel is latency-bound on the block chain (a 32x32 block is a 2 x 32^3 MAC inverse
+ * transform on one wave); deblocking and SAO are HBM-bound (each reads and writes the frame once).
+ */
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include "m2d_recon.h"
 #include "h265_dec.h"
-extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device) { (void)out; (void)device; return -1; }
+
+#define H265_CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
+#define H265_SPIN_LIMIT (1 << 22)
+
+namespace {
+
+typedef int __attribute__((address_space(1))) gi32;
+
+struct H265Args {
+	const h265r_tu_t *tu;
+	const int16_t *coef;
+	const int32_t *map;
+	const uint8_t *bs_v, *bs_h;
+	const h265r_sao_t *sao;
+	uint8_t *frame;   /* NV12, stride W */
+	uint8_t *copy;    /* the deblocked frame (SAO input) */
+	int *done;        /* per block */
+	int *counter;     /* next block */
+	int *err;         /* sticky: a hand-off that never came */
+	int W, H, pic_w, pic_h, ctb_log2, n_tu, flags;
+	int beta_offset, tc_offset, cb_qp_offset, cr_qp_offset;
+};
+
+__constant__ int c_cos[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
+                              61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0};
+__constant__ int c_dst[16] = {29, 55, 74, 84, 74, 74, 0, -74, 84, -29, -74, 55, 55, -84, 74, -29};
+__constant__ int c_ang[35] = {0,   0,   32,  26,  21,  17,  13,  9,  5,  2,  0,  -2, -5, -9, -13, -17, -21, -26,
+                              -32, -26, -21, -17, -13, -9,  -5,  -2, 0, 2, 5, 9, 13, 17, 21, 26, 32};
+__constant__ int c_inv[35] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -4096, -1638, -910, -630, -482, -390, -315,
+                              -256, -315, -390, -482, -630, -910, -1638, -4096, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+__constant__ uint8_t c_beta[36] = {6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28,
+                                   30, 32, 34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+__constant__ uint8_t c_tc[38] = {0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3,
+                                 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int sat16(int v) { return clampi(v, -32768, 32767); }
+
+/* the 32-point DCT coefficient of basis k, sample n (spec 8.6.4.2, eq. 8-315: 64 sqrt(2) cos((2n + 1) k pi / 64)
+ * as tabulated); the N-point matrix is T_N[k][n] = T_32[k * 32 / N][n] */
+__device__ __forceinline__ int dct32_coef(int k, int n)
+{
+	int m = ((2 * n + 1) * k) & 127, sign = 1;
+	if (m > 64) m = 128 - m;
+	if (m > 32) {
+		m = 64 - m;
+		sign = -1;
+	}
+	return sign * c_cos[m];
+}
+
+/* wave-private LDS of one block */
+struct Lds {
+	int16_t seq[2][132];   /* reference samples per component: [0 .. 4n] substitution order, filtered */
+	int16_t raw[132];      /* unfiltered copy (filter input) */
+	int16_t mat32[32 * 32]; /* the 32-point DCT matrix (built once per workgroup) */
+	int mat[32 * 32];      /* transform matrix of this block's size: mat[k * n + s] */
+	int t0[32 * 32];       /* coefficients, then the first-stage output */
+	int pred[2][32 * 32];  /* prediction, then prediction + residual */
+};
+
+__device__ __forceinline__ uint8_t *plane_px(const H265Args &a, int plane, int comp, int x, int y)
+{
+	return plane ? a.frame + (size_t)a.W * a.H + (size_t)y * a.W + (size_t)x * 2 + comp : a.frame + (size_t)y * a.W + x;
+}
+
+/* one block (wave-wide) */
+__device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane)
+{
+	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
+	const int ncomp = t.plane ? 2 : 1;
+	const bool luma = t.plane == 0;
+	/* ---- prediction */
+	for (int c = 0; c < ncomp; ++c) {
+		int *pred = s.pred[c];
+		if (!(t.flags & H265R_TU_PRED)) {
+			for (int i = lane; i < n2; i += 64) pred[i] = *plane_px(a, t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
+			continue;
+		}
+		const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
+		const bool top = at > 0, left = al > 0;
+		/* the available run [lo, hi] of the substitution order p[-1][2n-1] .. corner .. p[2n-1][-1] */
+		const int corner = 2 * n;
+		const int lo = left ? corner - al : (top ? corner + 1 : 0);
+		const int hi = top ? corner + at : (left ? corner - 1 : 0);
+		for (int i = lane; i <= 4 * n; i += 64) {
+			int v = 128;
+			if (top || left) {
+				const int k = clampi(i, lo, hi);
+				const int xx = k < corner ? -1 : (k == corner ? -1 : k - corner - 1);
+				const int yy = k < corner ? corner - 1 - k : -1;
+				v = *plane_px(a, t.plane, c, t.x + xx, t.y + yy);
+			}
+			s.raw[i] = (int16_t)v;
+		}
+		__syncthreads();
+		const int mode = t.mode;
+		bool filt = false;
+		if (luma && mode != 1 && n != 4) {
+			const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+			const int dist = d26 < d10 ? d26 : d10;
+			const int thres = n == 8 ? 7 : (n == 16 ? 1 : 0);
+			filt = mode == 0 || dist > thres;
+		}
+		const int last = 4 * n;
+		bool strong = false;
+		if (filt && t.strong && n == 32) {
+			const int cc = s.raw[corner], bl = s.raw[0], tr = s.raw[last];
+			strong = abs(cc + tr - 2 * s.raw[corner + n]) < 8 && abs(cc + bl - 2 * s.raw[corner - n]) < 8;
+		}
+		for (int i = lane; i <= last; i += 64) {
+			int v = s.raw[i];
+			if (strong) {
+				const int cc = s.raw[corner];
+				if (i > 0 && i < corner) v = ((63 - (corner - 1 - i)) * cc + (corner - i) * s.raw[0] + 32) >> 6;
+				else if (i > corner && i < last) v = ((63 - (i - corner - 1)) * cc + (i - corner) * s.raw[last] + 32) >> 6;
+			} else if (filt && i > 0 && i < last) {
+				v = (s.raw[i - 1] + 2 * s.raw[i] + s.raw[i + 1] + 2) >> 2;
+			}
+			s.seq[c][i] = (int16_t)v;
+		}
+		__syncthreads();
+		const int16_t *q = s.seq[c];
+#define LL(yy) ((int)q[corner - 1 - (yy)]) /* p[-1][y], y >= -1 */
+#define TT(xx) ((int)q[corner + 1 + (xx)]) /* p[x][-1], x >= -1 */
+		if (mode == 0) {
+			for (int i = lane; i < n2; i += 64) {
+				const int x = i & (n - 1), y = i >> log2;
+				pred[i] = ((n - 1 - x) * LL(y) + (x + 1) * TT(n) + (n - 1 - y) * TT(x) + (y + 1) * LL(n) + n) >> (log2 + 1);
+			}
+		} else if (mode == 1) {
+			int sum = 0;
+			for (int i = lane; i < n; i += 64) sum += TT(i) + LL(i);
+			for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+			const int dc = (sum + n) >> (log2 + 1);
+			for (int i = lane; i < n2; i += 64) {
+				const int x = i & (n - 1), y = i >> log2;
+				int v = dc;
+				if (luma && n < 32) {
+					if (x == 0 && y == 0) v = (LL(0) + 2 * dc + TT(0) + 2) >> 2;
+					else if (y == 0) v = (TT(x) + 3 * dc + 2) >> 2;
+					else if (x == 0) v = (LL(y) + 3 * dc + 2) >> 2;
+				}
+				pred[i] = v;
+			}
+		} else {
+			const int ang = c_ang[mode], inv = c_inv[mode];
+			const bool vert = mode >= 18;
+			for (int i = lane; i < n2; i += 64) {
+				const int x = i & (n - 1), y = i >> log2;
+				const int p = vert ? y : x, qq = vert ? x : y;
+				const int idx = ((p + 1) * ang) >> 5, fr = ((p + 1) * ang) & 31;
+				int r1, r2;
+				{
+					const int k = qq + idx + 1;
+					int kk = k;
+					if (kk >= 0) r1 = vert ? TT(kk - 1) : LL(kk - 1);
+					else r1 = vert ? LL(-1 + ((kk * inv + 128) >> 8)) : TT(-1 + ((kk * inv + 128) >> 8));
+					kk = k + 1;
+					if (kk >= 0) r2 = vert ? TT(kk - 1) : LL(kk - 1);
+					else r2 = vert ? LL(-1 + ((kk * inv + 128) >> 8)) : TT(-1 + ((kk * inv + 128) >> 8));
+				}
+				int v = fr ? ((32 - fr) * r1 + fr * r2 + 16) >> 5 : r1;
+				if (luma && n < 32) {
+					if (mode == 26 && x == 0) v = clampi(TT(0) + ((LL(y) - LL(-1)) >> 1), 0, 255);
+					if (mode == 10 && y == 0) v = clampi(LL(0) + ((TT(x) - TT(-1)) >> 1), 0, 255);
+				}
+				pred[i] = v;
+			}
+		}
+#undef LL
+#undef TT
+		__syncthreads();
+	}
+	/* ---- residual */
+	for (int c = 0; c < ncomp; ++c) {
+		const int kind = t.res[c];
+		int *pred = s.pred[c];
+		if (kind == H265R_RES_NONE) continue;
+		const int16_t *d = a.coef + t.coef[c];
+		if (kind == H265R_RES_DC) {
+			const int dc = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
+			for (int i = lane; i < n2; i += 64) pred[i] += dc;
+			continue;
+		}
+		if (kind == H265R_RES_SKIP) {
+			for (int i = lane; i < n2; i += 64) pred[i] += (d[i] + 16) >> 5;
+			continue;
+		}
+		const bool dstm = kind == H265R_RES_DST;
+		for (int i = lane; i < n2; i += 64) {
+			s.t0[i] = d[i];
+			const int k = i >> log2, sm = i & (n - 1);
+			s.mat[i] = dstm ? c_dst[k * 4 + sm] : s.mat32[(k << (5 - log2)) * 32 + sm];
+		}
+		__syncthreads();
+		/* first stage (columns): g[y][x] = sat16((sum_j M[j][y] d[j][x] + 64) >> 7) */
+		int g[16];
+		for (int r = 0, i = lane; i < n2; i += 64, ++r) {
+			const int x = i & (n - 1), y = i >> log2;
+			int e = 0;
+			for (int j = 0; j < n; ++j) e += s.mat[j * n + y] * s.t0[j * n + x];
+			g[r] = sat16((e + 64) >> 7);
+		}
+		__syncthreads();
+		for (int r = 0, i = lane; i < n2; i += 64, ++r) s.t0[i] = g[r];
+		__syncthreads();
+		/* second stage (rows): r[y][x] = sat16((sum_j M[j][x] g[y][j] + 2048) >> 12) */
+		for (int i = lane; i < n2; i += 64) {
+			const int x = i & (n - 1), y = i >> log2;
+			int e = 0;
+			for (int j = 0; j < n; ++j) e += s.mat[j * n + x] * s.t0[y * n + j];
+			pred[i] += sat16((e + 2048) >> 12);
+		}
+		__syncthreads();
+	}
+	/* ---- out */
+	for (int c = 0; c < ncomp; ++c)
+		for (int i = lane; i < n2; i += 64) {
+			const int x = i & (n - 1), y = i >> log2;
+			*plane_px(a, t.plane, c, t.x + x, t.y + y) = (uint8_t)clampi(s.pred[c][i], 0, 255);
+		}
+}
+
+__global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
+{
+	const H265Args a = *ap;
+	__shared__ Lds s;
+	const int lane = threadIdx.x;
+	for (int i = lane; i < 32 * 32; i += 64) s.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+	__syncthreads();
+	for (;;) {
+		const int v = __hip_atomic_fetch_add((gi32 *)&a.counter[0], lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const int idx = __builtin_amdgcn_readfirstlane(v);
+		if (idx >= a.n_tu) break;
+		const h265r_tu_t t = a.tu[idx];
+		/* wait for the owners of the neighbour samples: lane k < 2n/4 the top units, next the left units, last the corner */
+		{
+			const int n = 1 << t.log2;
+			const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
+			const int ntop = at > 0 ? (at + 3) >> 2 : 0, nleft = al > 0 ? (al + 3) >> 2 : 0;
+			const int mw = t.plane ? a.W / 8 : a.W / 4;
+			const int32_t *map = a.map + (t.plane ? (size_t)(a.W / 4) * (a.H / 4) : 0);
+			int dep = -1;
+			if (lane < ntop) dep = map[(size_t)((t.y >> 2) - 1) * mw + (t.x >> 2) + lane];
+			else if (lane < ntop + nleft) dep = map[(size_t)((t.y >> 2) + lane - ntop) * mw + (t.x >> 2) - 1];
+			else if (lane == ntop + nleft && ntop && nleft) dep = map[(size_t)((t.y >> 2) - 1) * mw + (t.x >> 2) - 1];
+			unsigned spins = 0;
+			for (;;) {
+				const bool ok = dep < 0 || dep >= idx ||
+				                __hip_atomic_load((gi32 *)&a.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+				if (__all(ok)) break;
+				if (++spins > H265_SPIN_LIMIT) {
+					__hip_atomic_store((gi32 *)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					break;
+				}
+				if (__hip_atomic_load((gi32 *)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+				__builtin_amdgcn_s_sleep(1);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+		}
+		do_block(a, t, s, lane);
+		/* publish: the samples, then the flag */
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+		__hip_atomic_store((gi32 *)&a.done[idx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+/* ---- deblocking (8.7.2; oracle/h265_oracle.c luma_edge / chroma_edge) */
+__device__ __forceinline__ void luma_edge(uint8_t *sp, int xs, int ls, int bs, int qp, int beta_off, int tc_off)
+{
+	const int bq = clampi(qp + beta_off, 0, 51), tq = clampi(qp + 2 * (bs - 1) + tc_off, 0, 51); /* tc QP clipped to 51 (reference) */
+	const int beta = bq < 16 ? 0 : c_beta[bq - 16], tc = tq < 16 ? 0 : c_tc[tq - 16];
+#define P(i, k) sp[(k) * ls - ((i) + 1) * xs]
+#define Q(i, k) sp[(k) * ls + (i) * xs]
+	const int dp0 = abs(P(2, 0) - 2 * P(1, 0) + P(0, 0)), dp3 = abs(P(2, 3) - 2 * P(1, 3) + P(0, 3));
+	const int dq0 = abs(Q(2, 0) - 2 * Q(1, 0) + Q(0, 0)), dq3 = abs(Q(2, 3) - 2 * Q(1, 3) + Q(0, 3));
+	if (!(dp0 + dq0 + dp3 + dq3 < beta)) return;
+	bool strong = true;
+	for (int k = 0; k < 4; k += 3) {
+		const int dpq = 2 * ((k ? dp3 : dp0) + (k ? dq3 : dq0));
+		if (!(dpq < (beta >> 2) && abs(P(3, k) - P(0, k)) + abs(Q(0, k) - Q(3, k)) < (beta >> 3) &&
+		      abs(P(0, k) - Q(0, k)) < ((5 * tc + 1) >> 1)))
+			strong = false;
+	}
+	const int dep = (dp0 + dp3) < ((beta + (beta >> 1)) >> 3), deq = (dq0 + dq3) < ((beta + (beta >> 1)) >> 3);
+	for (int k = 0; k < 4; ++k) {
+		const int p0 = P(0, k), p1 = P(1, k), p2 = P(2, k), p3 = P(3, k);
+		const int q0 = Q(0, k), q1 = Q(1, k), q2 = Q(2, k), q3 = Q(3, k);
+		if (strong) {
+			const int t2 = 2 * tc;
+			P(0, k) = (uint8_t)clampi((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, p0 - t2, p0 + t2);
+			P(1, k) = (uint8_t)clampi((p2 + p1 + p0 + q0 + 2) >> 2, p1 - t2, p1 + t2);
+			P(2, k) = (uint8_t)clampi((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, p2 - t2, p2 + t2);
+			Q(0, k) = (uint8_t)clampi((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, q0 - t2, q0 + t2);
+			Q(1, k) = (uint8_t)clampi((p0 + q0 + q1 + q2 + 2) >> 2, q1 - t2, q1 + t2);
+			Q(2, k) = (uint8_t)clampi((p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - t2, q2 + t2);
+		} else {
+			int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+			if (abs(delta) < tc * 10) {
+				delta = clampi(delta, -tc, tc);
+				P(0, k) = (uint8_t)clampi(p0 + delta, 0, 255);
+				Q(0, k) = (uint8_t)clampi(q0 - delta, 0, 255);
+				if (dep) P(1, k) = (uint8_t)clampi(p1 + clampi((((p2 + p0 + 1) >> 1) - p1 + delta) >> 1, -(tc >> 1), tc >> 1), 0, 255);
+				if (deq) Q(1, k) = (uint8_t)clampi(q1 + clampi((((q2 + q0 + 1) >> 1) - q1 - delta) >> 1, -(tc >> 1), tc >> 1), 0, 255);
+			}
+		}
+	}
+#undef P
+#undef Q
+}
+
+__device__ __forceinline__ int qpc_deb(int qpi)
+{
+	if (qpi < 30) return qpi;
+	if (qpi >= 43) return qpi - 6;
+	const int t[13] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37};
+	return t[qpi - 30];
+}
+
+__device__ __forceinline__ void chroma_edge(uint8_t *sp, int xs, int ls, int qp, int qp_off, int tc_off)
+{
+	const int q = clampi(qpc_deb(qp + qp_off) + 2 + tc_off, 0, 53);
+	if (q < 16) return;
+	const int tc = c_tc[q - 16];
+	for (int k = 0; k < 2; ++k) {
+		uint8_t *l = sp + k * ls;
+		const int p1 = l[-2 * xs], p0 = l[-xs], q0 = l[0], q1 = l[xs];
+		const int delta = clampi((((q0 - p0) * 4) + p1 - q1 + 4) >> 3, -tc, tc);
+		if (delta) {
+			l[-xs] = (uint8_t)clampi(p0 + delta, 0, 255);
+			l[0] = (uint8_t)clampi(q0 - delta, 0, 255);
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_h265_deblock(const H265Args *ap, int dir)
+{
+	const H265Args &a = *ap;
+	const int W = a.W, H = a.H;
+	const int rows = dir ? H / 8 : H / 4, cols = dir ? W / 4 : W / 8;
+	const int id = blockIdx.x * blockDim.x + threadIdx.x;
+	if (id >= rows * cols) return;
+	const int j = id / cols, i = id - j * cols;
+	const int v = (dir ? a.bs_h : a.bs_v)[id], b = v & 3, qp = v >> 2;
+	if (!b) return;
+	const int ex = dir ? 4 * i : 8 * i, ey = dir ? 8 * j : 4 * j;
+	uint8_t *luma = a.frame + (size_t)ey * W + ex;
+	if (dir == 0) luma_edge(luma, 1, W, b, qp, a.beta_offset, a.tc_offset);
+	else luma_edge(luma, W, 1, b, qp, a.beta_offset, a.tc_offset);
+	if (b == 2 && ((dir == 0 ? ex : ey) & 15) == 0) {
+		const int cx = ex >> 1, cy = ey >> 1;
+		for (int c = 0; c < 2; ++c) {
+			uint8_t *sp = a.frame + (size_t)W * H + (size_t)cy * W + (size_t)(2 * cx + c);
+			const int off = c ? a.cr_qp_offset : a.cb_qp_offset;
+			if (dir == 0) chroma_edge(sp, 2, W, qp, off, a.tc_offset);
+			else chroma_edge(sp, W, 2, qp, off, a.tc_offset);
+		}
+	}
+}
+
+/* ---- SAO (8.7.3; oracle/h265_oracle.c sao) */
+__global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
+{
+	const H265Args &a = *ap;
+	const int W = a.W, H = a.H;
+	const int nl = a.pic_w * a.pic_h, nc = (a.pic_w >> 1) * (a.pic_h >> 1) * 2;
+	const int id = blockIdx.x * blockDim.x + threadIdx.x;
+	if (id >= nl + nc) return;
+	int ci, x, y, pw, ph, step;
+	if (id < nl) {
+		ci = 0;
+		y = id / a.pic_w;
+		x = id - y * a.pic_w;
+		pw = a.pic_w;
+		ph = a.pic_h;
+		step = 1;
+	} else {
+		const int k = id - nl, cw = a.pic_w >> 1;
+		ci = 1 + (k & 1);
+		y = (k >> 1) / cw;
+		x = (k >> 1) - y * cw;
+		pw = cw;
+		ph = a.pic_h >> 1;
+		step = 2;
+	}
+	if (ci == 0 ? !(a.flags & H265R_PIC_SAO_LUMA) : !(a.flags & H265R_PIC_SAO_CHROMA)) return;
+	const int sub = ci ? 1 : 0, cs = (1 << a.ctb_log2) >> sub;
+	const int cols = (a.pic_w + (1 << a.ctb_log2) - 1) >> a.ctb_log2;
+	const h265r_sao_t sa = a.sao[(y / cs) * cols + x / cs];
+	const int type = sa.type[ci];
+	if (!type) return;
+	const uint8_t *src = ci ? a.copy + (size_t)W * H + (ci - 1) : a.copy;
+	uint8_t *dst = ci ? a.frame + (size_t)W * H + (ci - 1) : a.frame;
+	const int v = src[(size_t)y * W + (size_t)x * step];
+	int o = 0;
+	if (type == 1) {
+		const int k = (v >> 3) - sa.band[ci]; /* no band-table wrap (sao_bo_block, reference quirk) */
+		if (k >= 0 && k < 4) o = sa.off[ci][k];
+	} else {
+		const int e = sa.eo[ci];
+		const int dx0 = e == 1 ? 0 : (e == 3 ? 1 : -1), dy0 = e == 0 ? 0 : -1;
+		const int ax = x + dx0, ay = y + dy0, bx = x - dx0, by = y - dy0;
+		if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= pw || bx >= pw || ay >= ph || by >= ph) return;
+		const int pa = src[(size_t)ay * W + (size_t)ax * step], pb = src[(size_t)by * W + (size_t)bx * step];
+		const int ei = 2 + (v > pa) - (v < pa) + (v > pb) - (v < pb);
+		const int cat = ei == 0 ? 1 : (ei == 1 ? 2 : (ei == 3 ? 3 : (ei == 4 ? 4 : 0)));
+		if (cat) o = sa.off[ci][cat - 1];
+	}
+	dst[(size_t)y * W + (size_t)x * step] = (uint8_t)clampi(v + o, 0, 255);
+}
+
+/* ------------------------------------------------------------------ runtime */
+struct H265Gpu {
+	int dev = 0, cus = 0;
+	hipStream_t st = nullptr;
+	int W = 0, H = 0, n = 0;
+	size_t fsz = 0;
+	uint8_t *frames = nullptr, *copy = nullptr;
+	m2d_frame_t caller[H265R_MAX_FRAMES];
+	uint8_t *stg[H265R_MAX_FRAMES] = {};
+	hipEvent_t ev[H265R_MAX_FRAMES] = {};
+	bool pend[H265R_MAX_FRAMES] = {};
+	int *scratch = nullptr; /* done flags + the block counter */
+	int *err = nullptr;     /* sticky error word */
+	size_t scratch_n = 0;
+	struct Arena {
+		uint8_t *host = nullptr, *dev = nullptr;
+		size_t size = 0;
+		H265Args *args = nullptr;
+		hipEvent_t used = nullptr;
+	} ar[2];
+	int next = 0;
+	/* timing */
+	hipEvent_t t0[2] = {}, t1[2] = {};
+	double kernel_us = 0;
+	long pictures = 0;
+};
+
+static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int height)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g || n <= 0 || n > H265R_MAX_FRAMES || width <= 0 || height <= 0 || (width & 15) || (height & 15)) return -1;
+	H265_CHECK(hipSetDevice(g->dev));
+	H265_CHECK(hipStreamSynchronize(g->st));
+	const size_t fsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
+	if (!g->frames || fsz != g->fsz || n > g->n) {
+		if (g->frames) (void)hipFree(g->frames);
+		if (g->copy) (void)hipFree(g->copy);
+		g->frames = g->copy = nullptr;
+		H265_CHECK(hipMalloc((void **)&g->frames, fsz * (size_t)n));
+		H265_CHECK(hipMalloc((void **)&g->copy, fsz));
+		H265_CHECK(hipMemset(g->frames, 0, fsz * (size_t)n));
+	}
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
+		if (g->stg[i] && ((size_t)width * height != (size_t)g->W * g->H || i >= n)) {
+			(void)hipHostFree(g->stg[i]);
+			g->stg[i] = nullptr;
+		}
+		g->pend[i] = false;
+	}
+	g->fsz = fsz;
+	g->n = n;
+	g->W = width;
+	g->H = height;
+	memcpy(g->caller, frames, sizeof(m2d_frame_t) * (size_t)n);
+	return 0;
+}
+
+int h_submit(void *p, const h265r_picture_t *pic)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g || !g->frames || pic->width != g->W || pic->height != g->H || pic->slot < 0 || pic->slot >= g->n || pic->n_tu < 0)
+		return -1;
+	/* host-side checks of what the kernels assume: blocks inside the frame, coefficients inside the pool */
+	for (int i = 0; i < pic->n_tu; ++i) {
+		const h265r_tu_t &t = pic->tu[i];
+		const int n = 1 << t.log2, pw = t.plane ? g->W / 2 : g->W, ph = t.plane ? g->H / 2 : g->H;
+		if (t.log2 < 2 || t.log2 > 5 || t.x + n > pw || t.y + n > ph || t.mode > 34 || (t.x & 3) || (t.y & 3)) return -1;
+		for (int c = 0; c < 2; ++c)
+			if (t.res[c] && (int64_t)t.coef[c] + n * n > (int64_t)pic->n_coef) return -1;
+	}
+	H265_CHECK(hipSetDevice(g->dev));
+	const size_t units = (size_t)(g->W / 4) * (g->H / 4) + (size_t)(g->W / 8) * (g->H / 8);
+	const size_t nbs = (size_t)(g->H / 4) * (g->W / 8);
+	const int cols = (pic->pic_w + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2, rows = (pic->pic_h + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
+	const size_t o_tu = 0, o_coef = al16(o_tu + sizeof(h265r_tu_t) * (size_t)pic->n_tu);
+	const size_t o_map = al16(o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
+	const size_t o_bsv = al16(o_map + sizeof(int32_t) * units), o_bsh = al16(o_bsv + nbs);
+	const size_t o_sao = al16(o_bsh + nbs), total = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
+	/* per-block done flags + 2 counters */
+	const size_t sn = (size_t)pic->n_tu + 2;
+	if (sn > g->scratch_n) {
+		H265_CHECK(hipStreamSynchronize(g->st));
+		if (g->scratch) (void)hipFree(g->scratch);
+		H265_CHECK(hipMalloc((void **)&g->scratch, sizeof(int) * sn * 2));
+		g->scratch_n = sn * 2;
+	}
+	H265Gpu::Arena &a = g->ar[g->next];
+	g->next ^= 1;
+	H265_CHECK(hipEventSynchronize(a.used));
+	if (a.size < total) {
+		if (a.host) (void)hipHostFree(a.host);
+		if (a.dev) (void)hipFree(a.dev);
+		a.host = a.dev = nullptr;
+		H265_CHECK(hipHostMalloc((void **)&a.host, total, hipHostMallocDefault));
+		H265_CHECK(hipMalloc((void **)&a.dev, total));
+		a.size = total;
+	}
+	memcpy(a.host + o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
+	memcpy(a.host + o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
+	memcpy(a.host + o_map, pic->map, sizeof(int32_t) * units);
+	memcpy(a.host + o_bsv, pic->bs_v, nbs);
+	memcpy(a.host + o_bsh, pic->bs_h, nbs);
+	memcpy(a.host + o_sao, pic->sao, sizeof(h265r_sao_t) * (size_t)(cols * rows));
+	H265Args h;
+	h.tu = (const h265r_tu_t *)(a.dev + o_tu);
+	h.coef = (const int16_t *)(a.dev + o_coef);
+	h.map = (const int32_t *)(a.dev + o_map);
+	h.bs_v = a.dev + o_bsv;
+	h.bs_h = a.dev + o_bsh;
+	h.sao = (const h265r_sao_t *)(a.dev + o_sao);
+	h.frame = g->frames + (size_t)pic->slot * g->fsz;
+	h.copy = g->copy;
+	h.done = g->scratch;
+	h.counter = g->scratch + pic->n_tu;
+	h.err = g->err;
+	h.W = g->W;
+	h.H = g->H;
+	h.pic_w = pic->pic_w;
+	h.pic_h = pic->pic_h;
+	h.ctb_log2 = pic->ctb_log2;
+	h.n_tu = pic->n_tu;
+	h.flags = pic->flags;
+	h.beta_offset = pic->beta_offset;
+	h.tc_offset = pic->tc_offset;
+	h.cb_qp_offset = pic->cb_qp_offset;
+	h.cr_qp_offset = pic->cr_qp_offset;
+	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, g->st));
+	H265_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, g->st));
+	H265_CHECK(hipMemsetAsync(g->scratch, 0, sizeof(int) * sn, g->st));
+	const int k = (int)(g->pictures & 1);
+	H265_CHECK(hipEventRecord(g->t0[k], g->st));
+	if (pic->n_tu) {
+		const int grid = pic->n_tu < g->cus * 8 ? pic->n_tu : g->cus * 8;
+		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);
+		H265_CHECK(hipGetLastError());
+	}
+	if (pic->flags & H265R_PIC_DEBLOCK) {
+		const int nv = (g->H / 4) * (g->W / 8), nh = (g->H / 8) * (g->W / 4);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args, 0);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args, 1);
+		H265_CHECK(hipGetLastError());
+	}
+	if (pic->flags & (H265R_PIC_SAO_LUMA | H265R_PIC_SAO_CHROMA)) {
+		H265_CHECK(hipMemcpyAsync(g->copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, g->st));
+		const int nsa = pic->pic_w * pic->pic_h + (pic->pic_w >> 1) * (pic->pic_h >> 1) * 2;
+		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args);
+		H265_CHECK(hipGetLastError());
+	}
+	H265_CHECK(hipEventRecord(g->t1[k], g->st));
+	H265_CHECK(hipEventRecord(a.used, g->st));
+	/* the picture to its staging buffer, behind the kernels */
+	const int c = pic->slot;
+	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
+	if (!g->stg[c]) H265_CHECK(hipHostMalloc((void **)&g->stg[c], bytes, hipHostMallocDefault));
+	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, g->st));
+	H265_CHECK(hipEventRecord(g->ev[c], g->st));
+	g->pend[c] = true;
+	if (g->pictures > 0) { /* the previous picture's kernel time */
+		float ms = 0;
+		if (hipEventSynchronize(g->t1[k ^ 1]) == hipSuccess && hipEventElapsedTime(&ms, g->t0[k ^ 1], g->t1[k ^ 1]) == hipSuccess)
+			g->kernel_us += 1000.0 * ms;
+	}
+	g->pictures++;
+	return 0;
+}
+
+int h_sync(void *p, int slot)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g || slot < 0 || slot >= H265R_MAX_FRAMES) return -1;
+	if (!g->pend[slot]) return 0;
+	H265_CHECK(hipEventSynchronize(g->ev[slot]));
+	{
+		/* a block hand-off that never came (bounded spin): the sticky error word */
+		int err = 0;
+		H265_CHECK(hipMemcpy(&err, g->err, sizeof(int), hipMemcpyDeviceToHost));
+		if (err) {
+			fprintf(stderr, "m2dec_amd: H.265 block hand-off timed out on the GPU\n");
+			return -1;
+		}
+	}
+	const size_t ls = (size_t)g->W * g->H;
+	memcpy(g->caller[slot].luma, g->stg[slot], ls);
+	memcpy(g->caller[slot].chroma, g->stg[slot] + ls, ls / 2);
+	g->pend[slot] = false;
+	return 0;
+}
+
+void h_destroy(void *p)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g) return;
+	(void)hipSetDevice(g->dev);
+	(void)hipStreamSynchronize(g->st);
+	for (auto &a : g->ar) {
+		if (a.host) (void)hipHostFree(a.host);
+		if (a.dev) (void)hipFree(a.dev);
+		if (a.args) (void)hipFree(a.args);
+		if (a.used) (void)hipEventDestroy(a.used);
+	}
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
+		if (g->stg[i]) (void)hipHostFree(g->stg[i]);
+		if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
+	}
+	for (int i = 0; i < 2; ++i) {
+		if (g->t0[i]) (void)hipEventDestroy(g->t0[i]);
+		if (g->t1[i]) (void)hipEventDestroy(g->t1[i]);
+	}
+	if (g->scratch) (void)hipFree(g->scratch);
+	if (g->err) (void)hipFree(g->err);
+	if (g->frames) (void)hipFree(g->frames);
+	if (g->copy) (void)hipFree(g->copy);
+	(void)hipStreamDestroy(g->st);
+	delete g;
+}
+
+} // namespace
+
+extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
+{
+	int n = 0;
+	if (!out || hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return -1;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6) != 0) return -1;
+	H265Gpu *g = new H265Gpu();
+	g->dev = device;
+	g->cus = prop.multiProcessorCount;
+	if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking) != hipSuccess) {
+		delete g;
+		return -1;
+	}
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) (void)hipEventCreateWithFlags(&g->ev[i], hipEventDisableTiming);
+	for (int i = 0; i < 2; ++i) {
+		(void)hipEventCreate(&g->t0[i]);
+		(void)hipEventCreate(&g->t1[i]);
+	}
+	for (auto &a : g->ar) {
+		(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
+		(void)hipMalloc((void **)&a.args, sizeof(H265Args));
+	}
+	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess) {
+		h_destroy(g);
+		return -1;
+	}
+	out->self = g;
+	out->set_frames = h_set_frames;
+	out->submit = h_submit;
+	out->sync_frame = h_sync;
+	out->destroy = h_destroy;
+	return 0;
+}
+
 extern "C" int m2dec_amd_h265_hip_backend_create(h265r_backend_t *out, int device) { return h265_hip_backend_create(out, device); }
+
+/* kernel time of the pictures submitted so far (HIP events; the last picture's once it is synced) */
+extern "C" int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kernel_us, long *pictures)
+{
+	if (!be || !be->self || be->submit != h_submit) return -1;
+	H265Gpu *g = (H265Gpu *)be->self;
+	if (kernel_us) *kernel_us = g->kernel_us;
+	if (pictures) *pictures = g->pictures;
+	return 0;
+}

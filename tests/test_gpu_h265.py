@@ -1,0 +1,22 @@
+"""H.265 intra pictures reconstructed on gfx950 (m2dec_amd/csrc/hip/h265_hip.hip) through h265d_func, bit-exact
+against the goldens the CPU oracle produced (tests/golden/h265.json, tests/test_h265_cpu.py).  Parity
+against the reference itself is unpinned (no reference-produced H.265 output exists here)."""
+import json
+import os
+
+import pytest
+
+import m2dec_amd
+from test_h265_cpu import h265_stream
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "h265.json")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(GOLD))
+def test_hip_h265_matches_golden(built, name):
+    data = h265_stream(name)
+    md5s, err = m2dec_amd.decode_h265(data, device=0)
+    assert err == -2
+    assert md5s == GOLD[name]["md5"]

@@ -209,6 +209,11 @@ int m2dec_amd_h265_set_dump(const char *path);
 uint64_t m2dec_amd_h265_cabac_bins(const void *ctx);
 /* The gfx950 H.265 reconstruction back end (m2dec_amd/csrc/hip/h265_hip.hip). */
 int m2dec_amd_h265_hip_backend_create(h265r_backend_t *out, int device);
+/* Its kernel time (HIP events over the intra / deblocking / SAO launches of a picture, all but the last
+ * picture submitted), and the SURVEY.md §8d bytes of the pictures so far: R_pic (records uploaded) and
+ * F_write (1.5 W H each).  reset restarts the counts. */
+int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kernel_us, int64_t *timed_pictures,
+                              int64_t *record_bytes, int64_t *frame_bytes, int reset);
 
 /* ---- record traces (m2dec_amd/csrc/host/trace.c): a stream parsed once, records kept in memory */
 typedef struct m2dec_amd_trace m2dec_amd_trace_t;

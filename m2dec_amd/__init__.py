@@ -522,3 +522,37 @@ def decode_h265(data: bytes, backend: Optional[Backend265] = None, device: int =
     if errs:
         raise errs[0]
     return md5s, err.value
+
+
+class H265HipBackend:
+    """The gfx950 H.265 reconstruction (m2dec_amd_h265_hip_backend_create), borrowed by decode_h265 so that
+    its device buffers outlive one stream.  Raises if unavailable."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        L.m2dec_amd_h265_hip_backend_create.argtypes = [ctypes.POINTER(Backend265), ctypes.c_int]
+        L.m2dec_amd_h265_hip_backend_create.restype = ctypes.c_int
+        self.be = Backend265()
+        if L.m2dec_amd_h265_hip_backend_create(ctypes.byref(self.be), device) < 0:
+            raise RuntimeError(f"m2dec_amd: H.265 HIP back end unavailable on device {device} (needs a gfx950 GPU)")
+
+    def timing(self, reset: bool = False) -> dict:
+        L = lib()
+        i64 = ctypes.POINTER(ctypes.c_int64)
+        L.m2dec_amd_h265_hip_timing.argtypes = [ctypes.POINTER(Backend265), ctypes.POINTER(ctypes.c_double), i64, i64,
+                                                i64, ctypes.c_int]
+        us, n, rb, fb = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        L.m2dec_amd_h265_hip_timing(ctypes.byref(self.be), ctypes.byref(us), ctypes.byref(n), ctypes.byref(rb),
+                                    ctypes.byref(fb), int(reset))
+        return {"kernel_us": us.value, "pictures": n.value, "record_bytes": rb.value, "frame_bytes": fb.value}
+
+    def close(self) -> None:
+        if self.be.destroy:
+            ctypes.CFUNCTYPE(None, ctypes.c_void_p)(self.be.destroy)(self.be.self)
+            self.be.destroy = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -94,6 +94,21 @@ __device__ __forceinline__ uint8_t *plane_px(const H265Args &a, int plane, int c
 	return plane ? a.frame + (size_t)a.W * a.H + (size_t)y * a.W + (size_t)x * 2 + comp : a.frame + (size_t)y * a.W + x;
 }
 
+/* Block hand-off (cdna_hip_programming.md §6, Guideline 16; as recon_hip.hip's): a block's samples go out
+ * as 32-bit write-through stores (agent-scope relaxed atomics = sc1), drained before its done flag; a
+ * consumer polls the flags, then reads neighbour samples with sc1 loads — no L2 write-back / invalidate. */
+__device__ __forceinline__ int ld_px(const H265Args &a, int plane, int comp, int x, int y)
+{
+	const uint8_t *p = plane_px(a, plane, comp, x, y);
+	const uint32_t w = (uint32_t)__hip_atomic_load((gi32 *)((uintptr_t)p & ~(uintptr_t)3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	return (int)((w >> (8 * ((uintptr_t)p & 3))) & 255);
+}
+
+__device__ __forceinline__ void st_word(uint8_t *p, uint32_t v)
+{
+	__hip_atomic_store((gi32 *)p, (int)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 /* one block (wave-wide) */
 __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane)
 {
@@ -104,7 +119,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 	for (int c = 0; c < ncomp; ++c) {
 		int *pred = s.pred[c];
 		if (!(t.flags & H265R_TU_PRED)) {
-			for (int i = lane; i < n2; i += 64) pred[i] = *plane_px(a, t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
+			for (int i = lane; i < n2; i += 64) pred[i] = ld_px(a, t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
 			continue;
 		}
 		const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
@@ -119,7 +134,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 				const int k = clampi(i, lo, hi);
 				const int xx = k < corner ? -1 : (k == corner ? -1 : k - corner - 1);
 				const int yy = k < corner ? corner - 1 - k : -1;
-				v = *plane_px(a, t.plane, c, t.x + xx, t.y + yy);
+				v = ld_px(a, t.plane, c, t.x + xx, t.y + yy);
 			}
 			s.raw[i] = (int16_t)v;
 		}
@@ -244,12 +259,26 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 		}
 		__syncthreads();
 	}
-	/* ---- out */
-	for (int c = 0; c < ncomp; ++c)
-		for (int i = lane; i < n2; i += 64) {
-			const int x = i & (n - 1), y = i >> log2;
-			*plane_px(a, t.plane, c, t.x + x, t.y + y) = (uint8_t)clampi(s.pred[c][i], 0, 255);
+	/* ---- out: 32-bit write-through words (luma: 4 samples of a row; chroma: 2 CbCr pairs) */
+	if (luma) {
+		const int wpr = n >> 2;
+		for (int w = lane; w < n2 >> 2; w += 64) {
+			const int y = w / wpr, x = (w - y * wpr) * 4;
+			const int *q = s.pred[0] + y * n + x;
+			const uint32_t v = (uint32_t)clampi(q[0], 0, 255) | ((uint32_t)clampi(q[1], 0, 255) << 8) |
+			                   ((uint32_t)clampi(q[2], 0, 255) << 16) | ((uint32_t)clampi(q[3], 0, 255) << 24);
+			st_word(plane_px(a, 0, 0, t.x + x, t.y + y), v);
 		}
+	} else {
+		const int wpr = n >> 1;
+		for (int w = lane; w < n2 >> 1; w += 64) {
+			const int y = w / wpr, x = (w - y * wpr) * 2;
+			const int *cb = s.pred[0] + y * n + x, *cr = s.pred[1] + y * n + x;
+			const uint32_t v = (uint32_t)clampi(cb[0], 0, 255) | ((uint32_t)clampi(cr[0], 0, 255) << 8) |
+			                   ((uint32_t)clampi(cb[1], 0, 255) << 16) | ((uint32_t)clampi(cr[1], 0, 255) << 24);
+			st_word(plane_px(a, 1, 0, t.x + x, t.y + y), v);
+		}
+	}
 }
 
 __global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
@@ -287,11 +316,11 @@ __global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
 				if (__hip_atomic_load((gi32 *)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
 				__builtin_amdgcn_s_sleep(1);
 			}
-			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sample loads below the poll */
 		}
 		do_block(a, t, s, lane);
-		/* publish: the samples, then the flag */
-		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+		/* publish: the write-through sample stores drained, then the flag */
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__hip_atomic_store((gi32 *)&a.done[idx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
 }
@@ -465,6 +494,8 @@ struct H265Gpu {
 	hipEvent_t t0[2] = {}, t1[2] = {};
 	double kernel_us = 0;
 	long pictures = 0;
+	int64_t record_bytes = 0, frame_bytes = 0;
+	bool last_counted = true; /* the last submitted picture's kernel time is in kernel_us */
 };
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -569,6 +600,8 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.cb_qp_offset = pic->cb_qp_offset;
 	h.cr_qp_offset = pic->cr_qp_offset;
 	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, g->st));
+	g->record_bytes += (int64_t)total;
+	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
 	H265_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, g->st));
 	H265_CHECK(hipMemsetAsync(g->scratch, 0, sizeof(int) * sn, g->st));
 	const int k = (int)(g->pictures & 1);
@@ -599,11 +632,12 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, g->st));
 	H265_CHECK(hipEventRecord(g->ev[c], g->st));
 	g->pend[c] = true;
-	if (g->pictures > 0) { /* the previous picture's kernel time */
+	if (!g->last_counted) { /* the previous picture's kernel time */
 		float ms = 0;
 		if (hipEventSynchronize(g->t1[k ^ 1]) == hipSuccess && hipEventElapsedTime(&ms, g->t0[k ^ 1], g->t1[k ^ 1]) == hipSuccess)
 			g->kernel_us += 1000.0 * ms;
 	}
+	g->last_counted = false;
 	g->pictures++;
 	return 0;
 }
@@ -696,12 +730,28 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 
 extern "C" int m2dec_amd_h265_hip_backend_create(h265r_backend_t *out, int device) { return h265_hip_backend_create(out, device); }
 
-/* kernel time of the pictures submitted so far (HIP events; the last picture's once it is synced) */
-extern "C" int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kernel_us, long *pictures)
+/* kernel time (HIP events, all but the last picture submitted), pictures, and the §8d algorithmic bytes of
+ * the pictures so far: R_pic (records uploaded) and F_write (1.5 W H each); reset zeroes them */
+extern "C" int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kernel_us, int64_t *timed_pictures,
+                                         int64_t *record_bytes, int64_t *frame_bytes, int reset)
 {
 	if (!be || !be->self || be->submit != h_submit) return -1;
 	H265Gpu *g = (H265Gpu *)be->self;
+	(void)hipStreamSynchronize(g->st);
+	if (!g->last_counted && g->pictures > 0) {
+		const int k = (int)((g->pictures - 1) & 1);
+		float ms = 0;
+		if (hipEventElapsedTime(&ms, g->t0[k], g->t1[k]) == hipSuccess) g->kernel_us += 1000.0 * ms;
+		g->last_counted = true;
+	}
 	if (kernel_us) *kernel_us = g->kernel_us;
-	if (pictures) *pictures = g->pictures;
+	if (timed_pictures) *timed_pictures = g->pictures;
+	if (record_bytes) *record_bytes = g->record_bytes;
+	if (frame_bytes) *frame_bytes = g->frame_bytes;
+	if (reset) {
+		g->kernel_us = 0;
+		g->record_bytes = g->frame_bytes = 0;
+		g->pictures = 0;
+	}
 	return 0;
 }

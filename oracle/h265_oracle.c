@@ -382,6 +382,39 @@ static void sao(const h265r_picture_t *pic, uint8_t *luma, uint8_t *chroma)
 	free(copy);
 }
 
+/* ------------------------------------------------------------------ the block dependency graph (analysis) */
+static int64_t g_chain[2]; /* the longest chain of blocks (the GPU kernel's critical path), blocks */
+
+int64_t h265_oracle_chain(int which) { return g_chain[which & 1]; }
+
+static void chain_depth(const h265r_picture_t *pic)
+{
+	int *lv = (int *)calloc((size_t)pic->n_tu + 1, sizeof(int));
+	int best = 0;
+	if (!lv) return;
+	for (int i = 0; i < pic->n_tu; ++i) {
+		const h265r_tu_t *t = &pic->tu[i];
+		const int n = 1 << t->log2;
+		const int at = t->avail_top > 2 * n ? 2 * n : t->avail_top, al = t->avail_left > 2 * n ? 2 * n : t->avail_left;
+		const int mw = t->plane ? pic->width / 8 : pic->width / 4;
+		const int32_t *map = pic->map + (t->plane ? (size_t)(pic->width / 4) * (size_t)(pic->height / 4) : 0);
+		int m = 0;
+		for (int k = 0; at > 0 && k < (at + 3) / 4; ++k) {
+			const int j = map[(size_t)((t->y >> 2) - 1) * (size_t)mw + (size_t)((t->x >> 2) + k)];
+			if (j >= 0 && j < i && lv[j] > m) m = lv[j];
+		}
+		for (int k = 0; al > 0 && k < (al + 3) / 4; ++k) {
+			const int j = map[(size_t)((t->y >> 2) + k) * (size_t)mw + (size_t)((t->x >> 2) - 1)];
+			if (j >= 0 && j < i && lv[j] > m) m = lv[j];
+		}
+		lv[i] = m + 1;
+		if (lv[i] > best) best = lv[i];
+	}
+	g_chain[0] = best;
+	g_chain[1] = pic->n_tu;
+	free(lv);
+}
+
 /* ------------------------------------------------------------------ the picture */
 void h265_oracle_recon_picture(const h265r_picture_t *pic, const m2d_frame_t *frames, int nframes)
 {
@@ -393,6 +426,7 @@ void h265_oracle_recon_picture(const h265r_picture_t *pic, const m2d_frame_t *fr
 	if (pic->slot < 0 || pic->slot >= nframes) return;
 	uint8_t *luma = frames[pic->slot].luma, *chroma = frames[pic->slot].chroma;
 	const int W = pic->width;
+	chain_depth(pic);
 	int pred[32 * 32], res[32 * 32];
 	for (int i = 0; i < pic->n_tu; ++i) {
 		const h265r_tu_t *t = &pic->tu[i];

@@ -147,9 +147,11 @@ int main(int argc, char **argv)
 	case MODE_MPEG2:
 		m2dec_amd_decode_table(m2d_func, 0, data, (size_t)len, dpb, emptify, skip, write_frame, &w, &err);
 		break;
+	case MODE_H265: /* M2Decoder MODE_H265 (m2decoder.h:180-182): reconstructed on GPU 0 */
+		m2dec_amd_decode_h265(data, (size_t)len, NULL, 0, emptify, write_frame, &w, &err);
+		break;
 	default:
-		fprintf(stderr, "h264dec: %s input is not supported by this library\n",
-		        codec == MODE_MPEG2PS ? "MPEG-2 program stream" : "H.265");
+		fprintf(stderr, "h264dec: MPEG-2 program stream input is not supported by this library\n");
 		err = -1;
 		break;
 	}

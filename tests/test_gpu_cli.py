@@ -48,3 +48,15 @@ def test_cli_mpeg2_c1(built, tmp_path):
     r = subprocess.run([APP, "-O", str(src)], cwd=tmp_path, capture_output=True, timeout=300)
     assert r.returncode == 255, r.stderr  # MPEG-2 decode_picture ends with -1 (mpeg2.cpp:1583-1604)
     assert (tmp_path / "c1.out").read_bytes() == b"".join(m.encode() + b"\r\n" for m in GOLD["c1_480p_s1"]["md5"])
+
+
+@pytest.mark.gpu
+def test_cli_h265(built, tmp_path):
+    """`h264dec -O x.265` (M2Decoder MODE_H265 chosen by the extension, h264dec.cpp:153-154): the 1080p H.265
+    intra stream reconstructed on the GPU, its .out equal to the oracle's goldens."""
+    from tests.test_h265_cpu import GOLD as G265, h265_stream
+    src = tmp_path / "c_h265.265"
+    src.write_bytes(h265_stream("c_h265_1080p_s1"))
+    r = subprocess.run([APP, "-O", str(src)], cwd=tmp_path, capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "c_h265.out").read_bytes() == b"".join(m.encode() + b"\r\n" for m in G265["c_h265_1080p_s1"]["md5"])

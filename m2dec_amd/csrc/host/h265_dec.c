@@ -443,24 +443,38 @@ static void parse_slice_header(perr_t *e, h264_bits_t *b, const h265_sps_t *s, c
 }
 
 /* ------------------------------------------------------------------ CABAC (9.3.4.3) */
+/* The engine keeps the spec's 9-bit ivlOffset as the top bits of a 64-bit window: value == win >> cnt,
+ * with cnt look-ahead bits below it, refilled a byte at a time (bytes past the end read as 0, as the
+ * reference's bit reader does).  Renormalisation is one count-leading-zeros instead of a bit loop. */
 typedef struct {
 	const uint8_t *p, *end;
-	uint32_t range, value;
-	int bitpos; /* bits of *p still unread (8..1) */
+	uint64_t win;
+	uint32_t range;
+	int cnt;
 	uint8_t ctx[H265_NUM_CTX];
 	uint64_t bins;
 } cab_t;
 
-static inline int cab_bit(cab_t *c)
+static inline void cab_refill(cab_t *c)
 {
-	int v;
-	if (c->p >= c->end) return 0;
-	v = (*c->p >> (c->bitpos - 1)) & 1;
-	if (--c->bitpos == 0) {
-		c->p++;
-		c->bitpos = 8;
+	while (c->cnt <= 46) { /* value (9 bits) + look-ahead stays within 63 bits */
+		c->win = (c->win << 8) | (c->p < c->end ? *c->p++ : 0u);
+		c->cnt += 8;
 	}
-	return v;
+}
+
+/* context state transitions (9.3.4.3.2.2) for a context byte (pStateIdx << 1 | valMps) after an MPS (0) or
+ * an LPS (1), so that the decision below needs no data-dependent branch */
+static uint8_t cab_next[128][2];
+static pthread_once_t cab_once = PTHREAD_ONCE_INIT;
+
+static void cab_build_next(void)
+{
+	for (int v = 0; v < 128; ++v) {
+		const int s = v >> 1, mps = v & 1;
+		cab_next[v][0] = (uint8_t)(((s + (s < 62)) << 1) | mps);
+		cab_next[v][1] = (uint8_t)((h264_trans_idx_lps[s] << 1) | (s == 0 ? !mps : mps));
+	}
 }
 
 static void cab_init_ctx(cab_t *c, int init_type, int qp)
@@ -475,43 +489,43 @@ static void cab_init_ctx(cab_t *c, int init_type, int qp)
 
 static void cab_start(cab_t *c, const uint8_t *p, const uint8_t *end)
 {
+	pthread_once(&cab_once, cab_build_next);
 	c->p = p;
 	c->end = end;
-	c->bitpos = 8;
 	c->range = 510;
-	c->value = 0;
-	for (int i = 0; i < 9; ++i) c->value = (c->value << 1) | (uint32_t)cab_bit(c);
+	c->win = 0;
+	c->cnt = -9; /* the first 9 bits are ivlOffset itself */
+	cab_refill(c);
 }
 
 static inline int cab_decision(cab_t *c, int ci)
 {
-	const int s = c->ctx[ci] >> 1, mps = c->ctx[ci] & 1;
-	const uint32_t lps = h264_range_lps[s][(c->range >> 6) & 3];
-	int bin;
+	const int v = c->ctx[ci];
+	const uint32_t lps = h264_range_lps[v >> 1][(c->range >> 6) & 3];
+	const uint32_t rm = c->range - lps;
+	const uint64_t scaled = (uint64_t)rm << c->cnt;
+	const int is_lps = c->win >= scaled;
+	const uint64_t m = -(uint64_t)is_lps;
+	int n;
 	c->bins++;
-	c->range -= lps;
-	if (c->value < c->range) {
-		bin = mps;
-		c->ctx[ci] = (uint8_t)(((s + (s < 62)) << 1) | mps);
-	} else {
-		c->value -= c->range;
-		c->range = lps;
-		bin = !mps;
-		c->ctx[ci] = (uint8_t)((h264_trans_idx_lps[s] << 1) | (s == 0 ? !mps : mps));
-	}
-	while (c->range < 256) {
-		c->range <<= 1;
-		c->value = (c->value << 1) | (uint32_t)cab_bit(c);
-	}
-	return bin;
+	c->win -= scaled & m;
+	c->range = rm ^ ((rm ^ lps) & (uint32_t)m);
+	c->ctx[ci] = cab_next[v][is_lps];
+	n = __builtin_clz(c->range) - 23; /* shifts until range >= 256 */
+	c->range <<= n;
+	c->cnt -= n;
+	if (c->cnt < 16) cab_refill(c);
+	return (v & 1) ^ is_lps;
 }
 
 static inline int cab_bypass(cab_t *c)
 {
+	uint64_t r;
 	c->bins++;
-	c->value = (c->value << 1) | (uint32_t)cab_bit(c);
-	if (c->value >= c->range) {
-		c->value -= c->range;
+	if (--c->cnt < 16) cab_refill(c);
+	r = (uint64_t)c->range << c->cnt;
+	if (c->win >= r) {
+		c->win -= r;
 		return 1;
 	}
 	return 0;
@@ -528,10 +542,10 @@ static inline uint32_t cab_bypass_n(cab_t *c, int n)
 static inline int cab_terminate(cab_t *c)
 {
 	c->range -= 2;
-	if (c->value >= c->range) return 1;
+	if (c->win >= ((uint64_t)c->range << c->cnt)) return 1;
 	if (c->range < 256) {
 		c->range <<= 1;
-		c->value = (c->value << 1) | (uint32_t)cab_bit(c);
+		if (--c->cnt < 16) cab_refill(c);
 	}
 	return 0;
 }

@@ -137,6 +137,10 @@ typedef struct m2r_backend {
 	int (*sync_frame)(void *self, int slot);
 	void (*destroy)(void *self);
 	int (*bind)(void *self, int vid, int slot);
+	/* optional (ABI revision 4): submit may hold pictures back to launch several at once; flush launches
+	 * every held one.  The decoder calls it after the last submit of a burst (bind, sync_frame,
+	 * set_frames and acquire flush implicitly).  NULL: every submit is launched as it comes. */
+	int (*flush)(void *self);
 } m2r_backend_t;
 
 /* ---------------------------------------------------------------- MPEG-1/2 (m2d_func)

@@ -50,11 +50,12 @@ typedef struct {
 } m2dec_amd_stats_t;
 
 /* ABI revision of the structs in this header and m2d_recon.h.  3: m2r_backend_t gained `bind` (decode
- * ahead) and m2dec_amd_stats_t grew to its current size.  A caller compiled against another revision
+ * ahead) and m2dec_amd_stats_t grew to its current size; 4: m2r_backend_t gained `flush` (several
+ * pictures per launch).  A caller compiled against another revision
  * checks m2dec_amd_abi_version() before passing either struct; m2dec_amd_h264_set_backend2 accepts an
  * older (smaller) m2r_backend_t by size, and m2dec_amd_stats_size() is the size every stats pointer
  * must have room for. */
-#define M2DEC_AMD_ABI_VERSION 3
+#define M2DEC_AMD_ABI_VERSION 4
 int m2dec_amd_abi_version(void);
 size_t m2dec_amd_stats_size(void);
 /* 0 if the host CPU lacks the x86-64-v3 features the host library is built for (decoder inits then
@@ -176,6 +177,10 @@ int m2dec_amd_m2v_use_gpu(void *ctx, int device);
 uint64_t m2dec_amd_m2v_mc_out_of_frame(const void *ctx);
 /* the two counters of the calling thread's last whole-stream m2d_func decode (decode_table* / decode_m2v) */
 void m2dec_amd_m2v_last_checks(uint64_t *clip_violations, uint64_t *mc_out_of_frame);
+/* GPU MPEG-2 back end, process-wide: HIP-event time of its k_m2v launches, the pictures, and their
+ * SURVEY.md §8d algorithmic bytes (frame written + records read + one reference byte per predicted
+ * sample per direction) since the last reset; pictures of a destroyed back end are all counted. */
+int m2dec_amd_m2v_hip_timing(double *kernel_us, int64_t *pictures, int64_t *bytes, int reset);
 /* VLC probes for the table tests: one codeword at the MSB end of bits32.  DCT (table 0 = B.14,
  * 1 = B.15): length incl. the sign bit, run (-1: EOB / escape), sign-folded level (2|l| + s).
  * Plain tables (0: macroblock_address_increment after its leading 0, 1 / 2: dct_dc_size luma /

@@ -39,10 +39,10 @@ class Info(ctypes.Structure):
 
 
 class Backend(ctypes.Structure):
-    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind."""
+    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind/flush."""
     _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("acquire", ctypes.c_void_p),
                 ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p),
-                ("bind", ctypes.c_void_p)]
+                ("bind", ctypes.c_void_p), ("flush", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -375,6 +375,15 @@ def decode_m2v(data: bytes, device: Optional[int] = None, emptify: bool = False)
     if r == -3:
         raise RuntimeError(f"m2dec_amd: MPEG-2 decode on device {device} failed")
     return md5s
+
+
+def m2v_hip_timing(reset: bool = False) -> dict:
+    """Process-wide timing of the GPU MPEG-2 back end since the last reset: HIP-event time of its k_m2v
+    launches, the pictures, and their SURVEY.md §8d algorithmic bytes."""
+    L = lib()
+    us, n, b = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+    L.m2dec_amd_m2v_hip_timing(ctypes.byref(us), ctypes.byref(n), ctypes.byref(b), int(reset))
+    return {"kernel_us": us.value, "pictures": n.value, "bytes": b.value}
 
 
 class H264Decoder:

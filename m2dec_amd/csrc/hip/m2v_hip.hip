@@ -22,6 +22,7 @@
  * caller's thread — the same ownership rule as the H.264 back end (runtime.hip).
  */
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -250,9 +251,30 @@ struct M2vGpu {
 		size_t size = 0;
 		M2vArgs *args = nullptr;
 		hipEvent_t used = nullptr;
+		hipEvent_t t0 = nullptr, t1 = nullptr; /* timing: around the launch that used this arena last */
+		bool timed = false;
 	} ar[2];
 	int next = 0;
 };
+
+/* Process-wide kernel timing of the MPEG-2 back end (bench.py end_to_end_m2v): HIP-event time of the
+ * k_m2v launches and SURVEY.md §8d algorithmic bytes of their pictures (F_write 1.5 W H, the records and
+ * coefficients read, one reference byte per predicted sample per direction). */
+struct M2vTiming {
+	std::mutex mu;
+	double kernel_us = 0;
+	int64_t pictures = 0, bytes = 0;
+} g_m2v_tm;
+
+void arena_account(M2vGpu::Arena &a)
+{
+	float ms = 0;
+	if (!a.timed) return;
+	a.timed = false;
+	if (hipEventElapsedTime(&ms, a.t0, a.t1) != hipSuccess) return;
+	std::lock_guard<std::mutex> lk(g_m2v_tm.mu);
+	g_m2v_tm.kernel_us += ms * 1e3;
+}
 
 int arena_fit(M2vGpu *g, M2vGpu::Arena &a, size_t need)
 {
@@ -282,6 +304,8 @@ extern "C" void *m2v_hip_create(int device)
 	for (int i = 0; i < M2V_MAX_FRAMES; ++i) (void)hipEventCreateWithFlags(&g->ev[i], hipEventDisableTiming);
 	for (auto &a : g->ar) {
 		(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
+		(void)hipEventCreate(&a.t0);
+		(void)hipEventCreate(&a.t1);
 		(void)hipMalloc((void **)&a.args, sizeof(M2vArgs));
 	}
 	return g;
@@ -328,6 +352,7 @@ extern "C" int m2v_hip_submit(void *p, const m2v_picture_t *pic)
 	M2vGpu::Arena &a = g->ar[g->next];
 	g->next ^= 1;
 	M2V_CHECK(hipEventSynchronize(a.used)); /* the launch before last is done with this arena */
+	arena_account(a);
 	const size_t rb = sizeof(m2v_mb_t) * (size_t)pic->n_mbs, cb = sizeof(int16_t) * (size_t)pic->n_coef;
 	if (arena_fit(g, a, rb + cb + 256) < 0) return -1;
 	memcpy(a.host, pic->mb, rb);
@@ -346,9 +371,22 @@ extern "C" int m2v_hip_submit(void *p, const m2v_picture_t *pic)
 	h.n_mbs = pic->n_mbs;
 	M2V_CHECK(hipMemcpyAsync(a.dev, a.host, rb + cb, hipMemcpyHostToDevice, g->st));
 	M2V_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, g->st));
+	M2V_CHECK(hipEventRecord(a.t0, g->st));
 	hipLaunchKernelGGL(k_m2v, dim3(pic->n_mbs), dim3(64), 0, g->st, (const M2vArgs *)a.args);
 	M2V_CHECK(hipGetLastError());
+	M2V_CHECK(hipEventRecord(a.t1, g->st));
 	M2V_CHECK(hipEventRecord(a.used, g->st));
+	a.timed = true;
+	{
+		int64_t refb = 0;
+		for (int i = 0; i < pic->n_mbs; ++i) {
+			const unsigned f = pic->mb[i].flags;
+			refb += 384 * (((f & M2V_REC_FWD) != 0) + ((f & M2V_REC_BWD) != 0) + ((f & M2V_REC_COPY) != 0));
+		}
+		std::lock_guard<std::mutex> lk(g_m2v_tm.mu);
+		g_m2v_tm.pictures++;
+		g_m2v_tm.bytes += (int64_t)(rb + cb) + refb + (int64_t)g->W * g->H * 3 / 2;
+	}
 	/* the picture to its staging buffer, behind the kernel */
 	const int c = pic->cur;
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
@@ -380,6 +418,9 @@ extern "C" void m2v_hip_destroy(void *p)
 	(void)hipSetDevice(g->dev);
 	(void)hipStreamSynchronize(g->st);
 	for (auto &a : g->ar) {
+		arena_account(a);
+		if (a.t0) (void)hipEventDestroy(a.t0);
+		if (a.t1) (void)hipEventDestroy(a.t1);
 		if (a.host) (void)hipHostFree(a.host);
 		if (a.dev) (void)hipFree(a.dev);
 		if (a.args) (void)hipFree(a.args);
@@ -392,4 +433,19 @@ extern "C" void m2v_hip_destroy(void *p)
 	if (g->frames) (void)hipFree(g->frames);
 	(void)hipStreamDestroy(g->st);
 	delete g;
+}
+
+/* kernel time and algorithmic bytes of the k_m2v launches since the last reset (destroyed back ends
+ * included; a live one's last two launches are counted when their arenas are reused or it is destroyed) */
+extern "C" int m2dec_amd_m2v_hip_timing(double *kernel_us, int64_t *pictures, int64_t *bytes, int reset)
+{
+	std::lock_guard<std::mutex> lk(g_m2v_tm.mu);
+	if (kernel_us) *kernel_us = g_m2v_tm.kernel_us;
+	if (pictures) *pictures = g_m2v_tm.pictures;
+	if (bytes) *bytes = g_m2v_tm.bytes;
+	if (reset) {
+		g_m2v_tm.kernel_us = 0;
+		g_m2v_tm.pictures = g_m2v_tm.bytes = 0;
+	}
+	return 0;
 }

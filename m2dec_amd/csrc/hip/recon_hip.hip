@@ -2106,8 +2106,8 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
  *   phase B: deblocks both rows on waves 0..2 (loader / filter / storer, see deblock_pair) and
  *            finally flags the rows final for the motion compensation of later pictures.
  * Every wait points at a lower block index of the same launch or at an earlier launch, so FIFO
- * queues and in-order dispatch cannot deadlock; the host keeps at most NSTREAMS pictures in flight
- * so that they all fit on the device.
+ * queues and in-order dispatch cannot deadlock; the host reserves every launch's workgroups from a
+ * device-wide budget (SlotBudget, runtime.hip) so that all launches in flight fit on the device.
  */
 /* batch launches: before writing its slot, wait until the earlier batch pictures that read the
  * slot's previous content have finished their motion compensation, and the previous content's
@@ -2253,11 +2253,12 @@ __global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_batch(const PictureAr
 	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
 }
 
-/* the decode path's launch (one picture per launch, h264d_func): the same blocks as k_batch under
+/* the decode path's launch (up to BMAX pictures per launch, h264d_func): the same blocks as k_batch under
  * its own name, so that rocprofv3 reports the decode path and the trace replay separately */
-__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_picture(const PictureArgs *pic)
+__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_picture(const PictureArgs *pics, int bpp)
 {
-	picture_block(*pic, blockIdx.x, g_lds);
+	const int p = blockIdx.x / bpp;
+	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
 }
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)

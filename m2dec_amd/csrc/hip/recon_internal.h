@@ -85,7 +85,7 @@ struct PictureArgs {
 
 /* a batch of pictures in decode order, picture p owning blocks [p * bpp, (p + 1) * bpp) */
 __global__ void k_batch(const PictureArgs *pics, int bpp);
-__global__ void k_picture(const PictureArgs *pic);
+__global__ void k_picture(const PictureArgs *pics, int bpp);
 
 /* workgroups of one picture: persistent inter workers + one per pair of MB rows */
 static inline int picture_blocks(int inter_workers, int Hmb) { return inter_workers + (Hmb + 1) / 2; }

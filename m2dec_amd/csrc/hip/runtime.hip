@@ -46,7 +46,13 @@ static int dbg_knob(const char *name)
 	return v && atoi(v);
 }
 
-const int NSTREAMS = 3; /* pictures in flight: all of their k_inter + k_rows workgroups fit on the device */
+#ifndef M2DEC_NSTREAMS
+#define M2DEC_NSTREAMS 3
+#endif
+const int NSTREAMS = M2DEC_NSTREAMS; /* launches in flight: one hardware queue each, the copy stream the fourth */
+const int BMAX = 4; /* at most this many pictures per decode-path launch: the back end holds submitted
+                     * pictures back until the decoder flushes (the end of a burst of submits) or it holds
+                     * max_held, so that pictures parsed together run in one launch */
 
 /* Forward-progress invariant of the decode path.  A picture's workgroups spin on its references' row
  * flags, written by EARLIER launches that may sit on other HIP streams (hardware queues), and the
@@ -254,9 +260,9 @@ struct Sched {
 	size_t fsz = 0;
 	uint8_t *frames = nullptr; /* device frame pool [nslots] x fsz */
 	hipStream_t st[NSTREAMS] = {}; /* per in-flight index: uploads, k_picture, downloads */
-	int *prog = nullptr;       /* [NSTREAMS][SCR_WORDS(Hmb, Wmb)] per-launch scratch words */
-	PictureArgs *pargs = nullptr; /* [NSTREAMS] kernel arguments of the per-picture launches */
-	uint8_t *hand = nullptr;   /* [NSTREAMS][Hmb * Wmb * (HBI_BYTES + HBD_BYTES)] */
+	int *prog = nullptr;       /* [NSTREAMS] x (completion counters [2 BMAX], scratch [BMAX][SCR_WORDS]) */
+	PictureArgs *pargs = nullptr; /* [NSTREAMS][BMAX] kernel arguments of the decode-path launches */
+	uint8_t *hand = nullptr;   /* [NSTREAMS * BMAX][hand_bytes()] hand-off records */
 	int *err = nullptr;
 	unsigned long long *rowflag = nullptr; /* [ROWFLAG_N][Hmb]: ROWFLAG(seq, MB columns final) per picture row */
 	int seq = 0;               /* pictures launched */
@@ -308,7 +314,7 @@ struct Sched {
 		if (prog && (width / 16 != Wmb || height / 16 != Hmb)) {
 			batch_free();
 			g_dev.give(dev, prog, prog_bytes());
-			g_dev.give(dev, hand, hand_bytes() * NSTREAMS);
+			g_dev.give(dev, hand, hand_bytes() * NSTREAMS * BMAX);
 			g_dev.give(dev, rowflag, rowflag_bytes());
 			prog = nullptr;
 			hand = nullptr;
@@ -321,14 +327,14 @@ struct Sched {
 		fsz = nfsz;
 		if (!prog) {
 			CHECK(g_dev.take(dev, (void **)&prog, prog_bytes()));
-			if (!pargs) CHECK(hipMalloc(&pargs, sizeof(PictureArgs) * NSTREAMS));
-			CHECK(g_dev.take(dev, (void **)&hand, hand_bytes() * NSTREAMS));
+			if (!pargs) CHECK(hipMalloc(&pargs, sizeof(PictureArgs) * NSTREAMS * BMAX));
+			CHECK(g_dev.take(dev, (void **)&hand, hand_bytes() * NSTREAMS * BMAX));
 			CHECK(g_dev.take(dev, (void **)&rowflag, rowflag_bytes()));
 		}
 		CHECK(hipMemsetAsync(rowflag, 0, rowflag_bytes(), st[0]));
 		/* the I-picture hand-off words carry a tag derived from seq, which restarts here: no word of an
 		 * earlier picture (or decoder) may be left holding a tag a new picture will use */
-		CHECK(hipMemsetAsync(hand, 0, hand_bytes() * NSTREAMS, st[0]));
+		CHECK(hipMemsetAsync(hand, 0, hand_bytes() * NSTREAMS * BMAX, st[0]));
 		if (bt.hand) CHECK(hipMemsetAsync(bt.hand, 0, hand_bytes() * (size_t)bt.cap, st[0]));
 		CHECK(hipStreamSynchronize(st[0]));
 		seq = 0;
@@ -358,7 +364,8 @@ struct Sched {
 	}
 
 	size_t hand_bytes() const { return (size_t)Hmb * Wmb * (HBI_BYTES + HBD_BYTES) + (size_t)Hmb * NSEG(Wmb) * 8 * HBP_BYTES; }
-	size_t prog_bytes() const { return sizeof(int) * SCR_WORDS(Hmb, Wmb) * NSTREAMS; }
+	size_t stream_words() const { return 2 * BMAX + (size_t)BMAX * SCR_WORDS(Hmb, Wmb); }
+	size_t prog_bytes() const { return sizeof(int) * stream_words() * NSTREAMS; }
 	size_t rowflag_bytes() const { return sizeof(unsigned long long) * ROWFLAG_N * (size_t)Hmb; }
 
 	hipEvent_t next_event()
@@ -374,9 +381,23 @@ struct Sched {
 	 * references' row flags on the device, so it overlaps their deblocking. */
 	int begin(int slot, uint64_t refs)
 	{
-		(void)refs;
-		int k = rr;
+		const int k = pick();
+		return waits(k, slot, refs) < 0 ? -1 : k;
+	}
+
+	int pick()
+	{
+		const int k = rr;
 		rr = (rr + 1) % NSTREAMS;
+		return k;
+	}
+
+	/* on stream k, before a picture writing `slot` (launched in a later call on k): the waits for the
+	 * launches that read or wrote the slot's previous content (pictures of the same launch are ordered on
+	 * the device instead: war / war_writer) */
+	int waits(int k, int slot, uint64_t refs)
+	{
+		(void)refs;
 		hipStream_t s = st[k];
 		for (hipEvent_t e : readers[slot]) CHECK(hipStreamWaitEvent(s, e, 0));
 		if (slot_write[slot]) CHECK(hipStreamWaitEvent(s, slot_write[slot], 0));
@@ -384,53 +405,80 @@ struct Sched {
 			for (int i = 0; i < 64; ++i)
 				if (((refs >> i) & 1) && slot_write[i]) CHECK(hipStreamWaitEvent(st[k], slot_write[i], 0));
 		if (dbg_knob("M2DEC_AMD_SYNC")) CHECK(hipDeviceSynchronize());
-		return k;
+		return 0;
 	}
 
-	/* one picture = one k_batch launch of one picture on stream k; tev (optional): [0] recorded after it; inter_done: the event
-	 * after which the picture's reference reads are over */
-	int launch(int k, const PicJob &j, hipEvent_t *tev, hipEvent_t *inter_done)
+	/* n (<= BMAX) pictures in decode order = one k_picture launch on stream k (waits() done for each);
+	 * tev (optional): [0] recorded after it; inter_done: the event after which the pictures' reference
+	 * reads are over.  Inside the launch a picture that overwrites a slot an earlier one of the launch
+	 * read or wrote waits for it on the device (war / war_writer on the completion counters), as in a
+	 * replay batch; workgroups are dispatched in block order, so every such wait points backwards. */
+	int launch_multi(int k, const PicJob *jobs, int n, hipEvent_t *tev, hipEvent_t *inter_done)
 	{
+		if (n < 1 || n > BMAX) return -1;
 		hipStream_t s = st[k];
-		PictureArgs a;
-		memset(&a, 0, sizeof(a));
-		a.mbs = j.r.mb;
-		a.inters = j.r.it;
-		a.slices = j.r.sl;
-		a.pool = j.r.coef;
-		a.dbk = j.r.dbk;
-		a.frames = frames;
-		a.fsz = fsz;
-		a.W = W;
-		a.H = H;
-		a.Wmb = Wmb;
-		a.Hmb = Hmb;
-		a.slot = j.slot;
-		a.seq = seq++;
-		a.n_inter = j.n_inter;
-		a.n_intra = j.n_intra;
-		a.inter_workers = inter_grid;
-		a.row_wgs = row_wgs;
-		a.scratch = prog + (size_t)k * SCR_WORDS(Hmb, Wmb);
-		a.hbi = hand + (size_t)k * hand_bytes();
-		a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
-		a.hbp = a.hbd + (size_t)Hmb * Wmb * HBD_BYTES;
-		a.rowflag = rowflag;
-		a.err = err;
-		a.ss = slot_seq;
-		CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int) * SCR_WORDS(Hmb, Wmb), s));
-		/* the arguments go to device memory (pageable source: staged by the copy call) so that the kernel
-		 * reads them through a pointer, as in batch launches */
-		CHECK(hipMemcpyAsync(pargs + k, &a, sizeof(a), hipMemcpyHostToDevice, s));
+		PictureArgs ha[BMAX];
+		if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "launch_multi: stream %d, %d pictures, seq %d\n", k, n, seq);
+		int *words = prog + (size_t)k * stream_words();
+		int last_writer[64];
+		int rd[64][BMAX], nrd[64];
+		for (int i = 0; i < 64; ++i) last_writer[i] = -1, nrd[i] = 0;
+		for (int p = 0; p < n; ++p) {
+			const PicJob &j = jobs[p];
+			PictureArgs &a = ha[p];
+			memset(&a, 0, sizeof(a));
+			a.mbs = j.r.mb;
+			a.inters = j.r.it;
+			a.slices = j.r.sl;
+			a.pool = j.r.coef;
+			a.dbk = j.r.dbk;
+			a.frames = frames;
+			a.fsz = fsz;
+			a.W = W;
+			a.H = H;
+			a.Wmb = Wmb;
+			a.Hmb = Hmb;
+			a.slot = j.slot;
+			a.seq = seq++;
+			a.n_inter = j.n_inter;
+			a.n_intra = j.n_intra;
+			a.inter_workers = inter_grid;
+			a.row_wgs = row_wgs;
+			a.scratch = words + 2 * BMAX + (size_t)p * SCR_WORDS(Hmb, Wmb);
+			a.hbi = hand + ((size_t)k * BMAX + p) * hand_bytes();
+			a.hbd = a.hbi + (size_t)Hmb * Wmb * HBI_BYTES;
+			a.hbp = a.hbd + (size_t)Hmb * Wmb * HBD_BYTES;
+			a.rowflag = rowflag;
+			a.err = err;
+			a.ss = slot_seq;
+			a.fin = words;
+			a.pidx = p;
+			a.didx = p;
+			a.n_war = nrd[j.slot];
+			for (int i = 0; i < a.n_war; ++i) a.war[i] = rd[j.slot][i];
+			a.war_writer = last_writer[j.slot];
+			nrd[j.slot] = 0;
+			last_writer[j.slot] = p;
+			for (int r = 0; r < 64; ++r)
+				if ((j.refs >> r) & 1) rd[r][nrd[r]++] = p;
+			slot_seq.s[j.slot] = a.seq + 1;
+			tm.inter_launches += j.n_inter ? 1 : 0;
+			tm.intra_launches += j.n_intra ? 1 : 0;
+			tm.deblock_launches++;
+		}
+		hoist_intra(ha, n);
+		CHECK(hipMemsetAsync(words, 0, sizeof(int) * (2 * BMAX + (size_t)n * SCR_WORDS(Hmb, Wmb)), s));
+		/* the arguments go to device memory (pageable source: staged by the copy call) */
+		CHECK(hipMemcpyAsync(pargs + (size_t)k * BMAX, ha, sizeof(PictureArgs) * n, hipMemcpyHostToDevice, s));
 		{
 			/* the device-wide workgroup budget (SlotBudget): reserve, launch, register the release */
 			SlotBudget &bg = g_budget[dev & 15];
 			const int nb = picture_blocks(inter_grid, Hmb);
 			hipEvent_t done = bg.event();
 			if (!done) return -1;
-			const int held = bg.reserve(nb);
-			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
-			                   (const PictureArgs *)(pargs + k));
+			const int held = bg.reserve(nb * n);
+			hipLaunchKernelGGL(k_picture, dim3(nb * n), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
+			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), nb);
 			if (hipGetLastError() != hipSuccess || hipEventRecord(done, s) != hipSuccess) {
 				bg.cancel(held);
 				fprintf(stderr, "m2dec_amd: k_picture launch failed\n");
@@ -438,14 +486,15 @@ struct Sched {
 			}
 			bg.registered(done, held);
 		}
-		tm.inter_launches += j.n_inter ? 1 : 0;
-		tm.intra_launches += j.n_intra ? 1 : 0;
-		tm.deblock_launches++;
-		slot_seq.s[j.slot] = a.seq + 1;
 		*inter_done = next_event();
 		CHECK(hipEventRecord(*inter_done, s));
 		if (tev) CHECK(hipEventRecord(tev[0], s));
 		return 0;
+	}
+
+	int launch(int k, const PicJob &j, hipEvent_t *tev, hipEvent_t *inter_done)
+	{
+		return launch_multi(k, &j, 1, tev, inter_done);
 	}
 
 	/* ---- batch launches (trace replay): one k_batch per run of pictures, slot reuse ordered on the
@@ -642,7 +691,7 @@ struct Sched {
 		}
 		g_dev.give(dev, frames, fsz * (size_t)nslots);
 		if (prog) g_dev.give(dev, prog, prog_bytes());
-		if (hand) g_dev.give(dev, hand, hand_bytes() * NSTREAMS);
+		if (hand) g_dev.give(dev, hand, hand_bytes() * NSTREAMS * BMAX);
 		if (rowflag) g_dev.give(dev, rowflag, rowflag_bytes());
 		if (pargs) (void)hipFree(pargs);
 		if (err) (void)hipFree(err);
@@ -680,7 +729,7 @@ int64_t ref_bytes_of(const m2r_inter_t *it, int n)
 
 /* ======================================================================== decode-path back end */
 const int kSlicesCap = 64;
-const int kArenas = 2 * NSTREAMS;
+const int kArenas = NSTREAMS * BMAX + BMAX + 2; /* launched + held pictures, and the one being filled */
 
 struct Arena {
 	m2r_picture_t pic;
@@ -688,6 +737,7 @@ struct Arena {
 	size_t size = 0, off_mb = 0, off_dbk = 0, off_slice = 0, off_inter = 0, off_coef = 0;
 	hipEvent_t consumed = nullptr; /* the picture's kernels finished reading the device copy */
 	bool pending = false;
+	bool held = false;             /* submitted, not launched yet */
 };
 
 /* Pinned record arenas (+ their device twins) outlive a decoder context: a process decoding stream
@@ -798,10 +848,23 @@ struct HipBackend {
 	bool slot_pending[64];     /* stg[i] holds a picture not yet copied to the caller's frame */
 	Arena ar[kArenas];
 	int next = 0;
+	/* submitted pictures not launched yet (decode order); launched together by be_flush */
+	struct Held {
+		Arena *a;
+		PicJob j;
+		bool virt;
+		size_t rec_bytes;
+		int64_t ref_bytes;
+	} held[BMAX];
+	int nheld = 0;
+	int max_held = 3; /* M2DEC_AMD_PICS_PER_LAUNCH (r67 A/B on c3, median of 10 decodes: 1 -> 45.1 ms,
+	                   * 2 -> 42.6, 3 -> 41.3, 4 -> 43.3-43.5) */
 	TimingSlot tr[16];
 	int tr_next = 0;
 	bool timing = true;
 };
+
+int be_flush(void *self);
 
 void flush_timing(HipBackend *b, TimingSlot &t)
 {
@@ -829,6 +892,7 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 {
 	HipBackend *b = (HipBackend *)self;
 	const double t0 = wall_s();
+	if (be_flush(b) < 0) return -1;
 	if (b->sc.sync_all() < 0) return -1;
 	if (b->copy) CHECK(hipStreamSynchronize(b->copy)); /* every staging copy is complete */
 	if (n > 64) n = 64;
@@ -909,6 +973,7 @@ m2r_picture_t *be_acquire(void *self, int wm, int hm)
 	HipBackend *b = (HipBackend *)self;
 	Arena &a = b->ar[b->next];
 	b->next = (b->next + 1) % kArenas;
+	if (a.held && be_flush(b) < 0) return nullptr;
 	if (a.pending) {
 		/* the host copy is overwritten next: wait until that picture's kernels are done with it */
 		if (hipEventSynchronize(a.consumed) != hipSuccess) return nullptr;
@@ -925,14 +990,15 @@ int be_submit(void *self, m2r_picture_t *pic)
 	Arena *a = nullptr;
 	for (auto &x : b->ar)
 		if (&x.pic == pic) a = &x;
-	if (!a) return -1;
 	const int n = pic->width_mbs * pic->height_mbs;
 	const bool virt = (pic->flags & M2R_PIC_VIRTUAL) != 0;
-	if (pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots) return -1;
-	if (!virt && pic->slot >= b->nframes) return -1;
-	if (pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) return -1;
-	CHECK(hipSetDevice(sc.dev));
-	PicJob j;
+	if (!a || a->held || pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots ||
+	    (!virt && pic->slot >= b->nframes) || pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) {
+		fprintf(stderr, "m2dec_amd: submit: picture records rejected (arena %d, slot %d)\n", a ? (int)(a - b->ar) : -1, pic->slot);
+		return -1;
+	}
+	HipBackend::Held &h = b->held[b->nheld++];
+	PicJob &j = h.j;
 	j.slot = pic->slot;
 	j.n_inter = pic->n_inter;
 	j.n_intra = pic->n_intra;
@@ -943,12 +1009,35 @@ int be_submit(void *self, m2r_picture_t *pic)
 	j.r.sl = (const m2r_slice_t *)(a->dev + a->off_slice);
 	j.r.it = (const m2r_inter_t *)(a->dev + a->off_inter);
 	j.r.coef = (const int16_t *)(a->dev + a->off_coef);
-	size_t rec_bytes = n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t)) + pic->n_slices * sizeof(m2r_slice_t) +
-	                   pic->n_inter * sizeof(m2r_inter_t) + pic->n_coef * sizeof(int16_t);
+	h.a = a;
+	h.virt = virt;
+	h.rec_bytes = n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t)) + pic->n_slices * sizeof(m2r_slice_t) +
+	              pic->n_inter * sizeof(m2r_inter_t) + pic->n_coef * sizeof(int16_t);
+	h.ref_bytes = ref_bytes_of(pic->inter, pic->n_inter);
+	a->held = true;
+	/* a caller slot as the picture buffer (no decode ahead): copied out right behind its kernel, so
+	 * launched at once, as is a full hand */
+	if (!virt || b->nheld >= b->max_held) return be_flush(b);
+	return 0;
+}
 
-	const int k = sc.begin(j.slot, j.refs);
-	if (k < 0) return -1;
+/* launch the held pictures as one k_picture on the next stream: their slots' waits, the record uploads,
+ * the launch, then per picture the consumed event, the copy-out (caller slot), and the slot bookkeeping */
+int be_flush(void *self)
+{
+	HipBackend *b = (HipBackend *)self;
+	Sched &sc = b->sc;
+	const int n = b->nheld;
+	if (!n) return 0;
+	b->nheld = 0;
+	CHECK(hipSetDevice(sc.dev));
+	const int k = sc.pick();
 	hipStream_t s = sc.st[k];
+	PicJob jobs[BMAX];
+	for (int i = 0; i < n; ++i) {
+		jobs[i] = b->held[i].j;
+		if (sc.waits(k, jobs[i].slot, jobs[i].refs) < 0) return -1;
+	}
 	TimingSlot *ts = nullptr;
 	if (b->timing) {
 		ts = &b->tr[b->tr_next];
@@ -956,27 +1045,38 @@ int be_submit(void *self, m2r_picture_t *pic)
 		flush_timing(b, *ts);
 		CHECK(hipEventRecord(ts->e[0], s));
 	}
-	CHECK(hipMemcpyAsync(a->dev + a->off_mb, a->host + a->off_mb, a->off_slice - a->off_mb, hipMemcpyHostToDevice, s));
-	if (pic->n_slices) CHECK(hipMemcpyAsync(a->dev + a->off_slice, a->host + a->off_slice, pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
-	if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, a->host + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
-	if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+	for (int i = 0; i < n; ++i) {
+		const Arena *a = b->held[i].a;
+		const m2r_picture_t *pic = &a->pic;
+		CHECK(hipMemcpyAsync(a->dev + a->off_mb, a->host + a->off_mb, a->off_slice - a->off_mb, hipMemcpyHostToDevice, s));
+		if (pic->n_slices) CHECK(hipMemcpyAsync(a->dev + a->off_slice, a->host + a->off_slice, pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
+		if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, a->host + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
+		if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+	}
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	hipEvent_t inter_done;
-	if (sc.launch(k, j, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
-	CHECK(hipEventRecord(a->consumed, s));
-	a->pending = true;
+	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
 	const size_t ls = (size_t)sc.W * sc.H;
-	if (!virt) /* the caller's slot is the picture buffer: copy out right behind the kernel */
-		if (stage_copy(b, sc.frames + (size_t)pic->slot * sc.fsz, pic->slot, s) < 0) return -1;
+	for (int i = 0; i < n; ++i) {
+		HipBackend::Held &h = b->held[i];
+		CHECK(hipEventRecord(h.a->consumed, s));
+		h.a->pending = true;
+		h.a->held = false;
+		if (!h.virt) /* the caller's slot is the picture buffer: copy out right behind the kernel */
+			if (stage_copy(b, sc.frames + (size_t)h.j.slot * sc.fsz, h.j.slot, s) < 0) return -1;
+	}
 	if (ts) {
 		CHECK(hipEventRecord(ts->e[5], s));
 		ts->pending = true;
 	}
-	if (sc.end(k, j, inter_done) < 0) return -1;
-	sc.tm.pictures++;
-	sc.tm.record_bytes += (int64_t)rec_bytes;
-	sc.tm.ref_bytes += ref_bytes_of(pic->inter, pic->n_inter);
-	sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
+	for (int i = 0; i < n; ++i) {
+		const HipBackend::Held &h = b->held[i];
+		if (sc.end(k, h.j, inter_done) < 0) return -1;
+		sc.tm.pictures++;
+		sc.tm.record_bytes += (int64_t)h.rec_bytes;
+		sc.tm.ref_bytes += h.ref_bytes;
+		sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
+	}
 	return 0;
 }
 
@@ -987,7 +1087,12 @@ int be_bind(void *self, int vid, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	Sched &sc = b->sc;
-	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->nframes || !sc.slot_write[vid]) return -1;
+	if (be_flush(b) < 0) return -1; /* (the picture writing vid may be held) */
+	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->nframes || !sc.slot_write[vid]) {
+		fprintf(stderr, "m2dec_amd: bind: picture buffer %d (written: %d) to frame %d rejected\n", vid,
+		        vid >= 0 && vid < 64 && sc.slot_write[vid] != nullptr, slot);
+		return -1;
+	}
 	CHECK(hipSetDevice(sc.dev));
 	if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
 	CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[vid], 0));
@@ -1005,6 +1110,9 @@ int be_sync(void *self, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	if (slot < 0 || slot >= 64) return -1;
+	/* (no flush here: sync_frame runs on the API thread while a pool worker may be inside submit / bind /
+	 * flush — those three, acquire and set_frames are the serial back-end calls.  The slot's picture was
+	 * launched when it was bound, or when it was submitted without decode ahead.) */
 	if (b->slot_pending[slot]) {
 		CHECK(hipEventSynchronize(b->slot_ev[slot]));
 		if (b->sc.check_err() < 0) return -1;
@@ -1027,6 +1135,8 @@ void be_destroy(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
 	const double t0 = wall_s();
+	for (int i = 0; i < b->nheld; ++i) b->held[i].a->held = false; /* (dropped: nothing waits for them) */
+	b->nheld = 0;
 	b->sc.sync_all();
 	const double t1 = wall_s();
 	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: every staging copy is complete) */
@@ -1106,6 +1216,9 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->sync_frame = be_sync;
 	out->destroy = be_destroy;
 	out->bind = be_bind;
+	out->flush = be_flush;
+	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
+		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
 }
@@ -1490,11 +1603,11 @@ extern "C" int m2dec_amd_hip_replay_debug_scratch(m2dec_amd_hip_replay_t *r, int
 {
 	if (!r) return -1;
 	Sched &sc = r->sc;
-	int need = SCR_WORDS(sc.Hmb, sc.Wmb) * NSTREAMS + 1;
+	int need = (int)sc.stream_words() * NSTREAMS + 1;
 	if (n < need) return -1;
 	hipStream_t s;
 	CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-	CHECK(hipMemcpyAsync(out, sc.prog, sizeof(int) * SCR_WORDS(sc.Hmb, sc.Wmb) * NSTREAMS, hipMemcpyDeviceToHost, s));
+	CHECK(hipMemcpyAsync(out, sc.prog, sizeof(int) * sc.stream_words() * NSTREAMS, hipMemcpyDeviceToHost, s));
 	CHECK(hipMemcpyAsync(out + need - 1, sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
 	CHECK(hipStreamSynchronize(s));
 	CHECK(hipStreamDestroy(s));

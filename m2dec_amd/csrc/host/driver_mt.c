@@ -404,5 +404,6 @@ int m2dec_amd_null_backend_create(m2r_backend_t *out)
 	out->sync_frame = null_sync;
 	out->destroy = null_destroy;
 	out->bind = NULL;
+	out->flush = NULL;
 	return 0;
 }

@@ -127,6 +127,7 @@ struct h264_async {
 	long bnd;                 /* decode ahead: next job to bind: [tail, bnd) bound */
 	int ahead;                /* decode ahead: the back end has bind (M2R_PIC_VIRTUAL submissions) */
 	int driving;              /* decode ahead: a thread is inside pipe_drive (back-end calls are serial) */
+	int held;                 /* decode ahead: submitted since the last back-end flush */
 	int sub_err;
 	int ahead_all;            /* M2DEC_AMD_AHEAD_ALL (tests): the API context closes a picture only after the
 	                             pipe_drive submitted it, so every picture goes ahead whatever the thread timing */
@@ -825,7 +826,8 @@ static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 		as->t_copy += t2 - t1;
 		t1 = t2;
 	}
-	const int err = d->backend.submit(d->backend.self, dst) < 0;
+	int err = d->backend.submit(d->backend.self, dst) < 0;
+	if (!err && !virt && d->backend.flush) err = d->backend.flush(d->backend.self) < 0; /* (in API order: one at a time) */
 	if (as->stats) as->t_submit += now_s() - t1;
 	return err;
 }
@@ -905,11 +907,22 @@ static void pipe_drive(struct h264_async *as)
 				j->sub_err = err;
 				j->submitted = 1;
 				as->sub_err += err;
+				as->held |= !err && d->backend.flush != NULL;
 				as->sub++;
 				d->ahead_submits += ahead && !err;
 				pthread_cond_broadcast(&as->cv_done);
 				continue;
 			}
+		}
+		if (as->held) {
+			/* nothing more to do for now: launch what this drive submitted (the back end may have held
+			 * pictures back to launch them together) */
+			pthread_mutex_unlock(as->mu);
+			const int err = d->backend.flush(d->backend.self) < 0;
+			pthread_mutex_lock(as->mu);
+			as->held = 0;
+			as->sub_err += err;
+			continue;
 		}
 		break;
 	}

@@ -1019,6 +1019,7 @@ int h264_picture_finish(h264_dec_t *d)
 	int err;
 	h264_picture_resolve_deblock(d);
 	err = d->backend.submit(d->backend.self, d->pic);
+	if (!err && d->backend.flush) err = d->backend.flush(d->backend.self);
 	d->pic = NULL;
 	if (err < 0) return -1;
 	return h264_picture_mark(d);

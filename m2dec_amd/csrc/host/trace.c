@@ -185,6 +185,7 @@ int m2dec_amd_trace_capture(const uint8_t *data, size_t len, m2dec_amd_trace_t *
 	be.sync_frame = cap_sync;
 	be.destroy = cap_destroy;
 	be.bind = NULL;
+	be.flush = NULL;
 	n = m2dec_amd_decode_stream(data, len, &be, 0, cap_on_frame, &c, NULL);
 	free(c.arena);
 	if (n < 0 || c.failed) {

@@ -1259,5 +1259,6 @@ int oracle_backend_create(m2r_backend_t *out)
 	out->sync_frame = be_sync;
 	out->destroy = be_destroy;
 	out->bind = be_bind;
+	out->flush = NULL;
 	return 0;
 }

@@ -125,7 +125,7 @@ public:
 		context_ = new uint8_t[func_->context_size];
 		func_->init(context_, -1, header_callback, this);
 		if (g_oracle_create) { /* test-only: the CPU checker as the reconstruction back end */
-			m2r_backend_t be;
+			m2r_backend_t be = {};
 			if (g_oracle_create(&be) < 0 || m2dec_amd_h264_set_backend(context_, &be) < 0) exit(4);
 		}
 		if (g_threads >= 0) m2dec_amd_h264_set_parse_threads(context_, g_threads);

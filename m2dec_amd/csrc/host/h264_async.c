@@ -575,10 +575,32 @@ static void *pool_worker(void *arg)
 	return NULL;
 }
 
+/* Process exit with contexts still decoding (a caller that drops its decoders, m2decoder.h:39-50, and
+ * returns from main): the detached workers would go on parsing and driving back ends while the static
+ * destructors tear down the HIP runtime and the back ends' process pools under them.  So the first
+ * worker's creation registers this: every pipeline stops taking work, and exit waits (bounded) until no
+ * worker is inside a job or a back-end call; the idle workers then sleep on cv_work through exit. */
+static void pool_atexit(void)
+{
+	struct timespec ts;
+	pthread_mutex_lock(&g_parse.mu);
+	for (struct h264_async *p = g_parse.pipes; p; p = p->pnext) p->quit = 1;
+	clock_gettime(CLOCK_REALTIME, &ts);
+	ts.tv_sec += 2;
+	for (;;) {
+		struct h264_async *busy = NULL;
+		for (struct h264_async *p = g_parse.pipes; p && !busy; p = p->pnext)
+			if (p->running || p->driving) busy = p;
+		if (!busy || pthread_cond_timedwait(&busy->cv_done, &g_parse.mu, &ts) != 0) break;
+	}
+	pthread_mutex_unlock(&g_parse.mu);
+}
+
 /* at least n pool workers (mutex held) */
 static int pool_grow(int n)
 {
 	if (n > POOL_MAX) n = POOL_MAX;
+	if (g_parse.nth == 0 && n > 0) atexit(pool_atexit);
 	while (g_parse.nth < n) {
 		pthread_attr_t at;
 		pthread_attr_init(&at);

@@ -531,11 +531,43 @@ static inline int cab_bypass(cab_t *c)
 	return 0;
 }
 
+/* k <= 16 bypass bins at once, MSB first: k compare-subtract steps are one long division of the
+ * window by range << (cnt - k) (win < range << cnt bounds the quotient by 2^k) */
+static inline uint32_t cab_bypass_k(cab_t *c, int k)
+{
+	uint64_t scaled, q;
+	c->bins += (uint64_t)k;
+	c->cnt -= k;
+	scaled = (uint64_t)c->range << c->cnt;
+	q = c->win / scaled;
+	c->win -= q * scaled;
+	if (c->cnt < 16) cab_refill(c);
+	return (uint32_t)q;
+}
+
 static inline uint32_t cab_bypass_n(cab_t *c, int n)
 {
 	uint32_t v = 0;
-	for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)cab_bypass(c);
-	return v;
+	while (n > 16) {
+		v = (v << 16) | cab_bypass_k(c, 16);
+		n -= 16;
+	}
+	return n > 0 ? (v << n) | cab_bypass_k(c, n) : v;
+}
+
+/* a unary run of bypass 1s ended by a 0, looking at most 16 bins ahead: the number of 1s with the 0
+ * consumed, or -1 (nothing consumed) if the next 16 bins are all 1 */
+static inline int cab_bypass_ones(cab_t *c)
+{
+	const uint64_t scaled = (uint64_t)c->range << (c->cnt - 16);
+	const uint32_t q = (uint32_t)(c->win / scaled); /* the next 16 bins, not consumed */
+	const int ones = __builtin_clz(~(q << 16) | 1u);
+	if (ones >= 16) return -1;
+	c->bins += (uint64_t)ones + 1;
+	c->cnt -= ones + 1;
+	c->win -= (uint64_t)(q >> (15 - ones)) * ((uint64_t)c->range << c->cnt);
+	if (c->cnt < 16) cab_refill(c);
+	return ones;
 }
 
 /* end_of_slice_segment_flag (h265.cpp:1350-1365) */
@@ -794,8 +826,11 @@ static int residual_coding(sctx_t *x, int log2, int cidx, int scan, int is_intra
 				int a = lvl[j];
 				if (need_rem & (1 << j)) {
 					/* coeff_abs_level_remaining (h265.cpp:1335-1348) */
-					int pfx = 0;
-					while (pfx < 20 && cab_bypass(c)) pfx++;
+					int pfx = cab_bypass_ones(c);
+					if (pfx < 0) { /* 16 or more 1s: bin by bin up to the cap */
+						pfx = 0;
+						while (pfx < 20 && cab_bypass(c)) pfx++;
+					}
 					if (pfx < 4) a += (pfx << rice) + (int)cab_bypass_n(c, rice);
 					else a += (1 << (pfx - 4 + rice + 1)) + (2 << rice) + (int)cab_bypass_n(c, pfx - 4 + rice + 1);
 					if (a > (3 << rice) && rice < 4) rice++;

@@ -44,8 +44,11 @@ struct H265Args {
 	const h265r_sao_t *sao;
 	uint8_t *frame;   /* NV12, stride W */
 	uint8_t *copy;    /* the deblocked frame (SAO input) */
-	int *done;        /* per block */
-	int *counter;     /* next block */
+	int *done;        /* per block (block kernel) */
+	int *counter;     /* next block (block kernel) */
+	int *progress;    /* per CTU row: CTUs finished (CTU kernel) */
+	int *ctu_first;   /* [ctu_cols * ctu_rows + 1]: the first record of each CTU (CTU kernel) */
+	int ctu_cols, ctu_rows;
 	int *err;         /* sticky: a hand-off that never came */
 	int W, H, pic_w, pic_h, ctb_log2, n_tu, flags;
 	int beta_offset, tc_offset, cb_qp_offset, cr_qp_offset;
@@ -109,8 +112,26 @@ __device__ __forceinline__ void st_word(uint8_t *p, uint32_t v)
 	__hip_atomic_store((gi32 *)p, (int)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-/* one block (wave-wide) */
-__device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane)
+/* LDS ordering among the lanes of one wave (every block runs on one wave; the CTU kernel's two waves
+ * must not wait for each other per block) */
+__device__ __forceinline__ void wsync()
+{
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+/* samples straight from / to the frame (block kernel) */
+struct FrameSamples {
+	const H265Args &a;
+	__device__ int ld(int plane, int comp, int x, int y) const { return ld_px(a, plane, comp, x, y); }
+	/* 4 luma samples / 2 CbCr pairs of one row, little-endian in v */
+	__device__ void st(int plane, int x, int y, uint32_t v) const { st_word(plane_px(a, plane, 0, x, y), v); }
+};
+
+/* one block (wave-wide); Src: where neighbour samples come from and the block's samples go */
+template <class Src>
+__device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane, const Src &src)
 {
 	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
 	const int ncomp = t.plane ? 2 : 1;
@@ -119,7 +140,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 	for (int c = 0; c < ncomp; ++c) {
 		int *pred = s.pred[c];
 		if (!(t.flags & H265R_TU_PRED)) {
-			for (int i = lane; i < n2; i += 64) pred[i] = ld_px(a, t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
+			for (int i = lane; i < n2; i += 64) pred[i] = src.ld(t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
 			continue;
 		}
 		const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
@@ -134,11 +155,11 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 				const int k = clampi(i, lo, hi);
 				const int xx = k < corner ? -1 : (k == corner ? -1 : k - corner - 1);
 				const int yy = k < corner ? corner - 1 - k : -1;
-				v = ld_px(a, t.plane, c, t.x + xx, t.y + yy);
+				v = src.ld(t.plane, c, t.x + xx, t.y + yy);
 			}
 			s.raw[i] = (int16_t)v;
 		}
-		__syncthreads();
+		wsync();
 		const int mode = t.mode;
 		bool filt = false;
 		if (luma && mode != 1 && n != 4) {
@@ -164,7 +185,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			}
 			s.seq[c][i] = (int16_t)v;
 		}
-		__syncthreads();
+		wsync();
 		const int16_t *q = s.seq[c];
 #define LL(yy) ((int)q[corner - 1 - (yy)]) /* p[-1][y], y >= -1 */
 #define TT(xx) ((int)q[corner + 1 + (xx)]) /* p[x][-1], x >= -1 */
@@ -215,7 +236,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 		}
 #undef LL
 #undef TT
-		__syncthreads();
+		wsync();
 	}
 	/* ---- residual */
 	for (int c = 0; c < ncomp; ++c) {
@@ -238,7 +259,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			const int k = i >> log2, sm = i & (n - 1);
 			s.mat[i] = dstm ? c_dst[k * 4 + sm] : s.mat32[(k << (5 - log2)) * 32 + sm];
 		}
-		__syncthreads();
+		wsync();
 		/* first stage (columns): g[y][x] = sat16((sum_j M[j][y] d[j][x] + 64) >> 7) */
 		int g[16];
 		for (int r = 0, i = lane; i < n2; i += 64, ++r) {
@@ -247,9 +268,9 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			for (int j = 0; j < n; ++j) e += s.mat[j * n + y] * s.t0[j * n + x];
 			g[r] = sat16((e + 64) >> 7);
 		}
-		__syncthreads();
+		wsync();
 		for (int r = 0, i = lane; i < n2; i += 64, ++r) s.t0[i] = g[r];
-		__syncthreads();
+		wsync();
 		/* second stage (rows): r[y][x] = sat16((sum_j M[j][x] g[y][j] + 2048) >> 12) */
 		for (int i = lane; i < n2; i += 64) {
 			const int x = i & (n - 1), y = i >> log2;
@@ -257,7 +278,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			for (int j = 0; j < n; ++j) e += s.mat[j * n + x] * s.t0[y * n + j];
 			pred[i] += sat16((e + 2048) >> 12);
 		}
-		__syncthreads();
+		wsync();
 	}
 	/* ---- out: 32-bit write-through words (luma: 4 samples of a row; chroma: 2 CbCr pairs) */
 	if (luma) {
@@ -267,7 +288,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			const int *q = s.pred[0] + y * n + x;
 			const uint32_t v = (uint32_t)clampi(q[0], 0, 255) | ((uint32_t)clampi(q[1], 0, 255) << 8) |
 			                   ((uint32_t)clampi(q[2], 0, 255) << 16) | ((uint32_t)clampi(q[3], 0, 255) << 24);
-			st_word(plane_px(a, 0, 0, t.x + x, t.y + y), v);
+			src.st(0, t.x + x, t.y + y, v);
 		}
 	} else {
 		const int wpr = n >> 1;
@@ -276,7 +297,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			const int *cb = s.pred[0] + y * n + x, *cr = s.pred[1] + y * n + x;
 			const uint32_t v = (uint32_t)clampi(cb[0], 0, 255) | ((uint32_t)clampi(cr[0], 0, 255) << 8) |
 			                   ((uint32_t)clampi(cb[1], 0, 255) << 16) | ((uint32_t)clampi(cr[1], 0, 255) << 24);
-			st_word(plane_px(a, 1, 0, t.x + x, t.y + y), v);
+			src.st(1, t.x + x, t.y + y, v);
 		}
 	}
 }
@@ -318,11 +339,144 @@ __global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
 			}
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sample loads below the poll */
 		}
-		do_block(a, t, s, lane);
+		do_block(a, t, s, lane, FrameSamples{a});
 		/* publish: the write-through sample stores drained, then the flag */
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__hip_atomic_store((gi32 *)&a.done[idx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
+}
+
+/* ---- the CTU wavefront (default): one workgroup per CTU row, CTUs left to right; wave 0 reconstructs the
+ * CTU's luma blocks, wave 1 its chroma blocks, each in decoding order, entirely in LDS: the CTU's samples,
+ * the column left of it (kept from the previous CTU) and the row above it from the left-above corner to
+ * the end of the above-right CTU (loaded once per CTU after that CTU row published it).  A CTU starts when
+ * the row above finished the CTU above-right of it (HEVC's intra references reach no further), so the
+ * picture is a 2-CTU-lag wavefront of cols + 2 (rows - 1) CTU steps, each with two global round trips
+ * (the row above in, the CTU out) instead of two per block. */
+#define H265_CTB_MAX 64
+struct CtuTile {
+	uint8_t y[H265_CTB_MAX][H265_CTB_MAX];      /* luma */
+	uint8_t c[H265_CTB_MAX / 2][H265_CTB_MAX];  /* CbCr pairs */
+	uint8_t ly[H265_CTB_MAX], lc[H265_CTB_MAX];  /* the column left of the CTU (CbCr pairs) */
+	uint8_t ty[2 * H265_CTB_MAX + 4];            /* the row above: [0] the left-above corner, [1 + i] x0 + i */
+	uint8_t tc[2 * H265_CTB_MAX + 4];            /* CbCr pairs: [2 (1 + i) + comp] */
+};
+
+struct CtuSamples {
+	CtuTile &tl;
+	int x0, y0; /* the CTU's luma origin */
+	__device__ int ld(int plane, int comp, int x, int y) const
+	{
+		if (!plane) {
+			const int dx = x - x0, dy = y - y0;
+			return dy < 0 ? tl.ty[dx + 1] : (dx < 0 ? tl.ly[dy] : tl.y[dy][dx]);
+		}
+		const int dx = x - (x0 >> 1), dy = y - (y0 >> 1);
+		return dy < 0 ? tl.tc[2 * (dx + 1) + comp] : (dx < 0 ? tl.lc[2 * dy + comp] : tl.c[dy][2 * dx + comp]);
+	}
+	__device__ void st(int plane, int x, int y, uint32_t v) const
+	{
+		if (!plane) *(uint32_t *)&tl.y[y - y0][x - x0] = v;
+		else *(uint32_t *)&tl.c[y - (y0 >> 1)][2 * (x - (x0 >> 1))] = v;
+	}
+};
+
+/* first record of every CTU (records are in decoding order, CTUs in raster order) */
+__global__ __launch_bounds__(256) void k_h265_ctu_index(const H265Args *ap)
+{
+	const H265Args &a = *ap;
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	const int nctu = a.ctu_cols * a.ctu_rows;
+	if (i > a.n_tu) return;
+	auto ctu_of = [&](int k) {
+		const h265r_tu_t &t = a.tu[k];
+		const int x = t.plane ? 2 * t.x : t.x, y = t.plane ? 2 * t.y : t.y;
+		return (y >> a.ctb_log2) * a.ctu_cols + (x >> a.ctb_log2);
+	};
+	const int cur = i < a.n_tu ? ctu_of(i) : nctu;
+	const int prev = i > 0 ? ctu_of(i - 1) : -1;
+	for (int c = prev + 1; c <= cur && c <= nctu; ++c) a.ctu_first[c] = i;
+}
+
+__global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
+{
+	const H265Args a = *ap;
+	__shared__ Lds ls[2];
+	__shared__ CtuTile tl;
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
+	const int row = blockIdx.x;
+	const int ctb = 1 << a.ctb_log2, cctb = ctb >> 1;
+	Lds &s = ls[wave];
+	for (int i = lane; i < 32 * 32; i += 64) s.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+	const int y0 = row << a.ctb_log2;
+	const int rows_here = min(ctb, a.pic_h - y0), crows = rows_here >> 1;
+	for (int col = 0; col < a.ctu_cols; ++col) {
+		const int x0 = col << a.ctb_log2;
+		const int cols_here = min(ctb, a.pic_w - x0);
+		/* the column left of this CTU: the previous CTU's last column (unavailable at col 0) */
+		if (tid < ctb) {
+			tl.ly[tid] = col ? tl.y[tid][ctb - 1] : 128;
+			tl.lc[tid] = col ? tl.c[tid >> 1][ctb - 2 + (tid & 1)] : 128;
+		}
+		/* the row above, once that CTU row finished the CTU above-right */
+		if (row > 0) {
+			if (wave == 0) {
+				const int need = min(col + 2, a.ctu_cols);
+				unsigned spins = 0;
+				for (;;) {
+					const int got = __hip_atomic_load((gi32 *)&a.progress[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					if (got >= need) break;
+					if (++spins > H265_SPIN_LIMIT) {
+						__hip_atomic_store((gi32 *)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+						break;
+					}
+					if (__hip_atomic_load((gi32 *)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+					__builtin_amdgcn_s_sleep(1);
+				}
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+			}
+			__syncthreads();
+			for (int i = tid; i <= 2 * ctb; i += 128) {
+				const int x = x0 - 1 + i;
+				tl.ty[i] = (x >= 0 && x < a.pic_w) ? (uint8_t)ld_px(a, 0, 0, x, y0 - 1) : 128;
+			}
+			for (int i = tid; i < 2 * (ctb + 1); i += 128) {
+				const int x = (x0 >> 1) - 1 + (i >> 1);
+				tl.tc[i] = (x >= 0 && x < (a.pic_w >> 1)) ? (uint8_t)ld_px(a, 1, i & 1, x, (y0 >> 1) - 1) : 128;
+			}
+		}
+		__syncthreads();
+		/* the CTU's blocks, luma on wave 0, chroma on wave 1, in decoding order */
+		{
+			const CtuSamples src{tl, x0, y0};
+			const int c = row * a.ctu_cols + col;
+			const int i0 = a.ctu_first[c], i1 = a.ctu_first[c + 1];
+			for (int i = i0; i < i1; ++i) {
+				const h265r_tu_t t = a.tu[i];
+				if (t.plane != wave) continue;
+				do_block(a, t, s, lane, src);
+			}
+		}
+		__syncthreads();
+		/* out: the CTU's samples (inside the picture) as write-through words, drained, then the progress word */
+		{
+			const int wpr = (cols_here + 3) >> 2;
+			for (int w = tid; w < wpr * rows_here; w += 128) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				st_word(plane_px(a, 0, 0, x0 + xx, y0 + yy), *(const uint32_t *)&tl.y[yy][xx]);
+			}
+			const int cw = (cols_here + 3) >> 2; /* words of CbCr pairs per chroma row: cols_here bytes */
+			for (int w = tid; w < cw * crows; w += 128) {
+				const int yy = w / cw, xx = (w - yy * cw) * 4;
+				st_word(plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy), *(const uint32_t *)&tl.c[yy][xx]);
+			}
+			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			__syncthreads();
+			if (tid == 0) __hip_atomic_store((gi32 *)&a.progress[row], col + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		}
+	}
+	(void)cctb;
 }
 
 /* ---- deblocking (8.7.2; oracle/h265_oracle.c luma_edge / chroma_edge) */
@@ -496,6 +650,7 @@ struct H265Gpu {
 	long pictures = 0;
 	int64_t record_bytes = 0, frame_bytes = 0;
 	bool last_counted = true; /* the last submitted picture's kernel time is in kernel_us */
+	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 };
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -535,11 +690,18 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265Gpu *g = (H265Gpu *)p;
 	if (!g || !g->frames || pic->width != g->W || pic->height != g->H || pic->slot < 0 || pic->slot >= g->n || pic->n_tu < 0)
 		return -1;
-	/* host-side checks of what the kernels assume: blocks inside the frame, coefficients inside the pool */
-	for (int i = 0; i < pic->n_tu; ++i) {
+	/* host-side checks of what the kernels assume: blocks inside the frame and inside one CTU, CTUs in raster
+	 * order (the CTU kernel's per-CTU record ranges and LDS tile), coefficients inside the pool */
+	if (pic->ctb_log2 < 4 || pic->ctb_log2 > 6 || pic->pic_w > g->W || pic->pic_h > g->H) return -1;
+	for (int i = 0, last_ctu = 0; i < pic->n_tu; ++i) {
 		const h265r_tu_t &t = pic->tu[i];
 		const int n = 1 << t.log2, pw = t.plane ? g->W / 2 : g->W, ph = t.plane ? g->H / 2 : g->H;
 		if (t.log2 < 2 || t.log2 > 5 || t.x + n > pw || t.y + n > ph || t.mode > 34 || (t.x & 3) || (t.y & 3)) return -1;
+		const int lx = t.plane ? 2 * t.x : t.x, ly = t.plane ? 2 * t.y : t.y, ln = t.plane ? 2 * n : n;
+		const int ctb = 1 << pic->ctb_log2, cols_ = (pic->pic_w + ctb - 1) >> pic->ctb_log2;
+		const int ctu = (ly >> pic->ctb_log2) * cols_ + (lx >> pic->ctb_log2);
+		if (ctu < last_ctu || (lx & (ctb - 1)) + ln > ctb || (ly & (ctb - 1)) + ln > ctb) return -1;
+		last_ctu = ctu;
 		for (int c = 0; c < 2; ++c)
 			if (t.res[c] && (int64_t)t.coef[c] + n * n > (int64_t)pic->n_coef) return -1;
 	}
@@ -551,8 +713,9 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const size_t o_map = al16(o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
 	const size_t o_bsv = al16(o_map + sizeof(int32_t) * units), o_bsh = al16(o_bsv + nbs);
 	const size_t o_sao = al16(o_bsh + nbs), total = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
-	/* per-block done flags + 2 counters */
-	const size_t sn = (size_t)pic->n_tu + 2;
+	/* per-block done flags + 2 counters, then the CTU rows' progress words and the CTUs' first records */
+	const int nctu = cols * rows;
+	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + (size_t)nctu + 1;
 	if (sn > g->scratch_n) {
 		H265_CHECK(hipStreamSynchronize(g->st));
 		if (g->scratch) (void)hipFree(g->scratch);
@@ -587,6 +750,10 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.copy = g->copy;
 	h.done = g->scratch;
 	h.counter = g->scratch + pic->n_tu;
+	h.progress = h.counter + 2;
+	h.ctu_first = h.progress + rows;
+	h.ctu_cols = cols;
+	h.ctu_rows = rows;
 	h.err = g->err;
 	h.W = g->W;
 	h.H = g->H;
@@ -606,9 +773,13 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipMemsetAsync(g->scratch, 0, sizeof(int) * sn, g->st));
 	const int k = (int)(g->pictures & 1);
 	H265_CHECK(hipEventRecord(g->t0[k], g->st));
-	if (pic->n_tu) {
+	if (pic->n_tu && g->block_kernel) {
 		const int grid = pic->n_tu < g->cus * 8 ? pic->n_tu : g->cus * 8;
 		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);
+		H265_CHECK(hipGetLastError());
+	} else if (pic->n_tu) {
+		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, g->st, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, g->st, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & H265R_PIC_DEBLOCK) {
@@ -703,6 +874,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	H265Gpu *g = new H265Gpu();
 	g->dev = device;
 	g->cus = prop.multiProcessorCount;
+	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
 	if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking) != hipSuccess) {
 		delete g;
 		return -1;

@@ -130,6 +130,8 @@ struct SlotBudget {
 };
 
 SlotBudget g_budget[16]; /* per device ordinal */
+std::atomic<int> g_live_backends[16]; /* decode-path back ends alive per device (several pictures per launch
+                                       * only for a lone stream: concurrent streams already fill the budget) */
 
 /* Streams and events outlive a decoder context too (creating a stream and the ~160 events of a back
  * end costs ~10 ms): released ones are kept per device and handed to the next context. */
@@ -270,6 +272,7 @@ struct Sched {
 	int inter_grid = 80;       /* persistent inter workers per picture (5/16 of the CUs) */
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
+	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
 	hipEvent_t slot_write[64] = {};
@@ -358,6 +361,9 @@ struct Sched {
 			std::lock_guard<std::mutex> lk(bg.mu);
 			const int cap = std::max(1, per_cu * cus);
 			if (!bg.cap || cap < bg.cap) bg.cap = cap; /* contexts of several picture sizes: the smallest */
+			/* pictures per launch such that a launch on each stream fits the budget at once: a reserve
+			 * that has to wait would stall the thread driving the pipeline (a parse worker) */
+			pics_fit = std::max(1, std::min(BMAX, bg.cap / (NSTREAMS * picture_blocks(inter_grid, Hmb))));
 			if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "k_picture: %d workgroups resident (%d per CU)\n", bg.cap, per_cu);
 		}
 		return 0;
@@ -857,8 +863,9 @@ struct HipBackend {
 		int64_t ref_bytes;
 	} held[BMAX];
 	int nheld = 0;
-	int max_held = 3; /* M2DEC_AMD_PICS_PER_LAUNCH (r67 A/B on c3, median of 10 decodes: 1 -> 45.1 ms,
-	                   * 2 -> 42.6, 3 -> 41.3, 4 -> 43.3-43.5) */
+	int max_held = BMAX; /* M2DEC_AMD_PICS_PER_LAUNCH; also bounded by the budget (Sched::pics_fit: 2 at
+	                      * 1080p and 4K) and 1 while other decode-path back ends are alive.  r67 A/B on c3,
+	                      * median of 10 decodes: 1 -> 45.1 ms, 2 -> 42.6, 3 -> 41.3, 4 -> 43.3 */
 	TimingSlot tr[16];
 	int tr_next = 0;
 	bool timing = true;
@@ -1017,7 +1024,8 @@ int be_submit(void *self, m2r_picture_t *pic)
 	a->held = true;
 	/* a caller slot as the picture buffer (no decode ahead): copied out right behind its kernel, so
 	 * launched at once, as is a full hand */
-	if (!virt || b->nheld >= b->max_held) return be_flush(b);
+	const int limit = g_live_backends[sc.dev & 15].load(std::memory_order_relaxed) > 1 ? 1 : std::min(b->max_held, sc.pics_fit);
+	if (!virt || b->nheld >= limit) return be_flush(b);
 	return 0;
 }
 
@@ -1138,6 +1146,7 @@ void be_destroy(void *self)
 	for (int i = 0; i < b->nheld; ++i) b->held[i].a->held = false; /* (dropped: nothing waits for them) */
 	b->nheld = 0;
 	b->sc.sync_all();
+	g_live_backends[b->sc.dev & 15]--;
 	const double t1 = wall_s();
 	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: every staging copy is complete) */
 	b->copy = nullptr;
@@ -1217,6 +1226,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->destroy = be_destroy;
 	out->bind = be_bind;
 	out->flush = be_flush;
+	g_live_backends[device & 15]++;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
 		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));

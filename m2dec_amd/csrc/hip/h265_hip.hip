@@ -121,6 +121,50 @@ __device__ __forceinline__ void wsync()
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+/* One pass of the N-point inverse DCT (N = 8, 16, 32) over all N lines of a block, even / odd split:
+ * out[b] = E + O and out[N - 1 - b] = E - O with E / O the sums over the even / odd frequencies j of
+ * T[j][b] in[j] (T[j][N - 1 - b] = (-1)^j T[j][b]), exactly the matrix product's integers in half the
+ * multiplies.  Lane: line a = lane & (N - 1) (its N inputs held in registers), output pairs b =
+ * (lane >> log2 N) + k 64 / N.  COLS: pass 1 (line = column x: in[j] = src[j][x], out to dst[b][x] as
+ * sat16((v + 64) >> 7)); else pass 2 (line = row y: in[j] = src[y][j], dst[y][b] += sat16((v + 2048) >> 12)). */
+template <int N, bool COLS>
+__device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_t *mat32, int lane)
+{
+	constexpr int L = N == 8 ? 3 : (N == 16 ? 4 : 5), PAIRS = N * N / 2, PPL = PAIRS < 64 ? 1 : PAIRS / 64;
+	const int a = lane & (N - 1);
+	int in[N];
+#pragma unroll
+	for (int j = 0; j < N; ++j) in[j] = COLS ? src[j * N + a] : src[a * N + j];
+#pragma unroll
+	for (int k = 0; k < PPL; ++k) {
+		const int b = (lane >> L) + k * (64 >> L);
+		if (b < N / 2) {
+			int e = 0, o = 0;
+#pragma unroll
+			for (int j = 0; j < N; j += 2) {
+				e += mat32[(j << (5 - L)) * 32 + b] * in[j];
+				o += mat32[((j + 1) << (5 - L)) * 32 + b] * in[j + 1];
+			}
+			if (COLS) {
+				dst[b * N + a] = sat16((e + o + 64) >> 7);
+				dst[(N - 1 - b) * N + a] = sat16((e - o + 64) >> 7);
+			} else {
+				dst[a * N + b] += sat16((e + o + 2048) >> 12);
+				dst[a * N + N - 1 - b] += sat16((e - o + 2048) >> 12);
+			}
+		}
+	}
+}
+
+template <int N>
+__device__ __forceinline__ void idct_block(int *t0, int *tmp, int *pred, const int16_t *mat32, int lane)
+{
+	idct_pass<N, true>(t0, tmp, mat32, lane);
+	wsync();
+	idct_pass<N, false>(tmp, pred, mat32, lane);
+	wsync();
+}
+
 /* samples straight from / to the frame (block kernel) */
 struct FrameSamples {
 	const H265Args &a;
@@ -253,9 +297,16 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			for (int i = lane; i < n2; i += 64) pred[i] += (d[i] + 16) >> 5;
 			continue;
 		}
+		for (int i = lane; i < n2; i += 64) s.t0[i] = d[i];
 		const bool dstm = kind == H265R_RES_DST;
+		if (!dstm && n >= 8) {
+			wsync();
+			if (n == 8) idct_block<8>(s.t0, s.mat, pred, s.mat32, lane);
+			else if (n == 16) idct_block<16>(s.t0, s.mat, pred, s.mat32, lane);
+			else idct_block<32>(s.t0, s.mat, pred, s.mat32, lane);
+			continue;
+		}
 		for (int i = lane; i < n2; i += 64) {
-			s.t0[i] = d[i];
 			const int k = i >> log2, sm = i & (n - 1);
 			s.mat[i] = dstm ? c_dst[k * 4 + sm] : s.mat32[(k << (5 - log2)) * 32 + sm];
 		}
@@ -354,6 +405,7 @@ __global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
  * picture is a 2-CTU-lag wavefront of cols + 2 (rows - 1) CTU steps, each with two global round trips
  * (the row above in, the CTU out) instead of two per block. */
 #define H265_CTB_MAX 64
+#define H265_CTU_RECS 256
 struct CtuTile {
 	uint8_t y[H265_CTB_MAX][H265_CTB_MAX];      /* luma */
 	uint8_t c[H265_CTB_MAX / 2][H265_CTB_MAX];  /* CbCr pairs */
@@ -403,6 +455,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 	const H265Args a = *ap;
 	__shared__ Lds ls[2];
 	__shared__ CtuTile tl;
+	__shared__ h265r_tu_t recs[H265_CTU_RECS]; /* the CTU's records, staged (both waves read all of them) */
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
 	const int row = blockIdx.x;
@@ -452,10 +505,17 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 			const CtuSamples src{tl, x0, y0};
 			const int c = row * a.ctu_cols + col;
 			const int i0 = a.ctu_first[c], i1 = a.ctu_first[c + 1];
-			for (int i = i0; i < i1; ++i) {
-				const h265r_tu_t t = a.tu[i];
-				if (t.plane != wave) continue;
-				do_block(a, t, s, lane, src);
+			for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
+				const int m = min(H265_CTU_RECS, i1 - c0);
+				__syncthreads(); /* (the previous chunk is consumed) */
+				for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += 128)
+					((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
+				__syncthreads();
+				for (int k = 0; k < m; ++k) {
+					const h265r_tu_t t = recs[k];
+					if (t.plane != wave) continue;
+					do_block(a, t, s, lane, src);
+				}
 			}
 		}
 		__syncthreads();

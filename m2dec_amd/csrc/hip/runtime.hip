@@ -735,7 +735,7 @@ int64_t ref_bytes_of(const m2r_inter_t *it, int n)
 
 /* ======================================================================== decode-path back end */
 const int kSlicesCap = 64;
-const int kArenas = NSTREAMS * BMAX + BMAX + 2; /* launched + held pictures, and the one being filled */
+const int kArenas = NSTREAMS * BMAX + BMAX + 2; /* at most: launched + held pictures, and the one being filled */
 
 struct Arena {
 	m2r_picture_t pic;
@@ -777,7 +777,7 @@ struct ArenaPool {
 		if (!a.host) return;
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			if (free_blocks.size() < 32) {
+			if (free_blocks.size() < 64) {
 				free_blocks.push_back({dev, a.host, a.dev, a.size});
 				a.host = a.dev = nullptr;
 				a.size = 0;
@@ -863,6 +863,8 @@ struct HipBackend {
 		int64_t ref_bytes;
 	} held[BMAX];
 	int nheld = 0;
+	int limit = 1;        /* pictures per launch of this context (fixed at set_frames) */
+	int narenas = 2 * NSTREAMS; /* record arenas in use: NSTREAMS * limit + limit + 2 (fixed at set_frames) */
 	int max_held = BMAX; /* M2DEC_AMD_PICS_PER_LAUNCH; also bounded by the budget (Sched::pics_fit: 2 at
 	                      * 1080p and 4K) and 1 while other decode-path back ends are alive.  r67 A/B on c3,
 	                      * median of 10 decodes: 1 -> 45.1 ms, 2 -> 42.6, 3 -> 41.3, 4 -> 43.3 */
@@ -913,6 +915,12 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	b->stg_size = stg;
 	/* one device picture buffer per virtual id (decode ahead) — a caller slot also names one */
 	if (b->sc.configure(width, height, 64) < 0) return -1;
+	/* pictures per launch: bounded by the budget (pics_fit) and 1 while other decode-path back ends are
+	 * alive (concurrent streams fill the budget already); the arena ring covers what can be in flight
+	 * (every arena is one pinned + device allocation: a ring larger than needed churns the pools) */
+	b->limit = g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed) > 1 ? 1 : std::min(b->max_held, b->sc.pics_fit);
+	b->narenas = std::min(kArenas, NSTREAMS * b->limit + b->limit + 2);
+	if (b->next >= b->narenas) b->next = 0;
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "be_set_frames: configure %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
 }
@@ -979,7 +987,7 @@ m2r_picture_t *be_acquire(void *self, int wm, int hm)
 {
 	HipBackend *b = (HipBackend *)self;
 	Arena &a = b->ar[b->next];
-	b->next = (b->next + 1) % kArenas;
+	b->next = (b->next + 1) % b->narenas;
 	if (a.held && be_flush(b) < 0) return nullptr;
 	if (a.pending) {
 		/* the host copy is overwritten next: wait until that picture's kernels are done with it */
@@ -1024,8 +1032,7 @@ int be_submit(void *self, m2r_picture_t *pic)
 	a->held = true;
 	/* a caller slot as the picture buffer (no decode ahead): copied out right behind its kernel, so
 	 * launched at once, as is a full hand */
-	const int limit = g_live_backends[sc.dev & 15].load(std::memory_order_relaxed) > 1 ? 1 : std::min(b->max_held, sc.pics_fit);
-	if (!virt || b->nheld >= limit) return be_flush(b);
+	if (!virt || b->nheld >= b->limit) return be_flush(b);
 	return 0;
 }
 

@@ -505,6 +505,7 @@ static int cavlc_block(h264_bits_t *b, int cat, int nc, int16_t *out)
 	for (i = 0; i < total - 1; ++i) {
 		int r = 0;
 		if (zeros > 0) r = vlc_read(b, &rb_lut[imin(zeros, 7)]);
+		if (r > zeros) return -1; /* run_before beyond the zeros left: damaged data */
 		run[i] = r;
 		zeros -= r;
 	}

@@ -302,6 +302,12 @@ static int picture_open(mpeg2_dec_t *m)
 	return 0;
 }
 
+/* the current MB position lies inside the picture (a damaged stream's address increments may run past it) */
+static int mb_inside(const mpeg2_dec_t *m)
+{
+	return m->mb_x >= 0 && m->mb_x < m->mbmax_x && m->mb_y >= 0 && m->mb_y < m->mbmax_y;
+}
+
 static m2v_mb_t *rec_cur(mpeg2_dec_t *m)
 {
 	return &m->pic.mb[m->mb_y * m->mbmax_x + m->mb_x];
@@ -674,6 +680,7 @@ static int intra_mb(mpeg2_dec_t *m, h264_bits_t *b, int type, m2v_mb_t *r)
 	r->flags = M2V_REC_INTRA | (m->dct_type ? M2V_REC_DCT_FIELD : 0);
 	r->cbp = 63;
 	r->coef = (uint32_t)m->pic.n_coef;
+	if ((size_t)m->pic.n_coef + 6 * 64 > m->coef_cap) return -1; /* (an MB parsed twice: damaged slices) */
 	for (int i = 0; i < 6; ++i) {
 		int16_t *c = m->pic.coef + m->pic.n_coef;
 		m->coef[0] = (int16_t)intra_dc(m, b, i < 4 ? 0 : i - 3, &bad);
@@ -706,6 +713,7 @@ static int inter_mb(mpeg2_dec_t *m, h264_bits_t *b, int type, m2v_mb_t *r)
 		const int cbp = vlc(b, lut_cbp, CBP_BITS, &bad);
 		if (bad) return -1;
 		r->cbp = (uint8_t)cbp;
+		if ((size_t)m->pic.n_coef + 6 * 64 > m->coef_cap) return -1; /* (an MB parsed twice: damaged slices) */
 		for (int i = 0; i < 6; ++i)
 			if (cbp & (1 << (5 - i))) {
 				if (inter_block(m, b, m->pic.coef + m->pic.n_coef) < 0) return -1;
@@ -731,10 +739,18 @@ static int parse_mb(mpeg2_dec_t *m, h264_bits_t *b)
 			const int dc = (m->dc_max + 1) >> 1;
 			m->dc_pred[0] = m->dc_pred[1] = m->dc_pred[2] = (int16_t)dc;
 		}
-		return intra_mb(m, b, type, r);
+		if (intra_mb(m, b, type, r) < 0) goto bad;
+		return 0;
 	}
 	if (prev_intra) memset(m->pmv, 0, sizeof(m->pmv));
-	return inter_mb(m, b, type, r);
+	if (inter_mb(m, b, type, r) < 0) goto bad;
+	return 0;
+bad:
+	/* an undefined code inside the MB (damaged data): the record is dropped — its blocks may point past the
+	 * coefficients written — and the slice is abandoned by the caller */
+	r->flags = 0;
+	r->cbp = 0;
+	return -1;
 }
 
 /* skipped macroblocks before the current one (mb->skip_mb, mpeg2.cpp:740-766, 773-810): P (and I,
@@ -745,6 +761,7 @@ static void skip_mbs(mpeg2_dec_t *m, int n)
 	if (m->coding_type != M2V_B) {
 		for (int k = 0; k < n; ++k) {
 			inc_mb_pos(m);
+			if (!mb_inside(m)) break;
 			copy_mb(m);
 		}
 		mb_reset(m);
@@ -757,6 +774,7 @@ static void skip_mbs(mpeg2_dec_t *m, int n)
 		for (int k = 0; k < n; ++k) {
 			m2v_mb_t *r;
 			inc_mb_pos(m);
+			if (!mb_inside(m)) break;
 			r = rec_cur(m);
 			memset(r->mv, 0, sizeof(r->mv));
 			r->field_sel = 0;
@@ -829,6 +847,7 @@ static int slice(mpeg2_dec_t *m, h264_bits_t *b, int code)
 		if (bad) return 0;
 		if (1 < inc) skip_mbs(m, inc - 1);
 		inc_mb_pos(m);
+		if (!mb_inside(m)) return 0; /* an increment past the picture: slice abandoned */
 		if (parse_mb(m, b) < 0) return 0; /* undefined code: slice abandoned */
 		if (is_last(m)) {
 			m->mb_x = -1;

@@ -90,18 +90,18 @@ clean:
 
 # inter MB phase stamps (tools/stamps_interw.py)
 STW_LIB := build/dbg/libm2dec_amd_stampw.so
-$(STW_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o
+$(STW_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -DM2DEC_STAMPW -DM2DEC_NO_STAMPI -c $(HIP_SRC) -o build/dbg/recon_hip_stampw.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stampw.o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stampw.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o -Wl,--no-undefined
 
 stampw: $(STW_LIB)
 
 # deblocking filter sub-step stamps (tools/stamps_dbk.py)
 STD_LIB := build/dbg/libm2dec_amd_stampd.so
-$(STD_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o
+$(STD_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -DM2DEC_STAMPS -DM2DEC_STAMPD -DM2DEC_NO_STAMPI -c $(HIP_SRC) -o build/dbg/recon_hip_stampd.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stampd.o build/hip/runtime.o build/hip/m2v_hip.o -Wl,--no-undefined
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/dbg/recon_hip_stampd.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o -Wl,--no-undefined
 
 stampd: $(STD_LIB)

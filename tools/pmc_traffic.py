@@ -29,6 +29,9 @@ def per_dispatch(d):
             vals.setdefault(key, {})
             name = row["Counter_Name"]
             vals[key][name] = vals[key].get(name, 0.0) + float(row["Counter_Value"])
+            for g in ("Grid_Size", "Grid_Size_X"):
+                if g in row and row[g]:
+                    vals[key]["_grid"] = float(row[g])
     keys = sorted(vals)[1:] if KERNEL == "k_batch" else sorted(vals)  # k_batch: drop the parity-gate launch
     return [vals[k] for k in keys]
 
@@ -55,6 +58,16 @@ def main():
         out["write_bytes"] = int(w * 1024)
     if "read_bytes" in out and "write_bytes" in out:
         out["traffic_bytes"] = out["read_bytes"] + out["write_bytes"]
+    if KERNEL == "k_picture" and fetch and write and all("_grid" in v for v in fetch + write):
+        # the decode path launches 1..4 pictures at once: bytes per picture (sum over launches / pictures;
+        # a 1080p picture is 80 inter workers + 34 row-pair workgroups of 256 lanes), which bench.py scales
+        # by its own pictures per launch
+        bpp = 256 * (80 + 34)
+        pics_f = sum(v["_grid"] for v in fetch) / bpp
+        pics_w = sum(v["_grid"] for v in write) / bpp
+        out["traffic_bytes_per_picture"] = int(2 * 1024 * sum(v["FETCH_SIZE"] for v in fetch) / max(1.0, pics_f) +
+                                              1024 * sum(v["WRITE_SIZE"] for v in write) / max(1.0, pics_w))
+        out["pictures_per_launch"] = round(pics_f / len(fetch), 3)
     if hit:
         h = statistics.median(v["TCC_HIT_sum"] for v in hit)
         m = statistics.median(v["TCC_MISS_sum"] for v in hit)

@@ -1394,7 +1394,14 @@ __device__ __attribute__((noinline)) void intra_mb_wg(const int x, const int y, 
  * raises its done flag, which the picture's deblocking loader streams on.  The grid is kept small (a
  * fraction of the CUs) so that spinning items can never keep the work they wait for off the device.
  */
-__device__ void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *smem)
+/* (M2DEC_INTER_WORKER_NOINLINE: an out-of-line inter worker — r71: its MB loop spills more, 101 scratch
+ * operations per MB and wave instead of 63, so it stays inlined) */
+#ifdef M2DEC_INTER_WORKER_NOINLINE
+#define M2DEC_INTER_WORKER_ATTR __attribute__((noinline))
+#else
+#define M2DEC_INTER_WORKER_ATTR
+#endif
+__device__ M2DEC_INTER_WORKER_ATTR void inter_worker(const PictureArgs &a, const SlotSeq &ss, uint8_t *smem)
 {
 	__shared__ int s_item, s_rmin, s_rmax, s_cmax, s_intra, s_rec;
 	/* the item's MB records and the motion records of its inter MBs, staged once per item */

@@ -664,6 +664,43 @@ static void map_block(sctx_t *x, int plane, int px, int py, int log2, int t)
 static uint8_t scan_pos[3][4][64]; /* [scanIdx][log2 1..3 -> 0..2 used][k] */
 static pthread_once_t scan_once = PTHREAD_ONCE_INIT;
 
+/* sig_coeff_flag context offsets (9.3.4.2.5) by [size class: 4x4 / 8x8 diagonal (and chroma 8x8) / 8x8
+ * horizontal-vertical / 16+][chroma][prev csbf pattern 0..3][a sub-block other than the first][scan]
+ * [scan position k 0..15], H265_CTX_SIG-relative (chroma's +27 included): one table read per
+ * coefficient instead of the derivation's branches */
+static uint8_t sig_ctx_tab[4][2][4][2][3][16];
+
+static void build_sig_ctx(void)
+{
+	for (int cls = 0; cls < 4; ++cls)
+		for (int ch = 0; ch < 2; ++ch)
+			for (int prev = 0; prev < 4; ++prev)
+				for (int nf = 0; nf < 2; ++nf)
+					for (int scan = 0; scan < 3; ++scan)
+						for (int k = 0; k < 16; ++k) {
+							const int xp = scan_pos[scan][2][k] & 15, yp = scan_pos[scan][2][k] >> 4;
+							int sctx;
+							if (cls == 0) {
+								static const uint8_t m4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+								sctx = m4[(yp << 2) + xp];
+							} else if (!nf && xp + yp == 0) {
+								sctx = 0;
+							} else {
+								if (prev == 0) sctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
+								else if (prev == 1) sctx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
+								else if (prev == 2) sctx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
+								else sctx = 2;
+								if (!ch) {
+									if (nf) sctx += 3;
+									sctx += (cls == 1) ? 9 : (cls == 2 ? 15 : 21);
+								} else {
+									sctx += (cls == 3) ? 12 : 9;
+								}
+							}
+							sig_ctx_tab[cls][ch][prev][nf][scan][k] = (uint8_t)(sctx + (ch ? 27 : 0));
+						}
+}
+
 static void build_scans(void)
 {
 	for (int l = 1; l <= 3; ++l) {
@@ -682,6 +719,7 @@ static void build_scans(void)
 		for (int xx = 0; xx < n; ++xx)
 			for (int y = 0; y < n; ++y) scan_pos[2][l][k++] = (uint8_t)(xx | (y << 4)); /* vertical */
 	}
+	build_sig_ctx();
 }
 
 /* scanIdx from the intra mode (order_map, h265.cpp:2235-2244) */
@@ -731,6 +769,8 @@ static int residual_coding(sctx_t *x, int log2, int cidx, int scan, int is_intra
 		uint8_t csbf[8][8];
 		int last_sb = 0, last_pos = 0, greater1ctx = 1;
 		const int scale = x->scale[cidx];
+		/* size class of the sig_coeff_flag contexts (sig_ctx_tab); chroma 8x8 counts as diagonal */
+		const int cls = log2 == 2 ? 0 : (log2 == 3 ? ((scan == 0 || chroma) ? 1 : 2) : 3);
 		const int rnd = 1 << (log2 - 2), sh = log2 - 1;
 		memset(csbf, 0, sizeof(csbf));
 		/* the subblock and in-subblock scan positions of the last coefficient */
@@ -758,34 +798,15 @@ static int residual_coding(sctx_t *x, int log2, int cidx, int scan, int is_intra
 			if (!coded) continue;
 			/* sig_coeff_flag (9.3.4.2.5) for scan positions in the subblock, highest first */
 			int sig_pos[16], nsig = 0;
+			const uint8_t *const sctab = sig_ctx_tab[cls][chroma][prev][xs + ys > 0][scan];
 			for (int k = (i == last_sb) ? last_pos : 15; k >= 0; --k) {
-				const int xp = inscan[k] & 15, yp = inscan[k] >> 4;
-				const int xc = (xs << 2) + xp, yc = (ys << 2) + yp;
 				int sig;
 				if (i == last_sb && k == last_pos) {
 					sig = 1;
 				} else if (k == 0 && infer_dc && nsig == 0) {
 					sig = 1;
 				} else {
-					int sctx;
-					if (log2 == 2) {
-						static const uint8_t m4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-						sctx = m4[(yc << 2) + xc];
-					} else if (xc + yc == 0) {
-						sctx = 0;
-					} else {
-						if (prev == 0) sctx = (xp + yp == 0) ? 2 : (xp + yp < 3) ? 1 : 0;
-						else if (prev == 1) sctx = (yp == 0) ? 2 : (yp == 1) ? 1 : 0;
-						else if (prev == 2) sctx = (xp == 0) ? 2 : (xp == 1) ? 1 : 0;
-						else sctx = 2;
-						if (!chroma) {
-							if (xs + ys > 0) sctx += 3;
-							sctx += (log2 == 3) ? (scan == 0 ? 9 : 15) : 21;
-						} else {
-							sctx += (log2 == 3) ? 9 : 12;
-						}
-					}
-					sig = cab_decision(c, H265_CTX_SIG + (chroma ? 27 : 0) + sctx);
+					sig = cab_decision(c, H265_CTX_SIG + sctab[k]);
 				}
 				if (sig) sig_pos[nsig++] = k;
 			}

@@ -60,6 +60,8 @@ typedef struct md5_pipe {
 	int streams, ended;      /* streams using the pipe / past their last frame: hash at once */
 	int stats;
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
+	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
+	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
 	long batches;
@@ -83,8 +85,8 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
-		while (!p->quit && p->ended == 0 && p->head - p->next < MD5_MIN_BATCH) {
-			const double left = p->t_queued[p->next % MD5_RING] + MD5_WAIT_S - now_s();
+		while (!p->quit && p->ended == 0 && p->head - p->next < p->min_batch) {
+			const double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
 			struct timespec ts;
 			if (left <= 0) break;
 			clock_gettime(CLOCK_REALTIME, &ts);
@@ -172,6 +174,12 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	pthread_cond_init(&p->cv_job, NULL);
 	pthread_cond_init(&p->cv_free, NULL);
 	if (getenv("M2DEC_AMD_MD5_DELAY_US")) p->delay_us = atoi(getenv("M2DEC_AMD_MD5_DELAY_US"));
+	p->min_batch = MD5_MIN_BATCH;
+	p->wait_s = MD5_WAIT_S;
+	if (getenv("M2DEC_AMD_MD5_MIN_BATCH")) p->min_batch = atoi(getenv("M2DEC_AMD_MD5_MIN_BATCH")); /* tuning */
+	if (getenv("M2DEC_AMD_MD5_WAIT_US")) p->wait_s = 1e-6 * atoi(getenv("M2DEC_AMD_MD5_WAIT_US"));
+	if (p->min_batch < 1) p->min_batch = 1;
+	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	p->streams = streams;
 	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)

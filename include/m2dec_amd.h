@@ -201,6 +201,12 @@ int m2dec_amd_m2v_intra_ac(const uint8_t *bits, size_t n, int mpeg2, int intra_v
  * Returns the last decode_picture result (-2: end of the data). */
 int m2dec_amd_decode_h265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
                           void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
+/* The same loop with the `-O` MD5 line of every frame computed on the MD5 helper threads (16-lane batches,
+ * as m2dec_amd_decode_stream_md5): each delivered frame is copied into one of the driver's buffers and
+ * hashed there, since the H.265 frame LRU has no holds.  md5s: max x 35 bytes ("hex\r\n\0" each).
+ * Returns the frames (>= 0) or -1; *last_error gets decode_picture's last return (-2 at the end). */
+int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s, int max,
+                              int *last_error);
 /* Reconstruct an h265d_func context's pictures with `be` instead of the gfx950 back end (call after init,
  * before the first SPS; NULL detaches a borrowed one), or on GPU `device`. */
 int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be);

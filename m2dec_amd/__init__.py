@@ -533,6 +533,25 @@ def decode_h265(data: bytes, backend: Optional[Backend265] = None, device: int =
     return md5s, err.value
 
 
+def decode_h265_md5(data: bytes, backend: Optional[Backend265] = None, device: int = 0, max_frames: int = 4096) -> tuple:
+    """decode_h265 with the MD5 lines computed on the library's MD5 helper threads (16-lane batches) instead
+    of in Python on the caller's thread: (MD5 line of every output frame, last decode_picture result)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(35 * max_frames)
+    err = ctypes.c_int()
+    L.m2dec_amd_decode_h265_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Backend265), ctypes.c_int,
+                                            ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.m2dec_amd_decode_h265_md5.restype = ctypes.c_int
+    if backend is None and not L.m2dec_amd_hip_available():
+        raise RuntimeError("m2dec_amd: no usable gfx950 device for the H.265 reconstruction")
+    n = L.m2dec_amd_decode_h265_md5(data, len(data), ctypes.byref(backend) if backend is not None else None, device,
+                                    buf, max_frames, ctypes.byref(err))
+    if n < 0:
+        raise RuntimeError("m2dec_amd: H.265 MD5 decode failed")
+    raw = buf.raw
+    return [raw[35 * i:35 * i + 32].decode() for i in range(min(n, max_frames))], err.value
+
+
 class H265HipBackend:
     """The gfx950 H.265 reconstruction (m2dec_amd_h265_hip_backend_create), borrowed by decode_h265 so that
     its device buffers outlive one stream.  Raises if unavailable."""

@@ -251,6 +251,76 @@ int m2dec_amd_decode_stream_md5_backend(const uint8_t *data, size_t len, const m
 	return decode_md5(data, len, backend, 0, -1, parse_threads, md5_threads, md5s, max, stats);
 }
 
+/* ---- H.265 through the MD5 pipe (m2dec_amd_decode_h265_md5) */
+#define H265_MD5_RING 24 /* copies in flight: queued or being hashed */
+typedef struct {
+	md5_stream_t *s;
+	uint8_t *buf[H265_MD5_RING];
+	size_t bytes;
+	int next;
+	int failed;
+} h265_md5_t;
+
+static void h265_md5_on_frame(void *arg, const m2d_frame_t *f)
+{
+	h265_md5_t *h = (h265_md5_t *)arg;
+	const size_t ls = (size_t)f->width * (size_t)f->height, bytes = ls * 3 / 2;
+	uint8_t *b;
+	if (h->failed) return;
+	if (bytes != h->bytes) { /* (a new geometry: every queued copy hashed first) */
+		m2dec_hold_wait_idle(&h->s->hold);
+		for (int i = 0; i < H265_MD5_RING; ++i) {
+			free(h->buf[i]);
+			h->buf[i] = NULL;
+		}
+		h->bytes = bytes;
+	}
+	if (!h->buf[h->next] && !(h->buf[h->next] = (uint8_t *)malloc(bytes))) {
+		h->failed = 1;
+		return;
+	}
+	b = h->buf[h->next];
+	h->next = (h->next + 1) % H265_MD5_RING;
+	pthread_mutex_lock(&h->s->hold.mu); /* the buffer's previous frame is hashed */
+	while (m2dec_hold_busy(&h->s->hold, b)) pthread_cond_wait(&h->s->hold.cv, &h->s->hold.mu);
+	pthread_mutex_unlock(&h->s->hold.mu);
+	memcpy(b, f->luma, ls);
+	memcpy(b + ls, f->chroma, ls / 2);
+	{
+		m2d_frame_t c = *f;
+		c.luma = b;
+		c.chroma = b + ls;
+		md5_on_frame(h->s, &c);
+	}
+}
+
+int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s, int max,
+                              int *last_error)
+{
+	md5_pipe_t p;
+	md5_stream_t s;
+	h265_md5_t h;
+	int err = 0, r;
+	const char *e = getenv("M2DEC_AMD_MD5_THREADS");
+	if (pipe_open(&p, 1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS) < 0) return -1;
+	memset(&s, 0, sizeof(s));
+	s.pipe = &p;
+	s.md5s = md5s;
+	s.max = max;
+	m2dec_hold_init(&s.hold);
+	memset(&h, 0, sizeof(h));
+	h.s = &s;
+	r = m2dec_amd_decode_h265(data, len, be, device, 0, h265_md5_on_frame, &h, &err);
+	md5_on_end(&s);
+	m2dec_hold_wait_idle(&s.hold); /* every queued MD5 is written */
+	m2dec_hold_destroy(&s.hold);
+	pipe_close(&p);
+	for (int i = 0; i < H265_MD5_RING; ++i) free(h.buf[i]);
+	if (last_error) *last_error = err;
+	(void)r;
+	return h.failed ? -1 : s.n;
+}
+
 static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,
                       int parse_threads, int md5_threads, char *md5s, int max, m2dec_amd_stats_t *stats)
 {

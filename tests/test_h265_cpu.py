@@ -92,3 +92,14 @@ def test_p_slices_are_rejected(built):
         md5s, err = m2dec_amd.decode_h265(forged, backend=o.be)
     assert err == -2
     assert len(md5s) == 1
+
+
+@pytest.mark.parametrize("name", ["cov_h265_a_long_s3", "c_h265_1080p_s1"])
+def test_md5_driver_matches_golden(built, name):
+    """m2dec_amd_decode_h265_md5: the MD5 lines hashed on the helper threads from the driver's copies equal
+    the per-frame MD5s of the plain loop (and the goldens)."""
+    data = h265_stream(name)
+    with Oracle265Backend() as o:
+        md5s, err = m2dec_amd.decode_h265_md5(data, backend=o.be)
+    assert err == -2
+    assert md5s == GOLD[name]["md5"]

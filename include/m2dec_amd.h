@@ -207,6 +207,9 @@ int m2dec_amd_decode_h265(const uint8_t *data, size_t len, const h265r_backend_t
  * Returns the frames (>= 0) or -1; *last_error gets decode_picture's last return (-2 at the end). */
 int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s, int max,
                               int *last_error);
+/* MPEG-1/2 the same way (m2dec_amd_decode_m2v; device < 0: host reconstruction); -1 also when the GPU
+ * reconstruction was asked for and is unusable. */
+int m2dec_amd_decode_m2v_md5(const uint8_t *data, size_t len, int device, char *md5s, int max, int *last_error);
 /* Reconstruct an h265d_func context's pictures with `be` instead of the gfx950 back end (call after init,
  * before the first SPS; NULL detaches a borrowed one), or on GPU `device`. */
 int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be);

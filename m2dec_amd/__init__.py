@@ -552,6 +552,21 @@ def decode_h265_md5(data: bytes, backend: Optional[Backend265] = None, device: i
     return [raw[35 * i:35 * i + 32].decode() for i in range(min(n, max_frames))], err.value
 
 
+def decode_m2v_md5(data: bytes, device: Optional[int] = None, max_frames: int = 4096) -> List[str]:
+    """decode_m2v with the MD5 lines computed on the library's MD5 helper threads (m2dec_amd_decode_m2v_md5)."""
+    L = lib()
+    buf = ctypes.create_string_buffer(35 * max_frames)
+    err = ctypes.c_int()
+    L.m2dec_amd_decode_m2v_md5.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_int)]
+    L.m2dec_amd_decode_m2v_md5.restype = ctypes.c_int
+    n = L.m2dec_amd_decode_m2v_md5(data, len(data), -1 if device is None else device, buf, max_frames, ctypes.byref(err))
+    if n < 0:
+        raise RuntimeError(f"m2dec_amd: MPEG-2 MD5 decode on device {device} failed")
+    raw = buf.raw
+    return [raw[35 * i:35 * i + 32].decode() for i in range(min(n, max_frames))]
+
+
 class H265HipBackend:
     """The gfx950 H.265 reconstruction (m2dec_amd_h265_hip_backend_create), borrowed by decode_h265 so that
     its device buffers outlive one stream.  Raises if unavailable."""

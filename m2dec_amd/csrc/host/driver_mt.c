@@ -251,7 +251,8 @@ int m2dec_amd_decode_stream_md5_backend(const uint8_t *data, size_t len, const m
 	return decode_md5(data, len, backend, 0, -1, parse_threads, md5_threads, md5s, max, stats);
 }
 
-/* ---- H.265 through the MD5 pipe (m2dec_amd_decode_h265_md5) */
+/* ---- H.265 and MPEG-2 through the MD5 pipe (m2dec_amd_decode_h265_md5 / _m2v_md5): their frame LRUs
+ * know no holds, so each delivered frame is copied into one of the driver's buffers and hashed there */
 #define H265_MD5_RING 24 /* copies in flight: queued or being hashed */
 typedef struct {
 	md5_stream_t *s;
@@ -294,8 +295,8 @@ static void h265_md5_on_frame(void *arg, const m2d_frame_t *f)
 	}
 }
 
-int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s, int max,
-                              int *last_error)
+static int copy_md5(int codec, const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s,
+                    int max, int *last_error)
 {
 	md5_pipe_t p;
 	md5_stream_t s;
@@ -310,15 +311,26 @@ int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backe
 	m2dec_hold_init(&s.hold);
 	memset(&h, 0, sizeof(h));
 	h.s = &s;
-	r = m2dec_amd_decode_h265(data, len, be, device, 0, h265_md5_on_frame, &h, &err);
+	if (codec == 265) r = m2dec_amd_decode_h265(data, len, be, device, 0, h265_md5_on_frame, &h, &err);
+	else r = m2dec_amd_decode_m2v(data, len, device, 0, h265_md5_on_frame, &h, &err);
 	md5_on_end(&s);
 	m2dec_hold_wait_idle(&s.hold); /* every queued MD5 is written */
 	m2dec_hold_destroy(&s.hold);
 	pipe_close(&p);
 	for (int i = 0; i < H265_MD5_RING; ++i) free(h.buf[i]);
 	if (last_error) *last_error = err;
-	(void)r;
-	return h.failed ? -1 : s.n;
+	return h.failed || r == -3 ? -1 : s.n;
+}
+
+int m2dec_amd_decode_h265_md5(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, char *md5s, int max,
+                              int *last_error)
+{
+	return copy_md5(265, data, len, be, device, md5s, max, last_error);
+}
+
+int m2dec_amd_decode_m2v_md5(const uint8_t *data, size_t len, int device, char *md5s, int max, int *last_error)
+{
+	return copy_md5(2, data, len, NULL, device, md5s, max, last_error);
 }
 
 static int decode_md5(const uint8_t *data, size_t len, const m2r_backend_t *backend, int device, int dpb,

@@ -193,3 +193,9 @@ def test_gpu_reconstruction_has_no_host_fallback(built):
     silent host decode."""
     with pytest.raises(RuntimeError):
         m2dec_amd.decode_m2v(m2v_stream("cov_m2v_pb_s1"), device=64)
+
+
+@pytest.mark.parametrize("name", ["c1_480p_s1", "cov_m2v_pb_s1"])
+def test_md5_driver_matches_golden(built, name):
+    """m2dec_amd_decode_m2v_md5 (MD5 lines from the helper threads, host reconstruction) equals the goldens."""
+    assert m2dec_amd.decode_m2v_md5(m2v_stream(name)) == GOLD[name]["md5"]

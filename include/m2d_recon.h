@@ -138,8 +138,10 @@ typedef struct m2r_backend {
 	void (*destroy)(void *self);
 	int (*bind)(void *self, int vid, int slot);
 	/* optional (ABI revision 4): submit may hold pictures back to launch several at once; flush launches
-	 * every held one.  The decoder calls it after the last submit of a burst (bind, sync_frame,
-	 * set_frames and acquire flush implicitly).  NULL: every submit is launched as it comes. */
+	 * the held ones (0), or keeps them while the device is busy (1: the decoder calls it again on its next
+	 * step; bind launches a held picture anyway).  The decoder calls it after the last submit of a burst;
+	 * bind, set_frames and acquire launch held pictures implicitly.  NULL: every submit is launched as it
+	 * comes. */
 	int (*flush)(void *self);
 } m2r_backend_t;
 

@@ -273,6 +273,7 @@ struct Sched {
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
+	hipEvent_t last_launch[NSTREAMS] = {}; /* recorded after the latest decode-path launch on each stream */
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
 	hipEvent_t slot_write[64] = {};
@@ -494,6 +495,7 @@ struct Sched {
 		}
 		*inter_done = next_event();
 		CHECK(hipEventRecord(*inter_done, s));
+		last_launch[k] = *inter_done;
 		if (tev) CHECK(hipEventRecord(tev[0], s));
 		return 0;
 	}
@@ -865,6 +867,9 @@ struct HipBackend {
 	int nheld = 0;
 	int limit = 1;        /* pictures per launch of this context (fixed at set_frames) */
 	int narenas = 2 * NSTREAMS; /* record arenas in use: NSTREAMS * limit + limit + 2 (fixed at set_frames) */
+	bool hold_busy = false; /* M2DEC_AMD_HOLD_BUSY=1: flush keeps held pictures while every stream is busy (r73
+	                         * A/B on c3, medians of 10 decodes, 3 rounds: 42.3 / 41.1 / 40.7 ms vs 49.1 / 41.8 /
+	                         * 39.9 without — no gain over the box's noise, so off) */
 	int max_held = BMAX; /* M2DEC_AMD_PICS_PER_LAUNCH; also bounded by the budget (Sched::pics_fit: 2 at
 	                      * 1080p and 4K) and 1 while other decode-path back ends are alive.  r67 A/B on c3,
 	                      * median of 10 decodes: 1 -> 45.1 ms, 2 -> 42.6, 3 -> 41.3, 4 -> 43.3 */
@@ -873,7 +878,7 @@ struct HipBackend {
 	bool timing = true;
 };
 
-int be_flush(void *self);
+int launch_held(HipBackend *b);
 
 void flush_timing(HipBackend *b, TimingSlot &t)
 {
@@ -901,7 +906,7 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 {
 	HipBackend *b = (HipBackend *)self;
 	const double t0 = wall_s();
-	if (be_flush(b) < 0) return -1;
+	if (launch_held(b) < 0) return -1;
 	if (b->sc.sync_all() < 0) return -1;
 	if (b->copy) CHECK(hipStreamSynchronize(b->copy)); /* every staging copy is complete */
 	if (n > 64) n = 64;
@@ -988,7 +993,7 @@ m2r_picture_t *be_acquire(void *self, int wm, int hm)
 	HipBackend *b = (HipBackend *)self;
 	Arena &a = b->ar[b->next];
 	b->next = (b->next + 1) % b->narenas;
-	if (a.held && be_flush(b) < 0) return nullptr;
+	if (a.held && launch_held(b) < 0) return nullptr;
 	if (a.pending) {
 		/* the host copy is overwritten next: wait until that picture's kernels are done with it */
 		if (hipEventSynchronize(a.consumed) != hipSuccess) return nullptr;
@@ -1032,15 +1037,31 @@ int be_submit(void *self, m2r_picture_t *pic)
 	a->held = true;
 	/* a caller slot as the picture buffer (no decode ahead): copied out right behind its kernel, so
 	 * launched at once, as is a full hand */
-	if (!virt || b->nheld >= b->limit) return be_flush(b);
+	if (!virt || b->nheld >= b->limit) return launch_held(b);
 	return 0;
+}
+
+/* m2r_backend_t.flush, called by the decoder when a drive of its pipeline has nothing more to submit: while
+ * every stream still runs a launch, the held pictures wait (1: call again later — the next drive, or a
+ * bind, which launches them anyway), so that pictures parsed meanwhile join them in one launch; else
+ * they are launched now */
+int be_flush(void *self)
+{
+	HipBackend *b = (HipBackend *)self;
+	if (!b->nheld) return 0;
+	if (b->nheld < b->limit && b->hold_busy) {
+		int free_streams = 0;
+		for (int k = 0; k < NSTREAMS; ++k)
+			free_streams += !b->sc.last_launch[k] || hipEventQuery(b->sc.last_launch[k]) == hipSuccess;
+		if (!free_streams) return 1;
+	}
+	return launch_held(b) < 0 ? -1 : 0;
 }
 
 /* launch the held pictures as one k_picture on the next stream: their slots' waits, the record uploads,
  * the launch, then per picture the consumed event, the copy-out (caller slot), and the slot bookkeeping */
-int be_flush(void *self)
+int launch_held(HipBackend *b)
 {
-	HipBackend *b = (HipBackend *)self;
 	Sched &sc = b->sc;
 	const int n = b->nheld;
 	if (!n) return 0;
@@ -1102,7 +1123,7 @@ int be_bind(void *self, int vid, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	Sched &sc = b->sc;
-	if (be_flush(b) < 0) return -1; /* (the picture writing vid may be held) */
+	if (launch_held(b) < 0) return -1; /* (the picture writing vid may be held) */
 	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->nframes || !sc.slot_write[vid]) {
 		fprintf(stderr, "m2dec_amd: bind: picture buffer %d (written: %d) to frame %d rejected\n", vid,
 		        vid >= 0 && vid < 64 && sc.slot_write[vid] != nullptr, slot);
@@ -1234,6 +1255,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->bind = be_bind;
 	out->flush = be_flush;
 	g_live_backends[device & 15]++;
+	if (const char *e = getenv("M2DEC_AMD_HOLD_BUSY")) b->hold_busy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
 		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));

@@ -937,13 +937,14 @@ static void pipe_drive(struct h264_async *as)
 			}
 		}
 		if (as->held) {
-			/* nothing more to do for now: launch what this drive submitted (the back end may have held
-			 * pictures back to launch them together) */
+			/* nothing more to do for now: let the back end launch what it holds (it may keep them while the
+			 * device is busy, returning 1: the next drive asks again, and a bind launches them anyway) */
 			pthread_mutex_unlock(as->mu);
-			const int err = d->backend.flush(d->backend.self) < 0;
+			const int r = d->backend.flush(d->backend.self);
 			pthread_mutex_lock(as->mu);
+			as->sub_err += r < 0;
+			if (r > 0) break;
 			as->held = 0;
-			as->sub_err += err;
 			continue;
 		}
 		break;

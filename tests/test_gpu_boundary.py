@@ -45,3 +45,31 @@ def test_gpu_dropped_contexts_are_reclaimed(built, tmp_path):
     lines, md5 = harness(["-n", "3", "-k", F1, c3], oracle=False, env={"M2DEC_AMD_MAX_CONTEXTS": "3"})
     assert md5 == (f1 + gold) * 3
     assert max(x["contexts"] for x in iters(lines)) <= 3
+
+
+def test_gpu_resize_while_other_streams_run(built, tmp_path):
+    """One stream grows its geometry mid-stream (F1 then a 352x288 stream: the driver's header callback
+    hands the old frame block back to the process-wide pool and takes a bigger one) while three 1080p
+    streams decode concurrently in the same process (m2dec_amd_decode_streams_md5) and may take that
+    block from the pool at once: every 1080p frame, F1's frames before the reallocation and the second
+    stream's frames stay exact (frames still in the DPB at the reallocation are undefined, as in the
+    reference: tests/test_boundary_cpu.py)."""
+    import m2dec_amd
+    s = gen(tmp_path, "resize")
+    _, alone = harness([s])                                  # oracle
+    cat = open(F1, "rb").read() + open(s, "rb").read()
+    catp = str(tmp_path / "cat.264")
+    open(catp, "wb").write(cat)
+    lines, _ = harness([catp])                               # oracle: where the reallocation falls
+    frames = [ln for ln in lines if not ln.startswith("#iter")]
+    assert "#realloc" in frames
+    k = frames.index("#realloc")
+    f1 = golden_md5s(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"))
+    names = [f"c4_1080p_s{i}" for i in (2, 3, 4)]
+    for rep in range(2):
+        got = m2dec_amd.decode_streams([cat] + [stream(n) for n in names])
+        assert len(got[0]) == len(f1) + len(alone), rep
+        assert got[0][:k] == f1[:k], rep
+        assert got[0][-len(alone):] == alone, rep
+        for n, g in zip(names, got[1:]):
+            assert g == GOLDEN[n]["md5"], (rep, n)

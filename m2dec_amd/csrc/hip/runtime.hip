@@ -31,6 +31,8 @@
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
+extern "C" void m2d_tl(int kind, long a, long b); /* timeline.c (M2DEC_AMD_TIMELINE diagnostics) */
+
 namespace {
 
 static double wall_s()
@@ -1069,6 +1071,7 @@ int launch_held(HipBackend *b)
 	CHECK(hipSetDevice(sc.dev));
 	const int k = sc.pick();
 	hipStream_t s = sc.st[k];
+	m2d_tl('L', n, k);
 	PicJob jobs[BMAX];
 	for (int i = 0; i < n; ++i) {
 		jobs[i] = b->held[i].j;
@@ -1150,7 +1153,9 @@ int be_sync(void *self, int slot)
 	 * flush — those three, acquire and set_frames are the serial back-end calls.  The slot's picture was
 	 * launched when it was bound, or when it was submitted without decode ahead.) */
 	if (b->slot_pending[slot]) {
+		m2d_tl('Y', slot, 0);
 		CHECK(hipEventSynchronize(b->slot_ev[slot]));
+		m2d_tl('y', slot, 0);
 		if (b->sc.check_err() < 0) return -1;
 		if (b->timing) {
 			float ms;

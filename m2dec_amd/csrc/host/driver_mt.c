@@ -112,7 +112,9 @@ static void *md5_worker(void *arg)
 		if (p->delay_us) usleep((useconds_t)p->delay_us); /* (tests: MD5 slower than the decoder) */
 		char lines[MD5_BATCH][35];
 		const double th = now_s();
+		m2d_tl('H', n, n ? ix[0] : -1);
 		m2dec_amd_frames_md5(f, n, lines);
+		m2d_tl('h', n, n ? ix[0] : -1);
 		const double th1 = now_s();
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
@@ -144,6 +146,7 @@ static void md5_on_frame(void *arg, const m2d_frame_t *f)
 	if (p->stats) p->t_wait += now_s() - t0;
 	p->frm[k] = *f;
 	p->of[k] = s;
+	m2d_tl('O', s->n, 0);
 	p->idx[k] = s->n++;
 	p->t_queued[k] = now_s();
 	p->state[k] = 1;
@@ -222,6 +225,7 @@ static int stream_md5(md5_pipe_t *p, const uint8_t *data, size_t len, const m2r_
 	m2dec_hold_init(&s.hold);
 	memset(&st, 0, sizeof(st));
 	const char *ex = getenv("M2DEC_AMD_MD5_EXTRA"); /* (tests: fewer spare frames -> the decoder waits on holds) */
+	m2d_tl('D', 0, 0);
 	r = h264_decode_stream_held(data, len, backend, device, dpb, parse_threads, ex ? atoi(ex) : MD5_EXTRA, &s.hold,
 	                            md5_on_frame, md5_on_end, &s, &st);
 	md5_on_end(&s); /* (a decode that failed early did not reach on_end: do not hold the pipe up) */
@@ -231,6 +235,7 @@ static int stream_md5(md5_pipe_t *p, const uint8_t *data, size_t len, const m2r_
 	if (s.t_done > st.t_end) st.t_end = s.t_done; /* delivered = its MD5 line written */
 	pthread_mutex_unlock(&p->mu);
 	st.hold_waits = s.hold.waits;
+	m2d_tl('d', s.n, 0);
 	if (stats) *stats = st;
 	return r < 0 ? r : s.n;
 }

@@ -46,10 +46,13 @@ static double mono_s(void)
  *   - a state whose context the caller dropped is reclaimed by the registry: when init() is called
  *     on the same context address again (the caller reuses the memory), or when a new context
  *     would bring the registry over M2DEC_AMD_MAX_CONTEXTS (default 8) — then the least recently
- *     used state that finished its stream (decode_picture returned -2) or was not called for
- *     M2DEC_AMD_IDLE_EVICT_S seconds (default 30) goes first; at twice the cap, one idle for a second.
- *     A state is never reclaimed during a call on it.  Calls on a reclaimed context fail (-1;
- *     stream_pos returns an empty reader).
+ *     used state that is done with its stream goes first: decode_picture returned -2 AND a later
+ *     peek / get found the DPB empty (M2Decoder::decode drains it with peek / get after -2,
+ *     m2decoder.h:136-141, so a state is never taken out from under that loop).  A live stream is
+ *     never evicted for being idle unless M2DEC_AMD_IDLE_EVICT_S is set (opt-in: states not called
+ *     for that many seconds become reclaimable too).  A state is never reclaimed during a call on it.
+ *     Calls on a reclaimed context fail without looping the reference's drivers: decode_picture
+ *     returns -1, peek / get return 0 (no frame), stream_pos returns an empty reader.
  *   - m2dec_amd_h264_release() still frees a context at once (optional). */
 typedef struct {
 	uint64_t magic;
@@ -116,7 +119,8 @@ h264_dec_t *h264_state(void *ctx)
 static int reclaim_victims(const void *ctx, h264_dec_t **out, int max)
 {
 	const int cap = env_int("M2DEC_AMD_MAX_CONTEXTS", 8);
-	const double idle = (double)env_int("M2DEC_AMD_IDLE_EVICT_S", 30), now = mono_s();
+	const int idle_on = getenv("M2DEC_AMD_IDLE_EVICT_S") && *getenv("M2DEC_AMD_IDLE_EVICT_S");
+	const double idle = (double)env_int("M2DEC_AMD_IDLE_EVICT_S", 0), now = mono_s();
 	int n = 0;
 	for (h264_dec_t **pp = &reg_head; *pp && n < max;) {
 		h264_dec_t *d = *pp;
@@ -130,12 +134,10 @@ static int reclaim_victims(const void *ctx, h264_dec_t **out, int max)
 		}
 	}
 	while (reg_count >= cap && n < max) {
-		/* over twice the cap, any state idle for a second goes too (it is most likely dropped) */
-		const double lim = reg_count >= 2 * cap ? (idle < 1.0 ? idle : 1.0) : idle;
 		h264_dec_t **best = NULL;
 		for (h264_dec_t **pp = &reg_head; *pp; pp = &(*pp)->reg_next) {
 			const h264_dec_t *d = *pp;
-			if (d->in_call || !(d->finished || !d->owner || now - d->last_call >= lim)) continue;
+			if (d->in_call || !((d->finished && d->drained) || !d->owner || (idle_on && now - d->last_call >= idle))) continue;
 			if (!best || d->last_call < (*best)->last_call) best = pp;
 		}
 		if (!best) break;
@@ -396,10 +398,15 @@ static int api_decode_picture(void *ctx)
 	h264_dec_t *d = enter(ctx);
 	int r;
 	if (!d) return -1;
+	if (d->fault) { /* a frame could not be delivered (deliver): the stream is broken */
+		leave(d);
+		return -1;
+	}
 	d->eos = 0;
 	if (d->as) h264_async_resume(d);
 	r = h264_decode_loop(d);
 	d->finished = r == -2;
+	d->drained = 0;
 	if (d->finished) h264_async_trim(d);
 	leave(d);
 	return r;
@@ -408,12 +415,24 @@ static int api_decode_picture(void *ctx)
 static int deliver(h264_dec_t *d, int idx, m2d_frame_t *frame)
 {
 	double t0 = 0, t1 = 0;
-	if (idx < 0) return 0;
+	if (idx < 0) {
+		if (d->finished) d->drained = 1; /* the caller has every frame of its stream */
+		return 0;
+	}
 	if (d->stats) t0 = mono_s();
-	if (d->as && h264_async_drain(d, idx) < 0) return -1; /* the picture in that slot is parsed and submitted */
+	/* a failure here (a submission / bind error, a device fault) delivers no frame and fails the next
+	 * decode_picture: peek returning -1 would spin M2Decoder's `while (peek(ctx, &frm, 1))` drain
+	 * (m2decoder.h:138) forever */
+	if (d->as && h264_async_drain(d, idx) < 0) { /* the picture in that slot is parsed and submitted */
+		d->fault = 1;
+		return 0;
+	}
 	if (d->stats) t1 = mono_s();
 	/* (sync_frame copies the picture into the caller's frame, on this thread, inside this call) */
-	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) return -1;
+	if (d->have_backend && d->backend.sync_frame(d->backend.self, idx) < 0) {
+		d->fault = 1;
+		return 0;
+	}
 	if (d->stats) {
 		d->t_drain += t1 - t0;
 		d->t_sync += mono_s() - t1;
@@ -426,7 +445,7 @@ static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
 {
 	h264_dec_t *d = enter(ctx);
 	int r;
-	if (!d) return -1;
+	if (!d) return 0; /* reclaimed: no frame (a -1 would keep `while (peek(ctx, &f, 1))` loops going) */
 	r = frame ? deliver(d, h264_dpb_peek(&d->dpb, bypass), frame) : -1;
 	leave(d);
 	return r;
@@ -436,7 +455,7 @@ static int api_get(void *ctx, m2d_frame_t *frame, int bypass)
 {
 	h264_dec_t *d = enter(ctx);
 	int r;
-	if (!d) return -1;
+	if (!d) return 0;
 	r = frame ? deliver(d, h264_dpb_pop(&d->dpb, bypass), frame) : -1;
 	leave(d);
 	return r;

@@ -551,6 +551,7 @@ static void *pool_worker(void *arg)
 			pj->sl_done++;
 		} else {
 			const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
+			m2d_tl('P', j->seq, j->snap[0]->sh.slice_type);
 			if (dep_err) j->err = 1;
 			else if (!(as->slice_par && j->nsl > 1)) job_run(j);
 			else if (job_run_par(as, j) < 0) {
@@ -561,6 +562,7 @@ static void *pool_worker(void *arg)
 			}
 			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
+			m2d_tl('p', j->seq, j->snap[0]->sh.slice_type);
 			as->t_parse += te - tp;
 			if (as->stats > 1)
 				fprintf(stderr, "job %ld type %d slices %d: start %.1f ms, parse %.2f ms\n", j->seq,
@@ -905,7 +907,9 @@ static void pipe_drive(struct h264_async *as)
 			h264_job_t *j = as->fifo[as->bnd % AS_MAX];
 			const int skip = j->sub_err, vid = j->vid & 63, slot = j->slot;
 			pthread_mutex_unlock(as->mu);
+			m2d_tl('B', vid, slot);
 			const int err = !skip && d->backend.bind(d->backend.self, vid, slot) < 0;
+			m2d_tl('b', vid, slot);
 			pthread_mutex_lock(as->mu);
 			j->bound = 1;
 			as->sub_err += err;
@@ -924,7 +928,9 @@ static void pipe_drive(struct h264_async *as)
 				const int ahead = as->sub >= as->a_seq;
 				pthread_mutex_unlock(as->mu);
 				if (as->stats > 1 && j->err) fprintf(stderr, "job %ld: parse error, not submitted\n", j->seq);
+				m2d_tl('S', j->seq, 0);
 				const int err = j->err || copy_submit(d, j, 1);
+				m2d_tl('s', j->seq, 0);
 				pthread_mutex_lock(as->mu);
 				j->sub_err = err;
 				j->submitted = 1;

@@ -365,6 +365,8 @@ struct h264_dec {
 	int in_call;             /* API calls in progress (registry mutex) */
 	double last_call;        /* CLOCK_MONOTONIC seconds of the last API call */
 	int finished;            /* the last decode_picture returned -2 (end of the data) */
+	int drained;             /* ... and a peek / get since then found the DPB empty (registry: reclaimable) */
+	int fault;               /* a frame could not be delivered: every later decode_picture returns -1 */
 };
 
 /* h264_syntax.c */
@@ -384,6 +386,9 @@ int h264_dpb_pop(h264_dpb_t *dpb, int bypass);
 int h264_slice_data(h264_dec_t *d);
 
 /* h264_async.c */
+/* timeline.c: M2DEC_AMD_TIMELINE diagnostics (no-op unless set) */
+void m2d_tl(int kind, long a, long b);
+
 int h264_async_start(h264_dec_t *d, int threads);
 int h264_async_add_slice(h264_dec_t *d);
 int h264_async_close(h264_dec_t *d);

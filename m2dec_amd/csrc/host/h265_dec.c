@@ -196,6 +196,9 @@ static void st_rps_pred(perr_t *e, h264_bits_t *b, h265_st_rps_t *dst, const h26
 	const int num = ref->num_pics[0] + ref->num_pics[1];
 	uint32_t used_flag = 0, use_delta = 0;
 	int cnt = 0;
+	/* a predicted set holds at most num + 1 entries; delta_poc[s] has 16 per side, so a reference set of
+	 * 16 (the most st_rps_nopred lets through; a conformant one has <= 15) cannot be predicted from */
+	if (num >= 16) H265_ERR(e);
 	for (int j = 0; j <= num; ++j) {
 		const uint32_t used_by = hb_get1(b);
 		cnt += (int)used_by;
@@ -382,10 +385,13 @@ static void parse_slice_header(perr_t *e, h264_bits_t *b, const h265_sps_t *s, c
 		if (hb_get1(b)) {
 			int idx = 0;
 			if (s->num_st_rps > 1) idx = (int)hb_get(b, log2ceil((uint32_t)s->num_st_rps));
+			/* the reference reads log2ceil(n) bits, one more than the spec for a power of two (kept), and
+			 * never checks the index against the SPS's sets */
+			if (idx >= s->num_st_rps) H265_ERR(e);
 			sh->rps = s->st_rps[idx];
 		} else {
 			if (s->num_st_rps && hb_get1(b)) {
-				const int dm1 = ue_max(e, b, (uint32_t)s->num_st_rps);
+				const int dm1 = ue_max(e, b, (uint32_t)s->num_st_rps - 1);
 				st_rps_pred(e, b, &sh->rps, &s->st_rps[s->num_st_rps - dm1 - 1]);
 			} else {
 				st_rps_nopred(e, b, &sh->rps);

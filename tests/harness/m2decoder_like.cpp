@@ -34,6 +34,7 @@ extern "C" {
 static int (*g_oracle_create)(m2r_backend_t *);
 static int g_threads = -1;
 static int g_keep = 0;
+static int g_pause = 0; /* -p: all streams to their end, then drain (tests/test_boundary_cpu.py) */
 
 class Frames {
 	size_t luma_len_;
@@ -133,11 +134,27 @@ public:
 	}
 	~Decoder()
 	{
+		fwrite(out.data(), 1, out.size(), stdout);
 		delete frames_;
 		if (!g_keep) delete[] context_; /* no release: the reference API has none */
 	}
+	/* -p: the frames of this decoder go to `out` (printed when it is deleted), and run() returns at the
+	 * end of the data without draining the DPB: drain() does that later, after other contexts were made */
+	std::string out;
+	bool paused = false;
+	int drain()
+	{
+		m2d_frame_t frm;
+		int n = 0;
+		while (func_->peek_decoded_frame(context_, &frm, 1)) {
+			emit(frm);
+			n++;
+			func_->get_decoded_frame(context_, &frm, 1);
+		}
+		return n;
+	}
 	/* M2Decoder::decode / decode_residual; returns frames written, stops after max (>= 0) */
-	int run(int max)
+	int run(int max, bool stop_at_end = false)
 	{
 		m2d_frame_t frm;
 		int n = 0;
@@ -145,7 +162,12 @@ public:
 			while (func_->peek_decoded_frame(context_, &frm, 0) <= 0) {
 				const int err = func_->decode_picture(context_);
 				if (err < 0) {
-					while (func_->peek_decoded_frame(context_, &frm, 1) > 0) {
+					if (stop_at_end) {
+						paused = true;
+						return n;
+					}
+					/* m2decoder.h:138 tests peek's result for truth, so -1 would loop here as it does there */
+					while (func_->peek_decoded_frame(context_, &frm, 1)) {
 						if (max >= 0 && n >= max) return n;
 						emit(frm);
 						n++;
@@ -159,6 +181,10 @@ public:
 			emit(frm);
 			n++;
 			if (func_->decode_picture(context_) < 0) {
+				if (stop_at_end) {
+					paused = true;
+					return n;
+				}
 				while (func_->peek_decoded_frame(context_, &frm, 1) > 0) {
 					if (max >= 0 && n >= max) return n;
 					emit(frm);
@@ -169,11 +195,12 @@ public:
 			}
 		}
 	}
-	static void emit(const m2d_frame_t &f)
+	void emit(const m2d_frame_t &f)
 	{
 		char line[35];
 		m2dec_amd_frame_md5(&f, line);
-		fwrite(line, 1, 34, stdout);
+		if (g_pause) out.append(line, 34);
+		else fwrite(line, 1, 34, stdout);
 	}
 };
 
@@ -207,8 +234,10 @@ int main(int argc, char **argv)
 			max = atoi(argv[++i]);
 		} else if (!strcmp(argv[i], "-k")) {
 			g_keep = 1;
+		} else if (!strcmp(argv[i], "-p")) {
+			g_pause = 1;
 		} else {
-			fprintf(stderr, "usage: %s [-o liboracle.so] [-t threads] [-n iters] [-m max] stream...\n", argv[0]);
+			fprintf(stderr, "usage: %s [-o liboracle.so] [-t threads] [-n iters] [-m max] [-k] [-p] stream...\n", argv[0]);
 			return 2;
 		}
 	}
@@ -224,7 +253,25 @@ int main(int argc, char **argv)
 		data.push_back(s);
 	}
 	for (int it = 0; it < iters; ++it) {
+		if (g_pause) {
+			/* every stream decoded to its end (decode_picture -2) with its DPB not drained yet, all
+			 * contexts alive at once; then each is drained the way M2Decoder::decode does */
+			std::vector<Decoder *> ds;
+			for (auto &s : data) {
+				ds.push_back(new Decoder((const uint8_t *)s.data(), s.size()));
+				ds.back()->run(max, true);
+			}
+			int ctxs = 0;
+			long ev = 0;
+			m2dec_amd_h264_registry(&ctxs, &ev);
+			printf("#paused contexts %d evicted %ld\n", ctxs, ev);
+			for (Decoder *d : ds) {
+				d->drain();
+				delete d;
+			}
+		}
 		for (auto &s : data) {
+			if (g_pause) break;
 			Decoder *d = new Decoder((const uint8_t *)s.data(), s.size());
 			d->run(max);
 			delete d;

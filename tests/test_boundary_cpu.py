@@ -120,3 +120,19 @@ def test_context_cap_without_address_reuse(built, tmp_path):
                          env={"M2DEC_AMD_MAX_CONTEXTS": "4", "M2DEC_AMD_IDLE_EVICT_S": "0"})
     st = iters(lines)
     assert max(x["contexts"] for x in st) <= 4
+
+
+def test_finished_undrained_contexts_are_kept(built, tmp_path):
+    """ADVICE r3: after decode_picture returns -2, M2Decoder::decode still drains the DPB with
+    `while (peek_decoded_frame(ctx, &frm, 1))` (m2decoder.h:136-141).  A state in that window must not be
+    reclaimed when other contexts are created over the cap: four streams decoded to their end, none
+    drained, at M2DEC_AMD_MAX_CONTEXTS=2 — all four stay, then every frame comes out exactly."""
+    s = gen(tmp_path, "fit")
+    _, plain = harness(["-t", "4", F1, s, F1, s])
+    lines, md5 = harness(["-t", "4", "-p", "-k", F1, s, F1, s], env={"M2DEC_AMD_MAX_CONTEXTS": "2"})
+    paused = [ln for ln in lines if ln.startswith("#paused")]
+    assert paused and "contexts 4 evicted 0" in paused[0], paused
+    assert md5 == plain
+    # once drained they are reclaimable: the next contexts over the cap take their places
+    lines, _ = harness(["-t", "4", "-n", "3", "-p", "-k", F1, s], env={"M2DEC_AMD_MAX_CONTEXTS": "2"})
+    assert max(x["contexts"] for x in iters(lines)) <= 2

@@ -106,3 +106,77 @@ def test_damaged_streams_do_not_crash(built, codec, script):
                        env=env, cwd=ROOT)
     assert r.returncode == 0, (codec, r.returncode, r.stderr.decode()[-3000:])
     assert b"decoded 36" in r.stdout, r.stdout.decode()[-500:]
+
+
+H265_RPS_CHAIN = textwrap.dedent("""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, ROOT + "/tests")
+    import m2dec_amd
+    from _oracle import Oracle265Backend
+    from test_h265_cpu import h265_stream
+
+    class W:
+        def __init__(self):
+            self.bits = []
+        def u(self, v, n):
+            self.bits += [(v >> (n - 1 - i)) & 1 for i in range(n)]
+        def ue(self, v):
+            v += 1
+            n = v.bit_length()
+            self.u(0, n - 1)
+            self.u(v, n)
+        def rbsp(self):
+            self.bits.append(1)
+            while len(self.bits) % 8:
+                self.bits.append(0)
+            raw = bytes(int("".join(map(str, self.bits[i:i + 8])), 2) for i in range(0, len(self.bits), 8))
+            out, z = bytearray(), 0
+            for c in raw:  # emulation prevention
+                if z >= 2 and c <= 3:
+                    out.append(3)
+                    z = 0
+                out.append(c)
+                z = z + 1 if c == 0 else 0
+            return bytes(out)
+
+    def sps(chain):
+        w = W()
+        w.u(0, 4); w.u(0, 3); w.u(1, 1)
+        w.u(1, 8); w.u(0x60000000, 32); w.u(0, 24); w.u(0, 24); w.u(93, 8)  # profile_tier_level, 96 bits
+        w.ue(0); w.ue(1); w.ue(64); w.ue(64); w.u(0, 1)   # sps 0, 4:2:0, 64x64, no cropping
+        w.ue(0); w.ue(0); w.ue(4)                          # 8-bit, log2_max_poc_lsb 8
+        w.u(1, 1); w.ue(4); w.ue(0); w.ue(0)               # sub-layer ordering
+        w.ue(0); w.ue(1); w.ue(0); w.ue(3); w.ue(1); w.ue(1)   # CB 8..16, TB 4..32, depths
+        w.u(0, 1); w.u(0, 1); w.u(0, 1); w.u(0, 1)         # no scaling lists / AMP / SAO / PCM
+        w.ue(chain)
+        w.ue(1); w.ue(0); w.ue(0); w.u(1, 1)               # set 0: one negative picture (-1), used
+        for i in range(1, chain):                           # set i from set i-1: delta_rps -1, every entry kept
+            w.u(1, 1); w.u(1, 1); w.ue(0)
+            w.bits += [1] * (i + 1)                         # used_by_curr_pic_flag of the i + 1 candidates
+        w.u(0, 1); w.u(0, 1); w.u(0, 1); w.u(0, 1); w.u(0, 1)  # no long-term, TMVP, smoothing, VUI, ext
+        return b"\\x00\\x00\\x00\\x01\\x42\\x01" + w.rbsp()
+
+    data = h265_stream("cov_h265_a_s1")
+    at = data.find(b"\\x00\\x00\\x00\\x01\\x42\\x01")
+    end = data.find(b"\\x00\\x00\\x01", at + 4)
+    assert at >= 0 and end > at
+    for chain in (15, 16, 17, 40, 64):
+        # set k holds k + 1 entries, so set 16 would be predicted from 16 (> 16 after prediction)
+        forged = data[:at] + sps(chain) + data[end - (1 if data[end - 1] == 0 else 0):]
+        with Oracle265Backend() as o:
+            md5s, err = m2dec_amd.decode_h265(forged, backend=o.be)
+        assert err in (-1, -2), err
+        print("chain", chain, "frames", len(md5s), "err", err)
+    print("done")
+""")
+
+
+def test_h265_chained_inter_rps_is_bounded(built):
+    """an SPS whose inter-RPS predictions chain (each set one entry longer than the one it is
+    predicted from) must end in an error once a set would exceed the 16 entries of a reference picture set,
+    not write past h265_st_rps_t.delta_poc (a stack overflow of parse_sps's SPS copy)."""
+    r = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + H265_RPS_CHAIN], capture_output=True, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, (r.returncode, r.stderr.decode()[-3000:])
+    assert b"done" in r.stdout, r.stdout.decode()[-500:]

@@ -1,31 +1,175 @@
-"""Multi-GPU work-queue hand-off: independent streams, one per rank.
+"""Multi-GPU work queue: independent streams sharded over the ranks of one node.
 
-The data path has no collective.  The only exchanges are
-  * a broadcast of the job table (one stream seed per rank) from rank 0, and
-  * an all-gather of per-rank counters (pictures decoded, seconds) at the end,
-over torch.distributed: backend "nccl" (= RCCL over xGMI) with device tensors on the GPU box,
-"gloo" with CPU tensors in the CPU tests.
-"""
-from typing import List, Tuple
+One process per GPU.  The data path has no collective; the only exchanges are the work-queue
+hand-off below, over torch.distributed — backend "nccl" (= RCCL over xGMI) with device tensors on
+the GPU box, "gloo" with CPU tensors in the CPU tests:
+
+  * rank 0 owns the job list (stream id, seed, cost in pictures) and broadcasts it (`broadcast_jobs`);
+  * every rank derives the same assignment from it (`plan`: longest-processing-time first onto the
+    least loaded rank, so S >= N streams of unequal length balance), runs its jobs, and then
+  * a completion round all-gathers one row per job from every rank (`run_queue`): done, bit-exact,
+    frames, seconds.  Each job must be completed by exactly one rank; a job that failed or that no
+    rank completed is dealt again, round robin, in the next round (bounded rounds);
+  * counters are all-gathered at the end (`gather_counters`), and the per-rank parity results
+    all-reduced (`all_ranks`).
+
+bench.py's multi-rank orchestration is `timed_steps` (warmup, barrier + device sync, K timed steps,
+barrier, max-over-ranks time) over `run_queue`; tests/test_dist_gloo.py runs the same functions at
+world size 2 over 5 jobs on the CPU."""
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence, Tuple
+
+Job = Tuple[int, int, int]  # (job id, stream seed, cost: pictures)
+
+
+def make_jobs(n: int, first_seed: int = 1, cost: int = 60) -> List[Job]:
+    """Rank 0's job list: n independent streams, seeds first_seed.. (bench: C4 = one c3 stream per seed)."""
+    return [(i, first_seed + i, cost) for i in range(n)]
+
+
+def broadcast_jobs(dist, world: int, rank: int, jobs: Optional[Sequence[Job]], device: str) -> List[Job]:
+    """Rank 0's job list to every rank (two broadcasts: the count, then the table).  Other ranks pass None."""
+    if dist is None or world == 1:
+        return [tuple(int(x) for x in j) for j in jobs]
+    import torch
+
+    n = torch.tensor([len(jobs) if rank == 0 else 0], dtype=torch.int64, device=device)
+    dist.broadcast(n, 0)
+    t = torch.zeros((int(n.item()), 3), dtype=torch.int64, device=device)
+    if rank == 0:
+        t.copy_(torch.tensor([list(j) for j in jobs], dtype=torch.int64))
+    dist.broadcast(t, 0)
+    return [tuple(int(x) for x in row) for row in t.tolist()]
+
+
+def plan(jobs: Sequence[Job], world: int) -> List[List[Job]]:
+    """Longest-processing-time assignment: jobs by cost (descending, then id), each onto the rank with the
+    least cost so far (lowest rank on ties).  Deterministic, so every rank computes the same plan."""
+    load = [0] * world
+    out: List[List[Job]] = [[] for _ in range(world)]
+    for j in sorted(jobs, key=lambda j: (-j[2], j[0])):
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(j)
+        load[r] += j[2]
+    for o in out:
+        o.sort(key=lambda j: j[0])
+    return out
+
+
+@dataclass
+class QueueResult:
+    owner: List[int]                # job -> rank that completed it (-1: never)
+    frames: List[int]               # job -> frames delivered
+    seconds: List[float]            # job -> seconds its decode took
+    ok: List[bool]                  # job -> bit-exact
+    rank_seconds: List[float]       # rank -> sum of its jobs' seconds
+    rounds: int
+    attempts: List[int] = field(default_factory=list)  # job -> times it was run
+
+    @property
+    def total_frames(self) -> int:
+        return sum(self.frames)
+
+    @property
+    def all_ok(self) -> bool:
+        return all(self.ok) and all(o >= 0 for o in self.owner)
+
+
+def run_queue(dist, world: int, rank: int, jobs: Sequence[Job],
+              work: Callable[[Job], Tuple[int, float, bool]], device: str, max_rounds: int = 3) -> QueueResult:
+    """Run the job list over the ranks: round 0 follows `plan`; after each round a completion round
+    all-gathers one row (done, ok, frames, seconds) per job and rank; jobs left undone or not bit-exact are
+    dealt round robin in the next round.  `work(job)` -> (frames, seconds, bit-exact); an exception counts
+    as a failed attempt.  Every rank returns the same QueueResult."""
+    S = len(jobs)
+    idx = {j[0]: i for i, j in enumerate(jobs)}
+    owner, frames, secs, ok = [-1] * S, [0] * S, [0.0] * S, [False] * S
+    attempts = [0] * S
+    mine = plan(jobs, world)[rank]
+    rounds = 0
+    while rounds < max_rounds:
+        rounds += 1
+        row = [[0.0] * 4 for _ in range(S)]
+        for j in mine:
+            try:
+                f, s, good = work(j)
+            except Exception:  # noqa: BLE001 - a failed attempt; dealt again next round
+                f, s, good = 0, 0.0, False
+            row[idx[j[0]]] = [1.0, 1.0 if good else 0.0, float(f), float(s)]
+        if dist is None or world == 1:
+            rows = [row]
+        else:
+            import torch
+
+            r = torch.tensor(row, dtype=torch.float64, device=device)
+            rr = [torch.zeros_like(r) for _ in range(world)]
+            dist.all_gather(rr, r)
+            rows = [x.cpu().tolist() for x in rr]
+        for k, rr in enumerate(rows):
+            for i in range(S):
+                if rr[i][0] > 0:
+                    attempts[i] += 1
+                    if rr[i][1] > 0 and not ok[i]:
+                        owner[i], ok[i], frames[i], secs[i] = k, True, int(rr[i][2]), float(rr[i][3])
+        left = [jobs[i] for i in range(S) if not ok[i]]
+        if not left:
+            break
+        mine = [j for n, j in enumerate(left) if n % world == rank]
+    rank_seconds = [0.0] * world
+    for i in range(S):
+        if owner[i] >= 0:
+            rank_seconds[owner[i]] += secs[i]
+    return QueueResult(owner, frames, secs, ok, rank_seconds, rounds, attempts)
+
+
+def timed_steps(dist, world: int, rank: int, jobs: Sequence[Job], work: Callable[[Job], Tuple[int, float, bool]],
+                steps: int, warmup: int, device: str, sync: Callable[[], None] = lambda: None,
+                before_timed: Callable[[], None] = lambda: None) -> dict:
+    """bench.py's multi-rank leg: `warmup` untimed passes over the job list, then exactly `steps` timed
+    passes, each bracketed by a barrier and a device sync on both sides.  A pass = run_queue over the job
+    list.  Returns frames of all ranks, the max-over-ranks sum of decode seconds (each rank's own step
+    intervals), the wall time of the timed region, bit-exactness and the per-rank counters."""
+    import time
+
+    for _ in range(warmup):
+        if not run_queue(dist, world, rank, jobs, work, device).all_ok:
+            raise RuntimeError("warmup pass not bit-exact")
+    before_timed()
+    if dist is not None and world > 1:
+        dist.barrier()
+    sync()
+    w0 = time.perf_counter()
+    tot_frames, ok, per_rank = 0, True, [0.0] * world
+    results = []
+    for _ in range(steps):
+        q = run_queue(dist, world, rank, jobs, work, device)
+        results.append(q)
+        ok &= q.all_ok and all(n == 1 for n in q.attempts)  # (a timed job run twice had failed once)
+        tot_frames += q.total_frames
+        per_rank = [a + b for a, b in zip(per_rank, q.rank_seconds)]
+    sync()
+    if dist is not None and world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - w0
+    _, max_wall, _ = gather_counters(dist, world, 0, wall, device)
+    return {"frames": tot_frames, "max_seconds": max(per_rank) if per_rank else 0.0, "wall": max_wall,
+            "ok": ok, "per_rank_seconds": per_rank, "owners": results[-1].owner if results else [],
+            "rounds": max((q.rounds for q in results), default=0)}
 
 
 def job_table(dist, world: int, rank: int, device: str, first_seed: int = 1) -> List[int]:
-    import torch
-
-    seeds = list(range(first_seed, first_seed + world))
-    if dist is None or world == 1:
-        return seeds
-    t = torch.tensor(seeds if rank == 0 else [0] * world, dtype=torch.int64, device=device)
-    dist.broadcast(t, 0)
-    return [int(x) for x in t.tolist()]
+    """One stream seed per rank (the single-stream-per-GPU case of the queue): the broadcast job list's
+    seeds in plan order."""
+    jobs = broadcast_jobs(dist, world, rank, make_jobs(world, first_seed) if rank == 0 else None, device)
+    return [p[0][1] for p in plan(jobs, world)]
 
 
 def gather_counters(dist, world: int, frames: int, seconds: float, device: str) -> Tuple[int, float, List[Tuple[int, float]]]:
     """Returns (total frames over ranks, max seconds over ranks, per-rank list)."""
-    import torch
-
     if dist is None or world == 1:
         return frames, seconds, [(frames, seconds)]
+    import torch
+
     c = torch.tensor([float(frames), float(seconds)], dtype=torch.float64, device=device)
     outs = [torch.zeros_like(c) for _ in range(world)]
     dist.all_gather(outs, c)
@@ -35,10 +179,10 @@ def gather_counters(dist, world: int, frames: int, seconds: float, device: str) 
 
 def all_ranks(dist, world: int, ok: bool, device: str) -> bool:
     """True iff `ok` holds on every rank (all-reduce MIN of one int); used for the per-rank parity gate."""
-    import torch
-
     if dist is None or world == 1:
         return bool(ok)
+    import torch
+
     t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())

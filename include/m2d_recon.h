@@ -143,6 +143,10 @@ typedef struct m2r_backend {
 	 * bind, set_frames and acquire launch held pictures implicitly.  NULL: every submit is launched as it
 	 * comes. */
 	int (*flush)(void *self);
+	/* optional (ABI revision 5): 1 when sync_frame(slot) would return without waiting (the frame's copy out
+	 * of the device is complete), 0 otherwise; never blocks.  The decoder polls it while the caller waits
+	 * in peek / get and keeps its lookahead parsing meanwhile.  NULL: sync_frame is called at once. */
+	int (*ready)(void *self, int slot);
 } m2r_backend_t;
 
 /* ---------------------------------------------------------------- MPEG-1/2 (m2d_func)

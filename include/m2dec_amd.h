@@ -55,7 +55,7 @@ typedef struct {
  * checks m2dec_amd_abi_version() before passing either struct; m2dec_amd_h264_set_backend2 accepts an
  * older (smaller) m2r_backend_t by size, and m2dec_amd_stats_size() is the size every stats pointer
  * must have room for. */
-#define M2DEC_AMD_ABI_VERSION 4
+#define M2DEC_AMD_ABI_VERSION 5
 int m2dec_amd_abi_version(void);
 size_t m2dec_amd_stats_size(void);
 /* 0 if the host CPU lacks the x86-64-v3 features the host library is built for (decoder inits then

@@ -39,10 +39,10 @@ class Info(ctypes.Structure):
 
 
 class Backend(ctypes.Structure):
-    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind/flush."""
+    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind/flush/ready."""
     _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("acquire", ctypes.c_void_p),
                 ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p),
-                ("bind", ctypes.c_void_p), ("flush", ctypes.c_void_p)]
+                ("bind", ctypes.c_void_p), ("flush", ctypes.c_void_p), ("ready", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):

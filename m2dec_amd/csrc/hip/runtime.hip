@@ -1172,6 +1172,14 @@ int be_sync(void *self, int slot)
 	return 0;
 }
 
+/* m2r_backend_t.ready: sync_frame(slot) would not wait (no copy pending, or its event fired) */
+int be_ready(void *self, int slot)
+{
+	HipBackend *b = (HipBackend *)self;
+	if (slot < 0 || slot >= 64 || !b->slot_pending[slot]) return 1;
+	return hipEventQuery(b->slot_ev[slot]) == hipSuccess;
+}
+
 void be_destroy(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
@@ -1259,6 +1267,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->destroy = be_destroy;
 	out->bind = be_bind;
 	out->flush = be_flush;
+	out->ready = be_ready;
 	g_live_backends[device & 15]++;
 	if (const char *e = getenv("M2DEC_AMD_HOLD_BUSY")) b->hold_busy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */

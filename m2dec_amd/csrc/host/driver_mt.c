@@ -500,5 +500,6 @@ int m2dec_amd_null_backend_create(m2r_backend_t *out)
 	out->destroy = null_destroy;
 	out->bind = NULL;
 	out->flush = NULL;
+	out->ready = NULL;
 	return 0;
 }

@@ -988,6 +988,12 @@ int h264_async_drain(h264_dec_t *d, int slot)
 	while (as->bnd <= upto) {
 		pipe_drive(as);
 		if (as->bnd > upto) break;
+		/* waiting for the pool: keep the lookahead dispatching meanwhile (this is the caller's thread) */
+		pthread_mutex_unlock(as->mu);
+		const int stepped = h264_async_pump_step(d);
+		pthread_mutex_lock(as->mu);
+		if (stepped) continue;
+		if (as->bnd > upto) break;
 		pthread_cond_wait(&as->cv_done, as->mu);
 	}
 	const int err = take_error(as);
@@ -1066,6 +1072,28 @@ static void pump(h264_dec_t *d, int until_nal)
 		else if (r < 0) as->la_done = as->la_err = 1;
 	}
 	if (as->stats) as->t_la += now_s() - t0;
+}
+
+/* One step of the lookahead (one picture's headers + dispatch), if it may run now: the caller's thread
+ * calls this while it waits inside peek / get — for a bind (h264_async_drain) or for a frame's copy out
+ * of the device (h264_api.c deliver) — so that the lookahead keeps dispatching parse jobs while the
+ * caller is blocked on the device (before, it only ran inside decode_picture: while the caller waited
+ * for a frame the parse pool ran dry, profiles/r81_timeline.txt).  Returns 1 if it made a step. */
+int h264_async_pump_step(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	if (!as || as->la_done || as->seq - as->a_seq >= as->depth) return 0;
+	pthread_mutex_lock(as->mu);
+	const int full = as->head - as->tail >= AS_MAX - 2;
+	pthread_mutex_unlock(as->mu);
+	if (full) return 0;
+	const double t0 = as->stats ? now_s() : 0;
+	const long before = as->seq;
+	const int r = h264_decode_loop(as->la);
+	if (r == -2) as->la_done = 1;
+	else if (r < 0) as->la_done = as->la_err = 1;
+	if (as->stats) as->t_la += now_s() - t0;
+	return as->seq != before || r >= 0;
 }
 
 /* the lookahead context finished a NAL: hand it to the API context (buffers are swapped, not copied) */

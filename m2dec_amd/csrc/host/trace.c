@@ -175,6 +175,7 @@ int m2dec_amd_trace_capture(const uint8_t *data, size_t len, m2dec_amd_trace_t *
 	m2r_backend_t be;
 	int n;
 	memset(&c, 0, sizeof(c));
+	memset(&be, 0, sizeof(be));
 	c.t = (m2dec_amd_trace_t *)calloc(1, sizeof(m2dec_amd_trace_t));
 	if (!c.t) return -1;
 	for (int i = 0; i < 64; ++i) c.slot_pic[i] = -1;

@@ -1260,5 +1260,6 @@ int oracle_backend_create(m2r_backend_t *out)
 	out->destroy = be_destroy;
 	out->bind = be_bind;
 	out->flush = NULL;
+	out->ready = NULL;
 	return 0;
 }

@@ -48,10 +48,20 @@ static int dbg_knob(const char *name)
 	return v && atoi(v);
 }
 
-#ifndef M2DEC_NSTREAMS
-#define M2DEC_NSTREAMS 3
-#endif
-const int NSTREAMS = M2DEC_NSTREAMS; /* launches in flight: one hardware queue each, the copy stream the fourth */
+const int NSTREAMS = 8; /* most launch streams of a decoder context (arrays); g_nstreams of them are used */
+/* launch streams in use: one hardware queue each, the copy stream another — 3 with the default
+ * GPU_MAX_HW_QUEUES=4 (more streams than queues share a queue and serialise their launches);
+ * M2DEC_AMD_STREAMS = 1..8 (with GPU_MAX_HW_QUEUES raised to match) */
+static int nstreams()
+{
+	static int n = 0;
+	if (!n) {
+		const char *e = getenv("M2DEC_AMD_STREAMS");
+		int v = e ? atoi(e) : 3;
+		n = v < 1 ? 1 : (v > NSTREAMS ? NSTREAMS : v);
+	}
+	return n;
+}
 const int BMAX = 4; /* at most this many pictures per decode-path launch: the back end holds submitted
                      * pictures back until the decoder flushes (the end of a burst of submits) or it holds
                      * max_held, so that pictures parsed together run in one launch */
@@ -288,7 +298,7 @@ struct Sched {
 		dev = device;
 		memset(&tm, 0, sizeof(tm));
 		CHECK(hipSetDevice(dev));
-		for (auto &s : st) CHECK(g_pool.stream(dev, &s));
+		for (int k = 0; k < nstreams(); ++k) CHECK(g_pool.stream(dev, &st[k])); /* (the rest stay null) */
 		CHECK(hipMalloc(&err, 16)); /* (the sync events are created on first use: next_event) */
 		CHECK(hipMemset(err, 0, 16));
 		memset(&slot_seq, 0, sizeof(slot_seq));
@@ -306,7 +316,8 @@ struct Sched {
 	int configure(int width, int height, int n)
 	{
 		CHECK(hipSetDevice(dev));
-		for (auto &s : st) CHECK(hipStreamSynchronize(s));
+		for (auto &s : st)
+			if (s) CHECK(hipStreamSynchronize(s));
 		size_t nfsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
 		if (frames && (nfsz != fsz || n > nslots)) {
 			g_dev.give(dev, frames, fsz * (size_t)nslots);
@@ -366,7 +377,7 @@ struct Sched {
 			if (!bg.cap || cap < bg.cap) bg.cap = cap; /* contexts of several picture sizes: the smallest */
 			/* pictures per launch such that a launch on each stream fits the budget at once: a reserve
 			 * that has to wait would stall the thread driving the pipeline (a parse worker) */
-			pics_fit = std::max(1, std::min(BMAX, bg.cap / (NSTREAMS * picture_blocks(inter_grid, Hmb))));
+			pics_fit = std::max(1, std::min(BMAX, bg.cap / (nstreams() * picture_blocks(inter_grid, Hmb))));
 			if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "k_picture: %d workgroups resident (%d per CU)\n", bg.cap, per_cu);
 		}
 		return 0;
@@ -397,7 +408,7 @@ struct Sched {
 	int pick()
 	{
 		const int k = rr;
-		rr = (rr + 1) % NSTREAMS;
+		rr = (rr + 1) % nstreams();
 		return k;
 	}
 
@@ -672,7 +683,8 @@ struct Sched {
 	int sync_all()
 	{
 		CHECK(hipSetDevice(dev));
-		for (auto &s : st) CHECK(hipStreamSynchronize(s));
+		for (auto &s : st)
+			if (s) CHECK(hipStreamSynchronize(s));
 		return 0;
 	}
 
@@ -926,7 +938,7 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	 * alive (concurrent streams fill the budget already); the arena ring covers what can be in flight
 	 * (every arena is one pinned + device allocation: a ring larger than needed churns the pools) */
 	b->limit = g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed) > 1 ? 1 : std::min(b->max_held, b->sc.pics_fit);
-	b->narenas = std::min(kArenas, NSTREAMS * b->limit + b->limit + 2);
+	b->narenas = std::min(kArenas, nstreams() * b->limit + b->limit + 2);
 	if (b->next >= b->narenas) b->next = 0;
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "be_set_frames: configure %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
@@ -1053,7 +1065,7 @@ int be_flush(void *self)
 	if (!b->nheld) return 0;
 	if (b->nheld < b->limit && b->hold_busy) {
 		int free_streams = 0;
-		for (int k = 0; k < NSTREAMS; ++k)
+		for (int k = 0; k < nstreams(); ++k)
 			free_streams += !b->sc.last_launch[k] || hipEventQuery(b->sc.last_launch[k]) == hipSuccess;
 		if (!free_streams) return 1;
 	}

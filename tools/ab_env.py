@@ -1,0 +1,51 @@
+"""Interleaved A/B of environment configurations on the c3 end-to-end decode (median decode interval of N
+decodes per run, every decode bit-exact).  Usage: python3 tools/ab_env.py ROUNDS N 'NAME:K=V,K=V' ...
+(each configuration runs in its own process: GPU_MAX_HW_QUEUES etc. are read when HIP starts)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import os, sys, statistics
+sys.path.insert(0, %r)
+import m2dec_amd
+from tests._streams import stream, GOLDEN
+d = stream('c3_1080p_s1')
+ts = []
+for i in range(%d + 2):
+    st = m2dec_amd.Stats()
+    md5 = m2dec_amd.decode_stream_md5(d, device=0, stats=st)
+    assert md5 == GOLDEN['c3_1080p_s1']['md5']
+    if i >= 2:
+        ts.append(1e3 * (st.t_end - st.t_start))
+print('RESULT', statistics.median(ts), min(ts))
+"""
+
+
+def main():
+    rounds, n = int(sys.argv[1]), int(sys.argv[2])
+    cfgs = []
+    for a in sys.argv[3:]:
+        name, _, kv = a.partition(":")
+        env = dict(x.split("=", 1) for x in kv.split(",") if x)
+        cfgs.append((name, env))
+    res = {c[0]: [] for c in cfgs}
+    for r in range(rounds):
+        for name, env in cfgs:
+            e = dict(os.environ, **env)
+            out = subprocess.run([sys.executable, "-c", CHILD % (ROOT, n)], env=e, capture_output=True, text=True,
+                                 timeout=300)
+            line = [x for x in out.stdout.splitlines() if x.startswith("RESULT")]
+            if out.returncode or not line:
+                print(name, "FAILED", out.returncode, out.stderr[-800:], flush=True)
+                sys.exit(1)
+            med, mn = map(float, line[0].split()[1:])
+            res[name].append(med)
+            print(f"round {r} {name:12s} median {med:6.2f} ms  min {mn:6.2f} ms", flush=True)
+    print(json.dumps({k: sorted(v) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()

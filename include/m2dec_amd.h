@@ -77,6 +77,16 @@ int m2dec_amd_h264_set_parse_threads(void *ctx, int threads);
 /* Free the state behind a context at once (optional: as in the reference, a caller may also just
  * free the context memory; the library then reclaims the state itself — see h264_api.c). */
 void m2dec_amd_h264_release(void *ctx);
+/* Diagnostics: how often the H.264 parser took each reference-picture path (list modification idc 0 / 1 / 2,
+ * MMCO 1..6, long-term picture in an active list, POC type 1 / 2, temporal direct onto a long-term picture,
+ * IDR long_term_reference_flag, P list across the frame_num wrap), process-wide; reset clears them.
+ * Returns the counters written. */
+#define M2DEC_AMD_H264_HITS 16
+int m2dec_amd_h264_parser_hits(long *out, int n, int reset);
+/* Diagnostics: every P / B slice's active reference lists (POC, long-term flag per entry; the layout of
+ * tools/h264gen --dump-refs) appended to `path` from now on; NULL stops.  0, or -1 if it cannot be opened. */
+int m2dec_amd_h264_set_refdump(const char *path);
+
 /* Decoder states alive in the process registry, and how many were reclaimed over the cap. */
 int m2dec_amd_h264_registry(int *contexts, long *evicted);
 

@@ -386,6 +386,18 @@ int h264_dpb_pop(h264_dpb_t *dpb, int bypass);
 int h264_slice_data(h264_dec_t *d);
 
 /* h264_async.c */
+/* h264_syntax.c: reference-picture path counters (m2dec_amd_h264_parser_hits) */
+enum {
+	H264_HIT_MOD0 = 0,   /* ref_pic_list_modification idc 0, 1, 2 (long-term) */
+	H264_HIT_MMCO1 = 3,  /* MMCO 1 .. 6 */
+	H264_HIT_LT_LIST = 9, /* a long-term picture in an active list */
+	H264_HIT_POC1 = 10, H264_HIT_POC2 = 11,
+	H264_HIT_TD_LT = 12, /* temporal direct onto a long-term L0 picture (zero vectors) */
+	H264_HIT_LT_IDR = 13, /* IDR long_term_reference_flag */
+	H264_HIT_FN_WRAP = 14 /* a P list across the frame_num wrap */
+};
+void h264_hit(int i);
+
 /* timeline.c: M2DEC_AMD_TIMELINE diagnostics (no-op unless set) */
 void m2d_tl(int kind, long a, long b);
 

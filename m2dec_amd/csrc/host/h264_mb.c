@@ -702,6 +702,7 @@ static void direct_8x8(slice_ctx_t *s, int b8)
 		int ref = (0 <= map_idx) ? d->map_col_to_list0[map_idx] : 0;
 		m->ref[0][b8] = (int8_t)ref;
 		m->ref[1][b8] = 0;
+		if (0 <= map_idx && ref >= 0 && d->refs[0][ref].in_use == REF_LONG) h264_hit(H264_HIT_TD_LT);
 		if (0 <= map_idx && ref >= 0 && d->refs[0][ref].in_use != REF_LONG) {
 			int scale = d->dist_scale[ref];
 			for (int j = 0; j < 2; ++j) {

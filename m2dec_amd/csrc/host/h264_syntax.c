@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <limits.h>
+#include <pthread.h>
 #include "h264_dec.h"
 
 #define UE_RANGE(dst, b, max) do { uint32_t t_ = hb_ue(b); if ((uint32_t)(max) < t_) return -1; (dst) = (int)t_; } while (0)
@@ -503,6 +504,75 @@ static void sort_refs_b(h264_ref_t *ref, int n, int cur, int lx)
 	}
 }
 
+/* ------------------------------------------------------------------ diagnostics
+ * Counters of the reference-picture paths a stream took (tests/test_reflists_cpu.py asserts that each
+ * golden stream reaches the path it was made for), and M2DEC_AMD_H264_REFDUMP=path: the active lists of
+ * every P / B slice in tools/h264gen's gen_refdump_t layout, compared with the generator's own by
+ * tests/gen_check.py.  Both are written by the context that parses slice data (the lookahead context of a
+ * parse-ahead pipeline, or the decoder itself), not by the pipeline's API context. */
+static long g_hits[M2DEC_AMD_H264_HITS];
+#define HIT(i) __atomic_fetch_add(&g_hits[i], 1, __ATOMIC_RELAXED)
+
+int m2dec_amd_h264_parser_hits(long *out, int n, int reset)
+{
+	if (n > M2DEC_AMD_H264_HITS) n = M2DEC_AMD_H264_HITS;
+	for (int i = 0; i < n; ++i) out[i] = reset ? __atomic_exchange_n(&g_hits[i], 0, __ATOMIC_RELAXED) : __atomic_load_n(&g_hits[i], __ATOMIC_RELAXED);
+	return n;
+}
+
+void h264_hit(int i) { HIT(i); }
+
+static int counting(const h264_dec_t *d) { return !(d->as && !d->lookahead); }
+
+static pthread_mutex_t g_rd_mu = PTHREAD_MUTEX_INITIALIZER;
+static FILE *g_rd;
+static int g_rd_opened;
+
+/* the list dump to `path` from now on (NULL: off); M2DEC_AMD_H264_REFDUMP sets the first one */
+int m2dec_amd_h264_set_refdump(const char *path)
+{
+	pthread_mutex_lock(&g_rd_mu);
+	if (g_rd) fclose(g_rd);
+	g_rd = path && *path ? fopen(path, "wb") : NULL;
+	g_rd_opened = 1;
+	pthread_mutex_unlock(&g_rd_mu);
+	return path && *path && !g_rd ? -1 : 0;
+}
+
+static void refdump(const h264_dec_t *d, int nal_ref_idc)
+{
+	const h264_slice_t *h = &d->sh;
+	struct {
+		int32_t pic, first_mb, slice_type, poc, n[2], poc_l[2][16];
+		int8_t lt[2][16];
+	} r;
+	(void)nal_ref_idc;
+	pthread_mutex_lock(&g_rd_mu);
+	if (!g_rd_opened) {
+		const char *p = getenv("M2DEC_AMD_H264_REFDUMP");
+		g_rd_opened = 1;
+		g_rd = p && *p ? fopen(p, "wb") : NULL;
+	}
+	FILE *f = g_rd;
+	if (f) {
+		memset(&r, 0, sizeof(r));
+		r.pic = (int32_t)d->pictures;
+		r.first_mb = h->first_mb;
+		r.slice_type = h->slice_type;
+		r.poc = h->poc;
+		r.n[0] = h->slice_type != 2 ? h->num_ref_idx_active[0] : 0;
+		r.n[1] = h->slice_type == 1 ? h->num_ref_idx_active[1] : 0;
+		for (int lx = 0; lx < 2; ++lx)
+			for (int i = 0; i < r.n[lx] && i < 16; ++i) {
+				r.poc_l[lx][i] = d->refs[lx][i].in_use ? d->refs[lx][i].poc : -999999;
+				r.lt[lx][i] = (int8_t)(d->refs[lx][i].in_use == REF_LONG);
+			}
+		fwrite(&r, sizeof(r), 1, f);
+		fflush(f);
+	}
+	pthread_mutex_unlock(&g_rd_mu);
+}
+
 /* std::remove_if over [first, last): compacts survivors forward, tail keeps its old contents */
 static void remove_if_target(h264_ref_t *first, h264_ref_t *last, uint32_t num, int mode)
 {
@@ -516,7 +586,7 @@ static void remove_if_target(h264_ref_t *first, h264_ref_t *last, uint32_t num, 
 }
 
 /* ref_pic_list_reordering, h264.cpp:1608-1653 */
-static int list_modification(h264_bits_t *b, h264_ref_t *refs, uint32_t frame_num, int max_frame_num)
+static int list_modification(h264_bits_t *b, h264_ref_t *refs, uint32_t frame_num, int max_frame_num, int count)
 {
 	if (!hb_get1(b)) return 0;
 	for (int idx = 0; idx < 16; ++idx) {
@@ -525,6 +595,7 @@ static int list_modification(h264_bits_t *b, h264_ref_t *refs, uint32_t frame_nu
 		int mode;
 		UE_RANGE(op, b, 3);
 		if (op == 3) break;
+		if (count) HIT(H264_HIT_MOD0 + op);
 		num = hb_ue(b);
 		if (op < 2) {
 			int v;
@@ -705,9 +776,9 @@ int h264_slice_header(h264_dec_t *d, h264_bits_t *b, int nal_unit_type, int nal_
 				d->refs[1][i].in_use = REF_UNUSED;
 			}
 		}
-		if (list_modification(b, d->refs[0], h->frame_num, max_frame_num) < 0) return -1;
+		if (list_modification(b, d->refs[0], h->frame_num, max_frame_num, counting(d)) < 0) return -1;
 		if (h->slice_type == 1) {
-			if (list_modification(b, d->refs[1], h->frame_num, max_frame_num) < 0) return -1;
+			if (list_modification(b, d->refs[1], h->frame_num, max_frame_num, counting(d)) < 0) return -1;
 			if (!h->direct_spatial) {
 				/* create_map_col_to_list0, h264.cpp:1269-1277 */
 				const h264_colpic_t *col = &d->colpic[d->refs[1][0].col];
@@ -745,6 +816,27 @@ int h264_slice_header(h264_dec_t *d, h264_bits_t *b, int nal_unit_type, int nal_
 		if (dec_ref_pic_marking(b, h) < 0) return -1;
 	} else {
 		h->mmco5 = 0;
+	}
+	if (counting(d)) {
+		if (h->slice_type != 2) {
+			int lt = 0;
+			for (int lx = 0; lx < (h->slice_type == 1 ? 2 : 1); ++lx)
+				for (int i = 0; i < h->num_ref_idx_active[lx] && i < 16; ++i) lt |= d->refs[lx][i].in_use == REF_LONG;
+			if (lt) HIT(H264_HIT_LT_LIST);
+			if (h->slice_type == 0) {
+				for (int i = 0; i < h->num_ref_idx_active[0] && i < 16; ++i)
+					if (d->refs[0][i].in_use == REF_SHORT && d->refs[0][i].num > h->frame_num) {
+						HIT(H264_HIT_FN_WRAP);
+						break;
+					}
+			}
+		}
+		if (s->poc_type == 1) HIT(H264_HIT_POC1);
+		if (s->poc_type == 2) HIT(H264_HIT_POC2);
+		if (nal_ref_idc && h->idr && h->long_term_reference_flag) HIT(H264_HIT_LT_IDR);
+		if (nal_ref_idc && !h->idr && h->adaptive_marking)
+			for (int i = 0; i < 16 && h->mmco[i].op; ++i) HIT(H264_HIT_MMCO1 + h->mmco[i].op - 1);
+		refdump(d, nal_ref_idc);
 	}
 	h->cabac_init_idc = 0;
 	if (p->entropy_coding_mode_flag && h->slice_type != 2) UE_RANGE(h->cabac_init_idc, b, 2);

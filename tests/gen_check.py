@@ -31,7 +31,9 @@ DUMP_DT = np.dtype([("pic", "<i4"), ("mbaddr", "<i4"), ("kind", "u1"), ("cbp", "
                     ("exact_mv", "u1"), ("i16_pred", "u1"), ("cmode", "u1"), ("dir8", "u1"), ("ipm", "i1", 16),
                     ("ref", "i1", (2, 4)), ("mv", "<i2", (2, 16, 2)), ("ldc", "<i2", 16), ("luma", "<i2", 256),
                     ("cdc", "<i2", (2, 4)), ("cac", "<i2", (2, 4, 16))])
-assert MB_DT.itemsize == 32 and INTER_DT.itemsize == 144 and DUMP_DT.itemsize == 984
+REFDUMP_DT = np.dtype([("pic", "<i4"), ("first_mb", "<i4"), ("slice_type", "<i4"), ("poc", "<i4"), ("n", "<i4", 2),
+                       ("poc_l", "<i4", (2, 16)), ("lt", "i1", (2, 16))])
+assert MB_DT.itemsize == 32 and INTER_DT.itemsize == 144 and DUMP_DT.itemsize == 984 and REFDUMP_DT.itemsize == 184
 
 
 class Picture(ctypes.Structure):
@@ -91,10 +93,12 @@ class RecordingBackend:
         return SYNC(self.inner.sync_frame)(self.inner.self, slot)
 
 
-def generate(preset, out, dump=None, seed=1, extra=()):
+def generate(preset, out, dump=None, seed=1, extra=(), refdump=None):
     cmd = [GEN, "--preset", preset, "--seed", str(seed), "-o", out]
     if dump:
         cmd += ["--dump", dump]
+    if refdump:
+        cmd += ["--dump-refs", refdump]
     for kv in extra:
         cmd += ["--set", kv]
     subprocess.run(cmd, check=True, stderr=subprocess.DEVNULL)
@@ -220,20 +224,55 @@ def compare(pics, dump, max_errors=20, stats=None):
     return errs
 
 
-def check(preset, seed=1, extra=(), tmpdir="/tmp"):
+def compare_refs(gen, dec, max_errors=20):
+    """Every P / B slice's active lists (POC and long-term flag per entry): generator vs parser."""
+    errs = []
+    got = {(int(r["pic"]), int(r["first_mb"])): r for r in dec}
+    for g in gen:
+        key = (int(g["pic"]), int(g["first_mb"]))
+        d = got.get(key)
+        if d is None:
+            errs.append(f"pic {key[0]} slice at {key[1]}: no list dump from the parser")
+        elif int(d["slice_type"]) != int(g["slice_type"]) or int(d["poc"]) != int(g["poc"]) or list(d["n"]) != list(g["n"]):
+            errs.append(f"pic {key[0]} slice at {key[1]}: type/poc/n {int(d['slice_type'])}/{int(d['poc'])}/{list(d['n'])} != "
+                        f"{int(g['slice_type'])}/{int(g['poc'])}/{list(g['n'])}")
+        else:
+            for lx in range(2):
+                n = int(g["n"][lx])
+                a = [(int(p), int(t)) for p, t in zip(d["poc_l"][lx][:n], d["lt"][lx][:n])]
+                b = [(int(p), int(t)) for p, t in zip(g["poc_l"][lx][:n], g["lt"][lx][:n])]
+                if a != b:
+                    errs.append(f"pic {key[0]} slice at {key[1]} L{lx}: (poc, lt) {a} != {b}")
+        if len(errs) >= max_errors:
+            break
+    return errs
+
+
+def check(preset, seed=1, extra=(), tmpdir="/tmp", refs=True):
     out = os.path.join(tmpdir, f"gc_{preset}_{seed}.264")
     dmp = out + ".dump"
-    generate(preset, out, dmp, seed, extra)
+    rdg, rdd = out + ".refs", out + ".decrefs"
+    generate(preset, out, dmp, seed, extra, refdump=rdg if refs else None)
     data = open(out, "rb").read()
     dump = np.fromfile(dmp, dtype=DUMP_DT)
-    with OracleBackend() as ob:
-        rec = RecordingBackend(ob.be)
-        err = None
-        try:
-            m2dec_amd.decode_stream(data, backend=rec.be)
-        except RuntimeError as e:
-            err = str(e)
+    L = m2dec_amd.lib()
+    L.m2dec_amd_h264_set_refdump.argtypes = [ctypes.c_char_p]
+    if refs:
+        assert L.m2dec_amd_h264_set_refdump(rdd.encode()) == 0
+    try:
+        with OracleBackend() as ob:
+            rec = RecordingBackend(ob.be)
+            err = None
+            try:
+                m2dec_amd.decode_stream(data, backend=rec.be)
+            except RuntimeError as e:
+                err = str(e)
+    finally:
+        if refs:
+            L.m2dec_amd_h264_set_refdump(None)
     errs = compare(rec.pics, dump)
+    if refs:
+        errs = compare_refs(np.fromfile(rdg, dtype=REFDUMP_DT), np.fromfile(rdd, dtype=REFDUMP_DT)) + errs
     npics = int(dump["pic"].max()) + 1 if len(dump) else 0
     if err:
         errs.insert(0, f"decode error: {err}")

@@ -117,14 +117,13 @@ typedef struct {
 	/* motion */
 	int poc;
 	int ref_poc[2][32];
+	int ref_lt[2][32];      /* the list entry is a long-term reference */
 	int gv[2];
 	int16_t *region; /* per 4x4-MB region velocity (qpel / frame) */
 	int rw, rh;
 	/* direct prediction of B pictures (8.4.1.2) */
 	const struct gcol *col; /* co-located store of RefPicList1[0] */
-	int l0_all_poc[16];     /* the whole initial RefPicList0 (temporal direct maps into it) */
-	int n0_all;
-	int dsf[16];            /* DistScaleFactor per L0 index */
+	int dsf[32];            /* DistScaleFactor per L0 index */
 	int taint;              /* a direct block's motion is not defined by the spec: later MVs inexact */
 } gctx_t;
 
@@ -759,7 +758,8 @@ static void direct_motion(gctx_t *g, gmb_t *m, int b8)
 	int x0 = (b8 & 1) * 2, y0 = (b8 >> 1) * 2;
 	int ref[2], mv[2][2];
 	if (g->direct_spatial) {
-		int colzero = col->ref[b8] == 0 && mc[0] >= -1 && mc[0] <= 1 && mc[1] >= -1 && mc[1] <= 1;
+		/* colZeroFlag needs RefPicList1[0] short-term (8.4.1.2.2; h264.cpp:8507, 9960) */
+		int colzero = !g->ref_lt[1][0] && col->ref[b8] == 0 && mc[0] >= -1 && mc[0] <= 1 && mc[1] >= -1 && mc[1] <= 1;
 		for (int lx = 0; lx < 2; ++lx) {
 			nbm_t A, B, C;
 			unsigned r;
@@ -785,15 +785,21 @@ static void direct_motion(gctx_t *g, gmb_t *m, int b8)
 			mv[0][0] = mv[0][1] = mv[1][0] = mv[1][1] = 0;
 		} else {
 			int k = 0;
-			while (k < g->n0_all && g->l0_all_poc[k] != col->ref_poc[b8]) ++k;
+			while (k < g->l0n && g->ref_poc[0][k] != col->ref_poc[b8]) ++k;
 			if (k >= g->l0n) {
 				g->taint = 1;
 				k = 0;
 			}
 			ref[0] = k;
-			for (int c = 0; c < 2; ++c) {
-				mv[0][c] = (g->dsf[k] * mc[c] + 128) >> 8;
-				mv[1][c] = mv[0][c] - mc[c];
+			if (g->ref_lt[0][k]) {
+				/* RefPicList0[refIdxL0] long-term: the spec takes mvL0 = mvCol, mvL1 = 0 (8.4.1.2.3); the
+				 * reference gives both lists a zero vector (temporal_direct_block, h264.cpp:10049-10054) */
+				mv[0][0] = mv[0][1] = mv[1][0] = mv[1][1] = 0;
+			} else {
+				for (int c = 0; c < 2; ++c) {
+					mv[0][c] = (g->dsf[k] * mc[c] + 128) >> 8;
+					mv[1][c] = mv[0][c] - mc[c];
+				}
 			}
 		}
 	}
@@ -1336,7 +1342,7 @@ static void write_scaling_lists(bw_t *r, uint64_t seed)
 #undef rnd
 }
 
-static void write_sps(const params_t *p, bw_t *out, int log2_fn, int log2_poc)
+static void write_sps(const params_t *p, bw_t *out, int log2_fn, int log2_poc, int poc1_cycle)
 {
 	bw_t r;
 	bw_init(&r);
@@ -1353,8 +1359,16 @@ static void write_sps(const params_t *p, bw_t *out, int log2_fn, int log2_poc)
 		if (p->scaling) write_scaling_lists(&r, p->seed);
 	}
 	bw_ue(&r, (uint32_t)(log2_fn - 4));
-	bw_ue(&r, 0); /* poc type 0 */
-	bw_ue(&r, (uint32_t)(log2_poc - 4));
+	bw_ue(&r, (uint32_t)p->poc_type);
+	if (p->poc_type == 0) {
+		bw_ue(&r, (uint32_t)(log2_poc - 4));
+	} else if (p->poc_type == 1) {
+		bw_bit(&r, 0);  /* delta_pic_order_always_zero_flag */
+		bw_se(&r, 0);   /* offset_for_non_ref_pic */
+		bw_se(&r, 0);   /* offset_for_top_to_bottom_field */
+		bw_ue(&r, (uint32_t)poc1_cycle);
+		for (int i = 0; i < poc1_cycle; ++i) bw_se(&r, 1); /* offset_for_ref_frame[i] */
+	}
 	bw_ue(&r, (uint32_t)p->num_ref_frames);
 	bw_bit(&r, 0);
 	bw_ue(&r, (uint32_t)(p->width / 16 - 1));
@@ -1406,12 +1420,28 @@ static void write_pps(const params_t *p, bw_t *out, int cqp_off)
 /* ------------------------------------------------------------------ picture / stream */
 typedef struct {
 	int disp, type, idr, ref; /* type 0 P 1 B 2 I */
+	int mmco5;                /* a P picture whose marking is MMCO 5 (all references unused, POC / frame_num reset) */
 } picdesc_t;
 
+/* ------------------------------------------------------------------ reference pictures
+ * The generator restates the spec's reference-picture machinery (8.2.4 list initialisation and
+ * modification, 8.2.5 marking) and only writes streams on which the reference decoder agrees with it;
+ * where the reference deviates from the spec in a way a stream can reach, it follows the reference and
+ * says so (B lists order long-term pictures by POC, h264.cpp:10929-10935 — the generator keeps
+ * LongTermFrameIdx order equal to POC order, so both orders agree; no L1 swap when L1 == L0,
+ * h264.cpp:10985; zero vectors for temporal direct from a long-term reference, h264.cpp:10049-10054;
+ * POC type 1 of the IDR, h264.cpp:1183-1185). */
 typedef struct {
-	int disp, poc, frame_num, long_term;
-	int store; /* its co-located store (gen_stream's pool) */
+	int disp, poc, frame_num;
+	int long_term, lt_idx; /* long-term reference (LongTermFrameIdx) */
+	int store;             /* its co-located store (gen_stream's pool) */
 } dpbref_t;
+
+typedef struct {
+	dpbref_t e[16];
+	int n;
+	int max_lt_idx; /* MaxLongTermFrameIdx; -1: "no long-term frame indices" */
+} gdpb_t;
 
 /* DistScaleFactor (8.4.1.2.3) */
 static int dist_scale(int poc0, int poc1, int cur)
@@ -1420,6 +1450,231 @@ static int dist_scale(int poc0, int poc1, int cur)
 	if (td == 0) return 256; /* mvL0 = mvCol, mvL1 = 0 */
 	tx = (16384 + abs(td / 2)) / td;
 	return clampi((tb * tx + 32) >> 6, -1024, 1023);
+}
+
+/* FrameNumWrap / PicNum of a short-term frame (8.2.4.1) */
+static int pic_num(const dpbref_t *r, int cur_fn, int max_fn) { return r->frame_num > cur_fn ? r->frame_num - max_fn : r->frame_num; }
+
+static void sort_by(dpbref_t *v, int n, int (*before)(const dpbref_t *, const dpbref_t *, int, int), int a, int b)
+{
+	for (int i = 1; i < n; ++i) {
+		dpbref_t t = v[i];
+		int j = i - 1;
+		while (j >= 0 && before(&t, &v[j], a, b)) {
+			v[j + 1] = v[j];
+			j--;
+		}
+		v[j + 1] = t;
+	}
+}
+static int p_before(const dpbref_t *l, const dpbref_t *r, int cur_fn, int max_fn)
+{
+	if (l->long_term != r->long_term) return !l->long_term;
+	if (l->long_term) return l->lt_idx < r->lt_idx;                         /* ascending LongTermPicNum */
+	return pic_num(l, cur_fn, max_fn) > pic_num(r, cur_fn, max_fn);          /* descending PicNum */
+}
+static int b0_before(const dpbref_t *l, const dpbref_t *r, int cur, int unused)
+{
+	(void)unused;
+	if (l->long_term != r->long_term) return !l->long_term;
+	if (l->long_term) return l->poc < r->poc; /* (reference: by POC; LongTermFrameIdx order kept equal) */
+	if ((l->poc < cur) != (r->poc < cur)) return l->poc < cur;
+	return l->poc < cur ? l->poc > r->poc : l->poc < r->poc;
+}
+static int b1_before(const dpbref_t *l, const dpbref_t *r, int cur, int unused)
+{
+	(void)unused;
+	if (l->long_term != r->long_term) return !l->long_term;
+	if (l->long_term) return l->poc < r->poc;
+	if ((l->poc > cur) != (r->poc > cur)) return l->poc > cur;
+	return l->poc > cur ? l->poc < r->poc : l->poc > r->poc;
+}
+
+/* one ref_pic_list_modification operation (8.2.4.3) */
+typedef struct {
+	int idc, val;
+} lmod_t;
+
+static int same_pic(const dpbref_t *a, const dpbref_t *b) { return a->long_term == b->long_term && a->disp == b->disp; }
+
+/* choose up to 3 modifications of list `l` (n entries, `act` active) over the DPB, write them to `ops` and
+ * apply them (8.2.4.3.1 / 8.2.4.3.2); distinct targets (the reference's list arrays then stay
+ * permutations, h264.cpp:1640-1650).  Returns the number of operations. */
+static int choose_modification(const gdpb_t *dpb, dpbref_t *l, int n, int act, int cur_fn, int max_fn, lmod_t *ops)
+{
+	int nops = 1 + (int)(rnd() % 3u), k = 0, pred = cur_fn;
+	int used[16] = {0};
+	if (nops > act) nops = act;
+	for (int idx = 0; idx < nops; ++idx) {
+		int cand[16], nc = 0;
+		for (int i = 0; i < dpb->n; ++i)
+			if (!used[i]) cand[nc++] = i;
+		if (!nc) break;
+		const int t = cand[rnd() % (unsigned)nc];
+		const dpbref_t *tg = &dpb->e[t];
+		used[t] = 1;
+		if (tg->long_term) {
+			ops[k].idc = 2;
+			ops[k].val = tg->lt_idx;
+		} else {
+			const int pn = pic_num(tg, cur_fn, max_fn);
+			if (pn < pred) {
+				ops[k].idc = 0;
+				ops[k].val = pred - pn - 1; /* abs_diff_pic_num_minus1 */
+			} else {
+				ops[k].idc = 1;
+				ops[k].val = pn - pred - 1;
+			}
+			pred = pn;
+		}
+		k++;
+		/* insert at idx, shift, drop the later copy (the list is temporarily n + 1 long) */
+		{
+			dpbref_t tmp[17];
+			int m = 0;
+			for (int i = 0; i < idx; ++i) tmp[m++] = l[i];
+			tmp[m++] = *tg;
+			for (int i = idx; i < n; ++i)
+				if (!same_pic(&l[i], tg)) tmp[m++] = l[i];
+			for (int i = 0; i < n && i < m; ++i) l[i] = tmp[i];
+		}
+	}
+	return k;
+}
+
+static void write_modification(bw_t *r, const lmod_t *ops, int n)
+{
+	bw_bit(r, n > 0);
+	if (!n) return;
+	for (int i = 0; i < n; ++i) {
+		bw_ue(r, (uint32_t)ops[i].idc);
+		bw_ue(r, (uint32_t)ops[i].val);
+	}
+	bw_ue(r, 3);
+}
+
+/* adaptive marking operation (8.2.5.4) */
+typedef struct {
+	int op, a1, a2;
+} mmco_t;
+
+static int count_kind(const gdpb_t *d, int lt)
+{
+	int c = 0;
+	for (int i = 0; i < d->n; ++i) c += d->e[i].long_term == lt;
+	return c;
+}
+static void dpb_remove(gdpb_t *d, int i) { d->e[i] = d->e[--d->n]; }
+
+/* a LongTermFrameIdx for a picture of POC `poc` such that LongTermFrameIdx order equals POC order among the
+ * long-term frames (other than `skip`), or -1 */
+static int lt_idx_for(const gdpb_t *d, int poc, int skip)
+{
+	int cand[16], nc = 0;
+	for (int L = 0; L <= d->max_lt_idx; ++L) {
+		int ok = 1;
+		for (int i = 0; i < d->n && ok; ++i) {
+			const dpbref_t *e = &d->e[i];
+			if (i == skip || !e->long_term) continue;
+			if (e->lt_idx == L) ok = 0; /* (never replace: the reference's MMCO 6 would keep both) */
+			else if ((e->lt_idx < L) != (e->poc < poc)) ok = 0;
+		}
+		if (ok) cand[nc++] = L;
+	}
+	return nc ? cand[rnd() % (unsigned)nc] : -1;
+}
+
+/* choose the adaptive marking of the current (reference, non-IDR) picture and apply it to the DPB; the
+ * current picture itself is added by the caller (unless it became long-term: *cur_lt >= 0) */
+static int choose_mmco(const params_t *p, gdpb_t *d, int cur_fn, int max_fn, int cur_poc, mmco_t *ops, int *cur_lt)
+{
+	int k = 0;
+	*cur_lt = -1;
+	const int max_lt = imax(0, p->num_ref_frames - 2); /* keep a short-term frame beside the current one */
+	if (p->long_term && d->max_lt_idx < 0 && pct(70)) {
+		ops[k++] = (mmco_t){4, 2, 0}; /* MaxLongTermFrameIdx = 1 */
+		d->max_lt_idx = 1;
+	}
+	for (int step = 0; step < 3; ++step) {
+		const int r = (int)(rnd() % 100u);
+		if (p->long_term && d->max_lt_idx >= 0 && r < 30 && count_kind(d, 1) < max_lt && count_kind(d, 0) > 1) {
+			/* MMCO 3: a short-term frame (not the newest) becomes long-term */
+			int cand[16], nc = 0;
+			for (int i = 0; i < d->n; ++i)
+				if (!d->e[i].long_term) cand[nc++] = i;
+			const int i = cand[rnd() % (unsigned)nc];
+			const int L = lt_idx_for(d, d->e[i].poc, i);
+			if (L < 0) continue;
+			ops[k++] = (mmco_t){3, cur_fn - pic_num(&d->e[i], cur_fn, max_fn) - 1, L};
+			d->e[i].long_term = 1;
+			d->e[i].lt_idx = L;
+		} else if (r < 45 && count_kind(d, 1) > 0) {
+			/* MMCO 2: a long-term frame unused */
+			int cand[16], nc = 0;
+			for (int i = 0; i < d->n; ++i)
+				if (d->e[i].long_term) cand[nc++] = i;
+			const int i = cand[rnd() % (unsigned)nc];
+			ops[k++] = (mmco_t){2, d->e[i].lt_idx, 0};
+			dpb_remove(d, i);
+		} else if (r < 75 && count_kind(d, 0) > 1) {
+			/* MMCO 1: a short-term frame unused */
+			int cand[16], nc = 0;
+			for (int i = 0; i < d->n; ++i)
+				if (!d->e[i].long_term) cand[nc++] = i;
+			const int i = cand[rnd() % (unsigned)nc];
+			ops[k++] = (mmco_t){1, cur_fn - pic_num(&d->e[i], cur_fn, max_fn) - 1, 0};
+			dpb_remove(d, i);
+		} else if (p->long_term && d->max_lt_idx >= 0 && r < 90 && d->max_lt_idx >= 1 && count_kind(d, 1) > 0 && pct(30)) {
+			/* MMCO 4: MaxLongTermFrameIdx = 0 (long-term frames with index 1 unused) */
+			ops[k++] = (mmco_t){4, 1, 0};
+			d->max_lt_idx = 0;
+			for (int i = d->n - 1; i >= 0; --i)
+				if (d->e[i].long_term && d->e[i].lt_idx > 0) dpb_remove(d, i);
+		}
+	}
+	/* room for the current picture: spec marking has no sliding window after adaptive ops */
+	while (d->n + 1 > p->num_ref_frames) {
+		int oldest = -1;
+		for (int i = 0; i < d->n; ++i)
+			if (!d->e[i].long_term && (oldest < 0 || pic_num(&d->e[i], cur_fn, max_fn) < pic_num(&d->e[oldest], cur_fn, max_fn)))
+				oldest = i;
+		if (oldest < 0) { /* only long-term frames: drop one */
+			ops[k++] = (mmco_t){2, d->e[0].lt_idx, 0};
+			dpb_remove(d, 0);
+			continue;
+		}
+		ops[k++] = (mmco_t){1, cur_fn - pic_num(&d->e[oldest], cur_fn, max_fn) - 1, 0};
+		dpb_remove(d, oldest);
+	}
+	/* MMCO 6: the current picture long-term (last, as the reference applies it where it stands) */
+	if (p->long_term && d->max_lt_idx >= 0 && count_kind(d, 1) < max_lt && pct(25)) {
+		const int L = lt_idx_for(d, cur_poc, -1);
+		if (L >= 0) {
+			ops[k++] = (mmco_t){6, L, 0};
+			*cur_lt = L;
+		}
+	}
+	return k;
+}
+
+static void write_marking(bw_t *r, const picdesc_t *pd, int lt_idr, const mmco_t *ops, int n)
+{
+	if (pd->idr) {
+		bw_bit(r, 0); /* no_output_of_prior_pics */
+		bw_bit(r, lt_idr);
+		return;
+	}
+	bw_bit(r, n > 0); /* adaptive_ref_pic_marking_mode_flag */
+	if (!n) return;
+	for (int i = 0; i < n; ++i) {
+		bw_ue(r, (uint32_t)ops[i].op);
+		if (ops[i].op == 1 || ops[i].op == 2 || ops[i].op == 4 || ops[i].op == 6) bw_ue(r, (uint32_t)ops[i].a1);
+		if (ops[i].op == 3) {
+			bw_ue(r, (uint32_t)ops[i].a1);
+			bw_ue(r, (uint32_t)ops[i].a2);
+		}
+	}
+	bw_ue(r, 0);
 }
 
 static void write_pred_weight_table(gctx_t *g, bw_t *r, int nl)
@@ -1453,18 +1708,24 @@ static void write_pred_weight_table(gctx_t *g, bw_t *r, int nl)
 	}
 }
 
-int gen_stream(const params_t *p, bw_t *out, FILE *dump)
+int gen_stream(const params_t *p, bw_t *out, FILE *dump, FILE *refdump)
 {
 	gctx_t G, *g = &G;
 	picdesc_t *order;
-	int n = 0, log2_fn = 8, log2_poc = 10;
-	dpbref_t dpb[16];
+	const int log2_fn = p->log2_fn ? p->log2_fn : 8, log2_poc = 10, max_fn = 1 << log2_fn;
+	int n = 0;
+	gdpb_t dpb;
 	gcol_t *store[17];
-	int ndpb = 0, last_ref_fn = 0, idr_count = 0, cqp_off;
+	int last_ref_fn = 0, idr_count = 0, cqp_off;
+	int poc_base = 0;                      /* display index of the last IDR / MMCO 5 picture */
+	int prev_fn = 0, fn_offset = 0;        /* POC types 1 / 2: previous picture's frame_num, FrameNumOffset */
+	int poc1_cycle = 1;                    /* POC type 1: num_ref_frames_in_pic_order_cnt_cycle (offsets 1) */
 	bw_t r;
 	mbsyn_t *syn = (mbsyn_t *)calloc(1, sizeof(mbsyn_t));
 
 	memset(g, 0, sizeof(*g));
+	memset(&dpb, 0, sizeof(dpb));
+	dpb.max_lt_idx = -1;
 	rs = p->seed * 0x9E3779B97F4A7C15ull + 0x1234567ull;
 	if (!rs) rs = 1;
 	for (int i = 0; i < 8; ++i) rnd();
@@ -1478,62 +1739,81 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 	g->region = (int16_t *)calloc((size_t)(g->rw * g->rh * 2), sizeof(int16_t));
 	for (int i = 0; i < 17; ++i) store[i] = (gcol_t *)calloc((size_t)g->nmb, sizeof(gcol_t));
 	bw_init(&r);
+	if (p->poc_type == 1) poc1_cycle = 1 + (int)(p->seed % 3u);
 
 	/* coding order */
 	order = (picdesc_t *)calloc((size_t)p->frames, sizeof(picdesc_t));
 	{
-		int d = 0;
+		int d = 0, prev_nonref = 0;
 		int step = p->bframes + 1;
 		while (d < p->frames) {
-			int anchor = d;
-			int next = imin(d + step, p->frames - 1);
 			if (d == 0) {
-				order[n++] = (picdesc_t){0, 2, 1, 1};
+				order[n++] = (picdesc_t){0, 2, 1, 1, 0};
 				d = 1;
 				continue;
 			}
-			(void)anchor;
-			/* anchor at `next`, then the B pictures before it */
+			/* anchor at the end of the next group, then the B pictures before it */
 			{
 				int a = imin(d + step - 1, p->frames - 1);
 				int is_i = (p->gop > 0 && a % p->gop == 0);
 				int is_idr = is_i && p->idr_period > 0 && a % p->idr_period == 0;
-				if (is_idr) {
-					/* IDR cannot have B pictures referencing across it: emit Bs first as P */
-					for (int b = d; b < a; ++b) order[n++] = (picdesc_t){b, 0, 0, 1};
-					order[n++] = (picdesc_t){a, 2, 1, 1};
+				int is_m5 = !is_i && p->mmco5 > 0 && a % p->mmco5 == 0;
+				if (is_idr || is_m5) {
+					/* no B picture may reference across an IDR / MMCO 5 picture: emit the Bs first as P */
+					for (int b = d; b < a; ++b) order[n++] = (picdesc_t){b, 0, 0, 1, 0};
+					order[n++] = (picdesc_t){a, is_idr ? 2 : 0, is_idr, 1, is_m5};
+					prev_nonref = 0;
 				} else {
-					order[n++] = (picdesc_t){a, is_i ? 2 : 0, 0, 1};
-					for (int b = d; b < a; ++b) order[n++] = (picdesc_t){b, 1, 0, 0};
+					/* IPPP: some P pictures non-reference (never two in a row, never right after an IDR) */
+					int ref = 1;
+					if (step == 1 && !is_i && p->nonref_pct && !prev_nonref && n > 1 && pct(p->nonref_pct)) ref = 0;
+					prev_nonref = !ref;
+					order[n++] = (picdesc_t){a, is_i ? 2 : 0, 0, ref, 0};
+					for (int b = d; b < a; ++b) order[n++] = (picdesc_t){b, 1, 0, 0, 0};
 				}
 				d = a + 1;
 			}
-			(void)next;
 		}
 	}
 
 	cqp_off = rr(-2, 2);
-	write_sps(p, out, log2_fn, log2_poc);
+	write_sps(p, out, log2_fn, log2_poc, poc1_cycle);
 	write_pps(p, out, cqp_off);
 
 	for (int pi = 0; pi < n; ++pi) {
 		picdesc_t pd = order[pi];
-		int frame_num, poc = 2 * pd.disp, idr_base = 0;
+		int frame_num, poc, delta_poc0 = 0, lt_idr = 0;
 		int nsl = imax(1, p->slices), rows_per = (g->mbh + nsl - 1) / nsl;
+		lmod_t mods[2][4];
+		int nmods[2] = {0, 0};
+		mmco_t mmco[16];
+		int nmmco = 0, cur_lt = -1, td_ok = 1;
 		if (pd.idr) {
-			ndpb = 0;
+			dpb.n = 0;
+			dpb.max_lt_idx = -1;
 			frame_num = 0;
 			idr_count++;
+			poc_base = pd.disp;
 		} else {
-			frame_num = (last_ref_fn + 1) % (1 << log2_fn);
+			frame_num = (last_ref_fn + 1) % max_fn;
 		}
-		/* POC relative to the last IDR display index (poc type 0, lsb only) */
-		{
-			static int idr_disp = 0;
-			if (pd.idr) idr_disp = pd.disp;
-			idr_base = idr_disp;
+		/* POC (8.2.1) */
+		if (pd.idr) fn_offset = 0;
+		else if (prev_fn > frame_num) fn_offset += max_fn;
+		if (p->poc_type == 2) {
+			poc = 2 * (fn_offset + frame_num) - (pd.ref ? 0 : 1);
+		} else {
+			poc = 2 * (pd.disp - poc_base);
+			if (p->poc_type == 1) {
+				/* expectedPicOrderCnt with offset_for_ref_frame[i] = 1 (= absFrameNum), offset_for_non_ref_pic 0;
+				 * absFrameNum 0: the reference takes offset_for_ref_frame[0] (h264.cpp:1183-1185) */
+				int abs_fn = fn_offset + frame_num;
+				if (!pd.ref && abs_fn > 0) abs_fn--;
+				const int expected = abs_fn > 0 ? abs_fn : 1;
+				delta_poc0 = poc - expected;
+			}
 		}
-		poc = 2 * (pd.disp - idr_base);
+		prev_fn = frame_num;
 		g->poc = poc;
 		/* motion field for this picture */
 		{
@@ -1542,50 +1822,68 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			g->gv[1] = rr(-v / 2, v / 2);
 			for (int i = 0; i < g->rw * g->rh * 2; ++i) g->region[i] = (int16_t)rr(-v / 2, v / 2);
 		}
-		/* reference lists from the DPB (8.2.4.2) */
+		/* reference lists (8.2.4.2, then the modifications of 8.2.4.3) */
 		{
 			dpbref_t l0[16], l1[16];
 			int n0 = 0, n1 = 0;
+			for (int i = 0; i < dpb.n; ++i) l0[n0++] = l1[n1++] = dpb.e[i];
 			if (pd.type == 0) {
-				/* descending FrameNumWrap */
-				for (int i = 0; i < ndpb; ++i) l0[n0++] = dpb[i];
-				for (int i = 0; i < n0; ++i)
-					for (int j = i + 1; j < n0; ++j) {
-						int fi = l0[i].frame_num > frame_num ? l0[i].frame_num - (1 << log2_fn) : l0[i].frame_num;
-						int fj = l0[j].frame_num > frame_num ? l0[j].frame_num - (1 << log2_fn) : l0[j].frame_num;
-						if (fj > fi) { dpbref_t t = l0[i]; l0[i] = l0[j]; l0[j] = t; }
-					}
+				sort_by(l0, n0, p_before, frame_num, max_fn);
+				n1 = 0;
 			} else if (pd.type == 1) {
-				dpbref_t before[16], after[16];
-				int nb = 0, na = 0;
-				for (int i = 0; i < ndpb; ++i) {
-					if (dpb[i].poc < poc) before[nb++] = dpb[i];
-					else after[na++] = dpb[i];
-				}
-				for (int i = 0; i < nb; ++i)
-					for (int j = i + 1; j < nb; ++j)
-						if (before[j].poc > before[i].poc) { dpbref_t t = before[i]; before[i] = before[j]; before[j] = t; }
-				for (int i = 0; i < na; ++i)
-					for (int j = i + 1; j < na; ++j)
-						if (after[j].poc < after[i].poc) { dpbref_t t = after[i]; after[i] = after[j]; after[j] = t; }
-				for (int i = 0; i < nb; ++i) l0[n0++] = before[i];
-				for (int i = 0; i < na; ++i) l0[n0++] = after[i];
-				for (int i = 0; i < na; ++i) l1[n1++] = after[i];
-				for (int i = 0; i < nb; ++i) l1[n1++] = before[i];
+				sort_by(l0, n0, b0_before, poc, 0);
+				sort_by(l1, n1, b1_before, poc, 0);
+				/* (L1 == L0 with more than one entry: the spec swaps L1[0] / L1[1]; the reference never does,
+				 * h264.cpp:10985 — the generator follows the reference) */
+			} else {
+				n0 = n1 = 0;
 			}
 			g->l0n = imin(p->l0_active, n0);
 			g->l1n = imin(p->l1_active, n1);
-			g->taint = 0;
-			g->n0_all = n0;
-			for (int i = 0; i < n0; ++i) g->l0_all_poc[i] = l0[i].poc;
-			if (n1) {
-				g->col = store[l1[0].store];
-				for (int i = 0; i < n0; ++i) g->dsf[i] = dist_scale(l0[i].poc, l1[0].poc, poc);
-			}
-			for (int i = 0; i < g->l0n; ++i) g->ref_poc[0][i] = l0[i].poc;
-			for (int i = 0; i < g->l1n; ++i) g->ref_poc[1][i] = l1[i].poc;
 			if (pd.type == 1 && (g->l0n == 0 || g->l1n == 0)) pd.type = 0;
 			if (pd.type == 0 && g->l0n == 0) pd.type = 2;
+			if (pd.type == 0) {
+				sort_by(l0, n0, p_before, frame_num, max_fn);
+				n1 = 0;
+				g->l1n = 0;
+			}
+			if (pd.type != 2 && p->reorder_pct && pct(p->reorder_pct)) nmods[0] = choose_modification(&dpb, l0, n0, g->l0n, frame_num, max_fn, mods[0]);
+			if (pd.type == 1 && p->reorder_pct && pct(p->reorder_pct)) nmods[1] = choose_modification(&dpb, l1, n1, g->l1n, frame_num, max_fn, mods[1]);
+			g->taint = 0;
+			for (int i = 0; i < g->l0n; ++i) {
+				g->ref_poc[0][i] = l0[i].poc;
+				g->ref_lt[0][i] = l0[i].long_term;
+			}
+			for (int i = 0; i < g->l1n; ++i) {
+				g->ref_poc[1][i] = l1[i].poc;
+				g->ref_lt[1][i] = l1[i].long_term;
+			}
+			td_ok = 1;
+			if (pd.type == 1) {
+				g->col = store[l1[0].store];
+				for (int i = 0; i < g->l0n; ++i) g->dsf[i] = dist_scale(l0[i].poc, l1[0].poc, poc);
+				/* temporal direct needs every picture the co-located blocks reference in the active L0
+				 * (MapColToList0, 8.4.1.2.3); marking (MMCO 1 / 5, the sliding window) or list modification can
+				 * leave one out — spec-undefined, and the reference maps it through its marked list array
+				 * (h264.cpp:10962-10968): such pictures use spatial direct */
+				for (int a = 0; a < g->nmb && td_ok; ++a)
+					for (int b8 = 0; b8 < 4 && td_ok; ++b8) {
+						int k = 0;
+						if (g->col[a].ref[b8] < 0) continue;
+						while (k < g->l0n && g->ref_poc[0][k] != g->col[a].ref_poc[b8]) ++k;
+						td_ok = k < g->l0n;
+					}
+			}
+		}
+		/* marking of this picture (syntax in every slice header; applied after the picture) */
+		if (pd.ref && pd.idr) {
+			lt_idr = p->long_term && pct(30);
+		} else if (pd.ref && pd.mmco5) {
+			mmco[nmmco++] = (mmco_t){5, 0, 0};
+		} else if (pd.ref && p->mmco_pct && pct(p->mmco_pct)) {
+			gdpb_t after = dpb;
+			nmmco = choose_mmco(p, &after, frame_num, max_fn, poc, mmco, &cur_lt);
+			if (nmmco) dpb = after;
 		}
 		for (int i = 0; i < g->nmb; ++i) g->mb[i].slice = -1;
 
@@ -1600,11 +1898,28 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			g->qp = slice_qp;
 			g->prev_qpd_nz = 0;
 			g->direct_spatial = (p->direct == 2) ? pct(50) : p->direct;
+			if (!td_ok) g->direct_spatial = 1;
 			if (p->deblock) {
 				int r2 = (int)(rnd() % 100u);
 				didc = (r2 < 10) ? 1 : ((p->idc2 && r2 < 40) ? 2 : 0);
 				aoff = rr(-3, 3);
 				boff = rr(aoff, 3);
+			}
+			if (refdump) {
+				gen_refdump_t rd;
+				memset(&rd, 0, sizeof(rd));
+				rd.pic = pi;
+				rd.first_mb = first;
+				rd.slice_type = pd.type;
+				rd.poc = poc;
+				rd.n[0] = pd.type != 2 ? g->l0n : 0;
+				rd.n[1] = pd.type == 1 ? g->l1n : 0;
+				for (int lx = 0; lx < 2; ++lx)
+					for (int i = 0; i < rd.n[lx]; ++i) {
+						rd.poc_l[lx][i] = g->ref_poc[lx][i];
+						rd.lt[lx][i] = (int8_t)g->ref_lt[lx][i];
+					}
+				fwrite(&rd, sizeof(rd), 1, refdump);
 			}
 			bw_reset(&r);
 			bw_ue(&r, (uint32_t)first);
@@ -1612,24 +1927,18 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			bw_ue(&r, 0);
 			bw_bits(&r, (uint32_t)frame_num, log2_fn);
 			if (pd.idr) bw_ue(&r, (uint32_t)(idr_count & 1));
-			bw_bits(&r, (uint32_t)(poc & ((1 << log2_poc) - 1)), log2_poc);
+			if (p->poc_type == 0) bw_bits(&r, (uint32_t)(poc & ((1 << log2_poc) - 1)), log2_poc);
+			else if (p->poc_type == 1) bw_se(&r, delta_poc0);
 			if (pd.type == 1) bw_bit(&r, g->direct_spatial);
 			if (pd.type != 2) {
 				bw_bit(&r, 1); /* num_ref_idx_active_override */
 				bw_ue(&r, (uint32_t)(g->l0n - 1));
 				if (pd.type == 1) bw_ue(&r, (uint32_t)(g->l1n - 1));
-				bw_bit(&r, 0); /* no list modification l0 */
-				if (pd.type == 1) bw_bit(&r, 0);
+				write_modification(&r, mods[0], nmods[0]);
+				if (pd.type == 1) write_modification(&r, mods[1], nmods[1]);
 			}
 			if ((p->wp_p && pd.type == 0) || (p->wp_b == 1 && pd.type == 1)) write_pred_weight_table(g, &r, pd.type == 1 ? 2 : 1);
-			if (pd.ref) {
-				if (pd.idr) {
-					bw_bit(&r, 0);
-					bw_bit(&r, 0);
-				} else {
-					bw_bit(&r, 0);
-				}
-			}
+			if (pd.ref) write_marking(&r, &pd, lt_idr, mmco, nmmco);
 			if (p->cabac && pd.type != 2) bw_ue(&r, (uint32_t)cinit);
 			bw_se(&r, slice_qp - 26);
 			bw_ue(&r, (uint32_t)didc);
@@ -1763,20 +2072,22 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 			}
 			nal_emit(out, pd.ref ? 2 : 0, pd.idr ? 5 : 1, &r);
 		}
-		/* reference marking: sliding window (8.2.5.3) */
+		/* reference marking (8.2.5): IDR, MMCO 5, adaptive (applied above), or the sliding window */
 		if (pd.ref) {
 			int used[17] = {0}, st = 0;
-			if (ndpb == p->num_ref_frames) {
-				int oldest = 0;
-				for (int i = 1; i < ndpb; ++i) {
-					int fi = dpb[i].frame_num > frame_num ? dpb[i].frame_num - (1 << log2_fn) : dpb[i].frame_num;
-					int fo = dpb[oldest].frame_num > frame_num ? dpb[oldest].frame_num - (1 << log2_fn) : dpb[oldest].frame_num;
-					if (fi < fo) oldest = i;
-				}
-				dpb[oldest] = dpb[--ndpb];
+			dpbref_t cur;
+			if (pd.mmco5) {
+				dpb.n = 0;
+				dpb.max_lt_idx = -1;
+			} else if (!pd.idr && !nmmco && dpb.n == p->num_ref_frames) {
+				int oldest = -1;
+				for (int i = 0; i < dpb.n; ++i)
+					if (!dpb.e[i].long_term && (oldest < 0 || pic_num(&dpb.e[i], frame_num, max_fn) < pic_num(&dpb.e[oldest], frame_num, max_fn)))
+						oldest = i;
+				if (oldest >= 0) dpb_remove(&dpb, oldest);
 			}
 			/* the picture's co-located store: L0 motion (anchors are I / P) or intra */
-			for (int i = 0; i < ndpb; ++i) used[dpb[i].store] = 1;
+			for (int i = 0; i < dpb.n; ++i) used[dpb.e[i].store] = 1;
 			while (used[st]) ++st;
 			for (int a = 0; a < g->nmb; ++a) {
 				const gmb_t *m = &g->mb[a];
@@ -1791,8 +2102,25 @@ int gen_stream(const params_t *p, bw_t *out, FILE *dump)
 					c->mv[k][1] = on ? m->mv[0][k][1] : 0;
 				}
 			}
-			dpb[ndpb++] = (dpbref_t){pd.disp, poc, frame_num, 0, st};
-			last_ref_fn = frame_num;
+			cur = (dpbref_t){pd.disp, poc, frame_num, 0, 0, st};
+			if (pd.idr && lt_idr) {
+				cur.long_term = 1; /* LongTermFrameIdx 0, MaxLongTermFrameIdx 0 */
+				dpb.max_lt_idx = 0;
+			}
+			if (cur_lt >= 0) {
+				cur.long_term = 1;
+				cur.lt_idx = cur_lt;
+			}
+			if (pd.mmco5) {
+				/* after MMCO 5 the picture counts as frame_num 0, POC 0 (8.2.1), and later POCs restart from it */
+				cur.frame_num = 0;
+				cur.poc = 0;
+				poc_base = pd.disp;
+				fn_offset = 0;
+				prev_fn = 0;
+			}
+			dpb.e[dpb.n++] = cur;
+			last_ref_fn = cur.frame_num;
 		}
 	}
 	free(r.b);

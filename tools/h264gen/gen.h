@@ -43,6 +43,15 @@ typedef struct {
 	int quirks;             /* reach the reference quirks the kernels reproduce: explicit weights up to 127
 	                           (SSE2 int16 saturation, A#1), log2 denominator 7 with default weights (the
 	                           int8 store of 128, A#16), DC-only 4x4 blocks with |adj| 200..255 (SWAR, A#17) */
+	/* reference-picture machinery (h264.cpp:1417-1567 slice header, :1608-1653 list
+	 * modification, :10665-11050 marking / DPB) */
+	int poc_type;           /* 0, 1 (offsets of 1 per reference frame, deltas per slice) or 2 (IPPP only) */
+	int log2_fn;            /* log2_max_frame_num (4: frame_num wraps every 16 pictures) */
+	int reorder_pct;        /* P / B slices carrying ref_pic_list_modification */
+	int mmco_pct;           /* reference pictures marked by adaptive MMCO ops 1 / 2 / 3 / 4 / 6 */
+	int long_term;          /* allow long-term references (MMCO 3 / 4 / 6, IDR long_term_reference_flag) */
+	int mmco5;              /* every mmco5-th anchor (display index) is a P picture with MMCO 5 (0: none) */
+	int nonref_pct;         /* IPPP: P pictures coded as non-reference (nal_ref_idc 0) */
 	uint64_t seed;
 } params_t;
 
@@ -66,6 +75,18 @@ typedef struct {
 	int16_t cac[2][4][16]; /* raster, [0] unused */
 } gen_dump_t;
 
-int gen_stream(const params_t *p, bw_t *out, FILE *dump);
+/* Per-slice reference lists of P / B slices (--dump-refs), compared with the decoder's (M2DEC_AMD_H264_REFDUMP,
+ * tests/gen_check.py): the POC and long-term flag of every active entry of RefPicList0 / 1. */
+typedef struct {
+	int32_t pic;          /* coding-order picture index */
+	int32_t first_mb;
+	int32_t slice_type;   /* 0 P, 1 B, 2 I */
+	int32_t poc;
+	int32_t n[2];
+	int32_t poc_l[2][16];
+	int8_t lt[2][16];
+} gen_refdump_t;
+
+int gen_stream(const params_t *p, bw_t *out, FILE *dump, FILE *refdump);
 
 #endif

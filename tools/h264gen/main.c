@@ -80,6 +80,39 @@ static void preset(params_t *p, const char *name)
 		p->width = 384; p->height = 256; p->crop_bottom = 0; p->frames = 12; p->slices = 5; p->gop = 6;
 		return;
 	}
+	if (!strcmp(name, "cov_reflists")) {
+		/* list modification, adaptive marking (MMCO 1 / 2 / 3 / 4 / 6), long-term references in P and B
+		 * lists and in temporal direct, frame_num wrapping every 16 pictures */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 40; p->gop = 20; p->num_ref_frames = 4;
+		p->l0_active = 3; p->l1_active = 2; p->direct = 0; p->log2_fn = 4; p->reorder_pct = 60; p->mmco_pct = 60;
+		p->long_term = 1; p->mv_px = 40;
+		return;
+	}
+	if (!strcmp(name, "cov_reflists_cavlc")) {
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 30; p->cabac = 0; p->t8x8 = 0; p->profile = 77;
+		p->level = 30; p->i8_pct = 0; p->i4_pct = 60; p->gop = 15; p->num_ref_frames = 4; p->l0_active = 4;
+		p->l1_active = 2; p->direct = 2; p->log2_fn = 4; p->reorder_pct = 70; p->mmco_pct = 50; p->long_term = 1;
+		p->mv_px = 40;
+		return;
+	}
+	if (!strcmp(name, "cov_mmco5")) {
+		/* MMCO 5 every 9th anchor: references dropped, frame_num and POC restart at the picture */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 30; p->gop = 0; p->mmco5 = 9;
+		p->num_ref_frames = 3; p->reorder_pct = 30; p->mv_px = 40;
+		return;
+	}
+	if (!strcmp(name, "cov_poc1")) {
+		/* POC type 1 (offset_for_ref_frame 1 per frame, delta_pic_order_cnt[0] per picture) with B pictures */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 24; p->gop = 12; p->poc_type = 1;
+		p->log2_fn = 4; p->mv_px = 40;
+		return;
+	}
+	if (!strcmp(name, "cov_poc2")) {
+		/* POC type 2 (output order = decoding order), IPPP with non-reference P pictures */
+		p->width = 320; p->height = 192; p->crop_bottom = 0; p->frames = 24; p->gop = 12; p->poc_type = 2;
+		p->bframes = 0; p->log2_fn = 4; p->nonref_pct = 35; p->mmco_pct = 30; p->mv_px = 40;
+		return;
+	}
 	fprintf(stderr, "h264gen: unknown preset %s\n", name);
 	exit(2);
 }
@@ -98,6 +131,7 @@ static void set_kv(params_t *p, const char *kv)
 	F(profile) F(level) F(wp_p) F(wp_b) F(direct) F(qp_min) F(qp_max) F(deblock) F(pcm_permille) F(mv_px)
 	F(num_ref_frames) F(l0_active) F(l1_active) F(p_skip_pct) F(p_intra_pct) F(i4_pct) F(i8_pct)
 	F(sub8x8_pct) F(coef_pct) F(planar) F(cip) F(idc2) F(scaling) F(quirks)
+	F(poc_type) F(log2_fn) F(reorder_pct) F(mmco_pct) F(long_term) F(mmco5) F(nonref_pct)
 #undef F
 	fprintf(stderr, "h264gen: unknown key %s\n", key);
 	exit(2);
@@ -106,8 +140,8 @@ static void set_kv(params_t *p, const char *kv)
 int main(int argc, char **argv)
 {
 	params_t p;
-	const char *out = NULL, *dump = NULL;
-	FILE *df = NULL;
+	const char *out = NULL, *dump = NULL, *refdump = NULL;
+	FILE *df = NULL, *rf = NULL;
 	bw_t o;
 	FILE *f;
 	int n;
@@ -121,6 +155,7 @@ int main(int argc, char **argv)
 		} else if (!strcmp(argv[i], "--set") && i + 1 < argc) set_kv(&p, argv[++i]);
 		else if (!strcmp(argv[i], "-o") && i + 1 < argc) out = argv[++i];
 		else if (!strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
+		else if (!strcmp(argv[i], "--dump-refs") && i + 1 < argc) refdump = argv[++i];
 		else {
 			fprintf(stderr, "usage: h264gen --preset NAME [--seed N] [--frames N] [--size WxH] [--set k=v] -o out.264\n");
 			return 2;
@@ -133,8 +168,10 @@ int main(int argc, char **argv)
 	if (!p.cabac) p.t8x8 = 0;
 	bw_init(&o);
 	if (dump && !(df = fopen(dump, "wb"))) return 1;
-	n = gen_stream(&p, &o, df);
+	if (refdump && !(rf = fopen(refdump, "wb"))) return 1;
+	n = gen_stream(&p, &o, df, rf);
 	if (df) fclose(df);
+	if (rf) fclose(rf);
 	f = fopen(out, "wb");
 	if (!f) return 1;
 	fwrite(o.b, 1, o.n, f);

@@ -34,6 +34,16 @@ STREAMS = [
     # explicit weights at the SSE2 int16 saturation and the int8 weight 128 (A#1, A#16), SWAR DC-only
     # adds of 200..255 (A#17): tests/test_quirks.py asserts the oracle's hit counters
     ("cov_wp_quirks_s1", "cov_wp_quirks", 1, 16),
+    # reference-picture machinery: list modification idc 0 / 1 / 2, MMCO 1..6, long-term
+    # pictures in P / B lists and in temporal direct, IDR long_term_reference_flag, POC types 1 and 2,
+    # frame_num wrap, non-reference P pictures; recorded only when the parser's lists and every syntax
+    # element equal the generator's (tests/gen_check.py) — tests/test_reflists_cpu.py asserts each path ran
+    ("cov_reflists_s1", "cov_reflists", 1, 40),
+    ("cov_reflists_s2", "cov_reflists", 2, 40),
+    ("cov_reflists_cavlc_s1", "cov_reflists_cavlc", 1, 30),
+    ("cov_mmco5_s1", "cov_mmco5", 1, 30),
+    ("cov_poc1_s1", "cov_poc1", 1, 24),
+    ("cov_poc2_s1", "cov_poc2", 1, 24),
 ] + [(f"c4_1080p_s{s}", "c3", s, 60) for s in range(2, 9)] \
   + [(f"c5_4k_s{s}", "c5", s, 16) for s in range(2, 9)]  # C4 / C5: one stream per GPU, seed 1 + rank
 
@@ -54,6 +64,11 @@ def main():
         if name in res:
             continue
         data = gen(preset, seed, frames, os.path.join(tmp, name + ".264"))
+        if preset.startswith(("cov_reflists", "cov_mmco5", "cov_poc")):
+            from tests import gen_check
+            errs = gen_check.check(preset, seed=seed, extra=(f"frames={frames}",), tmpdir=tmp)
+            if errs:
+                raise SystemExit(f"{name}: parser and generator disagree: {errs[:3]}")
         with OracleBackend() as ob:
             md5s = m2dec_amd.decode_stream(data, backend=ob.be)
         res[name] = {"preset": preset, "seed": seed, "frames": frames, "bytes": len(data),

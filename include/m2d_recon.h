@@ -212,6 +212,17 @@ typedef struct {
 	uint32_t coef[2];     /* coefficient-pool offsets (dequantised int16, (1 << log2)^2 raster) */
 } h265r_tu_t;
 
+/* One inter prediction block (P / B pictures): motion compensation of the luma and chroma samples of the
+ * rectangle from one or two reference frames (inter_pred_onedir / merge_pred, h265.cpp:3552-3595, 3868-3903):
+ * 8-tap luma / 4-tap chroma interpolation with the reference's rounding, bi-prediction averaged.  Written
+ * before any transform block of the picture (every PU reads only reference frames). */
+typedef struct {
+	uint16_t x, y;        /* top-left luma sample */
+	uint8_t w, h;         /* luma size, 4..64 */
+	int8_t ref[2];        /* frame slot of the L0 / L1 reference (-1: list unused) */
+	int16_t mv[2][2];     /* quarter-sample luma vectors (chroma: the same, eighth-sample) */
+} h265r_pu_t;
+
 typedef struct {
 	uint8_t type[3];      /* per component: 0 off, 1 band offset, 2 edge offset */
 	uint8_t band[3];      /* band position */
@@ -238,6 +249,8 @@ typedef struct {
 	uint8_t *bs_v;               /* vertical edges [height/4][width/8]: (qp << 2) | bS, edge x = 8 i, rows 4 j.. */
 	uint8_t *bs_h;               /* horizontal edges [height/8][width/4]: edge y = 8 j, columns 4 i.. */
 	h265r_sao_t *sao;            /* per CTU, raster */
+	int32_t n_pu;                /* inter prediction blocks (P / B pictures; 0 in I pictures) */
+	h265r_pu_t *pu;
 } h265r_picture_t;
 
 /* An H.265 reconstruction back end (default: the gfx950 one, m2dec_amd/csrc/hip/h265_hip.hip). */

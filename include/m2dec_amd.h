@@ -229,6 +229,11 @@ void m2dec_amd_h265_release(void *ctx);
 /* Test hook: the parsed syntax (CU modes, residual levels) of later H.265 decodes into `path`, in
  * tools/h265gen --dump's format (NULL: stop). */
 int m2dec_amd_h265_set_dump(const char *path);
+/* test hook: coverage counters of the H.265 inter derivation (merge candidate kinds, AMVP predictor
+ * sources, bi-prediction, low-delay slices, stale collocated index, motion-based deblocking strengths,
+ * intra CUs of inter pictures), process-wide; returns the number of counters */
+#define M2DEC_AMD_H265_HITS 16
+int m2dec_amd_h265_parser_hits(long *out, int n, int reset);
 /* CABAC bins decoded by a context (host-parse measurement). */
 uint64_t m2dec_amd_h265_cabac_bins(const void *ctx);
 /* The gfx950 H.265 reconstruction back end (m2dec_amd/csrc/hip/h265_hip.hip). */

@@ -32,6 +32,21 @@ extern int m2dec_host_cpu_ok;           /* cpucheck.c */
 static FILE *g_dump;
 static int g_dump_init;
 
+/* coverage counters of the inter derivation (tests/test_h265_cpu.py: which paths the goldens exercise) */
+enum { H265_HIT_MERGE_SPATIAL, H265_HIT_MERGE_TEMPORAL, H265_HIT_MERGE_COMBINED, H265_HIT_MERGE_ZERO, H265_HIT_NO_BIDIR,
+       H265_HIT_MVP_A, H265_HIT_MVP_B, H265_HIT_MVP_SCALED, H265_HIT_MVP_TEMPORAL, H265_HIT_MVP_ZERO, H265_HIT_BI,
+       H265_HIT_LOWDELAY, H265_HIT_NOT_LOWDELAY, H265_HIT_COL_STALE, H265_HIT_BS_MOTION, H265_HIT_INTRA_CU, H265_HIT_N };
+static long g_hits[H265_HIT_N];
+#define HIT(k) __atomic_fetch_add(&g_hits[k], 1, __ATOMIC_RELAXED)
+
+int m2dec_amd_h265_parser_hits(long *out, int n, int reset)
+{
+	for (int i = 0; i < n && i < H265_HIT_N; ++i) out[i] = __atomic_load_n(&g_hits[i], __ATOMIC_RELAXED);
+	if (reset)
+		for (int i = 0; i < H265_HIT_N; ++i) __atomic_store_n(&g_hits[i], 0, __ATOMIC_RELAXED);
+	return H265_HIT_N;
+}
+
 typedef struct {
 	h265_dec_t *d;
 	jmp_buf *jb;
@@ -364,6 +379,78 @@ static void update_poc(h265_slice_t *sh, unsigned lsb, const h265_sps_t *s)
 	sh->poc = ((16 * sh->poc_msb) << (s->log2_max_poc_lsb - 4)) + (int)lsb;
 }
 
+/* find_frame_idx_from_dpb (h265.cpp:785-793): by POC in the output DPB, data[0]'s frame (or 0) otherwise */
+static int find_frame_idx(const h265_dec_t *d, int poc)
+{
+	for (int i = 0; i < d->dpb_size; ++i)
+		if (d->dpb[i].poc == poc) return d->dpb[i].frame_idx;
+	return d->dpb_size ? d->dpb[0].frame_idx : 0;
+}
+
+/* init_ref_pic_list_short_lx (h265.cpp:795-809): entries of one RPS side from list position `at`; unused
+ * entries are skipped but counted, and keep what the list held (the lists persist across slices) */
+static int ref_list_side(h265_dec_t *d, int lx, int at, int side, int rest)
+{
+	h265_slice_t *sh = &d->sh;
+	unsigned used = sh->rps.used[side];
+	int i;
+	for (i = 0; i < sh->rps.num_pics[side] && i < rest; ++i) {
+		if (used & 1) {
+			const int poc = sh->poc + sh->rps.delta_poc[side][i];
+			sh->ref_poc[lx][at + i] = poc;
+			sh->ref_frame[lx][at + i] = (int8_t)find_frame_idx(d, poc);
+		}
+		used >>= 1;
+	}
+	return i;
+}
+
+/* init_ref_pic_list (h265.cpp:811-820), as written: every round restarts the list's own side at entry 0 */
+static void init_ref_lists(perr_t *e)
+{
+	h265_slice_t *sh = &e->d->sh;
+	if (sh->rps.num_pics[0] + sh->rps.num_pics[1] == 0) H265_ERR(e); /* (the reference loops forever) */
+	for (int lx = 0; lx < 2; ++lx) {
+		const int num = imax(sh->num_ref_idx[lx], sh->rps.total_curr);
+		int idx = 0;
+		while (idx < num) {
+			idx += ref_list_side(e->d, lx, 0, lx, num - idx);
+			idx += ref_list_side(e->d, lx, idx, lx ^ 1, num - idx);
+		}
+	}
+}
+
+/* slice_header_nonintra (h265.cpp:822-856).  Fields a slice does not code keep the previous slice's value,
+ * as in the reference (collocated_ref_idx, cabac_init_flag, mvd_l1_zero_flag, num_ref_idx of L1 in P) */
+static void slice_header_inter(perr_t *e, h264_bits_t *b, const h265_sps_t *s, const h265_pps_t *p)
+{
+	h265_slice_t *sh = &e->d->sh;
+	const int bslice = sh->slice_type == 0;
+	if (hb_get1(b)) {
+		sh->num_ref_idx[0] = ue_max(e, b, 14) + 1;
+		if (bslice) sh->num_ref_idx[1] = ue_max(e, b, 14) + 1;
+	} else {
+		sh->num_ref_idx[0] = p->num_ref_idx_default[0];
+		sh->num_ref_idx[1] = p->num_ref_idx_default[1];
+	}
+	if (p->lists_modification && sh->rps.total_curr > 1) H265_ERR(e); /* assert(0) in the reference */
+	init_ref_lists(e);
+	if (bslice) sh->mvd_l1_zero = (int)hb_get1(b);
+	if (p->cabac_init_present) sh->cabac_init_flag = (int)hb_get1(b);
+	if (sh->temporal_mvp) {
+		const int l0 = bslice ? (int)hb_get1(b) : 1;
+		sh->col_from_l0 = l0;
+		if (l0 && sh->num_ref_idx[0] > 1) sh->col_ref_idx = ue_max(e, b, (uint32_t)sh->num_ref_idx[0] - 1);
+		else if (!l0 && sh->num_ref_idx[1] > 1) sh->col_ref_idx = ue_max(e, b, (uint32_t)sh->num_ref_idx[1] - 1);
+		else if (sh->col_ref_idx) HIT(H265_HIT_COL_STALE);
+	}
+	if ((bslice && p->weighted_bipred) || (sh->slice_type == 1 && p->weighted_pred)) H265_ERR(e); /* assert(0) */
+	sh->max_merge_cand = 5 - ue_max(e, b, 4);
+	/* the merge-level test compares CTU-relative positions (h265.cpp:3597-3599); a conformant level is at
+	 * most the CTB size, where absolute positions give the same answer */
+	if (p->log2_parallel_merge_level > s->log2_ctb) H265_ERR(e);
+}
+
 static void parse_slice_header(perr_t *e, h264_bits_t *b, const h265_sps_t *s, const h265_pps_t *p)
 {
 	h265_slice_t *sh = &e->d->sh;
@@ -409,7 +496,7 @@ static void parse_slice_header(perr_t *e, h264_bits_t *b, const h265_sps_t *s, c
 	} else {
 		sh->sao_luma = sh->sao_chroma = 0;
 	}
-	if (sh->slice_type != 2) H265_ERR(e); /* P / B slices: the inter path is not built yet */
+	if (sh->slice_type != 2) slice_header_inter(e, b, s, p);
 	sh->slice_qp = p->init_qp + hb_se(b);
 	if (sh->slice_qp < 0 || sh->slice_qp > 51) H265_ERR(e);
 	{
@@ -599,6 +686,14 @@ typedef struct {
 	int qp_y, scale[3];
 	int order_luma[4], order_chroma, intra_split;
 	int W4;                    /* luma 4x4 units per row (frame width / 4) */
+	/* P / B slices */
+	int inter, bslice;
+	int lowdelay;              /* no frame's POC above the current one (colpics_t::update_lowdelay) */
+	int16_t colmv[8][8], tmv[8][8]; /* temporal_mvscale_t over the 8 frames' POCs (h265modules.h:684-708) */
+	const h265_col_t *col_ref; /* the collocated picture's motion field */
+	const int8_t (*col_lists)[16]; /* ... and the frames of its reference lists (frameidx_record_t) */
+	h265_col_t *col_cur;       /* the current picture's motion field */
+	int col_stride;
 	int16_t blk[32 * 32];
 	int lev[32 * 32];          /* raw levels (the syntax dump only) */
 } sctx_t;
@@ -1087,7 +1182,645 @@ static void coding_unit(sctx_t *x, int x0, int y0, int log2, int vx, int vy, int
 	transform_tree(x, x0, y0, log2, 0, 3, vx, vy, ua, 0, 0, NULL);
 }
 
-/* coding_quadtree (quad_tree, h265.cpp:4100-4123) */
+/* ------------------------------------------------------------------ P / B coding units (h265.cpp:3012-4123) */
+/* The reference keeps what later blocks read of a block in left / top neighbour arrays per CTU; every read
+ * it makes of them (for positions its availability bits allow) is the block at that picture position, so
+ * here they are one map of 4x4 units (d->nb) addressed by position.  Positions outside the picture read
+ * the arrays' initial state (neighbour_init, h265.cpp:4743-4750: intra, not skipped). */
+static const h265_nb_t nb_outside = {1, 0, 0, 0, 0, 0, {{{0, 0}, {0, 0}}, {-1, -1}}};
+
+static inline h265_nb_t *nb_at(sctx_t *x, int px, int py)
+{
+	if (px < 0 || py < 0 || px >= x->s->pic_w || py >= x->s->pic_h) return (h265_nb_t *)&nb_outside;
+	return &x->d->nb[(size_t)(py >> 2) * (size_t)x->W4 + (size_t)(px >> 2)];
+}
+
+/* the 4x4 units of a rectangle inside the picture */
+#define NB_RECT(x, px, py, w, h, u, body)                                                                      \
+	for (int yy_ = (py); yy_ < (py) + (h) && yy_ < (x)->s->pic_h; yy_ += 4)                                  \
+		for (int xx_ = (px); xx_ < (px) + (w) && xx_ < (x)->s->pic_w; xx_ += 4) {                            \
+			h265_nb_t *u = &(x)->d->nb[(size_t)(yy_ >> 2) * (size_t)(x)->W4 + (size_t)(xx_ >> 2)];       \
+			body;                                                                                     \
+		}
+
+/* colpics_t::fill (h265modules.h:835-850): the 16x16 units whose top-left sample the block covers */
+static void col_fill(sctx_t *x, int px, int py, int w, int h, int intra, const h265_pred_t *pred)
+{
+	for (int y = (py + 15) & ~15; y < py + h; y += 16)
+		for (int xx = (px + 15) & ~15; xx < px + w; xx += 16) {
+			h265_col_t *c = &x->col_cur[(size_t)(y >> 4) * (size_t)x->col_stride + (size_t)(xx >> 4)];
+			c->intra = (uint8_t)intra;
+			if (!intra) c->pred = *pred;
+		}
+}
+
+/* temporal_mvscale_t::scale (h265modules.h:685-696) */
+static int16_t tmv_scale_of(int poc0, int refpoc0, int poc1, int refpoc1)
+{
+	const int diff1 = poc1 - refpoc1, diff0 = poc0 - refpoc0;
+	if (diff1 == 0) return 4096;
+	const int td = diff1 < -128 ? -128 : (diff1 > 127 ? 127 : diff1), tb = diff0 < -128 ? -128 : (diff0 > 127 ? 127 : diff0);
+	const int tx = (16384 + (abs(td) >> 1)) / td;
+	const int v = (tb * tx + 32) >> 6;
+	return (int16_t)(v < -4096 ? -4096 : (v > 4095 ? 4095 : v));
+}
+
+/* scale_mv (h265.cpp:3622-3631) */
+static int16_t scale_mv(int mv, int scale)
+{
+	int v = mv * scale;
+	if (v >= 0) {
+		v = (v + 127) >> 8;
+		return (int16_t)(v <= 32767 ? v : 32767);
+	}
+	v = -((127 - v) >> 8);
+	return (int16_t)(v >= -32768 ? v : -32768);
+}
+
+/* frameidx_record_t::frameidx (h265modules.h:667-669) of the current slice's lists */
+static inline int cur_frame(const sctx_t *x, int lx, int ref) { return x->sh->ref_frame[lx][ref] & 7; }
+
+/* colpics_t::get_ref (h265modules.h:793-807): the bottom-right 16x16 unit if it is inside the CTU row and the
+ * picture and not intra, else the centre unit */
+static const h265_col_t *col_get(const sctx_t *x, int px, int py, int w, int h)
+{
+	const int ctb = x->s->log2_ctb;
+	int bx = px + w, by = py + h;
+	if (!((((py & ((1 << ctb) - 1)) + h) >> ctb)) && bx < x->s->pic_w && by < x->s->pic_h) {
+		const h265_col_t *r = &x->col_ref[(size_t)(by >> 4) * (size_t)x->col_stride + (size_t)(bx >> 4)];
+		if (!r->intra) return r;
+	}
+	bx = px + (w >> 1);
+	by = py + (h >> 1);
+	return &x->col_ref[(size_t)(by >> 4) * (size_t)x->col_stride + (size_t)(bx >> 4)];
+}
+
+/* add_colpic_candidate (h265.cpp:3633-3645) */
+static void add_col(const sctx_t *x, h265_pred_t *pred, const h265_col_t *col, int lx, int ref_idx)
+{
+	int col_lx = x->lowdelay ? lx : x->sh->col_from_l0;
+	int col_ref = col->pred.ref[col_lx];
+	if (col_ref < 0) {
+		col_lx ^= 1;
+		col_ref = col->pred.ref[col_lx];
+	}
+	pred->ref[lx] = (int8_t)ref_idx;
+	const int sc = x->colmv[cur_frame(x, lx, ref_idx)][x->col_lists[col_lx][col_ref] & 7];
+	pred->mv[lx][0] = scale_mv(col->pred.mv[col_lx][0], sc);
+	pred->mv[lx][1] = scale_mv(col->pred.mv[col_lx][1], sc);
+}
+
+/* add_merge_candidate (h265.cpp:3597-3610) */
+static void add_merge(sctx_t *x, h265_pred_t *list, int *num, int px, int py, int nx, int ny)
+{
+	const h265_nb_t *n = nb_at(x, nx, ny);
+	const int s = x->p->log2_parallel_merge_level;
+	if (n->pu_intra || ((px >> s) == (nx >> s) && (py >> s) == (ny >> s))) return;
+	for (int i = 0; i < *num; ++i)
+		if (!memcmp(&n->pred, &list[i], sizeof(h265_pred_t))) return;
+	list[(*num)++] = n->pred;
+}
+
+/* the merge candidate merge_idx selects (prediction_unit_merge, h265.cpp:3685-3721) */
+static void merge_cand(sctx_t *x, int ua, int px, int py, int w, int h, int idx, h265_pred_t *out)
+{
+	h265_pred_t list[5];
+	int num = 0, spatial;
+	memset(list, 0, sizeof(list));
+	if (!(ua & 1)) add_merge(x, list, &num, px, py, px - 1, py + h - 1);
+	if (num <= idx) {
+		if (!(ua & 2)) add_merge(x, list, &num, px, py, px + w - 1, py - 1);
+		if (!(ua & 8)) add_merge(x, list, &num, px, py, px + w, py - 1);
+		if (!(ua & 4)) add_merge(x, list, &num, px, py, px - 1, py + h);
+		if (num <= idx && num < 4) add_merge(x, list, &num, px, py, px - 1, py - 1); /* (no availability test) */
+	}
+	spatial = num;
+	if (num <= idx && x->sh->temporal_mvp) { /* add_colpic_candidate_merge (:3647-3656) */
+		const h265_col_t *col = col_get(x, px, py, w, h);
+		if (!col->intra) {
+			add_col(x, &list[num], col, 0, 0);
+			if (x->bslice) add_col(x, &list[num], col, 1, 0);
+			else list[num].ref[1] = -1; /* (left uninitialised in a P slice by the reference: the spec's value) */
+			num++;
+		}
+	}
+	const int temporal_end = num;
+	if (num > 1 && num <= idx && x->bslice) { /* add_merge_combind_candidate (:3658-3683) */
+		static const int8_t l0_cand[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
+		const int cutoff = num * (num - 1);
+		for (int c = 0; c < cutoff; ++c) {
+			const int i0 = l0_cand[c], i1 = l0_cand[c ^ 1];
+			if (idx <= i0 || idx <= i1) break;
+			const h265_pred_t a = list[i0], bb = list[i1];
+			if (a.ref[0] >= 0 && bb.ref[1] >= 0) {
+				if (memcmp(a.mv[0], bb.mv[1], sizeof(a.mv[0])) || x->sh->ref_poc[0][a.ref[0]] != x->sh->ref_poc[1][bb.ref[1]]) {
+					memcpy(list[num].mv[0], a.mv[0], sizeof(a.mv[0]));
+					memcpy(list[num].mv[1], bb.mv[1], sizeof(a.mv[0]));
+					list[num].ref[0] = a.ref[0];
+					list[num].ref[1] = bb.ref[1];
+					if (idx < ++num) break;
+				}
+			}
+		}
+	}
+	const int combined_end = num;
+	HIT(idx < spatial ? H265_HIT_MERGE_SPATIAL
+	                  : (idx < temporal_end ? H265_HIT_MERGE_TEMPORAL : (idx < combined_end ? H265_HIT_MERGE_COMBINED : H265_HIT_MERGE_ZERO)));
+	while (num <= idx) { /* merge_zero_mv (:3612-3620): the selected one always takes reference 0 */
+		const int nref = x->bslice ? imin(x->sh->num_ref_idx[0], x->sh->num_ref_idx[1]) : x->sh->num_ref_idx[0];
+		const int m = idx - num, r = m < nref ? m : 0;
+		list[num].ref[0] = (int8_t)r;
+		list[num].ref[1] = (int8_t)(x->bslice ? r : -1);
+		memset(list[num].mv, 0, sizeof(list[num].mv));
+		num++;
+	}
+	*out = list[idx];
+}
+
+/* mvp2nd (h265.cpp:3755-3767) */
+static void mvp2nd(const sctx_t *x, int lx, int ref_idx, const h265_pred_t *n, int16_t dst[2])
+{
+	int lxi = lx;
+	for (int l = 0; l < 2; ++l) {
+		const int nr = n->ref[lxi];
+		if (nr >= 0) {
+			const int sc = x->tmv[cur_frame(x, lx, ref_idx)][cur_frame(x, lxi, nr)];
+			dst[0] = scale_mv(n->mv[lxi][0], sc);
+			dst[1] = scale_mv(n->mv[lxi][1], sc);
+			break;
+		}
+		lxi ^= 1;
+	}
+}
+
+/* find_spatial_mvp (h265.cpp:3769-3790) */
+static const int16_t *find_spatial_mvp(const sctx_t *x, const h265_nb_t *n, int lx, int refpoc, int ref_idx, int16_t m2[2],
+                                       int *skip2nd, int *match2nd)
+{
+	if (n->pu_intra) return NULL;
+	int lxi = lx;
+	for (int li = 0; li < 2; ++li) {
+		if (n->pred.ref[lxi] >= 0) {
+			if (x->sh->ref_poc[lxi][n->pred.ref[lxi]] == refpoc) {
+				*skip2nd = 1;
+				return n->pred.mv[lxi];
+			} else if (!*skip2nd && !*match2nd) {
+				mvp2nd(x, lx, ref_idx, &n->pred, m2);
+				*match2nd = 1;
+			}
+		}
+		lxi ^= 1;
+	}
+	*skip2nd = 1;
+	return NULL;
+}
+
+/* mvp_one_dir (h265.cpp:3792-3819): side 0 = A0, A1; side 1 = B0, B1 and (left and top available) B2 */
+static const int16_t *mvp_one_dir(sctx_t *x, int ua, int side, int px, int py, int w, int h, int lx, int ref_idx, int16_t m2[2],
+                                  int *skip2nd)
+{
+	const int dir = side ? ua >> 1 : ua;
+	const int refpoc = x->sh->ref_poc[lx][ref_idx];
+	int match2nd = 0;
+	const int16_t *mv;
+	if (!(dir & 4)) {
+		mv = find_spatial_mvp(x, side ? nb_at(x, px + w, py - 1) : nb_at(x, px - 1, py + h), lx, refpoc, ref_idx, m2, skip2nd, &match2nd);
+		if (mv) return mv;
+	}
+	if (!(dir & 1)) {
+		mv = find_spatial_mvp(x, side ? nb_at(x, px + w - 1, py - 1) : nb_at(x, px - 1, py + h - 1), lx, refpoc, ref_idx, m2, skip2nd,
+		                      &match2nd);
+		if (mv) return mv;
+	}
+	if (side && !(ua & 3)) {
+		mv = find_spatial_mvp(x, nb_at(x, px - 1, py - 1), lx, refpoc, ref_idx, m2, skip2nd, &match2nd);
+		if (mv) return mv;
+	}
+	return match2nd ? m2 : NULL;
+}
+
+/* add_mvp (h265.cpp:3742-3753) */
+static int add_mvp(const int16_t mv[2], int16_t list[2][2], int mvp_idx, int *n)
+{
+	const int16_t a = mv[0], b = mv[1];
+	for (int i = 0; i < *n; ++i)
+		if (list[i][0] == a && list[i][1] == b) return 0;
+	list[*n][0] = a;
+	list[*n][1] = b;
+	return mvp_idx < ++*n;
+}
+
+/* calc_mv (h265.cpp:3821-3839) */
+static void calc_mv(sctx_t *x, int ua, int px, int py, int w, int h, int lx, int ref_idx, int mvp_idx, const int mvd[2],
+                    const h265_col_t *col, int16_t out[2])
+{
+	int16_t list[2][2], m2[2] = {0, 0};
+	int n = 0, skip2nd = 0;
+	const int16_t *mvp = mvp_one_dir(x, ua, 0, px, py, w, h, lx, ref_idx, m2, &skip2nd);
+	int hit = H265_HIT_MVP_A;
+	if (!mvp || !add_mvp(mvp, list, mvp_idx, &n)) {
+		mvp = mvp_one_dir(x, ua, 1, px, py, w, h, lx, ref_idx, m2, &skip2nd);
+		hit = H265_HIT_MVP_B;
+		if (!mvp || !add_mvp(mvp, list, mvp_idx, &n)) {
+			h265_pred_t t;
+			int ok = 0;
+			hit = H265_HIT_MVP_TEMPORAL;
+			if (col) {
+				add_col(x, &t, col, lx, ref_idx);
+				ok = add_mvp(t.mv[lx], list, mvp_idx, &n);
+			}
+			if (!ok) {
+				memset(list[n], 0, sizeof(list[0]) * (size_t)(2 - n));
+				hit = H265_HIT_MVP_ZERO;
+			}
+		}
+	}
+	HIT(hit);
+	if (mvp == m2) HIT(H265_HIT_MVP_SCALED);
+	out[0] = (int16_t)(mvd[0] + list[mvp_idx][0]);
+	out[1] = (int16_t)(mvd[1] + list[mvp_idx][1]);
+}
+
+/* deblocking strengths of a prediction block's left / top edges (h265d_deblocking_t::record_pu,
+ * h265modules.h:504-582, 636-642): written over whatever the edge held */
+static inline int mv_big(const int16_t a[2], const int16_t b[2])
+{
+	const int dx = a[0] - b[0], dy = a[1] - b[1];
+	return dx * dx >= 16 || dy * dy >= 16;
+}
+
+static int pu_strength_motion(const sctx_t *x, const h265_nb_t *n, const int16_t cmv[2][2], int cf0, int cf1, int c_sw);
+
+static int pu_strength(const sctx_t *x, const h265_nb_t *n, const int16_t cmv[2][2], int cf0, int cf1, int c_sw)
+{
+	if (n->pu_intra) return 2;
+	if (n->pu_nz) return 1;
+	int r = pu_strength_motion(x, n, cmv, cf0, cf1, c_sw);
+	if (r) HIT(H265_HIT_BS_MOTION);
+	return r;
+}
+
+static int pu_strength_motion(const sctx_t *x, const h265_nb_t *n, const int16_t cmv[2][2], int cf0, int cf1, int c_sw)
+{
+	int nf0 = n->pred.ref[0] >= 0 ? x->sh->ref_frame[0][n->pred.ref[0]] : -1;
+	int nf1 = n->pred.ref[1] >= 0 ? x->sh->ref_frame[1][n->pred.ref[1]] : -1;
+	int n_sw = 0;
+	if (nf0 < nf1) {
+		const int t = nf0;
+		nf0 = nf1;
+		nf1 = t;
+		n_sw = 1;
+	}
+	/* inter_strength (:532-542), called with the two swap flags exchanged (h265modules.h:559) */
+	const int a_sw = c_sw, b_sw = n_sw;
+	if (nf0 != cf0 || nf1 != cf1) return 1;
+	if (nf0 == nf1)
+		return (mv_big(n->pred.mv[0], cmv[0]) || mv_big(n->pred.mv[1], cmv[1])) && (mv_big(n->pred.mv[0], cmv[1]) || mv_big(n->pred.mv[1], cmv[0]));
+	return (nf0 >= 0 && mv_big(n->pred.mv[a_sw], cmv[b_sw])) || (nf1 >= 0 && mv_big(n->pred.mv[a_sw ^ 1], cmv[b_sw ^ 1]));
+}
+
+static void record_pu(sctx_t *x, int px, int py, int w, int h, int r0, int r1, const int16_t mv[2][2])
+{
+	h265_dec_t *d = x->d;
+	if (x->sh->deblocking_disabled) return;
+	int f0 = r0 >= 0 ? x->sh->ref_frame[0][r0] : -1, f1 = r1 >= 0 ? x->sh->ref_frame[1][r1] : -1, c_sw = 0;
+	if (f0 < f1) {
+		const int t = f0;
+		f0 = f1;
+		f1 = t;
+		c_sw = 1;
+	}
+	const int q = x->qp_y << 2;
+	if (!(px & 7) && px > 0)
+		for (int j = 0; j < h >> 2; ++j)
+			d->pic.bs_v[(size_t)((py >> 2) + j) * (size_t)(d->frame_w / 8) + (size_t)(px >> 3)] =
+			    (uint8_t)(q | pu_strength(x, nb_at(x, px - 1, py + 4 * j), mv, f0, f1, c_sw));
+	if (!(py & 7) && py > 0)
+		for (int i = 0; i < w >> 2; ++i)
+			d->pic.bs_h[(size_t)(py >> 3) * (size_t)(d->frame_w / 4) + (size_t)((px >> 2) + i)] =
+			    (uint8_t)(q | pu_strength(x, nb_at(x, px + 4 * i, py - 1), mv, f0, f1, c_sw));
+}
+
+/* transform-block edges of an inter CU (record_tu, h265modules.h:507-524, 627-634): the larger of what the
+ * edge holds, the block's coded luma and the neighbour's transform block */
+static void record_tu_inter(sctx_t *x, int x0, int y0, int log2, int nz)
+{
+	h265_dec_t *d = x->d;
+	const int n = 1 << (log2 - 2), q = x->qp_y << 2;
+	if (x->sh->deblocking_disabled) return;
+	if (!(x0 & 7) && x0 > 0)
+		for (int j = 0; j < n; ++j) {
+			uint8_t *e = &d->pic.bs_v[(size_t)((y0 >> 2) + j) * (size_t)(d->frame_w / 8) + (size_t)(x0 >> 3)];
+			const h265_nb_t *nb = nb_at(x, x0 - 1, y0 + 4 * j);
+			const int s = imax(imax(nz, nb->tu_intra ? 2 : nb->tu_nz), *e & 3);
+			*e = (uint8_t)(q | s);
+		}
+	if (!(y0 & 7) && y0 > 0)
+		for (int i = 0; i < n; ++i) {
+			uint8_t *e = &d->pic.bs_h[(size_t)(y0 >> 3) * (size_t)(d->frame_w / 4) + (size_t)((x0 >> 2) + i)];
+			const h265_nb_t *nb = nb_at(x, x0 + 4 * i, y0 - 1);
+			const int s = imax(imax(nz, nb->tu_intra ? 2 : nb->tu_nz), *e & 3);
+			*e = (uint8_t)(q | s);
+		}
+}
+
+/* one prediction block out: the motion compensation record, deblocking, the neighbour map and the motion field */
+static void emit_pu(sctx_t *x, int px, int py, int w, int h, int r0, int r1, const int16_t mv[2][2])
+{
+	h265_dec_t *d = x->d;
+	if ((size_t)d->pic.n_pu >= d->cap_pu) {
+		const size_t cap = d->cap_pu ? 2 * d->cap_pu : 4096;
+		h265r_pu_t *n = (h265r_pu_t *)realloc(d->pic.pu, cap * sizeof(h265r_pu_t));
+		if (!n) H265_ERR(x->e);
+		d->pic.pu = n;
+		d->cap_pu = cap;
+	}
+	h265r_pu_t *u = &d->pic.pu[d->pic.n_pu++];
+	u->x = (uint16_t)px;
+	u->y = (uint16_t)py;
+	u->w = (uint8_t)w;
+	u->h = (uint8_t)h;
+	u->ref[0] = (int8_t)(r0 >= 0 ? x->sh->ref_frame[0][r0] : -1);
+	u->ref[1] = (int8_t)(r1 >= 0 ? x->sh->ref_frame[1][r1] : -1);
+	memcpy(u->mv, mv, sizeof(u->mv));
+	if (r0 < 0) memset(u->mv[0], 0, sizeof(u->mv[0]));
+	if (r1 < 0) memset(u->mv[1], 0, sizeof(u->mv[1]));
+}
+
+/* prediction_unit_merge (h265.cpp:3685-3721) with merge_pred (:3572-3595) */
+static void merge_pu(sctx_t *x, int ua, int px, int py, int w, int h)
+{
+	cab_t *c = &x->c;
+	h265_pred_t p;
+	{
+		const int max = x->sh->max_merge_cand;
+		int idx = 0;
+		if (max > 1 && cab_decision(c, H265_CTX_MERGE_IDX)) { /* merge_idx (:1143-1155) */
+			for (idx = 1; idx < max - 1; ++idx)
+				if (!cab_bypass(c)) break;
+		}
+		merge_cand(x, ua, px, py, w, h, idx, &p);
+		const int no_bidir = p.ref[0] >= 0 && p.ref[1] >= 0 && w + h == 12;
+		if (no_bidir) HIT(H265_HIT_NO_BIDIR);
+		else if (p.ref[0] >= 0 && p.ref[1] >= 0) HIT(H265_HIT_BI);
+		const int r0 = p.ref[0], r1 = (no_bidir || (p.ref[0] < 0 && p.ref[1] < 0)) ? -1 : p.ref[1];
+		emit_pu(x, px, py, w, h, r0, r1, (const int16_t(*)[2])p.mv);
+		record_pu(x, px, py, w, h, r0, no_bidir ? -1 : p.ref[1], (const int16_t(*)[2])p.mv);
+		{ /* copy_predinfo (:3119-3130) */
+			h265_pred_t q = p;
+			if (no_bidir) q.ref[1] = -1;
+			NB_RECT(x, px, py, w, h, u, {
+				u->pu_nz = 0;
+				u->pu_intra = 0;
+				u->skip = 1;
+				u->pred = q;
+			})
+		}
+		col_fill(x, px, py, w, h, 0, &p);
+		if (g_dump)
+			fprintf(g_dump, "pu %d %d %d %d m%d r %d %d mv %d %d %d %d\n", px, py, w, h, idx, p.ref[0], no_bidir ? -1 : p.ref[1], p.mv[0][0],
+			        p.mv[0][1], p.mv[1][0], p.mv[1][1]);
+	}
+}
+
+/* prediction_unit (h265.cpp:3905-3931): 1 if merged */
+static int prediction_unit(sctx_t *x, int log2, int ua, int px, int py, int w, int h, int pred_ua)
+{
+	cab_t *c = &x->c;
+	h265_pred_t p;
+	if (cab_decision(c, H265_CTX_MERGE_FLAG)) {
+		merge_pu(x, ua | pred_ua, px, py, w, h);
+		return 1;
+	}
+	int pred_idc = 0;
+	if (x->bslice) { /* inter_pred_idc (:1210-1216) */
+		const int depth = x->s->log2_ctb - log2;
+		if (w + h != 12 && cab_decision(c, H265_CTX_INTER_PRED_IDC + depth)) pred_idc = 2;
+		else pred_idc = cab_decision(c, H265_CTX_INTER_PRED_IDC + 4);
+	}
+	/* the collocated block (a null one dereferenced by the reference when TMVP is off: none here) */
+	const h265_col_t *col = x->sh->temporal_mvp ? col_get(x, px, py, w, h) : NULL;
+	if (col && col->intra) col = NULL;
+	int16_t mv[2][2] = {{0, 0}, {0, 0}};
+	int ref[2] = {-1, -1};
+	for (int lx = 0; lx < 2; ++lx) {
+		if (pred_idc == (lx ^ 1)) continue; /* L0 only: no L1; L1 only: no L0 */
+		int r = 0;
+		const int num = x->sh->num_ref_idx[lx] - 1;
+		if (num > 0) { /* ref_idx_lx (:1218-1237) */
+			const int m2 = imin(num, 2);
+			for (r = 0; r < m2; ++r)
+				if (!cab_decision(c, H265_CTX_REF_IDX + r)) break;
+			if (r == m2)
+				for (; r < num; ++r)
+					if (!cab_bypass(c)) break;
+		}
+		int mvd[2] = {0, 0};
+		if (lx == 0 || pred_idc == 1 || !x->sh->mvd_l1_zero) { /* mvd_coding (:3723-3740) */
+			int a0 = cab_decision(c, H265_CTX_ABS_MVD_GT), a1 = cab_decision(c, H265_CTX_ABS_MVD_GT);
+			if (a0) a0 += cab_decision(c, H265_CTX_ABS_MVD_GT + 1);
+			if (a1) a1 += cab_decision(c, H265_CTX_ABS_MVD_GT + 1);
+			int v[2] = {a0, a1};
+			for (int k = 0; k < 2; ++k) {
+				if (!v[k]) continue;
+				if (v[k] > 1) { /* abs_mvd_minus2: EG1 (:1243-1247) */
+					int bits = 0;
+					while (cab_bypass(c)) bits++;
+					v[k] += (2 << bits) - 2 + (int)cab_bypass_n(c, bits + 1);
+				}
+				if (cab_bypass(c)) v[k] = -v[k];
+			}
+			mvd[0] = v[0];
+			mvd[1] = v[1];
+		}
+		const int mvp_idx = cab_decision(c, H265_CTX_MVP_FLAG);
+		ref[lx] = r;
+		calc_mv(x, ua, px, py, w, h, lx, r, mvp_idx, mvd, col, mv[lx]);
+	}
+	if (pred_idc == 2) HIT(H265_HIT_BI);
+	emit_pu(x, px, py, w, h, ref[0], ref[1], (const int16_t(*)[2])mv);
+	record_pu(x, px, py, w, h, ref[0], ref[1], (const int16_t(*)[2])mv);
+	p.ref[0] = (int8_t)ref[0];
+	p.ref[1] = (int8_t)ref[1];
+	memcpy(p.mv, mv, sizeof(mv));
+	NB_RECT(x, px, py, w, h, u, { /* fill_pred (:3851-3866) */
+		u->pu_intra = 0;
+		u->pu_nz = 0;
+		u->skip = 0;
+		u->pred = p;
+	})
+	col_fill(x, px, py, w, h, 0, &p);
+	if (g_dump)
+		fprintf(g_dump, "pu %d %d %d %d a%d r %d %d mv %d %d %d %d\n", px, py, w, h, pred_idc, ref[0], ref[1], mv[0][0], mv[0][1], mv[1][0],
+		        mv[1][1]);
+	return 0;
+}
+
+/* transform_tree of an inter CU (h265.cpp:3026-3075 with is_intra false): residual-only records */
+static void transform_tree_inter(sctx_t *x, int x0, int y0, int log2, int depth, int cbf_cbcr, int blk)
+{
+	const h265_sps_t *s = x->s;
+	cab_t *c = &x->c;
+	int split, cbf = 0;
+	if (s->log2_max_tb < log2) split = 1;
+	else if (s->log2_min_tb < log2 && depth < s->max_th_depth_inter) split = cab_decision(c, H265_CTX_SPLIT_TRANSFORM + 5 - log2);
+	else split = depth == 0 && x->intra_split;
+	if (log2 > 2) {
+		if (cbf_cbcr & 2) cbf |= cab_decision(c, H265_CTX_CBF_CHROMA + depth) << 1;
+		if (cbf_cbcr & 1) cbf |= cab_decision(c, H265_CTX_CBF_CHROMA + depth);
+	} else {
+		cbf = cbf_cbcr;
+	}
+	if (split) {
+		const int h = 1 << (log2 - 1);
+		transform_tree_inter(x, x0, y0, log2 - 1, depth + 1, cbf, 0);
+		transform_tree_inter(x, x0 + h, y0, log2 - 1, depth + 1, cbf, 1);
+		transform_tree_inter(x, x0, y0 + h, log2 - 1, depth + 1, cbf, 2);
+		transform_tree_inter(x, x0 + h, y0 + h, log2 - 1, depth + 1, cbf, 3);
+		return;
+	}
+	cbf = cbf * 2 | ((depth || cbf) ? cab_decision(c, H265_CTX_CBF_LUMA + (depth == 0)) : 1);
+	if (cbf & 1) { /* transform_unit (:2246-2270), scans all 0 (zero_scan_order) */
+		h265r_tu_t *t = new_tu(x);
+		const int k = (int)(t - x->d->pic.tu);
+		t->x = (uint16_t)x0;
+		t->y = (uint16_t)y0;
+		t->log2 = (uint8_t)log2;
+		map_block(x, 0, x0, y0, log2, k);
+		put_residual(x, &x->d->pic.tu[k], 0, log2, residual_coding(x, log2, 0, 0, 0));
+	}
+	if ((cbf & 6) && (log2 > 2 || blk == 3)) {
+		const int cl = log2 > 2 ? log2 - 1 : 2, cx = log2 > 2 ? x0 >> 1 : (x0 - 4) >> 1, cy = log2 > 2 ? y0 >> 1 : (y0 - 4) >> 1;
+		h265r_tu_t *t = new_tu(x);
+		const int k = (int)(t - x->d->pic.tu);
+		t->x = (uint16_t)cx;
+		t->y = (uint16_t)cy;
+		t->log2 = (uint8_t)cl;
+		t->plane = 1;
+		map_block(x, 1, cx, cy, cl, k);
+		if (cbf & 4) put_residual(x, &x->d->pic.tu[k], 0, cl, residual_coding(x, cl, 1, 0, 0));
+		if (cbf & 2) put_residual(x, &x->d->pic.tu[k], 1, cl, residual_coding(x, cl, 2, 0, 0));
+	}
+	record_tu_inter(x, x0, y0, log2, cbf & 1);
+	NB_RECT(x, x0, y0, 1 << log2, 1 << log2, u, { /* cu_inter_tu_fill (:3012-3024) */
+		u->pu_nz = (uint8_t)(cbf & 1);
+		u->tu_intra = 0;
+		u->tu_nz = (uint8_t)(cbf & 1);
+		u->pu_intra = 0;
+	})
+}
+
+/* availability of the blocks of a split (h265.cpp:3933-3947): bit 1 left, 2 top, 4 bottom-left, 8 top-right */
+static const int8_t av4x4[3][16] = {{0, 5, 10, 15, 0, 5, 10, 15, 0, 5, 10, 15, 0, 5, 10, 15},
+                                    {4, 4, 6, 6, 4, 4, 6, 6, 12, 12, 14, 14, 12, 12, 14, 14},
+                                    {0, 1, 0, 1, 4, 5, 4, 5, 0, 1, 0, 1, 4, 5, 4, 5}};
+static const int8_t av2x1[2][16] = {{0, 1, 2, 3, 0, 5, 2, 7, 8, 9, 10, 11, 8, 13, 10, 15},
+                                    {8, 9, 8, 9, 12, 13, 12, 13, 8, 9, 8, 9, 12, 13, 12, 13}};
+static const int8_t av1x2[2][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 10, 11, 4, 5, 14, 15},
+                                    {4, 4, 6, 6, 4, 4, 6, 6, 12, 12, 14, 14, 12, 12, 14, 14}};
+
+/* pred_inter (h265.cpp:4061-4084) with prediction_unit_cases (:3949-4009) */
+static void coding_unit_inter(sctx_t *x, int x0, int y0, int log2, int vx, int vy, int ua)
+{
+	h265_dec_t *d = x->d;
+	cab_t *c = &x->c;
+	const int len = 1 << log2;
+	for (int j = 0; j < (1 << (log2 - 2)); ++j)
+		memset(d->cb_log2 + (size_t)((y0 >> 2) + j) * (size_t)x->W4 + (size_t)(x0 >> 2), log2, (size_t)1 << (log2 - 2));
+	{
+		const int ctx = (!(ua & 1) && nb_at(x, x0 - 1, y0)->skip) + (!(ua & 2) && nb_at(x, x0, y0 - 1)->skip);
+		if (cab_decision(c, H265_CTX_CU_SKIP + ctx)) { /* cu_skip_flag (:1138-1141) */
+			if (g_dump) fprintf(g_dump, "icu %d %d l%d skip\n", x0, y0, log2);
+			merge_pu(x, ua, x0, y0, len, len);
+			NB_RECT(x, x0, y0, len, len, u, {
+				u->tu_intra = 0;
+				u->skip = 1;
+				u->pu_nz = 0;
+				u->tu_nz = 0;
+			})
+			return;
+		}
+	}
+	if (cab_decision(c, H265_CTX_PRED_MODE)) { /* pred_mode_flag: intra */
+		HIT(H265_HIT_INTRA_CU);
+		coding_unit(x, x0, y0, log2, vx, vy, ua & 3);
+		NB_RECT(x, x0, y0, len, len, u, { /* cu_intra_pred_mode_fill (:3077-3088) */
+			u->tu_intra = 1;
+			u->pu_intra = 1;
+			u->skip = 0;
+		})
+		col_fill(x, x0, y0, len, len, 1, NULL);
+		return;
+	}
+	/* part_mode (:1165-1208) */
+	int part;
+	{
+		const int min = x->s->log2_min_cb;
+		if (cab_decision(c, H265_CTX_PART_MODE)) {
+			part = 0;
+		} else {
+			part = 2 - cab_decision(c, H265_CTX_PART_MODE + 1);
+			if (min < log2) {
+				if (x->s->amp && !cab_decision(c, H265_CTX_PART_MODE + 3)) part = (part + 1) * 2 + cab_bypass(c);
+			} else if (log2 > 3 && part == 2) {
+				part += cab_decision(c, H265_CTX_PART_MODE + 2) ^ 1;
+			}
+		}
+	}
+	if (g_dump) fprintf(g_dump, "icu %d %d l%d p%d\n", x0, y0, log2, part);
+	int merged = 0;
+	{
+		const int hl = len >> 1, ql = len >> 2;
+		switch (part) {
+		case 0: merged = prediction_unit(x, log2, ua, x0, y0, len, len, 0); break;
+		case 1:
+			prediction_unit(x, log2, av2x1[0][ua], x0, y0, len, hl, 0);
+			prediction_unit(x, log2, av2x1[1][ua], x0, y0 + hl, len, hl, 2);
+			break;
+		case 2:
+			prediction_unit(x, log2, av1x2[0][ua], x0, y0, hl, len, 0);
+			prediction_unit(x, log2, av1x2[1][ua], x0 + hl, y0, hl, len, 1);
+			break;
+		case 3: /* NxN (the reference's fourth block reads an unset top-left neighbour: its position here) */
+			prediction_unit(x, log2, av4x4[0][ua], x0, y0, hl, hl, 0);
+			prediction_unit(x, log2, av4x4[1][ua], x0 + hl, y0, hl, hl, 0);
+			prediction_unit(x, log2, av4x4[2][ua], x0, y0 + hl, hl, hl, 0);
+			prediction_unit(x, log2, 12, x0 + hl, y0 + hl, hl, hl, 0);
+			break;
+		case 4:
+			prediction_unit(x, log2, av2x1[0][ua], x0, y0, len, ql, 0);
+			prediction_unit(x, log2, av2x1[1][ua], x0, y0 + ql, len, len - ql, 2);
+			break;
+		case 5:
+			prediction_unit(x, log2, av2x1[0][ua], x0, y0, len, len - ql, 0);
+			prediction_unit(x, log2, av2x1[1][ua], x0, y0 + len - ql, len, ql, 2);
+			break;
+		case 6:
+			prediction_unit(x, log2, av1x2[0][ua], x0, y0, ql, len, 0);
+			prediction_unit(x, log2, av1x2[1][ua], x0 + ql, y0, len - ql, len, 1);
+			break;
+		default:
+			prediction_unit(x, log2, av1x2[0][ua], x0, y0, len - ql, len, 0);
+			prediction_unit(x, log2, av1x2[1][ua], x0 + len - ql, y0, ql, len, 1);
+			break;
+		}
+	}
+	if ((part == 0 && merged) || cab_decision(c, H265_CTX_RQT_ROOT_CBF)) {
+		x->intra_split = part != 0 && x->s->max_th_depth_inter == 0;
+		transform_tree_inter(x, x0, y0, log2, 0, 3, 0);
+	} else {
+		NB_RECT(x, x0, y0, len, len, u, { /* cu_inter_zerocoef_fill (:3101-3108) */
+			u->pu_nz = 0;
+			u->tu_nz = 0;
+		})
+	}
+	NB_RECT(x, x0, y0, len, len, u, { /* cu_inter_skip_mode_fill (:3090-3099) */
+		u->tu_intra = 0;
+		u->skip = 0;
+	})
+}
+
+/* coding_quadtree (quad_tree, h265.cpp:4100-4123); ua: the 4 availability bits of the block */
 static void quad_tree(sctx_t *x, int x0, int y0, int log2, int vx, int vy, int ua)
 {
 	h265_dec_t *d = x->d;
@@ -1103,14 +1836,15 @@ static void quad_tree(sctx_t *x, int x0, int y0, int log2, int vx, int vy, int u
 		}
 		if (split) {
 			const int h = 1 << (log2 - 1);
-			quad_tree(x, x0, y0, log2 - 1, vx, vy, ua);
-			quad_tree(x, x0 + h, y0, log2 - 1, vx - h, imin(vy, h), ua & ~1);
-			quad_tree(x, x0, y0 + h, log2 - 1, imin(vx, 2 * h), vy - h, ua & ~2);
-			quad_tree(x, x0 + h, y0 + h, log2 - 1, imin(vx - h, h), imin(vy - h, h), 0);
+			quad_tree(x, x0, y0, log2 - 1, vx, vy, av4x4[0][ua]);
+			quad_tree(x, x0 + h, y0, log2 - 1, vx - h, imin(vy, h), av4x4[1][ua]);
+			quad_tree(x, x0, y0 + h, log2 - 1, imin(vx, 2 * h), vy - h, av4x4[2][ua]);
+			quad_tree(x, x0 + h, y0 + h, log2 - 1, imin(vx - h, h), imin(vy - h, h), 12);
 			return;
 		}
 	}
-	coding_unit(x, x0, y0, log2, vx, vy, ua);
+	if (x->inter) coding_unit_inter(x, x0, y0, log2, vx, vy, ua);
+	else coding_unit(x, x0, y0, log2, vx, vy, ua & 3);
 }
 
 /* sao (h265.cpp:1017-1130) into the picture's per-CTU record, merges resolved */
@@ -1189,7 +1923,24 @@ static void pic_arrays(perr_t *e, int fw, int fh, int cols, int rows)
 		d->ipm = (uint8_t *)malloc(units);
 		d->cap_units = (d->cb_log2 && d->ipm) ? units : 0;
 	}
-	if (!d->cap_map || !d->cap_bs || !d->cap_sao || !d->cap_units) H265_ERR(e);
+	if (units > d->cap_nb) {
+		free(d->nb);
+		d->nb = (h265_nb_t *)malloc(units * sizeof(h265_nb_t));
+		d->cap_nb = d->nb ? units : 0;
+	}
+	{
+		const size_t ncol = (size_t)(fw / 16) * (size_t)(fh / 16);
+		if (ncol > d->cap_col) {
+			int ok = 1;
+			for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
+				free(d->col[i]);
+				d->col[i] = (h265_col_t *)calloc(ncol, sizeof(h265_col_t));
+				ok &= d->col[i] != NULL;
+			}
+			d->cap_col = ok ? ncol : 0;
+		}
+	}
+	if (!d->cap_map || !d->cap_bs || !d->cap_sao || !d->cap_units || !d->cap_nb || !d->cap_col) H265_ERR(e);
 	memset(d->pic.map, 0xff, nmap * sizeof(int32_t));
 	memset(d->pic.bs_v, 0, nbs);
 	memset(d->pic.bs_h, 0, nbs);
@@ -1197,7 +1948,29 @@ static void pic_arrays(perr_t *e, int fw, int fh, int cols, int rows)
 	memset(d->ipm, 1, units);
 }
 
-/* slice_data (h265.cpp:4735-4845) of an I slice */
+/* the temporal motion state of a P / B slice (colpics_t::init, h265modules.h:758-774) */
+static void inter_setup(sctx_t *x)
+{
+	h265_dec_t *d = x->d;
+	const h265_slice_t *sh = x->sh;
+	const int cl = sh->col_from_l0 ^ 1;
+	const int col_frm = sh->ref_frame[cl][sh->col_ref_idx] & 7, col_poc = sh->ref_poc[cl][sh->col_ref_idx];
+	x->col_ref = d->col[col_frm];
+	x->col_lists = (const int8_t(*)[16])d->col_frame[col_frm];
+	for (int i = 0; i < 8; ++i)
+		for (int j = 0; j < 8; ++j) {
+			x->colmv[i][j] = tmv_scale_of(sh->poc, d->frame_poc[i], col_poc, d->frame_poc[j]);
+			x->tmv[i][j] = tmv_scale_of(sh->poc, d->frame_poc[i], sh->poc, d->frame_poc[j]);
+		}
+	x->lowdelay = 1;
+	for (int i = 0; i < 8; ++i)
+		if (sh->poc < d->frame_poc[i]) x->lowdelay = 0;
+	HIT(x->lowdelay ? H265_HIT_LOWDELAY : H265_HIT_NOT_LOWDELAY);
+	/* the neighbour map starts as neighbour_init's state everywhere (only decoded positions are read) */
+	for (size_t i = 0, n = (size_t)x->W4 * (size_t)(d->frame_h / 4); i < n; ++i) d->nb[i] = nb_outside;
+}
+
+/* slice_data (h265.cpp:4735-4845) */
 static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, const uint8_t *data, const uint8_t *end)
 {
 	h265_dec_t *d = e->d;
@@ -1210,8 +1983,18 @@ static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, cons
 	x->p = p;
 	x->sh = &d->sh;
 	x->W4 = d->frame_w / 4;
+	x->inter = d->sh.slice_type < 2;
+	x->bslice = d->sh.slice_type == 0;
+	x->col_cur = d->col[d->index];
+	x->col_stride = (s->pic_w + 15) >> 4;
 	set_qp(x, d->sh.slice_qp);
-	cab_init_ctx(&x->c, 0, d->sh.slice_qp);
+	/* initType (ctu_init, h265.cpp:4756) */
+	cab_init_ctx(&x->c, x->inter ? 2 - (d->sh.slice_type ^ d->sh.cabac_init_flag) : 0, d->sh.slice_qp);
+	if (x->inter) {
+		inter_setup(x);
+	} else { /* every block of an I picture is intra in its motion field (pred_intra's colpics fill) */
+		for (size_t i = 0, n = (size_t)x->col_stride * (size_t)((s->pic_h + 15) >> 4); i < n; ++i) x->col_cur[i].intra = 1;
+	}
 	cab_start(&x->c, data, end);
 	{
 		const int ctb = 1 << s->log2_ctb;
@@ -1221,7 +2004,7 @@ static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, cons
 			const int x0 = cx << s->log2_ctb, y0 = cy << s->log2_ctb;
 			/* availability at the CTU (coding_tree_unit, h265.cpp:4738): left / top inside the slice */
 			const int idx = addr - d->sh.address;
-			const int ua = ((cy == 0 || idx < s->ctb_cols) ? 2 : 0) | ((cx == 0 || idx == 0) ? 1 : 0);
+			const int ua = ((cy == 0 || idx < s->ctb_cols) ? 10 : 0) | ((cx == 0 || idx == 0) ? 5 : 0) | 4;
 			sao_syntax(x, cx, cy);
 			quad_tree(x, x0, y0, s->log2_ctb, s->pic_w - x0, imin(s->pic_h - y0, ctb), ua);
 			addr++;
@@ -1298,7 +2081,13 @@ static void slice_layer(perr_t *e, int nal_type)
 		const h265_sps_t *s = &d->sps[p->sps_id];
 		if (!p->valid || !s->valid) H265_ERR(e);
 		if (s->stride != d->frame_w || (s->ctb_rows << s->log2_ctb) != d->frame_h) H265_ERR(e);
+		/* the reference has motion-field buffers for min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8)
+		 * frames (set_second_frame, h265.cpp:121-128) and writes the current frame's for every picture */
+		if (d->index >= s->frame_num) H265_ERR(e);
 		parse_slice_header(e, &b, s, p);
+		/* ctu_init (h265.cpp:4777) and colpics_t::init's register_reflist (h265modules.h:769): every slice */
+		d->frame_poc[d->index] = sh->poc;
+		memcpy(d->col_frame[d->index], sh->ref_frame, sizeof(sh->ref_frame));
 		/* the frame's geometry as the reference sets it in ctu_init (h265.cpp:4776-4783) */
 		{
 			m2d_frame_t *f = &d->frames[d->index];
@@ -1313,6 +2102,7 @@ static void slice_layer(perr_t *e, int nal_type)
 		if (g_dump) fprintf(g_dump, "pic %d\n", d->pictures);
 		d->pic.n_tu = 0;
 		d->pic.n_coef = 0;
+		d->pic.n_pu = 0;
 		{
 			const size_t pos = (size_t)(b.p - (d->unit + 2)) - (size_t)(b.bits >> 3);
 			slice_data(e, s, p, d->unit + 2 + pos, d->unit + d->unit_len);
@@ -1524,6 +2314,14 @@ void m2dec_amd_h265_release(void *ctx)
 	free(d->pic.sao);
 	free(d->cb_log2);
 	free(d->ipm);
+	free(d->nb);
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
+		free(d->col[i]);
+		d->col[i] = NULL;
+	}
+	free(d->pic.pu);
+	d->nb = NULL;
+	d->cap_nb = d->cap_col = d->cap_pu = 0;
 	d->unit = NULL;
 	d->unit_cap = 0;
 	memset(&d->pic, 0, sizeof(d->pic));

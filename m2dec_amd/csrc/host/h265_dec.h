@@ -112,6 +112,8 @@ typedef struct {
 	int sao_luma, sao_chroma;
 	int num_ref_idx[2];
 	int mvd_l1_zero, cabac_init_flag, col_from_l0, col_ref_idx, max_merge_cand;
+	int ref_poc[2][16];                 /* the reference lists (init_ref_pic_list, h265.cpp:795-820) */
+	int8_t ref_frame[2][16];
 	int slice_qp, qpc_delta[2];
 	int deblocking_disabled, deblocking_override;
 	int beta_offset_div2, tc_offset_div2; /* set only by an override: kept from the previous slice otherwise (h265.cpp:894-901) */
@@ -123,6 +125,24 @@ typedef struct {
 	int8_t frame_idx;
 	uint8_t is_idr;
 } h265_dpb_elem_t;
+
+/* prediction info of a block (pred_info_t, h265modules.h:420-423): compared with memcmp by the merge list */
+typedef struct {
+	int16_t mv[2][2];
+	int8_t ref[2];
+} h265_pred_t;
+
+/* what later blocks read of a 4x4 luma unit of the current picture (h265d_neighbour_t, h265modules.h:425-434) */
+typedef struct {
+	uint8_t pu_intra, pu_nz, tu_intra, tu_nz, skip, pad;
+	h265_pred_t pred;
+} h265_nb_t;
+
+/* a 16x16 unit of a picture's motion field (colpics_t, h265modules.h:731-874) */
+typedef struct {
+	uint8_t intra, pad;
+	h265_pred_t pred;
+} h265_col_t;
 
 /* the decoder state: the caller's context memory (m2d_func_table_t.context_size), plus heap arrays */
 typedef struct h265_dec {
@@ -149,6 +169,12 @@ typedef struct h265_dec {
 	size_t cap_tu, cap_coef, cap_map, cap_bs, cap_sao, cap_units;
 	uint8_t *cb_log2;         /* per luma 4x4 unit: log2 size of its CU (0: not decoded) */
 	uint8_t *ipm;             /* per luma 4x4 unit: intra prediction mode */
+	/* inter pictures */
+	h265_nb_t *nb;            /* per luma 4x4 unit of the current picture */
+	h265_col_t *col[H265R_MAX_FRAMES]; /* per frame: its motion field, 16x16 units (stride (pic_w + 15) / 16) */
+	size_t cap_nb, cap_col, cap_pu;
+	int8_t col_frame[H265R_MAX_FRAMES][2][16]; /* per frame: the frame slots of its reference lists (frameidx_record_t) */
+	int frame_poc[H265R_MAX_FRAMES];   /* h265d_frame_info_t.poc */
 	/* reconstruction back end */
 	h265r_backend_t be;
 	int have_be;

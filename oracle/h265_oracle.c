@@ -16,6 +16,13 @@
  *   - SAO (h265.cpp:4386-4729) on the deblocked picture: band offset without the band-table wrap of
  *     the spec (sao_bo_block, a reference quirk), edge offset skipping samples whose neighbour lies
  *     outside the picture.
+ *   - motion compensation of P / B pictures (h265.cpp:3132-3595), before the picture's transform blocks:
+ *     luma with the 8-tap quarter-sample filters and clamped reference positions (the reference's
+ *     fir1 / fir2 / fir3 and its 1-D / 2-D paths, whose integers equal spec 8.5.3.3.3.1), chroma with
+ *     the reference's packed two-component uint64 arithmetic restated literally (interp_chroma*: Cb in
+ *     the high half, Cr in the low half behind a 0x80000000 guard and the & ~0xf8000000 mask, which
+ *     does not hold a negative horizontal Cr sum apart from the Cb half — kept as it is), default
+ *     weighted bi-prediction (store_pix<0> into int16, then add_store_pix);
  * Every CLIP255C argument outside the reference table's domain [-256, 767] (m2d.cpp:157-289) and
  * every DC-only term the reference's byte-wise SWAR add would corrupt (|dc| > 255) is counted:
  * golden streams must have none.
@@ -382,6 +389,123 @@ static void sao(const h265r_picture_t *pic, uint8_t *luma, uint8_t *chroma)
 	free(copy);
 }
 
+/* ------------------------------------------------------------------ motion compensation (h265.cpp:3132-3595) */
+/* luma filters by quarter-sample phase over positions -3..4 (fir1 / fir2 / fir3 with their window offsets) */
+static const int luma_fir[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0},
+                                   {-1, 4, -10, 58, 17, -5, 1, 0},
+                                   {-1, 4, -11, 40, 40, -11, 4, -1},
+                                   {0, 1, -5, 17, 58, -10, 4, -1}};
+static const int chroma_fir[8][4] = {{0, 64, 0, 0},  {2, 58, 10, 2}, {4, 54, 16, 2}, {6, 46, 28, 4},
+                                     {4, 36, 36, 4}, {4, 28, 46, 6}, {2, 16, 54, 4}, {2, 10, 58, 2}};
+
+static inline int clampx(int v, int m) { return v < 0 ? 0 : (v >= m ? m - 1 : v); } /* CLAMPX (h265.cpp:3158) */
+
+/* the value and shift one luma sample of one list hands the reference's Store functor (interp_luma,
+ * h265.cpp:3388-3446): integer position << 12 with the full shift; 1-D filtered with shift - 6; 2-D: the
+ * horizontal sums as int16, then the vertical sum with the full shift */
+static int mc_luma(const uint8_t *ref, int W, int pw, int ph, int x, int y, int fx, int fy, int full, int *shift)
+{
+#define RS(xx, yy) ((int)ref[(size_t)clampx(yy, ph) * (size_t)W + (size_t)clampx(xx, pw)])
+	int v = 0;
+	if (!fx && !fy) {
+		*shift = full;
+		return RS(x, y) << 12;
+	}
+	if (!fy) {
+		for (int k = 0; k < 8; ++k) v += luma_fir[fx][k] * RS(x - 3 + k, y);
+		*shift = full - 6;
+		return v;
+	}
+	if (!fx) {
+		for (int k = 0; k < 8; ++k) v += luma_fir[fy][k] * RS(x, y - 3 + k);
+		*shift = full - 6;
+		return v;
+	}
+	for (int r = 0; r < 8; ++r) {
+		int h = 0;
+		for (int k = 0; k < 8; ++k) h += luma_fir[fx][k] * RS(x - 3 + k, y - 3 + r);
+		v += luma_fir[fy][r] * (int16_t)h;
+	}
+	*shift = full;
+	return v;
+#undef RS
+}
+
+/* load2pix(umv) + interp_chroma1hline_base (h265.cpp:3448-3490): one row's horizontal sums, packed */
+static uint64_t chroma_h(const uint8_t *ch, int W, int cw, int chh, int x, int y, int fx)
+{
+	const uint8_t *row = ch + (size_t)clampx(y, chh) * (size_t)W;
+	uint64_t a[4];
+	for (int k = 0; k < 4; ++k) {
+		const int p = clampx(x - 1 + k, cw) * 2;
+		a[k] = ((uint64_t)row[p] << 32) | row[p + 1];
+	}
+	const uint64_t c0 = (uint64_t)chroma_fir[fx][0], c1 = (uint64_t)chroma_fir[fx][1], c2 = (uint64_t)chroma_fir[fx][2],
+	               c3 = (uint64_t)chroma_fir[fx][3];
+	return (((c1 * a[1] + c2 * a[2]) | 0x80000000ull) - (c0 * a[0] + c3 * a[3])) & ~0xf8000000ull;
+}
+
+/* interp_chroma1hline_vert_base (h265.cpp:3493-3511): the Cb and Cr values of one position */
+static void mc_chroma(const uint8_t *ch, int W, int cw, int chh, int x, int y, int fx, int fy, int v[2])
+{
+	const uint64_t h0 = chroma_h(ch, W, cw, chh, x, y - 1, fx), h1 = chroma_h(ch, W, cw, chh, x, y, fx);
+	const uint64_t h2 = chroma_h(ch, W, cw, chh, x, y + 1, fx), h3 = chroma_h(ch, W, cw, chh, x, y + 2, fx);
+	const uint64_t k0 = (uint64_t)chroma_fir[fy][0], k1 = (uint64_t)chroma_fir[fy][1], k2 = (uint64_t)chroma_fir[fy][2],
+	               k3 = (uint64_t)chroma_fir[fy][3];
+	const uint64_t w = ((h1 * k1 + h2 * k2) | 0x80000000ull) - (h0 * k0 + h3 * k3);
+	v[0] = (int32_t)(uint32_t)(w >> 32);
+	v[1] = (int32_t)((uint32_t)w ^ 0x80000000u);
+}
+
+/* store_pix<1> / store_pix<0> / add_store_pix (h265.cpp:3160-3178), with the int wrap of the reference's adds */
+static inline uint8_t st_uni(int val, int shift) { return (uint8_t)clampx((int)((unsigned)val + (1u << (shift - 1))) >> shift, 256); }
+static inline int16_t st_bi0(int val, int shift) { return (int16_t)(val >> shift); }
+static inline uint8_t st_bi1(int16_t d, int val, int shift) { return (uint8_t)clampx((int)((unsigned)d + (unsigned)(val >> shift) + 64u) >> 7, 256); }
+
+/* merge_pred / pred_amvp_l0 / pred_amvp_l1 (h265.cpp:3572-3595, 3868-3903) for every prediction block */
+static void mc_picture(const h265r_picture_t *pic, const m2d_frame_t *frames, int nframes, uint8_t *luma, uint8_t *chroma)
+{
+	const int W = pic->width, pw = pic->pic_w, ph = pic->pic_h;
+	static int16_t tl[64 * 64], tc[64 * 64];
+	for (int i = 0; i < pic->n_pu; ++i) {
+		const h265r_pu_t *u = &pic->pu[i];
+		const int bi = u->ref[0] >= 0 && u->ref[1] >= 0;
+		int first = 1;
+		for (int l = 0; l < 2; ++l) {
+			if (u->ref[l] < 0 || u->ref[l] >= nframes) continue;
+			const uint8_t *rl = frames[u->ref[l]].luma, *rc = frames[u->ref[l]].chroma;
+			const int mvx = u->mv[l][0], mvy = u->mv[l][1], full = bi ? 6 : 12;
+			{
+				const int xi = u->x + (mvx >> 2), yi = u->y + (mvy >> 2), fx = mvx & 3, fy = mvy & 3;
+				for (int y = 0; y < u->h; ++y)
+					for (int x = 0; x < u->w; ++x) {
+						int sh;
+						const int v = mc_luma(rl, W, pw, ph, xi + x, yi + y, fx, fy, full, &sh);
+						uint8_t *o = &luma[(size_t)(u->y + y) * (size_t)W + (size_t)(u->x + x)];
+						if (!bi) *o = st_uni(v, sh);
+						else if (first) tl[y * 64 + x] = st_bi0(v, sh);
+						else *o = st_bi1(tl[y * 64 + x], v, sh);
+					}
+			}
+			{
+				const int xi = (u->x >> 1) + (mvx >> 3), yi = (u->y >> 1) + (mvy >> 3), fx = mvx & 7, fy = mvy & 7;
+				for (int y = 0; y < u->h / 2; ++y)
+					for (int x = 0; x < u->w / 2; ++x) {
+						int v[2];
+						mc_chroma(rc, W, pw >> 1, ph >> 1, xi + x, yi + y, fx, fy, v);
+						for (int c = 0; c < 2; ++c) {
+							uint8_t *o = &chroma[(size_t)((u->y >> 1) + y) * (size_t)W + (size_t)(u->x + 2 * x + c)];
+							if (!bi) *o = st_uni(v[c], full);
+							else if (first) tc[y * 64 + 2 * x + c] = st_bi0(v[c], full);
+							else *o = st_bi1(tc[y * 64 + 2 * x + c], v[c], full);
+						}
+					}
+			}
+			first = 0;
+		}
+	}
+}
+
 /* ------------------------------------------------------------------ the block dependency graph (analysis) */
 static int64_t g_chain[2]; /* the longest chain of blocks (the GPU kernel's critical path), blocks */
 
@@ -427,6 +551,7 @@ void h265_oracle_recon_picture(const h265r_picture_t *pic, const m2d_frame_t *fr
 	uint8_t *luma = frames[pic->slot].luma, *chroma = frames[pic->slot].chroma;
 	const int W = pic->width;
 	chain_depth(pic);
+	if (pic->n_pu) mc_picture(pic, frames, nframes, luma, chroma);
 	int pred[32 * 32], res[32 * 32];
 	for (int i = 0; i < pic->n_tu; ++i) {
 		const h265r_tu_t *t = &pic->tu[i];

@@ -53,10 +53,16 @@ def test_oracle_matches_golden(built, name):
     assert h265_violations(True) == 0
 
 
-@pytest.mark.parametrize("name", ["cov_h265_a_s1", "cov_h265_b_s2", "cov_h265_c_s3", "cov_h265_hiqp_s1"])
+INTER = [k for k in GOLD if GOLD[k]["preset"] in ("cov_h265_p", "cov_h265_hb", "cov_h265_ldb", "cov_h265_pnodbk")]
+
+
+@pytest.mark.parametrize("name", ["cov_h265_a_s1", "cov_h265_b_s2", "cov_h265_c_s3", "cov_h265_hiqp_s1"] + INTER)
 def test_parser_matches_generator_syntax(built, name, tmp_path):
     """Every CU's luma / chroma modes and every residual level the parser reads equal what the generator
-    wrote (tools/h265gen --dump), and each slice's CABAC data ends exactly on end_of_slice_segment_flag."""
+    wrote (tools/h265gen --dump), and each slice's CABAC data ends exactly on end_of_slice_segment_flag.
+    P / B pictures add every coding unit's skip / part mode and every prediction block's merge index or AMVP
+    direction with its final references and vectors: the parser's merge / AMVP / TMVP derivation
+    (m2dec_amd/csrc/host/h265_dec.c) against the generator's own (tools/h265gen)."""
     gdump, ddump = str(tmp_path / "gen.txt"), str(tmp_path / "dec.txt")
     data = h265_stream(name, gdump)
     L = m2dec_amd.lib()
@@ -79,9 +85,39 @@ def test_long_stream_follows_reference_dpb(built):
     assert len(GOLD["cov_h265_a_long_s3"]["md5"]) == 18
 
 
-def test_p_slices_are_rejected(built):
-    """P / B slices are not decoded yet: decode_picture returns -2 (the reference's error return,
-    h265.cpp:4904-4906) instead of producing frames."""
+HITS = ["merge_spatial", "merge_temporal", "merge_combined", "merge_zero", "no_bidir", "mvp_a", "mvp_b", "mvp_scaled",
+        "mvp_temporal", "mvp_zero", "bi", "lowdelay", "not_lowdelay", "col_stale", "bs_motion", "intra_cu"]
+
+
+def test_inter_goldens_cover_the_derivation(built):
+    """The P / B goldens reach every branch of the inter derivation: merge candidates of each kind selected
+    (spatial, temporal — B slices only: a P slice's temporal candidate leaves its L1 reference unset in the
+    reference, h265.cpp:3655, so h265gen never selects it —, combined bi-predictive, zero), 8x4 / 4x8 bi
+    candidates cut to L0, AMVP predictors from A, B, scaled (mvp2nd), temporal and zero fill, bi-prediction,
+    low-delay and non-low-delay B slices (TMVP list choice), a collocated_ref_idx kept from an earlier slice,
+    motion-based deblocking strengths and intra CUs inside inter pictures."""
+    L = m2dec_amd.lib()
+    L.m2dec_amd_h265_parser_hits.argtypes = [ctypes.POINTER(ctypes.c_long), ctypes.c_int, ctypes.c_int]
+    h = (ctypes.c_long * 16)()
+    L.m2dec_amd_h265_parser_hits(h, 16, 1)
+    total = [0] * 16
+    p_temporal = 0
+    for name in INTER:
+        with Oracle265Backend() as o:
+            md5s, err = m2dec_amd.decode_h265(h265_stream(name), backend=o.be)
+        assert err == -2 and md5s == GOLD[name]["md5"]
+        L.m2dec_amd_h265_parser_hits(h, 16, 1)
+        total = [a + b for a, b in zip(total, h)]
+        if GOLD[name]["preset"] in ("cov_h265_p", "cov_h265_pnodbk"):
+            p_temporal += h[1]
+    missing = [n for n, v in zip(HITS, total) if v == 0]
+    assert not missing, missing
+    assert p_temporal == 0
+
+
+def test_truncated_p_slice_is_an_error(built):
+    """A P slice whose header runs out of data: decode_picture returns -2 (the reference's error return,
+    h265.cpp:4904-4906) and the pictures before it are still output."""
     data = bytearray(h265_stream("cov_h265_a_s1"))
     # the second picture's NAL: TRAIL_R (type 1); flip its slice_type ue(2) -> ue(0) is not a byte edit, so
     # instead cut the stream after the first picture and append a forged P-slice header

@@ -41,6 +41,10 @@ typedef struct {
 	int sign_hiding, tskip, strong, sao, deblock, beta, tc;
 	int split_pct, nxn_pct, cbf_pct, big_pct; /* split / NxN / coded-block / large-level probabilities */
 	int frames;
+	/* P / B pictures (0: an intra stream) */
+	int gop;                  /* picture structure: 1 I P P P..., 2 hierarchical B, 3 low-delay B */
+	int amp, depth_inter, cabac_init, merge_level, max_merge;
+	int skip_pct, intra_pct, merge_pct, bi_pct, rqt_pct, mvd_max;
 } cfg_t;
 
 static const cfg_t presets[] = {
@@ -52,7 +56,12 @@ static const cfg_t presets[] = {
 	{"cov_h265_nosao", 192, 128, 6, 5, 2, 24, 0, 0, 0, 0, 1, 0, 1, 0, 1, 6, 6, 50, 30, 60, 5, 2},
 	{"cov_h265_hiqp", 160, 96, 4, 4, 1, 45, 3, 3, 0, 0, 1, 1, 1, 1, 1, 6, 6, 50, 30, 40, 0, 2},
 	{"c_h265_1080p", 1920, 1080, 6, 5, 1, 30, 0, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0, 35, 20, 50, 3, 8},
-	{NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+	/* P / B:        w    h   ctb tb dep qp  cbo cro sco scr sdh ts st sao dbk  b   t  spl nxn cbf big fr  gop amp dpi cin mrg mx skp int mrp bi rqt mvd */
+	{"cov_h265_p", 200, 120, 5, 4, 1, 30, 0, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0, 45, 20, 50, 3, 6, 1, 1, 1, 0, 2, 5, 20, 10, 40, 0, 60, 24},
+	{"cov_h265_hb", 232, 136, 4, 4, 1, 28, 1, -1, 0, 0, 1, 0, 1, 1, 1, 2, 2, 45, 20, 50, 3, 8, 2, 0, 0, 1, 3, 3, 25, 10, 40, 50, 55, 16},
+	{"cov_h265_ldb", 296, 168, 6, 5, 2, 32, 0, 0, 1, -1, 0, 1, 1, 1, 1, -2, 0, 40, 20, 45, 3, 8, 3, 1, 2, 1, 4, 4, 20, 8, 45, 40, 60, 40},
+	{"cov_h265_pnodbk", 168, 104, 4, 3, 1, 26, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 45, 20, 55, 3, 5, 1, 0, 1, 1, 2, 1, 15, 15, 50, 0, 65, 12},
+	{NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
 };
 
 static cfg_t C;
@@ -61,11 +70,11 @@ static FILE *dumpf;
 /* ------------------------------------------------------------------ CABAC encoder on the H.265 contexts */
 static cenc_t E;
 
-static void ctx_init(int qp)
+static void ctx_init(int qp, int init_type)
 {
 	const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
 	for (int i = 0; i < H265_NUM_CTX; ++i) {
-		int pre = ((h265_cabac_init_mn[0][i][0] * q) >> 4) + h265_cabac_init_mn[0][i][1];
+		int pre = ((h265_cabac_init_mn[init_type][i][0] * q) >> 4) + h265_cabac_init_mn[init_type][i][1];
 		pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
 		E.st[i] = (pre <= 63) ? (uint8_t)((63 - pre) << 1) : (uint8_t)(((pre - 64) << 1) | 1);
 	}
@@ -471,7 +480,573 @@ static void coding_unit(int x0, int y0, int log2)
 	transform_tree(x0, y0, log2, 0, 3, 0, 0);
 }
 
-static void quad_tree(int x0, int y0, int log2, int vx, int vy)
+/* ------------------------------------------------------------------ P / B pictures */
+/* The generator derives every block's motion itself (merge, AMVP, TMVP as the reference does them:
+ * h265.cpp:3572-3931) to write AMVP differences against the predictor and to dump the motion for
+ * tests/gen_check.py-style comparison with the parser.  Where the reference's result would depend on
+ * memory it never wrote, the generator avoids the syntax (h265gen's own rules):
+ *   - an L0-only AMVP block leaves its L1 vector unset (prediction_unit's mvxy[1]); a merge list whose
+ *     pruning (memcmp of the whole motion) would compare such bytes with different ones is not chosen;
+ *   - a P slice's temporal merge candidate leaves its L1 reference unset: never selected;
+ *   - B slices code no L1-only AMVP block (the deblocking strength would read an unset vector);
+ *   - prediction blocks at the top-right corner of a last-column CTU whose right edge is the picture's
+ *     read past the neighbour array when the picture width is a multiple of the CTB: intra there. */
+typedef struct {
+	int16_t mv[2][2];
+	int8_t ref[2];
+} gpred_t;
+
+typedef struct {
+	gpred_t p;
+	int undef;  /* mv[1] is the reference's unset stack memory (AMVP L0-only); 2: ref[1] unset (P temporal) */
+	int origin; /* the block that made the motion (undef ones compare equal only with the same origin) */
+} gmot_t;
+
+typedef struct {
+	uint8_t pu_intra, skip;
+	gmot_t m;
+} gnb_t;
+
+typedef struct {
+	uint8_t intra;
+	gpred_t p;
+} gcol_t;
+
+static gnb_t *gnb;                       /* per 4x4 unit of the picture */
+static gcol_t *gcol[8];                  /* per frame, 16x16 units */
+static int gcol_stride, origin_seq;
+static int8_t reg_frame[8][2][16];       /* per frame: its lists' frames (registered by every slice) */
+static int frame_poc[8];
+static int ref_poc[2][16];               /* the lists (persistent across slices, as in the reference) */
+static int8_t ref_frm[2][16];
+static int num_ref[2] = {1, 1}, col_l0 = 1, col_idx, cabac_init_flag, mvd_l1_zero, max_merge = 5;
+static int cur_slot, cur_poc, bslice, inter_pic, lowdelay;
+static int16_t colmv[8][8], tmvs[8][8];
+static const gcol_t *col_ref;
+static const int8_t (*col_lists)[16];
+static const gnb_t nb_out = {1, 0, {{{{0, 0}, {0, 0}}, {-1, -1}}, 0, 0}};
+
+static const gnb_t *gnb_at(int x, int y)
+{
+	if (x < 0 || y < 0 || x >= W || y >= H) return &nb_out;
+	return &gnb[(size_t)(y >> 2) * W4 + (x >> 2)];
+}
+
+static void gnb_rect(int px, int py, int w, int h, int what, const gmot_t *m)
+{
+	for (int y = py; y < py + h && y < H; y += 4)
+		for (int x = px; x < px + w && x < W; x += 4) {
+			gnb_t *u = &gnb[(size_t)(y >> 2) * W4 + (x >> 2)];
+			if (what == 0) { /* intra */
+				u->pu_intra = 1;
+				u->skip = 0;
+			} else if (what == 1) { /* motion of a merged block */
+				u->pu_intra = 0;
+				u->skip = 1;
+				u->m = *m;
+			} else if (what == 2) { /* motion of an AMVP block */
+				u->pu_intra = 0;
+				u->skip = 0;
+				u->m = *m;
+			} else { /* the CU's skip flag */
+				u->skip = (uint8_t)(what == 4);
+			}
+		}
+}
+
+static void gcol_fill(int px, int py, int w, int h, int intra, const gpred_t *p)
+{
+	for (int y = (py + 15) & ~15; y < py + h; y += 16)
+		for (int x = (px + 15) & ~15; x < px + w; x += 16) {
+			gcol_t *c = &gcol[cur_slot][(size_t)(y >> 4) * gcol_stride + (x >> 4)];
+			c->intra = (uint8_t)intra;
+			if (!intra) c->p = *p;
+		}
+}
+
+static int16_t gscale(int poc0, int refpoc0, int poc1, int refpoc1)
+{
+	const int d1 = poc1 - refpoc1, d0 = poc0 - refpoc0;
+	if (!d1) return 4096;
+	const int td = d1 < -128 ? -128 : (d1 > 127 ? 127 : d1), tb = d0 < -128 ? -128 : (d0 > 127 ? 127 : d0);
+	const int tx = (16384 + (abs(td) >> 1)) / td, v = (tb * tx + 32) >> 6;
+	return (int16_t)(v < -4096 ? -4096 : (v > 4095 ? 4095 : v));
+}
+
+static int16_t gscale_mv(int mv, int sc)
+{
+	long v = (long)mv * sc;
+	if (v >= 0) {
+		v = (v + 127) >> 8;
+		return (int16_t)(v > 32767 ? 32767 : v);
+	}
+	v = -((127 - v) >> 8);
+	return (int16_t)(v < -32768 ? -32768 : v);
+}
+
+static const gcol_t *gcol_get(int px, int py, int w, int h)
+{
+	int bx = px + w, by = py + h;
+	if ((py % CTB) + h < CTB && bx < W && by < H) {
+		const gcol_t *r = &col_ref[(size_t)(by >> 4) * gcol_stride + (bx >> 4)];
+		if (!r->intra) return r;
+	}
+	bx = px + w / 2;
+	by = py + h / 2;
+	return &col_ref[(size_t)(by >> 4) * gcol_stride + (bx >> 4)];
+}
+
+static void gadd_col(gpred_t *p, const gcol_t *col, int lx, int ref_idx)
+{
+	int cl = lowdelay ? lx : col_l0;
+	int cr = col->p.ref[cl];
+	if (cr < 0) {
+		cl ^= 1;
+		cr = col->p.ref[cl];
+	}
+	p->ref[lx] = (int8_t)ref_idx;
+	const int sc = colmv[ref_frm[lx][ref_idx] & 7][col_lists[cl][cr] & 7];
+	p->mv[lx][0] = gscale_mv(col->p.mv[cl][0], sc);
+	p->mv[lx][1] = gscale_mv(col->p.mv[cl][1], sc);
+}
+
+/* the motion comparison of the merge list's pruning: 1 equal, 0 different, -1 depends on unset memory */
+static int gmot_cmp(const gmot_t *a, const gmot_t *b)
+{
+	if (a->undef || b->undef) {
+		if (a->undef && b->undef && a->origin == b->origin) return 1;
+		if (a->p.ref[0] == b->p.ref[0] && a->p.ref[1] == b->p.ref[1] && !memcmp(a->p.mv[0], b->p.mv[0], 4)) return -1;
+		return 0;
+	}
+	return !memcmp(&a->p, &b->p, sizeof(gpred_t));
+}
+
+/* the merge candidate idx selects; -1 if the reference's choice would read unset memory */
+static int gmerge(int ua, int px, int py, int w, int h, int idx, gmot_t *out)
+{
+	gmot_t list[5];
+	int num = 0, amb = 0;
+	const int s = C.merge_level;
+	memset(list, 0, sizeof(list));
+#define ADD(nx, ny)                                                                                 \
+	do {                                                                                            \
+		const gnb_t *n_ = gnb_at(nx, ny);                                                           \
+		if (!n_->pu_intra && (((px) >> s) != ((nx) >> s) || ((py) >> s) != ((ny) >> s))) {         \
+			int dup_ = 0;                                                                       \
+			for (int i_ = 0; i_ < num; ++i_) {                                                  \
+				const int c_ = gmot_cmp(&n_->m, &list[i_]);                                     \
+				if (c_ < 0) amb = 1;                                                            \
+				if (c_ > 0) dup_ = 1;                                                           \
+			}                                                                                   \
+			if (!dup_) list[num++] = n_->m;                                                     \
+		}                                                                                       \
+	} while (0)
+	if (!(ua & 1)) ADD(px - 1, py + h - 1);
+	if (num <= idx) {
+		if (!(ua & 2)) ADD(px + w - 1, py - 1);
+		if (!(ua & 8)) ADD(px + w, py - 1);
+		if (!(ua & 4)) ADD(px - 1, py + h);
+		if (num <= idx && num < 4) ADD(px - 1, py - 1);
+	}
+#undef ADD
+	if (num <= idx) {
+		const gcol_t *col = gcol_get(px, py, w, h);
+		if (!col->intra) {
+			memset(&list[num], 0, sizeof(list[num]));
+			gadd_col(&list[num].p, col, 0, 0);
+			if (bslice) gadd_col(&list[num].p, col, 1, 0);
+			else {
+				list[num].p.ref[1] = -1;
+				list[num].undef = 2;
+			}
+			num++;
+		}
+	}
+	if (num > 1 && num <= idx && bslice) {
+		static const int8_t l0c[12] = {0, 1, 0, 2, 1, 2, 0, 3, 1, 3, 2, 3};
+		const int cut = num * (num - 1);
+		for (int c = 0; c < cut; ++c) {
+			const int i0 = l0c[c], i1 = l0c[c ^ 1];
+			if (idx <= i0 || idx <= i1) break;
+			const gpred_t a = list[i0].p, b = list[i1].p;
+			if (a.ref[0] >= 0 && b.ref[1] >= 0 && (memcmp(a.mv[0], b.mv[1], 4) || ref_poc[0][a.ref[0]] != ref_poc[1][b.ref[1]])) {
+				memset(&list[num], 0, sizeof(list[num]));
+				memcpy(list[num].p.mv[0], a.mv[0], 4);
+				memcpy(list[num].p.mv[1], b.mv[1], 4);
+				list[num].p.ref[0] = a.ref[0];
+				list[num].p.ref[1] = b.ref[1];
+				if (idx < ++num) break;
+			}
+		}
+	}
+	while (num <= idx) {
+		const int nref = bslice ? (num_ref[0] < num_ref[1] ? num_ref[0] : num_ref[1]) : num_ref[0];
+		const int m = idx - num, r = m < nref ? m : 0;
+		memset(&list[num], 0, sizeof(list[num]));
+		list[num].p.ref[0] = (int8_t)r;
+		list[num].p.ref[1] = (int8_t)(bslice ? r : -1);
+		num++;
+	}
+	if (amb || list[idx].undef == 2) return -1;
+	*out = list[idx];
+	return 0;
+}
+
+/* AMVP (calc_mv and its helpers, h265.cpp:3742-3839) */
+static void gmvp2nd(int lx, int ri, const gpred_t *n, int16_t d[2])
+{
+	int l = lx;
+	for (int k = 0; k < 2; ++k) {
+		if (n->ref[l] >= 0) {
+			const int sc = tmvs[ref_frm[lx][ri] & 7][ref_frm[l][n->ref[l]] & 7];
+			d[0] = gscale_mv(n->mv[l][0], sc);
+			d[1] = gscale_mv(n->mv[l][1], sc);
+			return;
+		}
+		l ^= 1;
+	}
+}
+
+static const int16_t *gspatial(const gnb_t *n, int lx, int refpoc, int ri, int16_t m2[2], int *skip2, int *match2)
+{
+	if (n->pu_intra) return NULL;
+	int l = lx;
+	for (int k = 0; k < 2; ++k) {
+		if (n->m.p.ref[l] >= 0) {
+			if (ref_poc[l][n->m.p.ref[l]] == refpoc) {
+				*skip2 = 1;
+				return n->m.p.mv[l];
+			}
+			if (!*skip2 && !*match2) {
+				gmvp2nd(lx, ri, &n->m.p, m2);
+				*match2 = 1;
+			}
+		}
+		l ^= 1;
+	}
+	*skip2 = 1;
+	return NULL;
+}
+
+static const int16_t *gmvp_side(int ua, int side, int px, int py, int w, int h, int lx, int ri, int16_t m2[2], int *skip2)
+{
+	const int dir = side ? ua >> 1 : ua, refpoc = ref_poc[lx][ri];
+	int match2 = 0;
+	const int16_t *mv;
+	if (!(dir & 4) && (mv = gspatial(side ? gnb_at(px + w, py - 1) : gnb_at(px - 1, py + h), lx, refpoc, ri, m2, skip2, &match2))) return mv;
+	if (!(dir & 1) && (mv = gspatial(side ? gnb_at(px + w - 1, py - 1) : gnb_at(px - 1, py + h - 1), lx, refpoc, ri, m2, skip2, &match2)))
+		return mv;
+	if (side && !(ua & 3) && (mv = gspatial(gnb_at(px - 1, py - 1), lx, refpoc, ri, m2, skip2, &match2))) return mv;
+	return match2 ? m2 : NULL;
+}
+
+static int gadd_mvp(const int16_t mv[2], int16_t l[2][2], int idx, int *n)
+{
+	const int16_t a = mv[0], b = mv[1];
+	for (int i = 0; i < *n; ++i)
+		if (l[i][0] == a && l[i][1] == b) return 0;
+	l[*n][0] = a;
+	l[*n][1] = b;
+	return idx < ++*n;
+}
+
+static void gpredictor(int ua, int px, int py, int w, int h, int lx, int ri, int mvp_idx, const gcol_t *col, int16_t out[2])
+{
+	int16_t l[2][2], m2[2] = {0, 0};
+	int n = 0, skip2 = 0;
+	const int16_t *mvp = gmvp_side(ua, 0, px, py, w, h, lx, ri, m2, &skip2);
+	if (!mvp || !gadd_mvp(mvp, l, mvp_idx, &n)) {
+		mvp = gmvp_side(ua, 1, px, py, w, h, lx, ri, m2, &skip2);
+		if (!mvp || !gadd_mvp(mvp, l, mvp_idx, &n)) {
+			gpred_t t;
+			int ok = 0;
+			if (col) {
+				gadd_col(&t, col, lx, ri);
+				ok = gadd_mvp(t.mv[lx], l, mvp_idx, &n);
+			}
+			if (!ok) memset(l[n], 0, sizeof(l[0]) * (size_t)(2 - n));
+		}
+	}
+	out[0] = l[mvp_idx][0];
+	out[1] = l[mvp_idx][1];
+}
+
+/* mvd_coding (7.3.8.9) */
+static void write_mvd(int dx, int dy)
+{
+	const int v[2] = {dx, dy};
+	for (int k = 0; k < 2; ++k) dec(H265_CTX_ABS_MVD_GT, v[k] != 0);
+	for (int k = 0; k < 2; ++k)
+		if (v[k]) dec(H265_CTX_ABS_MVD_GT + 1, abs(v[k]) > 1);
+	for (int k = 0; k < 2; ++k) {
+		if (!v[k]) continue;
+		if (abs(v[k]) > 1) { /* abs_mvd_minus2: EG1 */
+			const int r = abs(v[k]) - 2;
+			int bits = 0;
+			while (r >= (2 << bits) - 2 + (2 << bits)) bits++;
+			for (int t = 0; t < bits; ++t) byp(1);
+			byp(0);
+			bypn((uint32_t)(r - ((2 << bits) - 2)), bits + 1);
+		}
+		byp(v[k] < 0);
+	}
+}
+
+static void write_merge_idx(int idx)
+{
+	if (max_merge > 1) {
+		dec(H265_CTX_MERGE_IDX, idx > 0);
+		for (int i = 1; i < max_merge - 1 && i <= idx; ++i) byp(idx > i);
+	}
+}
+
+/* a merged block: its motion to the neighbour map and the motion field, and the dump */
+static void gmerge_apply(int px, int py, int w, int h, int idx, const gmot_t *m)
+{
+	gmot_t q = *m;
+	const int no_bidir = m->p.ref[0] >= 0 && m->p.ref[1] >= 0 && w + h == 12;
+	if (no_bidir) q.p.ref[1] = -1;
+	gnb_rect(px, py, w, h, 1, &q);
+	gcol_fill(px, py, w, h, 0, &m->p);
+	if (dumpf)
+		fprintf(dumpf, "pu %d %d %d %d m%d r %d %d mv %d %d %d %d\n", px, py, w, h, idx, m->p.ref[0], no_bidir ? -1 : m->p.ref[1],
+		        m->p.mv[0][0], m->p.mv[0][1], m->p.mv[1][0], m->p.mv[1][1]);
+}
+
+/* a merge index whose candidate the reference derives from written memory only (-1: none) */
+static int gpick_merge(int ua, int px, int py, int w, int h, gmot_t *m)
+{
+	const int start = rn(max_merge);
+	for (int k = 0; k < max_merge; ++k) {
+		const int idx = (start + k) % max_merge;
+		if (gmerge(ua, px, py, w, h, idx, m) == 0) return idx;
+	}
+	return -1;
+}
+
+/* prediction_unit: merge when allowed and drawn, else AMVP; returns 1 if merged */
+static int gpu(int log2, int ua, int pred_ua, int px, int py, int w, int h)
+{
+	gmot_t m;
+	int idx = -1;
+	if (chance(C.merge_pct)) idx = gpick_merge(ua | pred_ua, px, py, w, h, &m);
+	dec(H265_CTX_MERGE_FLAG, idx >= 0);
+	if (idx >= 0) {
+		write_merge_idx(idx);
+		gmerge_apply(px, py, w, h, idx, &m);
+		return 1;
+	}
+	int idc = 0;
+	if (bslice) {
+		idc = (w + h != 12 && chance(C.bi_pct)) ? 2 : 0; /* (no L1-only blocks) */
+		if (w + h != 12) dec(H265_CTX_INTER_PRED_IDC + (C.ctb_log2 - log2), idc == 2);
+		if (idc != 2) dec(H265_CTX_INTER_PRED_IDC + 4, 0);
+	}
+	const gcol_t *col = gcol_get(px, py, w, h);
+	if (col->intra) col = NULL;
+	memset(&m, 0, sizeof(m));
+	m.p.ref[0] = m.p.ref[1] = -1;
+	for (int lx = 0; lx < 2; ++lx) {
+		if (lx == 1 && idc != 2) continue;
+		const int ri = rn(num_ref[lx]);
+		if (num_ref[lx] > 1) {
+			const int nb = num_ref[lx] - 1, m2 = nb < 2 ? nb : 2;
+			for (int i = 0; i < m2 && i <= ri; ++i) dec(H265_CTX_REF_IDX + i, ri > i);
+			for (int i = 2; i < nb && i <= ri; ++i) byp(ri > i);
+		}
+		int dx = 0, dy = 0;
+		if (lx == 0 || !mvd_l1_zero) {
+			const int r = chance(15) ? 4 * C.mvd_max : C.mvd_max;
+			dx = rn(2 * r + 1) - r;
+			dy = rn(2 * r + 1) - r;
+			write_mvd(dx, dy);
+		}
+		const int mvp_idx = rn(2);
+		dec(H265_CTX_MVP_FLAG, mvp_idx);
+		int16_t mvp[2];
+		gpredictor(ua, px, py, w, h, lx, ri, mvp_idx, col, mvp);
+		m.p.ref[lx] = (int8_t)ri;
+		m.p.mv[lx][0] = (int16_t)(mvp[0] + dx);
+		m.p.mv[lx][1] = (int16_t)(mvp[1] + dy);
+	}
+	if (idc == 0) {
+		m.undef = 1;
+		m.origin = ++origin_seq;
+	}
+	gnb_rect(px, py, w, h, 2, &m);
+	gcol_fill(px, py, w, h, 0, &m.p);
+	if (dumpf)
+		fprintf(dumpf, "pu %d %d %d %d a%d r %d %d mv %d %d %d %d\n", px, py, w, h, idc, m.p.ref[0], m.p.ref[1], m.p.mv[0][0], m.p.mv[0][1],
+		        m.p.mv[1][0], m.p.mv[1][1]);
+	return 0;
+}
+
+/* transform_tree of an inter CU */
+static void transform_tree_inter(int x0, int y0, int log2, int depth, int cbf_cbcr, int blk)
+{
+	int split = 0, cbf = 0;
+	if (C.max_tb_log2 < log2) {
+		split = 1;
+	} else if (2 < log2 && depth < C.depth_inter) {
+		split = chance(C.split_pct);
+		dec(H265_CTX_SPLIT_TRANSFORM + 5 - log2, split);
+	} else {
+		split = depth == 0 && intra_split;
+	}
+	if (log2 > 2) {
+		if (cbf_cbcr & 2) {
+			const int b = chance(C.cbf_pct);
+			dec(H265_CTX_CBF_CHROMA + depth, b);
+			cbf |= b << 1;
+		}
+		if (cbf_cbcr & 1) {
+			const int b = chance(C.cbf_pct);
+			dec(H265_CTX_CBF_CHROMA + depth, b);
+			cbf |= b;
+		}
+	} else {
+		cbf = cbf_cbcr;
+	}
+	if (split) {
+		const int h = 1 << (log2 - 1);
+		transform_tree_inter(x0, y0, log2 - 1, depth + 1, cbf, 0);
+		transform_tree_inter(x0 + h, y0, log2 - 1, depth + 1, cbf, 1);
+		transform_tree_inter(x0, y0 + h, log2 - 1, depth + 1, cbf, 2);
+		transform_tree_inter(x0 + h, y0 + h, log2 - 1, depth + 1, cbf, 3);
+		return;
+	}
+	int cl = 1;
+	if (depth || cbf) {
+		cl = chance(C.cbf_pct);
+		dec(H265_CTX_CBF_LUMA + (depth == 0), cl);
+	}
+	if (cl) residual(log2, 0, 0);
+	if (cbf && (log2 > 2 || blk == 3)) {
+		const int c = log2 > 2 ? log2 - 1 : 2;
+		if (cbf & 2) residual(c, 1, 0);
+		if (cbf & 1) residual(c, 2, 0);
+	}
+}
+
+static const int8_t gav4[3][16] = {{0, 5, 10, 15, 0, 5, 10, 15, 0, 5, 10, 15, 0, 5, 10, 15},
+                                   {4, 4, 6, 6, 4, 4, 6, 6, 12, 12, 14, 14, 12, 12, 14, 14},
+                                   {0, 1, 0, 1, 4, 5, 4, 5, 0, 1, 0, 1, 4, 5, 4, 5}};
+static const int8_t gav21[2][16] = {{0, 1, 2, 3, 0, 5, 2, 7, 8, 9, 10, 11, 8, 13, 10, 15}, {8, 9, 8, 9, 12, 13, 12, 13, 8, 9, 8, 9, 12, 13, 12, 13}};
+static const int8_t gav12[2][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 10, 11, 4, 5, 14, 15}, {4, 4, 6, 6, 4, 4, 6, 6, 12, 12, 14, 14, 12, 12, 14, 14}};
+
+static void coding_unit(int x0, int y0, int log2);
+
+static void coding_unit_inter(int x0, int y0, int log2, int ua)
+{
+	const int len = 1 << log2;
+	for (int j = 0; j < (1 << (log2 - 2)); ++j) memset(cb_log2 + (size_t)((y0 >> 2) + j) * W4 + (x0 >> 2), log2, (size_t)1 << (log2 - 2));
+	/* the top-right corner of a last-column CTU at the picture's right edge (W a multiple of the CTB) */
+	const int corner = (W % CTB) == 0 && x0 + len == W && (y0 % CTB) == 0 && y0 > 0;
+	{
+		const int ctx = (!(ua & 1) && gnb_at(x0 - 1, y0)->skip) + (!(ua & 2) && gnb_at(x0, y0 - 1)->skip);
+		gmot_t m;
+		int idx = -1;
+		if (!corner && chance(C.skip_pct)) idx = gpick_merge(ua, x0, y0, len, len, &m);
+		dec(H265_CTX_CU_SKIP + ctx, idx >= 0);
+		if (idx >= 0) {
+			if (dumpf) fprintf(dumpf, "icu %d %d l%d skip\n", x0, y0, log2);
+			write_merge_idx(idx);
+			gmerge_apply(x0, y0, len, len, idx, &m);
+			gnb_rect(x0, y0, len, len, 4, NULL);
+			return;
+		}
+	}
+	if (corner || chance(C.intra_pct)) {
+		dec(H265_CTX_PRED_MODE, 1);
+		coding_unit(x0, y0, log2);
+		gnb_rect(x0, y0, len, len, 0, NULL);
+		gcol_fill(x0, y0, len, len, 1, NULL);
+		return;
+	}
+	dec(H265_CTX_PRED_MODE, 0);
+	/* part_mode: 2Nx2N, 2NxN, Nx2N, and the AMP modes when enabled above the minimum CU (no inter NxN) */
+	int part = 0;
+	{
+		const int r = rn(100);
+		if (r < 45) part = 0;
+		else if (r < 65) part = 1;
+		else if (r < 85) part = 2;
+		else part = (C.amp && log2 > 3) ? 4 + rn(4) : 1 + rn(2);
+		dec(H265_CTX_PART_MODE, part == 0);
+		if (part) {
+			const int horiz = part == 1 || part == 4 || part == 5;
+			dec(H265_CTX_PART_MODE + 1, horiz);
+			if (log2 > 3) {
+				if (C.amp) {
+					dec(H265_CTX_PART_MODE + 3, part < 4);
+					if (part >= 4) byp(part & 1);
+				}
+			}
+		}
+	}
+	if (dumpf) fprintf(dumpf, "icu %d %d l%d p%d\n", x0, y0, log2, part);
+	int merged = 0;
+	{
+		const int hl = len >> 1, ql = len >> 2;
+		switch (part) {
+		case 0: merged = gpu(log2, ua, 0, x0, y0, len, len); break;
+		case 1:
+			gpu(log2, gav21[0][ua], 0, x0, y0, len, hl);
+			gpu(log2, gav21[1][ua], 2, x0, y0 + hl, len, hl);
+			break;
+		case 2:
+			gpu(log2, gav12[0][ua], 0, x0, y0, hl, len);
+			gpu(log2, gav12[1][ua], 1, x0 + hl, y0, hl, len);
+			break;
+		case 4:
+			gpu(log2, gav21[0][ua], 0, x0, y0, len, ql);
+			gpu(log2, gav21[1][ua], 2, x0, y0 + ql, len, len - ql);
+			break;
+		case 5:
+			gpu(log2, gav21[0][ua], 0, x0, y0, len, len - ql);
+			gpu(log2, gav21[1][ua], 2, x0, y0 + len - ql, len, ql);
+			break;
+		case 6:
+			gpu(log2, gav12[0][ua], 0, x0, y0, ql, len);
+			gpu(log2, gav12[1][ua], 1, x0 + ql, y0, len - ql, len);
+			break;
+		default:
+			gpu(log2, gav12[0][ua], 0, x0, y0, len - ql, len);
+			gpu(log2, gav12[1][ua], 1, x0 + len - ql, y0, ql, len);
+			break;
+		}
+	}
+	int rqt = 1;
+	if (!(part == 0 && merged)) {
+		rqt = chance(C.rqt_pct);
+		dec(H265_CTX_RQT_ROOT_CBF, rqt);
+	}
+	if (rqt) {
+		intra_split = part != 0 && C.depth_inter == 0;
+		transform_tree_inter(x0, y0, log2, 0, 3, 0);
+	}
+	gnb_rect(x0, y0, len, len, 3, NULL);
+}
+
+/* the slice's temporal state (colpics_t::init) */
+static void inter_slice_setup(void)
+{
+	const int cl = col_l0 ^ 1;
+	const int cf = ref_frm[cl][col_idx] & 7, cp = ref_poc[cl][col_idx];
+	col_ref = gcol[cf];
+	col_lists = (const int8_t(*)[16])reg_frame[cf];
+	for (int i = 0; i < 8; ++i)
+		for (int j = 0; j < 8; ++j) {
+			colmv[i][j] = gscale(cur_poc, frame_poc[i], cp, frame_poc[j]);
+			tmvs[i][j] = gscale(cur_poc, frame_poc[i], cur_poc, frame_poc[j]);
+		}
+	lowdelay = 1;
+	for (int i = 0; i < 8; ++i)
+		if (cur_poc < frame_poc[i]) lowdelay = 0;
+	for (size_t i = 0; i < (size_t)W4 * (FH / 4); ++i) gnb[i] = nb_out;
+}
+
+static void quad_tree(int x0, int y0, int log2, int vx, int vy, int ua)
 {
 	if (vx <= 0 || vy <= 0) return;
 	if (3 < log2) {
@@ -484,14 +1059,15 @@ static void quad_tree(int x0, int y0, int log2, int vx, int vy)
 		}
 		if (split) {
 			const int h = 1 << (log2 - 1);
-			quad_tree(x0, y0, log2 - 1, vx, vy);
-			quad_tree(x0 + h, y0, log2 - 1, vx - h, vy < h ? vy : h);
-			quad_tree(x0, y0 + h, log2 - 1, vx < 2 * h ? vx : 2 * h, vy - h);
-			quad_tree(x0 + h, y0 + h, log2 - 1, (vx - h) < h ? vx - h : h, (vy - h) < h ? vy - h : h);
+			quad_tree(x0, y0, log2 - 1, vx, vy, gav4[0][ua]);
+			quad_tree(x0 + h, y0, log2 - 1, vx - h, vy < h ? vy : h, gav4[1][ua]);
+			quad_tree(x0, y0 + h, log2 - 1, vx < 2 * h ? vx : 2 * h, vy - h, gav4[2][ua]);
+			quad_tree(x0 + h, y0 + h, log2 - 1, (vx - h) < h ? vx - h : h, (vy - h) < h ? vy - h : h, 12);
 			return;
 		}
 	}
-	coding_unit(x0, y0, log2);
+	if (inter_pic) coding_unit_inter(x0, y0, log2, ua);
+	else coding_unit(x0, y0, log2);
 }
 
 typedef struct {
@@ -628,19 +1204,30 @@ static void write_sps(bw_t *out)
 	bw_ue(&w, (uint32_t)(C.ctb_log2 - 3));    /* ctb */
 	bw_ue(&w, 0);                             /* min tb 4 */
 	bw_ue(&w, (uint32_t)(C.max_tb_log2 - 2)); /* max tb */
-	bw_ue(&w, 1);                             /* depth inter */
+	bw_ue(&w, (uint32_t)(C.gop ? C.depth_inter : 1)); /* depth inter */
 	bw_ue(&w, (uint32_t)C.depth_intra);
 	bw_bit(&w, 0); /* scaling lists */
-	bw_bit(&w, 0); /* amp */
+	bw_bit(&w, (uint32_t)C.amp);
 	bw_bit(&w, (uint32_t)C.sao);
 	bw_bit(&w, 0); /* pcm */
-	bw_ue(&w, 1);  /* one short-term RPS: {-1} */
-	bw_ue(&w, 1);
-	bw_ue(&w, 0);
-	bw_ue(&w, 0);
-	bw_bit(&w, 1);
+	/* 8 short-term RPS sets (I slices name set 0): the reference sizes its motion-field buffers by their
+	 * count, min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8) frames (h265.cpp:121-128) */
+	bw_ue(&w, 8);
+	for (int i = 0; i < 8; ++i) {
+		if (i) bw_bit(&w, 0); /* inter_ref_pic_set_prediction_flag */
+		bw_ue(&w, (uint32_t)(1 + (i & 3)));
+		bw_ue(&w, (uint32_t)(i >> 2));
+		for (int k = 0; k < 1 + (i & 3); ++k) {
+			bw_ue(&w, 0);
+			bw_bit(&w, 1);
+		}
+		for (int k = 0; k < (i >> 2); ++k) {
+			bw_ue(&w, 0);
+			bw_bit(&w, 1);
+		}
+	}
 	bw_bit(&w, 0); /* long-term */
-	bw_bit(&w, 0); /* temporal mvp */
+	bw_bit(&w, (uint32_t)(C.gop != 0)); /* temporal mvp */
 	bw_bit(&w, (uint32_t)C.strong);
 	bw_bit(&w, 0); /* vui */
 	bw_bit(&w, 0); /* extension */
@@ -659,7 +1246,7 @@ static void write_pps(bw_t *out)
 	bw_bit(&w, 0);
 	bw_bits(&w, 0, 3);
 	bw_bit(&w, (uint32_t)C.sign_hiding);
-	bw_bit(&w, 0);
+	bw_bit(&w, (uint32_t)C.cabac_init); /* cabac_init_present */
 	bw_ue(&w, 0);
 	bw_ue(&w, 0);
 	bw_se(&w, 0); /* init_qp 26 */
@@ -682,7 +1269,7 @@ static void write_pps(bw_t *out)
 	bw_se(&w, 0);
 	bw_bit(&w, 0); /* scaling list data */
 	bw_bit(&w, 0);
-	bw_ue(&w, 0);
+	bw_ue(&w, (uint32_t)(C.gop ? C.merge_level - 2 : 0));
 	bw_bit(&w, 0);
 	bw_bit(&w, 0);
 	bw_trailing(&w);
@@ -690,23 +1277,94 @@ static void write_pps(bw_t *out)
 	free(w.b);
 }
 
+/* the picture structures (decode order: POC and slice type, 2 = I, 1 = P, 0 = B) */
+static const int gop_poc[4][8] = {{0}, {0, 1, 2, 3, 4, 5, 6, 7}, {0, 4, 2, 1, 3, 8, 6, 5}, {0, 1, 2, 3, 4, 5, 6, 7}};
+static const int gop_type[4][8] = {{2}, {2, 1, 1, 1, 1, 1, 1, 1}, {2, 1, 0, 0, 0, 1, 0, 0}, {2, 0, 0, 1, 2, 0, 0, 0}};
+
 static void write_slice(bw_t *out, int idx)
 {
 	bw_t w;
 	const int idr = idx == 0;
+	const int type = C.gop ? gop_type[C.gop][idx] : 2, poc = C.gop ? gop_poc[C.gop][idx] : idx;
 	bw_init(&w);
 	bw_bit(&w, 1); /* first slice */
 	if (idr) bw_bit(&w, 0); /* no_output_of_prior_pics */
 	bw_ue(&w, 0);
-	bw_ue(&w, 2); /* I */
+	bw_ue(&w, (uint32_t)type);
+	cur_slot = idx & 7; /* (P / B streams: at most 8 pictures, never output before the end: picture k in frame k) */
+	cur_poc = poc;
+	inter_pic = type < 2;
+	bslice = type == 0;
 	if (!idr) {
-		bw_bits(&w, (uint32_t)(idx & 255), 8);
-		bw_bit(&w, 1); /* the SPS RPS */
+		bw_bits(&w, (uint32_t)(poc & 255), 8);
+		if (!inter_pic) {
+			bw_bit(&w, 1); /* the SPS RPS, index in log2ceil(8) = 4 bits (the reference's count, h265.cpp:757-759) */
+			bw_bits(&w, 0, 4);
+		} else {
+			/* every picture decoded so far, nearest first on each side, all used */
+			int neg[8], pos[8], nn = 0, np = 0;
+			for (int d = poc - 1; d >= 0; --d)
+				for (int k = 0; k < idx; ++k)
+					if (gop_poc[C.gop][k] == d && nn < 4) neg[nn++] = d;
+			for (int d = poc + 1; d < 64; ++d)
+				for (int k = 0; k < idx; ++k)
+					if (gop_poc[C.gop][k] == d && np < 4) pos[np++] = d;
+			bw_bit(&w, 0); /* short_term_ref_pic_set_sps_flag */
+			bw_bit(&w, 0); /* inter_ref_pic_set_prediction_flag */
+			bw_ue(&w, (uint32_t)nn);
+			bw_ue(&w, (uint32_t)np);
+			for (int k = 0, prev = poc; k < nn; prev = neg[k], ++k) {
+				bw_ue(&w, (uint32_t)(prev - neg[k] - 1));
+				bw_bit(&w, 1);
+			}
+			for (int k = 0, prev = poc; k < np; prev = pos[k], ++k) {
+				bw_ue(&w, (uint32_t)(pos[k] - prev - 1));
+				bw_bit(&w, 1);
+			}
+			/* init_ref_pic_list with every entry used: L0 = negatives then positives, L1 the other way */
+			const int tot = nn + np;
+			for (int lx = 0; lx < 2; ++lx)
+				for (int k = 0; k < tot; ++k) {
+					const int pc = lx == 0 ? (k < nn ? neg[k] : pos[k - nn]) : (k < np ? pos[k] : neg[k - np]);
+					ref_poc[lx][k] = pc;
+					for (int f = 0; f < idx; ++f)
+						if (gop_poc[C.gop][f] == pc) ref_frm[lx][k] = (int8_t)f;
+				}
+			num_ref[0] = 1 + rn(tot < 15 ? tot : 15);
+			if (bslice) num_ref[1] = 1 + rn(tot < 15 ? tot : 15);
+		}
+		if (C.gop) bw_bit(&w, 1); /* slice_temporal_mvp_enabled_flag */
 	}
+	frame_poc[cur_slot] = poc;
 	if (C.sao) {
 		bw_bit(&w, 1);
 		bw_bit(&w, 1);
 	}
+	if (inter_pic) {
+		bw_bit(&w, 1); /* num_ref_idx_active_override_flag */
+		bw_ue(&w, (uint32_t)(num_ref[0] - 1));
+		if (bslice) bw_ue(&w, (uint32_t)(num_ref[1] - 1));
+		if (bslice) {
+			mvd_l1_zero = rn(2);
+			bw_bit(&w, (uint32_t)mvd_l1_zero);
+		}
+		if (C.cabac_init) {
+			cabac_init_flag = rn(2);
+			bw_bit(&w, (uint32_t)cabac_init_flag);
+		}
+		col_l0 = bslice ? rn(2) : 1;
+		if (bslice) bw_bit(&w, (uint32_t)col_l0);
+		if (num_ref[col_l0 ^ 1] > 1) { /* else collocated_ref_idx keeps the previous slice's value */
+			col_idx = rn(num_ref[col_l0 ^ 1]);
+			bw_ue(&w, (uint32_t)col_idx);
+		}
+		max_merge = C.max_merge - rn(2);
+		if (max_merge < 1) max_merge = 1;
+		bw_ue(&w, (uint32_t)(5 - max_merge));
+	}
+	/* every slice registers its (possibly stale) lists for the frame (colpics_t::init) */
+	memcpy(reg_frame[cur_slot][0], ref_frm[0], 16);
+	memcpy(reg_frame[cur_slot][1], ref_frm[1], 16);
 	bw_se(&w, C.qp - 26);
 	bw_se(&w, C.slice_cb);
 	bw_se(&w, C.slice_cr);
@@ -722,16 +1380,19 @@ static void write_slice(bw_t *out, int idx)
 	while (!bw_aligned(&w)) bw_bit(&w, 0);
 	/* slice data */
 	cenc_start(&E, &w);
-	ctx_init(C.qp);
+	ctx_init(C.qp, inter_pic ? 2 - (type ^ cabac_init_flag) : 0);
 	memset(cb_log2, 0, (size_t)W4 * (FH / 4));
 	memset(ipm, 1, (size_t)W4 * (FH / 4));
+	if (inter_pic) inter_slice_setup();
+	else if (gcol[cur_slot])
+		for (size_t i = 0; i < (size_t)gcol_stride * (size_t)((H + 15) >> 4); ++i) gcol[cur_slot][i].intra = 1;
 	{
 		sao_t *map = (sao_t *)calloc((size_t)(cols * rows), sizeof(sao_t));
 		for (int cy = 0; cy < rows; ++cy)
 			for (int cx = 0; cx < cols; ++cx) {
 				const int x0 = cx * CTB, y0 = cy * CTB;
 				sao_ctu(map, cx, cy);
-				quad_tree(x0, y0, C.ctb_log2, W - x0, (H - y0) < CTB ? H - y0 : CTB);
+				quad_tree(x0, y0, C.ctb_log2, W - x0, (H - y0) < CTB ? H - y0 : CTB, (cy == 0 ? 10 : 0) | (cx == 0 ? 5 : 0) | 4);
 				if (cx != cols - 1 || cy != rows - 1) cenc_terminate(&E, 0);
 			}
 		free(map);
@@ -739,6 +1400,7 @@ static void write_slice(bw_t *out, int idx)
 	cenc_terminate(&E, 1); /* end_of_slice_segment_flag (flush; its last bit is rbsp_stop_one_bit) */
 	while (!bw_aligned(&w)) bw_bit(&w, 0);
 	nal(out, idr ? H265_IDR_W_RADL : H265_TRAIL_R, &w);
+	if (C.gop && idx + 1 > 8) fprintf(stderr, "h265gen: more than 8 pictures\n");
 	free(w.b);
 }
 
@@ -778,6 +1440,10 @@ int main(int argc, char **argv)
 	W4 = FW / 4;
 	cb_log2 = (uint8_t *)malloc((size_t)W4 * (FH / 4));
 	ipm = (uint8_t *)malloc((size_t)W4 * (FH / 4));
+	gnb = (gnb_t *)malloc(sizeof(gnb_t) * (size_t)W4 * (FH / 4));
+	gcol_stride = (W + 15) >> 4;
+	for (int i = 0; i < 8; ++i) gcol[i] = (gcol_t *)calloc((size_t)gcol_stride * (size_t)((H + 15) >> 4), sizeof(gcol_t));
+	if (C.gop && C.frames > 8) C.frames = 8;
 	bw_t out;
 	bw_init(&out);
 	write_vps(&out);

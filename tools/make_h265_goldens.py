@@ -27,7 +27,12 @@ STREAMS = [("cov_h265_a_s1", "cov_h265_a", 1, 3), ("cov_h265_a_s2", "cov_h265_a"
            ("cov_h265_c_s2", "cov_h265_c", 2, 3), ("cov_h265_c_s3", "cov_h265_c", 3, 3),
            ("cov_h265_nodbk_s1", "cov_h265_nodbk", 1, 2), ("cov_h265_nosao_s1", "cov_h265_nosao", 1, 2),
            ("cov_h265_hiqp_s1", "cov_h265_hiqp", 1, 2), ("cov_h265_a_long_s3", "cov_h265_a", 3, 20),
-           ("c_h265_1080p_s1", "c_h265_1080p", 1, 8)]
+           ("c_h265_1080p_s1", "c_h265_1080p", 1, 8),
+           # P / B pictures: merge / AMVP / TMVP, bi-prediction, AMP, inter transform trees, inter deblocking
+           ("cov_h265_p_s1", "cov_h265_p", 1, 6), ("cov_h265_p_s2", "cov_h265_p", 2, 6),
+           ("cov_h265_hb_s1", "cov_h265_hb", 1, 8), ("cov_h265_hb_s2", "cov_h265_hb", 2, 8),
+           ("cov_h265_ldb_s1", "cov_h265_ldb", 1, 8), ("cov_h265_ldb_s2", "cov_h265_ldb", 2, 8),
+           ("cov_h265_pnodbk_s1", "cov_h265_pnodbk", 1, 5)]
 
 
 def gen(preset, seed, frames, dump=None):
@@ -52,7 +57,7 @@ def check_syntax(preset, seed, frames):
         finally:
             m2dec_amd.lib().m2dec_amd_h265_set_dump(None)
         a, b = open(g).read().splitlines(), open(p).read().splitlines()
-        return a == [line for line in b if line.startswith(("pic", "cu", "res"))], len(a), b
+        return a == [line for line in b if line.startswith(("pic", "cu", "res", "icu", "pu"))], len(a), b
 
 
 def main():

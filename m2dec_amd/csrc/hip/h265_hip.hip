@@ -1,5 +1,5 @@
 /*
- * gfx950 reconstruction of H.265 intra pictures (h265d_func): the records of one picture (include/m2d_recon.h
+ * gfx950 reconstruction of H.265 pictures (h265d_func): the records of one picture (include/m2d_recon.h
  * h265r_*, made by m2dec_amd/csrc/host/h265_dec.c) in, the picture's NV12 samples in its device frame out.
  * It restates the reference decoder's reconstruction (h265.cpp:1693-2913 intra prediction and residual,
  * :4125-4384 deblocking, :4386-4729 SAO), exactly as oracle/h265_oracle.c does on the CPU.
@@ -19,6 +19,12 @@
  *   sample, so every segment of a direction is independent.  Chroma rides on the luma segment (bS 2,
  *   16-sample grid).
  * k_h265_sao — one thread per sample, from a copy of the deblocked frame.
+ * k_h265_mc — P / B pictures, before the blocks: one 64-lane workgroup per prediction block (grid-stride),
+ *   each list's reference window ((w + 7) x (h + 7) luma bytes, (w / 2 + 3) x (h / 2 + 3) CbCr pairs, positions
+ *   clamped to the picture as the reference's address_umv does) staged in LDS, then every sample computed
+ *   from LDS: the 8-tap luma filters (1-D with shift - 6, 2-D through int16 horizontal sums) and the
+ *   reference's packed two-component chroma arithmetic in 64-bit integers, bi-prediction averaged through an
+ *   int16 LDS buffer.  The CTU kernel then starts each CTU from these samples and adds the residuals.
  * Bounds: the intra kernel is latency-bound on the block chain (a 32x32 block is a 2 x 32^3 MAC inverse
  * transform on one wave); deblocking and SAO are HBM-bound (each reads and writes the frame once).
  */
@@ -52,6 +58,11 @@ struct H265Args {
 	int *err;         /* sticky: a hand-off that never came */
 	int W, H, pic_w, pic_h, ctb_log2, n_tu, flags;
 	int beta_offset, tc_offset, cb_qp_offset, cr_qp_offset;
+	/* P / B pictures */
+	const h265r_pu_t *pu;
+	const uint8_t *frames; /* every frame (the references), fsz bytes apart */
+	size_t fsz;
+	int n_pu;
 };
 
 __constant__ int c_cos[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
@@ -472,6 +483,19 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 			tl.ly[tid] = col ? tl.y[tid][ctb - 1] : 128;
 			tl.lc[tid] = col ? tl.c[tid >> 1][ctb - 2 + (tid & 1)] : 128;
 		}
+		/* P / B pictures: the CTU starts from its motion-compensated samples (k_h265_mc, an earlier launch) */
+		if (a.n_pu) {
+			__syncthreads(); /* (the previous CTU's last column is in tl.ly) */
+			const int wpr = (cols_here + 3) >> 2;
+			for (int w = tid; w < wpr * rows_here; w += 128) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
+			}
+			for (int w = tid; w < wpr * crows; w += 128) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
+			}
+		}
 		/* the row above, once that CTU row finished the CTU above-right */
 		if (row > 0) {
 			if (wave == 0) {
@@ -537,6 +561,123 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 		}
 	}
 	(void)cctb;
+}
+
+/* ---- motion compensation (h265.cpp:3132-3595; oracle/h265_oracle.c mc_picture) */
+__constant__ int8_t c_luma_fir[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0}, {-1, 4, -10, 58, 17, -5, 1, 0}, {-1, 4, -11, 40, 40, -11, 4, -1}, {0, 1, -5, 17, 58, -10, 4, -1}};
+__constant__ int8_t c_chroma_fir[8][4] = {{0, 64, 0, 0}, {2, 58, 10, 2}, {4, 54, 16, 2}, {6, 46, 28, 4}, {4, 36, 36, 4}, {4, 28, 46, 6}, {2, 16, 54, 4}, {2, 10, 58, 2}};
+
+#define MC_WIN 72 /* luma window row pitch: 64 + 7 */
+struct McLds {
+	uint8_t win[(64 + 7) * MC_WIN];     /* luma reference window */
+	uint8_t cwin[(32 + 3) * (32 + 3) * 2]; /* CbCr pairs */
+	int16_t acc[64 * 64];               /* bi-prediction: the first list's luma */
+	int16_t cacc[32 * 64];              /* ... and chroma (Cb, Cr interleaved) */
+};
+
+__device__ __forceinline__ int mc_clampx(int v, int m) { return v < 0 ? 0 : (v >= m ? m - 1 : v); }
+
+/* store_pix<1> / store_pix<0> / add_store_pix, with the reference's 32-bit wrap */
+__device__ __forceinline__ uint8_t mc_uni(int v, int sh) { return (uint8_t)mc_clampx((int)((unsigned)v + (1u << (sh - 1))) >> sh, 256); }
+__device__ __forceinline__ int16_t mc_bi0(int v, int sh) { return (int16_t)(v >> sh); }
+__device__ __forceinline__ uint8_t mc_bi1(int16_t d, int v, int sh) { return (uint8_t)mc_clampx((int)((unsigned)d + (unsigned)(v >> sh) + 64u) >> 7, 256); }
+
+__device__ __forceinline__ uint64_t mc_chroma_h(const uint8_t *cw, int pitch, int r, int x, int fx)
+{
+	const uint8_t *q = cw + (size_t)(r * pitch + x) * 2;
+	const uint64_t a0 = ((uint64_t)q[0] << 32) | q[1], a1 = ((uint64_t)q[2] << 32) | q[3];
+	const uint64_t a2 = ((uint64_t)q[4] << 32) | q[5], a3 = ((uint64_t)q[6] << 32) | q[7];
+	const uint64_t c0 = (uint64_t)c_chroma_fir[fx][0], c1 = (uint64_t)c_chroma_fir[fx][1], c2 = (uint64_t)c_chroma_fir[fx][2],
+	               c3 = (uint64_t)c_chroma_fir[fx][3];
+	return (((c1 * a1 + c2 * a2) | 0x80000000ull) - (c0 * a0 + c3 * a3)) & ~0xf8000000ull;
+}
+
+__global__ __launch_bounds__(64) void k_h265_mc(const H265Args *ap)
+{
+	const H265Args &a = *ap;
+	__shared__ McLds s;
+	const int lane = threadIdx.x;
+	const int W = a.W, pw = a.pic_w, ph = a.pic_h, cw = a.pic_w >> 1, chh = a.pic_h >> 1;
+	for (int pi = blockIdx.x; pi < a.n_pu; pi += gridDim.x) {
+		const h265r_pu_t u = a.pu[pi];
+		const int w = u.w, h = u.h;
+		const bool bi = u.ref[0] >= 0 && u.ref[1] >= 0;
+		const int full = bi ? 6 : 12;
+		uint8_t *luma = a.frame, *chroma = a.frame + (size_t)W * a.H;
+		bool first = true;
+		for (int l = 0; l < 2; ++l) {
+			if (u.ref[l] < 0) continue;
+			const uint8_t *rl = a.frames + (size_t)u.ref[l] * a.fsz, *rc = rl + (size_t)W * a.H;
+			const int mvx = u.mv[l][0], mvy = u.mv[l][1];
+			const int fx = mvx & 3, fy = mvy & 3, xi = u.x + (mvx >> 2) - 3, yi = u.y + (mvy >> 2) - 3;
+			const int cfx = mvx & 7, cfy = mvy & 7, cxi = (u.x >> 1) + (mvx >> 3) - 1, cyi = (u.y >> 1) + (mvy >> 3) - 1;
+			const int ww = w + 7, wh = h + 7, cww = (w >> 1) + 3, cwh = (h >> 1) + 3;
+			__syncthreads(); /* (the previous list's / block's windows are consumed) */
+			for (int i = lane; i < ww * wh; i += 64) {
+				const int r = i / ww, c = i - r * ww;
+				s.win[r * MC_WIN + c] = rl[(size_t)mc_clampx(yi + r, ph) * W + mc_clampx(xi + c, pw)];
+			}
+			for (int i = lane; i < cww * cwh; i += 64) {
+				const int r = i / cww, c = i - r * cww;
+				const uint8_t *q = rc + (size_t)mc_clampx(cyi + r, chh) * W + (size_t)mc_clampx(cxi + c, cw) * 2;
+				s.cwin[(r * cww + c) * 2] = q[0];
+				s.cwin[(r * cww + c) * 2 + 1] = q[1];
+			}
+			__syncthreads();
+			for (int i = lane; i < w * h; i += 64) {
+				const int y = i / w, x = i - y * w;
+				int v = 0, sh = full;
+				if (!fx && !fy) {
+					v = (int)s.win[(y + 3) * MC_WIN + x + 3] << 12;
+				} else if (!fy) {
+					const uint8_t *q = &s.win[(y + 3) * MC_WIN + x];
+#pragma unroll
+					for (int k = 0; k < 8; ++k) v += c_luma_fir[fx][k] * (int)q[k];
+					sh = full - 6;
+				} else if (!fx) {
+					const uint8_t *q = &s.win[y * MC_WIN + x + 3];
+#pragma unroll
+					for (int k = 0; k < 8; ++k) v += c_luma_fir[fy][k] * (int)q[k * MC_WIN];
+					sh = full - 6;
+				} else {
+#pragma unroll
+					for (int r = 0; r < 8; ++r) {
+						const uint8_t *q = &s.win[(y + r) * MC_WIN + x];
+						int hs = 0;
+#pragma unroll
+						for (int k = 0; k < 8; ++k) hs += c_luma_fir[fx][k] * (int)q[k];
+						v += c_luma_fir[fy][r] * (int)(int16_t)hs;
+					}
+				}
+				uint8_t *o = luma + (size_t)(u.y + y) * W + u.x + x;
+				if (!bi) *o = mc_uni(v, sh);
+				else if (first) s.acc[y * 64 + x] = mc_bi0(v, sh);
+				else *o = mc_bi1(s.acc[y * 64 + x], v, sh);
+			}
+			for (int i = lane; i < (w >> 1) * (h >> 1); i += 64) {
+				const int y = i / (w >> 1), x = i - y * (w >> 1);
+				const uint64_t h0 = mc_chroma_h(s.cwin, cww, y, x, cfx), h1 = mc_chroma_h(s.cwin, cww, y + 1, x, cfx);
+				const uint64_t h2 = mc_chroma_h(s.cwin, cww, y + 2, x, cfx), h3 = mc_chroma_h(s.cwin, cww, y + 3, x, cfx);
+				const uint64_t k0 = (uint64_t)c_chroma_fir[cfy][0], k1 = (uint64_t)c_chroma_fir[cfy][1], k2 = (uint64_t)c_chroma_fir[cfy][2],
+				               k3 = (uint64_t)c_chroma_fir[cfy][3];
+				const uint64_t wv = ((h1 * k1 + h2 * k2) | 0x80000000ull) - (h0 * k0 + h3 * k3);
+				const int vb = (int)(uint32_t)(wv >> 32), vr = (int)((uint32_t)wv ^ 0x80000000u);
+				uint8_t *o = chroma + (size_t)((u.y >> 1) + y) * W + u.x + 2 * x;
+				int16_t *ca = &s.cacc[y * 64 + 2 * x];
+				if (!bi) {
+					o[0] = mc_uni(vb, full);
+					o[1] = mc_uni(vr, full);
+				} else if (first) {
+					ca[0] = mc_bi0(vb, full);
+					ca[1] = mc_bi0(vr, full);
+				} else {
+					o[0] = mc_bi1(ca[0], vb, full);
+					o[1] = mc_bi1(ca[1], vr, full);
+				}
+			}
+			first = false;
+		}
+	}
 }
 
 /* ---- deblocking (8.7.2; oracle/h265_oracle.c luma_edge / chroma_edge) */
@@ -765,6 +906,16 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		for (int c = 0; c < 2; ++c)
 			if (t.res[c] && (int64_t)t.coef[c] + n * n > (int64_t)pic->n_coef) return -1;
 	}
+	/* prediction blocks: inside the frame, 4..64 samples a side, references other frames of this context */
+	if (pic->n_pu < 0 || (pic->n_pu && !pic->pu)) return -1;
+	for (int i = 0; i < pic->n_pu; ++i) {
+		const h265r_pu_t &u = pic->pu[i];
+		if (u.w < 4 || u.h < 4 || u.w > 64 || u.h > 64 || (u.w & 3) || (u.h & 3) || (u.x & 3) || (u.y & 3) || u.x + u.w > g->W ||
+		    u.y + u.h > g->H || (u.ref[0] < 0 && u.ref[1] < 0))
+			return -1;
+		for (int l = 0; l < 2; ++l)
+			if (u.ref[l] >= g->n || (u.ref[l] >= 0 && u.ref[l] == pic->slot)) return -1;
+	}
 	H265_CHECK(hipSetDevice(g->dev));
 	const size_t units = (size_t)(g->W / 4) * (g->H / 4) + (size_t)(g->W / 8) * (g->H / 8);
 	const size_t nbs = (size_t)(g->H / 4) * (g->W / 8);
@@ -772,7 +923,8 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const size_t o_tu = 0, o_coef = al16(o_tu + sizeof(h265r_tu_t) * (size_t)pic->n_tu);
 	const size_t o_map = al16(o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
 	const size_t o_bsv = al16(o_map + sizeof(int32_t) * units), o_bsh = al16(o_bsv + nbs);
-	const size_t o_sao = al16(o_bsh + nbs), total = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
+	const size_t o_sao = al16(o_bsh + nbs), o_pu = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
+	const size_t total = al16(o_pu + sizeof(h265r_pu_t) * (size_t)pic->n_pu);
 	/* per-block done flags + 2 counters, then the CTU rows' progress words and the CTUs' first records */
 	const int nctu = cols * rows;
 	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + (size_t)nctu + 1;
@@ -799,6 +951,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	memcpy(a.host + o_bsv, pic->bs_v, nbs);
 	memcpy(a.host + o_bsh, pic->bs_h, nbs);
 	memcpy(a.host + o_sao, pic->sao, sizeof(h265r_sao_t) * (size_t)(cols * rows));
+	if (pic->n_pu) memcpy(a.host + o_pu, pic->pu, sizeof(h265r_pu_t) * (size_t)pic->n_pu);
 	H265Args h;
 	h.tu = (const h265r_tu_t *)(a.dev + o_tu);
 	h.coef = (const int16_t *)(a.dev + o_coef);
@@ -826,6 +979,10 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.tc_offset = pic->tc_offset;
 	h.cb_qp_offset = pic->cb_qp_offset;
 	h.cr_qp_offset = pic->cr_qp_offset;
+	h.pu = (const h265r_pu_t *)(a.dev + o_pu);
+	h.frames = g->frames;
+	h.fsz = g->fsz;
+	h.n_pu = pic->n_pu;
 	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, g->st));
 	g->record_bytes += (int64_t)total;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
@@ -833,6 +990,11 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipMemsetAsync(g->scratch, 0, sizeof(int) * sn, g->st));
 	const int k = (int)(g->pictures & 1);
 	H265_CHECK(hipEventRecord(g->t0[k], g->st));
+	if (pic->n_pu) {
+		const int grid = pic->n_pu < g->cus * 8 ? pic->n_pu : g->cus * 8;
+		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);
+		H265_CHECK(hipGetLastError());
+	}
 	if (pic->n_tu && g->block_kernel) {
 		const int grid = pic->n_tu < g->cus * 8 ? pic->n_tu : g->cus * 8;
 		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);

@@ -1,4 +1,4 @@
-"""H.265 intra pictures reconstructed on gfx950 (m2dec_amd/csrc/hip/h265_hip.hip) through h265d_func, bit-exact
+"""H.265 pictures (intra, and P / B with motion compensation) reconstructed on gfx950 (m2dec_amd/csrc/hip/h265_hip.hip) through h265d_func, bit-exact
 against the goldens the CPU oracle produced (tests/golden/h265.json, tests/test_h265_cpu.py).  Parity
 against the reference itself is unpinned (no reference-produced H.265 output exists here)."""
 import json

@@ -285,7 +285,6 @@ struct Sched {
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
-	hipEvent_t last_launch[NSTREAMS] = {}; /* recorded after the latest decode-path launch on each stream */
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
 	hipEvent_t slot_write[64] = {};
@@ -508,7 +507,6 @@ struct Sched {
 		}
 		*inter_done = next_event();
 		CHECK(hipEventRecord(*inter_done, s));
-		last_launch[k] = *inter_done;
 		if (tev) CHECK(hipEventRecord(tev[0], s));
 		return 0;
 	}
@@ -881,9 +879,6 @@ struct HipBackend {
 	int nheld = 0;
 	int limit = 1;        /* pictures per launch of this context (fixed at set_frames) */
 	int narenas = 2 * NSTREAMS; /* record arenas in use: NSTREAMS * limit + limit + 2 (fixed at set_frames) */
-	bool hold_busy = false; /* M2DEC_AMD_HOLD_BUSY=1: flush keeps held pictures while every stream is busy (r73
-	                         * A/B on c3, medians of 10 decodes, 3 rounds: 42.3 / 41.1 / 40.7 ms vs 49.1 / 41.8 /
-	                         * 39.9 without — no gain over the box's noise, so off) */
 	int max_held = BMAX; /* M2DEC_AMD_PICS_PER_LAUNCH; also bounded by the budget (Sched::pics_fit: 2 at
 	                      * 1080p and 4K) and 1 while other decode-path back ends are alive.  r67 A/B on c3,
 	                      * median of 10 decodes: 1 -> 45.1 ms, 2 -> 42.6, 3 -> 41.3, 4 -> 43.3 */
@@ -1055,20 +1050,14 @@ int be_submit(void *self, m2r_picture_t *pic)
 	return 0;
 }
 
-/* m2r_backend_t.flush, called by the decoder when a drive of its pipeline has nothing more to submit: while
- * every stream still runs a launch, the held pictures wait (1: call again later — the next drive, or a
- * bind, which launches them anyway), so that pictures parsed meanwhile join them in one launch; else
- * they are launched now */
+/* m2r_backend_t.flush, called by the decoder when a drive of its pipeline has nothing more to submit: the
+ * held pictures are launched now.  (A variant that kept them while every stream was busy, so that pictures
+ * parsed meanwhile would join the launch, measured no gain in r73 — 42.3 / 41.1 / 40.7 ms vs 49.1 / 41.8 /
+ * 39.9 ms, medians of 10 c3 decodes — and was removed.) */
 int be_flush(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
 	if (!b->nheld) return 0;
-	if (b->nheld < b->limit && b->hold_busy) {
-		int free_streams = 0;
-		for (int k = 0; k < nstreams(); ++k)
-			free_streams += !b->sc.last_launch[k] || hipEventQuery(b->sc.last_launch[k]) == hipSuccess;
-		if (!free_streams) return 1;
-	}
 	return launch_held(b) < 0 ? -1 : 0;
 }
 
@@ -1281,7 +1270,6 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->flush = be_flush;
 	out->ready = be_ready;
 	g_live_backends[device & 15]++;
-	if (const char *e = getenv("M2DEC_AMD_HOLD_BUSY")) b->hold_busy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
 		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));

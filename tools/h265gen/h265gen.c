@@ -61,6 +61,7 @@ static const cfg_t presets[] = {
 	{"cov_h265_hb", 232, 136, 4, 4, 1, 28, 1, -1, 0, 0, 1, 0, 1, 1, 1, 2, 2, 45, 20, 50, 3, 8, 2, 0, 0, 1, 3, 3, 25, 10, 40, 50, 55, 16},
 	{"cov_h265_ldb", 296, 168, 6, 5, 2, 32, 0, 0, 1, -1, 0, 1, 1, 1, 1, -2, 0, 40, 20, 45, 3, 8, 3, 1, 2, 1, 4, 4, 20, 8, 45, 40, 60, 40},
 	{"cov_h265_pnodbk", 168, 104, 4, 3, 1, 26, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 45, 20, 55, 3, 5, 1, 0, 1, 1, 2, 1, 15, 15, 50, 0, 65, 12},
+	{"c_h265_1080p_pb", 1920, 1080, 6, 5, 1, 30, 0, 0, 0, 0, 1, 1, 1, 1, 1, 0, 0, 35, 20, 50, 3, 8, 2, 1, 1, 1, 2, 5, 25, 5, 45, 40, 50, 32},
 	{NULL, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
 };
 

@@ -32,7 +32,7 @@ STREAMS = [("cov_h265_a_s1", "cov_h265_a", 1, 3), ("cov_h265_a_s2", "cov_h265_a"
            ("cov_h265_p_s1", "cov_h265_p", 1, 6), ("cov_h265_p_s2", "cov_h265_p", 2, 6),
            ("cov_h265_hb_s1", "cov_h265_hb", 1, 8), ("cov_h265_hb_s2", "cov_h265_hb", 2, 8),
            ("cov_h265_ldb_s1", "cov_h265_ldb", 1, 8), ("cov_h265_ldb_s2", "cov_h265_ldb", 2, 8),
-           ("cov_h265_pnodbk_s1", "cov_h265_pnodbk", 1, 5)]
+           ("cov_h265_pnodbk_s1", "cov_h265_pnodbk", 1, 5), ("c_h265_1080p_pb_s1", "c_h265_1080p_pb", 1, 8)]
 
 
 def gen(preset, seed, frames, dump=None):

@@ -285,6 +285,8 @@ struct Sched {
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
+	hipEvent_t busy[NSTREAMS] = {}; /* recorded behind each decode-path launch on the stream (its own event) */
+	bool busy_set[NSTREAMS] = {};
 	hipEvent_t ev[NEVENTS] = {};
 	int ev_next = 0;
 	hipEvent_t slot_write[64] = {};
@@ -297,7 +299,10 @@ struct Sched {
 		dev = device;
 		memset(&tm, 0, sizeof(tm));
 		CHECK(hipSetDevice(dev));
-		for (int k = 0; k < nstreams(); ++k) CHECK(g_pool.stream(dev, &st[k])); /* (the rest stay null) */
+		for (int k = 0; k < nstreams(); ++k) {
+			CHECK(g_pool.stream(dev, &st[k])); /* (the rest stay null) */
+			CHECK(g_pool.event(dev, false, &busy[k]));
+		}
 		CHECK(hipMalloc(&err, 16)); /* (the sync events are created on first use: next_event) */
 		CHECK(hipMemset(err, 0, 16));
 		memset(&slot_seq, 0, sizeof(slot_seq));
@@ -404,11 +409,37 @@ struct Sched {
 		return waits(k, slot, refs) < 0 ? -1 : k;
 	}
 
+	/* the stream of the next launch: the first idle one after the last pick, else round robin */
 	int pick()
 	{
-		const int k = rr;
-		rr = (rr + 1) % nstreams();
+		const int n = nstreams();
+		int k = rr;
+		for (int i = 0; i < n; ++i) {
+			const int c = (rr + i) % n;
+			if (idle(c)) {
+				k = c;
+				break;
+			}
+		}
+		rr = (k + 1) % n;
 		return k;
+	}
+
+	/* no decode-path launch of this context still runs on stream k */
+	bool idle(int k) { return !busy_set[k] || hipEventQuery(busy[k]) == hipSuccess; }
+
+	bool any_idle()
+	{
+		for (int k = 0; k < nstreams(); ++k)
+			if (idle(k)) return true;
+		return false;
+	}
+
+	int mark_busy(int k)
+	{
+		CHECK(hipEventRecord(busy[k], st[k]));
+		busy_set[k] = true;
+		return 0;
 	}
 
 	/* on stream k, before a picture writing `slot` (launched in a later call on k): the waits for the
@@ -709,6 +740,10 @@ struct Sched {
 			g_pool.put_event(dev, false, e);
 			e = nullptr;
 		}
+		for (auto &e : busy) {
+			if (e) g_pool.put_event(dev, false, e);
+			e = nullptr;
+		}
 		g_dev.give(dev, frames, fsz * (size_t)nslots);
 		if (prog) g_dev.give(dev, prog, prog_bytes());
 		if (hand) g_dev.give(dev, hand, hand_bytes() * NSTREAMS * BMAX);
@@ -879,6 +914,7 @@ struct HipBackend {
 	int nheld = 0;
 	int limit = 1;        /* pictures per launch of this context (fixed at set_frames) */
 	int narenas = 2 * NSTREAMS; /* record arenas in use: NSTREAMS * limit + limit + 2 (fixed at set_frames) */
+	bool hold = true;    /* flush holds pictures while every stream is busy (M2DEC_AMD_HOLD=0: never) */
 	int max_held = BMAX; /* M2DEC_AMD_PICS_PER_LAUNCH; also bounded by the budget (Sched::pics_fit: 2 at
 	                      * 1080p and 4K) and 1 while other decode-path back ends are alive.  r67 A/B on c3,
 	                      * median of 10 decodes: 1 -> 45.1 ms, 2 -> 42.6, 3 -> 41.3, 4 -> 43.3 */
@@ -1050,14 +1086,18 @@ int be_submit(void *self, m2r_picture_t *pic)
 	return 0;
 }
 
-/* m2r_backend_t.flush, called by the decoder when a drive of its pipeline has nothing more to submit: the
- * held pictures are launched now.  (A variant that kept them while every stream was busy, so that pictures
- * parsed meanwhile would join the launch, measured no gain in r73 — 42.3 / 41.1 / 40.7 ms vs 49.1 / 41.8 /
- * 39.9 ms, medians of 10 c3 decodes — and was removed.) */
+/* m2r_backend_t.flush, called by the decoder when a drive of its pipeline has nothing more to submit.
+ * While every stream of this context still runs a launch, held pictures wait (returns 1: the decoder asks
+ * again on its next drive — a parse finishing, an API call — and a bind of a held picture's buffer or a
+ * full hand launches them anyway), so that pictures submitted meanwhile join them in one launch: the
+ * decode path is latency-bound per launch (a 2-picture k_picture takes about as long as a 1-picture one,
+ * r83 timeline), so a fuller launch is throughput.  With an idle stream they are launched now.
+ * M2DEC_AMD_HOLD=0 launches at every flush (the r4 A/B baseline). */
 int be_flush(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
 	if (!b->nheld) return 0;
+	if (b->hold && b->nheld < b->limit && !b->sc.any_idle()) return 1;
 	return launch_held(b) < 0 ? -1 : 0;
 }
 
@@ -1096,6 +1136,7 @@ int launch_held(HipBackend *b)
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	hipEvent_t inter_done;
 	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
+	if (sc.mark_busy(k) < 0) return -1;
 	const size_t ls = (size_t)sc.W * sc.H;
 	for (int i = 0; i < n; ++i) {
 		HipBackend::Held &h = b->held[i];
@@ -1127,7 +1168,12 @@ int be_bind(void *self, int vid, int slot)
 {
 	HipBackend *b = (HipBackend *)self;
 	Sched &sc = b->sc;
-	if (launch_held(b) < 0) return -1; /* (the picture writing vid may be held) */
+	/* the picture writing vid may be held: then the held pictures go now (others keep waiting) */
+	for (int i = 0; i < b->nheld; ++i)
+		if (b->held[i].virt && b->held[i].j.slot == vid) {
+			if (launch_held(b) < 0) return -1;
+			break;
+		}
 	if (vid < 0 || vid >= sc.nslots || slot < 0 || slot >= b->nframes || !sc.slot_write[vid]) {
 		fprintf(stderr, "m2dec_amd: bind: picture buffer %d (written: %d) to frame %d rejected\n", vid,
 		        vid >= 0 && vid < 64 && sc.slot_write[vid] != nullptr, slot);
@@ -1270,6 +1316,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->flush = be_flush;
 	out->ready = be_ready;
 	g_live_backends[device & 15]++;
+	if (const char *e = getenv("M2DEC_AMD_HOLD")) b->hold = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
 		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-4 GPU checks on the box, each step under its own time limit, stopping at the first failure:
+#   h265    the H.265 GPU parity tests (I and P / B goldens) + the H.265 bench legs
+#   tl      host + rocprof timeline of one C3 decode (tools/timeline.sh)
+#   streams interleaved end-to-end A/B of the launch stream count (tools/ab_env.py)
+#   gpu     the whole GPU test suite
+# Usage: bash tools/gpu_round4.sh TAG STEP...
+set -o pipefail
+TAG=$1; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+for step in "$@"; do
+  case $step in
+  h265)
+    timeout -k 10 300 python -u -m pytest tests/test_gpu_h265.py -x -q --timeout 120 --timeout-method thread > gpurun_out/h265_tests_$TAG.log 2>&1 || { tail -30 gpurun_out/h265_tests_$TAG.log; exit 1; }
+    tail -1 gpurun_out/h265_tests_$TAG.log
+    timeout -k 10 300 python -u tools/h265_bench.py 3 > gpurun_out/h265_bench_$TAG.json 2> gpurun_out/h265_bench_$TAG.err || { tail -5 gpurun_out/h265_bench_$TAG.err; exit 1; }
+    cat gpurun_out/h265_bench_$TAG.json ;;
+  tl)
+    bash tools/timeline.sh $TAG 4 || exit 1 ;;
+  streams)
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "s3:" "s6q8:M2DEC_AMD_STREAMS=6,GPU_MAX_HW_QUEUES=8" "s7q8:M2DEC_AMD_STREAMS=7,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_streams_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_streams_$TAG.txt; exit 1; }
+    tail -6 gpurun_out/ab_streams_$TAG.txt ;;
+  hold)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py -k "c3_1080p or reflists or mmco5" > gpurun_out/pytest_hold_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_hold_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_hold_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "hold1:" "hold0:M2DEC_AMD_HOLD=0" "hold1s4:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=5" > gpurun_out/ab_hold_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_hold_$TAG.txt; exit 1; }
+    tail -4 gpurun_out/ab_hold_$TAG.txt ;;
+  gpu)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+    tail -2 gpurun_out/pytest_gpu_$TAG.log ;;
+  *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -26,6 +26,11 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_hold_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "hold1:" "hold0:M2DEC_AMD_HOLD=0" "hold1s4:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=5" > gpurun_out/ab_hold_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_hold_$TAG.txt; exit 1; }
     tail -4 gpurun_out/ab_hold_$TAG.txt ;;
+  crew)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py -k "c3_1080p or reflists" > gpurun_out/pytest_crew_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_crew_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_crew_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "crew3:" "crew0:M2DEC_AMD_COPY_CREW=0" "crew3hold0:M2DEC_AMD_HOLD=0" > gpurun_out/ab_crew_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_crew_$TAG.txt; exit 1; }
+    tail -4 gpurun_out/ab_crew_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -31,6 +31,10 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_crew_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "crew3:" "crew0:M2DEC_AMD_COPY_CREW=0" "crew3hold0:M2DEC_AMD_HOLD=0" > gpurun_out/ab_crew_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_crew_$TAG.txt; exit 1; }
     tail -4 gpurun_out/ab_crew_$TAG.txt ;;
+  md5)
+    lscpu | grep -E "Model name|Flags" | cut -c1-200 > gpurun_out/md5_batch_$TAG.txt
+    timeout -k 10 120 python3 tools/md5_batch_bench.py >> gpurun_out/md5_batch_$TAG.txt 2>&1 && M2DEC_AMD_MD5_LANES8=0 timeout -k 10 120 python3 tools/md5_batch_bench.py | sed 's/^/lanes16 /' >> gpurun_out/md5_batch_$TAG.txt 2>&1 || exit 1
+    cat gpurun_out/md5_batch_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

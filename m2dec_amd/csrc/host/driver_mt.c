@@ -29,8 +29,9 @@
                               this many (or MD5_WAIT_S after the oldest was queued, or the end) */
 #define MD5_WAIT_S 0.004
 #define MD5_THREADS_MAX 16
-#define MD5_THREADS 3      /* one stream: a 16-frame batch of 1080p takes one core ~4 ms; the third thread
-                              shortens the stream's tail (profiles/r59_knobs.txt); M2DEC_AMD_MD5_THREADS */
+#define MD5_THREADS 16     /* one stream: a 16-frame batch of 1080p takes one core ~6.5 ms on the box's EPYC
+                              9575F, one frame alone 3.3 ms (tools/md5_batch_bench.py, profiles/r85_md5_batch.txt);
+                              most threads only work in tail mode (below); M2DEC_AMD_MD5_THREADS */
 
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
  * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
@@ -61,6 +62,8 @@ typedef struct md5_pipe {
 	int stats;
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
+	int idle;                /* threads waiting for frames */
+	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
@@ -83,9 +86,16 @@ static void *md5_worker(void *arg)
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	pthread_mutex_lock(&p->mu);
 	for (;;) {
+		p->idle++;
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
+		p->idle--;
 		if (p->next == p->head) break;
-		while (!p->quit && p->ended == 0 && p->head - p->next < p->min_batch) {
+		/* tail mode: the parse pool has nothing in hand (a stream's last frames are coming out) and an idle
+		 * thread for every queued frame: hash one frame at once, alone — 3.3 ms instead of a batch's 6.5 ms
+		 * after the stream's last output.  While parsing runs, batches keep the MD5 CPU time small. */
+		const int tail = p->tail_mode && m2dec_parse_busy() == 0;
+		const int share = tail ? (p->head - p->next + p->idle) / (p->idle + 1) : MD5_BATCH; /* frames per thread */
+		while (!tail && !p->quit && p->ended == 0 && p->head - p->next < p->min_batch) {
 			const double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
 			struct timespec ts;
 			if (left <= 0) break;
@@ -99,7 +109,7 @@ static void *md5_worker(void *arg)
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];
 		int ks[MD5_BATCH], ix[MD5_BATCH], n = 0;
-		while (n < MD5_BATCH && p->next < p->head) {
+		while (n < share && n < MD5_BATCH && p->next < p->head) {
 			const int k = p->next % MD5_RING;
 			p->next++;
 			p->state[k] = 2;
@@ -184,6 +194,7 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	if (p->min_batch < 1) p->min_batch = 1;
 	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
+	p->tail_mode = getenv("M2DEC_AMD_MD5_TAIL") ? atoi(getenv("M2DEC_AMD_MD5_TAIL")) != 0 : 1;
 	p->streams = streams;
 	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)
 		if (pthread_create(&p->th[p->nth], NULL, md5_worker, p) != 0) break;

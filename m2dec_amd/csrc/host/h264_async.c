@@ -515,6 +515,11 @@ static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *s
 	return NULL;
 }
 
+/* pool workers inside a job or slice, all pipelines (m2dec_parse_busy: the MD5 pipe's tail mode) */
+static int g_parse_running;
+
+int m2dec_parse_busy(void) { return __atomic_load_n(&g_parse_running, __ATOMIC_RELAXED); }
+
 /* Pool workers take the oldest queued job whose dependencies have finished, so a B picture waiting
  * for its co-located P does not hold a worker while later P pictures could be parsed; pipelines are
  * served round robin.  A finished job may let its pipeline submit: the worker drives it. */
@@ -541,6 +546,7 @@ static void *pool_worker(void *arg)
 		}
 		g_parse.rr = as->pnext;
 		as->running++;
+		__atomic_fetch_add(&g_parse_running, 1, __ATOMIC_RELAXED);
 		pthread_mutex_unlock(&g_parse.mu);
 		if (pj) {
 			const double ts = now_s();
@@ -571,6 +577,7 @@ static void *pool_worker(void *arg)
 			pthread_cond_broadcast(&g_parse.cv_work); /* jobs waiting on this one may be ready */
 		}
 		as->running--;
+		__atomic_fetch_sub(&g_parse_running, 1, __ATOMIC_RELAXED);
 		pthread_cond_broadcast(&as->cv_done);
 		if (j) pipe_drive(as);
 	}
@@ -1408,10 +1415,12 @@ static int la_close(h264_dec_t *la)
 				la->colpic[c].mb = nb;
 				for (int k = 0; k < j->nsl; ++k) j->snap[k]->colpic[c].mb = nb;
 			} else {
+				m2d_tl('W', j->seq, (int)last);
 				pthread_mutex_lock(as->mu);
 				for (long i = as->tail; i < as->head && i <= last; ++i) /* (jobs seq = fifo index) */
 					while (i >= as->tail && !as->fifo[i % AS_MAX]->done) pthread_cond_wait(&as->cv_done, as->mu);
 				pthread_mutex_unlock(as->mu);
+				m2d_tl('w', j->seq, 0);
 			}
 			if (as->stats) as->t_col_wait += now_s() - tw;
 		}
@@ -1422,6 +1431,7 @@ static int la_close(h264_dec_t *la)
 	la->pic = NULL;
 	if (h264_picture_mark(la) < 0) return -1;
 	/* dispatch */
+	m2d_tl('Q', j->seq, (int)(as->seq - as->a_seq));
 	pthread_mutex_lock(as->mu);
 	as->fifo[as->head % AS_MAX] = j;
 	as->head++;

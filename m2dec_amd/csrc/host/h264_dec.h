@@ -406,6 +406,7 @@ int h264_async_add_slice(h264_dec_t *d);
 int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 int h264_async_pump_step(h264_dec_t *d);
+int m2dec_parse_busy(void); /* parse-pool workers inside a job right now (all pipelines) */
 void h264_async_stop(h264_dec_t *d);
 double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback);
 int h264_async_nal_next(h264_dec_t *d);

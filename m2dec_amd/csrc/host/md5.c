@@ -214,81 +214,6 @@ void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
 #define TH 0x96
 #define TI 0x39
 
-/* the 64 steps of one block, in order (RFC 1321 3.4) */
-#define MD5_ROUNDS(S) \
-	S(TF, a, b, c, d, 0, 0xd76aa478u, 7); \
-	S(TF, d, a, b, c, 1, 0xe8c7b756u, 12); \
-	S(TF, c, d, a, b, 2, 0x242070dbu, 17); \
-	S(TF, b, c, d, a, 3, 0xc1bdceeeu, 22); \
-	S(TF, a, b, c, d, 4, 0xf57c0fafu, 7); \
-	S(TF, d, a, b, c, 5, 0x4787c62au, 12); \
-	S(TF, c, d, a, b, 6, 0xa8304613u, 17); \
-	S(TF, b, c, d, a, 7, 0xfd469501u, 22); \
-	S(TF, a, b, c, d, 8, 0x698098d8u, 7); \
-	S(TF, d, a, b, c, 9, 0x8b44f7afu, 12); \
-	S(TF, c, d, a, b, 10, 0xffff5bb1u, 17); \
-	S(TF, b, c, d, a, 11, 0x895cd7beu, 22); \
-	S(TF, a, b, c, d, 12, 0x6b901122u, 7); \
-	S(TF, d, a, b, c, 13, 0xfd987193u, 12); \
-	S(TF, c, d, a, b, 14, 0xa679438eu, 17); \
-	S(TF, b, c, d, a, 15, 0x49b40821u, 22); \
-	S(TG, a, b, c, d, 1, 0xf61e2562u, 5); \
-	S(TG, d, a, b, c, 6, 0xc040b340u, 9); \
-	S(TG, c, d, a, b, 11, 0x265e5a51u, 14); \
-	S(TG, b, c, d, a, 0, 0xe9b6c7aau, 20); \
-	S(TG, a, b, c, d, 5, 0xd62f105du, 5); \
-	S(TG, d, a, b, c, 10, 0x02441453u, 9); \
-	S(TG, c, d, a, b, 15, 0xd8a1e681u, 14); \
-	S(TG, b, c, d, a, 4, 0xe7d3fbc8u, 20); \
-	S(TG, a, b, c, d, 9, 0x21e1cde6u, 5); \
-	S(TG, d, a, b, c, 14, 0xc33707d6u, 9); \
-	S(TG, c, d, a, b, 3, 0xf4d50d87u, 14); \
-	S(TG, b, c, d, a, 8, 0x455a14edu, 20); \
-	S(TG, a, b, c, d, 13, 0xa9e3e905u, 5); \
-	S(TG, d, a, b, c, 2, 0xfcefa3f8u, 9); \
-	S(TG, c, d, a, b, 7, 0x676f02d9u, 14); \
-	S(TG, b, c, d, a, 12, 0x8d2a4c8au, 20); \
-	S(TH, a, b, c, d, 5, 0xfffa3942u, 4); \
-	S(TH, d, a, b, c, 8, 0x8771f681u, 11); \
-	S(TH, c, d, a, b, 11, 0x6d9d6122u, 16); \
-	S(TH, b, c, d, a, 14, 0xfde5380cu, 23); \
-	S(TH, a, b, c, d, 1, 0xa4beea44u, 4); \
-	S(TH, d, a, b, c, 4, 0x4bdecfa9u, 11); \
-	S(TH, c, d, a, b, 7, 0xf6bb4b60u, 16); \
-	S(TH, b, c, d, a, 10, 0xbebfbc70u, 23); \
-	S(TH, a, b, c, d, 13, 0x289b7ec6u, 4); \
-	S(TH, d, a, b, c, 0, 0xeaa127fau, 11); \
-	S(TH, c, d, a, b, 3, 0xd4ef3085u, 16); \
-	S(TH, b, c, d, a, 6, 0x04881d05u, 23); \
-	S(TH, a, b, c, d, 9, 0xd9d4d039u, 4); \
-	S(TH, d, a, b, c, 12, 0xe6db99e5u, 11); \
-	S(TH, c, d, a, b, 15, 0x1fa27cf8u, 16); \
-	S(TH, b, c, d, a, 2, 0xc4ac5665u, 23); \
-	S(TI, a, b, c, d, 0, 0xf4292244u, 6); \
-	S(TI, d, a, b, c, 7, 0x432aff97u, 10); \
-	S(TI, c, d, a, b, 14, 0xab9423a7u, 15); \
-	S(TI, b, c, d, a, 5, 0xfc93a039u, 21); \
-	S(TI, a, b, c, d, 12, 0x655b59c3u, 6); \
-	S(TI, d, a, b, c, 3, 0x8f0ccc92u, 10); \
-	S(TI, c, d, a, b, 10, 0xffeff47du, 15); \
-	S(TI, b, c, d, a, 1, 0x85845dd1u, 21); \
-	S(TI, a, b, c, d, 8, 0x6fa87e4fu, 6); \
-	S(TI, d, a, b, c, 15, 0xfe2ce6e0u, 10); \
-	S(TI, c, d, a, b, 6, 0xa3014314u, 15); \
-	S(TI, b, c, d, a, 13, 0x4e0811a1u, 21); \
-	S(TI, a, b, c, d, 4, 0xf7537e82u, 6); \
-	S(TI, d, a, b, c, 11, 0xbd3af235u, 10); \
-	S(TI, c, d, a, b, 2, 0x2ad7d2bbu, 15); \
-	S(TI, b, c, d, a, 9, 0xeb86d391u, 21);
-
-/* the 8-lane form (AVX-512VL on 256-bit registers) */
-#define VSTEP8(imm, a, b, c, d, wi, k, s) \
-	do { \
-		a = _mm256_add_epi32(a, _mm256_add_epi32(w[wi], _mm256_set1_epi32((int)(k)))); \
-		a = _mm256_add_epi32(a, _mm256_ternarylogic_epi32(b, c, d, imm)); \
-		a = _mm256_add_epi32(_mm256_rol_epi32(a, s), b); \
-	} while (0)
-
 /* 16 rows of 16 dwords -> 16 columns (r[i] lane l = row l word i) */
 __attribute__((target("avx512f"))) static inline void transpose16(__m512i r[16])
 {
@@ -326,7 +251,70 @@ __attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16],
 		__m512i a = va, b = vb, c = vc, d = vd;
 		for (int l = 0; l < 16; ++l) w[l] = _mm512_loadu_si512(lp[l] + 64 * n);
 		transpose16(w);
-		MD5_ROUNDS(VSTEP)
+		VSTEP(TF, a, b, c, d, 0, 0xd76aa478u, 7);
+		VSTEP(TF, d, a, b, c, 1, 0xe8c7b756u, 12);
+		VSTEP(TF, c, d, a, b, 2, 0x242070dbu, 17);
+		VSTEP(TF, b, c, d, a, 3, 0xc1bdceeeu, 22);
+		VSTEP(TF, a, b, c, d, 4, 0xf57c0fafu, 7);
+		VSTEP(TF, d, a, b, c, 5, 0x4787c62au, 12);
+		VSTEP(TF, c, d, a, b, 6, 0xa8304613u, 17);
+		VSTEP(TF, b, c, d, a, 7, 0xfd469501u, 22);
+		VSTEP(TF, a, b, c, d, 8, 0x698098d8u, 7);
+		VSTEP(TF, d, a, b, c, 9, 0x8b44f7afu, 12);
+		VSTEP(TF, c, d, a, b, 10, 0xffff5bb1u, 17);
+		VSTEP(TF, b, c, d, a, 11, 0x895cd7beu, 22);
+		VSTEP(TF, a, b, c, d, 12, 0x6b901122u, 7);
+		VSTEP(TF, d, a, b, c, 13, 0xfd987193u, 12);
+		VSTEP(TF, c, d, a, b, 14, 0xa679438eu, 17);
+		VSTEP(TF, b, c, d, a, 15, 0x49b40821u, 22);
+		VSTEP(TG, a, b, c, d, 1, 0xf61e2562u, 5);
+		VSTEP(TG, d, a, b, c, 6, 0xc040b340u, 9);
+		VSTEP(TG, c, d, a, b, 11, 0x265e5a51u, 14);
+		VSTEP(TG, b, c, d, a, 0, 0xe9b6c7aau, 20);
+		VSTEP(TG, a, b, c, d, 5, 0xd62f105du, 5);
+		VSTEP(TG, d, a, b, c, 10, 0x02441453u, 9);
+		VSTEP(TG, c, d, a, b, 15, 0xd8a1e681u, 14);
+		VSTEP(TG, b, c, d, a, 4, 0xe7d3fbc8u, 20);
+		VSTEP(TG, a, b, c, d, 9, 0x21e1cde6u, 5);
+		VSTEP(TG, d, a, b, c, 14, 0xc33707d6u, 9);
+		VSTEP(TG, c, d, a, b, 3, 0xf4d50d87u, 14);
+		VSTEP(TG, b, c, d, a, 8, 0x455a14edu, 20);
+		VSTEP(TG, a, b, c, d, 13, 0xa9e3e905u, 5);
+		VSTEP(TG, d, a, b, c, 2, 0xfcefa3f8u, 9);
+		VSTEP(TG, c, d, a, b, 7, 0x676f02d9u, 14);
+		VSTEP(TG, b, c, d, a, 12, 0x8d2a4c8au, 20);
+		VSTEP(TH, a, b, c, d, 5, 0xfffa3942u, 4);
+		VSTEP(TH, d, a, b, c, 8, 0x8771f681u, 11);
+		VSTEP(TH, c, d, a, b, 11, 0x6d9d6122u, 16);
+		VSTEP(TH, b, c, d, a, 14, 0xfde5380cu, 23);
+		VSTEP(TH, a, b, c, d, 1, 0xa4beea44u, 4);
+		VSTEP(TH, d, a, b, c, 4, 0x4bdecfa9u, 11);
+		VSTEP(TH, c, d, a, b, 7, 0xf6bb4b60u, 16);
+		VSTEP(TH, b, c, d, a, 10, 0xbebfbc70u, 23);
+		VSTEP(TH, a, b, c, d, 13, 0x289b7ec6u, 4);
+		VSTEP(TH, d, a, b, c, 0, 0xeaa127fau, 11);
+		VSTEP(TH, c, d, a, b, 3, 0xd4ef3085u, 16);
+		VSTEP(TH, b, c, d, a, 6, 0x04881d05u, 23);
+		VSTEP(TH, a, b, c, d, 9, 0xd9d4d039u, 4);
+		VSTEP(TH, d, a, b, c, 12, 0xe6db99e5u, 11);
+		VSTEP(TH, c, d, a, b, 15, 0x1fa27cf8u, 16);
+		VSTEP(TH, b, c, d, a, 2, 0xc4ac5665u, 23);
+		VSTEP(TI, a, b, c, d, 0, 0xf4292244u, 6);
+		VSTEP(TI, d, a, b, c, 7, 0x432aff97u, 10);
+		VSTEP(TI, c, d, a, b, 14, 0xab9423a7u, 15);
+		VSTEP(TI, b, c, d, a, 5, 0xfc93a039u, 21);
+		VSTEP(TI, a, b, c, d, 12, 0x655b59c3u, 6);
+		VSTEP(TI, d, a, b, c, 3, 0x8f0ccc92u, 10);
+		VSTEP(TI, c, d, a, b, 10, 0xffeff47du, 15);
+		VSTEP(TI, b, c, d, a, 1, 0x85845dd1u, 21);
+		VSTEP(TI, a, b, c, d, 8, 0x6fa87e4fu, 6);
+		VSTEP(TI, d, a, b, c, 15, 0xfe2ce6e0u, 10);
+		VSTEP(TI, c, d, a, b, 6, 0xa3014314u, 15);
+		VSTEP(TI, b, c, d, a, 13, 0x4e0811a1u, 21);
+		VSTEP(TI, a, b, c, d, 4, 0xf7537e82u, 6);
+		VSTEP(TI, d, a, b, c, 11, 0xbd3af235u, 10);
+		VSTEP(TI, c, d, a, b, 2, 0x2ad7d2bbu, 15);
+		VSTEP(TI, b, c, d, a, 9, 0xeb86d391u, 21);
 		va = _mm512_add_epi32(va, a);
 		vb = _mm512_add_epi32(vb, b);
 		vc = _mm512_add_epi32(vc, c);
@@ -336,64 +324,6 @@ __attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16],
 	_mm512_storeu_si512(st[1], vb);
 	_mm512_storeu_si512(st[2], vc);
 	_mm512_storeu_si512(st[3], vd);
-}
-
-/* 8 rows of 8 dwords -> 8 columns */
-__attribute__((target("avx512f,avx512vl"))) static inline void transpose8(__m256i r[8])
-{
-	__m256i t[8], u[8];
-	for (int i = 0; i < 4; ++i) {
-		t[2 * i] = _mm256_unpacklo_epi32(r[2 * i], r[2 * i + 1]);
-		t[2 * i + 1] = _mm256_unpackhi_epi32(r[2 * i], r[2 * i + 1]);
-	}
-	for (int h = 0; h < 2; ++h) {
-		u[4 * h + 0] = _mm256_unpacklo_epi64(t[4 * h], t[4 * h + 2]);
-		u[4 * h + 1] = _mm256_unpackhi_epi64(t[4 * h], t[4 * h + 2]);
-		u[4 * h + 2] = _mm256_unpacklo_epi64(t[4 * h + 1], t[4 * h + 3]);
-		u[4 * h + 3] = _mm256_unpackhi_epi64(t[4 * h + 1], t[4 * h + 3]);
-	}
-	for (int i = 0; i < 4; ++i) {
-		r[i] = _mm256_permute2x128_si256(u[i], u[4 + i], 0x20);
-		r[4 + i] = _mm256_permute2x128_si256(u[i], u[4 + i], 0x31);
-	}
-}
-
-/* md5x16_blocks on 8 lanes: a batch of at most 8 frames takes about half the 16-lane time on hosts that
- * run 512-bit operations as two 256-bit halves: the latency of a stream's last frames */
-__attribute__((target("avx512f,avx512vl"))) static void md5x8_blocks(uint32_t st[4][16], const uint8_t *const lp[16], size_t nblocks)
-{
-	__m256i va = _mm256_loadu_si256((const __m256i *)st[0]), vb = _mm256_loadu_si256((const __m256i *)st[1]);
-	__m256i vc = _mm256_loadu_si256((const __m256i *)st[2]), vd = _mm256_loadu_si256((const __m256i *)st[3]);
-	for (size_t n = 0; n < nblocks; ++n) {
-		__m256i w[16];
-		__m256i a = va, b = vb, c = vc, d = vd;
-		for (int l = 0; l < 8; ++l) {
-			w[l] = _mm256_loadu_si256((const __m256i *)(lp[l] + 64 * n));
-			w[8 + l] = _mm256_loadu_si256((const __m256i *)(lp[l] + 64 * n + 32));
-		}
-		transpose8(w);
-		transpose8(w + 8);
-		MD5_ROUNDS(VSTEP8)
-		va = _mm256_add_epi32(va, a);
-		vb = _mm256_add_epi32(vb, b);
-		vc = _mm256_add_epi32(vc, c);
-		vd = _mm256_add_epi32(vd, d);
-	}
-	_mm256_storeu_si256((__m256i *)st[0], va);
-	_mm256_storeu_si256((__m256i *)st[1], vb);
-	_mm256_storeu_si256((__m256i *)st[2], vc);
-	_mm256_storeu_si256((__m256i *)st[3], vd);
-}
-
-static int have_avx512vl(void)
-{
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("M2DEC_AMD_MD5_LANES8"); /* 0: batches of <= 8 frames on 16 lanes too */
-		__builtin_cpu_init();
-		v = __builtin_cpu_supports("avx512vl") && !(e && !atoi(e));
-	}
-	return v;
 }
 
 static int have_avx512(void)
@@ -432,13 +362,8 @@ int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
 			pb[l] = g->chroma + (size_t)stride * (f[0].crop[2] >> 1);
 			for (int k = 0; k < 4; ++k) st[k][l] = iv[k];
 		}
-		if (n <= 8 && have_avx512vl()) {
-			md5x8_blocks(st, pa, na);
-			md5x8_blocks(st, pb, nb);
-		} else {
-			md5x16_blocks(st, pa, na);
-			md5x16_blocks(st, pb, nb);
-		}
+		md5x16_blocks(st, pa, na);
+		md5x16_blocks(st, pb, nb);
 		for (int l = 0; l < n; ++l) {
 			md5_t m;
 			uint8_t dg[16];

@@ -35,6 +35,11 @@ for step in "$@"; do
     lscpu | grep -E "Model name|Flags" | cut -c1-200 > gpurun_out/md5_batch_$TAG.txt
     timeout -k 10 120 python3 tools/md5_batch_bench.py >> gpurun_out/md5_batch_$TAG.txt 2>&1 && M2DEC_AMD_MD5_LANES8=0 timeout -k 10 120 python3 tools/md5_batch_bench.py | sed 's/^/lanes16 /' >> gpurun_out/md5_batch_$TAG.txt 2>&1 || exit 1
     cat gpurun_out/md5_batch_$TAG.txt ;;
+  tail)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py -k "c3_1080p or md5 or reflists" > gpurun_out/pytest_tail_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_tail_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_tail_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "tail1:" "tail0:M2DEC_AMD_MD5_TAIL=0,M2DEC_AMD_MD5_THREADS=3" "tail1t8:M2DEC_AMD_MD5_THREADS=8" > gpurun_out/ab_tail_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_tail_$TAG.txt; exit 1; }
+    tail -4 gpurun_out/ab_tail_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -38,10 +38,19 @@ for t, k, a, b in win:
         sub[a] = [ms(t), None]
     elif k == "s" and a in sub:
         sub[a][1] = ms(t)
-print("\njob  type  parse start..end    submit")
+disp = {a: (ms(t), b) for t, k, a, b in win if k == "Q"}
+colw, cw0 = [], {}
+for t, k, a, b in win:
+    if k == "W":
+        cw0[a] = (ms(t), b)
+    elif k == "w" and a in cw0:
+        colw.append((a, cw0[a][0], ms(t) - cw0[a][0], cw0[a][1]))
+print("\njob  type  dispatch (ahead)  parse start..end    submit")
 for s in sorted(parse):
     p = parse[s]
-    print(f"{s:4d}  {p[2]:4d}  {p[0]:7.2f} .. {p[1] if p[1] else -1:7.2f}   {sub.get(s, [-1])[0]:7.2f}")
+    dq = disp.get(s, (-1, -1))
+    print(f"{s:4d}  {p[2]:4d}  {dq[0]:7.2f} ({dq[1]:3d})   {p[0]:7.2f} .. {p[1] if p[1] else -1:7.2f}   {sub.get(s, [-1])[0]:7.2f}")
+print("lookahead col-store waits (job, start, ms, until job):", [(a, round(t, 2), round(w, 2), u) for a, t, w, u in colw])
 
 launch = [(ms(t), a, b) for t, k, a, b in win if k == "L"]
 kp = sorted([r for r in kern if r["Kernel_Name"].startswith("k_picture")], key=lambda r: int(r["Start_Timestamp"]))

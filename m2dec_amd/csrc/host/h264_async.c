@@ -488,6 +488,8 @@ static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err
 	return 1;
 }
 
+static int g_parse_prio = 1; /* M2DEC_AMD_PARSE_PRIO (read when the pool starts) */
+
 /* A ready job (or a slice to help with) of pipeline `as`, marked taken; NULL if none.  Mutex held. */
 static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *slice_k, int *dep_err)
 {
@@ -503,15 +505,20 @@ static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *s
 	/* a taken job leaves the queue at once (its entry is cleared): once finished and retired it is
 	 * recycled for a later picture, and a stale entry would hand that one out half built */
 	while (as->qtail < as->qhead && !as->queue[as->qtail % AS_MAX]) as->qtail++;
-	for (long k = as->qtail; k < as->qhead; ++k) {
-		h264_job_t *c = as->queue[k % AS_MAX];
-		*dep_err = 0;
-		if (c && deps_ready(as, c, dep_err)) {
-			c->taken = 1;
-			as->queue[k % AS_MAX] = NULL;
-			return c;
+	/* reference pictures first (the oldest ready one), then any: the pictures later B pictures wait for
+	 * are parsed as early as they can be, instead of behind every older B picture whose anchor is done —
+	 * which left the stream's last anchors to start ~10 ms late and the last B pictures after them
+	 * (profiles/r86_timeline.txt); M2DEC_AMD_PARSE_PRIO=0: oldest ready job only */
+	for (int pass = g_parse_prio ? 0 : 1; pass < 2; ++pass)
+		for (long k = as->qtail; k < as->qhead; ++k) {
+			h264_job_t *c = as->queue[k % AS_MAX];
+			*dep_err = 0;
+			if (c && (pass || !c->nonref) && deps_ready(as, c, dep_err)) {
+				c->taken = 1;
+				as->queue[k % AS_MAX] = NULL;
+				return c;
+			}
 		}
-	}
 	return NULL;
 }
 
@@ -609,7 +616,11 @@ static void pool_atexit(void)
 static int pool_grow(int n)
 {
 	if (n > POOL_MAX) n = POOL_MAX;
-	if (g_parse.nth == 0 && n > 0) atexit(pool_atexit);
+	if (g_parse.nth == 0 && n > 0) {
+		const char *e = getenv("M2DEC_AMD_PARSE_PRIO");
+		if (e) g_parse_prio = atoi(e) != 0;
+		atexit(pool_atexit);
+	}
 	while (g_parse.nth < n) {
 		pthread_attr_t at;
 		pthread_attr_init(&at);

@@ -40,6 +40,11 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_tail_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "tail1:" "tail0:M2DEC_AMD_MD5_TAIL=0,M2DEC_AMD_MD5_THREADS=3" "tail1t8:M2DEC_AMD_MD5_THREADS=8" > gpurun_out/ab_tail_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_tail_$TAG.txt; exit 1; }
     tail -4 gpurun_out/ab_tail_$TAG.txt ;;
+  prio)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py -k "c3_1080p or reflists or mmco5 or poc" > gpurun_out/pytest_prio_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_prio_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_prio_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "prio1:" "prio0:M2DEC_AMD_PARSE_PRIO=0" > gpurun_out/ab_prio_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_prio_$TAG.txt; exit 1; }
+    tail -3 gpurun_out/ab_prio_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

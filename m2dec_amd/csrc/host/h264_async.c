@@ -941,7 +941,9 @@ static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 	const m2r_picture_t *src = &j->pic;
 	const int n = src->width_mbs * src->height_mbs;
 	double t1 = as->stats ? now_s() : 0;
+	m2d_tl('A', j->seq, 0);
 	m2r_picture_t *dst = d->backend.acquire(d->backend.self, src->width_mbs, src->height_mbs);
+	m2d_tl('a', j->seq, 0);
 	if (!dst || dst->cap_slices < src->n_slices || dst->cap_inter < src->n_inter || dst->cap_coef < src->n_coef) return 1;
 	dst->slot = virt ? (j->vid & 63) : j->slot;
 	dst->flags = virt ? M2R_PIC_VIRTUAL : 0;
@@ -977,6 +979,7 @@ static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 		as->t_copy += t2 - t1;
 		t1 = t2;
 	}
+	m2d_tl('C', j->seq, 0);
 	int err = d->backend.submit(d->backend.self, dst) < 0;
 	if (!err && !virt && d->backend.flush) err = d->backend.flush(d->backend.self) < 0; /* (in API order: one at a time) */
 	if (as->stats) as->t_submit += now_s() - t1;

@@ -52,6 +52,19 @@ for s in sorted(parse):
     print(f"{s:4d}  {p[2]:4d}  {dq[0]:7.2f} ({dq[1]:3d})   {p[0]:7.2f} .. {p[1] if p[1] else -1:7.2f}   {sub.get(s, [-1])[0]:7.2f}")
 print("lookahead col-store waits (job, start, ms, until job):", [(a, round(t, 2), round(w, 2), u) for a, t, w, u in colw])
 
+# the serial submission of one picture: acquire (A..a), record copy (a..C), back-end submit (C..s)
+acq, cpy, smt = [], [], []
+st = {}
+for t, k, a, b in win:
+    if k in "AaC":
+        st[(k, a)] = ms(t)
+    elif k == "s" and ("A", a) in st and ("a", a) in st and ("C", a) in st:
+        acq.append(st[("a", a)] - st[("A", a)])
+        cpy.append(st[("C", a)] - st[("a", a)])
+        smt.append(ms(t) - st[("C", a)])
+if acq:
+    print(f"submission per picture (mean ms): acquire {sum(acq) / len(acq):.3f}  copy {sum(cpy) / len(cpy):.3f}  "
+          f"submit {sum(smt) / len(smt):.3f}  (max acquire {max(acq):.3f}, max submit {max(smt):.3f})")
 launch = [(ms(t), a, b) for t, k, a, b in win if k == "L"]
 kp = sorted([r for r in kern if r["Kernel_Name"].startswith("k_picture")], key=lambda r: int(r["Start_Timestamp"]))
 print(f"\n{len(launch)} launches (host), {len(kp)} k_picture kernels")

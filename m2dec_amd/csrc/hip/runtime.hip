@@ -32,6 +32,9 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
 extern "C" void m2d_tl(int kind, long a, long b); /* timeline.c (M2DEC_AMD_TIMELINE diagnostics) */
+/* parcopy.c: a large host copy spread over a thread crew (h264_dec.h; declared here, C linkage) */
+extern "C" void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
+enum { M2DEC_CREW_SYNC_ = 1 }; /* = M2DEC_CREW_SYNC (h264_dec.h) */
 
 namespace {
 
@@ -1134,9 +1137,11 @@ int launch_held(HipBackend *b)
 		if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
 	}
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
+	m2d_tl('M', n, k);
 	hipEvent_t inter_done;
 	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
 	if (sc.mark_busy(k) < 0) return -1;
+	m2d_tl('N', n, k);
 	const size_t ls = (size_t)sc.W * sc.H;
 	for (int i = 0; i < n; ++i) {
 		HipBackend::Held &h = b->held[i];
@@ -1158,6 +1163,7 @@ int launch_held(HipBackend *b)
 		sc.tm.ref_bytes += h.ref_bytes;
 		sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
 	}
+	m2d_tl('l', n, k);
 	return 0;
 }
 
@@ -1211,8 +1217,12 @@ int be_sync(void *self, int slot)
 		const double t0 = wall_s();
 		const m2d_frame_t &f = b->frames[slot];
 		const size_t ls = b->stg_size / 3 * 2;
-		memcpy(f.luma, b->stg[slot], ls);
-		memcpy(f.chroma, b->stg[slot] + ls, ls / 2);
+		{ /* (on the API thread, once per output frame: spread over the sync copy crew, parcopy.c) */
+			void *const to[2] = {f.luma, f.chroma};
+			const void *const from[2] = {b->stg[slot], b->stg[slot] + ls};
+			const size_t len[2] = {ls, ls / 2};
+			m2dec_par_memcpy(M2DEC_CREW_SYNC_, 2, to, from, len);
+		}
 		b->sc.tm.host_copy_us += (wall_s() - t0) * 1e6;
 		stage_drop(b, slot);
 	}

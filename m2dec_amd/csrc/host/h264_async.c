@@ -830,111 +830,6 @@ static void job_put(struct h264_async *as, h264_job_t *j)
  * sync_frame. */
 
 /* records into the back end's arena (virtual ids as they are, or translated to slots) + submit */
-/* ---- the record copy into the back end's arena, spread over a small process-wide crew of threads.  The
- * submitting thread is the decode path's one serial stage (submissions go in decoding order), and the
- * copy of a 1080p picture's records (~4.5 MB) on one core was ~0.25 ms of its ~0.3 ms per picture
- * (r84 timeline): the submission rate, not the GPU, bounded the pictures in flight.  Copies of at least
- * PAR_MIN bytes are cut into pieces the crew and the caller take from a shared counter. */
-#define PAR_CREW 3
-#define PAR_MIN (512 << 10)
-#define PAR_PIECE (256 << 10)
-typedef struct {
-	pthread_mutex_t mu;
-	pthread_cond_t cv_go, cv_done;
-	uint8_t *dst[4];
-	const uint8_t *src[4];
-	size_t len[4], off[5];  /* the copies of one call, and their start offsets in the joint range */
-	int ncopies;
-	size_t total;
-	long gen;               /* a new call */
-	int busy;               /* crew members still in the current call */
-	size_t next;            /* next piece's offset (atomic) */
-	int started;
-} par_crew_t;
-static par_crew_t g_crew;
-static pthread_once_t g_crew_once = PTHREAD_ONCE_INIT;
-
-static void par_pieces(par_crew_t *c)
-{
-	for (;;) {
-		const size_t o = __atomic_fetch_add(&c->next, (size_t)PAR_PIECE, __ATOMIC_RELAXED);
-		if (o >= c->total) return;
-		size_t end = o + PAR_PIECE < c->total ? o + PAR_PIECE : c->total;
-		for (int k = 0; k < c->ncopies; ++k) { /* the piece may span the end of one copy and the start of the next */
-			const size_t a = o > c->off[k] ? o : c->off[k], b = end < c->off[k + 1] ? end : c->off[k + 1];
-			if (a < b) memcpy(c->dst[k] + (a - c->off[k]), c->src[k] + (a - c->off[k]), b - a);
-		}
-	}
-}
-
-static void *par_crew_main(void *arg)
-{
-	par_crew_t *c = (par_crew_t *)arg;
-	long seen = 0;
-	pthread_setname_np(pthread_self(), "m2d-copy");
-	pthread_mutex_lock(&c->mu);
-	for (;;) {
-		while (c->gen == seen) pthread_cond_wait(&c->cv_go, &c->mu);
-		seen = c->gen;
-		pthread_mutex_unlock(&c->mu);
-		par_pieces(c);
-		pthread_mutex_lock(&c->mu);
-		if (--c->busy == 0) pthread_cond_signal(&c->cv_done);
-	}
-	return NULL;
-}
-
-static void par_crew_start(void)
-{
-	const char *e = getenv("M2DEC_AMD_COPY_CREW"); /* threads helping the record copy (0: none) */
-	const int n = e ? atoi(e) : PAR_CREW;
-	pthread_mutex_init(&g_crew.mu, NULL);
-	pthread_cond_init(&g_crew.cv_go, NULL);
-	pthread_cond_init(&g_crew.cv_done, NULL);
-	for (int i = 0; i < n && i < 8; ++i) {
-		pthread_t t;
-		if (pthread_create(&t, NULL, par_crew_main, &g_crew) != 0) break;
-		pthread_detach(t);
-		g_crew.started++;
-	}
-}
-
-/* copies k = 0..n-1 (n <= 4) of len[k] bytes; one caller at a time (the submitting thread of a context;
- * concurrent contexts serialise on the crew's mutex) */
-static void par_memcpy(int n, void *const *dst, const void *const *src, const size_t *len)
-{
-	static pthread_mutex_t one = PTHREAD_MUTEX_INITIALIZER;
-	size_t total = 0;
-	for (int k = 0; k < n; ++k) total += len[k];
-	pthread_once(&g_crew_once, par_crew_start);
-	if (total < PAR_MIN || !g_crew.started || pthread_mutex_trylock(&one) != 0) {
-		for (int k = 0; k < n; ++k)
-			if (len[k]) memcpy(dst[k], src[k], len[k]);
-		return;
-	}
-	par_crew_t *c = &g_crew;
-	pthread_mutex_lock(&c->mu);
-	c->ncopies = n;
-	c->off[0] = 0;
-	for (int k = 0; k < n; ++k) {
-		c->dst[k] = (uint8_t *)dst[k];
-		c->src[k] = (const uint8_t *)src[k];
-		c->len[k] = len[k];
-		c->off[k + 1] = c->off[k] + len[k];
-	}
-	c->total = total;
-	c->next = 0;
-	c->busy = c->started;
-	c->gen++;
-	pthread_cond_broadcast(&c->cv_go);
-	pthread_mutex_unlock(&c->mu);
-	par_pieces(c);
-	pthread_mutex_lock(&c->mu);
-	while (c->busy) pthread_cond_wait(&c->cv_done, &c->mu);
-	pthread_mutex_unlock(&c->mu);
-	pthread_mutex_unlock(&one);
-}
-
 static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 {
 	struct h264_async *as = d->as;
@@ -958,7 +853,7 @@ static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 		const void *const from[4] = {src->mb, src->dbk, src->inter, src->coef};
 		const size_t len[4] = {sizeof(m2r_mb_t) * (size_t)n, sizeof(m2r_deblock_t) * (size_t)n,
 		                       sizeof(m2r_inter_t) * (size_t)src->n_inter, sizeof(int16_t) * (size_t)src->n_coef};
-		par_memcpy(4, to, from, len);
+		m2dec_par_memcpy(M2DEC_CREW_SUBMIT, 4, to, from, len);
 	} else {
 		memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
 		memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);

@@ -407,6 +407,9 @@ int h264_async_close(h264_dec_t *d);
 int h264_async_drain(h264_dec_t *d, int slot);
 int h264_async_pump_step(h264_dec_t *d);
 int m2dec_parse_busy(void); /* parse-pool workers inside a job right now (all pipelines) */
+/* parcopy.c: a large copy (up to 4 pieces) spread over a process-wide thread crew */
+enum { M2DEC_CREW_SUBMIT, M2DEC_CREW_SYNC, M2DEC_CREWS };
+void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
 void h264_async_stop(h264_dec_t *d);
 double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback);
 int h264_async_nal_next(h264_dec_t *d);

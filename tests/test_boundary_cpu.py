@@ -91,11 +91,11 @@ def test_dropped_contexts_are_reclaimed(built, tmp_path):
     s = gen(tmp_path, "resize")
     f1 = golden_md5s(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"))
     # (the parse pool is sized for the host share, M2DEC_AMD_POOL_THREADS; 4 here to bound the count; the
-    # record-copy crew, M2DEC_AMD_COPY_CREW, 3 threads, is process-wide too)
+    # copy crews, M2DEC_AMD_COPY_CREW, 2 x 3 threads, are process-wide too)
     lines, md5 = harness(["-t", "4", "-n", "10", "-m", "7", F1, s], env={"M2DEC_AMD_POOL_THREADS": "4"})
     st = iters(lines)
     assert len(st) == 10
-    assert len({x["threads"] for x in st}) == 1 and st[0]["threads"] <= 1 + 4 + 3
+    assert len({x["threads"] for x in st}) == 1 and st[0]["threads"] <= 1 + 4 + 6
     assert max(x["contexts"] for x in st) <= 2
     assert md5[:7] == f1[:7]
     lines, md5 = harness(["-t", "4", "-n", "10", F1])

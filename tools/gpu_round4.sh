@@ -45,6 +45,11 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_prio_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "prio1:" "prio0:M2DEC_AMD_PARSE_PRIO=0" > gpurun_out/ab_prio_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_prio_$TAG.txt; exit 1; }
     tail -3 gpurun_out/ab_prio_$TAG.txt ;;
+  sync)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py -k "c3_1080p or md5 or reflists" > gpurun_out/pytest_sync_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_sync_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_sync_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "crew3:" "crew0:M2DEC_AMD_COPY_CREW=0" > gpurun_out/ab_sync_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_sync_$TAG.txt; exit 1; }
+    tail -3 gpurun_out/ab_sync_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -65,6 +65,23 @@ for t, k, a, b in win:
 if acq:
     print(f"submission per picture (mean ms): acquire {sum(acq) / len(acq):.3f}  copy {sum(cpy) / len(cpy):.3f}  "
           f"submit {sum(smt) / len(smt):.3f}  (max acquire {max(acq):.3f}, max submit {max(smt):.3f})")
+ph = {"waits+H2D": [], "launch_multi": [], "after": []}
+lt = None
+for t, k, a, b in win:
+    if k == "L":
+        lt = [ms(t), None, None]
+    elif k == "M" and lt:
+        lt[1] = ms(t)
+    elif k == "N" and lt:
+        lt[2] = ms(t)
+    elif k == "l" and lt and lt[1] is not None and lt[2] is not None:
+        ph["waits+H2D"].append(lt[1] - lt[0])
+        ph["launch_multi"].append(lt[2] - lt[1])
+        ph["after"].append(ms(t) - lt[2])
+        lt = None
+if ph["after"]:
+    print("launch_held per launch (mean ms):", {k: round(sum(v) / len(v), 3) for k, v in ph.items()},
+          "max launch_multi", round(max(ph["launch_multi"]), 3))
 launch = [(ms(t), a, b) for t, k, a, b in win if k == "L"]
 kp = sorted([r for r in kern if r["Kernel_Name"].startswith("k_picture")], key=lambda r: int(r["Start_Timestamp"]))
 print(f"\n{len(launch)} launches (host), {len(kp)} k_picture kernels")

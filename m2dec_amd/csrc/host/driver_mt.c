@@ -63,6 +63,7 @@ typedef struct md5_pipe {
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
 	int idle;                /* threads waiting for frames */
+	int waiting;             /* threads waiting for a batch to fill */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
@@ -93,18 +94,25 @@ static void *md5_worker(void *arg)
 		/* tail mode: the parse pool has nothing in hand (a stream's last frames are coming out) and an idle
 		 * thread for every queued frame: hash one frame at once, alone — 3.3 ms instead of a batch's 6.5 ms
 		 * after the stream's last output.  While parsing runs, batches keep the MD5 CPU time small. */
-		const int tail = p->tail_mode && m2dec_parse_busy() == 0;
-		const int share = tail ? (p->head - p->next + p->idle) / (p->idle + 1) : MD5_BATCH; /* frames per thread */
-		while (!tail && !p->quit && p->ended == 0 && p->head - p->next < p->min_batch) {
-			const double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
-			struct timespec ts;
+		int tail = 0;
+		p->waiting++;
+		for (;;) { /* (the tail test is redone on every wake: the parse pool may finish while a thread waits) */
+			tail = p->tail_mode && m2dec_parse_busy() == 0;
+			if (tail || p->quit || p->ended || p->head - p->next >= p->min_batch) break;
+			double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
 			if (left <= 0) break;
+			if (p->tail_mode && left > 5e-4) left = 5e-4;
+			struct timespec ts;
 			clock_gettime(CLOCK_REALTIME, &ts);
 			ts.tv_nsec += (long)(left * 1e9);
 			ts.tv_sec += ts.tv_nsec / 1000000000L;
 			ts.tv_nsec %= 1000000000L;
 			pthread_cond_timedwait(&p->cv_job, &p->mu, &ts);
 		}
+		p->waiting--;
+		/* frames per thread: in tail mode the queue is shared with every thread that is free */
+		const int free_ = p->idle + p->waiting;
+		const int share = tail ? (p->head - p->next + free_) / (free_ + 1) : MD5_BATCH;
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];

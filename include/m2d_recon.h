@@ -112,12 +112,47 @@ typedef struct m2r_picture {
 	int16_t *coef;         /* [cap_coef] */
 	int32_t cap_slices, cap_inter, cap_coef;
 	int32_t flags;         /* M2R_PIC_* */
+	/* with M2R_PIC_REFS (ABI revision 6): a summary of inter[0, n_inter) the producer formed while the
+	 * records were in its cache, so the back end does not scan them on the submission path */
+	int32_t ref_blocks;    /* 8x8 (list, block) predictions: slot[l][b] >= 0 entries */
+	uint64_t ref_slots;    /* bit s: some slot[l][b] == s */
 } m2r_picture_t;
 
 /* m2r_picture_t.flags: `slot` and every m2r_inter_t.slot are the back end's picture buffers (virtual
  * frame ids 0..63 of the parse-ahead pipeline), not caller frame slots; the picture reaches a caller
  * frame only through bind().  Set only for back ends that provide bind. */
 #define M2R_PIC_VIRTUAL 1
+/* m2r_picture_t.flags: the record arrays are not the acquired arena's but the parser's own, in host memory
+ * the device runtime has pinned, laid out as m2r_arena_layout() from `mb` on (the back end uploads them
+ * straight from there — no copy into its arena).  The parser keeps them unchanged until records_busy() says
+ * the back end is done with them.  Set only for back ends that provide records_busy. */
+#define M2R_PIC_EXTERNAL 2
+/* m2r_picture_t.flags: ref_blocks / ref_slots hold the summary of inter[] */
+#define M2R_PIC_REFS 4
+
+/* Record arena layout shared by the parser's job arenas and the back ends' arenas (byte offsets from the
+ * arena base, 256-byte aligned): mb | dbk | slice[M2R_ARENA_SLICES] | inter[n] | coef[n * 416].  The fixed
+ * part (mb, dbk, slices) and each used prefix of inter / coef are contiguous, so an upload is two copies. */
+#define M2R_ARENA_SLICES 256
+#define M2R_COEF_PER_MB 416
+typedef struct m2r_arena_layout {
+	size_t mb, dbk, slice, inter, coef, size;
+} m2r_arena_layout_t;
+
+static inline m2r_arena_layout_t m2r_arena_layout(int n_mbs)
+{
+	m2r_arena_layout_t l;
+	const size_t n = (size_t)n_mbs;
+#define M2R_AL_(v) (((v) + 255) & ~(size_t)255)
+	l.mb = 0;
+	l.dbk = M2R_AL_(l.mb + n * sizeof(m2r_mb_t));
+	l.slice = M2R_AL_(l.dbk + n * sizeof(m2r_deblock_t));
+	l.inter = M2R_AL_(l.slice + M2R_ARENA_SLICES * sizeof(m2r_slice_t));
+	l.coef = M2R_AL_(l.inter + n * sizeof(m2r_inter_t));
+	l.size = M2R_AL_(l.coef + n * M2R_COEF_PER_MB * sizeof(int16_t));
+#undef M2R_AL_
+	return l;
+}
 
 /* A reconstruction back end.  The parser acquires an arena, fills it, and submits it; frames are
  * caller-owned NV12 buffers (set_frames), synchronised on demand (sync_frame) before the caller
@@ -147,6 +182,12 @@ typedef struct m2r_backend {
 	 * of the device is complete), 0 otherwise; never blocks.  The decoder polls it while the caller waits
 	 * in peek / get and keeps its lookahead parsing meanwhile.  NULL: sync_frame is called at once. */
 	int (*ready)(void *self, int slot);
+	/* optional (ABI revision 6): the back end takes M2R_PIC_EXTERNAL pictures.  1 while it may still read
+	 * the external records starting at `records` (a submitted picture's `mb`), 0 once it never will again.
+	 * wait = 0 never blocks (any thread, while the decoder's serial calls run); wait = 1 blocks until 0,
+	 * launching a held picture first (only while no other call of this back end runs).  NULL: pictures are
+	 * always copied into the acquired arena. */
+	int (*records_busy)(void *self, const void *records, int wait);
 } m2r_backend_t;
 
 /* ---------------------------------------------------------------- MPEG-1/2 (m2d_func)

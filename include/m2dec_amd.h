@@ -51,11 +51,12 @@ typedef struct {
 
 /* ABI revision of the structs in this header and m2d_recon.h.  3: m2r_backend_t gained `bind` (decode
  * ahead) and m2dec_amd_stats_t grew to its current size; 4: m2r_backend_t gained `flush` (several
- * pictures per launch).  A caller compiled against another revision
+ * pictures per launch); 5: `ready`; 6: `records_busy` (M2R_PIC_EXTERNAL: uploads from the parser's own
+ * pinned records).  A caller compiled against another revision
  * checks m2dec_amd_abi_version() before passing either struct; m2dec_amd_h264_set_backend2 accepts an
  * older (smaller) m2r_backend_t by size, and m2dec_amd_stats_size() is the size every stats pointer
  * must have room for. */
-#define M2DEC_AMD_ABI_VERSION 5
+#define M2DEC_AMD_ABI_VERSION 6
 int m2dec_amd_abi_version(void);
 size_t m2dec_amd_stats_size(void);
 /* 0 if the host CPU lacks the x86-64-v3 features the host library is built for (decoder inits then

@@ -39,10 +39,12 @@ class Info(ctypes.Structure):
 
 
 class Backend(ctypes.Structure):
-    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind/flush/ready."""
+    """m2r_backend_t (include/m2d_recon.h): self + set_frames/acquire/submit/sync_frame/destroy/bind/flush/ready/
+    records_busy."""
     _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("acquire", ctypes.c_void_p),
                 ("submit", ctypes.c_void_p), ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p),
-                ("bind", ctypes.c_void_p), ("flush", ctypes.c_void_p), ("ready", ctypes.c_void_p)]
+                ("bind", ctypes.c_void_p), ("flush", ctypes.c_void_p), ("ready", ctypes.c_void_p),
+                ("records_busy", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):

@@ -785,6 +785,20 @@ int64_t ref_bytes_of(const m2r_inter_t *it, int n)
 	return s;
 }
 
+/* pinned host memory for the parser's record arenas (h264_async.c job_arena: uploaded in place,
+ * M2R_PIC_EXTERNAL); portable, so any device's back end may read it.  NULL without a device. */
+extern "C" void *m2dec_amd_pinned_alloc(size_t n)
+{
+	void *p = nullptr;
+	if (hipHostMalloc(&p, n, hipHostMallocPortable) != hipSuccess) return nullptr;
+	return p;
+}
+
+extern "C" void m2dec_amd_pinned_free(void *p)
+{
+	if (p) (void)hipHostFree(p);
+}
+
 /* ======================================================================== decode-path back end */
 const int kSlicesCap = 64;
 const int kArenas = NSTREAMS * BMAX + BMAX + 2; /* at most: launched + held pictures, and the one being filled */
@@ -796,6 +810,7 @@ struct Arena {
 	hipEvent_t consumed = nullptr; /* the picture's kernels finished reading the device copy */
 	bool pending = false;
 	bool held = false;             /* submitted, not launched yet */
+	const uint8_t *ext = nullptr;  /* M2R_PIC_EXTERNAL: the parser's records the upload reads (else `host`) */
 };
 
 /* Pinned record arenas (+ their device twins) outlive a decoder context: a process decoding stream
@@ -924,6 +939,9 @@ struct HipBackend {
 	TimingSlot tr[16];
 	int tr_next = 0;
 	bool timing = true;
+	/* guards Arena::held / pending / ext: records_busy reads them from any thread while the decoder's
+	 * serial calls (acquire, submit, flush, bind) change them */
+	std::mutex arena_mu;
 };
 
 int launch_held(HipBackend *b);
@@ -997,13 +1015,14 @@ int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
 int arena_alloc(Arena &a, int wm, int hm)
 {
 	size_t n = (size_t)wm * hm;
-	size_t off = 0;
-	auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-	a.off_mb = off; off = al(off + n * sizeof(m2r_mb_t));
-	a.off_dbk = off; off = al(off + n * sizeof(m2r_deblock_t));
-	a.off_slice = off; off = al(off + kSlicesCap * sizeof(m2r_slice_t));
-	a.off_inter = off; off = al(off + n * sizeof(m2r_inter_t));
-	a.off_coef = off; off = al(off + n * 416 * sizeof(int16_t));
+	/* the parser's job arenas have this layout too: an M2R_PIC_EXTERNAL picture uploads the same way */
+	const m2r_arena_layout_t l = m2r_arena_layout((int)n);
+	a.off_mb = l.mb;
+	a.off_dbk = l.dbk;
+	a.off_slice = l.slice;
+	a.off_inter = l.inter;
+	a.off_coef = l.coef;
+	const size_t off = l.size;
 	if (a.size < off) {
 		int dev = 0;
 		CHECK(hipGetDevice(&dev));
@@ -1045,7 +1064,9 @@ m2r_picture_t *be_acquire(void *self, int wm, int hm)
 	if (a.pending) {
 		/* the host copy is overwritten next: wait until that picture's kernels are done with it */
 		if (hipEventSynchronize(a.consumed) != hipSuccess) return nullptr;
+		std::lock_guard<std::mutex> lk(b->arena_mu);
 		a.pending = false;
+		a.ext = nullptr;
 	}
 	if (arena_alloc(a, wm, hm) < 0) return nullptr;
 	return &a.pic;
@@ -1060,6 +1081,16 @@ int be_submit(void *self, m2r_picture_t *pic)
 		if (&x.pic == pic) a = &x;
 	const int n = pic->width_mbs * pic->height_mbs;
 	const bool virt = (pic->flags & M2R_PIC_VIRTUAL) != 0;
+	/* external records: the parser's arena, in the same layout as ours (checked), uploaded from there */
+	const uint8_t *ext = nullptr;
+	if (pic->flags & M2R_PIC_EXTERNAL) {
+		ext = (const uint8_t *)pic->mb;
+		if (!a || (const uint8_t *)pic->dbk != ext + a->off_dbk || (const uint8_t *)pic->slice != ext + a->off_slice ||
+		    (const uint8_t *)pic->inter != ext + a->off_inter || (const uint8_t *)pic->coef != ext + a->off_coef) {
+			fprintf(stderr, "m2dec_amd: submit: external records not in the arena layout\n");
+			return -1;
+		}
+	}
 	if (!a || a->held || pic->width_mbs != sc.Wmb || pic->height_mbs != sc.Hmb || pic->slot < 0 || pic->slot >= sc.nslots ||
 	    (!virt && pic->slot >= b->nframes) || pic->n_slices > kSlicesCap || pic->n_inter > n || pic->n_coef > n * 416) {
 		fprintf(stderr, "m2dec_amd: submit: picture records rejected (arena %d, slot %d)\n", a ? (int)(a - b->ar) : -1, pic->slot);
@@ -1071,7 +1102,8 @@ int be_submit(void *self, m2r_picture_t *pic)
 	j.n_inter = pic->n_inter;
 	j.n_intra = pic->n_intra;
 	j.deblock = pic->deblock;
-	j.refs = refs_of(pic->inter, pic->n_inter) & ~(1ull << pic->slot);
+	const bool sum = (pic->flags & M2R_PIC_REFS) != 0; /* (the producer summarised inter[]) */
+	j.refs = (sum ? pic->ref_slots : refs_of(pic->inter, pic->n_inter)) & ~(1ull << pic->slot);
 	j.r.mb = (const m2r_mb_t *)(a->dev + a->off_mb);
 	j.r.dbk = (const m2r_deblock_t *)(a->dev + a->off_dbk);
 	j.r.sl = (const m2r_slice_t *)(a->dev + a->off_slice);
@@ -1081,8 +1113,12 @@ int be_submit(void *self, m2r_picture_t *pic)
 	h.virt = virt;
 	h.rec_bytes = n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t)) + pic->n_slices * sizeof(m2r_slice_t) +
 	              pic->n_inter * sizeof(m2r_inter_t) + pic->n_coef * sizeof(int16_t);
-	h.ref_bytes = ref_bytes_of(pic->inter, pic->n_inter);
-	a->held = true;
+	h.ref_bytes = sum ? (int64_t)pic->ref_blocks * (64 + 32) : ref_bytes_of(pic->inter, pic->n_inter);
+	{
+		std::lock_guard<std::mutex> lk(b->arena_mu);
+		a->ext = ext;
+		a->held = true;
+	}
 	/* a caller slot as the picture buffer (no decode ahead): copied out right behind its kernel, so
 	 * launched at once, as is a full hand */
 	if (!virt || b->nheld >= b->limit) return launch_held(b);
@@ -1129,12 +1165,13 @@ int launch_held(HipBackend *b)
 		CHECK(hipEventRecord(ts->e[0], s));
 	}
 	for (int i = 0; i < n; ++i) {
+		/* mb | dbk | used slices in one copy, then the used inter and coefficient prefixes (m2r_arena_layout) */
 		const Arena *a = b->held[i].a;
 		const m2r_picture_t *pic = &a->pic;
-		CHECK(hipMemcpyAsync(a->dev + a->off_mb, a->host + a->off_mb, a->off_slice - a->off_mb, hipMemcpyHostToDevice, s));
-		if (pic->n_slices) CHECK(hipMemcpyAsync(a->dev + a->off_slice, a->host + a->off_slice, pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
-		if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, a->host + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
-		if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, a->host + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+		const uint8_t *src = a->ext ? a->ext : a->host;
+		CHECK(hipMemcpyAsync(a->dev, src, a->off_slice + pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
+		if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, src + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
+		if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, src + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
 	}
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	m2d_tl('M', n, k);
@@ -1146,6 +1183,7 @@ int launch_held(HipBackend *b)
 	for (int i = 0; i < n; ++i) {
 		HipBackend::Held &h = b->held[i];
 		CHECK(hipEventRecord(h.a->consumed, s));
+		std::lock_guard<std::mutex> lk(b->arena_mu);
 		h.a->pending = true;
 		h.a->held = false;
 		if (!h.virt) /* the caller's slot is the picture buffer: copy out right behind the kernel */
@@ -1237,6 +1275,39 @@ int be_ready(void *self, int slot)
 	return hipEventQuery(b->slot_ev[slot]) == hipSuccess;
 }
 
+/* m2r_backend_t.records_busy: 1 while an arena's upload may still read the external records at `records`
+ * (held, or launched and its consumed event not reached); the arena forgets them once it is reached */
+int be_records_busy(void *self, const void *records, int wait)
+{
+	HipBackend *b = (HipBackend *)self;
+	for (auto &a : b->ar) {
+		bool held, pending;
+		hipEvent_t ev;
+		{
+			std::lock_guard<std::mutex> lk(b->arena_mu);
+			if (a.ext != records) continue;
+			held = a.held;
+			pending = a.pending;
+			ev = a.consumed;
+		}
+		if (held) {
+			if (!wait) return 1;
+			if (launch_held(b) < 0) return 1; /* (only while no other call runs: see m2d_recon.h) */
+			std::lock_guard<std::mutex> lk(b->arena_mu);
+			pending = a.pending;
+			ev = a.consumed;
+		}
+		if (pending) {
+			const hipError_t q = wait ? hipEventSynchronize(ev) : hipEventQuery(ev);
+			if (q != hipSuccess) return 1;
+		}
+		std::lock_guard<std::mutex> lk(b->arena_mu);
+		if (a.ext == records && !a.held) a.ext = nullptr;
+		return a.ext == records;
+	}
+	return 0;
+}
+
 void be_destroy(void *self)
 {
 	HipBackend *b = (HipBackend *)self;
@@ -1325,6 +1396,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->bind = be_bind;
 	out->flush = be_flush;
 	out->ready = be_ready;
+	out->records_busy = be_records_busy;
 	g_live_backends[device & 15]++;
 	if (const char *e = getenv("M2DEC_AMD_HOLD")) b->hold = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */

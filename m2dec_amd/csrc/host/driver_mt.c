@@ -520,5 +520,6 @@ int m2dec_amd_null_backend_create(m2r_backend_t *out)
 	out->bind = NULL;
 	out->flush = NULL;
 	out->ready = NULL;
+	out->records_busy = NULL;
 	return 0;
 }

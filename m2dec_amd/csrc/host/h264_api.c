@@ -486,6 +486,7 @@ int m2dec_amd_h264_set_backend2(void *ctx, const m2r_backend_t *be, size_t be_si
 	if (be && (be_size < offsetof(m2r_backend_t, bind) || be_size > sizeof(m2r_backend_t))) return -1;
 	d = enter(ctx);
 	if (!d) return -1;
+	h264_async_records_wait(d); /* (the old back end may still upload job records) */
 	if (!be) { /* detach a borrowed back end without destroying it */
 		d->have_backend = 0;
 	} else {

@@ -80,8 +80,10 @@ typedef struct h264_job {
 	h264_mbinfo_t *mbi;       /* private neighbour state */
 	size_t mbi_n;
 	m2r_picture_t pic;        /* private record arena (frame ids are virtual until submission) */
-	uint8_t *arena;
+	uint8_t *arena;           /* laid out as m2r_arena_layout() */
 	size_t arena_size;
+	int arena_pinned;         /* the arena is pinned host memory (m2dec_amd_pinned_alloc) */
+	int ext_busy;             /* submitted as M2R_PIC_EXTERNAL: the back end may still read the arena */
 	int vid;                  /* virtual frame id of the picture (lookahead context) */
 	int slot;                 /* frame slot (API context; -1 until A closed the picture) */
 	int poc;                  /* consistency check between the two contexts */
@@ -126,6 +128,8 @@ struct h264_async {
 	long sub;                 /* next job to submit: [tail, sub) submitted */
 	long bnd;                 /* decode ahead: next job to bind: [tail, bnd) bound */
 	int ahead;                /* decode ahead: the back end has bind (M2R_PIC_VIRTUAL submissions) */
+	int ext;                  /* decode ahead, and the back end takes M2R_PIC_EXTERNAL pictures: job arenas
+	                             are pinned and uploaded from where the workers wrote them (no record copy) */
 	int driving;              /* decode ahead: a thread is inside pipe_drive (back-end calls are serial) */
 	int held;                 /* decode ahead: submitted since the last back-end flush */
 	int sub_err;
@@ -183,31 +187,42 @@ static struct {
 } g_parse = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, {0}, 0, NULL, NULL};
 
 static void pipe_drive(struct h264_async *as);
+static int job_ext_idle(struct h264_async *as, h264_job_t *j, int wait);
 
-static int job_arena(h264_job_t *j, int wm, int hm)
+static void arena_free(h264_job_t *j)
+{
+	if (j->arena_pinned) m2dec_amd_pinned_free(j->arena);
+	else free(j->arena);
+	j->arena = NULL;
+	j->arena_size = 0;
+	j->arena_pinned = 0;
+}
+
+/* the job's record arena for a wm x hm picture (pinned when the pipeline uploads from it: `pinned`) */
+static int job_arena(h264_job_t *j, int wm, int hm, int pinned)
 {
 	const int n = wm * hm;
-	const size_t need = (size_t)n * (sizeof(m2r_mb_t) + sizeof(m2r_deblock_t) + sizeof(m2r_inter_t) + 416 * sizeof(int16_t)) +
-	                    256 * sizeof(m2r_slice_t) + 64;
-	if (need > j->arena_size) {
-		free(j->arena);
-		j->arena = (uint8_t *)malloc(need);
-		j->arena_size = j->arena ? need : 0;
+	const m2r_arena_layout_t l = m2r_arena_layout(n);
+	if (l.size > j->arena_size || (pinned && !j->arena_pinned)) {
+		arena_free(j);
+		if (pinned && (j->arena = (uint8_t *)m2dec_amd_pinned_alloc(l.size))) j->arena_pinned = 1;
+		else j->arena = (uint8_t *)malloc(l.size);
 		if (!j->arena) return -1;
+		j->arena_size = l.size;
 	}
 	uint8_t *p = j->arena;
 	m2r_picture_t *pic = &j->pic;
 	memset(pic, 0, sizeof(*pic));
 	pic->width_mbs = wm;
 	pic->height_mbs = hm;
-	pic->mb = (m2r_mb_t *)p; p += (size_t)n * sizeof(m2r_mb_t);
-	pic->dbk = (m2r_deblock_t *)p; p += (size_t)n * sizeof(m2r_deblock_t);
-	pic->slice = (m2r_slice_t *)p; p += 256 * sizeof(m2r_slice_t);
-	pic->inter = (m2r_inter_t *)p; p += (size_t)n * sizeof(m2r_inter_t);
-	pic->coef = (int16_t *)p;
-	pic->cap_slices = 256;
+	pic->mb = (m2r_mb_t *)(p + l.mb);
+	pic->dbk = (m2r_deblock_t *)(p + l.dbk);
+	pic->slice = (m2r_slice_t *)(p + l.slice);
+	pic->inter = (m2r_inter_t *)(p + l.inter);
+	pic->coef = (int16_t *)(p + l.coef);
+	pic->cap_slices = M2R_ARENA_SLICES;
 	pic->cap_inter = n;
-	pic->cap_coef = n * 416;
+	pic->cap_coef = n * M2R_COEF_PER_MB;
 	if ((size_t)n > j->mbi_n) {
 		free(j->mbi);
 		j->mbi = (h264_mbinfo_t *)malloc(sizeof(h264_mbinfo_t) * (size_t)n);
@@ -246,7 +261,7 @@ static void job_free(h264_job_t *j)
 	free(j->sw);
 	free(j->spic);
 	free(j->sret);
-	free(j->arena);
+	arena_free(j);
 	free(j->w);
 	free(j);
 }
@@ -267,6 +282,24 @@ static void job_release(h264_job_t *j) /* (mutex held) */
 }
 
 /* ---------------------------------------------------------------- worker */
+/* the reference summary of a parsed picture's motion records (M2R_PIC_REFS), formed by the worker while
+ * they are in its cache */
+static void pic_refs(m2r_picture_t *p)
+{
+	uint64_t m = 0;
+	int nb = 0;
+	for (int i = 0; i < p->n_inter; ++i) {
+		const int8_t *s = &p->inter[i].slot[0][0];
+		for (int k = 0; k < 8; ++k) {
+			nb += s[k] >= 0;
+			m |= (uint64_t)(s[k] >= 0) << (s[k] & 63);
+		}
+	}
+	p->ref_blocks = nb;
+	p->ref_slots = m;
+	p->flags |= M2R_PIC_REFS;
+}
+
 static void job_run(h264_job_t *j)
 {
 	h264_dec_t *w = j->w;
@@ -573,6 +606,7 @@ static void *pool_worker(void *arg)
 			} else {
 				__atomic_fetch_add(&as->n_par, 1, __ATOMIC_RELAXED);
 			}
+			if (!j->err) pic_refs(&j->pic);
 			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
 			m2d_tl('p', j->seq, j->snap[0]->sh.slice_type);
@@ -691,6 +725,7 @@ int h264_async_start(h264_dec_t *d, int threads)
 	for (int i = 0; i < 17; ++i) as->col_last[i] = as->col_writer[i] = -1;
 	as->la_sps_nal = -1;
 	as->ahead = d->have_backend && d->backend.bind && !getenv("M2DEC_AMD_NO_AHEAD");
+	as->ext = as->ahead && d->backend.records_busy && !(getenv("M2DEC_AMD_EXTERNAL") && atoi(getenv("M2DEC_AMD_EXTERNAL")) == 0);
 	as->stats = getenv("M2DEC_AMD_ASYNC_STATS") ? atoi(getenv("M2DEC_AMD_ASYNC_STATS")) : 0;
 	as->slice_par = !getenv("M2DEC_AMD_SLICE_PAR") || atoi(getenv("M2DEC_AMD_SLICE_PAR")) != 0;
 	as->t0 = now_s();
@@ -738,6 +773,29 @@ double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback)
 	return t;
 }
 
+/* Wait until the back end reads no job arena of this pipeline any more (before the jobs leave it, or
+ * the back end is replaced).  Caller's thread; no worker or driver of the pipeline may run. */
+void h264_async_records_wait(h264_dec_t *d)
+{
+	struct h264_async *as = d->as;
+	h264_job_t *busy[2 * AS_MAX];
+	int n = 0;
+	if (!as || !as->ext) return;
+	pthread_mutex_lock(as->mu);
+	while (as->driving) pthread_cond_wait(&as->cv_done, as->mu);
+	as->driving = 1; /* (no back-end call of a pool worker meanwhile; job_get runs on this thread) */
+	for (long i = as->tail; i < as->head; ++i)
+		if (as->fifo[i % AS_MAX]->ext_busy) busy[n++] = as->fifo[i % AS_MAX];
+	for (int i = 0; i < as->nfree; ++i)
+		if (as->free_jobs[i]->ext_busy) busy[n++] = as->free_jobs[i];
+	pthread_mutex_unlock(as->mu);
+	for (int i = 0; i < n; ++i) (void)job_ext_idle(as, busy[i], 1);
+	pthread_mutex_lock(as->mu);
+	as->driving = 0;
+	pthread_cond_broadcast(&as->cv_done);
+	pthread_mutex_unlock(as->mu);
+}
+
 void h264_async_stop(h264_dec_t *d)
 {
 	struct h264_async *as = d->as;
@@ -758,6 +816,11 @@ void h264_async_stop(h264_dec_t *d)
 			break;
 		}
 	if (g_parse.rr == as) g_parse.rr = NULL;
+	pthread_mutex_unlock(as->mu);
+	/* (no worker or driver of this pipeline runs now: the back end is ours to wait on, outside the pool's
+	 * mutex) jobs another context may take next must not be read by this back end any more */
+	h264_async_records_wait(d);
+	pthread_mutex_lock(as->mu);
 	for (long i = as->tail; i < as->head; ++i) job_release(as->fifo[i % AS_MAX]);
 	job_release(as->cur);
 	for (int i = 0; i < as->nfree; ++i) job_release(as->free_jobs[i]);
@@ -781,8 +844,15 @@ void h264_async_trim(h264_dec_t *d)
 	int idle;
 	if (!as) return;
 	pthread_mutex_lock(as->mu);
-	for (int i = 0; i < as->nfree; ++i) job_release(as->free_jobs[i]);
-	as->nfree = 0;
+	{
+		int keep = 0;
+		for (int i = 0; i < as->nfree; ++i) {
+			h264_job_t *j = as->free_jobs[i];
+			if (job_ext_idle(as, j, 0)) job_release(j);
+			else as->free_jobs[keep++] = j; /* (still uploading: job_get or stop takes it later) */
+		}
+		as->nfree = keep;
+	}
 	idle = as->head == as->tail;
 	pthread_mutex_unlock(as->mu);
 	if (idle) { /* no job may still read a spare (the lookahead runs on this thread) */
@@ -791,10 +861,24 @@ void h264_async_trim(h264_dec_t *d)
 	}
 }
 
+/* the back end no longer reads job j's arena (wait = 0: never blocks; wait = 1: see records_busy) */
+static int job_ext_idle(struct h264_async *as, h264_job_t *j, int wait)
+{
+	const m2r_backend_t *be = &as->api->backend;
+	if (j->ext_busy && !(be->records_busy && be->records_busy(be->self, j->arena, wait) != 0)) j->ext_busy = 0;
+	return !j->ext_busy;
+}
+
 static h264_job_t *job_get(struct h264_async *as)
 {
 	h264_job_t *j;
-	if (as->nfree) return as->free_jobs[--as->nfree];
+	/* (the newest retired jobs may still be uploading: take the first one that is not) */
+	for (int i = 0; i < as->nfree; ++i)
+		if (job_ext_idle(as, as->free_jobs[i], 0)) {
+			j = as->free_jobs[i];
+			as->free_jobs[i] = as->free_jobs[--as->nfree];
+			return j;
+		}
 	if (g_njobs) return g_jobs[--g_njobs];
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
@@ -847,14 +931,35 @@ static int copy_submit(h264_dec_t *d, h264_job_t *j, int virt)
 	dst->n_slices = src->n_slices;
 	dst->n_intra = src->n_intra;
 	dst->deblock = src->deblock;
-	memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
-	if (virt) {
+	if (src->flags & M2R_PIC_REFS) {
+		dst->flags |= M2R_PIC_REFS;
+		dst->ref_blocks = src->ref_blocks;
+		dst->ref_slots = src->ref_slots;
+		if (!virt) {
+			dst->ref_slots = 0;
+			for (int v = 0; v < 64; ++v)
+				if (((src->ref_slots >> v) & 1) && j->map[v] >= 0) dst->ref_slots |= 1ull << (j->map[v] & 63);
+		}
+	}
+	if (virt && as->ext && j->arena_pinned && d->backend.records_busy) {
+		/* the back end uploads the job's own (pinned) records: nothing to copy; the job is not reused
+		 * until records_busy says the upload is done (job_get) */
+		dst->flags |= M2R_PIC_EXTERNAL;
+		dst->mb = src->mb;
+		dst->dbk = src->dbk;
+		dst->slice = src->slice;
+		dst->inter = src->inter;
+		dst->coef = src->coef;
+		j->ext_busy = 1;
+	} else if (virt) {
+		memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
 		void *const to[4] = {dst->mb, dst->dbk, dst->inter, dst->coef};
 		const void *const from[4] = {src->mb, src->dbk, src->inter, src->coef};
 		const size_t len[4] = {sizeof(m2r_mb_t) * (size_t)n, sizeof(m2r_deblock_t) * (size_t)n,
 		                       sizeof(m2r_inter_t) * (size_t)src->n_inter, sizeof(int16_t) * (size_t)src->n_coef};
 		m2dec_par_memcpy(M2DEC_CREW_SUBMIT, 4, to, from, len);
 	} else {
+		memcpy(dst->slice, src->slice, sizeof(m2r_slice_t) * (size_t)src->n_slices);
 		memcpy(dst->mb, src->mb, sizeof(m2r_mb_t) * (size_t)n);
 		memcpy(dst->dbk, src->dbk, sizeof(m2r_deblock_t) * (size_t)n);
 		for (int i = 0; i < src->n_inter; ++i) {
@@ -1210,7 +1315,7 @@ int h264_async_add_slice(h264_dec_t *la)
 		pthread_mutex_lock(as->mu); /* (pipe_drive recycles jobs) */
 		j = job_get(as);
 		pthread_mutex_unlock(as->mu);
-		if (!j || job_arena(j, la->mb_w, la->mb_h) < 0) return -1;
+		if (!j || job_arena(j, la->mb_w, la->mb_h, as->ext) < 0) return -1;
 		j->vid = la->curr_idx;
 		j->slot = -1;
 		j->sps_nal = as->la_sps_nal;

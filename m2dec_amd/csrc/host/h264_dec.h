@@ -411,6 +411,10 @@ int m2dec_parse_busy(void); /* parse-pool workers inside a job right now (all pi
 enum { M2DEC_CREW_SUBMIT, M2DEC_CREW_SYNC, M2DEC_CREWS };
 void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
 void h264_async_stop(h264_dec_t *d);
+void h264_async_records_wait(h264_dec_t *d);
+/* pinned host memory from the device runtime (runtime.hip; NULL without a device) */
+void *m2dec_amd_pinned_alloc(size_t n);
+void m2dec_amd_pinned_free(void *p);
 double h264_async_parse_seconds(h264_dec_t *d, long *par, long *par_fallback);
 int h264_async_nal_next(h264_dec_t *d);
 void h264_async_resume(h264_dec_t *d);

@@ -1261,5 +1261,6 @@ int oracle_backend_create(m2r_backend_t *out)
 	out->bind = be_bind;
 	out->flush = NULL;
 	out->ready = NULL;
+	out->records_busy = NULL;
 	return 0;
 }

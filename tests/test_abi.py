@@ -80,11 +80,12 @@ def test_abi_revision_and_sized_backend(built):
     ctx = ctypes.create_string_buffer(t.context_size)
     init = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)(t.init)
     assert init(ctx, -1, None, None) == 0
-    be = (ctypes.c_void_p * 9)()  # self + 8 function pointers (revision 5)
+    be = (ctypes.c_void_p * 10)()  # self + 9 function pointers (revision 6)
     lib.m2dec_amd_h264_set_backend2.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     ptr = ctypes.sizeof(ctypes.c_void_p)
     assert lib.m2dec_amd_h264_set_backend2(ctx, be, 3 * ptr) == -1   # shorter than any revision
-    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 10 * ptr) == -1  # longer than this revision
+    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 11 * ptr) == -1  # longer than this revision
+    assert lib.m2dec_amd_h264_set_backend2(ctx, be, 9 * ptr) == 0    # revision 5: no records_busy
     assert lib.m2dec_amd_h264_set_backend2(ctx, be, 8 * ptr) == 0    # revision 4: no ready
     assert lib.m2dec_amd_h264_set_backend2(ctx, be, 6 * ptr) == 0    # revision 2: no bind
     assert lib.m2dec_amd_h264_set_backend2(ctx, be, 7 * ptr) == 0    # revision 3: no flush

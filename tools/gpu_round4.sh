@@ -3,6 +3,7 @@
 #   h265    the H.265 GPU parity tests (I and P / B goldens) + the H.265 bench legs
 #   tl      host + rocprof timeline of one C3 decode (tools/timeline.sh)
 #   streams interleaved end-to-end A/B of the launch stream count (tools/ab_env.py)
+#   ext     decode-path GPU tests + A/B of uploads from the parser's pinned records (M2DEC_AMD_EXTERNAL)
 #   gpu     the whole GPU test suite
 # Usage: bash tools/gpu_round4.sh TAG STEP...
 set -o pipefail
@@ -50,6 +51,11 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_sync_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "crew3:" "crew0:M2DEC_AMD_COPY_CREW=0" > gpurun_out/ab_sync_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_sync_$TAG.txt; exit 1; }
     tail -3 gpurun_out/ab_sync_$TAG.txt ;;
+  ext)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py tests/test_gpu_batch.py tests/test_gpu_boundary.py > gpurun_out/pytest_ext_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_ext_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_ext_$TAG.log
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "ext1:" "ext0:M2DEC_AMD_EXTERNAL=0" > gpurun_out/ab_ext_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_ext_$TAG.txt; exit 1; }
+    tail -3 gpurun_out/ab_ext_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

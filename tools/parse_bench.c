@@ -18,8 +18,10 @@ int main(int argc,char**argv){
   if(fi<0){perror("perf_event_open");}
   for(int r=0;r<reps;r++){ m2r_backend_t be; m2dec_amd_null_backend_create(&be);
     if(fi>=0){ioctl(fi,PERF_EVENT_IOC_RESET,0);ioctl(fc,PERF_EVENT_IOC_RESET,0);ioctl(fb,PERF_EVENT_IOC_RESET,0);ioctl(fi,PERF_EVENT_IOC_ENABLE,0);ioctl(fc,PERF_EVENT_IOC_ENABLE,0);ioctl(fb,PERF_EVENT_IOC_ENABLE,0);}
+    struct timespec t0,t1; clock_gettime(CLOCK_MONOTONIC,&t0);
     int fr=m2dec_amd_decode_stream3(d,n,&be,0,-1,0,NULL,NULL,NULL);
+    clock_gettime(CLOCK_MONOTONIC,&t1);
     long long ins=0,cyc=0,bm=0; if(fi>=0){ioctl(fi,PERF_EVENT_IOC_DISABLE,0);ioctl(fc,PERF_EVENT_IOC_DISABLE,0);ioctl(fb,PERF_EVENT_IOC_DISABLE,0);if(read(fi,&ins,8)<0||read(fc,&cyc,8)<0||read(fb,&bm,8)<0)return 1;}
     be.destroy(be.self);
-    printf("%d frames  Minstr/frame %.2f  Mcyc/frame %.2f  Kbrmiss/frame %.1f\n",fr,ins/1e6/fr,cyc/1e6/fr,bm/1e3/fr);}
+    printf("%.3f ms/frame  %d frames  Minstr/frame %.2f  Mcyc/frame %.2f  Kbrmiss/frame %.1f\n",((t1.tv_sec-t0.tv_sec)*1e3+(t1.tv_nsec-t0.tv_nsec)/1e6)/fr,fr,ins/1e6/fr,cyc/1e6/fr,bm/1e3/fr);}
   return 0;}

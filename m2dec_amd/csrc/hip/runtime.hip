@@ -52,18 +52,29 @@ static int dbg_knob(const char *name)
 }
 
 const int NSTREAMS = 8; /* most launch streams of a decoder context (arrays); g_nstreams of them are used */
-/* launch streams in use: one hardware queue each, the copy stream another — 3 with the default
- * GPU_MAX_HW_QUEUES=4 (more streams than queues share a queue and serialise their launches);
- * M2DEC_AMD_STREAMS = 1..8 (with GPU_MAX_HW_QUEUES raised to match) */
+/* launch streams in use: one hardware queue each, the copy stream another — more streams than queues
+ * share a queue and serialise their launches.  4 when the runtime has at least 5 queues (the library
+ * asks for 8 when it is loaded, below; at 1080p 4 x 2 pictures fill the workgroup budget:
+ * profiles/r95_ab_prio_streams.txt), else 3 (HIP's default GPU_MAX_HW_QUEUES=4);
+ * M2DEC_AMD_STREAMS = 1..8 */
 static int nstreams()
 {
 	static int n = 0;
 	if (!n) {
 		const char *e = getenv("M2DEC_AMD_STREAMS");
-		int v = e ? atoi(e) : 3;
+		const char *q = getenv("GPU_MAX_HW_QUEUES");
+		int v = e ? atoi(e) : (q && atoi(q) >= 5 ? 4 : 3);
 		n = v < 1 ? 1 : (v > NSTREAMS ? NSTREAMS : v);
 	}
 	return n;
+}
+
+/* Hardware queues for the launch streams + the copy stream: the runtime reads GPU_MAX_HW_QUEUES when it
+ * starts, so the library asks for 8 as it is loaded (a caller's own setting wins; a process whose HIP
+ * runtime started earlier keeps its queues, and nstreams() falls back to 3 unless it says 5 or more) */
+__attribute__((constructor)) static void hw_queues_default()
+{
+	setenv("GPU_MAX_HW_QUEUES", "8", 0);
 }
 const int BMAX = 4; /* at most this many pictures per decode-path launch: the back end holds submitted
                      * pictures back until the decoder flushes (the end of a burst of submits) or it holds

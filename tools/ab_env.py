@@ -21,6 +21,7 @@ for i in range(%d + 2):
     if i >= 2:
         ts.append(1e3 * (st.t_end - st.t_start))
 print('RESULT', statistics.median(ts), min(ts))
+print('ALL', ' '.join('%%.3f' %% t for t in ts))
 """
 
 
@@ -32,6 +33,7 @@ def main():
         env = dict(x.split("=", 1) for x in kv.split(",") if x)
         cfgs.append((name, env))
     res = {c[0]: [] for c in cfgs}
+    every = {c[0]: [] for c in cfgs}
     for r in range(rounds):
         for name, env in cfgs:
             e = dict(os.environ, **env)
@@ -43,7 +45,13 @@ def main():
                 sys.exit(1)
             med, mn = map(float, line[0].split()[1:])
             res[name].append(med)
+            every[name] += [float(x) for x in [y for y in out.stdout.splitlines() if y.startswith("ALL")][0].split()[1:]]
             print(f"round {r} {name:12s} median {med:6.2f} ms  min {mn:6.2f} ms", flush=True)
+    import statistics
+    for k, v in every.items():  # every decode of every round: the comparison to read
+        v = sorted(v)
+        print(f"all {k:12s} n {len(v):3d}  median {statistics.median(v):6.2f}  mean {statistics.mean(v):6.2f}  "
+              f"p25 {v[len(v) // 4]:6.2f}  p75 {v[3 * len(v) // 4]:6.2f} ms", flush=True)
     print(json.dumps({k: sorted(v) for k, v in res.items()}))
 
 

@@ -20,7 +20,7 @@ for step in "$@"; do
   tl)
     bash tools/timeline.sh $TAG 4 || exit 1 ;;
   streams)
-    timeout -k 10 600 python3 tools/ab_env.py 3 10 "s3:" "s6q8:M2DEC_AMD_STREAMS=6,GPU_MAX_HW_QUEUES=8" "s7q8:M2DEC_AMD_STREAMS=7,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_streams_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_streams_$TAG.txt; exit 1; }
+    timeout -k 10 600 python3 tools/ab_env.py 3 10 "s3:" "s4q5:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=5" "s4q8:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=8" "s3q8:GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_streams_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_streams_$TAG.txt; exit 1; }
     tail -6 gpurun_out/ab_streams_$TAG.txt ;;
   hold)
     timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py -k "c3_1080p or reflists or mmco5" > gpurun_out/pytest_hold_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_hold_$TAG.log; exit 1; }
@@ -56,6 +56,14 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_ext_$TAG.log
     timeout -k 10 600 python3 tools/ab_env.py 3 10 "ext1:" "ext0:M2DEC_AMD_EXTERNAL=0" > gpurun_out/ab_ext_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_ext_$TAG.txt; exit 1; }
     tail -3 gpurun_out/ab_ext_$TAG.txt ;;
+  prio2)
+    timeout -k 10 900 python3 tools/ab_env.py 5 16 "prio1:" "prio0:M2DEC_AMD_PARSE_PRIO=0" "prio1s4:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=8" "prio0s4:M2DEC_AMD_PARSE_PRIO=0,M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_prio2_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_prio2_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_prio2_$TAG.txt ;;
+  win)
+    timeout -k 10 900 python3 tools/ab_env.py 4 16 "w20:GPU_MAX_HW_QUEUES=8" "w0:M2DEC_AMD_PARSE_PRIO=0,GPU_MAX_HW_QUEUES=8" "w12:M2DEC_AMD_PARSE_PRIO=12,GPU_MAX_HW_QUEUES=8" "w32:M2DEC_AMD_PARSE_PRIO=32,GPU_MAX_HW_QUEUES=8" "w20s3:M2DEC_AMD_STREAMS=3,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_win_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_win_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_win_$TAG.txt ;;
+  tlq8)
+    GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -62,8 +62,6 @@ typedef struct md5_pipe {
 	int stats;
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
-	int idle;                /* threads waiting for frames */
-	int waiting;             /* threads waiting for a batch to fill */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
@@ -87,15 +85,12 @@ static void *md5_worker(void *arg)
 	md5_pipe_t *p = (md5_pipe_t *)arg;
 	pthread_mutex_lock(&p->mu);
 	for (;;) {
-		p->idle++;
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
-		p->idle--;
 		if (p->next == p->head) break;
-		/* tail mode: the parse pool has nothing in hand (a stream's last frames are coming out) and an idle
-		 * thread for every queued frame: hash one frame at once, alone — 3.3 ms instead of a batch's 6.5 ms
-		 * after the stream's last output.  While parsing runs, batches keep the MD5 CPU time small. */
+		/* tail mode: the parse pool has nothing in hand (a stream's last frames are coming out): hash one
+		 * frame at once, alone — 3.3 ms instead of a batch's 6.5 ms after the stream's last output.  While
+		 * parsing runs, batches keep the MD5 CPU time small. */
 		int tail = 0;
-		p->waiting++;
 		for (;;) { /* (the tail test is redone on every wake: the parse pool may finish while a thread waits) */
 			tail = p->tail_mode && m2dec_parse_busy() == 0;
 			if (tail || p->quit || p->ended || p->head - p->next >= p->min_batch) break;
@@ -109,10 +104,10 @@ static void *md5_worker(void *arg)
 			ts.tv_nsec %= 1000000000L;
 			pthread_cond_timedwait(&p->cv_job, &p->mu, &ts);
 		}
-		p->waiting--;
-		/* frames per thread: in tail mode the queue is shared with every thread that is free */
-		const int free_ = p->idle + p->waiting;
-		const int share = tail ? (p->head - p->next + free_) / (free_ + 1) : MD5_BATCH;
+		/* frames per thread: in tail mode one each (the threads still hashing finish within ~3 ms and take
+		 * the rest; a thread that took all queued frames alone ran 6.7 ms past the last frame: r97), more
+		 * only when the queue outnumbers the threads */
+		const int share = tail ? (p->head - p->next + p->nth - 1) / p->nth : MD5_BATCH;
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];

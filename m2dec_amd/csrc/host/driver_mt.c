@@ -32,6 +32,7 @@
 #define MD5_THREADS 16     /* one stream: a 16-frame batch of 1080p takes one core ~6.5 ms on the box's EPYC
                               9575F, one frame alone 3.3 ms (tools/md5_batch_bench.py, profiles/r85_md5_batch.txt);
                               most threads only work in tail mode (below); M2DEC_AMD_MD5_THREADS */
+#define MD5_TAIL_PARSE_BUSY 4 /* tail mode once at most this many parse workers are busy */
 
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
  * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
@@ -87,12 +88,13 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
-		/* tail mode: the parse pool has nothing in hand (a stream's last frames are coming out): hash one
-		 * frame at once, alone — 3.3 ms instead of a batch's 6.5 ms after the stream's last output.  While
-		 * parsing runs, batches keep the MD5 CPU time small. */
+		/* tail mode: the parse pool is (nearly) out of work — a stream's last pictures are being parsed or
+		 * coming out: hash one frame at once, alone — 3.3 ms instead of a batch's 6.5 ms after the stream's
+		 * last output (a batch taken as the last 2-4 pictures parse ends last: r98).  While the pool is
+		 * busy, batches keep the MD5 CPU time small. */
 		int tail = 0;
 		for (;;) { /* (the tail test is redone on every wake: the parse pool may finish while a thread waits) */
-			tail = p->tail_mode && m2dec_parse_busy() == 0;
+			tail = p->tail_mode && m2dec_parse_busy() <= MD5_TAIL_PARSE_BUSY;
 			if (tail || p->quit || p->ended || p->head - p->next >= p->min_batch) break;
 			double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
 			if (left <= 0) break;

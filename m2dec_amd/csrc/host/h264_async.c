@@ -521,7 +521,7 @@ static int deps_ready(const struct h264_async *as, const h264_job_t *j, int *err
 	return 1;
 }
 
-static int g_parse_prio = 12; /* M2DEC_AMD_PARSE_PRIO (read when the pool starts): pick_job's window */
+static int g_parse_prio = 20; /* M2DEC_AMD_PARSE_PRIO (read when the pool starts): pick_job's window */
 
 /* A ready job (or a slice to help with) of pipeline `as`, marked taken; NULL if none.  Mutex held. */
 static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *slice_k, int *dep_err)
@@ -538,13 +538,14 @@ static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *s
 	/* a taken job leaves the queue at once (its entry is cleared): once finished and retired it is
 	 * recycled for a later picture, and a stale entry would hand that one out half built */
 	while (as->qtail < as->qhead && !as->queue[as->qtail % AS_MAX]) as->qtail++;
-	/* Reference pictures within g_parse_prio (12) jobs of the oldest queued one first (the oldest such), then
+	/* Reference pictures within g_parse_prio (20) jobs of the oldest queued one first (the oldest such), then
 	 * the oldest ready job.  The oldest-first order alone feeds the in-order submission evenly but starts
 	 * the stream's last anchors late, and the B pictures waiting for them leave workers idle for ~8 ms
 	 * (profiles/r96_timeline.txt); anchors first without a bound (a window of 64) parse the B pictures,
 	 * and with them the submission, late (profiles/r86_timeline.txt).  An anchor parsed about one round
 	 * of the pool ahead of the oldest job is done when its B pictures come up (tools/parse_sched_sim.py;
-	 * profiles/r97_ab_window.txt: windows 0 / 12 / 20 / 32 -> median 32.7 / 31.7 / 32.5 / 33.3 ms).
+	 * profiles/r97_ab_window.txt, r99: windows 0 / 12 / 20 / 32 / 64 -> median 32.7 / 31.7-33.2 / 32.0-32.5 /
+	 * 33.3 / 33.7 ms).
 	 * M2DEC_AMD_PARSE_PRIO = the window (0: oldest first). */
 	const long window_end = as->qtail + g_parse_prio;
 	for (int pass = g_parse_prio ? 0 : 1; pass < 2; ++pass)

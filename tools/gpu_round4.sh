@@ -60,7 +60,7 @@ for step in "$@"; do
     timeout -k 10 900 python3 tools/ab_env.py 5 16 "prio1:" "prio0:M2DEC_AMD_PARSE_PRIO=0" "prio1s4:M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=8" "prio0s4:M2DEC_AMD_PARSE_PRIO=0,M2DEC_AMD_STREAMS=4,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_prio2_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_prio2_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_prio2_$TAG.txt ;;
   win)
-    timeout -k 10 900 python3 tools/ab_env.py 4 16 "w12:GPU_MAX_HW_QUEUES=8" "w0:M2DEC_AMD_PARSE_PRIO=0,GPU_MAX_HW_QUEUES=8" "w20:M2DEC_AMD_PARSE_PRIO=20,GPU_MAX_HW_QUEUES=8" "w8:M2DEC_AMD_PARSE_PRIO=8,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_win_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_win_$TAG.txt; exit 1; }
+    timeout -k 10 900 python3 tools/ab_env.py 4 16 "w20:GPU_MAX_HW_QUEUES=8" "w12:M2DEC_AMD_PARSE_PRIO=12,GPU_MAX_HW_QUEUES=8" "w32:M2DEC_AMD_PARSE_PRIO=32,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_win_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_win_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_win_$TAG.txt ;;
   tlq8)
     GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;

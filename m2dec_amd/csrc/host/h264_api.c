@@ -249,7 +249,7 @@ static int alloc_geometry(h264_dec_t *d, int w, int h)
 	d->mbi = (h264_mbinfo_t *)calloc((size_t)n, sizeof(h264_mbinfo_t));
 	for (int i = 0; i < 17; ++i) {
 		free(d->colpic[i].mb);
-		d->colpic[i].mb = (h264_colmb_t *)calloc((size_t)n, sizeof(h264_colmb_t));
+		d->colpic[i].mb = (h264_colmb_t *)calloc(H264_COL_ENTRIES(n), sizeof(h264_colmb_t));
 		memset(d->colpic[i].map_col_frameidx, 0, sizeof(d->colpic[i].map_col_frameidx));
 		if (!d->colpic[i].mb) return -1;
 	}

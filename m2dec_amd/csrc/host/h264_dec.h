@@ -180,8 +180,18 @@ typedef struct {
 
 typedef struct {
 	int8_t map_col_frameidx[16];
-	h264_colmb_t *mb;       /* [n_mbs] */
+	h264_colmb_t *mb;       /* [H264_COL_ENTRIES(n_mbs)] */
 } h264_colpic_t;
+
+/* A co-located store buffer holds one entry more than the picture has MBs: its first 4-aligned int is
+ * the progress word of the parse writing the buffer (h264_col_progress; row pipelining, h264_async.c):
+ * MBs stored so far, H264_COL_FINAL(n) once the picture parsed, -1 if its parse failed */
+#define H264_COL_ENTRIES(n) ((size_t)(n) + 1)
+#define H264_COL_FINAL(n) ((n) + 1)
+static inline int *h264_col_progress(h264_colmb_t *mb, int n_mbs)
+{
+	return (int *)(((uintptr_t)(mb + n_mbs) + 3) & ~(uintptr_t)3);
+}
 
 /* ---------------------------------------------------------------- per-MB neighbour state */
 enum {
@@ -349,6 +359,15 @@ struct h264_dec {
 	int parse_threads;       /* requested workers (m2dec_amd_h264_set_parse_threads / env) */
 	int par_first_mb;        /* slice-parallel parse: this slice's first MB; the MB-edge bS toward an MB
 	                            before it (an earlier slice, parsed concurrently) is left to h264_fix_bs */
+	/* row-pipelined co-located stores (h264_async.c "Co-located row pipelining"; worker contexts only):
+	 * col_pub: progress word this picture's parse publishes into as its MBs' co-located motion is stored;
+	 * col_sub: progress word of the picture whose store this B picture reads, still being parsed — direct
+	 * prediction of MB addr waits until it passes addr (col_sub_ok: MBs known stored; col_sub_fail: that
+	 * parse failed) */
+	int *col_pub;
+	const int *col_sub;
+	int col_sub_ok, col_sub_fail;
+	int col_pub_delay_us;    /* (tests: M2DEC_AMD_COL_PIPE_DELAY_US, a pause after each published MB row) */
 	/* 1: this is the pipeline's lookahead context: it runs the header-level state machine ahead of
 	 * the API-visible context, names pictures by virtual frame ids instead of frame slots (no DPB
 	 * output, no caller frames, no header callback) and creates the slice-data jobs */

@@ -12,6 +12,8 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sched.h>
+#include <unistd.h>
 #include "h264_dec.h"
 
 /* blkIdx -> 4x4 position (spec 6.4.3) and inverse */
@@ -660,10 +662,31 @@ static void spatial_ref_mv(slice_ctx_t *s)
 	s->direct_ready = 1;
 }
 
+/* the co-located MB of the current one is stored: wait for the parse writing it (row pipelining) */
+static void col_wait(slice_ctx_t *s)
+{
+	h264_dec_t *d = s->d;
+	for (int spins = 0;; ++spins) {
+		const int v = __atomic_load_n(d->col_sub, __ATOMIC_ACQUIRE);
+		if (v < 0) { /* that parse failed: this picture fails too (job_run) */
+			d->col_sub_fail = 1;
+			d->col_sub_ok = 1 << 30;
+			return;
+		}
+		if (v > s->addr) {
+			d->col_sub_ok = v;
+			return;
+		}
+		if (spins < 64) __builtin_ia32_pause();
+		else sched_yield(); /* (the writer may be waiting for a CPU) */
+	}
+}
+
 /* derive direct motion of 8x8 partition b8 into cur (pred_direct8x8_spatial_dec / temporal_direct_block) */
 static void direct_8x8(slice_ctx_t *s, int b8)
 {
 	h264_dec_t *d = s->d;
+	if (d->col_sub && s->addr >= d->col_sub_ok) col_wait(s);
 	h264_mbinfo_t *m = s->cur;
 	const h264_ref_t *l1 = &d->refs[1][0];
 	const h264_colmb_t *col = &d->colpic[l1->col].mb[s->addr];
@@ -1225,6 +1248,11 @@ static void store_col(slice_ctx_t *s)
 				col->mv[r][0] = m->mv[lx][r][0];
 				col->mv[r][1] = m->mv[lx][r][1];
 			}
+	}
+	/* (single-slice pictures store in raster order: MBs [0, addr] are stored) */
+	if (s->d->col_pub) {
+		__atomic_store_n(s->d->col_pub, s->addr + 1, __ATOMIC_RELEASE);
+		if (s->d->col_pub_delay_us && s->mbx == s->d->mb_w - 1) usleep((useconds_t)s->d->col_pub_delay_us);
 	}
 }
 

@@ -127,3 +127,51 @@ def test_slice_parallel_parse(built, monkeypatch, name):
         st = m2dec_amd.Stats()
         assert m2dec_amd.decode_stream(stream(name), backend=ob.be, parse_threads=6, stats=st) == want
     assert st.slice_par_pictures == 0
+
+
+_COL_CHILD = r"""
+import sys
+sys.path.insert(0, %r)
+import m2dec_amd
+from tests._oracle import OracleBackend
+from tests._streams import GOLDEN, stream
+with OracleBackend() as ob:
+    got = m2dec_amd.decode_stream(stream(%r), backend=ob.be, parse_threads=6)
+print('MD5OK', got == GOLDEN[%r]['md5'])
+"""
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("name", ["cov_cabac_s1", "cov_cabac_s2", "cov_wp_s1", "cov_reflists_s1"])
+def test_col_row_pipelining(built, tmp_path, name, pipe):
+    """Co-located row pipelining (h264_async.c deps_ready / job_run, h264_mb.c col_wait): a single-slice B
+    picture starts while the anchor whose co-located store it reads is still being parsed, its direct
+    prediction waiting per MB for the anchor's progress word.  The frames equal the goldens, and from the
+    host timeline some B picture's parse starts before its anchor's ends (never with
+    M2DEC_AMD_COL_PIPE=0)."""
+    import csv
+    import subprocess
+    import sys
+    tl = tmp_path / "tl.csv"
+    # (anchors pause 2 ms per MB row, so that readers are picked while they run, whatever the host's CPUs)
+    env = dict(os.environ, M2DEC_AMD_TIMELINE=str(tl), M2DEC_AMD_COL_PIPE=pipe, M2DEC_AMD_COL_PIPE_DELAY_US="2000")
+    out = subprocess.run([sys.executable, "-c", _COL_CHILD % (ROOT, name, name)], env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert "MD5OK True" in out.stdout, out.stdout + out.stderr[-2000:]
+    start, end, typ = {}, {}, {}
+    for r in csv.DictReader(open(tl)):
+        if r["kind"] == "P":
+            start[int(r["a"])], typ[int(r["a"])] = int(r["t_ns"]), int(r["b"])
+        elif r["kind"] == "p":
+            end[int(r["a"])] = int(r["t_ns"])
+    early = 0
+    for j in sorted(start):
+        if typ[j] != 1:
+            continue
+        anchors = [k for k in start if k < j and typ[k] != 1]  # (its col writer: the last anchor before it)
+        if anchors and start[j] < end[max(anchors)]:
+            early += 1
+    if pipe == "1":
+        assert early > 0
+    elif name != "cov_reflists_s1":  # (reordered lists: a B picture's anchor is not always the last one)
+        assert early == 0

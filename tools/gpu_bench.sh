@@ -18,5 +18,10 @@ rc=$?; echo "rocprof rc=$rc"; tail -2 $R/gpurun_out/prof_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_replay -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --replay-only > $R/gpurun_out/prof_${TAG}_replay.log 2>&1
 rc=$?; echo "rocprof replay rc=$rc"; tail -2 $R/gpurun_out/prof_${TAG}_replay.log
-find $R/gpurun_out/prof_$TAG $R/gpurun_out/prof_${TAG}_replay -name "*kernel_stats*"
+if [ $rc -ne 0 ]; then exit $rc; fi
+# every leg of the default bench (decode path, replay, H.265 I and P / B, MPEG-2): one summary naming
+# k_picture, k_batch, k_h265_mc / k_h265_ctu_rows / k_h265_deblock / k_h265_sao and k_m2v
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_${TAG}_all -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $R/gpurun_out/prof_${TAG}_all.log 2>&1
+rc=$?; echo "rocprof all rc=$rc"; tail -2 $R/gpurun_out/prof_${TAG}_all.log
+find $R/gpurun_out/prof_$TAG $R/gpurun_out/prof_${TAG}_replay $R/gpurun_out/prof_${TAG}_all -name "*kernel_stats*"
 exit $rc

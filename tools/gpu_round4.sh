@@ -62,6 +62,11 @@ for step in "$@"; do
   win)
     timeout -k 10 900 python3 tools/ab_env.py 4 16 "w20:GPU_MAX_HW_QUEUES=8" "w12:M2DEC_AMD_PARSE_PRIO=12,GPU_MAX_HW_QUEUES=8" "w32:M2DEC_AMD_PARSE_PRIO=32,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_win_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_win_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_win_$TAG.txt ;;
+  col)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py tests/test_gpu_batch.py tests/test_gpu_boundary.py > gpurun_out/pytest_col_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_col_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_col_$TAG.log
+    timeout -k 10 900 python3 tools/ab_env.py 4 16 "col1:GPU_MAX_HW_QUEUES=8" "col0:M2DEC_AMD_COL_PIPE=0,GPU_MAX_HW_QUEUES=8" "col1w0:M2DEC_AMD_PARSE_PRIO=0,GPU_MAX_HW_QUEUES=8" "col1w8:M2DEC_AMD_PARSE_PRIO=8,GPU_MAX_HW_QUEUES=8" > gpurun_out/ab_col_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_col_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_col_$TAG.txt ;;
   tlq8)
     GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
   gpu)

@@ -671,8 +671,12 @@ static void *pool_worker(void *arg)
 		} else {
 			const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
 			m2d_tl('P', j->seq, j->snap[0]->sh.slice_type);
-			if (dep_err) j->err = 1;
-			else if (!(as->slice_par && j->nsl > 1)) job_run(j);
+			if (dep_err) {
+				j->err = 1;
+				if (j->nsl == 1 && !j->nonref) /* (a reader may have started on this writer: release it) */
+					__atomic_store_n(h264_col_progress(j->snap[0]->colpic[j->col_store].mb, j->snap[0]->n_mbs), -1,
+					                 __ATOMIC_RELEASE);
+			} else if (!(as->slice_par && j->nsl > 1)) job_run(j);
 			else if (job_run_par(as, j) < 0) {
 				job_run(j);
 				__atomic_fetch_add(&as->n_par_fallback, 1, __ATOMIC_RELAXED);

@@ -328,9 +328,18 @@ struct InterRes {
  * LDS segment. */
 __device__ M2DEC_INTER_MB_ATTR void inter_mb(const int addr, const m2r_mb_t m, const m2r_inter_t &it,
                          const m2r_slice_t *__restrict__ slices, const int16_t *__restrict__ pool, uint8_t *frames,
-                         size_t fsz, int W, int H, int Wmb, uint8_t *seg, InterRes *res, const int lane, const int scnt = 0)
+                         size_t fsz, int W, int H, int Wmb, uint8_t *seg, InterRes *res, const int lane_in, const int scnt = 0)
 {
 	STAMPW(scnt, 0);
+	/* the lane index through an opaque copy: every per-lane address below is then computed inside the MB
+	 * loop of the caller instead of being hoisted out of it as loop invariants, which held ~60 VGPRs across
+	 * the loop and spilled them to scratch at the 128-VGPR budget */
+#ifndef M2DEC_NO_LANE_LAUNDER
+	int lane;
+	asm volatile("v_mov_b32 %0, %1" : "=v"(lane) : "v"(lane_in));
+#else
+	const int lane = lane_in; /* r99 and before: 740 B of scratch per lane, 63 scratch operations per MB */
+#endif
 	const int mbx = addr % Wmb, mby = addr / Wmb;
 	const m2r_slice_t *sl = &slices[m.slice];
 	const int CH = H >> 1;

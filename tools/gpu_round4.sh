@@ -69,6 +69,13 @@ for step in "$@"; do
     grep "^all" gpurun_out/ab_col_$TAG.txt ;;
   tlq8)
     GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
+  lane)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_batch.py > gpurun_out/pytest_lane_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_lane_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_lane_$TAG.log
+    V=hoist timeout -k 10 600 bash tools/ab_replay.sh lane_$TAG || exit 1
+    cat gpurun_out/ab_lane_$TAG.txt
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "lane1:GPU_MAX_HW_QUEUES=8" "hoist:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_LIB=$R/build/var/lib_hoist.so" > gpurun_out/ab_lane_e2e_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_lane_e2e_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_lane_e2e_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

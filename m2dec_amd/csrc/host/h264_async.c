@@ -76,8 +76,11 @@ static double now_s(void)
 
 typedef struct h264_job {
 	int nsl, capsl;
+	int nkeep;                /* snap / rbsp entries allocated (kept across pictures: no malloc, page
+	                             faults or heap trims on the lookahead's per-picture path) */
 	h264_dec_t **snap;        /* [nsl] lookahead context right after each slice header */
 	uint8_t **rbsp;           /* [nsl] slice RBSP copies (32 zero bytes of padding) */
+	size_t *rbsp_cap;         /* [nkeep] their capacities */
 	h264_mbinfo_t *mbi;       /* private neighbour state */
 	size_t mbi_n;
 	m2r_picture_t pic;        /* private record arena (frame ids are virtual until submission) */
@@ -240,10 +243,6 @@ static int job_arena(h264_job_t *j, int wm, int hm, int pinned)
 
 static void job_clear(h264_job_t *j)
 {
-	for (int i = 0; i < j->nsl; ++i) {
-		free(j->snap[i]);
-		free(j->rbsp[i]);
-	}
 	j->nsl = 0;
 	j->ndeps = 0;
 	j->taken = 0;
@@ -259,8 +258,13 @@ static void job_free(h264_job_t *j)
 {
 	if (!j) return;
 	job_clear(j);
+	for (int i = 0; i < j->nkeep; ++i) {
+		free(j->snap[i]);
+		free(j->rbsp[i]);
+	}
 	free(j->snap);
 	free(j->rbsp);
+	free(j->rbsp_cap);
 	free(j->mbi);
 	free(j->priv_col);
 	for (int i = 0; i < j->capsw; ++i) free(j->sw[i]);
@@ -1412,17 +1416,32 @@ int h264_async_add_slice(h264_dec_t *la)
 		r = (uint8_t **)realloc(j->rbsp, sizeof(*r) * (size_t)cap);
 		if (!r) return -1;
 		j->rbsp = r;
+		{
+			size_t *c = (size_t *)realloc(j->rbsp_cap, sizeof(*c) * (size_t)cap);
+			if (!c) return -1;
+			j->rbsp_cap = c;
+		}
 		j->capsl = cap;
 	}
 	{
 		const size_t len = (size_t)(la->slice_rbsp_end - la->slice_rbsp);
-		h264_dec_t *snap = (h264_dec_t *)malloc(sizeof(h264_dec_t));
-		uint8_t *rb = (uint8_t *)malloc(len + 32);
-		if (!snap || !rb) {
-			free(snap);
-			free(rb);
-			return -1;
+		const int k = j->nsl;
+		if (k == j->nkeep) { /* a new entry (kept with the job from then on) */
+			j->snap[k] = (h264_dec_t *)malloc(sizeof(h264_dec_t));
+			j->rbsp[k] = NULL;
+			j->rbsp_cap[k] = 0;
+			if (!j->snap[k]) return -1;
+			j->nkeep++;
 		}
+		if (j->rbsp_cap[k] < len + 32) {
+			const size_t cap = (len + 32) + (len + 32) / 4; /* room for the next pictures' sizes */
+			free(j->rbsp[k]);
+			j->rbsp[k] = (uint8_t *)malloc(cap);
+			j->rbsp_cap[k] = j->rbsp[k] ? cap : 0;
+			if (!j->rbsp[k]) return -1;
+		}
+		h264_dec_t *snap = j->snap[k];
+		uint8_t *rb = j->rbsp[k];
 		memcpy(snap, la, sizeof(*snap));
 		memcpy(rb, la->slice_rbsp, len);
 		memset(rb + len, 0, 32);

@@ -76,6 +76,9 @@ for step in "$@"; do
     cat gpurun_out/ab_lane_$TAG.txt
     timeout -k 10 900 python3 tools/ab_env.py 4 12 "lane1:GPU_MAX_HW_QUEUES=8" "hoist:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_LIB=$R/build/var/lib_hoist.so" > gpurun_out/ab_lane_e2e_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_lane_e2e_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_lane_e2e_$TAG.txt ;;
+  sab)
+    timeout -k 10 900 python3 tools/ab_streams.py 2 3 "def:GPU_MAX_HW_QUEUES=8" "col0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_COL_PIPE=0" "s3:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=3" "tail0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_MD5_TAIL=0" "prio0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_PARSE_PRIO=0" "ext0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_EXTERNAL=0" "crew0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_COPY_CREW=0" "hold0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_HOLD=0" > gpurun_out/ab_streams8_$TAG.txt 2>&1 || { tail -20 gpurun_out/ab_streams8_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_streams8_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -279,8 +279,11 @@ static void job_free(h264_job_t *j)
 /* Jobs (each with a record arena of ~1 KB per MB) outlive a pipeline: a context's jobs go back to a
  * process-wide pool when it stops or reaches the end of its stream, and the next context takes them —
  * no allocation or page faults while decoding, no frees when a context goes.  Mutex: g_parse.mu. */
-#define JOB_POOL_MAX 96
+#define JOB_POOL_MAX 320 /* r101: 96 freed most of eight concurrent streams' jobs at every stream end, and the
+                            * next streams pinned their arenas again (hipHostMalloc, ~2 ms each, on the
+                            * lookahead's thread): 8 streams 1000 fps, 1490 with unpinned arenas */
 static h264_job_t *g_jobs[JOB_POOL_MAX];
+static long g_jobs_new; /* jobs created (each pins its arena on first use): M2DEC_AMD_ASYNC_STATS */
 static int g_njobs;
 
 static void job_release(h264_job_t *j) /* (mutex held) */
@@ -887,9 +890,9 @@ void h264_async_stop(h264_dec_t *d)
 	if (as->stats)
 		fprintf(stderr, "async: %ld jobs, depth %d; caller: lookahead %.3f s (col-store waits %.3f s, slice copies "
 		                "%.3f s), oldest-done waits %.3f s, record copies %.3f s, back-end submit %.3f s; workers "
-		                "parse %.3f s\n",
+		                "parse %.3f s; jobs created so far in the process %ld\n",
 		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
-		        as->t_parse);
+		        as->t_parse, g_jobs_new);
 	/* no pool worker starts anything of this pipeline any more; wait for the ones inside it */
 	pthread_mutex_lock(as->mu);
 	as->quit = 1;
@@ -966,6 +969,7 @@ static h264_job_t *job_get(struct h264_async *as)
 	if (g_njobs) return g_jobs[--g_njobs];
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
+	g_jobs_new++;
 	j->slot = -1;
 	j->w = (h264_dec_t *)malloc(sizeof(h264_dec_t));
 	if (!j->w) {

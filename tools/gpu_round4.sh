@@ -79,6 +79,14 @@ for step in "$@"; do
   sab)
     timeout -k 10 900 python3 tools/ab_streams.py 2 3 "def:GPU_MAX_HW_QUEUES=8" "col0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_COL_PIPE=0" "s3:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=3" "tail0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_MD5_TAIL=0" "prio0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_PARSE_PRIO=0" "ext0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_EXTERNAL=0" "crew0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_COPY_CREW=0" "hold0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_HOLD=0" > gpurun_out/ab_streams8_$TAG.txt 2>&1 || { tail -20 gpurun_out/ab_streams8_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_streams8_$TAG.txt ;;
+  dp)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py tests/test_gpu_boundary.py tests/test_gpu_f1.py > gpurun_out/pytest_dp_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_dp_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_dp_$TAG.log
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "s4:GPU_MAX_HW_QUEUES=8" "s5:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=5" "s6i64:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=6,M2DEC_AMD_INTER_WG=64" "s4i64:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_INTER_WG=64" > gpurun_out/ab_dp_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_dp_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_dp_$TAG.txt ;;
+  pb)
+    bash tools/pb_ab3.sh > gpurun_out/pb_ab3_$TAG.txt 2>&1 || exit 1
+    cat gpurun_out/pb_ab3_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -2269,12 +2269,18 @@ __global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_batch(const PictureAr
 	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
 }
 
-/* the decode path's launch (up to BMAX pictures per launch, h264d_func): the same blocks as k_batch under
- * its own name, so that rocprofv3 reports the decode path and the trace replay separately */
-__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_picture(const PictureArgs *pics, int bpp)
+/* the decode path's launch (up to BMAX pictures per launch, h264d_func): the blocks of k_batch that have
+ * work, under its own name so that rocprofv3 reports the decode path and the trace replay separately.
+ * Picture p owns blocks [blk0, blk0 + nblk) (increasing in p); a picture without inter MBs starts at its
+ * row workgroups (no idle inter workers holding workgroup slots of the device-wide budget), a P / B
+ * picture has only its row_wgs row workgroups. */
+__global__ __launch_bounds__(256, M2DEC_MIN_BLOCKS) void k_picture(const PictureArgs *pics, int n)
 {
-	const int p = blockIdx.x / bpp;
-	picture_block(pics[p], blockIdx.x - p * bpp, g_lds);
+	int p = 0;
+	while (p + 1 < n && (int)blockIdx.x >= pics[p + 1].blk0) ++p;
+	const PictureArgs &a = pics[p];
+	const int b = (int)blockIdx.x - a.blk0;
+	picture_block(a, a.n_inter ? b : b + a.inter_workers, g_lds);
 }
 
 size_t m2r_deblock_lds_bytes(int W, int Wmb)

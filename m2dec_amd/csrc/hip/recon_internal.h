@@ -81,14 +81,24 @@ struct PictureArgs {
 	int war[WAR_MAX]; /* ... (their inter workers must be done) */
 	int war_writer;   /* the batch picture that wrote the previous content (its rows must be done), or -1 */
 	uint8_t *capture; /* verification only: the finished frame is copied here before the slot is released */
+	/* decode-path launches (k_picture): the picture's workgroups [blk0, blk0 + nblk) of the launch — a
+	 * picture without inter MBs has no inter workers, a P / B picture only its row_wgs row workgroups */
+	int blk0, nblk;
 };
 
 /* a batch of pictures in decode order, picture p owning blocks [p * bpp, (p + 1) * bpp) */
 __global__ void k_batch(const PictureArgs *pics, int bpp);
-__global__ void k_picture(const PictureArgs *pics, int bpp);
+__global__ void k_picture(const PictureArgs *pics, int n);
 
-/* workgroups of one picture: persistent inter workers + one per pair of MB rows */
+/* workgroups of one picture in a k_batch launch: persistent inter workers + one per pair of MB rows */
 static inline int picture_blocks(int inter_workers, int Hmb) { return inter_workers + (Hmb + 1) / 2; }
+/* workgroups of one picture in a k_picture launch: only those with work (an I picture: its row pairs; a P / B
+ * picture: its inter workers and row_wgs row workgroups) */
+static inline int picture_blocks_dp(int inter_workers, int row_wgs, int Hmb, bool has_inter)
+{
+	const int pairs = (Hmb + 1) / 2;
+	return has_inter ? inter_workers + (row_wgs < pairs ? row_wgs : pairs) : pairs;
+}
 
 /* dynamic LDS bytes of one k_deblock workgroup for a W-sample-wide picture */
 size_t m2r_deblock_lds_bytes(int W, int Wmb);

@@ -63,6 +63,9 @@ static int nstreams()
 	if (!n) {
 		const char *e = getenv("M2DEC_AMD_STREAMS");
 		const char *q = getenv("GPU_MAX_HW_QUEUES");
+		/* one hardware queue per launch stream + one for the copy stream: 4 launch streams from 5 queues (with
+		 * the per-picture grids 5 and 6 streams fit the budget too: A/Bs r104 / r105 within noise, 30.1-32.3
+		 * ms per c3 decode for 4, 5 and 6) */
 		int v = e ? atoi(e) : (q && atoi(q) >= 5 ? 4 : 3);
 		n = v < 1 ? 1 : (v > NSTREAMS ? NSTREAMS : v);
 	}
@@ -395,7 +398,7 @@ struct Sched {
 			if (!bg.cap || cap < bg.cap) bg.cap = cap; /* contexts of several picture sizes: the smallest */
 			/* pictures per launch such that a launch on each stream fits the budget at once: a reserve
 			 * that has to wait would stall the thread driving the pipeline (a parse worker) */
-			pics_fit = std::max(1, std::min(BMAX, bg.cap / (nstreams() * picture_blocks(inter_grid, Hmb))));
+			pics_fit = std::max(1, std::min(BMAX, bg.cap / (nstreams() * picture_blocks_dp(inter_grid, row_wgs, Hmb, true))));
 			if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "k_picture: %d workgroups resident (%d per CU)\n", bg.cap, per_cu);
 		}
 		return 0;
@@ -531,18 +534,23 @@ struct Sched {
 			tm.deblock_launches++;
 		}
 		hoist_intra(ha, n);
+		int nb = 0; /* the launch's workgroups: each picture's own (picture_blocks_dp), in dispatch order */
+		for (int p = 0; p < n; ++p) {
+			ha[p].blk0 = nb;
+			ha[p].nblk = picture_blocks_dp(inter_grid, row_wgs, Hmb, ha[p].n_inter != 0);
+			nb += ha[p].nblk;
+		}
 		CHECK(hipMemsetAsync(words, 0, sizeof(int) * (2 * BMAX + (size_t)n * SCR_WORDS(Hmb, Wmb)), s));
 		/* the arguments go to device memory (pageable source: staged by the copy call) */
 		CHECK(hipMemcpyAsync(pargs + (size_t)k * BMAX, ha, sizeof(PictureArgs) * n, hipMemcpyHostToDevice, s));
 		{
 			/* the device-wide workgroup budget (SlotBudget): reserve, launch, register the release */
 			SlotBudget &bg = g_budget[dev & 15];
-			const int nb = picture_blocks(inter_grid, Hmb);
 			hipEvent_t done = bg.event();
 			if (!done) return -1;
-			const int held = bg.reserve(nb * n);
-			hipLaunchKernelGGL(k_picture, dim3(nb * n), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
-			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), nb);
+			const int held = bg.reserve(nb);
+			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
+			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), n);
 			if (hipGetLastError() != hipSuccess || hipEventRecord(done, s) != hipSuccess) {
 				bg.cancel(held);
 				fprintf(stderr, "m2dec_amd: k_picture launch failed\n");

@@ -87,6 +87,11 @@ for step in "$@"; do
   pb)
     bash tools/pb_ab3.sh > gpurun_out/pb_ab3_$TAG.txt 2>&1 || exit 1
     cat gpurun_out/pb_ab3_$TAG.txt ;;
+  s5)
+    timeout -k 10 120 tools/_build/ipprof tools/_build/c3.264 3 bm > gpurun_out/ipprof_bm_$TAG.txt 2> gpurun_out/ipprof_bm_$TAG.err || exit 1
+    timeout -k 10 900 python3 tools/ab_env.py 5 12 "s5:GPU_MAX_HW_QUEUES=8" "s4:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=4" "s6:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=6" > gpurun_out/ab_s5_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_s5_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_s5_$TAG.txt
+    GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

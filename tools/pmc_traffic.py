@@ -59,12 +59,19 @@ def main():
     if "read_bytes" in out and "write_bytes" in out:
         out["traffic_bytes"] = out["read_bytes"] + out["write_bytes"]
     if KERNEL == "k_picture" and fetch and write and all("_grid" in v for v in fetch + write):
-        # the decode path launches 1..4 pictures at once: bytes per picture (sum over launches / pictures;
-        # a 1080p picture is 80 inter workers + 34 row-pair workgroups of 256 lanes), which bench.py scales
-        # by its own pictures per launch
-        bpp = 256 * (80 + 34)
-        pics_f = sum(v["_grid"] for v in fetch) / bpp
-        pics_w = sum(v["_grid"] for v in write) / bpp
+        # the decode path launches 1..4 pictures at once: bytes per picture (sum over launches / pictures),
+        # which bench.py scales by its own pictures per launch.  A 1080p picture is 34 row-pair workgroups of
+        # 256 lanes without inter MBs, else 80 inter workers + 12 row workgroups (runtime.hip
+        # picture_blocks_dp): a launch's grid names its picture counts uniquely
+        def pics_of(grid):
+            g = int(round(grid / 256))
+            for n in range(1, 5):
+                for i in range(n + 1):
+                    if 34 * i + 92 * (n - i) == g:
+                        return n
+            return g / 92.0
+        pics_f = sum(pics_of(v["_grid"]) for v in fetch)
+        pics_w = sum(pics_of(v["_grid"]) for v in write)
         out["traffic_bytes_per_picture"] = int(2 * 1024 * sum(v["FETCH_SIZE"] for v in fetch) / max(1.0, pics_f) +
                                               1024 * sum(v["WRITE_SIZE"] for v in write) / max(1.0, pics_w))
         out["pictures_per_launch"] = round(pics_f / len(fetch), 3)

@@ -1877,6 +1877,9 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 		const int seg_l = (t & 15) >> 2, seg_c = cl >> 1;
 		const int seg = luma ? seg_l : seg_c;
 		uint8_t *const sink = dummy + t;
+		/* bit offset of v[i] in its dword for the vertical edges, by i & 3: luma byte i & 3; chroma (Cb / Cr
+		 * interleaved) byte 2 (i & 1) + comp */
+		const int vsh[4] = {luma ? 0 : 8 * comp, luma ? 8 : 16 + 8 * comp, luma ? 16 : 8 * comp, luma ? 24 : 16 + 8 * comp};
 		unsigned spins = 0;
 		/* the last values seen of the loader's and row A's words: a word is polled again only when the value
 		 * seen does not cover this MB (the acquire that returned it still orders the reads below) */
@@ -1924,6 +1927,28 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 					/* branch-free sample access: a masked-off sample goes to the lane's dummy byte (an
 					 * exec-masked load/store per sample would cost a branch each) */
 					int v[20];
+#ifndef M2DEC_DBK_BYTE_V
+					if (dir == 0) {
+						/* vertical edges: the line's 20 bytes from 4 left of the MB are 5 aligned dwords of the
+						 * ring line (a chroma line's samples are every other byte of the first 4: v[2..5] /
+						 * v[10..13] sit in the same dwords as the luma lanes' bytes 2..5 / 10..13) */
+						uint32_t dw[5];
+#pragma unroll
+						for (int k = 0; k < 5; ++k) dw[k] = *(const uint32_t *)(lb + ((base - 4 + 4 * k) & M));
+#pragma unroll
+						for (int i = 0; i < 20; ++i) v[i] = (int)__builtin_amdgcn_ubfe(dw[i >> 2], (uint32_t)vsh[i & 3], 8);
+					} else
+#endif
+#ifndef M2DEC_DBK_BYTE_H
+					if (dir == 1) {
+						/* horizontal edges: one byte per line at a fixed stride, so every load is an immediate
+						 * offset from one of two per-lane bases (a chroma lane's v[2..5] / v[10..13] are its
+						 * samples 0..3 / 4..7; its other v[] read in-bounds bytes it never uses) */
+						const uint8_t *const blo = luma ? lb : lb - 2 * S, *const bhi = luma ? lb : lb - 6 * S;
+#pragma unroll
+						for (int i = 0; i < 20; ++i) v[i] = (i < 6 ? blo : bhi)[i * S];
+					} else
+#endif
 #pragma unroll
 					for (int i = 0; i < 20; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6; /* chroma sample index for v[i] */
@@ -1979,6 +2004,40 @@ __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const
 					/* write back; at x == 0 the 4 columns left of the MB wrap onto a slot the loader may
 					 * be filling, and edge 0 is off there anyway */
 					const int i0 = (dir == 0 && x == 0) ? 4 : 1;
+#ifndef M2DEC_DBK_BYTE_V
+					if (dir == 0) {
+						/* luma lines back as dwords (bytes 0 and 19 are p3 / q3, never changed); chroma lanes
+						 * share dwords between Cb and Cr, so their 8 samples stay byte stores */
+						if (luma) {
+#pragma unroll
+							for (int k = (x == 0 ? 1 : 0); k < 5; ++k)
+								*(uint32_t *)(lb + ((base - 4 + 4 * k) & M)) =
+								    (uint32_t)v[4 * k] | ((uint32_t)v[4 * k + 1] << 8) | ((uint32_t)v[4 * k + 2] << 16) | ((uint32_t)v[4 * k + 3] << 24);
+						} else if (active) {
+							/* (ring columns wrap at every 16th MB: c0 is negative there) */
+#pragma unroll
+							for (int i = 2; i < 14; ++i) {
+								if (i > 5 && i < 10) continue;
+								const int ci = (i < 6) ? i - 2 : i - 6;
+								if (i >= i0) *DBK_ADDR(ci) = (uint8_t)v[i];
+							}
+						}
+					} else
+#endif
+#ifndef M2DEC_DBK_BYTE_H
+					if (dir == 1) {
+						if (luma) {
+#pragma unroll
+							for (int i = 1; i < 19; ++i) lb[i * S] = (uint8_t)v[i];
+						} else if (active) {
+#pragma unroll
+							for (int i = 2; i < 14; ++i) {
+								if (i > 5 && i < 10) continue;
+								lb[((i < 6) ? i - 2 : i - 6) * S] = (uint8_t)v[i];
+							}
+						}
+					} else
+#endif
 #pragma unroll
 					for (int i = 1; i < 19; ++i) {
 						const int ci = (i < 6) ? i - 2 : i - 6;

@@ -92,6 +92,16 @@ for step in "$@"; do
     timeout -k 10 900 python3 tools/ab_env.py 5 12 "s5:GPU_MAX_HW_QUEUES=8" "s4:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=4" "s6:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=6" > gpurun_out/ab_s5_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_s5_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_s5_$TAG.txt
     GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
+  dbk)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_batch.py tests/test_gpu_f1.py > gpurun_out/pytest_dbk_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_dbk_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_dbk_$TAG.log
+    V=dbkbyte timeout -k 10 600 bash tools/ab_replay.sh dbk_$TAG || exit 1
+    cat gpurun_out/ab_dbk_$TAG.txt
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "dw:GPU_MAX_HW_QUEUES=8" "byte:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_LIB=$R/build/var/lib_dbkbyte.so" > gpurun_out/ab_dbk_e2e_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_dbk_e2e_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_dbk_e2e_$TAG.txt ;;
+  iw)
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "i80:GPU_MAX_HW_QUEUES=8" "i160:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_INTER_WG=160" "i120r17:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_INTER_WG=120,M2DEC_AMD_ROW_WG=17" "i80r17:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_ROW_WG=17" > gpurun_out/ab_iw_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_iw_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_iw_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

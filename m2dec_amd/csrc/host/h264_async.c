@@ -343,7 +343,7 @@ static void job_run(h264_job_t *j)
 static void job_run_slices(h264_job_t *j)
 {
 	h264_dec_t *w = j->w;
-	int mbs = 0, slice_num = 0, slice_rec = 0, last_firstline = 0, ret = 0;
+	int mbs = 0, coded = 0, slice_num = 0, slice_rec = 0, last_firstline = 0, ret = 0;
 	w->par_first_mb = 0;
 	int8_t idc[1024], alpha[1024], beta[1024];
 	const int n = j->snap[0]->n_mbs;
@@ -371,6 +371,7 @@ static void job_run_slices(h264_job_t *j)
 		w->pic = &j->pic;
 		if (j->nonref) w->colpic[w->curr_col].mb = j->priv_col;
 		w->mbs_decoded = mbs;
+		w->mbs_coded = coded;
 		w->slice_num = slice_num;
 		w->slice_rec = slice_rec;
 		w->last_firstline = last_firstline;
@@ -388,6 +389,7 @@ static void job_run_slices(h264_job_t *j)
 			return;
 		}
 		mbs = w->mbs_decoded;
+		coded = w->mbs_coded;
 		slice_rec = w->slice_rec;
 		last_firstline = w->last_firstline;
 		memcpy(idc + slice_num, w->slice_idc + slice_num, (size_t)(w->slice_num - slice_num));

@@ -323,6 +323,8 @@ struct h264_dec {
 	/* picture geometry / state */
 	int mb_w, mb_h, n_mbs;
 	int mbs_decoded;
+	int mbs_coded;          /* distinct MBs of the picture coded so far (mbs_decoded counts an MB of
+	                           overlapping slices twice) */
 	int slice_num;
 	int in_picture;
 	int last_firstline;      /* picture-final `firstline` (deblock idc 2 quirk) */

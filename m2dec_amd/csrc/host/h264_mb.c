@@ -1311,6 +1311,7 @@ static void init_mb(slice_ctx_t *s)
 	memset(s->rec, 0, sizeof(*s->rec));
 	s->rec->coef = (uint32_t)(s->coef - d->pic->coef);
 	s->direct_ready = 0;
+	d->mbs_coded += m->slice < 0;
 	m->slice = (int16_t)d->slice_num;
 	m->skip = 0;
 	m->t8x8 = 0;
@@ -1702,7 +1703,11 @@ int h264_slice_data(h264_dec_t *d)
 		cabac_start(&d->cabac, d->cabac_start, d->slice_rbsp_end);
 	}
 
+	/* every MB record / coefficient / motion slot of the picture arena is sized for n_mbs MBs: slices that
+	 * overlap (a damaged stream) would decode more than that and run past it; the picture is an error */
+#define MB_ROOM() do { if (d->mbs_decoded + d->par_first_mb >= d->n_mbs) return -1; } while (0)
 	for (;;) {
+		MB_ROOM();
 		if (s.slice_type != 2) {
 			if (s.cabac) {
 				init_mb(&s);
@@ -1719,6 +1724,7 @@ int h264_slice_data(h264_dec_t *d)
 				int more;
 				if (run > (uint32_t)(d->n_mbs - s.addr)) run = (uint32_t)(d->n_mbs - s.addr);
 				while (run--) {
+					MB_ROOM();
 					init_mb(&s);
 					decode_skip(&s);
 					d->mbs_decoded++;
@@ -1727,6 +1733,7 @@ int h264_slice_data(h264_dec_t *d)
 				}
 				more = hb_pos(&d->bs, d->slice_rbsp) < d->slice_rbsp_bits;
 				if (!more) break;
+				MB_ROOM();
 				init_mb(&s);
 			}
 		} else {
@@ -1744,8 +1751,14 @@ int h264_slice_data(h264_dec_t *d)
 		}
 		next_mb(&s);
 	}
+#undef MB_ROOM
 out:
 	d->pic->n_coef = (int32_t)(s.coef - d->pic->coef);
+	/* a damaged stream's slices can reach the picture's last MB with MBs of it never coded (a slice header
+	 * jumping ahead, overlapping slices): their records would be another picture's, whose coefficient /
+	 * motion offsets this picture's pools do not hold.  Such a picture is an error, not a frame.  (A
+	 * slice-parallel slice, par_first_mb > 0, counts only its own range; job_run_par checks the tiling.) */
+	if (ret == 1 && d->par_first_mb == 0 && d->mbs_coded != d->n_mbs) ret = -1;
 	/* picture-final firstline: value during the last MB of the picture (increment_mb_pos) */
 	if (ret == 1) {
 		int k = s.addr - first_in_slice; /* index of the last MB inside its slice */

@@ -1009,6 +1009,7 @@ int h264_picture_begin(h264_dec_t *d)
 	for (int i = 0; i < 4; ++i) f->crop[i] = (int16_t)s->crop[i];
 	f->cnt = d->sh.poc;
 	d->mbs_decoded = 0;
+	d->mbs_coded = 0;
 	d->slice_num = 0;
 	d->in_picture = 1;
 	if (d->as) { /* parse-ahead: the job owns MB info and records (h264_async.c) */

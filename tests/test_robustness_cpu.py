@@ -81,6 +81,31 @@ H265 = MUTATE + textwrap.dedent("""
     print("decoded", done)
 """)
 
+# multi-slice pictures whose damaged slice headers overlap or skip MBs: the sequential parse (after the
+# slice-parallel one refused the tiling) decoded more MBs than the picture arena holds and overflowed its
+# coefficient pool (heap corruption), or reached the last MB with MBs of the picture never coded and
+# submitted their stale records (an out-of-range coefficient offset).  These seeds hit both before the
+# fix (h264_slice_data: MB_ROOM, mbs_coded); each variant is decoded several times with 2 and 4 workers.
+H264_SLICES = MUTATE + textwrap.dedent("""
+    import sys
+    sys.path.insert(0, ROOT)
+    import m2dec_amd
+    from tests._oracle import OracleBackend
+    from tests._streams import stream
+    done = 0
+    data = stream("cov_slices_s1")
+    for seed, idx in [(1000, 11), (1001, 7), (2000, 11), (2010, 4), (3000, 0), (3012, 4), (4002, 4)]:
+        d = variants(data, seed, 12)[idx]
+        for threads in (2, 4, 2, 4):
+            with OracleBackend() as ob:
+                try:
+                    m2dec_amd.decode_stream(d, backend=ob.be, parse_threads=threads)
+                except RuntimeError:
+                    pass
+            done += 1
+    print("decoded", done)
+""")
+
 M2V = MUTATE + textwrap.dedent("""
     import sys
     sys.path.insert(0, ROOT)
@@ -106,6 +131,13 @@ def test_damaged_streams_do_not_crash(built, codec, script):
                        env=env, cwd=ROOT)
     assert r.returncode == 0, (codec, r.returncode, r.stderr.decode()[-3000:])
     assert b"decoded 36" in r.stdout, r.stdout.decode()[-500:]
+
+
+def test_damaged_slices_overlapping(built):
+    r = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + H264_SLICES], capture_output=True, timeout=600,
+                       cwd=ROOT)
+    assert r.returncode == 0, (r.returncode, r.stderr.decode()[-3000:])
+    assert b"decoded 28" in r.stdout, r.stdout.decode()[-500:]
 
 
 H265_RPS_CHAIN = textwrap.dedent("""

@@ -1,6 +1,7 @@
 """Interleaved A/B of environment configurations on the c3 end-to-end decode (median decode interval of N
 decodes per run, every decode bit-exact).  Usage: python3 tools/ab_env.py ROUNDS N 'NAME:K=V,K=V' ...
-(each configuration runs in its own process: GPU_MAX_HW_QUEUES etc. are read when HIP starts)."""
+(each configuration runs in its own process: GPU_MAX_HW_QUEUES etc. are read when HIP starts).
+AB_STREAM=<golden name> picks another stream (default c3_1080p_s1)."""
 import json
 import os
 import subprocess
@@ -12,12 +13,13 @@ import os, sys, statistics
 sys.path.insert(0, %r)
 import m2dec_amd
 from tests._streams import stream, GOLDEN
-d = stream('c3_1080p_s1')
+NAME = os.environ.get('AB_STREAM', 'c3_1080p_s1')
+d = stream(NAME)
 ts = []
 for i in range(%d + 2):
     st = m2dec_amd.Stats()
     md5 = m2dec_amd.decode_stream_md5(d, device=0, stats=st)
-    assert md5 == GOLDEN['c3_1080p_s1']['md5']
+    assert md5 == GOLDEN[NAME]['md5']
     if i >= 2:
         ts.append(1e3 * (st.t_end - st.t_start))
 print('RESULT', statistics.median(ts), min(ts))

@@ -102,6 +102,9 @@ for step in "$@"; do
   iw)
     timeout -k 10 900 python3 tools/ab_env.py 4 12 "i80:GPU_MAX_HW_QUEUES=8" "i160:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_INTER_WG=160" "i120r17:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_INTER_WG=120,M2DEC_AMD_ROW_WG=17" "i80r17:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_ROW_WG=17" > gpurun_out/ab_iw_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_iw_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_iw_$TAG.txt ;;
+  c5)
+    AB_STREAM=c5_4k_s1 timeout -k 10 900 python3 tools/ab_env.py 4 8 "def:GPU_MAX_HW_QUEUES=8" "p1:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_PICS_PER_LAUNCH=1" "s3:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=3" > gpurun_out/ab_c5_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_c5_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_c5_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

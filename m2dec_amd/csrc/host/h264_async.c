@@ -61,6 +61,7 @@
 #include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <unistd.h>
 #include <string.h>
 #include <time.h>
 #include "h264_dec.h"
@@ -99,6 +100,8 @@ typedef struct h264_job {
 	long col_dep;             /* seq of the job writing the co-located store this (single-slice B) picture
 	                             reads, if it may start while that one is still parsing (-1: no) */
 	int col_early;            /* started so: direct prediction waits for the writer's rows (job_run) */
+	uint64_t refmask;         /* virtual ids any slice of the picture may read (every in-use entry of its
+	                             reference lists, known at dispatch: pipe_drive's early submission) */
 	int nonref;               /* no slice has nal_ref_idc: its co-located store is never read ... */
 	h264_colmb_t *priv_col;   /* ... so it writes this private one (no ordering against other jobs) */
 	size_t priv_n;
@@ -175,6 +178,7 @@ struct h264_async {
 	int npar;
 	int slice_par;            /* M2DEC_AMD_SLICE_PAR (default 1): slices of a picture on several workers */
 	long n_par, n_par_fallback; /* pictures parsed slice-parallel / re-parsed sequentially after a try */
+	long n_early;             /* reference pictures submitted ahead of older jobs (early_ok) */
 };
 
 /* The parse pool: one set of worker threads per process, shared by every decoder's pipeline (a
@@ -195,6 +199,8 @@ static struct {
 
 static void pipe_drive(struct h264_async *as);
 static int g_col_pipe = 1; /* M2DEC_AMD_COL_PIPE: co-located row pipelining (deps_ready) */
+static int g_early = 1;    /* M2DEC_AMD_EARLY: parsed reference pictures submitted ahead of older B pictures */
+static int g_nonref_delay_us; /* M2DEC_AMD_NONREF_DELAY_US (tests): non-reference pictures finish late */
 static int g_col_delay_us; /* M2DEC_AMD_COL_PIPE_DELAY_US (tests: anchors slowed down, readers start early) */
 static int job_ext_idle(struct h264_async *as, h264_job_t *j, int wait);
 
@@ -693,6 +699,7 @@ static void *pool_worker(void *arg)
 				__atomic_fetch_add(&as->n_par, 1, __ATOMIC_RELAXED);
 			}
 			if (!j->err) pic_refs(&j->pic);
+			if (g_nonref_delay_us && j->nonref) usleep((useconds_t)g_nonref_delay_us);
 			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
 			m2d_tl('p', j->seq, j->snap[0]->sh.slice_type);
@@ -739,6 +746,8 @@ static int pool_grow(int n)
 	if (g_parse.nth == 0 && n > 0) {
 		const char *c = getenv("M2DEC_AMD_COL_PIPE");
 		if (c) g_col_pipe = atoi(c) != 0;
+		if (getenv("M2DEC_AMD_EARLY")) g_early = atoi(getenv("M2DEC_AMD_EARLY")) != 0;
+		if (getenv("M2DEC_AMD_NONREF_DELAY_US")) g_nonref_delay_us = atoi(getenv("M2DEC_AMD_NONREF_DELAY_US"));
 		if (getenv("M2DEC_AMD_COL_PIPE_DELAY_US")) g_col_delay_us = atoi(getenv("M2DEC_AMD_COL_PIPE_DELAY_US"));
 		const char *e = getenv("M2DEC_AMD_PARSE_PRIO");
 		if (e) g_parse_prio = atoi(e) < 0 ? 0 : atoi(e);
@@ -892,9 +901,9 @@ void h264_async_stop(h264_dec_t *d)
 	if (as->stats)
 		fprintf(stderr, "async: %ld jobs, depth %d; caller: lookahead %.3f s (col-store waits %.3f s, slice copies "
 		                "%.3f s), oldest-done waits %.3f s, record copies %.3f s, back-end submit %.3f s; workers "
-		                "parse %.3f s; jobs created so far in the process %ld\n",
+		                "parse %.3f s; jobs created so far in the process %ld; early submissions %ld\n",
 		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
-		        as->t_parse, g_jobs_new);
+		        as->t_parse, g_jobs_new, as->n_early);
 	/* no pool worker starts anything of this pipeline any more; wait for the ones inside it */
 	pthread_mutex_lock(as->mu);
 	as->quit = 1;
@@ -1110,6 +1119,36 @@ static int ahead_ok(const struct h264_async *as, const h264_job_t *j)
 	return 1;
 }
 
+/* Early submission (M2DEC_AMD_EARLY).  Submission is in decode order, and the pool finishes the
+ * reference pictures (I / P) well before the B pictures decoded before them (anchors first in pick_job,
+ * B pictures are longer): the r105 timeline had the stream's last anchors parsed at 15-17 ms but submitted
+ * at 21-23 ms behind their B pictures, so the device ran the anchor chain P52 -> P55 -> P58 after the
+ * parse had ended.  A parsed reference picture j may go to the back end before older unsubmitted jobs
+ * when (mutex held):
+ *   - ahead_ok: no header callback pending before it, the previous picture of its virtual buffer bound;
+ *   - RAW: the newest job before it writing each buffer it may read (refmask) was submitted;
+ *   - WAR: no older unsubmitted job may read its buffer's previous content (their refmasks, known at
+ *     dispatch, so unparsed jobs count too).
+ * The back end then sees every reference before its readers and every reader of a buffer's old content
+ * before its overwrite, as with decode order; its device-side ordering (row flags by launch sequence,
+ * WAR events, in-launch war / war_writer) only needs that.  Binding stays in decode order. */
+static int early_ok(const struct h264_async *as, const h264_job_t *j)
+{
+	if (!j->done || j->err || j->submitted || j->nonref || !ahead_ok(as, j)) return 0;
+	const int v = j->vid & 63;
+	uint64_t need = j->refmask;
+	for (long i = j->seq - 1; i >= as->tail; --i) {
+		const h264_job_t *o = as->fifo[i % AS_MAX];
+		const int ov = o->vid & 63;
+		if (!o->submitted) {
+			if ((o->refmask >> v) & 1) return 0;         /* reads the buffer's old content */
+			if ((need >> ov) & 1) return 0;              /* the reference is not on the device yet */
+		}
+		need &= ~(1ull << ov);                           /* (older writers of that buffer: overwritten) */
+	}
+	return 1;
+}
+
 /* Decode ahead: make every step the state allows — bind the oldest closed, submitted job (and retire
  * what is bound), or submit the next parsed job that is closed or allowed ahead.  There is no
  * submitter thread: whoever changes what is possible (a pool worker that finished a job, the API
@@ -1142,6 +1181,10 @@ static void pipe_drive(struct h264_async *as)
 			pthread_cond_broadcast(&as->cv_done);
 			continue;
 		}
+		if (as->sub < as->head && as->fifo[as->sub % AS_MAX]->submitted) { /* (went early) */
+			as->sub++;
+			continue;
+		}
 		if (as->sub < as->head) {
 			h264_job_t *j = as->fifo[as->sub % AS_MAX];
 			if (j->done && (as->sub < as->a_seq || ahead_ok(as, j))) {
@@ -1158,6 +1201,26 @@ static void pipe_drive(struct h264_async *as)
 				as->held |= !err && d->backend.flush != NULL;
 				as->sub++;
 				d->ahead_submits += ahead && !err;
+				pthread_cond_broadcast(&as->cv_done);
+				continue;
+			}
+		}
+		if (g_early) {
+			h264_job_t *e = NULL;
+			for (long i = as->sub + 1; i < as->head && i < as->sub + 32 && !e; ++i)
+				if (early_ok(as, as->fifo[i % AS_MAX])) e = as->fifo[i % AS_MAX];
+			if (e) {
+				pthread_mutex_unlock(as->mu);
+				m2d_tl('S', e->seq, 1);
+				const int err = copy_submit(d, e, 1);
+				m2d_tl('s', e->seq, 1);
+				pthread_mutex_lock(as->mu);
+				e->sub_err = err;
+				e->submitted = 1;
+				as->sub_err += err;
+				as->held |= !err && d->backend.flush != NULL;
+				d->ahead_submits += !err;
+				as->n_early += !err;
 				pthread_cond_broadcast(&as->cv_done);
 				continue;
 			}
@@ -1488,7 +1551,14 @@ static int la_close(h264_dec_t *la)
 	j->poc = j->snap[0]->sh.poc;
 	/* a non-reference picture is never anyone's refs[1][0]: its co-located store is dead data */
 	j->nonref = 1;
-	for (int k = 0; k < j->nsl; ++k) j->nonref &= (j->snap[k]->sh.nal_ref_idc == 0);
+	j->refmask = 0;
+	for (int k = 0; k < j->nsl; ++k) {
+		const h264_dec_t *sk = j->snap[k];
+		j->nonref &= (sk->sh.nal_ref_idc == 0);
+		for (int l = 0; l < 2; ++l)
+			for (int i = 0; i < 16; ++i)
+				if (sk->refs[l][i].in_use && sk->refs[l][i].frame_idx >= 0) j->refmask |= 1ull << (sk->refs[l][i].frame_idx & 63);
+	}
 	if (j->nonref && (size_t)j->snap[0]->n_mbs > j->priv_n) {
 		free(j->priv_col);
 		j->priv_col = (h264_colmb_t *)malloc(sizeof(h264_colmb_t) * (size_t)j->snap[0]->n_mbs);

@@ -175,3 +175,24 @@ def test_col_row_pipelining(built, tmp_path, name, pipe):
         assert early > 0
     elif name != "cov_reflists_s1":  # (reordered lists: a B picture's anchor is not always the last one)
         assert early == 0
+
+
+@pytest.mark.parametrize("name", ["cov_reflists_s1", "cov_reflists_s2", "cov_reflists_cavlc_s1", "cov_mmco5_s1",
+                                  "cov_poc1_s1", "cov_tools_s1", "cov_wp_s1", "cov_slices_s1"])
+def test_early_reference_submission(built, tmp_path, name):
+    """Early submission (h264_async.c early_ok): a parsed reference picture goes to the back end ahead of
+    older pictures still parsing, when every picture it may read is submitted and no older unsubmitted
+    picture may read its buffer's previous content.  With the non-reference pictures held back
+    (M2DEC_AMD_NONREF_DELAY_US, longer than the CPU checker's submission of a picture) the timeline shows early submissions ('S' events with b = 1) and the frames
+    equal the goldens (list modification, MMCO 5, long-term references, POC types, weighted prediction,
+    slices)."""
+    import csv
+    import subprocess
+    import sys
+    tl = tmp_path / "tl.csv"
+    env = dict(os.environ, M2DEC_AMD_TIMELINE=str(tl), M2DEC_AMD_NONREF_DELAY_US="200000", M2DEC_AMD_EARLY="1")
+    out = subprocess.run([sys.executable, "-c", _COL_CHILD % (ROOT, name, name)], env=env, capture_output=True,
+                         text=True, timeout=600)
+    assert "MD5OK True" in out.stdout, out.stdout + out.stderr[-2000:]
+    early = sum(1 for r in csv.DictReader(open(tl)) if r["kind"] == "S" and r["b"] == "1")
+    assert early > 0

@@ -105,6 +105,15 @@ for step in "$@"; do
   c5)
     AB_STREAM=c5_4k_s1 timeout -k 10 900 python3 tools/ab_env.py 4 8 "def:GPU_MAX_HW_QUEUES=8" "p1:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_PICS_PER_LAUNCH=1" "s3:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=3" > gpurun_out/ab_c5_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_c5_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_c5_$TAG.txt ;;
+  p1)
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "def:GPU_MAX_HW_QUEUES=8" "s6p1:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_STREAMS=6,M2DEC_AMD_PICS_PER_LAUNCH=1" "s8p1:GPU_MAX_HW_QUEUES=12,M2DEC_AMD_STREAMS=8,M2DEC_AMD_PICS_PER_LAUNCH=1" "s8p1h0:GPU_MAX_HW_QUEUES=12,M2DEC_AMD_STREAMS=8,M2DEC_AMD_PICS_PER_LAUNCH=1,M2DEC_AMD_HOLD=0" > gpurun_out/ab_p1_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_p1_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_p1_$TAG.txt ;;
+  early)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_cli.py tests/test_gpu_boundary.py tests/test_gpu_f1.py > gpurun_out/pytest_early_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_early_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_early_$TAG.log
+    timeout -k 10 900 python3 tools/ab_env.py 5 12 "e1:GPU_MAX_HW_QUEUES=8" "e0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_EARLY=0" > gpurun_out/ab_early_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_early_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_early_$TAG.txt
+    GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

@@ -1450,6 +1450,11 @@ __device__ M2DEC_INTER_WORKER_ATTR void inter_worker(const PictureArgs &a, const
 		__syncthreads();
 		const int item = __builtin_amdgcn_readfirstlane(s_item);
 		if (item >= nitems) break;
+#ifndef M2DEC_NO_ITEM_LAUNDER
+		/* (as in inter_mb: per-lane values re-derived per item instead of held across the item loop) */
+		int t = threadIdx.x;
+		asm volatile("" : "+v"(t));
+#endif
 		const int y = item / nseg, seg = item % nseg, x0 = seg * 8, x1 = min(x0 + 8, Wmb);
 		STAMPI(96 + (blockIdx.x & 63), 0, nst_dbg & 255, item);
 		/* ---- the item's records into LDS: MB records, then the motion records they point at */

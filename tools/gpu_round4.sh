@@ -114,6 +114,11 @@ for step in "$@"; do
     timeout -k 10 900 python3 tools/ab_env.py 5 12 "e1:GPU_MAX_HW_QUEUES=8" "e0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_EARLY=0" > gpurun_out/ab_early_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_early_$TAG.txt; exit 1; }
     grep "^all" gpurun_out/ab_early_$TAG.txt
     GPU_MAX_HW_QUEUES=8 bash tools/timeline.sh $TAG 4 || exit 1 ;;
+  item)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_streams.py tests/test_gpu_batch.py > gpurun_out/pytest_item_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_item_$TAG.log; exit 1; }
+    tail -1 gpurun_out/pytest_item_$TAG.log
+    V=noitem timeout -k 10 600 bash tools/ab_replay.sh item_$TAG || exit 1
+    cat gpurun_out/ab_item_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

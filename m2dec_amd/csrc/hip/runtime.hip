@@ -480,7 +480,7 @@ struct Sched {
 	 * reads are over.  Inside the launch a picture that overwrites a slot an earlier one of the launch
 	 * read or wrote waits for it on the device (war / war_writer on the completion counters), as in a
 	 * replay batch; workgroups are dispatched in block order, so every such wait points backwards. */
-	int launch_multi(int k, const PicJob *jobs, int n, hipEvent_t *tev, hipEvent_t *inter_done)
+	int launch_multi(int k, const PicJob *jobs, int n, hipEvent_t *tev, hipEvent_t *inter_done, hipEvent_t *tstart = nullptr)
 	{
 		if (n < 1 || n > BMAX) return -1;
 		hipStream_t s = st[k];
@@ -549,6 +549,7 @@ struct Sched {
 			hipEvent_t done = bg.event();
 			if (!done) return -1;
 			const int held = bg.reserve(nb);
+			if (tstart) CHECK(hipEventRecord(*tstart, s)); /* (decode path: TimingSlot e[3], the kernel's start) */
 			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
 			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), n);
 			if (hipGetLastError() != hipSuccess || hipEventRecord(done, s) != hipSuccess) {
@@ -879,7 +880,7 @@ struct ArenaPool {
 ArenaPool g_arenas;
 
 struct TimingSlot {
-	hipEvent_t e[6]; /* start, uploaded, after the kernel, (unused), (unused), end */
+	hipEvent_t e[6]; /* start, uploaded, after the kernel, right before the kernel, (unused), end */
 	bool pending = false;
 };
 
@@ -972,7 +973,10 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 	(void)hipEventSynchronize(t.e[5]);
 	m2dec_amd_hip_timing_t &tm = b->sc.tm;
 	if (hipEventElapsedTime(&ms, t.e[0], t.e[1]) == hipSuccess) tm.h2d_us += ms * 1e3;
-	if (hipEventElapsedTime(&ms, t.e[1], t.e[2]) == hipSuccess) {
+	/* the kernel alone: from the event recorded right before it (after the launch's argument copy and the
+	 * stream's waits on other launches) to the one after it, so that rocprofv3's kernel duration and this
+	 * agree (r114: from the upload's end the interval also held those, 1352 vs 1198 us) */
+	if (hipEventElapsedTime(&ms, t.e[3], t.e[2]) == hipSuccess) {
 		tm.picture_us += ms * 1e3;
 		tm.kernel_launches++;
 	}
@@ -1195,7 +1199,7 @@ int launch_held(HipBackend *b)
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	m2d_tl('M', n, k);
 	hipEvent_t inter_done;
-	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done) < 0) return -1;
+	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done, ts ? ts->e + 3 : nullptr) < 0) return -1;
 	if (sc.mark_busy(k) < 0) return -1;
 	m2d_tl('N', n, k);
 	const size_t ls = (size_t)sc.W * sc.H;

@@ -967,7 +967,7 @@ static int job_ext_idle(struct h264_async *as, h264_job_t *j, int wait)
 	return !j->ext_busy;
 }
 
-static h264_job_t *job_get(struct h264_async *as)
+static h264_job_t *job_get(struct h264_async *as, size_t need)
 {
 	h264_job_t *j;
 	/* (the newest retired jobs may still be uploading: take the first one that is not) */
@@ -977,7 +977,18 @@ static h264_job_t *job_get(struct h264_async *as)
 			as->free_jobs[i] = as->free_jobs[--as->nfree];
 			return j;
 		}
-	if (g_njobs) return g_jobs[--g_njobs];
+	if (g_njobs) {
+		/* the newest pooled job whose arena already fits this geometry (pinned if the pipeline uploads from it):
+		 * a 4K stream after 1080p ones otherwise re-pins a pooled 1080p job's arena (~27 MB, several ms on
+		 * the lookahead's thread) for each job it takes */
+		for (int i = g_njobs - 1; i >= 0; --i)
+			if (g_jobs[i]->arena_size >= need && (!as->ext || g_jobs[i]->arena_pinned)) {
+				j = g_jobs[i];
+				g_jobs[i] = g_jobs[--g_njobs];
+				return j;
+			}
+		return g_jobs[--g_njobs];
+	}
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
 	g_jobs_new++;
@@ -1466,7 +1477,7 @@ int h264_async_add_slice(h264_dec_t *la)
 	const double ts = as->stats ? now_s() : 0;
 	if (!j) {
 		pthread_mutex_lock(as->mu); /* (pipe_drive recycles jobs) */
-		j = job_get(as);
+		j = job_get(as, m2r_arena_layout(la->mb_w * la->mb_h).size);
 		pthread_mutex_unlock(as->mu);
 		if (!j || job_arena(j, la->mb_w, la->mb_h, as->ext) < 0) return -1;
 		j->vid = la->curr_idx;

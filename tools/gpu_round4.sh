@@ -119,6 +119,9 @@ for step in "$@"; do
     tail -1 gpurun_out/pytest_item_$TAG.log
     V=noitem timeout -k 10 600 bash tools/ab_replay.sh item_$TAG || exit 1
     cat gpurun_out/ab_item_$TAG.txt ;;
+  md5t)
+    timeout -k 10 900 python3 tools/ab_env.py 4 12 "def:GPU_MAX_HW_QUEUES=8" "mb4:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_MD5_MIN_BATCH=4" "mb16:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_MD5_MIN_BATCH=16" "tail0:GPU_MAX_HW_QUEUES=8,M2DEC_AMD_MD5_TAIL=0" > gpurun_out/ab_md5t_$TAG.txt 2>&1 || { tail -5 gpurun_out/ab_md5t_$TAG.txt; exit 1; }
+    grep "^all" gpurun_out/ab_md5t_$TAG.txt ;;
   gpu)
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
     tail -2 gpurun_out/pytest_gpu_$TAG.log ;;

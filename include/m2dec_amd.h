@@ -130,6 +130,44 @@ typedef struct {
 } m2dec_amd_hip_timing_t;
 int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out);
 
+/* The decode path's admission against the device-wide workgroup budget (DESIGN §5 "Forward-progress
+ * invariant"): what this back end plans with at its current geometry, and what the device's budget saw. */
+typedef struct {
+	int resident_per_cu; /* k_picture workgroups resident per CU at this context's geometry */
+	int cap_workgroups;  /* ... on the whole device */
+	int wg_units;        /* budget units one of its workgroups costs */
+	int cap_units;       /* the device's budget in units (all processes) */
+	int pics_fit;        /* pictures per launch with which a launch per stream fits the capacity */
+	int launch_limit;    /* pictures per launch this context uses (1 while other contexts decode on the device) */
+	int streams;         /* launch streams of a decoder context */
+	int shared;          /* 1: the budget is the device's cross-process segment (devshare.c) */
+	int max_procs;       /* most processes seen holding budget units at once */
+	int max_units;       /* most units seen in use at once */
+} m2dec_amd_hip_budget_t;
+int m2dec_amd_hip_backend_budget(const m2r_backend_t *be, m2dec_amd_hip_budget_t *out);
+
+/* Hardware queues for the HIP runtime of this process: sets GPU_MAX_HW_QUEUES to n unless the caller's
+ * environment has it already, and returns the value in effect.  The runtime reads it once, when it starts,
+ * so call this before anything in the process uses HIP.  With 5 or more queues a decoder context uses 4
+ * launch streams + a copy stream, else 3 (runtime.hip nstreams).  The library itself never changes the
+ * caller's HIP configuration; the h264dec CLI and bench.py ask for 8. */
+int m2dec_amd_configure_queues(int n);
+
+/* Free what the process keeps pooled between decoder contexts: the parse pool's jobs with their page-locked
+ * record arenas, the back ends' pinned record arenas and staging buffers, pooled device buffers (a service
+ * that stops decoding for a while).  Live contexts are untouched.  m2dec_amd_pinned_bytes: page-locked bytes
+ * of the parse jobs' record arenas (all; pooled in *pooled), bounded by M2DEC_AMD_POOL_PINNED_MB. */
+void m2dec_amd_release_pools(void);
+long long m2dec_amd_pinned_bytes(long long *pooled);
+
+/* The device-wide workgroup budget segment (devshare.c) under an arbitrary key, for tests and
+ * diagnostics: open (creating it with cap_units), reserve (1 / 0), release, state, close. */
+void *m2dec_amd_share_open(const char *key, int cap_units);
+int m2dec_amd_share_try(void *s, int units);
+void m2dec_amd_share_release(void *s, int units);
+int m2dec_amd_share_state(void *s, int *cap, int *total, int *mine, int *procs, long *reclaimed);
+void m2dec_amd_share_close(void *s);
+
 /* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);
 /* MD5 lines of n <= 16 frames at once (16-lane AVX-512 multi-buffer MD5 when the CPU has it and the

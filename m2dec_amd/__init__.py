@@ -71,6 +71,15 @@ class HipTiming(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class HipBudget(ctypes.Structure):
+    """m2dec_amd_hip_budget_t (include/m2dec_amd.h)."""
+    _fields_ = [(k, ctypes.c_int) for k in ("resident_per_cu", "cap_workgroups", "wg_units", "cap_units", "pics_fit",
+                                            "launch_limit", "streams", "shared", "max_procs", "max_units")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class TracePic(ctypes.Structure):
     """m2dec_amd_trace_pic_t (include/m2dec_amd.h)."""
     _fields_ = [("slot", ctypes.c_int32), ("width_mbs", ctypes.c_int32), ("height_mbs", ctypes.c_int32),
@@ -106,6 +115,12 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_available.restype = ctypes.c_int
         L.m2dec_amd_hip_backend_timing.argtypes = [ctypes.POINTER(Backend), ctypes.POINTER(HipTiming)]
         L.m2dec_amd_hip_backend_timing.restype = ctypes.c_int
+        L.m2dec_amd_hip_backend_budget.argtypes = [ctypes.POINTER(Backend), ctypes.POINTER(HipBudget)]
+        L.m2dec_amd_hip_backend_budget.restype = ctypes.c_int
+        L.m2dec_amd_pinned_bytes.argtypes = [ctypes.POINTER(ctypes.c_longlong)]
+        L.m2dec_amd_pinned_bytes.restype = ctypes.c_longlong
+        L.m2dec_amd_release_pools.argtypes = []
+        L.m2dec_amd_release_pools.restype = None
         L.m2dec_amd_frame_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_char_p]
         L.m2dec_amd_frame_md5.restype = None
         L.m2dec_amd_frames_md5.argtypes = [ctypes.POINTER(Frame), ctypes.c_int, ctypes.c_char_p]
@@ -195,6 +210,12 @@ class HipBackend:
         t = HipTiming()
         lib().m2dec_amd_hip_backend_timing(ctypes.byref(self.be), ctypes.byref(t))
         return t.as_dict()
+
+    def budget(self) -> dict:
+        """What this context plans with against the device-wide workgroup budget (m2dec_amd_hip_backend_budget)."""
+        b = HipBudget()
+        lib().m2dec_amd_hip_backend_budget(ctypes.byref(self.be), ctypes.byref(b))
+        return b.as_dict()
 
     def close(self) -> None:
         _call_destroy(self.be)

@@ -93,6 +93,9 @@ int main(int argc, char **argv)
 {
 	int opt, wmode = 0, dpb = -1, codec = MODE_NONE, emptify = 0, force_exec = 0, skip = 0, err = -1;
 	writer_t w = {0, 0};
+	/* this process's HIP runtime: 8 hardware queues (4 launch streams + the copy stream per decoder), asked for
+	 * before anything uses HIP; the library leaves a caller's setting alone */
+	m2dec_amd_configure_queues(8);
 	while ((opt = getopt(argc, argv, "bd:ef:moOsx")) != -1) {
 		switch (opt) {
 		case 'b': dpb = 1; break;

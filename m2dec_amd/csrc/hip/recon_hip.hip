@@ -1220,7 +1220,13 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 			const int nw = do_luma ? 6 : 4;
 			const int xs = (t < 3) ? x : ((do_luma && t < 5) ? x + 1 : x - 1);
 			const int wi = (t < 3) ? t : ((do_luma && t < 5) ? t - 3 : 2);
-			const bool mine_w = t < nw && xs >= 0 && xs < Wmb && up_intra(xs);
+			/* only the neighbours this MB's predictor may read: its avail bits (top 2, top-right 4, top-left 8)
+			 * are slice-aware (get_availability, h264.cpp:9704-9715), so the first MB row of a slice waits for
+			 * nothing of the slice above and each slice of an I picture runs its own intra wavefront (C5's 8
+			 * slices: 8 chains of Wmb + 2 (rows of the slice) steps instead of one of Wmb + 2 Hmb) */
+			const int av = do_luma ? m.avail_luma : m.avail_chroma;
+			const int need = (t < 3) ? 2 : ((do_luma && t < 5) ? 4 : 8);
+			const bool mine_w = t < nw && xs >= 0 && xs < Wmb && (av & need) && up_intra(xs);
 			const uint8_t *src = hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + (do_luma ? 0 : 24) + wi * 8;
 			unsigned long long v = 0;
 			unsigned spins = 0;

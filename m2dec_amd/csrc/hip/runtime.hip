@@ -21,6 +21,7 @@
 #include <string.h>
 #include <time.h>
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <deque>
 #include <mutex>
@@ -28,6 +29,7 @@
 #include <vector>
 #include "recon_internal.h"
 #include "m2dec_amd.h"
+#include "devshare.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
@@ -53,10 +55,13 @@ static int dbg_knob(const char *name)
 
 const int NSTREAMS = 8; /* most launch streams of a decoder context (arrays); g_nstreams of them are used */
 /* launch streams in use: one hardware queue each, the copy stream another — more streams than queues
- * share a queue and serialise their launches.  4 when the runtime has at least 5 queues (the library
- * asks for 8 when it is loaded, below; at 1080p 4 x 2 pictures fill the workgroup budget:
- * profiles/r95_ab_prio_streams.txt), else 3 (HIP's default GPU_MAX_HW_QUEUES=4);
- * M2DEC_AMD_STREAMS = 1..8 */
+ * share a queue and serialise their launches.  4 when the runtime has at least 5 queues (at 1080p 4 x 2
+ * pictures fill the workgroup budget: profiles/r95_ab_prio_streams.txt), else 3 (HIP's default
+ * GPU_MAX_HW_QUEUES=4); M2DEC_AMD_STREAMS = 1..8.  The runtime reads GPU_MAX_HW_QUEUES once, when it
+ * starts, and offers no query for it: the value in the environment when the library first uses HIP is taken
+ * as what the runtime got.  The library never sets it (a caller's HIP configuration is the caller's): a
+ * process that wants 4 launch streams calls m2dec_amd_configure_queues() before anything uses HIP, as the
+ * h264dec CLI and bench.py do. */
 static int nstreams()
 {
 	static int n = 0;
@@ -72,13 +77,6 @@ static int nstreams()
 	return n;
 }
 
-/* Hardware queues for the launch streams + the copy stream: the runtime reads GPU_MAX_HW_QUEUES when it
- * starts, so the library asks for 8 as it is loaded (a caller's own setting wins; a process whose HIP
- * runtime started earlier keeps its queues, and nstreams() falls back to 3 unless it says 5 or more) */
-__attribute__((constructor)) static void hw_queues_default()
-{
-	setenv("GPU_MAX_HW_QUEUES", "8", 0);
-}
 const int BMAX = 4; /* at most this many pictures per decode-path launch: the back end holds submitted
                      * pictures back until the decoder flushes (the end of a burst of submits) or it holds
                      * max_held, so that pictures parsed together run in one launch */
@@ -95,39 +93,94 @@ const int BMAX = 4; /* at most this many pictures per decode-path launch: the ba
  * kernel whose waits point at lower block indices: in-order dispatch inside a launch.) */
 struct SlotBudget {
 	std::mutex mu;
-	int cap = 0, used = 0;
-	std::deque<std::pair<hipEvent_t, int>> pend; /* completion event of a launch, its workgroups */
+	bool ready = false;
+	int cap_units = 0;  /* the device's budget: M2D_SHARE_UNITS_PER_CU x CUs (devshare.h) */
+	int used_local = 0; /* process-local account, when no shared segment could be opened */
+	m2d_share_t *share = nullptr; /* the device's cross-process budget (devshare.c), normally */
+	int max_procs = 0, max_total = 0; /* diagnostics: the most processes / units seen holding the budget */
+	std::deque<std::pair<hipEvent_t, int>> pend; /* completion event of a launch, its units */
 	std::vector<hipEvent_t> pool;
 
-	/* returns the workgroups reserved (the launch's, or the whole capacity for a bigger launch) */
-	int reserve(int blocks)
+	/* once per device: the capacity in units and the shared segment keyed by the PCI bus id
+	 * (M2DEC_AMD_SHARE=0: a process-local budget, which is safe only while this is the one process
+	 * decoding on the device) */
+	void setup_locked(int dev)
+	{
+		if (ready) return;
+		ready = true;
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
+		cap_units = M2D_SHARE_UNITS_PER_CU * cus;
+		const char *e = getenv("M2DEC_AMD_SHARE");
+		if (!e || atoi(e)) {
+			char bus[64] = {0};
+			if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) == hipSuccess && bus[0])
+				share = m2d_share_open(bus, cap_units);
+			if (share) cap_units = std::min(cap_units, m2d_share_cap(share));
+			else fprintf(stderr, "m2dec_amd: no shared workgroup budget for device %d (%s): process-local budget\n", dev, bus);
+		}
+	}
+	void setup(int dev)
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		setup_locked(dev);
+	}
+
+	bool take(int units)
+	{
+		if (share) {
+			int total = 0, procs = 0;
+			const bool ok = m2d_share_try(share, units, &total, &procs) != 0;
+			max_procs = std::max(max_procs, procs);
+			if (ok) max_total = std::max(max_total, total);
+			return ok;
+		}
+		if (used_local + units > cap_units) return false;
+		used_local += units;
+		max_procs = 1;
+		max_total = std::max(max_total, used_local);
+		return true;
+	}
+	void give(int units)
+	{
+		if (share) m2d_share_release(share, units);
+		else used_local -= units;
+	}
+	void retire()
+	{
+		for (size_t i = 0; i < pend.size();) {
+			if (hipEventQuery(pend[i].first) == hipSuccess) {
+				give(pend[i].second);
+				pool.push_back(pend[i].first);
+				pend.erase(pend.begin() + (long)i);
+			} else {
+				++i;
+			}
+		}
+	}
+
+	/* reserve `units` (a launch's workgroups x the context's cost per workgroup, or the whole budget for a
+	 * bigger launch); returns the units reserved.  Waits for this process's oldest launch when its own launches
+	 * hold the budget, else (other processes', or a launch of this process between reserve and registered)
+	 * polls */
+	int reserve(int units)
 	{
 		std::unique_lock<std::mutex> lk(mu);
-		const int want = std::min(blocks, cap);
+		const int want = std::min(units, cap_units);
 		for (;;) {
-			for (size_t i = 0; i < pend.size();) {
-				if (hipEventQuery(pend[i].first) == hipSuccess) {
-					used -= pend[i].second;
-					pool.push_back(pend[i].first);
-					pend.erase(pend.begin() + (long)i);
-				} else {
-					++i;
-				}
-			}
-			if (used + want <= cap) break;
-			if (pend.empty()) { /* in flight but not registered yet (another thread between launch and
-			                     * register): let it finish registering */
+			retire();
+			if (take(want)) break;
+			if (!pend.empty()) {
+				hipEvent_t e = pend.front().first;
 				lk.unlock();
-				std::this_thread::yield();
+				(void)hipEventSynchronize(e);
 				lk.lock();
 				continue;
 			}
-			hipEvent_t e = pend.front().first;
 			lk.unlock();
-			(void)hipEventSynchronize(e);
+			std::this_thread::sleep_for(std::chrono::microseconds(50));
 			lk.lock();
 		}
-		used += want;
 		return want;
 	}
 
@@ -144,7 +197,7 @@ struct SlotBudget {
 		return e;
 	}
 
-	/* the launch's completion event is recorded: it returns `n` workgroups once it fires */
+	/* the launch's completion event is recorded: it returns `n` units once it fires */
 	void registered(hipEvent_t e, int n)
 	{
 		std::lock_guard<std::mutex> lk(mu);
@@ -154,13 +207,32 @@ struct SlotBudget {
 	void cancel(int n)
 	{
 		std::lock_guard<std::mutex> lk(mu);
-		used -= n;
+		give(n);
+	}
+
+	/* decode-path back ends alive on the device, all processes (delta: this process's change) */
+	int contexts(int delta, int local)
+	{
+		std::lock_guard<std::mutex> lk(mu);
+		return share ? m2d_share_contexts(share, delta) : local;
 	}
 };
 
 SlotBudget g_budget[16]; /* per device ordinal */
-std::atomic<int> g_live_backends[16]; /* decode-path back ends alive per device (several pictures per launch
-                                       * only for a lone stream: concurrent streams already fill the budget) */
+
+/* M2DEC_AMD_SHARE_REPORT=1: at exit, what each device's budget saw (tests/test_gpu_cli.py's concurrent-process
+ * case prints it: the overlap the decoding processes had) */
+__attribute__((destructor)) static void budget_report()
+{
+	if (!getenv("M2DEC_AMD_SHARE_REPORT")) return;
+	for (int d = 0; d < 16; ++d)
+		if (g_budget[d].ready)
+			fprintf(stderr, "m2dec_amd budget: device %d shared %d, max processes %d, max units %d / %d\n", d,
+			        g_budget[d].share != nullptr, g_budget[d].max_procs, g_budget[d].max_total, g_budget[d].cap_units);
+}
+std::atomic<int> g_live_backends[16]; /* decode-path back ends alive per device in this process (several pictures
+                                       * per launch only for a lone stream: concurrent streams already fill the
+                                       * budget) */
 
 /* Streams and events outlive a decoder context too (creating a stream and the ~160 events of a back
  * end costs ~10 ms): released ones are kept per device and handed to the next context. */
@@ -302,6 +374,9 @@ struct Sched {
 	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
 	int rr = 0;
 	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
+	int resident_per_cu = 0;   /* k_picture workgroups resident per CU at this geometry */
+	int wg_units = 0;          /* budget units per k_picture workgroup (SlotBudget, devshare.h) */
+	int cap_wg = 0;            /* k_picture workgroups the device holds at once at this geometry */
 	hipEvent_t busy[NSTREAMS] = {}; /* recorded behind each decode-path launch on the stream (its own event) */
 	bool busy_set[NSTREAMS] = {};
 	hipEvent_t ev[NEVENTS] = {};
@@ -388,18 +463,23 @@ struct Sched {
 			lds_set = lds;
 		}
 		{
-			/* resident-workgroup capacity of k_picture at this picture size: the decode path's budget */
+			/* resident-workgroup capacity of k_picture at THIS picture size (its LDS sets the occupancy): the
+			 * cost of one of its workgroups in the device budget, and the capacity this context plans with.
+			 * Per context: another context's geometry (a 4K one before a 1080p one) changes neither. */
 			int per_cu = 0, cus = 0;
 			CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_picture, 256, lds));
 			CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-			SlotBudget &bg = g_budget[dev & 15];
-			std::lock_guard<std::mutex> lk(bg.mu);
-			const int cap = std::max(1, per_cu * cus);
-			if (!bg.cap || cap < bg.cap) bg.cap = cap; /* contexts of several picture sizes: the smallest */
+			per_cu = std::max(1, per_cu);
+			g_budget[dev & 15].setup(dev);
+			resident_per_cu = per_cu;
+			wg_units = (M2D_SHARE_UNITS_PER_CU + per_cu - 1) / per_cu;
+			cap_wg = std::max(1, std::min(per_cu * std::max(1, cus), g_budget[dev & 15].cap_units / wg_units));
 			/* pictures per launch such that a launch on each stream fits the budget at once: a reserve
 			 * that has to wait would stall the thread driving the pipeline (a parse worker) */
-			pics_fit = std::max(1, std::min(BMAX, bg.cap / (nstreams() * picture_blocks_dp(inter_grid, row_wgs, Hmb, true))));
-			if (dbg_knob("M2DEC_AMD_DEBUG")) fprintf(stderr, "k_picture: %d workgroups resident (%d per CU)\n", bg.cap, per_cu);
+			pics_fit = std::max(1, std::min(BMAX, cap_wg / (nstreams() * picture_blocks_dp(inter_grid, row_wgs, Hmb, true))));
+			if (dbg_knob("M2DEC_AMD_DEBUG"))
+				fprintf(stderr, "k_picture: %d workgroups resident (%d per CU, %d units each), %d pictures per launch fit\n",
+				        cap_wg, per_cu, wg_units, pics_fit);
 		}
 		return 0;
 	}
@@ -548,7 +628,7 @@ struct Sched {
 			SlotBudget &bg = g_budget[dev & 15];
 			hipEvent_t done = bg.event();
 			if (!done) return -1;
-			const int held = bg.reserve(nb);
+			const int held = bg.reserve(nb * std::max(1, wg_units));
 			if (tstart) CHECK(hipEventRecord(*tstart, s)); /* (decode path: TimingSlot e[3], the kernel's start) */
 			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
 			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), n);
@@ -1012,7 +1092,8 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	/* pictures per launch: bounded by the budget (pics_fit) and 1 while other decode-path back ends are
 	 * alive (concurrent streams fill the budget already); the arena ring covers what can be in flight
 	 * (every arena is one pinned + device allocation: a ring larger than needed churns the pools) */
-	b->limit = g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed) > 1 ? 1 : std::min(b->max_held, b->sc.pics_fit);
+	b->limit = g_budget[b->sc.dev & 15].contexts(0, g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed)) > 1
+	           ? 1 : std::min(b->max_held, b->sc.pics_fit);
 	b->narenas = std::min(kArenas, nstreams() * b->limit + b->limit + 2);
 	if (b->next >= b->narenas) b->next = 0;
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "be_set_frames: configure %.2f ms\n", 1e3 * (wall_s() - t0));
@@ -1338,7 +1419,7 @@ void be_destroy(void *self)
 	for (int i = 0; i < b->nheld; ++i) b->held[i].a->held = false; /* (dropped: nothing waits for them) */
 	b->nheld = 0;
 	b->sc.sync_all();
-	g_live_backends[b->sc.dev & 15]--;
+	g_budget[b->sc.dev & 15].contexts(-1, --g_live_backends[b->sc.dev & 15]);
 	const double t1 = wall_s();
 	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: every staging copy is complete) */
 	b->copy = nullptr;
@@ -1420,12 +1501,78 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	out->flush = be_flush;
 	out->ready = be_ready;
 	out->records_busy = be_records_busy;
-	g_live_backends[device & 15]++;
+	g_budget[device & 15].setup(device);
+	g_budget[device & 15].contexts(+1, ++g_live_backends[device & 15]);
 	if (const char *e = getenv("M2DEC_AMD_HOLD")) b->hold = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_PICS_PER_LAUNCH")) /* tuning: 1 = one picture per launch */
 		b->max_held = std::max(1, std::min(BMAX, atoi(e)));
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "hip_backend_create: %.2f ms\n", 1e3 * (wall_s() - t0));
 	return 0;
+}
+
+extern "C" int m2dec_amd_hip_backend_budget(const m2r_backend_t *be, m2dec_amd_hip_budget_t *out)
+{
+	if (!be || !be->self || !out) return -1;
+	HipBackend *b = (HipBackend *)be->self;
+	const Sched &sc = b->sc;
+	SlotBudget &bg = g_budget[sc.dev & 15];
+	memset(out, 0, sizeof(*out));
+	out->resident_per_cu = sc.resident_per_cu;
+	out->cap_workgroups = sc.cap_wg;
+	out->wg_units = sc.wg_units;
+	out->pics_fit = sc.pics_fit;
+	out->launch_limit = b->limit;
+	out->streams = nstreams();
+	std::lock_guard<std::mutex> lk(bg.mu);
+	out->cap_units = bg.cap_units;
+	out->shared = bg.share != nullptr;
+	out->max_procs = bg.max_procs;
+	out->max_units = bg.max_total;
+	return 0;
+}
+
+extern "C" void h264_async_pool_release(void);
+extern "C" long long h264_async_pinned_bytes(long long *pooled);
+
+/* Everything the process keeps pooled between decoder contexts: the parse pool's jobs with their
+ * page-locked record arenas, the back ends' pinned record arenas and staging buffers, pooled device buffers.
+ * Live contexts keep what they use. */
+extern "C" void m2dec_amd_release_pools(void)
+{
+	h264_async_pool_release();
+	{
+		std::lock_guard<std::mutex> lk(g_arenas.mu);
+		for (auto &bl : g_arenas.free_blocks) {
+			(void)hipHostFree(bl.host);
+			(void)hipFree(bl.dev_ptr);
+		}
+		g_arenas.free_blocks.clear();
+	}
+	{
+		std::lock_guard<std::mutex> lk(g_stage.mu);
+		for (auto &bl : g_stage.free_blocks) (void)hipHostFree(bl.first);
+		g_stage.free_blocks.clear();
+		g_stage.kept = 0;
+	}
+	{
+		std::lock_guard<std::mutex> lk(g_dev.mu);
+		for (auto &bl : g_dev.blocks) (void)hipFree(bl.p);
+		g_dev.blocks.clear();
+		g_dev.kept = 0;
+	}
+}
+
+extern "C" long long m2dec_amd_pinned_bytes(long long *pooled)
+{
+	return h264_async_pinned_bytes(pooled);
+}
+
+extern "C" int m2dec_amd_configure_queues(int n)
+{
+	char v[16];
+	snprintf(v, sizeof v, "%d", n < 1 ? 1 : n);
+	setenv("GPU_MAX_HW_QUEUES", v, 0); /* (a value the caller set already wins) */
+	return atoi(getenv("GPU_MAX_HW_QUEUES"));
 }
 
 extern "C" int m2dec_amd_hip_backend_timing(const m2r_backend_t *be, m2dec_amd_hip_timing_t *out)

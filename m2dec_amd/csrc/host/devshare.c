@@ -1,0 +1,398 @@
+/*
+ * The device-wide workgroup budget shared by every process that decodes on one GPU.
+ *
+ * Why (DESIGN §5 "Forward-progress invariant"): a decode-path k_picture launch has workgroups that spin on
+ * row-progress words written by EARLIER launches of the same process, possibly queued on another HIP stream,
+ * and the hardware may dispatch a later launch first.  The launches are therefore admitted against a budget
+ * equal to the device's resident capacity for k_picture: all admitted launches fit on the device together,
+ * every wait points at an earlier admitted launch, so the oldest unfinished one always runs.  The reference
+ * runs one decoder process per stream (test.sh:2, `parallel src/app/h264dec -O` = one process per core), so
+ * the budget has to be the DEVICE's, not the process's: two processes with private budgets could together
+ * fill the device with spinners whose producers never get a slot.
+ *
+ * So the budget lives in a small shared-memory segment named after the GPU's PCI bus id
+ * (/dev/shm/m2dec_amd.budget.<bus id>).  Each process holds one lease {pid, start time, units, contexts};
+ * the segment's total is the sum of the leases.  A robust process-shared mutex guards it (a holder that dies
+ * inside the critical section leaves EOWNERDEAD: the next locker recomputes the total from the leases).  A
+ * lease whose process is gone (kill(pid, 0) = ESRCH, or the pid now names a process started at another
+ * time) is reclaimed when a reservation does not fit: its launches died with their process (the driver
+ * tears down a dead process's queues), so its units are free again.
+ *
+ * Units: k_picture's workgroups cost ceil(M2D_SHARE_UNITS_PER_CU / resident-per-CU) units each and the
+ * capacity is M2D_SHARE_UNITS_PER_CU x CUs, so contexts whose occupancy differs (LDS per picture width)
+ * share one account (the runtime computes the cost per context, not a single smallest capacity).
+ *
+ * Host code only, no HIP: the CPU test (tests/test_devshare_cpu.py) forks processes against a segment.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <signal.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+#include "devshare.h"
+
+#define SHARE_MAGIC 0x6d326462u /* "m2db" */
+#define SHARE_VERSION 1
+#define SHARE_LEASES 256
+
+typedef struct {
+	int32_t pid;
+	int32_t units;    /* workgroup units this process holds now */
+	int32_t contexts; /* live decode-path back ends of this process on the device */
+	int32_t pad;
+	uint64_t start;   /* /proc/<pid>/stat start time: a recycled pid is another process */
+} lease_t;
+
+typedef struct {
+	uint32_t magic, version;
+	pthread_mutex_t mu;
+	int32_t cap;          /* units */
+	int32_t total;        /* sum of the leases' units */
+	int64_t reclaimed;    /* units taken back from dead processes (diagnostics) */
+	lease_t lease[SHARE_LEASES];
+} seg_t;
+
+struct m2d_share {
+	seg_t *seg;
+	int idx;           /* this process's lease */
+	int32_t pid;
+	uint64_t start;
+	char path[160];
+	struct m2d_share *next; /* open handles of this process (closed at exit) */
+};
+
+static pthread_mutex_t g_open_mu = PTHREAD_MUTEX_INITIALIZER;
+static m2d_share_t *g_open;
+
+static uint64_t proc_start(int pid)
+{
+	char p[64], buf[1024];
+	snprintf(p, sizeof p, "/proc/%d/stat", pid);
+	int fd = open(p, O_RDONLY | O_CLOEXEC);
+	if (fd < 0) return 0;
+	ssize_t n = read(fd, buf, sizeof buf - 1);
+	close(fd);
+	if (n <= 0) return 0;
+	buf[n] = 0;
+	/* field 22 (starttime), counted after the ")" that closes the command name */
+	char *s = strrchr(buf, ')');
+	if (!s) return 0;
+	int field = 2;
+	for (; *s && field < 22; ++s)
+		if (*s == ' ') ++field;
+	return strtoull(s, NULL, 10);
+}
+
+static int lease_dead(const lease_t *l)
+{
+	if (l->pid <= 0) return 1;
+	if (kill(l->pid, 0) < 0 && errno == ESRCH) return 1;
+	const uint64_t st = proc_start(l->pid);
+	return st && l->start && st != l->start;
+}
+
+static void recount(seg_t *g)
+{
+	int32_t t = 0;
+	for (int i = 0; i < SHARE_LEASES; ++i) t += g->lease[i].units;
+	g->total = t;
+}
+
+static int lock(seg_t *g)
+{
+	int r = pthread_mutex_lock(&g->mu);
+	if (r == EOWNERDEAD) { /* the holder died inside: the leases are the truth */
+		recount(g);
+		pthread_mutex_consistent(&g->mu);
+		r = 0;
+	}
+	return r;
+}
+
+/* reclaim the leases of processes that are gone; returns the units freed */
+static int sweep(seg_t *g, int self)
+{
+	int freed = 0;
+	for (int i = 0; i < SHARE_LEASES; ++i) {
+		lease_t *l = &g->lease[i];
+		if (i == self || l->pid == 0) continue;
+		if (lease_dead(l)) {
+			freed += l->units;
+			memset(l, 0, sizeof *l);
+		}
+	}
+	if (freed) {
+		g->reclaimed += freed;
+		recount(g);
+	}
+	return freed;
+}
+
+static void seg_init(seg_t *g, int cap)
+{
+	memset(g, 0, sizeof *g);
+	pthread_mutexattr_t at;
+	pthread_mutexattr_init(&at);
+	pthread_mutexattr_setpshared(&at, PTHREAD_PROCESS_SHARED);
+	pthread_mutexattr_setrobust(&at, PTHREAD_MUTEX_ROBUST);
+	pthread_mutex_init(&g->mu, &at);
+	pthread_mutexattr_destroy(&at);
+	g->cap = cap;
+	g->version = SHARE_VERSION;
+	__atomic_store_n(&g->magic, SHARE_MAGIC, __ATOMIC_RELEASE);
+}
+
+static seg_t *map_fd(int fd)
+{
+	void *p = mmap(NULL, sizeof(seg_t), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+	return p == MAP_FAILED ? NULL : (seg_t *)p;
+}
+
+/* Publish an initialised segment atomically: build it under a private name, then link() it to the final name
+ * (fails if another process published first: then use theirs). */
+static seg_t *open_seg(const char *path, int cap)
+{
+	for (int attempt = 0; attempt < 50; ++attempt) {
+		int fd = open(path, O_RDWR | O_CLOEXEC);
+		if (fd >= 0) {
+			struct stat sb;
+			seg_t *g = NULL;
+			if (fstat(fd, &sb) == 0 && (size_t)sb.st_size >= sizeof(seg_t)) g = map_fd(fd);
+			close(fd);
+			if (g && __atomic_load_n(&g->magic, __ATOMIC_ACQUIRE) == SHARE_MAGIC && g->version == SHARE_VERSION)
+				return g;
+			if (g) munmap(g, sizeof(seg_t));
+			/* a segment of another layout version: leave it alone, use a private budget */
+			return NULL;
+		}
+		if (errno != ENOENT) return NULL;
+		char tmp[200];
+		snprintf(tmp, sizeof tmp, "%s.%d.tmp", path, (int)getpid());
+		int tfd = open(tmp, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
+		if (tfd < 0) return NULL;
+		(void)fchmod(tfd, 0666); /* processes of other users decode on the same GPU too */
+		if (ftruncate(tfd, sizeof(seg_t)) != 0) {
+			close(tfd);
+			unlink(tmp);
+			return NULL;
+		}
+		seg_t *g = map_fd(tfd);
+		close(tfd);
+		if (!g) {
+			unlink(tmp);
+			return NULL;
+		}
+		seg_init(g, cap);
+		const int linked = link(tmp, path) == 0;
+		const int link_errno = errno;
+		unlink(tmp);
+		if (linked) return g;
+		munmap(g, sizeof(seg_t));
+		if (link_errno != EEXIST) return NULL;
+		/* lost the race: open theirs */
+	}
+	return NULL;
+}
+
+m2d_share_t *m2d_share_open(const char *key, int cap_units)
+{
+	if (!key || cap_units <= 0) return NULL;
+	m2d_share_t *s = (m2d_share_t *)calloc(1, sizeof *s);
+	if (!s) return NULL;
+	const char *dir = getenv("M2DEC_AMD_SHARE_DIR");
+	if (!dir) dir = access("/dev/shm", W_OK) == 0 ? "/dev/shm" : "/tmp";
+	snprintf(s->path, sizeof s->path, "%s/m2dec_amd.budget.%s", dir, key);
+	for (char *c = s->path + strlen(dir) + 1; *c; ++c)
+		if (*c == '/') *c = '_';
+	s->pid = (int32_t)getpid();
+	s->start = proc_start(s->pid);
+	s->idx = -1;
+	seg_t *g = NULL;
+	for (int attempt = 0; attempt < 50 && !g; ++attempt) {
+		g = open_seg(s->path, cap_units);
+		if (!g) break;
+		if (lock(g) != 0) {
+			munmap(g, sizeof(seg_t));
+			g = NULL;
+			break;
+		}
+		if (g->magic != SHARE_MAGIC) { /* retired by its last user between our open and lock: open anew */
+			pthread_mutex_unlock(&g->mu);
+			munmap(g, sizeof(seg_t));
+			g = NULL;
+		}
+	}
+	if (!g) {
+		free(s);
+		return NULL;
+	}
+	s->seg = g;
+	/* our lease: one left by this very process (a second open), else a free or dead one */
+	for (int pass = 0; pass < 2 && s->idx < 0; ++pass) {
+		for (int i = 0; i < SHARE_LEASES; ++i) {
+			lease_t *l = &g->lease[i];
+			if (pass == 0 ? (l->pid == s->pid && l->start == s->start) : l->pid == 0) {
+				s->idx = i;
+				break;
+			}
+		}
+		if (s->idx < 0 && pass == 0) sweep(g, -1);
+	}
+	if (s->idx >= 0 && g->lease[s->idx].pid != s->pid) {
+		lease_t *l = &g->lease[s->idx];
+		memset(l, 0, sizeof *l);
+		l->pid = s->pid;
+		l->start = s->start;
+	}
+	pthread_mutex_unlock(&g->mu);
+	if (s->idx < 0) { /* 256 live decoding processes on one GPU: fall back to a private budget */
+		munmap(g, sizeof(seg_t));
+		free(s);
+		return NULL;
+	}
+	pthread_mutex_lock(&g_open_mu);
+	s->next = g_open;
+	g_open = s;
+	pthread_mutex_unlock(&g_open_mu);
+	return s;
+}
+
+int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
+{
+	seg_t *g = s->seg;
+	if (lock(g) != 0) return 0;
+	int ok = 0;
+	for (int pass = 0; pass < 2; ++pass) {
+		if (g->total + units <= g->cap) {
+			g->lease[s->idx].units += units;
+			g->total += units;
+			ok = 1;
+			break;
+		}
+		if (pass == 0 && !sweep(g, s->idx)) break;
+	}
+	if (total) *total = g->total;
+	if (procs) { /* processes holding units now (diagnostics: the concurrency the budget saw) */
+		int np = 0;
+		for (int i = 0; i < SHARE_LEASES; ++i) np += g->lease[i].pid && g->lease[i].units > 0;
+		*procs = np;
+	}
+	pthread_mutex_unlock(&g->mu);
+	return ok;
+}
+
+void m2d_share_release(m2d_share_t *s, int units)
+{
+	seg_t *g = s->seg;
+	if (units <= 0 || lock(g) != 0) return;
+	lease_t *l = &g->lease[s->idx];
+	if (units > l->units) units = l->units;
+	l->units -= units;
+	g->total -= units;
+	pthread_mutex_unlock(&g->mu);
+}
+
+int m2d_share_contexts(m2d_share_t *s, int delta)
+{
+	seg_t *g = s->seg;
+	if (lock(g) != 0) return 1;
+	g->lease[s->idx].contexts += delta;
+	if (g->lease[s->idx].contexts < 0) g->lease[s->idx].contexts = 0;
+	int n = 0;
+	for (int i = 0; i < SHARE_LEASES; ++i)
+		if (g->lease[i].pid && (i == s->idx || !lease_dead(&g->lease[i]))) n += g->lease[i].contexts;
+	pthread_mutex_unlock(&g->mu);
+	return n;
+}
+
+int m2d_share_state(m2d_share_t *s, int *cap, int *total, int *mine, int *procs, long *reclaimed)
+{
+	seg_t *g = s->seg;
+	if (lock(g) != 0) return -1;
+	int np = 0;
+	for (int i = 0; i < SHARE_LEASES; ++i)
+		if (g->lease[i].pid && g->lease[i].units) ++np;
+	if (cap) *cap = g->cap;
+	if (total) *total = g->total;
+	if (mine) *mine = g->lease[s->idx].units;
+	if (procs) *procs = np;
+	if (reclaimed) *reclaimed = (long)g->reclaimed;
+	pthread_mutex_unlock(&g->mu);
+	return 0;
+}
+
+int m2d_share_cap(const m2d_share_t *s)
+{
+	return s->seg->cap;
+}
+
+/* drop this process's lease; the last live user retires the segment (magic cleared under the lock, so an
+ * opener that mapped it meanwhile opens anew) and removes its file, so nothing is left in /dev/shm */
+static void share_drop(m2d_share_t *s)
+{
+	seg_t *g = s->seg;
+	if (lock(g) == 0) {
+		lease_t *l = &g->lease[s->idx];
+		g->total -= l->units;
+		memset(l, 0, sizeof *l);
+		int live = 0;
+		for (int i = 0; i < SHARE_LEASES; ++i)
+			live += g->lease[i].pid != 0 && !lease_dead(&g->lease[i]);
+		if (!live) {
+			g->magic = 0;
+			unlink(s->path);
+		}
+		pthread_mutex_unlock(&g->mu);
+	}
+	munmap(g, sizeof(seg_t));
+}
+
+void m2d_share_close(m2d_share_t *s)
+{
+	if (!s) return;
+	pthread_mutex_lock(&g_open_mu);
+	for (m2d_share_t **p = &g_open; *p; p = &(*p)->next)
+		if (*p == s) {
+			*p = s->next;
+			break;
+		}
+	pthread_mutex_unlock(&g_open_mu);
+	share_drop(s);
+	free(s);
+}
+
+/* process exit: the runtime keeps its per-device handles for the life of the process */
+__attribute__((destructor)) static void share_exit(void)
+{
+	pthread_mutex_lock(&g_open_mu);
+	m2d_share_t *s = g_open;
+	g_open = NULL;
+	pthread_mutex_unlock(&g_open_mu);
+	while (s) {
+		m2d_share_t *n = s->next;
+		share_drop(s);
+		free(s);
+		s = n;
+	}
+}
+
+/* ---- C-ABI for tests and diagnostics (include/m2dec_amd.h) */
+void *m2dec_amd_share_open(const char *key, int cap_units) { return m2d_share_open(key, cap_units); }
+int m2dec_amd_share_try(void *s, int units) { return s ? m2d_share_try((m2d_share_t *)s, units, NULL, NULL) : 0; }
+void m2dec_amd_share_release(void *s, int units)
+{
+	if (s) m2d_share_release((m2d_share_t *)s, units);
+}
+int m2dec_amd_share_state(void *s, int *cap, int *total, int *mine, int *procs, long *reclaimed)
+{
+	return s ? m2d_share_state((m2d_share_t *)s, cap, total, mine, procs, reclaimed) : -1;
+}
+void m2dec_amd_share_close(void *s) { m2d_share_close((m2d_share_t *)s); }

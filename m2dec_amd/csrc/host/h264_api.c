@@ -133,14 +133,29 @@ static int reclaim_victims(const void *ctx, h264_dec_t **out, int max)
 			pp = &d->reg_next;
 		}
 	}
+	/* hard ceiling: at twice the cap, a state idle for M2DEC_AMD_HARD_IDLE_S (default 10 s) goes
+	 * too, whatever M2DEC_AMD_IDLE_EVICT_S says: a context its caller dropped mid-stream without release (and
+	 * whose memory is never reused for an init) would otherwise hold its frames, back end and pinned arenas
+	 * for the life of the process */
+	const double hard_idle = (double)env_int("M2DEC_AMD_HARD_IDLE_S", 10);
 	while (reg_count >= cap && n < max) {
 		h264_dec_t **best = NULL;
+		const int hard = reg_count >= 2 * cap;
 		for (h264_dec_t **pp = &reg_head; *pp; pp = &(*pp)->reg_next) {
 			const h264_dec_t *d = *pp;
-			if (d->in_call || !((d->finished && d->drained) || !d->owner || (idle_on && now - d->last_call >= idle))) continue;
+			if (d->in_call || !((d->finished && d->drained) || !d->owner || (idle_on && now - d->last_call >= idle) ||
+			                    (hard && now - d->last_call >= hard_idle)))
+				continue;
 			if (!best || d->last_call < (*best)->last_call) best = pp;
 		}
-		if (!best) break;
+		if (!best) {
+			static int warned;
+			if (reg_count >= 2 * cap && !__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
+				fprintf(stderr, "m2dec_amd: %d live decoder contexts, over twice M2DEC_AMD_MAX_CONTEXTS=%d and none "
+				                "idle for M2DEC_AMD_HARD_IDLE_S=%.0f s (contexts dropped without release?)\n",
+				        reg_count, cap, hard_idle);
+			break;
+		}
 		h264_dec_t *d = *best;
 		*best = d->reg_next;
 		reg_count--;

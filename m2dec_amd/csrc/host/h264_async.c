@@ -204,10 +204,17 @@ static int g_nonref_delay_us; /* M2DEC_AMD_NONREF_DELAY_US (tests): non-referenc
 static int g_col_delay_us; /* M2DEC_AMD_COL_PIPE_DELAY_US (tests: anchors slowed down, readers start early) */
 static int job_ext_idle(struct h264_async *as, h264_job_t *j, int wait);
 
+/* page-locked bytes held by job arenas of the process (in use and pooled): M2DEC_AMD_ASYNC_STATS */
+static long long g_pinned_bytes;
+
 static void arena_free(h264_job_t *j)
 {
-	if (j->arena_pinned) m2dec_amd_pinned_free(j->arena);
-	else free(j->arena);
+	if (j->arena_pinned) {
+		m2dec_amd_pinned_free(j->arena);
+		__atomic_fetch_sub(&g_pinned_bytes, (long long)j->arena_size, __ATOMIC_RELAXED);
+	} else {
+		free(j->arena);
+	}
 	j->arena = NULL;
 	j->arena_size = 0;
 	j->arena_pinned = 0;
@@ -220,8 +227,12 @@ static int job_arena(h264_job_t *j, int wm, int hm, int pinned)
 	const m2r_arena_layout_t l = m2r_arena_layout(n);
 	if (l.size > j->arena_size || (pinned && !j->arena_pinned)) {
 		arena_free(j);
-		if (pinned && (j->arena = (uint8_t *)m2dec_amd_pinned_alloc(l.size))) j->arena_pinned = 1;
-		else j->arena = (uint8_t *)malloc(l.size);
+		if (pinned && (j->arena = (uint8_t *)m2dec_amd_pinned_alloc(l.size))) {
+			j->arena_pinned = 1;
+			__atomic_fetch_add(&g_pinned_bytes, (long long)l.size, __ATOMIC_RELAXED);
+		} else {
+			j->arena = (uint8_t *)malloc(l.size);
+		}
 		if (!j->arena) return -1;
 		j->arena_size = l.size;
 	}
@@ -291,13 +302,64 @@ static void job_free(h264_job_t *j)
 static h264_job_t *g_jobs[JOB_POOL_MAX];
 static long g_jobs_new; /* jobs created (each pins its arena on first use): M2DEC_AMD_ASYNC_STATS */
 static int g_njobs;
+static long long g_pool_pinned; /* page-locked bytes of the pooled jobs' arenas */
+static h264_job_t *pool_take(int i);
 
-static void job_release(h264_job_t *j) /* (mutex held) */
+/* the pool is bounded by the page-locked bytes it keeps, not only by its job count: at ~8.5 MB per
+ * 1080p job and ~27 MB per 4K job, 320 pooled jobs would keep up to 8.6 GB locked.  M2DEC_AMD_POOL_PINNED_MB
+ * (default 2048: the eight concurrent 1080p streams of the bench leg keep ~1.4 GB of jobs in flight). */
+static long long pool_pinned_cap(void)
+{
+	static long long cap = -1;
+	if (cap < 0) {
+		const char *e = getenv("M2DEC_AMD_POOL_PINNED_MB");
+		cap = (e && *e ? atoll(e) : 2048) << 20;
+	}
+	return cap;
+}
+
+static void job_release(h264_job_t *j) /* (mutex held; the back end no longer reads its arena) */
 {
 	if (!j) return;
 	job_clear(j);
-	if (g_njobs < JOB_POOL_MAX) g_jobs[g_njobs++] = j;
-	else job_free(j);
+	const long long pin = j->arena_pinned ? (long long)j->arena_size : 0;
+	if (pin > pool_pinned_cap()) {
+		job_free(j);
+		return;
+	}
+	/* the pool is ordered oldest first: over the count or the pinned bytes, the oldest pooled jobs go (a 4K
+	 * stream after 1080p ones keeps its own jobs, not the 1080p ones it will not take) */
+	while (g_njobs && (g_njobs >= JOB_POOL_MAX || g_pool_pinned + pin > pool_pinned_cap())) job_free(pool_take(0));
+	g_jobs[g_njobs++] = j;
+	g_pool_pinned += pin;
+}
+
+static h264_job_t *pool_take(int i) /* (mutex held; keeps the pool's order) */
+{
+	h264_job_t *j = g_jobs[i];
+	memmove(&g_jobs[i], &g_jobs[i + 1], sizeof(g_jobs[0]) * (size_t)(g_njobs - 1 - i));
+	g_njobs--;
+	if (j->arena_pinned) g_pool_pinned -= (long long)j->arena_size;
+	return j;
+}
+
+/* Free every pooled job (their page-locked arenas included): m2dec_amd_release_pools().  Jobs in use by live
+ * pipelines are untouched. */
+void h264_async_pool_release(void)
+{
+	pthread_mutex_lock(&g_parse.mu);
+	while (g_njobs) job_free(pool_take(g_njobs - 1));
+	pthread_mutex_unlock(&g_parse.mu);
+}
+
+long long h264_async_pinned_bytes(long long *pooled)
+{
+	if (pooled) {
+		pthread_mutex_lock(&g_parse.mu);
+		*pooled = g_pool_pinned;
+		pthread_mutex_unlock(&g_parse.mu);
+	}
+	return __atomic_load_n(&g_pinned_bytes, __ATOMIC_RELAXED);
 }
 
 /* ---------------------------------------------------------------- worker */
@@ -901,9 +963,11 @@ void h264_async_stop(h264_dec_t *d)
 	if (as->stats)
 		fprintf(stderr, "async: %ld jobs, depth %d; caller: lookahead %.3f s (col-store waits %.3f s, slice copies "
 		                "%.3f s), oldest-done waits %.3f s, record copies %.3f s, back-end submit %.3f s; workers "
-		                "parse %.3f s; jobs created so far in the process %ld; early submissions %ld\n",
+		                "parse %.3f s; jobs created so far in the process %ld; early submissions %ld; page-locked job "
+		                "arenas %.1f MB (pooled %.1f MB)\n",
 		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
-		        as->t_parse, g_jobs_new, as->n_early);
+		        as->t_parse, g_jobs_new, as->n_early, (double)__atomic_load_n(&g_pinned_bytes, __ATOMIC_RELAXED) / 1e6,
+		        (double)g_pool_pinned / 1e6);
 	/* no pool worker starts anything of this pipeline any more; wait for the ones inside it */
 	pthread_mutex_lock(as->mu);
 	as->quit = 1;
@@ -982,12 +1046,8 @@ static h264_job_t *job_get(struct h264_async *as, size_t need)
 		 * a 4K stream after 1080p ones otherwise re-pins a pooled 1080p job's arena (~27 MB, several ms on
 		 * the lookahead's thread) for each job it takes */
 		for (int i = g_njobs - 1; i >= 0; --i)
-			if (g_jobs[i]->arena_size >= need && (!as->ext || g_jobs[i]->arena_pinned)) {
-				j = g_jobs[i];
-				g_jobs[i] = g_jobs[--g_njobs];
-				return j;
-			}
-		return g_jobs[--g_njobs];
+			if (g_jobs[i]->arena_size >= need && (!as->ext || g_jobs[i]->arena_pinned)) return pool_take(i);
+		return pool_take(g_njobs - 1);
 	}
 	j = (h264_job_t *)calloc(1, sizeof(*j));
 	if (!j) return NULL;
@@ -1001,11 +1061,26 @@ static h264_job_t *job_get(struct h264_async *as, size_t need)
 	return j;
 }
 
+/* (mutex held; the caller drives the pipeline, so it may wait on the back end: records_busy) */
 static void job_put(struct h264_async *as, h264_job_t *j)
 {
 	job_clear(j);
-	if (as->nfree < AS_MAX) as->free_jobs[as->nfree++] = j;
-	else job_free(j);
+	if (as->nfree < AS_MAX) {
+		as->free_jobs[as->nfree++] = j;
+		return;
+	}
+	/* full: free a job whose arena the back end no longer reads (a just-retired job's upload may still
+	 * read its pinned records) — an idle free one in j's place, else j once its upload is done */
+	if (j->ext_busy)
+		for (int i = 0; i < as->nfree; ++i)
+			if (job_ext_idle(as, as->free_jobs[i], 0)) {
+				h264_job_t *o = as->free_jobs[i];
+				as->free_jobs[i] = j;
+				j = o;
+				break;
+			}
+	(void)job_ext_idle(as, j, 1);
+	job_free(j);
 }
 
 /* ---------------------------------------------------------------- API context: submission */

@@ -444,6 +444,10 @@ void h264_async_api_sps(h264_dec_t *d);
 int h264_async_sps(h264_dec_t *d);
 int h264_async_push_nal(h264_dec_t *la);
 void h264_async_trim(h264_dec_t *d);
+/* the process-wide job pool (h264_async.c): free every pooled job; page-locked bytes of job arenas (all, and
+ * pooled) */
+void h264_async_pool_release(void);
+long long h264_async_pinned_bytes(long long *pooled);
 
 /* bitio.c */
 int h264_nal_next(h264_dec_t *d);

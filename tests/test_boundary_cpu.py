@@ -123,6 +123,26 @@ def test_context_cap_without_address_reuse(built, tmp_path):
     assert max(x["contexts"] for x in st) <= 4
 
 
+def test_abandoned_contexts_hit_the_hard_ceiling(built, tmp_path):
+    """contexts dropped mid-stream without release and never freed (-k: no address reuse, so no
+    reclaim on init) are not evictable under the cap unless idle eviction is opted into; the registry still
+    stops at twice M2DEC_AMD_MAX_CONTEXTS by evicting the least recently used state idle for
+    M2DEC_AMD_HARD_IDLE_S."""
+    s = gen(tmp_path, "fit")
+    env = {"M2DEC_AMD_MAX_CONTEXTS": "3", "M2DEC_AMD_HARD_IDLE_S": "0"}
+    lines, md5 = harness(["-t", "4", "-n", "12", "-k", "-m", "5", F1, s], env=env)
+    st = iters(lines)
+    assert len(st) == 12
+    assert max(x["contexts"] for x in st) <= 6
+    assert st[-1]["evicted"] >= 12 * 2 - 6
+    f1 = golden_md5s(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"))
+    assert md5[:5] == f1[:5]
+    # without the hard ceiling's idle time reached, nothing mid-stream is evicted: the registry grows
+    lines, _ = harness(["-t", "4", "-n", "4", "-k", "-m", "5", F1, s],
+                       env={"M2DEC_AMD_MAX_CONTEXTS": "3", "M2DEC_AMD_HARD_IDLE_S": "3600"})
+    assert max(x["contexts"] for x in iters(lines)) == 8
+
+
 def test_finished_undrained_contexts_are_kept(built, tmp_path):
     """ADVICE r3: after decode_picture returns -2, M2Decoder::decode still drains the DPB with
     `while (peek_decoded_frame(ctx, &frm, 1))` (m2decoder.h:136-141).  A state in that window must not be

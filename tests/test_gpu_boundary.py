@@ -73,3 +73,59 @@ def test_gpu_resize_while_other_streams_run(built, tmp_path):
         assert got[0][-len(alone):] == alone, rep
         for n, g in zip(names, got[1:]):
             assert g == GOLDEN[n]["md5"], (rep, n)
+
+
+@pytest.mark.gpu
+def test_gpu_budget_per_context_after_4k(built):
+    """a context's admission numbers depend on its own geometry only.  A 1080p context reads
+    the same capacity / cost / pictures per launch before and after a 4K decode in the same process (round 4
+    kept the smallest capacity any context had registered, for the life of the process)."""
+    import m2dec_amd
+    c3 = stream("c3_1080p_s1")
+    with m2dec_amd.HipBackend(0) as hb:
+        assert m2dec_amd.decode_stream(c3, backend=hb.be) == GOLDEN["c3_1080p_s1"]["md5"]
+        before = hb.budget()
+        assert m2dec_amd.decode_stream_md5(stream("c5_4k_s1"), device=0) == GOLDEN["c5_4k_s1"]["md5"]
+        assert m2dec_amd.decode_stream(c3, backend=hb.be) == GOLDEN["c3_1080p_s1"]["md5"]
+        after = hb.budget()
+    print(before, after)
+    for k in ("resident_per_cu", "cap_workgroups", "wg_units", "cap_units", "pics_fit", "streams", "shared"):
+        assert before[k] == after[k], (k, before, after)
+    assert before["shared"] == 1 and before["cap_workgroups"] > 0 and before["pics_fit"] >= 1
+
+
+_POOL_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import ctypes, m2dec_amd
+from tests._streams import GOLDEN, stream
+L = m2dec_amd.lib()
+for name in ("c3_1080p_s1", "c5_4k_s1", "c3_1080p_s1"):
+    assert m2dec_amd.decode_stream_md5(stream(name), device=0) == GOLDEN[name]["md5"], name
+pooled = ctypes.c_longlong()
+total = L.m2dec_amd_pinned_bytes(ctypes.byref(pooled))
+print("pinned", total, pooled.value, flush=True)
+L.m2dec_amd_release_pools()
+total2 = L.m2dec_amd_pinned_bytes(ctypes.byref(pooled))
+print("released", total2, pooled.value, flush=True)
+assert m2dec_amd.decode_stream_md5(stream("c3_1080p_s1"), device=0) == GOLDEN["c3_1080p_s1"]["md5"]
+print("ok", flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_gpu_pooled_pinned_bytes_are_capped(built):
+    """the parse pool's page-locked job arenas are bounded by M2DEC_AMD_POOL_PINNED_MB, and
+    m2dec_amd_release_pools() returns them (the next decode pins anew and is still exact)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, M2DEC_AMD_POOL_PINNED_MB="64")
+    r = subprocess.run([sys.executable, "-c", _POOL_SCRIPT, ROOT], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = {ln.split()[0]: [int(x) for x in ln.split()[1:]] for ln in r.stdout.splitlines() if ln.strip()}
+    total, pooled = lines["pinned"]
+    assert 0 < pooled <= 64 << 20, lines
+    assert pooled <= total
+    assert lines["released"][1] == 0 and lines["released"][0] == 0, lines
+    assert "ok" in lines

@@ -60,3 +60,34 @@ def test_cli_h265(built, tmp_path):
     r = subprocess.run([APP, "-O", str(src)], cwd=tmp_path, capture_output=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "c_h265.out").read_bytes() == b"".join(m.encode() + b"\r\n" for m in G265["c_h265_1080p_s1"]["md5"])
+
+
+@pytest.mark.gpu
+def test_cli_concurrent_processes_like_test_sh(built, tmp_path):
+    """test.sh:2 runs `ls *.264 | parallel src/app/h264dec -O` — one decoder PROCESS per core, all on GPU 0.
+    The decode path's forward-progress invariant (admission of k_picture launches against the device's
+    resident capacity) must hold across those processes: the budget is the device's shared segment
+    (devshare.c), not a per-process one.  Six h264dec -O processes started together, run once; every .out
+    must equal its golden."""
+    names = ["f1_realshort", "cov_cabac_s1", "cov_tools_s1", "c2_720p_s1", "c3_1080p_s1", "c4_1080p_s2"]
+    want = {}
+    for name in names:
+        if name == "f1_realshort":
+            src = tmp_path / "f1_realshort.264"
+            src.write_bytes(open(os.path.join(ROOT, "tests", "golden", "f1_realshort.264"), "rb").read())
+            want[name] = open(os.path.join(ROOT, "tests", "golden", "f1_realshort.md5"), "rb").read()
+        else:
+            (tmp_path / f"{name}.264").write_bytes(stream(name))
+            want[name] = "".join(m + "\r\n" for m in GOLDEN[name]["md5"]).encode()
+    env = dict(os.environ, M2DEC_AMD_SHARE_REPORT="1")
+    procs = [subprocess.Popen([APP, "-O", f"{n}.264"], cwd=tmp_path, env=env, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.PIPE, text=True) for n in names]
+    errs = {}
+    for n, p in zip(names, procs):
+        _, errs[n] = p.communicate(timeout=300)
+        assert p.returncode == 0, (n, errs[n][-2000:])
+    seen = [ln for n in names for ln in errs[n].splitlines() if ln.startswith("m2dec_amd budget:")]
+    print("\n".join(seen))
+    assert seen and all(" shared 1," in ln for ln in seen), "a process decoded without the device's shared budget"
+    for n in names:
+        assert (tmp_path / f"{n}.out").read_bytes() == want[n], n

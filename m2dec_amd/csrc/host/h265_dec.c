@@ -2082,8 +2082,11 @@ static void slice_layer(perr_t *e, int nal_type)
 		if (!p->valid || !s->valid) H265_ERR(e);
 		if (s->stride != d->frame_w || (s->ctb_rows << s->log2_ctb) != d->frame_h) H265_ERR(e);
 		/* the reference has motion-field buffers for min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8)
-		 * frames (set_second_frame, h265.cpp:121-128) and writes the current frame's for every picture */
-		if (d->index >= s->frame_num) H265_ERR(e);
+		 * frames (set_second_frame, h265.cpp:121-128) and writes the current frame's for every picture: a frame
+		 * index at or above that count is reference UB (parity unpinned).  Here every one of the
+		 * H265R_MAX_FRAMES frames has its motion field, so only an index beyond those is an error (an
+		 * all-intra stream with few RPS sets decodes) */
+		if (d->index >= H265R_MAX_FRAMES) H265_ERR(e);
 		parse_slice_header(e, &b, s, p);
 		/* ctu_init (h265.cpp:4777) and colpics_t::init's register_reflist (h265modules.h:769): every slice */
 		d->frame_poc[d->index] = sh->poc;

@@ -139,3 +139,24 @@ def test_md5_driver_matches_golden(built, name):
         md5s, err = m2dec_amd.decode_h265_md5(data, backend=o.be)
     assert err == -2
     assert md5s == GOLD[name]["md5"]
+
+
+@pytest.mark.parametrize("rps", [1, 2, 3])
+def test_few_rps_sets_intra_stream(built, rps, tmp_path):
+    """an all-intra stream whose SPS carries fewer than 8 short-term RPS sets.  The reference sizes its
+    motion-field buffers by min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8) (h265.cpp:121-128)
+    and writes the current frame's for every picture, so a frame index at or above that count is reference UB
+    (parity unpinned); the decoder keeps a motion field for every frame and decodes the stream to its end.  The
+    application allocates that many frames too (get_info's frame_num), so the frame LRU and the output differ
+    from the 8-set stream's, but every frame handed out holds one of the same pictures (cov_h265_a_long_s3: 20
+    intra pictures)."""
+    g = GOLD["cov_h265_a_long_s3"]
+    out = str(tmp_path / "s.265")
+    subprocess.run([GEN, "--preset", g["preset"], "--seed", str(g["seed"]), "--frames", str(g["frames"]), "--rps",
+                    str(rps), "-o", out], check=True)
+    data = open(out, "rb").read()
+    assert hashlib.sha256(data).hexdigest() != g["sha256"]  # (a different SPS)
+    with Oracle265Backend() as o:
+        md5s, err = m2dec_amd.decode_h265(data, backend=o.be)
+    assert err == -2
+    assert md5s and set(md5s) <= set(g["md5"]), md5s

@@ -1176,6 +1176,10 @@ static void write_vps(bw_t *out)
 	free(w.b);
 }
 
+/* --rps N (intra presets only): N short-term RPS sets in the SPS instead of 8, so the reference's motion-field
+ * buffer count min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8) is N */
+static int g_rps_sets = 8;
+
 static void write_sps(bw_t *out)
 {
 	bw_t w;
@@ -1213,8 +1217,8 @@ static void write_sps(bw_t *out)
 	bw_bit(&w, 0); /* pcm */
 	/* 8 short-term RPS sets (I slices name set 0): the reference sizes its motion-field buffers by their
 	 * count, min(num_long_term_ref_pics_sps + num_short_term_ref_pic_sets, 8) frames (h265.cpp:121-128) */
-	bw_ue(&w, 8);
-	for (int i = 0; i < 8; ++i) {
+	bw_ue(&w, (uint32_t)g_rps_sets);
+	for (int i = 0; i < g_rps_sets; ++i) {
 		if (i) bw_bit(&w, 0); /* inter_ref_pic_set_prediction_flag */
 		bw_ue(&w, (uint32_t)(1 + (i & 3)));
 		bw_ue(&w, (uint32_t)(i >> 2));
@@ -1299,8 +1303,14 @@ static void write_slice(bw_t *out, int idx)
 	if (!idr) {
 		bw_bits(&w, (uint32_t)(poc & 255), 8);
 		if (!inter_pic) {
-			bw_bit(&w, 1); /* the SPS RPS, index in log2ceil(8) = 4 bits (the reference's count, h265.cpp:757-759) */
-			bw_bits(&w, 0, 4);
+			/* the SPS RPS, index in log2ceil(n) bits (1 + floor(log2 n): 4 bits for the 8 sets, the reference's count,
+			 * h265.cpp:757-759), none for a single set */
+			bw_bit(&w, 1);
+			if (g_rps_sets > 1) {
+				int nb = 0;
+				for (int n = g_rps_sets; n; n >>= 1) nb++;
+				bw_bits(&w, 0, nb);
+			}
 		} else {
 			/* every picture decoded so far, nearest first on each side, all used */
 			int neg[8], pos[8], nn = 0, np = 0;
@@ -1415,6 +1425,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(argv[i], "--frames") && i + 1 < argc) frames = atoi(argv[++i]);
 		else if (!strcmp(argv[i], "-o") && i + 1 < argc) outp = argv[++i];
 		else if (!strcmp(argv[i], "--dump") && i + 1 < argc) dumpf = fopen(argv[++i], "w");
+		else if (!strcmp(argv[i], "--rps") && i + 1 < argc) g_rps_sets = atoi(argv[++i]);
 	}
 	{
 		int found = 0;
@@ -1429,6 +1440,10 @@ int main(int argc, char **argv)
 		}
 	}
 	if (frames > 0) C.frames = frames;
+	if (g_rps_sets < 1 || g_rps_sets > 8 || (C.gop && g_rps_sets != 8)) {
+		fprintf(stderr, "h265gen: --rps 1..8, and only for intra presets\n");
+		return 2;
+	}
 	rs = 0x9E3779B97F4A7C15ull ^ ((uint64_t)seed * 0x100000001B3ull);
 	build_scans();
 	W = C.w;

@@ -263,6 +263,9 @@ int m2dec_amd_decode_m2v_md5(const uint8_t *data, size_t len, int device, char *
  * before the first SPS; NULL detaches a borrowed one), or on GPU `device`. */
 int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be);
 int m2dec_amd_h265_set_device(void *ctx, int device);
+/* parse-ahead workers of an H.265 context (0: the whole decode on the caller's thread; default
+ * M2DEC_AMD_H265_THREADS, 8); call before the first picture */
+int m2dec_amd_h265_set_threads(void *ctx, int threads);
 /* Free the heap and device state an h265d_func context owns. */
 void m2dec_amd_h265_release(void *ctx);
 /* Test hook: the parsed syntax (CU modes, residual levels) of later H.265 decodes into `path`, in

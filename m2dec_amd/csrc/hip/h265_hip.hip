@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <vector>
 #include "m2d_recon.h"
 #include "h265_dec.h"
 
@@ -824,51 +825,90 @@ __global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
 	dst[(size_t)y * W + (size_t)x * step] = (uint8_t)clampi(v + o, 0, 255);
 }
 
-/* ------------------------------------------------------------------ runtime */
+/* ------------------------------------------------------------------ runtime
+ * Pictures are dealt over up to 4 HIP streams (M2DEC_AMD_H265_STREAMS, default 4), each with its own record
+ * arenas, scratch words and SAO copy buffer.  Dependencies between pictures are host-ordered with events (no
+ * kernel waits on another launch, so nothing here needs a workgroup budget):
+ *   - read-after-write: a P / B picture's stream waits for the kernels of every reference frame's last picture;
+ *   - write-after-read / -write: a picture's stream waits for the pictures that read its frame's previous
+ *     content (their kernels) and for that content's copy-out to the staging buffer.
+ * Independent pictures (an all-intra stream, the B pictures of one hierarchy level) then reconstruct side by
+ * side: a 1080p CTU-row kernel has 17 workgroups, far from filling 256 CUs. */
 struct H265Gpu {
-	int dev = 0, cus = 0;
-	hipStream_t st = nullptr;
+	static const int NS = 4;
+	static const int NEV = 512; /* recycled per-picture events: far more than a dependency can span */
+	int dev = 0, cus = 0, ns = NS;
+	hipStream_t st[NS] = {};
 	int W = 0, H = 0, n = 0;
 	size_t fsz = 0;
-	uint8_t *frames = nullptr, *copy = nullptr;
+	uint8_t *frames = nullptr;
 	m2d_frame_t caller[H265R_MAX_FRAMES];
 	uint8_t *stg[H265R_MAX_FRAMES] = {};
-	hipEvent_t ev[H265R_MAX_FRAMES] = {};
+	hipEvent_t ev[H265R_MAX_FRAMES] = {};   /* the frame's copy to staging is complete */
 	bool pend[H265R_MAX_FRAMES] = {};
-	int *scratch = nullptr; /* done flags + the block counter */
+	hipEvent_t kdone[H265R_MAX_FRAMES] = {}; /* the kernels of the frame's last picture are done (null: none) */
+	std::vector<hipEvent_t> readers[H265R_MAX_FRAMES]; /* kernels of the pictures that read the frame's content */
+	hipEvent_t evr[NEV] = {};
+	int ev_next = 0;
 	int *err = nullptr;     /* sticky error word */
-	size_t scratch_n = 0;
 	struct Arena {
 		uint8_t *host = nullptr, *dev = nullptr;
 		size_t size = 0;
 		H265Args *args = nullptr;
 		hipEvent_t used = nullptr;
-	} ar[2];
-	int next = 0;
-	/* timing */
-	hipEvent_t t0[2] = {}, t1[2] = {};
+	};
+	struct Lane {
+		uint8_t *copy = nullptr; /* the deblocked frame (SAO input) */
+		int *scratch = nullptr;  /* done flags + the block counter + CTU progress */
+		size_t scratch_n = 0;
+		Arena ar[2];
+		int next = 0;
+	} lane[NS];
+	int rr = 0;
+	/* timing: per picture, its kernels' start / end on its stream */
+	struct Timing {
+		hipEvent_t t0 = nullptr, t1 = nullptr;
+		bool pending = false;
+	} tr[32];
+	int tr_next = 0;
 	double kernel_us = 0;
 	long pictures = 0;
 	int64_t record_bytes = 0, frame_bytes = 0;
-	bool last_counted = true; /* the last submitted picture's kernel time is in kernel_us */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 };
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+static void flush_timing(H265Gpu *g, H265Gpu::Timing &t)
+{
+	if (!t.pending) return;
+	float ms = 0;
+	if (hipEventSynchronize(t.t1) == hipSuccess && hipEventElapsedTime(&ms, t.t0, t.t1) == hipSuccess) g->kernel_us += 1000.0 * ms;
+	t.pending = false;
+}
+
+static int sync_all(H265Gpu *g)
+{
+	for (int k = 0; k < g->ns; ++k) H265_CHECK(hipStreamSynchronize(g->st[k]));
+	return 0;
+}
 
 int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int height)
 {
 	H265Gpu *g = (H265Gpu *)p;
 	if (!g || n <= 0 || n > H265R_MAX_FRAMES || width <= 0 || height <= 0 || (width & 15) || (height & 15)) return -1;
 	H265_CHECK(hipSetDevice(g->dev));
-	H265_CHECK(hipStreamSynchronize(g->st));
+	if (sync_all(g) < 0) return -1;
 	const size_t fsz = ((size_t)width * height * 3 / 2 + 4095) & ~(size_t)4095;
 	if (!g->frames || fsz != g->fsz || n > g->n) {
 		if (g->frames) (void)hipFree(g->frames);
-		if (g->copy) (void)hipFree(g->copy);
-		g->frames = g->copy = nullptr;
+		g->frames = nullptr;
+		for (auto &l : g->lane) {
+			if (l.copy) (void)hipFree(l.copy);
+			l.copy = nullptr;
+		}
 		H265_CHECK(hipMalloc((void **)&g->frames, fsz * (size_t)n));
-		H265_CHECK(hipMalloc((void **)&g->copy, fsz));
+		for (int k = 0; k < g->ns; ++k) H265_CHECK(hipMalloc((void **)&g->lane[k].copy, fsz));
 		H265_CHECK(hipMemset(g->frames, 0, fsz * (size_t)n));
 	}
 	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
@@ -877,6 +917,8 @@ int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int heigh
 			g->stg[i] = nullptr;
 		}
 		g->pend[i] = false;
+		g->kdone[i] = nullptr;
+		g->readers[i].clear();
 	}
 	g->fsz = fsz;
 	g->n = n;
@@ -884,6 +926,14 @@ int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int heigh
 	g->H = height;
 	memcpy(g->caller, frames, sizeof(m2d_frame_t) * (size_t)n);
 	return 0;
+}
+
+static hipEvent_t next_event(H265Gpu *g)
+{
+	hipEvent_t &e = g->evr[g->ev_next];
+	g->ev_next = (g->ev_next + 1) % H265Gpu::NEV;
+	if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+	return e;
 }
 
 int h_submit(void *p, const h265r_picture_t *pic)
@@ -908,15 +958,36 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	}
 	/* prediction blocks: inside the frame, 4..64 samples a side, references other frames of this context */
 	if (pic->n_pu < 0 || (pic->n_pu && !pic->pu)) return -1;
+	unsigned refs = 0;
 	for (int i = 0; i < pic->n_pu; ++i) {
 		const h265r_pu_t &u = pic->pu[i];
 		if (u.w < 4 || u.h < 4 || u.w > 64 || u.h > 64 || (u.w & 3) || (u.h & 3) || (u.x & 3) || (u.y & 3) || u.x + u.w > g->W ||
 		    u.y + u.h > g->H || (u.ref[0] < 0 && u.ref[1] < 0))
 			return -1;
-		for (int l = 0; l < 2; ++l)
+		for (int l = 0; l < 2; ++l) {
 			if (u.ref[l] >= g->n || (u.ref[l] >= 0 && u.ref[l] == pic->slot)) return -1;
+			if (u.ref[l] >= 0) refs |= 1u << u.ref[l];
+		}
 	}
 	H265_CHECK(hipSetDevice(g->dev));
+	/* the stream: the first idle one after the last, else round robin */
+	int k = g->rr;
+	for (int i = 0; i < g->ns; ++i) {
+		const int c = (g->rr + i) % g->ns;
+		if (hipStreamQuery(g->st[c]) == hipSuccess) {
+			k = c;
+			break;
+		}
+	}
+	g->rr = (k + 1) % g->ns;
+	hipStream_t s = g->st[k];
+	H265Gpu::Lane &ln = g->lane[k];
+	/* dependencies on other streams' pictures */
+	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
+		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
+	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
+	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
+	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
 	const size_t units = (size_t)(g->W / 4) * (g->H / 4) + (size_t)(g->W / 8) * (g->H / 8);
 	const size_t nbs = (size_t)(g->H / 4) * (g->W / 8);
 	const int cols = (pic->pic_w + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2, rows = (pic->pic_h + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
@@ -928,14 +999,14 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	/* per-block done flags + 2 counters, then the CTU rows' progress words and the CTUs' first records */
 	const int nctu = cols * rows;
 	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + (size_t)nctu + 1;
-	if (sn > g->scratch_n) {
-		H265_CHECK(hipStreamSynchronize(g->st));
-		if (g->scratch) (void)hipFree(g->scratch);
-		H265_CHECK(hipMalloc((void **)&g->scratch, sizeof(int) * sn * 2));
-		g->scratch_n = sn * 2;
+	if (sn > ln.scratch_n) {
+		H265_CHECK(hipStreamSynchronize(s));
+		if (ln.scratch) (void)hipFree(ln.scratch);
+		H265_CHECK(hipMalloc((void **)&ln.scratch, sizeof(int) * sn * 2));
+		ln.scratch_n = sn * 2;
 	}
-	H265Gpu::Arena &a = g->ar[g->next];
-	g->next ^= 1;
+	H265Gpu::Arena &a = ln.ar[ln.next];
+	ln.next ^= 1;
 	H265_CHECK(hipEventSynchronize(a.used));
 	if (a.size < total) {
 		if (a.host) (void)hipHostFree(a.host);
@@ -960,9 +1031,9 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.bs_h = a.dev + o_bsh;
 	h.sao = (const h265r_sao_t *)(a.dev + o_sao);
 	h.frame = g->frames + (size_t)pic->slot * g->fsz;
-	h.copy = g->copy;
-	h.done = g->scratch;
-	h.counter = g->scratch + pic->n_tu;
+	h.copy = ln.copy;
+	h.done = ln.scratch;
+	h.counter = ln.scratch + pic->n_tu;
 	h.progress = h.counter + 2;
 	h.ctu_first = h.progress + rows;
 	h.ctu_cols = cols;
@@ -983,54 +1054,60 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.frames = g->frames;
 	h.fsz = g->fsz;
 	h.n_pu = pic->n_pu;
-	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, g->st));
+	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
 	g->record_bytes += (int64_t)total;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
-	H265_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, g->st));
-	H265_CHECK(hipMemsetAsync(g->scratch, 0, sizeof(int) * sn, g->st));
-	const int k = (int)(g->pictures & 1);
-	H265_CHECK(hipEventRecord(g->t0[k], g->st));
+	H265_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, s));
+	H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
+	H265Gpu::Timing &tm = g->tr[g->tr_next];
+	g->tr_next = (g->tr_next + 1) % 32;
+	flush_timing(g, tm);
+	H265_CHECK(hipEventRecord(tm.t0, s));
 	if (pic->n_pu) {
 		const int grid = pic->n_pu < g->cus * 8 ? pic->n_pu : g->cus * 8;
-		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, s, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->n_tu && g->block_kernel) {
 		const int grid = pic->n_tu < g->cus * 8 ? pic->n_tu : g->cus * 8;
-		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, g->st, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, s, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	} else if (pic->n_tu) {
-		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, g->st, (const H265Args *)a.args);
-		hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, g->st, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, s, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, s, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & H265R_PIC_DEBLOCK) {
 		const int nv = (g->H / 4) * (g->W / 8), nh = (g->H / 8) * (g->W / 4);
-		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args, 0);
-		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args, 1);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args, 0);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args, 1);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & (H265R_PIC_SAO_LUMA | H265R_PIC_SAO_CHROMA)) {
-		H265_CHECK(hipMemcpyAsync(g->copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, g->st));
+		H265_CHECK(hipMemcpyAsync(ln.copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, s));
 		const int nsa = pic->pic_w * pic->pic_h + (pic->pic_w >> 1) * (pic->pic_h >> 1) * 2;
-		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, g->st, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	}
-	H265_CHECK(hipEventRecord(g->t1[k], g->st));
-	H265_CHECK(hipEventRecord(a.used, g->st));
+	H265_CHECK(hipEventRecord(tm.t1, s));
+	tm.pending = true;
+	H265_CHECK(hipEventRecord(a.used, s));
+	/* this picture's kernels: what later readers of its frame wait for, and what the next writers of its
+	 * references' frames wait for */
+	hipEvent_t kd = next_event(g);
+	if (!kd) return -1;
+	H265_CHECK(hipEventRecord(kd, s));
+	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
+		if ((refs >> r) & 1) g->readers[r].push_back(kd);
+	g->readers[pic->slot].clear();
+	g->kdone[pic->slot] = kd;
 	/* the picture to its staging buffer, behind the kernels */
 	const int c = pic->slot;
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
 	if (!g->stg[c]) H265_CHECK(hipHostMalloc((void **)&g->stg[c], bytes, hipHostMallocDefault));
-	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, g->st));
-	H265_CHECK(hipEventRecord(g->ev[c], g->st));
+	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
+	H265_CHECK(hipEventRecord(g->ev[c], s));
 	g->pend[c] = true;
-	if (!g->last_counted) { /* the previous picture's kernel time */
-		float ms = 0;
-		if (hipEventSynchronize(g->t1[k ^ 1]) == hipSuccess && hipEventElapsedTime(&ms, g->t0[k ^ 1], g->t1[k ^ 1]) == hipSuccess)
-			g->kernel_us += 1000.0 * ms;
-	}
-	g->last_counted = false;
 	g->pictures++;
 	return 0;
 }
@@ -1062,26 +1139,31 @@ void h_destroy(void *p)
 	H265Gpu *g = (H265Gpu *)p;
 	if (!g) return;
 	(void)hipSetDevice(g->dev);
-	(void)hipStreamSynchronize(g->st);
-	for (auto &a : g->ar) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
-		if (a.args) (void)hipFree(a.args);
-		if (a.used) (void)hipEventDestroy(a.used);
+	(void)sync_all(g);
+	for (auto &l : g->lane) {
+		for (auto &a : l.ar) {
+			if (a.host) (void)hipHostFree(a.host);
+			if (a.dev) (void)hipFree(a.dev);
+			if (a.args) (void)hipFree(a.args);
+			if (a.used) (void)hipEventDestroy(a.used);
+		}
+		if (l.scratch) (void)hipFree(l.scratch);
+		if (l.copy) (void)hipFree(l.copy);
 	}
 	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
 		if (g->stg[i]) (void)hipHostFree(g->stg[i]);
 		if (g->ev[i]) (void)hipEventDestroy(g->ev[i]);
 	}
-	for (int i = 0; i < 2; ++i) {
-		if (g->t0[i]) (void)hipEventDestroy(g->t0[i]);
-		if (g->t1[i]) (void)hipEventDestroy(g->t1[i]);
+	for (auto &e : g->evr)
+		if (e) (void)hipEventDestroy(e);
+	for (auto &t : g->tr) {
+		if (t.t0) (void)hipEventDestroy(t.t0);
+		if (t.t1) (void)hipEventDestroy(t.t1);
 	}
-	if (g->scratch) (void)hipFree(g->scratch);
 	if (g->err) (void)hipFree(g->err);
 	if (g->frames) (void)hipFree(g->frames);
-	if (g->copy) (void)hipFree(g->copy);
-	(void)hipStreamDestroy(g->st);
+	for (int k = 0; k < g->ns; ++k)
+		if (g->st[k]) (void)hipStreamDestroy(g->st[k]);
 	delete g;
 }
 
@@ -1097,19 +1179,26 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	g->dev = device;
 	g->cus = prop.multiProcessorCount;
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
-	if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking) != hipSuccess) {
+	if (const char *e = getenv("M2DEC_AMD_H265_STREAMS")) g->ns = atoi(e) < 1 ? 1 : (atoi(e) > H265Gpu::NS ? H265Gpu::NS : atoi(e));
+	if (hipSetDevice(device) != hipSuccess) {
 		delete g;
 		return -1;
 	}
+	for (int k = 0; k < g->ns; ++k)
+		if (hipStreamCreateWithFlags(&g->st[k], hipStreamNonBlocking) != hipSuccess) {
+			h_destroy(g);
+			return -1;
+		}
 	for (int i = 0; i < H265R_MAX_FRAMES; ++i) (void)hipEventCreateWithFlags(&g->ev[i], hipEventDisableTiming);
-	for (int i = 0; i < 2; ++i) {
-		(void)hipEventCreate(&g->t0[i]);
-		(void)hipEventCreate(&g->t1[i]);
+	for (auto &t : g->tr) {
+		(void)hipEventCreate(&t.t0);
+		(void)hipEventCreate(&t.t1);
 	}
-	for (auto &a : g->ar) {
-		(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
-		(void)hipMalloc((void **)&a.args, sizeof(H265Args));
-	}
+	for (int k = 0; k < g->ns; ++k)
+		for (auto &a : g->lane[k].ar) {
+			(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
+			(void)hipMalloc((void **)&a.args, sizeof(H265Args));
+		}
 	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess) {
 		h_destroy(g);
 		return -1;
@@ -1124,20 +1213,16 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 
 extern "C" int m2dec_amd_h265_hip_backend_create(h265r_backend_t *out, int device) { return h265_hip_backend_create(out, device); }
 
-/* kernel time (HIP events, all but the last picture submitted), pictures, and the §8d algorithmic bytes of
- * the pictures so far: R_pic (records uploaded) and F_write (1.5 W H each); reset zeroes them */
+/* kernel time (HIP events per picture on its stream: pictures on different streams overlap, so this is the
+ * sum of the pictures' kernel latencies), pictures, and the §8d algorithmic bytes of the pictures so far: R_pic
+ * (records uploaded) and F_write (1.5 W H each); reset zeroes them */
 extern "C" int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kernel_us, int64_t *timed_pictures,
                                          int64_t *record_bytes, int64_t *frame_bytes, int reset)
 {
 	if (!be || !be->self || be->submit != h_submit) return -1;
 	H265Gpu *g = (H265Gpu *)be->self;
-	(void)hipStreamSynchronize(g->st);
-	if (!g->last_counted && g->pictures > 0) {
-		const int k = (int)((g->pictures - 1) & 1);
-		float ms = 0;
-		if (hipEventElapsedTime(&ms, g->t0[k], g->t1[k]) == hipSuccess) g->kernel_us += 1000.0 * ms;
-		g->last_counted = true;
-	}
+	(void)sync_all(g);
+	for (auto &t : g->tr) flush_timing(g, t);
 	if (kernel_us) *kernel_us = g->kernel_us;
 	if (timed_pictures) *timed_pictures = g->pictures;
 	if (record_bytes) *record_bytes = g->record_bytes;

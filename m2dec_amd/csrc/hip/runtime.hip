@@ -22,6 +22,7 @@
 #include <time.h>
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <atomic>
 #include <deque>
 #include <mutex>
@@ -100,6 +101,11 @@ struct SlotBudget {
 	int max_procs = 0, max_total = 0; /* diagnostics: the most processes / units seen holding the budget */
 	std::deque<std::pair<hipEvent_t, int>> pend; /* completion event of a launch, its units */
 	std::vector<hipEvent_t> pool;
+	/* with the shared budget, units go back as soon as their launch completes, by a reaper thread: another
+	 * process may be waiting for them while this one makes no further launch (a test driver idle while its child
+	 * decodes) */
+	std::condition_variable cv;
+	bool reaper_on = false;
 
 	/* once per device: the capacity in units and the shared segment keyed by the PCI bus id
 	 * (M2DEC_AMD_SHARE=0: a process-local budget, which is safe only while this is the one process
@@ -191,7 +197,7 @@ struct SlotBudget {
 		if (!pool.empty()) {
 			e = pool.back();
 			pool.pop_back();
-		} else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+		} else if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
 			e = nullptr;
 		}
 		return e;
@@ -202,6 +208,26 @@ struct SlotBudget {
 	{
 		std::lock_guard<std::mutex> lk(mu);
 		pend.emplace_back(e, n);
+		if (share && !reaper_on) {
+			reaper_on = true;
+			std::thread([this] { reap(); }).detach();
+		}
+		cv.notify_one();
+	}
+
+	/* the reaper: waits (blocking-sync events: no spinning core) for the oldest pending launch, returns its
+	 * units; sleeps on the condition variable while nothing is pending */
+	void reap()
+	{
+		std::unique_lock<std::mutex> lk(mu);
+		for (;;) {
+			cv.wait(lk, [this] { return !pend.empty(); });
+			hipEvent_t e = pend.front().first;
+			lk.unlock();
+			(void)hipEventSynchronize(e);
+			lk.lock();
+			retire();
+		}
 	}
 
 	void cancel(int n)

@@ -15,6 +15,8 @@
  *   - the slice's POC from the previous slice's lsb / msb (h265.cpp:736-750);
  *   - the sign-hidden coefficient is negated after dequantisation (h265.cpp:1645-1647).
  */
+#include <limits.h>
+#include <pthread.h>
 #include <setjmp.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -694,6 +696,7 @@ typedef struct {
 	const int8_t (*col_lists)[16]; /* ... and the frames of its reference lists (frameidx_record_t) */
 	h265_col_t *col_cur;       /* the current picture's motion field */
 	int col_stride;
+	struct h265_job *job;      /* parse-ahead: the job this parse runs for (CTU-row hooks), NULL sequentially */
 	int16_t blk[32 * 32];
 	int lev[32 * 32];          /* raw levels (the syntax dump only) */
 } sctx_t;
@@ -1970,8 +1973,12 @@ static void inter_setup(sctx_t *x)
 	for (size_t i = 0, n = (size_t)x->W4 * (size_t)(d->frame_h / 4); i < n; ++i) d->nb[i] = nb_outside;
 }
 
-/* slice_data (h265.cpp:4735-4845) */
-static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, const uint8_t *data, const uint8_t *end)
+static void job_row_wait(struct h265_job *j, int row);
+static void job_row_done(struct h265_job *j, int rows);
+
+/* slice_data (h265.cpp:4735-4845); job: the parse-ahead job it runs for (NULL: the caller's thread) */
+static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, const uint8_t *data, const uint8_t *end,
+                       struct h265_job *job)
 {
 	h265_dec_t *d = e->d;
 	sctx_t *x = (sctx_t *)malloc(sizeof(sctx_t));
@@ -1987,6 +1994,7 @@ static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, cons
 	x->bslice = d->sh.slice_type == 0;
 	x->col_cur = d->col[d->index];
 	x->col_stride = (s->pic_w + 15) >> 4;
+	x->job = job;
 	set_qp(x, d->sh.slice_qp);
 	/* initType (ctu_init, h265.cpp:4756) */
 	cab_init_ctx(&x->c, x->inter ? 2 - (d->sh.slice_type ^ d->sh.cabac_init_flag) : 0, d->sh.slice_qp);
@@ -2005,8 +2013,11 @@ static void slice_data(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, cons
 			/* availability at the CTU (coding_tree_unit, h265.cpp:4738): left / top inside the slice */
 			const int idx = addr - d->sh.address;
 			const int ua = ((cy == 0 || idx < s->ctb_cols) ? 10 : 0) | ((cx == 0 || idx == 0) ? 5 : 0) | 4;
+			/* parse ahead: the collocated picture's motion field is read up to this CTU row (TMVP) */
+			if (job && (cx == 0 || idx == 0)) job_row_wait(job, cy);
 			sao_syntax(x, cx, cy);
 			quad_tree(x, x0, y0, s->log2_ctb, s->pic_w - x0, imin(s->pic_h - y0, ctb), ua);
+			if (job && cx == s->ctb_cols - 1) job_row_done(job, cy + 1);
 			addr++;
 			if (addr >= s->ctb_cols * s->ctb_rows) break;
 			if (cab_terminate(&x->c)) break;
@@ -2062,6 +2073,359 @@ static void insert_dpb(h265_dec_t *d, int frame_idx, int poc, int is_idr)
 	d->dpb_size = size + 1;
 }
 
+/* the slice data of the picture in frame d->index into d->pic (records) and the frame's motion field: on the
+ * caller's thread (job NULL) or on a parse-ahead worker over the job's private view d */
+static void picture_parse(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, const uint8_t *data, const uint8_t *end,
+                          struct h265_job *job)
+{
+	h265_dec_t *d = e->d;
+	const h265_slice_t *sh = &d->sh;
+	pic_arrays(e, d->frame_w, d->frame_h, s->ctb_cols, s->ctb_rows);
+	if (g_dump) fprintf(g_dump, "pic %d\n", d->pictures);
+	d->pic.n_tu = 0;
+	d->pic.n_coef = 0;
+	d->pic.n_pu = 0;
+	slice_data(e, s, p, data, end, job);
+	h265r_picture_t *pic = &d->pic;
+	pic->width = d->frame_w;
+	pic->height = d->frame_h;
+	pic->pic_w = s->pic_w;
+	pic->pic_h = s->pic_h;
+	pic->ctb_log2 = s->log2_ctb;
+	pic->slot = d->index;
+	pic->flags = (sh->deblocking_disabled ? 0 : H265R_PIC_DEBLOCK) | (sh->sao_luma ? H265R_PIC_SAO_LUMA : 0) |
+	             (sh->sao_chroma ? H265R_PIC_SAO_CHROMA : 0);
+	pic->beta_offset = sh->beta_offset_div2 * 2;
+	pic->tc_offset = sh->tc_offset_div2 * 2;
+	pic->cb_qp_offset = p->cb_qp_offset;
+	pic->cr_qp_offset = p->cr_qp_offset;
+}
+
+/* ------------------------------------------------------------------ parse ahead
+ *
+ * The reference decodes a picture per decode_picture call on the caller's thread (h265.cpp:4898-5008).  Here
+ * the caller's thread keeps everything header-level — NAL units, parameter sets, the slice header, the frame
+ * LRU, POC, reference lists, DPB and output — in the reference's order, and hands each picture's slice data
+ * (the CABAC parse into records: ~10-20 ms for a 1080p picture) to a worker of the context's pool; parsed
+ * pictures go to the back end in decode order, by whichever worker finishes the next one.
+ *
+ * A picture's parse reads one other picture's state, the collocated picture's motion field (TMVP,
+ * h265modules.h:731-874), and of it only the CTU rows up to the current one (the bottom-right candidate is
+ * taken inside the CTU row, else the centre): a P / B picture starts once its collocated picture's parse has
+ * started and follows it row by row.  It writes its own frame's motion field, after every earlier reader and
+ * writer of that field finished.  Workers never touch the caller's context memory (which the caller may
+ * free): a job carries a private decoder view (slice header, frame geometry, the frames' POC / list
+ * snapshots, its records and maps), copies of its SPS / PPS and its slice NAL; the motion fields and the
+ * back end's copy live in the pipeline's heap state.  peek / get wait until the picture of the frame they
+ * hand out was submitted.  M2DEC_AMD_H265_THREADS (default 8; 0 = the sequential path, as with the syntax
+ * dump). */
+#define H265_RING 16
+
+enum { JOB_FREE, JOB_QUEUED, JOB_RUNNING, JOB_PARSED };
+
+typedef struct h265_job {
+	long seq;
+	int state, err;
+	h265_dec_t *w;                 /* private view: sh, index, geometry, frame_poc / col_frame, records, maps */
+	h265_sps_t sps;
+	h265_pps_t pps;
+	uint8_t *nal;
+	size_t nal_len, nal_cap, data_off;
+	long after;                    /* every job up to this seq is parsed before this one starts (-1: none) */
+	struct h265_job *col;          /* the job writing the collocated motion field, while in flight */
+	long col_seq;
+	int rows_done;                 /* CTU rows parsed; INT_MAX once the job ended */
+	struct h265_pipe *P;
+} h265_job_t;
+
+typedef struct h265_pipe {
+	pthread_mutex_t mu;
+	pthread_cond_t cv_work, cv_done;
+	pthread_t th[16];
+	int nth, started, quit, submitting;
+	h265_job_t jobs[H265_RING];    /* the job of seq s: jobs[s % H265_RING] */
+	long head;                     /* jobs dispatched */
+	long sub;                      /* jobs submitted to the back end (decode order) */
+	long parsed_below;             /* every job below this seq is parsed */
+	long col_writer[H265R_MAX_FRAMES], col_reader[H265R_MAX_FRAMES]; /* motion fields: last writer, latest reader */
+	long frame_seq[H265R_MAX_FRAMES]; /* the last picture decoded into each frame (-1: none) */
+	h265_col_t *col[H265R_MAX_FRAMES];
+	size_t cap_col;
+	h265r_backend_t be;
+	int have_be;
+	int err_seen;                  /* a picture failed: decode_picture returns -2 from now on */
+	uint64_t bins;
+} h265_pipe_t;
+
+static int pipe_threads(const h265_dec_t *d)
+{
+	if (d->threads >= 0) return d->threads > 16 ? 16 : d->threads;
+	const char *e = getenv("M2DEC_AMD_H265_THREADS");
+	const int n = e && *e ? atoi(e) : 8;
+	return n < 0 ? 0 : (n > 16 ? 16 : n);
+}
+
+/* the parse-ahead path is in use (the syntax dump is written in decode order: sequential) */
+static int pipe_on(h265_dec_t *d)
+{
+	if (d->pipe) return 1;
+	if (g_dump || !d->have_be || pipe_threads(d) == 0) return 0;
+	h265_pipe_t *P = (h265_pipe_t *)calloc(1, sizeof(h265_pipe_t));
+	if (!P) return 0;
+	pthread_mutex_init(&P->mu, NULL);
+	pthread_cond_init(&P->cv_work, NULL);
+	pthread_cond_init(&P->cv_done, NULL);
+	P->nth = pipe_threads(d);
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) P->col_writer[i] = P->col_reader[i] = P->frame_seq[i] = -1;
+	for (int i = 0; i < H265_RING; ++i) P->jobs[i].P = P;
+	P->be = d->be;
+	P->have_be = d->have_be;
+	d->pipe = P;
+	return 1;
+}
+
+static void job_row_wait(h265_job_t *j, int row)
+{
+	h265_job_t *c = j->col;
+	if (!c) return;
+	h265_pipe_t *P = j->P;
+	pthread_mutex_lock(&P->mu);
+	while (c->seq == j->col_seq && c->rows_done <= row) pthread_cond_wait(&P->cv_done, &P->mu);
+	pthread_mutex_unlock(&P->mu);
+}
+
+static void job_row_done(h265_job_t *j, int rows)
+{
+	h265_pipe_t *P = j->P;
+	pthread_mutex_lock(&P->mu);
+	j->rows_done = rows;
+	pthread_cond_broadcast(&P->cv_done);
+	pthread_mutex_unlock(&P->mu);
+}
+
+/* submit the parsed jobs that are next in decode order (mutex held; one submitter at a time, the back end's
+ * calls made outside the mutex) */
+static void pipe_submit_locked(h265_pipe_t *P)
+{
+	while (!P->submitting && P->sub < P->head && P->jobs[P->sub % H265_RING].state == JOB_PARSED) {
+		h265_job_t *j = &P->jobs[P->sub % H265_RING];
+		P->submitting = 1;
+		pthread_mutex_unlock(&P->mu);
+		int r = -1;
+		if (!j->err && P->have_be) r = P->be.submit(P->be.self, &j->w->pic);
+		pthread_mutex_lock(&P->mu);
+		if (r < 0) P->err_seen = 1;
+		P->bins += j->w->cabac_bins;
+		j->state = JOB_FREE;
+		P->sub++;
+		P->submitting = 0;
+		pthread_cond_broadcast(&P->cv_done);
+	}
+}
+
+static void job_run(h265_pipe_t *P, h265_job_t *j)
+{
+	h265_dec_t *w = j->w;
+	jmp_buf jb;
+	perr_t e;
+	e.d = w;
+	e.jb = &jb;
+	w->cabac_bins = 0;
+	if (setjmp(jb)) {
+		j->err = 1;
+		return;
+	}
+	picture_parse(&e, &j->sps, &j->pps, j->nal + j->data_off, j->nal + j->nal_len, j);
+	(void)P;
+}
+
+static void *pipe_worker(void *arg)
+{
+	h265_pipe_t *P = (h265_pipe_t *)arg;
+	pthread_mutex_lock(&P->mu);
+	for (;;) {
+		h265_job_t *j = NULL;
+		/* the oldest job whose writes may start and whose collocated picture's parse has started (a worker then
+		 * waits only on a running job: the chain of such waits ends at one that does not wait) */
+		for (long sq = P->parsed_below; sq < P->head && !j; ++sq) {
+			h265_job_t *c = &P->jobs[sq % H265_RING];
+			if (c->state != JOB_QUEUED || c->after >= P->parsed_below) continue;
+			if (c->col && c->col->seq == c->col_seq && c->col->state == JOB_QUEUED) continue;
+			j = c;
+		}
+		if (!j) {
+			if (P->quit) break;
+			pthread_cond_wait(&P->cv_work, &P->mu);
+			continue;
+		}
+		j->state = JOB_RUNNING;
+		pthread_mutex_unlock(&P->mu);
+		job_run(P, j);
+		pthread_mutex_lock(&P->mu);
+		j->state = JOB_PARSED;
+		j->rows_done = INT_MAX;
+		while (P->parsed_below < P->head && P->jobs[P->parsed_below % H265_RING].state == JOB_PARSED) P->parsed_below++;
+		pthread_cond_broadcast(&P->cv_done);
+		pthread_cond_broadcast(&P->cv_work);
+		pipe_submit_locked(P);
+	}
+	pthread_mutex_unlock(&P->mu);
+	return NULL;
+}
+
+/* wait until every dispatched picture went to the back end (before the motion fields or the back end change) */
+static void pipe_drain(h265_dec_t *d)
+{
+	h265_pipe_t *P = d->pipe;
+	if (!P) return;
+	pthread_mutex_lock(&P->mu);
+	while (P->sub < P->head) pthread_cond_wait(&P->cv_done, &P->mu);
+	pthread_mutex_unlock(&P->mu);
+}
+
+/* the motion fields of the frames, sized for the CTB-aligned frame as pic_arrays sizes them (on the caller's
+ * thread, no job in flight) */
+static size_t col_units(int fw, int fh) { return (size_t)(fw / 16) * (size_t)(fh / 16); }
+
+static int pipe_cols(h265_pipe_t *P, int fw, int fh)
+{
+	const size_t ncol = col_units(fw, fh);
+	if (ncol <= P->cap_col) return 0;
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
+		free(P->col[i]);
+		P->col[i] = (h265_col_t *)calloc(ncol, sizeof(h265_col_t));
+		if (!P->col[i]) {
+			P->cap_col = 0;
+			return -1;
+		}
+	}
+	P->cap_col = ncol;
+	return 0;
+}
+
+static int pipe_dispatch(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, size_t data_off)
+{
+	h265_dec_t *d = e->d;
+	h265_pipe_t *P = d->pipe;
+	const h265_slice_t *sh = &d->sh;
+	if (col_units(d->frame_w, d->frame_h) > P->cap_col) {
+		pipe_drain(d);
+		if (pipe_cols(P, d->frame_w, d->frame_h) < 0) return -1;
+	}
+	pthread_mutex_lock(&P->mu);
+	while (P->head - P->sub >= H265_RING && !P->err_seen) pthread_cond_wait(&P->cv_done, &P->mu);
+	const int failed = P->err_seen;
+	h265_job_t *j = &P->jobs[P->head % H265_RING];
+	pthread_mutex_unlock(&P->mu);
+	if (failed) return -1;
+	/* (the job is FREE: no worker reads it until it is queued below) */
+	if (!j->w && !(j->w = (h265_dec_t *)calloc(1, sizeof(h265_dec_t)))) return -1;
+	h265_dec_t *w = j->w;
+	if (d->unit_len + 16 > j->nal_cap) {
+		free(j->nal);
+		j->nal_cap = d->unit_len + 16 + (d->unit_len >> 2);
+		if (!(j->nal = (uint8_t *)malloc(j->nal_cap))) {
+			j->nal_cap = 0;
+			return -1;
+		}
+	}
+	memcpy(j->nal, d->unit, d->unit_len + 16); /* (next_unit zero-pads 16 bytes) */
+	j->nal_len = d->unit_len;
+	j->data_off = data_off;
+	j->sps = *s;
+	j->pps = *p;
+	j->err = 0;
+	w->sh = *sh;
+	w->index = d->index;
+	w->frame_w = d->frame_w;
+	w->frame_h = d->frame_h;
+	w->pictures = d->pictures;
+	memcpy(w->frame_poc, d->frame_poc, sizeof(w->frame_poc));
+	memcpy(w->col_frame, d->col_frame, sizeof(w->col_frame));
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) w->col[i] = P->col[i];
+	w->cap_col = P->cap_col;
+	pthread_mutex_lock(&P->mu);
+	const long sq = P->head;
+	const int idx = d->index;
+	j->seq = sq;
+	j->after = P->col_writer[idx] > P->col_reader[idx] ? P->col_writer[idx] : P->col_reader[idx];
+	j->col = NULL;
+	j->col_seq = -1;
+	if (sh->slice_type < 2) {
+		const int cf = sh->ref_frame[sh->col_from_l0 ^ 1][sh->col_ref_idx] & 7;
+		const long k = P->col_writer[cf];
+		if (k >= P->sub) { /* (in flight: not submitted yet) */
+			j->col = &P->jobs[k % H265_RING];
+			j->col_seq = k;
+		}
+		if (P->col_reader[cf] < sq) P->col_reader[cf] = sq;
+	}
+	P->col_writer[idx] = sq;
+	P->col_reader[idx] = -1;
+	P->frame_seq[idx] = sq;
+	j->rows_done = 0;
+	j->state = JOB_QUEUED;
+	P->head++;
+	while (P->started < P->nth) {
+		if (pthread_create(&P->th[P->started], NULL, pipe_worker, P) != 0) break;
+		P->started++;
+	}
+	if (!P->started) { /* no thread: parse it here */
+		pthread_mutex_unlock(&P->mu);
+		return -1;
+	}
+	pthread_cond_broadcast(&P->cv_work);
+	pthread_mutex_unlock(&P->mu);
+	return 0;
+}
+
+static void pipe_stop(h265_dec_t *d)
+{
+	h265_pipe_t *P = d->pipe;
+	if (!P) return;
+	pipe_drain(d);
+	pthread_mutex_lock(&P->mu);
+	P->quit = 1;
+	pthread_cond_broadcast(&P->cv_work);
+	pthread_mutex_unlock(&P->mu);
+	for (int i = 0; i < P->started; ++i) pthread_join(P->th[i], NULL);
+	d->cabac_bins += P->bins;
+	for (int i = 0; i < H265_RING; ++i) {
+		h265_job_t *j = &P->jobs[i];
+		if (j->w) {
+			h265_dec_t *w = j->w;
+			free(w->pic.tu);
+			free(w->pic.coef);
+			free(w->pic.map);
+			free(w->pic.bs_v);
+			free(w->pic.bs_h);
+			free(w->pic.sao);
+			free(w->pic.pu);
+			free(w->cb_log2);
+			free(w->ipm);
+			free(w->nb);
+			free(w);
+		}
+		free(j->nal);
+	}
+	for (int i = 0; i < H265R_MAX_FRAMES; ++i) free(P->col[i]);
+	pthread_cond_destroy(&P->cv_work);
+	pthread_cond_destroy(&P->cv_done);
+	pthread_mutex_destroy(&P->mu);
+	free(P);
+	d->pipe = NULL;
+}
+
+/* peek / get: the picture of frame idx was submitted (its reconstruction is the back end's to wait for) */
+static void pipe_wait_frame(h265_dec_t *d, int idx)
+{
+	h265_pipe_t *P = d->pipe;
+	if (!P || idx < 0 || idx >= H265R_MAX_FRAMES) return;
+	pthread_mutex_lock(&P->mu);
+	while (P->frame_seq[idx] >= P->sub) pthread_cond_wait(&P->cv_done, &P->mu);
+	pthread_mutex_unlock(&P->mu);
+}
+
 /* slice_layer (h265.cpp:4849-4866) */
 static void slice_layer(perr_t *e, int nal_type)
 {
@@ -2101,30 +2465,12 @@ static void slice_layer(perr_t *e, int nal_type)
 			f->crop[2] = (int16_t)s->crop[2];
 			f->crop[3] = (int16_t)(s->crop[3] + f->height - s->pic_h);
 		}
-		pic_arrays(e, d->frame_w, d->frame_h, s->ctb_cols, s->ctb_rows);
-		if (g_dump) fprintf(g_dump, "pic %d\n", d->pictures);
-		d->pic.n_tu = 0;
-		d->pic.n_coef = 0;
-		d->pic.n_pu = 0;
-		{
-			const size_t pos = (size_t)(b.p - (d->unit + 2)) - (size_t)(b.bits >> 3);
-			slice_data(e, s, p, d->unit + 2 + pos, d->unit + d->unit_len);
-		}
-		{
-			h265r_picture_t *pic = &d->pic;
-			pic->width = d->frame_w;
-			pic->height = d->frame_h;
-			pic->pic_w = s->pic_w;
-			pic->pic_h = s->pic_h;
-			pic->ctb_log2 = s->log2_ctb;
-			pic->slot = d->index;
-			pic->flags = (sh->deblocking_disabled ? 0 : H265R_PIC_DEBLOCK) | (sh->sao_luma ? H265R_PIC_SAO_LUMA : 0) |
-			             (sh->sao_chroma ? H265R_PIC_SAO_CHROMA : 0);
-			pic->beta_offset = sh->beta_offset_div2 * 2;
-			pic->tc_offset = sh->tc_offset_div2 * 2;
-			pic->cb_qp_offset = p->cb_qp_offset;
-			pic->cr_qp_offset = p->cr_qp_offset;
-			if (!d->have_be || d->be.submit(d->be.self, pic) < 0) H265_ERR(e);
+		const size_t pos = (size_t)(b.p - (d->unit + 2)) - (size_t)(b.bits >> 3);
+		if (pipe_on(d)) {
+			if (pipe_dispatch(e, s, p, 2 + pos) < 0) H265_ERR(e);
+		} else {
+			picture_parse(e, s, p, d->unit + 2 + pos, d->unit + d->unit_len, NULL);
+			if (!d->have_be || d->be.submit(d->be.self, &d->pic) < 0) H265_ERR(e);
 		}
 	}
 	d->pictures++;
@@ -2158,6 +2504,7 @@ static int api_init(void *ctx, int dpb_max, int (*cb)(void *, void *), void *arg
 	d->dpb_max = 16;
 	d->dpb_output = -1;
 	d->device = 0;
+	d->threads = -1;
 	dec_bits_open(&d->stream_i, NULL);
 	return 0;
 }
@@ -2190,6 +2537,7 @@ static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, 
 	(void)work_len;
 	if (!d || n < 1 || !frames || !work) return -1;
 	const h265_sps_t *s = &d->sps[d->pps[d->sh.pps_id].sps_id];
+	pipe_drain(d); /* (the back end is reconfigured below: nothing of the old geometry may still go to it) */
 	d->num_frames = imin(n, H265R_MAX_FRAMES);
 	memcpy(d->frames, frames, sizeof(m2d_frame_t) * (size_t)d->num_frames);
 	memset(d->lru, 0, sizeof(d->lru));
@@ -2204,6 +2552,10 @@ static int api_set_frames(void *ctx, int n, m2d_frame_t *frames, uint8_t *work, 
 			return -1;
 		}
 		d->have_be = 1;
+		if (d->pipe) {
+			d->pipe->be = d->be;
+			d->pipe->have_be = 1;
+		}
 	}
 	return d->be.set_frames(d->be.self, d->num_frames, d->frames, d->frame_w, d->frame_h);
 }
@@ -2218,6 +2570,7 @@ static int api_decode_picture(void *ctx)
 	e.d = d;
 	e.jb = &jb;
 	if (setjmp(jb)) return -2;
+	if (d->pipe && __atomic_load_n(&d->pipe->err_seen, __ATOMIC_ACQUIRE)) return -2; /* (as the reference at that picture) */
 	for (;;) {
 		if (next_unit(d) < 0 || d->unit_len < 2) H265_ERR(&e);
 		const int type = (d->unit[0] >> 1) & 63;
@@ -2254,6 +2607,7 @@ static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
 	if (!d || !frame) return -1;
 	const int idx = peek_idx(d, bypass);
 	if (idx < 0) return 0;
+	pipe_wait_frame(d, idx);
 	if (d->have_be && d->be.sync_frame(d->be.self, idx) < 0) return -1;
 	*frame = d->frames[idx];
 	return 1;
@@ -2283,13 +2637,16 @@ int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be)
 {
 	h265_dec_t *d = CTX(ctx);
 	if (!d) return -1;
+	pipe_drain(d); /* (no picture in flight goes to the old back end after this) */
 	if (!be) {
+		pipe_stop(d);
 		d->have_be = 0;
 		return 0;
 	}
 	if (d->have_be && d->be.destroy) d->be.destroy(d->be.self);
 	d->be = *be;
 	d->have_be = 1;
+	if (d->pipe) d->pipe->be = d->be;
 	return 0;
 }
 
@@ -2306,6 +2663,7 @@ void m2dec_amd_h265_release(void *ctx)
 	h265_dec_t *d = CTX(ctx);
 	if (!d) return;
 	if (g_dump) fflush(g_dump);
+	pipe_stop(d);
 	if (d->have_be && d->be.destroy) d->be.destroy(d->be.self);
 	d->have_be = 0;
 	free(d->unit);
@@ -2341,4 +2699,24 @@ int m2dec_amd_h265_set_dump(const char *path)
 	return path && !g_dump ? -1 : 0;
 }
 
-uint64_t m2dec_amd_h265_cabac_bins(const void *ctx) { return ctx ? ((const h265_dec_t *)ctx)->cabac_bins : 0; }
+uint64_t m2dec_amd_h265_cabac_bins(const void *ctx)
+{
+	const h265_dec_t *d = (const h265_dec_t *)ctx;
+	if (!d) return 0;
+	uint64_t n = d->cabac_bins;
+	if (d->pipe) {
+		pthread_mutex_lock(&d->pipe->mu);
+		n += d->pipe->bins;
+		pthread_mutex_unlock(&d->pipe->mu);
+	}
+	return n;
+}
+
+/* parse-ahead workers of this context (0: sequential, on the caller's thread); before the first picture */
+int m2dec_amd_h265_set_threads(void *ctx, int threads)
+{
+	h265_dec_t *d = CTX(ctx);
+	if (!d || d->pipe) return -1;
+	d->threads = threads < 0 ? 0 : threads;
+	return 0;
+}

@@ -181,6 +181,9 @@ typedef struct h265_dec {
 	int device;
 	int pictures;
 	uint64_t cabac_bins;
+	/* parse-ahead pipeline (h265_dec.c "parse-ahead"): heap state, never caller memory; NULL = sequential */
+	struct h265_pipe *pipe;
+	int threads;              /* parse workers: -1 default (M2DEC_AMD_H265_THREADS, 8), 0 sequential */
 } h265_dec_t;
 
 /* default back end: the gfx950 reconstruction (m2dec_amd/csrc/hip/h265_hip.hip) */

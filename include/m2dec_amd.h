@@ -160,6 +160,13 @@ int m2dec_amd_configure_queues(int n);
 void m2dec_amd_release_pools(void);
 long long m2dec_amd_pinned_bytes(long long *pooled);
 
+/* NUMA placement of the library's threads (numa.c): the CPUs chosen for a GPU given its PCI bus id, from
+ * <sysfs_root>/sys/bus/pci/devices/<id>/numa_node and .../node<n>/cpulist intersected with the process's
+ * affinity (sysfs_root "" = the real sysfs); returns the CPU count written to cpus (node: -1 unknown).
+ * m2dec_amd_numa_node: the node the library's threads run on (-1: not placed; M2DEC_AMD_NUMA=0 disables). */
+int m2dec_amd_numa_cpus(const char *sysfs_root, const char *pci_bus_id, int *cpus, int max, int *node);
+int m2dec_amd_numa_node(void);
+
 /* The device-wide workgroup budget segment (devshare.c) under an arbitrary key, for tests and
  * diagnostics: open (creating it with cap_units), reserve (1 / 0), release, state, close. */
 void *m2dec_amd_share_open(const char *key, int cap_units);

@@ -35,6 +35,7 @@
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
 extern "C" void m2d_tl(int kind, long a, long b); /* timeline.c (M2DEC_AMD_TIMELINE diagnostics) */
+extern "C" void m2d_place_device(const char *bus_id); /* numa.c: the library's threads near this GPU */
 /* parcopy.c: a large host copy spread over a thread crew (h264_dec.h; declared here, C linkage) */
 extern "C" void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
 enum { M2DEC_CREW_SYNC_ = 1 }; /* = M2DEC_CREW_SYNC (h264_dec.h) */
@@ -118,10 +119,11 @@ struct SlotBudget {
 		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
 		cap_units = M2D_SHARE_UNITS_PER_CU * cus;
 		const char *e = getenv("M2DEC_AMD_SHARE");
+		char bus[64] = {0};
+		if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) != hipSuccess) bus[0] = 0;
+		if (bus[0]) m2d_place_device(bus); /* (numa.c: the library's threads near this GPU) */
 		if (!e || atoi(e)) {
-			char bus[64] = {0};
-			if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) == hipSuccess && bus[0])
-				share = m2d_share_open(bus, cap_units);
+			if (bus[0]) share = m2d_share_open(bus, cap_units);
 			if (share) cap_units = std::min(cap_units, m2d_share_cap(share));
 			else fprintf(stderr, "m2dec_amd: no shared workgroup budget for device %d (%s): process-local budget\n", dev, bus);
 		}

@@ -88,6 +88,7 @@ static void *md5_worker(void *arg)
 	for (;;) {
 		while (p->next == p->head && !p->quit) pthread_cond_wait(&p->cv_job, &p->mu);
 		if (p->next == p->head) break;
+		m2d_place_self(); /* (numa.c) */
 		/* tail mode: the parse pool is (nearly) out of work — a stream's last pictures are being parsed or
 		 * coming out: hash one frame at once, alone — 3.3 ms instead of a batch's 6.5 ms after the stream's
 		 * last output (a batch taken as the last 2-4 pictures parse ends last: r98).  While the pool is

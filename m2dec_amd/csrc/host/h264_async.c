@@ -732,6 +732,7 @@ static void *pool_worker(void *arg)
 		}
 		if (!as) {
 			pthread_cond_wait(&g_parse.cv_work, &g_parse.mu);
+			m2d_place_self(); /* (numa.c: near the GPU once a device back end exists) */
 			continue;
 		}
 		g_parse.rr = as->pnext;

@@ -447,6 +447,10 @@ void h264_async_trim(h264_dec_t *d);
 /* the process-wide job pool (h264_async.c): free every pooled job; page-locked bytes of job arenas (all, and
  * pooled) */
 void h264_async_pool_release(void);
+/* numa.c: the library's threads near the GPU of the process's first device back end (bus id from
+ * hipDeviceGetPCIBusId); each library thread calls m2d_place_self before its work */
+void m2d_place_device(const char *bus_id);
+void m2d_place_self(void);
 long long h264_async_pinned_bytes(long long *pooled);
 
 /* bitio.c */

@@ -2260,6 +2260,7 @@ static void *pipe_worker(void *arg)
 		}
 		j->state = JOB_RUNNING;
 		pthread_mutex_unlock(&P->mu);
+		m2d_place_self(); /* (numa.c) */
 		job_run(P, j);
 		pthread_mutex_lock(&P->mu);
 		j->state = JOB_PARSED;

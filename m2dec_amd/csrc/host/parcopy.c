@@ -63,6 +63,7 @@ static void *crew_main(void *arg)
 		while (c->gen == seen) pthread_cond_wait(&c->cv_go, &c->mu);
 		seen = c->gen;
 		pthread_mutex_unlock(&c->mu);
+		m2d_place_self(); /* (numa.c) */
 		par_pieces(c);
 		pthread_mutex_lock(&c->mu);
 		if (--c->busy == 0) pthread_cond_signal(&c->cv_done);

@@ -14,13 +14,19 @@ if [ "$K" = k_batch ]; then
   CMD="python3 $R/bench.py --steps 3 --warmup 0 --no-cpu-baseline --replay-only"
 elif [ "$K" = k_batch8 ]; then  # the 8-stream replay (bench gpu_recon_streams)
   CMD="python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --replay-only --replay-streams 8"
+elif [ "$K" = h265 ]; then  # the bench's H.265 intra leg: every k_h265_* kernel of its pictures
+  CMD="python3 $R/tools/h265_bench.py 2 c_h265_1080p_s1"
+elif [ "$K" = h265_pb ]; then  # the H.265 P / B leg
+  CMD="python3 $R/tools/h265_bench.py 2 c_h265_1080p_pb_s1"
 else
   CMD="python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-extras"
 fi
 # the 4th group is the wave-state split of MI355X_MICROARCH.md §PMC (quad-cycles, disjoint:
 # WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) plus VALU issue and the clock
-for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
-  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+GROUPS=(FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
+case "$K" in h265*) GROUPS=(FETCH_SIZE WRITE_SIZE) ;; esac
+for C in "${GROUPS[@]}"; do
   N=$(echo $C | tr ' ' '_')
   timeout -s KILL 240 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_$TAG/$N -o run --output-format csv -- $CMD \
     > $R/gpurun_out/pmc_${TAG}_$N.log 2>&1

@@ -23,7 +23,10 @@ def per_dispatch(d):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if not row["Kernel_Name"].startswith(KERNEL):
+            kn = row["Kernel_Name"]
+            if KERNEL == "h265" and "k_h265_" not in kn:
+                continue
+            if KERNEL != "h265" and not kn.startswith(KERNEL):
                 continue
             key = int(row["Dispatch_Id"])
             vals.setdefault(key, {})
@@ -32,18 +35,52 @@ def per_dispatch(d):
             for g in ("Grid_Size", "Grid_Size_X"):
                 if g in row and row[g]:
                     vals[key]["_grid"] = float(row[g])
+            vals[key]["_name"] = kn
     keys = sorted(vals)[1:] if KERNEL == "k_batch" else sorted(vals)  # k_batch: drop the parity-gate launch
     return [vals[k] for k in keys]
+
+
+def h265(root, label, out):
+    """The H.265 legs: every k_h265_* dispatch of the run (2 passes of the 8-picture stream + its warmup),
+    summed, per picture (one k_h265_ctu_index per picture with blocks)."""
+    out["preset"] = "c_h265_1080p_pb_s1" if label == "h265_pb" else "c_h265_1080p_s1"
+    out["frames"] = 8
+    fetch = per_dispatch(os.path.join(root, "FETCH_SIZE"))
+    write = per_dispatch(os.path.join(root, "WRITE_SIZE"))
+    pics_f = max(1, sum(1 for v in fetch if "k_h265_ctu_index" in v["_name"]))
+    pics_w = max(1, sum(1 for v in write if "k_h265_ctu_index" in v["_name"]))
+    f = sum(v["FETCH_SIZE"] for v in fetch) / pics_f
+    w = sum(v["WRITE_SIZE"] for v in write) / pics_w
+    out["pictures"] = pics_f
+    out["fetch_size_kib_per_picture"] = round(f, 1)
+    out["write_size_kib_per_picture"] = round(w, 1)
+    out["read_bytes_raw"] = int(f * 1024)
+    out["read_bytes_doubled"] = int(2 * f * 1024)
+    out["write_bytes"] = int(w * 1024)
+    by = {}
+    for v in fetch:
+        k = v["_name"].split("(")[0].replace("(anonymous namespace)::", "")
+        by[k] = by.get(k, 0.0) + v["FETCH_SIZE"] * 1024 / pics_f
+    out["read_bytes_raw_by_kernel"] = {k: int(x) for k, x in sorted(by.items())}
+    # FETCH_SIZE x 2 holds for wide coalesced streaming reads (MI355X_MICROARCH.md §HBM); the deblocking and
+    # SAO passes are such reads, the CTU kernel's sample / record reads narrower: both bounds reported,
+    # the doubled figure (the upper bound) as the traffic
+    out["traffic_bytes_per_picture"] = out["read_bytes_doubled"] + out["write_bytes"]
+    out["traffic_bytes_per_picture_raw"] = out["read_bytes_raw"] + out["write_bytes"]
 
 
 def main():
     global KERNEL
     root = sys.argv[1]
     label = sys.argv[2] if len(sys.argv) > 2 else "k_batch"
-    KERNEL = "k_batch" if label == "k_batch8" else label
+    KERNEL = {"k_batch8": "k_batch", "h265_pb": "h265"}.get(label, label)
     out = {"kernel": KERNEL, "source": "rocprofv3 --pmc, one pass per counter group (tools/gpu_pmc.sh)"}
     if label == "k_batch8":
         out["preset"] = "c3x8"  # bench.py gpu_recon_streams: the 8 C4 streams in one replay
+    if KERNEL == "h265":
+        h265(root, label, out)
+        print(json.dumps(out, indent=1))
+        return
     fetch = per_dispatch(os.path.join(root, "FETCH_SIZE"))
     write = per_dispatch(os.path.join(root, "WRITE_SIZE"))
     hit = per_dispatch(os.path.join(root, "TCC_HIT_sum_TCC_MISS_sum"))
@@ -51,6 +88,7 @@ def main():
         f = statistics.median(v["FETCH_SIZE"] for v in fetch)
         out["fetch_size_kib"] = f
         out["read_bytes"] = int(2 * f * 1024)
+        out["read_bytes_raw"] = int(f * 1024)  # FETCH_SIZE undoubled: the lower bound (narrow gathers)
         out["launches_read"] = len(fetch)
     if write:
         w = statistics.median(v["WRITE_SIZE"] for v in write)
@@ -58,6 +96,7 @@ def main():
         out["write_bytes"] = int(w * 1024)
     if "read_bytes" in out and "write_bytes" in out:
         out["traffic_bytes"] = out["read_bytes"] + out["write_bytes"]
+        out["traffic_bytes_raw"] = out["read_bytes_raw"] + out["write_bytes"]
     if KERNEL == "k_picture" and fetch and write and all("_grid" in v for v in fetch + write):
         # the decode path launches 1..4 pictures at once: bytes per picture (sum over launches / pictures),
         # which bench.py scales by its own pictures per launch.  A 1080p picture is 34 row-pair workgroups of
@@ -74,6 +113,8 @@ def main():
         pics_w = sum(pics_of(v["_grid"]) for v in write)
         out["traffic_bytes_per_picture"] = int(2 * 1024 * sum(v["FETCH_SIZE"] for v in fetch) / max(1.0, pics_f) +
                                               1024 * sum(v["WRITE_SIZE"] for v in write) / max(1.0, pics_w))
+        out["traffic_bytes_per_picture_raw"] = int(1024 * sum(v["FETCH_SIZE"] for v in fetch) / max(1.0, pics_f) +
+                                                  1024 * sum(v["WRITE_SIZE"] for v in write) / max(1.0, pics_w))
         out["pictures_per_launch"] = round(pics_f / len(fetch), 3)
     if hit:
         h = statistics.median(v["TCC_HIT_sum"] for v in hit)

@@ -20,6 +20,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -175,9 +176,25 @@ struct SlotBudget {
 	{
 		std::unique_lock<std::mutex> lk(mu);
 		const int want = std::min(units, cap_units);
+		double t_wait = 0;
 		for (;;) {
 			retire();
 			if (take(want)) break;
+			if (const char *lp = getenv("M2DEC_AMD_BUDGET_LOG")) { /* diagnostics: a reservation waiting long */
+				const double now = wall_s();
+				if (t_wait == 0) t_wait = now;
+				else if (now - t_wait > 0.5) {
+					int cap = 0, total = 0, mine = 0, procs = 0;
+					long rec = 0;
+					if (share) m2d_share_state(share, &cap, &total, &mine, &procs, &rec);
+					if (FILE *f = fopen(lp, "a")) {
+						fprintf(f, "pid %d: reserve %d units waits %.1f s: shared %d cap %d total %d mine %d procs %d pend %zu used_local %d\n",
+						        (int)getpid(), want, now - t_wait, share != nullptr, cap, total, mine, procs, pend.size(), used_local);
+						fclose(f);
+					}
+					t_wait = now;
+				}
+			}
 			if (!pend.empty()) {
 				hipEvent_t e = pend.front().first;
 				lk.unlock();
@@ -246,7 +263,10 @@ struct SlotBudget {
 	}
 };
 
-SlotBudget g_budget[16]; /* per device ordinal */
+/* per device ordinal; never destroyed: a static array's destructors would run at process exit and destroy the
+ * condition variable the reaper thread still waits on, and pthread_cond_destroy waits for its waiters — an
+ * exit that never ends (the round-5 GPU runs' harness hang: every picture decoded, the process never exited) */
+SlotBudget *const g_budget = new SlotBudget[16];
 
 /* M2DEC_AMD_SHARE_REPORT=1: at exit, what each device's budget saw (tests/test_gpu_cli.py's concurrent-process
  * case prints it: the overlap the decoding processes had) */

@@ -68,3 +68,22 @@ def test_cpulist_parsing(built, tmp_path, cl, want):
     node, got = _cpus(_lib(), root, BUS)
     assert node == 0
     assert got == want & os.sched_getaffinity(0) or got == os.sched_getaffinity(0)
+
+
+def test_one_thread_per_core(built, tmp_path, monkeypatch):
+    """M2DEC_AMD_NUMA_SMT=1: of each core's sibling hardware threads only the lowest is kept."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 4:
+        pytest.skip("needs 4 CPUs")
+    a, b, c, d = allowed[:4]
+    root = _sysfs(tmp_path, 0, {0: f"{a},{b},{c},{d}"})
+    for cpu, sib in ((a, f"{a},{c}"), (c, f"{a},{c}"), (b, f"{b},{d}"), (d, f"{b},{d}")):
+        t = tmp_path / "sys" / "devices" / "system" / "cpu" / f"cpu{cpu}" / "topology"
+        t.mkdir(parents=True)
+        (t / "thread_siblings_list").write_text(sib + "\n")
+    monkeypatch.setenv("M2DEC_AMD_NUMA_SMT", "1")
+    node, got = _cpus(_lib(), root, BUS)
+    assert node == 0 and got == {a, b}
+    monkeypatch.setenv("M2DEC_AMD_NUMA_SMT", "0")
+    node, got = _cpus(_lib(), root, BUS)
+    assert got == {a, b, c, d}

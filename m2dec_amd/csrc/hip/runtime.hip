@@ -216,7 +216,7 @@ struct SlotBudget {
 		if (!pool.empty()) {
 			e = pool.back();
 			pool.pop_back();
-		} else if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) {
+		} else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
 			e = nullptr;
 		}
 		return e;
@@ -234,18 +234,21 @@ struct SlotBudget {
 		cv.notify_one();
 	}
 
-	/* the reaper: waits (blocking-sync events: no spinning core) for the oldest pending launch, returns its
-	 * units; sleeps on the condition variable while nothing is pending */
+	/* the reaper: returns the units of completed launches, polling the pending launches' events every 100 us
+	 * (hipEventQuery) and sleeping on the condition variable while nothing is pending.  Not
+	 * hipEventSynchronize: a thread blocked in it holds up other threads' HIP calls on that launch's stream
+	 * (the first reaper serialised every submission behind the previous picture's completion: the end-to-end
+	 * C3 decode fell from 31 to 72 ms, one picture per launch) */
 	void reap()
 	{
 		std::unique_lock<std::mutex> lk(mu);
 		for (;;) {
 			cv.wait(lk, [this] { return !pend.empty(); });
-			hipEvent_t e = pend.front().first;
-			lk.unlock();
-			(void)hipEventSynchronize(e);
-			lk.lock();
 			retire();
+			if (pend.empty()) continue;
+			lk.unlock();
+			std::this_thread::sleep_for(std::chrono::microseconds(100));
+			lk.lock();
 		}
 	}
 
@@ -1140,8 +1143,11 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	/* pictures per launch: bounded by the budget (pics_fit) and 1 while other decode-path back ends are
 	 * alive (concurrent streams fill the budget already); the arena ring covers what can be in flight
 	 * (every arena is one pinned + device allocation: a ring larger than needed churns the pools) */
-	b->limit = g_budget[b->sc.dev & 15].contexts(0, g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed)) > 1
-	           ? 1 : std::min(b->max_held, b->sc.pics_fit);
+	const int ctxs = g_budget[b->sc.dev & 15].contexts(0, g_live_backends[b->sc.dev & 15].load(std::memory_order_relaxed));
+	b->limit = ctxs > 1 ? 1 : std::min(b->max_held, b->sc.pics_fit);
+	if (dbg_knob("M2DEC_AMD_DEBUG"))
+		fprintf(stderr, "be_set_frames: %d decode contexts on the device, %d pictures per launch (fit %d, max %d)\n", ctxs,
+		        b->limit, b->sc.pics_fit, b->max_held);
 	b->narenas = std::min(kArenas, nstreams() * b->limit + b->limit + 2);
 	if (b->next >= b->narenas) b->next = 0;
 	if (dbg_knob("M2DEC_AMD_ASYNC_STATS")) fprintf(stderr, "be_set_frames: configure %.2f ms\n", 1e3 * (wall_s() - t0));

@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include "h264_dec.h" /* bit reader (hb_*) and the CABAC range tables, shared with the H.264 parser */
 #include "h265_dec.h"
 
@@ -2157,6 +2158,13 @@ typedef struct h265_pipe {
 	uint64_t bins;
 } h265_pipe_t;
 
+static double h265_now(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 static int pipe_threads(const h265_dec_t *d)
 {
 	if (d->threads >= 0) return d->threads > 16 ? 16 : d->threads;
@@ -2261,7 +2269,9 @@ static void *pipe_worker(void *arg)
 		j->state = JOB_RUNNING;
 		pthread_mutex_unlock(&P->mu);
 		m2d_place_self(); /* (numa.c) */
+		if (getenv("M2DEC_AMD_H265_TRACE")) fprintf(stderr, "h265 job %ld start %.3f\n", j->seq, h265_now());
 		job_run(P, j);
+		if (getenv("M2DEC_AMD_H265_TRACE")) fprintf(stderr, "h265 job %ld end %.3f\n", j->seq, h265_now());
 		pthread_mutex_lock(&P->mu);
 		j->state = JOB_PARSED;
 		j->rows_done = INT_MAX;

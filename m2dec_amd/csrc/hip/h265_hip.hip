@@ -497,8 +497,21 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
 			}
 		}
-		/* the row above, once that CTU row finished the CTU above-right */
+		/* does a block of this CTU read the row above?  Only an intra-predicted block on the CTU's top edge does
+		 * (a block below it reads the tile; inter blocks start from the motion-compensated samples, an earlier
+		 * launch).  A CTU without one neither waits for the row above nor loads it: in P / B pictures, where
+		 * most CTUs hold only inter blocks, the CTU rows run side by side instead of as a 2-CTU-lag wavefront */
+		int above = 0;
 		if (row > 0) {
+			const int c = row * a.ctu_cols + col;
+			for (int k = a.ctu_first[c] + tid; k < a.ctu_first[c + 1]; k += 128) {
+				const h265r_tu_t &t = a.tu[k];
+				if ((t.flags & H265R_TU_PRED) && (t.plane ? 2 * t.y : t.y) == y0) above = 1;
+			}
+			above = __syncthreads_or(above);
+		}
+		/* the row above, once that CTU row finished the CTU above-right */
+		if (above) {
 			if (wave == 0) {
 				const int need = min(col + 2, a.ctu_cols);
 				unsigned spins = 0;

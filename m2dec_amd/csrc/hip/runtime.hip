@@ -242,9 +242,25 @@ struct SlotBudget {
 	void reap()
 	{
 		std::unique_lock<std::mutex> lk(mu);
+		std::vector<hipEvent_t> snap, done;
 		for (;;) {
 			cv.wait(lk, [this] { return !pend.empty(); });
-			retire();
+			/* the queries outside the mutex: the submitting threads reserve under it */
+			snap.clear();
+			for (auto &p : pend) snap.push_back(p.first);
+			lk.unlock();
+			done.clear();
+			for (hipEvent_t e : snap)
+				if (hipEventQuery(e) == hipSuccess) done.push_back(e);
+			lk.lock();
+			for (hipEvent_t e : done)
+				for (size_t i = 0; i < pend.size(); ++i)
+					if (pend[i].first == e) {
+						give(pend[i].second);
+						pool.push_back(e);
+						pend.erase(pend.begin() + (long)i);
+						break;
+					}
 			if (pend.empty()) continue;
 			lk.unlock();
 			std::this_thread::sleep_for(std::chrono::microseconds(100));

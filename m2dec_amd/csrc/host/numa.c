@@ -11,7 +11,7 @@
  * The node comes from sysfs: /sys/bus/pci/devices/<bus id>/numa_node (the id hipDeviceGetPCIBusId gives), its
  * CPUs from /sys/devices/system/node/node<n>/cpulist, intersected with the CPUs this process may use
  * (sched_getaffinity: a container's or a launcher's cpuset wins).  An unknown node (-1, no sysfs), an empty
- * intersection or M2DEC_AMD_NUMA=0 leaves the threads where they are.  The caller's own threads are never
+ * intersection, or the placement not asked for (M2DEC_AMD_NUMA=1) leaves the threads where they are.  The caller's own threads are never
  * moved: each library thread applies the placement to itself (m2d_place_self) when it starts and whenever the
  * placement changed since it last looked.
  */
@@ -114,8 +114,11 @@ int m2d_numa_cpus(const char *root, const char *bus_id, cpu_set_t *out)
 
 void m2d_place_device(const char *bus_id)
 {
+	/* opt-in (M2DEC_AMD_NUMA=1; bench.py sets it for its ranks when it runs on several GPUs): on the one-GPU box
+	 * the unbound threads measured steadier — NUMA off 2036 / 2048 / 2046 fps, bound to the node 2084 / 2007 /
+	 * 1451 (profiles/r121_ab_place.txt) */
 	const char *e = getenv("M2DEC_AMD_NUMA");
-	if (e && !atoi(e)) return;
+	if (!e || !atoi(e)) return;
 	cpu_set_t set;
 	const int node = m2d_numa_cpus(getenv("M2DEC_AMD_SYSFS_ROOT"), bus_id, &set);
 	pthread_mutex_lock(&g_place_mu);

@@ -23,10 +23,10 @@ else
 fi
 # the 4th group is the wave-state split of MI355X_MICROARCH.md §PMC (quad-cycles, disjoint:
 # WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) plus VALU issue and the clock
-GROUPS=(FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
+CGROUPS=(FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
-case "$K" in h265*) GROUPS=(FETCH_SIZE WRITE_SIZE) ;; esac
-for C in "${GROUPS[@]}"; do
+case "$K" in h265*) CGROUPS=(FETCH_SIZE WRITE_SIZE) ;; esac
+for C in "${CGROUPS[@]}"; do
   N=$(echo $C | tr ' ' '_')
   timeout -s KILL 240 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_$TAG/$N -o run --output-format csv -- $CMD \
     > $R/gpurun_out/pmc_${TAG}_$N.log 2>&1

@@ -4,7 +4,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_calib -o calib -- $R/tools/_build/pmc_calib || exit $?
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_calib -o calib --output-format csv -- $R/tools/_build/pmc_calib || exit $?
 python3 - "$R/gpurun_out/pmc_calib" <<'PY'
 import csv, glob, sys, collections
 per = collections.defaultdict(float)

@@ -18,7 +18,7 @@
  *   picture, then (second launch) horizontal edges: HEVC's edges 8 samples apart never touch the same
  *   sample, so every segment of a direction is independent.  Chroma rides on the luma segment (bS 2,
  *   16-sample grid).
- * k_h265_sao — one thread per sample, from a copy of the deblocked frame.
+ * k_h265_sao — one thread per 4 bytes of an NV12 row, from a copy of the deblocked frame, dword stores.
  * k_h265_mc — P / B pictures, before the blocks: one 64-lane workgroup per prediction block (grid-stride),
  *   each list's reference window ((w + 7) x (h + 7) luma bytes, (w / 2 + 3) x (h / 2 + 3) CbCr pairs, positions
  *   clamped to the picture as the reference's address_umv does) staged in LDS, then every sample computed
@@ -788,39 +788,16 @@ __global__ __launch_bounds__(256) void k_h265_deblock(const H265Args *ap, int di
 }
 
 /* ---- SAO (8.7.3; oracle/h265_oracle.c sao) */
-__global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
+/* SAO of one sample (sao_bo_block / sao_eo_block, h265.cpp:4386-4729): plane ci (0 luma, 1 Cb, 2 Cr) at sample
+ * (x, y) of a plane of pw x ph samples, `step` bytes apart in rows of W bytes; v its deblocked value */
+__device__ __forceinline__ int sao_sample(const H265Args &a, const uint8_t *src, int ci, int x, int y, int pw, int ph, int step, int v)
 {
-	const H265Args &a = *ap;
-	const int W = a.W, H = a.H;
-	const int nl = a.pic_w * a.pic_h, nc = (a.pic_w >> 1) * (a.pic_h >> 1) * 2;
-	const int id = blockIdx.x * blockDim.x + threadIdx.x;
-	if (id >= nl + nc) return;
-	int ci, x, y, pw, ph, step;
-	if (id < nl) {
-		ci = 0;
-		y = id / a.pic_w;
-		x = id - y * a.pic_w;
-		pw = a.pic_w;
-		ph = a.pic_h;
-		step = 1;
-	} else {
-		const int k = id - nl, cw = a.pic_w >> 1;
-		ci = 1 + (k & 1);
-		y = (k >> 1) / cw;
-		x = (k >> 1) - y * cw;
-		pw = cw;
-		ph = a.pic_h >> 1;
-		step = 2;
-	}
-	if (ci == 0 ? !(a.flags & H265R_PIC_SAO_LUMA) : !(a.flags & H265R_PIC_SAO_CHROMA)) return;
+	const int W = a.W;
 	const int sub = ci ? 1 : 0, cs = (1 << a.ctb_log2) >> sub;
 	const int cols = (a.pic_w + (1 << a.ctb_log2) - 1) >> a.ctb_log2;
-	const h265r_sao_t sa = a.sao[(y / cs) * cols + x / cs];
+	const h265r_sao_t &sa = a.sao[(y / cs) * cols + x / cs];
 	const int type = sa.type[ci];
-	if (!type) return;
-	const uint8_t *src = ci ? a.copy + (size_t)W * H + (ci - 1) : a.copy;
-	uint8_t *dst = ci ? a.frame + (size_t)W * H + (ci - 1) : a.frame;
-	const int v = src[(size_t)y * W + (size_t)x * step];
+	if (!type) return v;
 	int o = 0;
 	if (type == 1) {
 		const int k = (v >> 3) - sa.band[ci]; /* no band-table wrap (sao_bo_block, reference quirk) */
@@ -829,13 +806,45 @@ __global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
 		const int e = sa.eo[ci];
 		const int dx0 = e == 1 ? 0 : (e == 3 ? 1 : -1), dy0 = e == 0 ? 0 : -1;
 		const int ax = x + dx0, ay = y + dy0, bx = x - dx0, by = y - dy0;
-		if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= pw || bx >= pw || ay >= ph || by >= ph) return;
+		if (ax < 0 || ay < 0 || bx < 0 || by < 0 || ax >= pw || bx >= pw || ay >= ph || by >= ph) return v;
 		const int pa = src[(size_t)ay * W + (size_t)ax * step], pb = src[(size_t)by * W + (size_t)bx * step];
 		const int ei = 2 + (v > pa) - (v < pa) + (v > pb) - (v < pb);
 		const int cat = ei == 0 ? 1 : (ei == 1 ? 2 : (ei == 3 ? 3 : (ei == 4 ? 4 : 0)));
 		if (cat) o = sa.off[ci][cat - 1];
 	}
-	dst[(size_t)y * W + (size_t)x * step] = (uint8_t)clampi(v + o, 0, 255);
+	return clampi(v + o, 0, 255);
+}
+
+/* one thread per 4 bytes of an NV12 row (4 luma samples, or 2 CbCr pairs), from the copy of the deblocked frame,
+ * written back as one dword: bytes outside the picture or without SAO keep their (deblocked) value, which the
+ * frame already holds.  (r122: one byte store per sample wrote 21 MB per 1080p picture, PMC WRITE_SIZE;
+ * profiles/r122_pmc_h265.json) */
+__global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
+{
+	const H265Args &a = *ap;
+	const int W = a.W, H = a.H, wpr = W >> 2;
+	const int ch = a.pic_h >> 1;
+	const int id = blockIdx.x * blockDim.x + threadIdx.x;
+	if (id >= (a.pic_h + ch) * wpr) return;
+	const bool chroma = id >= a.pic_h * wpr;
+	const int row = chroma ? id / wpr - a.pic_h : id / wpr, x4 = (id % wpr) * 4;
+	if (chroma ? !(a.flags & H265R_PIC_SAO_CHROMA) : !(a.flags & H265R_PIC_SAO_LUMA)) return;
+	const uint8_t *src = a.copy + (chroma ? (size_t)W * H : 0);
+	uint8_t *dst = a.frame + (chroma ? (size_t)W * H : 0);
+	const uint32_t in = *(const uint32_t *)(src + (size_t)row * W + x4);
+	uint32_t out = 0;
+#pragma unroll
+	for (int b = 0; b < 4; ++b) {
+		int v = (int)((in >> (8 * b)) & 255);
+		if (!chroma) {
+			if (x4 + b < a.pic_w) v = sao_sample(a, src, 0, x4 + b, row, a.pic_w, a.pic_h, 1, v);
+		} else {
+			const int x = (x4 + b) >> 1, comp = (x4 + b) & 1;
+			if (x < (a.pic_w >> 1)) v = sao_sample(a, src + comp, 1 + comp, x, row, a.pic_w >> 1, ch, 2, v);
+		}
+		out |= (uint32_t)v << (8 * b);
+	}
+	if (out != in) *(uint32_t *)(dst + (size_t)row * W + x4) = out;
 }
 
 /* ------------------------------------------------------------------ runtime
@@ -1098,7 +1107,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	}
 	if (pic->flags & (H265R_PIC_SAO_LUMA | H265R_PIC_SAO_CHROMA)) {
 		H265_CHECK(hipMemcpyAsync(ln.copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, s));
-		const int nsa = pic->pic_w * pic->pic_h + (pic->pic_w >> 1) * (pic->pic_h >> 1) * 2;
+		const int nsa = (pic->pic_h + (pic->pic_h >> 1)) * (g->W >> 2); /* (4 bytes of a row per thread) */
 		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args);
 		H265_CHECK(hipGetLastError());
 	}

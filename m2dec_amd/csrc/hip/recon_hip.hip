@@ -1183,6 +1183,24 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 			if (k >= 64) return up_hi != 0;
 			return (up_mask >> k) & 1;
 		};
+		/* the row above's hand-off word this lane reads for intra MB xx (record mm), and whether it reads one:
+		 * luma wave lanes 0-2 MB xx words 0-2, lanes 3-4 MB xx+1 words 0-1, lane 5 MB xx-1 word 2; chroma wave
+		 * lanes 0-2 MB xx words 3-5, lane 3 MB xx-1 word 5.  Only the neighbours the MB's predictor may read:
+		 * its avail bits (top 2, top-right 4, top-left 8) are slice-aware (get_availability,
+		 * h264.cpp:9704-9715), so the first MB row of a slice waits for nothing of the slice above and each
+		 * slice of an I picture runs its own intra wavefront (C5's 8 slices: 8 chains of Wmb + 2 (rows of the
+		 * slice) steps instead of one of Wmb + 2 Hmb) */
+		auto handoff_src = [&](int xx, const m2r_mb_t &mm, bool &mw) -> const uint8_t * {
+			const int nw = do_luma ? 6 : 4;
+			const int xs = (t < 3) ? xx : ((do_luma && t < 5) ? xx + 1 : xx - 1);
+			const int wi = (t < 3) ? t : ((do_luma && t < 5) ? t - 3 : 2);
+			const int av = do_luma ? mm.avail_luma : mm.avail_chroma;
+			const int need = (t < 3) ? 2 : ((do_luma && t < 5) ? 4 : 8);
+			mw = y > 0 && t < nw && xs >= 0 && xs < Wmb && (av & need) && up_intra(xs);
+			return hbi + ((size_t)(y - 1) * Wmb + (mw ? xs : 0)) * HBI_BYTES + (do_luma ? 0 : 24) + wi * 8;
+		};
+		unsigned long long pv = 0; /* the hand-off word prefetched for intra MB pv_x */
+		int pv_x = -1;
 		if (cur_mask) {
 			/* the chunk's first intra MB: stage its coefficients now (later ones are prefetched) */
 			const m2r_mb_t m0 = lane_mb(mine, __builtin_ctzll(cur_mask));
@@ -1199,11 +1217,21 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 		/* prefetch the next intra MB's coefficients into registers; they land in Q[qb ^ 1] at the end */
 		int16_t qv[7];
 		int nqn = 0;
+		/* ... and its upper neighbours' hand-off words (pv, for MB pv_x): issued before this MB's body, so that
+		 * their round trip is hidden behind it when the row above is ahead (self-validating: a word without this
+		 * picture's tag yet is polled again) */
+		unsigned long long pv_next = 0;
+		int pv_next_x = -1;
 		if (cur_mask) {
 			const m2r_mb_t mn = lane_mb(mine, __builtin_ctzll(cur_mask));
 			nqn = d_mb_ncoef(mn);
 #pragma unroll
 			for (int i = 0; i < 7; ++i) qv[i] = (t + 64 * i < nqn) ? pool[mn.coef + t + 64 * i] : (int16_t)0;
+			const int xn = xb + __builtin_ctzll(cur_mask);
+			bool mw;
+			const uint8_t *ps = handoff_src(xn, mn, mw);
+			if (mw) pv_next = ld_sc1(ps);
+			pv_next_x = xn;
 		}
 		const int x0 = x * 16;
 		const int left_in_lds = (prev_x == x - 1);
@@ -1217,27 +1245,19 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 			/* the row above's hand-off words (self-validating: a word is this picture's once its tag is):
 			 * luma wave lanes 0-2 MB x words 0-2, lanes 3-4 MB x+1 words 0-1, lane 5 MB x-1 word 2;
 			 * chroma wave lanes 0-2 MB x words 3-5, lane 3 MB x-1 word 5 */
-			const int nw = do_luma ? 6 : 4;
-			const int xs = (t < 3) ? x : ((do_luma && t < 5) ? x + 1 : x - 1);
 			const int wi = (t < 3) ? t : ((do_luma && t < 5) ? t - 3 : 2);
-			/* only the neighbours this MB's predictor may read: its avail bits (top 2, top-right 4, top-left 8)
-			 * are slice-aware (get_availability, h264.cpp:9704-9715), so the first MB row of a slice waits for
-			 * nothing of the slice above and each slice of an I picture runs its own intra wavefront (C5's 8
-			 * slices: 8 chains of Wmb + 2 (rows of the slice) steps instead of one of Wmb + 2 Hmb) */
-			const int av = do_luma ? m.avail_luma : m.avail_chroma;
-			const int need = (t < 3) ? 2 : ((do_luma && t < 5) ? 4 : 8);
-			const bool mine_w = t < nw && xs >= 0 && xs < Wmb && (av & need) && up_intra(xs);
-			const uint8_t *src = hbi + ((size_t)(y - 1) * Wmb + xs) * HBI_BYTES + (do_luma ? 0 : 24) + wi * 8;
-			unsigned long long v = 0;
+			bool mine_w;
+			const uint8_t *src = handoff_src(x, m, mine_w);
+			unsigned long long v = pv_x == x ? pv : 0; /* (prefetched during the previous MB) */
 			unsigned spins = 0;
-			for (;;) {
+			for (bool first = pv_x == x;; first = false) {
 				bool ok = true;
 				if (mine_w) {
-					v = ld_sc1(src);
+					if (!first) v = ld_sc1(src);
 					ok = (uint32_t)(v >> 48) == tag;
 				}
 				if (__all(ok)) break;
-				if (!spin_ok(spins, err, 2)) break;
+				if (!first && !spin_ok(spins, err, 2)) break;
 			}
 			if (mine_w) {
 #pragma unroll
@@ -1295,6 +1315,8 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 		}
 		qb ^= 1;
 		prev_x = x;
+		pv = pv_next;
+		pv_x = pv_next_x;
 		WSYNC();
 		}
 	}

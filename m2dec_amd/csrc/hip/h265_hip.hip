@@ -187,7 +187,7 @@ struct FrameSamples {
 
 /* one block (wave-wide); Src: where neighbour samples come from and the block's samples go */
 template <class Src>
-__device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane, const Src &src)
+__device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lane, const Src &src, const int16_t *cbase, uint32_t clo)
 {
 	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
 	const int ncomp = t.plane ? 2 : 1;
@@ -299,7 +299,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 		const int kind = t.res[c];
 		int *pred = s.pred[c];
 		if (kind == H265R_RES_NONE) continue;
-		const int16_t *d = a.coef + t.coef[c];
+		const int16_t *d = cbase + (t.coef[c] - clo); /* (the pool, or the CTU's coefficients staged in LDS) */
 		if (kind == H265R_RES_DC) {
 			const int dc = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
 			for (int i = lane; i < n2; i += 64) pred[i] += dc;
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(64) void k_h265_intra(const H265Args *ap)
 			}
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sample loads below the poll */
 		}
-		do_block(a, t, s, lane, FrameSamples{a});
+		do_block(a, t, s, lane, FrameSamples{a}, a.coef, 0);
 		/* publish: the write-through sample stores drained, then the flag */
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		__hip_atomic_store((gi32 *)&a.done[idx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -445,6 +445,47 @@ struct CtuSamples {
 	}
 };
 
+/* the coefficients of records [c0, c0 + m) (staged in recs) into LDS when their pool range fits: one bulk
+ * coalesced read per CTU instead of one dependent global round trip per block.  Returns the base / offset the
+ * blocks read through. */
+#define H265_CTU_COEF 6144 /* a 64 x 64 CTU's luma + chroma coefficients */
+__device__ __forceinline__ const int16_t *stage_coef(const H265Args &a, const h265r_tu_t *recs, int m, int16_t *cc, int *red,
+                                                     int tid, uint32_t &clo)
+{
+	uint32_t lo = 0xffffffffu, hi = 0;
+	for (int k = tid; k < m; k += 128) {
+		const h265r_tu_t &t = recs[k];
+		const uint32_t n2 = 1u << (2 * t.log2);
+		for (int c = 0; c < 2; ++c)
+			if (t.res[c] != H265R_RES_NONE && (c == 0 || t.plane)) {
+				lo = min(lo, t.coef[c]);
+				hi = max(hi, t.coef[c] + n2);
+			}
+	}
+	if (tid == 0) {
+		red[0] = -1;
+		red[1] = 0;
+	}
+	__syncthreads();
+	if (lo <= hi) {
+		atomicMin((unsigned *)&red[0], lo);
+		atomicMax((unsigned *)&red[1], hi);
+	}
+	__syncthreads();
+	lo = (uint32_t)red[0];
+	hi = (uint32_t)red[1];
+	if (lo > hi || hi - lo > H265_CTU_COEF) {
+		clo = 0;
+		return a.coef;
+	}
+	const uint32_t base = lo & ~1u, nw = (hi - base + 1) >> 1; /* whole dwords from an even offset */
+	const uint32_t *src = (const uint32_t *)(a.coef + base);
+	for (uint32_t w = tid; w < nw; w += 128) ((uint32_t *)cc)[w] = src[w];
+	__syncthreads();
+	clo = base;
+	return cc;
+}
+
 /* first record of every CTU (records are in decoding order, CTUs in raster order) */
 __global__ __launch_bounds__(256) void k_h265_ctu_index(const H265Args *ap)
 {
@@ -468,6 +509,8 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 	__shared__ Lds ls[2];
 	__shared__ CtuTile tl;
 	__shared__ h265r_tu_t recs[H265_CTU_RECS]; /* the CTU's records, staged (both waves read all of them) */
+	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
+	__shared__ int red[2];
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
 	const int row = blockIdx.x;
@@ -549,10 +592,12 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 				for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += 128)
 					((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
 				__syncthreads();
+				uint32_t clo;
+				const int16_t *cb = stage_coef(a, recs, m, ccoef, red, tid, clo);
 				for (int k = 0; k < m; ++k) {
 					const h265r_tu_t t = recs[k];
 					if (t.plane != wave) continue;
-					do_block(a, t, s, lane, src);
+					do_block(a, t, s, lane, src, cb, clo);
 				}
 			}
 		}
@@ -575,6 +620,132 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 		}
 	}
 	(void)cctb;
+}
+
+/* ---- P / B pictures: one workgroup per CTU (k_h265_ctu_rows's body without the row carry).  Most CTUs of an
+ * inter picture hold only inter blocks: they start from the motion-compensated samples and add their residuals,
+ * side by side with every other CTU.  A CTU with an intra-predicted block on its left / top edge waits for the
+ * neighbour CTUs that block reads (left, above-left, above, above-right: lower raster indices, i.e. workgroups
+ * dispatched earlier, so a wait always ends) and loads their published edge samples; the row kernel's 17
+ * workgroups of a 1080p picture instead walked their 30 CTUs one after another. */
+__global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
+{
+	const H265Args a = *ap;
+	__shared__ Lds ls[2];
+	__shared__ CtuTile tl;
+	__shared__ h265r_tu_t recs[H265_CTU_RECS];
+	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
+	__shared__ int red[2];
+	const int tid = threadIdx.x, lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
+	const int c = blockIdx.x, row = c / a.ctu_cols, col = c - row * a.ctu_cols;
+	const int ctb = 1 << a.ctb_log2;
+	const int x0 = col << a.ctb_log2, y0 = row << a.ctb_log2;
+	const int rows_here = min(ctb, a.pic_h - y0), crows = rows_here >> 1, cols_here = min(ctb, a.pic_w - x0);
+	const int i0 = a.ctu_first[c], i1 = a.ctu_first[c + 1];
+	gi32 *done = (gi32 *)(a.ctu_first + a.ctu_cols * a.ctu_rows + 1);
+	__shared__ int s_need;
+	if (i0 < i1) {
+		Lds &s = ls[wave];
+		for (int i = lane; i < 32 * 32; i += 64) s.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+		/* the neighbour CTUs the CTU's edge intra blocks read: 1 left, 2 above-left, 4 above, 8 above-right */
+		int need = 0;
+		if (tid == 0) s_need = 0;
+		__syncthreads();
+		for (int k = i0 + tid; k < i1; k += 128) {
+			const h265r_tu_t &t = a.tu[k];
+			if (!(t.flags & H265R_TU_PRED)) continue;
+			const int n = 1 << t.log2, sc = t.plane ? 2 : 1, lx = sc * t.x, ly = sc * t.y;
+			const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
+			const bool top = at > 0, left = al > 0;
+			if (lx == x0 && left) need |= 1;
+			if (lx == x0 && ly == y0 && top && left) need |= 2;
+			if (ly == y0 && top) need |= 4 | (lx + sc * at > x0 + ctb ? 8 : 0);
+		}
+		if (need) atomicOr(&s_need, need);
+		__syncthreads();
+		need = s_need;
+		/* wave 0 lanes 0..3 poll one neighbour each */
+		if (wave == 0 && need) {
+			int dep = -1;
+			if (lane == 0 && (need & 1)) dep = c - 1;
+			if (lane == 1 && (need & 2)) dep = c - a.ctu_cols - 1;
+			if (lane == 2 && (need & 4)) dep = c - a.ctu_cols;
+			if (lane == 3 && (need & 8) && col + 1 < a.ctu_cols) dep = c - a.ctu_cols + 1;
+			unsigned spins = 0;
+			for (;;) {
+				const bool ok = dep < 0 || __hip_atomic_load(&done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+				if (__all(ok)) break;
+				if (++spins > H265_SPIN_LIMIT) {
+					__hip_atomic_store((gi32 *)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					break;
+				}
+				if (__hip_atomic_load((gi32 *)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+				__builtin_amdgcn_s_sleep(1);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		}
+		__syncthreads();
+		/* the motion-compensated samples (k_h265_mc, an earlier launch) */
+		if (a.n_pu) {
+			const int wpr = (cols_here + 3) >> 2;
+			for (int w = tid; w < wpr * rows_here; w += 128) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
+			}
+			for (int w = tid; w < wpr * crows; w += 128) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
+			}
+		}
+		/* the neighbours' edge samples (published as write-through words: read at agent scope) */
+		if (need & 1)
+			for (int i = tid; i < 2 * ctb; i += 128) {
+				if (i < ctb) tl.ly[i] = i < rows_here ? (uint8_t)ld_px(a, 0, 0, x0 - 1, y0 + i) : 128;
+				else tl.lc[i - ctb] = (i - ctb) < rows_here ? (uint8_t)ld_px(a, 1, (i - ctb) & 1, (x0 >> 1) - 1, (y0 >> 1) + ((i - ctb) >> 1)) : 128;
+			}
+		if (need & 14) {
+			for (int i = tid; i <= 2 * ctb; i += 128) {
+				const int x = x0 - 1 + i;
+				const bool in = x >= 0 && x < a.pic_w && (i > 0 || (need & 2)) && (i <= ctb || (need & 8));
+				tl.ty[i] = in ? (uint8_t)ld_px(a, 0, 0, x, y0 - 1) : 128;
+			}
+			for (int i = tid; i < 2 * (ctb + 1); i += 128) {
+				const int x = (x0 >> 1) - 1 + (i >> 1);
+				const bool in = x >= 0 && x < (a.pic_w >> 1) && (i > 1 || (need & 2)) && (i < ctb + 2 || (need & 8));
+				tl.tc[i] = in ? (uint8_t)ld_px(a, 1, i & 1, x, (y0 >> 1) - 1) : 128;
+			}
+		}
+		/* the CTU's blocks, luma on wave 0, chroma on wave 1, in decoding order */
+		const CtuSamples src{tl, x0, y0};
+		for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
+			const int m = min(H265_CTU_RECS, i1 - c0);
+			__syncthreads(); /* (the tile / the previous chunk) */
+			for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += 128) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
+			__syncthreads();
+			uint32_t clo;
+			const int16_t *cb = stage_coef(a, recs, m, ccoef, red, tid, clo);
+			for (int k = 0; k < m; ++k) {
+				const h265r_tu_t t = recs[k];
+				if (t.plane != wave) continue;
+				do_block(a, t, s, lane, src, cb, clo);
+			}
+		}
+		__syncthreads();
+		/* out: the CTU's samples as write-through words, drained before the done flag */
+		const int wpr = (cols_here + 3) >> 2;
+		for (int w = tid; w < wpr * rows_here; w += 128) {
+			const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+			st_word(plane_px(a, 0, 0, x0 + xx, y0 + yy), *(const uint32_t *)&tl.y[yy][xx]);
+		}
+		for (int w = tid; w < wpr * crows; w += 128) {
+			const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+			st_word(plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy), *(const uint32_t *)&tl.c[yy][xx]);
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		__syncthreads();
+	}
+	if (tid == 0) __hip_atomic_store(&done[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* ---- motion compensation (h265.cpp:3132-3595; oracle/h265_oracle.c mc_picture) */
@@ -848,7 +1019,8 @@ __global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
 }
 
 /* ------------------------------------------------------------------ runtime
- * Pictures are dealt over up to 4 HIP streams (M2DEC_AMD_H265_STREAMS, default 4), each with its own record
+ * Pictures are dealt over up to 8 HIP streams (M2DEC_AMD_H265_STREAMS; default 8 when the process has 8 hardware
+ * queues — GPU_MAX_HW_QUEUES, m2dec_amd_configure_queues — else 4), each with its own record
  * arenas, scratch words and SAO copy buffer.  Dependencies between pictures are host-ordered with events (no
  * kernel waits on another launch, so nothing here needs a workgroup budget):
  *   - read-after-write: a P / B picture's stream waits for the kernels of every reference frame's last picture;
@@ -857,7 +1029,7 @@ __global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
  * Independent pictures (an all-intra stream, the B pictures of one hierarchy level) then reconstruct side by
  * side: a 1080p CTU-row kernel has 17 workgroups, far from filling 256 CUs. */
 struct H265Gpu {
-	static const int NS = 4;
+	static const int NS = 8;
 	static const int NEV = 512; /* recycled per-picture events: far more than a dependency can span */
 	int dev = 0, cus = 0, ns = NS;
 	hipStream_t st[NS] = {};
@@ -873,10 +1045,10 @@ struct H265Gpu {
 	hipEvent_t evr[NEV] = {};
 	int ev_next = 0;
 	int *err = nullptr;     /* sticky error word */
+	int *err_host = nullptr; /* page-locked: the error word as of each frame's copy-out ([H265R_MAX_FRAMES]) */
 	struct Arena {
 		uint8_t *host = nullptr, *dev = nullptr;
 		size_t size = 0;
-		H265Args *args = nullptr;
 		hipEvent_t used = nullptr;
 	};
 	struct Lane {
@@ -896,7 +1068,9 @@ struct H265Gpu {
 	double kernel_us = 0;
 	long pictures = 0;
 	int64_t record_bytes = 0, frame_bytes = 0;
+	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
+	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
 };
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -932,6 +1106,24 @@ int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int heigh
 		H265_CHECK(hipMalloc((void **)&g->frames, fsz * (size_t)n));
 		for (int k = 0; k < g->ns; ++k) H265_CHECK(hipMalloc((void **)&g->lane[k].copy, fsz));
 		H265_CHECK(hipMemset(g->frames, 0, fsz * (size_t)n));
+	}
+	for (uint8_t *p : g->grave_host) (void)hipHostFree(p);
+	for (uint8_t *p : g->grave_dev) (void)hipFree(p);
+	g->grave_host.clear();
+	g->grave_dev.clear();
+	{
+		/* scratch words of the largest picture the frame holds: 4 x 4 luma and chroma blocks, 16 x 16 CTUs */
+		const size_t sn = (size_t)(width / 4) * (height / 4) + (size_t)(width / 8) * (height / 8) + 2 + (size_t)(height / 16 + 1) +
+		                  2 * (size_t)(width / 16 + 1) * (height / 16 + 1) + 1;
+		for (int k = 0; k < g->ns; ++k) {
+			H265Gpu::Lane &ln = g->lane[k];
+			if (sn <= ln.scratch_n) continue;
+			if (ln.scratch) (void)hipFree(ln.scratch);
+			ln.scratch = nullptr;
+			ln.scratch_n = 0;
+			H265_CHECK(hipMalloc((void **)&ln.scratch, sizeof(int) * sn));
+			ln.scratch_n = sn;
+		}
 	}
 	for (int i = 0; i < H265R_MAX_FRAMES; ++i) {
 		if (g->stg[i] && ((size_t)width * height != (size_t)g->W * g->H || i >= n)) {
@@ -1004,12 +1196,6 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	g->rr = (k + 1) % g->ns;
 	hipStream_t s = g->st[k];
 	H265Gpu::Lane &ln = g->lane[k];
-	/* dependencies on other streams' pictures */
-	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
-		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
-	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
-	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
-	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
 	const size_t units = (size_t)(g->W / 4) * (g->H / 4) + (size_t)(g->W / 8) * (g->H / 8);
 	const size_t nbs = (size_t)(g->H / 4) * (g->W / 8);
 	const int cols = (pic->pic_w + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2, rows = (pic->pic_h + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
@@ -1017,27 +1203,38 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const size_t o_map = al16(o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
 	const size_t o_bsv = al16(o_map + sizeof(int32_t) * units), o_bsh = al16(o_bsv + nbs);
 	const size_t o_sao = al16(o_bsh + nbs), o_pu = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
-	const size_t total = al16(o_pu + sizeof(h265r_pu_t) * (size_t)pic->n_pu);
-	/* per-block done flags + 2 counters, then the CTU rows' progress words and the CTUs' first records */
+	/* the kernels' argument block rides in the arena (one upload from page-locked memory: a hipMemcpyAsync
+	 * from the stack is a pageable copy, which can block this thread until the stream — waiting on other
+	 * streams' pictures — reaches it) */
+	const size_t o_args = al16(o_pu + sizeof(h265r_pu_t) * (size_t)pic->n_pu);
+	const size_t total = al16(o_args + sizeof(H265Args));
+	/* per-block done flags + 2 counters, then the CTU rows' progress words, the CTUs' first records and the CTUs'
+	 * done flags (sized for the frame at set_frames: a block is at least 4 x 4) */
 	const int nctu = cols * rows;
-	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + (size_t)nctu + 1;
-	if (sn > ln.scratch_n) {
-		H265_CHECK(hipStreamSynchronize(s));
-		if (ln.scratch) (void)hipFree(ln.scratch);
-		H265_CHECK(hipMalloc((void **)&ln.scratch, sizeof(int) * sn * 2));
-		ln.scratch_n = sn * 2;
-	}
+	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + 2 * (size_t)nctu + 1;
+	if (sn > ln.scratch_n) return -1;
+	/* the lane's arena: free once its last picture's upload and kernels are done (its own event: no wait on
+	 * the dependencies below); a larger one replaces it with headroom, the old one freed at the next
+	 * set_frames / destroy (hipFree waits for the whole device) */
 	H265Gpu::Arena &a = ln.ar[ln.next];
 	ln.next ^= 1;
 	H265_CHECK(hipEventSynchronize(a.used));
 	if (a.size < total) {
-		if (a.host) (void)hipHostFree(a.host);
-		if (a.dev) (void)hipFree(a.dev);
+		if (a.host) g->grave_host.push_back(a.host);
+		if (a.dev) g->grave_dev.push_back(a.dev);
 		a.host = a.dev = nullptr;
-		H265_CHECK(hipHostMalloc((void **)&a.host, total, hipHostMallocDefault));
-		H265_CHECK(hipMalloc((void **)&a.dev, total));
-		a.size = total;
+		a.size = 0;
+		const size_t sz = al16(total + total / 4);
+		H265_CHECK(hipHostMalloc((void **)&a.host, sz, hipHostMallocDefault));
+		H265_CHECK(hipMalloc((void **)&a.dev, sz));
+		a.size = sz;
 	}
+	/* dependencies on other streams' pictures */
+	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
+		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
+	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
+	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
+	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
 	memcpy(a.host + o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
 	memcpy(a.host + o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
 	memcpy(a.host + o_map, pic->map, sizeof(int32_t) * units);
@@ -1076,10 +1273,11 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.frames = g->frames;
 	h.fsz = g->fsz;
 	h.n_pu = pic->n_pu;
+	memcpy(a.host + o_args, &h, sizeof(h));
+	const H265Args *args = (const H265Args *)(a.dev + o_args);
 	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
-	g->record_bytes += (int64_t)total;
+	g->record_bytes += (int64_t)o_args;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
-	H265_CHECK(hipMemcpyAsync(a.args, &h, sizeof(h), hipMemcpyHostToDevice, s));
 	H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
 	H265Gpu::Timing &tm = g->tr[g->tr_next];
 	g->tr_next = (g->tr_next + 1) % 32;
@@ -1087,28 +1285,31 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipEventRecord(tm.t0, s));
 	if (pic->n_pu) {
 		const int grid = pic->n_pu < g->cus * 8 ? pic->n_pu : g->cus * 8;
-		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, s, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, s, args);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->n_tu && g->block_kernel) {
 		const int grid = pic->n_tu < g->cus * 8 ? pic->n_tu : g->cus * 8;
-		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, s, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_intra, dim3(grid), dim3(64), 0, s, args);
 		H265_CHECK(hipGetLastError());
 	} else if (pic->n_tu) {
-		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, s, (const H265Args *)a.args);
-		hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, s, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, s, args);
+		if (pic->n_pu && g->ctu_grid)
+			hipLaunchKernelGGL(k_h265_ctu_grid, dim3(nctu), dim3(128), 0, s, args);
+		else
+			hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, s, args);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & H265R_PIC_DEBLOCK) {
 		const int nv = (g->H / 4) * (g->W / 8), nh = (g->H / 8) * (g->W / 4);
-		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args, 0);
-		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args, 1);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, s, args, 0);
+		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, s, args, 1);
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & (H265R_PIC_SAO_LUMA | H265R_PIC_SAO_CHROMA)) {
 		H265_CHECK(hipMemcpyAsync(ln.copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, s));
 		const int nsa = (pic->pic_h + (pic->pic_h >> 1)) * (g->W >> 2); /* (4 bytes of a row per thread) */
-		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, s, (const H265Args *)a.args);
+		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, s, args);
 		H265_CHECK(hipGetLastError());
 	}
 	H265_CHECK(hipEventRecord(tm.t1, s));
@@ -1128,6 +1329,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
 	if (!g->stg[c]) H265_CHECK(hipHostMalloc((void **)&g->stg[c], bytes, hipHostMallocDefault));
 	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
+	H265_CHECK(hipMemcpyAsync(&g->err_host[c], g->err, sizeof(int), hipMemcpyDeviceToHost, s));
 	H265_CHECK(hipEventRecord(g->ev[c], s));
 	g->pend[c] = true;
 	g->pictures++;
@@ -1142,8 +1344,9 @@ int h_sync(void *p, int slot)
 	H265_CHECK(hipEventSynchronize(g->ev[slot]));
 	{
 		/* a block hand-off that never came (bounded spin): the sticky error word */
-		int err = 0;
-		H265_CHECK(hipMemcpy(&err, g->err, sizeof(int), hipMemcpyDeviceToHost));
+		/* (copied behind the frame on its stream: a synchronous hipMemcpy here would queue behind whatever shares
+		 * the null stream's hardware queue, and hold up the submitting thread meanwhile) */
+		const int err = __atomic_load_n(&g->err_host[slot], __ATOMIC_ACQUIRE);
 		if (err) {
 			fprintf(stderr, "m2dec_amd: H.265 block hand-off timed out on the GPU\n");
 			return -1;
@@ -1166,7 +1369,6 @@ void h_destroy(void *p)
 		for (auto &a : l.ar) {
 			if (a.host) (void)hipHostFree(a.host);
 			if (a.dev) (void)hipFree(a.dev);
-			if (a.args) (void)hipFree(a.args);
 			if (a.used) (void)hipEventDestroy(a.used);
 		}
 		if (l.scratch) (void)hipFree(l.scratch);
@@ -1178,11 +1380,14 @@ void h_destroy(void *p)
 	}
 	for (auto &e : g->evr)
 		if (e) (void)hipEventDestroy(e);
+	for (uint8_t *p : g->grave_host) (void)hipHostFree(p);
+	for (uint8_t *p : g->grave_dev) (void)hipFree(p);
 	for (auto &t : g->tr) {
 		if (t.t0) (void)hipEventDestroy(t.t0);
 		if (t.t1) (void)hipEventDestroy(t.t1);
 	}
 	if (g->err) (void)hipFree(g->err);
+	if (g->err_host) (void)hipHostFree(g->err_host);
 	if (g->frames) (void)hipFree(g->frames);
 	for (int k = 0; k < g->ns; ++k)
 		if (g->st[k]) (void)hipStreamDestroy(g->st[k]);
@@ -1201,6 +1406,11 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	g->dev = device;
 	g->cus = prop.multiProcessorCount;
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
+	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
+	{
+		const char *q = getenv("GPU_MAX_HW_QUEUES");
+		g->ns = q && atoi(q) >= 8 ? 8 : 4;
+	}
 	if (const char *e = getenv("M2DEC_AMD_H265_STREAMS")) g->ns = atoi(e) < 1 ? 1 : (atoi(e) > H265Gpu::NS ? H265Gpu::NS : atoi(e));
 	if (hipSetDevice(device) != hipSuccess) {
 		delete g;
@@ -1219,12 +1429,13 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	for (int k = 0; k < g->ns; ++k)
 		for (auto &a : g->lane[k].ar) {
 			(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
-			(void)hipMalloc((void **)&a.args, sizeof(H265Args));
 		}
-	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess) {
+	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess ||
+	    hipHostMalloc((void **)&g->err_host, sizeof(int) * H265R_MAX_FRAMES, hipHostMallocDefault) != hipSuccess) {
 		h_destroy(g);
 		return -1;
 	}
+	memset(g->err_host, 0, sizeof(int) * H265R_MAX_FRAMES);
 	out->self = g;
 	out->set_frames = h_set_frames;
 	out->submit = h_submit;

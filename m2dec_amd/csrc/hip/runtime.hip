@@ -353,7 +353,8 @@ HipPool g_pool;
 /* Device buffers outlive a decoder context as well: the picture buffers (64 x 1.5 W H, 200 MB at
  * 1080p), the hand-off records and the progress words are handed to the next context of the same
  * geometry instead of hipFree + hipMalloc (several ms per context at 1080p).  Exact-size match; at
- * most 4 GiB kept per process. */
+ * most 4 GiB kept per process, least recently given out first. */
+const size_t kPoolDevBytes = (size_t)4 << 30;
 struct DevPool {
 	std::mutex mu;
 	struct Block {
@@ -361,14 +362,14 @@ struct DevPool {
 		void *p;
 		size_t n;
 	};
-	std::vector<Block> blocks;
+	std::vector<Block> blocks; /* oldest given first */
 	size_t kept = 0;
 
 	hipError_t take(int dev, void **p, size_t n)
 	{
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			for (size_t i = 0; i < blocks.size(); ++i)
+			for (size_t i = blocks.size(); i-- > 0;)
 				if (blocks[i].dev == dev && blocks[i].n == n) {
 					*p = blocks[i].p;
 					kept -= n;
@@ -378,18 +379,27 @@ struct DevPool {
 		}
 		return hipMalloc(p, n);
 	}
+	/* over the cap, the OLDEST blocks go, not the one given: a 4K stream after 1080p ones keeps its own
+	 * buffers (the 1080p ones it will not take are what leaves) */
 	void give(int dev, void *p, size_t n)
 	{
 		if (!p) return;
+		std::vector<void *> drop;
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			if (kept + n <= ((size_t)4 << 30)) {
+			if (n <= kPoolDevBytes) {
+				while (!blocks.empty() && kept + n > kPoolDevBytes) {
+					drop.push_back(blocks.front().p);
+					kept -= blocks.front().n;
+					blocks.erase(blocks.begin());
+				}
 				blocks.push_back({dev, p, n});
 				kept += n;
-				return;
+				p = nullptr;
 			}
 		}
-		(void)hipFree(p);
+		for (void *q : drop) (void)hipFree(q);
+		if (p) (void)hipFree(p);
 	}
 } g_dev;
 
@@ -990,38 +1000,59 @@ struct ArenaPool {
 		size_t size;
 	};
 	std::mutex mu;
-	std::vector<Block> free_blocks;
+	std::vector<Block> free_blocks; /* oldest given first */
+	size_t kept = 0;
 
+	/* the smallest block that fits (a 1080p context does not take a 4K stream's arenas), newest of those */
 	bool take(int dev, size_t need, Arena &a)
 	{
 		std::lock_guard<std::mutex> lk(mu);
-		for (size_t i = 0; i < free_blocks.size(); ++i)
-			if (free_blocks[i].dev == dev && free_blocks[i].size >= need) {
-				a.host = free_blocks[i].host;
-				a.dev = free_blocks[i].dev_ptr;
-				a.size = free_blocks[i].size;
-				free_blocks.erase(free_blocks.begin() + (long)i);
-				return true;
-			}
-		return false;
+		long best = -1;
+		for (size_t i = free_blocks.size(); i-- > 0;)
+			if (free_blocks[i].dev == dev && free_blocks[i].size >= need && (best < 0 || free_blocks[i].size < free_blocks[(size_t)best].size))
+				best = (long)i;
+		if (best < 0) return false;
+		const Block bl = free_blocks[(size_t)best];
+		free_blocks.erase(free_blocks.begin() + best);
+		kept -= bl.size;
+		a.host = bl.host;
+		a.dev = bl.dev_ptr;
+		a.size = bl.size;
+		return true;
 	}
 
+	/* at most 64 blocks / 2 GiB (page-locked + the same in HBM); over that the OLDEST go, not the one given (r5:
+	 * after the 8-stream leg's 64 1080p arenas filled the pool, each 4K decode pinned 6 new 34 MB arenas at
+	 * 5-13 ms apiece and freed them at its end: C5 80-105 ms per decode instead of 50) */
 	void give(int dev, Arena &a)
 	{
 		if (!a.host) return;
+		const size_t cap = (size_t)2 << 30;
+		std::vector<Block> drop;
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			if (free_blocks.size() < 64) {
+			if (a.size <= cap) {
+				while (!free_blocks.empty() && (free_blocks.size() >= 64 || kept + a.size > cap)) {
+					drop.push_back(free_blocks.front());
+					kept -= free_blocks.front().size;
+					free_blocks.erase(free_blocks.begin());
+				}
 				free_blocks.push_back({dev, a.host, a.dev, a.size});
+				kept += a.size;
 				a.host = a.dev = nullptr;
 				a.size = 0;
-				return;
 			}
 		}
-		(void)hipHostFree(a.host);
-		(void)hipFree(a.dev);
-		a.host = a.dev = nullptr;
-		a.size = 0;
+		for (auto &bl : drop) {
+			(void)hipHostFree(bl.host);
+			(void)hipFree(bl.dev_ptr);
+		}
+		if (a.host) {
+			(void)hipHostFree(a.host);
+			(void)hipFree(a.dev);
+			a.host = a.dev = nullptr;
+			a.size = 0;
+		}
 	}
 };
 ArenaPool g_arenas;
@@ -1036,14 +1067,14 @@ struct TimingSlot {
  * caller has the frame. */
 struct StagePool {
 	std::mutex mu;
-	std::vector<std::pair<uint8_t *, size_t>> free_blocks;
+	std::vector<std::pair<uint8_t *, size_t>> free_blocks; /* oldest given first */
 	size_t kept = 0;
 
 	uint8_t *take(size_t need)
 	{
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			for (size_t i = 0; i < free_blocks.size(); ++i)
+			for (size_t i = free_blocks.size(); i-- > 0;)
 				if (free_blocks[i].second == need) {
 					uint8_t *p = free_blocks[i].first;
 					free_blocks.erase(free_blocks.begin() + (long)i);
@@ -1055,18 +1086,27 @@ struct StagePool {
 		if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return nullptr;
 		return (uint8_t *)p;
 	}
+	/* up to 1 GiB kept for the next contexts; over that the OLDEST blocks go, not the one given */
 	void give(uint8_t *p, size_t n)
 	{
 		if (!p) return;
+		const size_t cap = (size_t)1 << 30;
+		std::vector<uint8_t *> drop;
 		{
 			std::lock_guard<std::mutex> lk(mu);
-			if (kept + n <= ((size_t)1 << 30)) { /* keep up to 1 GiB for the next contexts */
+			if (n <= cap) {
+				while (!free_blocks.empty() && kept + n > cap) {
+					drop.push_back(free_blocks.front().first);
+					kept -= free_blocks.front().second;
+					free_blocks.erase(free_blocks.begin());
+				}
 				free_blocks.emplace_back(p, n);
 				kept += n;
-				return;
+				p = nullptr;
 			}
 		}
-		(void)hipHostFree(p);
+		for (uint8_t *q : drop) (void)hipHostFree(q);
+		if (p) (void)hipHostFree(p);
 	}
 } g_stage;
 
@@ -1076,13 +1116,16 @@ struct StagePool {
  * slot (asynchronously, bind / submit), and staging -> the caller's frame on the caller's thread
  * inside sync_frame, i.e. inside peek / get_decoded_frame.  Between API calls nothing in flight
  * points into caller memory. */
+const size_t kStgTail = 64;
+
 struct HipBackend {
 	Sched sc;
 	hipStream_t copy = nullptr; /* decode ahead: bind's copies out of the picture buffers */
 	m2d_frame_t frames[64];
 	int nframes = 0;
 	uint8_t *stg[64];          /* staging buffer holding / receiving slot i's picture (null: none) */
-	size_t stg_size = 0;       /* bytes per staging buffer (1.5 W H) */
+	size_t stg_size = 0;       /* picture bytes per staging buffer (1.5 W H); the buffer has kStgTail more: the
+	                            * error word as of the copy (read after the copy's event, no hipMemcpy) */
 	hipEvent_t slot_ev[64];    /* the copy into stg[i] is complete */
 	hipEvent_t d2h_ev[64][2];  /* timing: start / end of that copy */
 	bool slot_pending[64];     /* stg[i] holds a picture not yet copied to the caller's frame */
@@ -1133,7 +1176,7 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 /* slot i's staging buffer goes back to the pool (its copy, if any, is complete) */
 void stage_drop(HipBackend *b, int i)
 {
-	g_stage.give(b->stg[i], b->stg_size);
+	g_stage.give(b->stg[i], b->stg_size + kStgTail);
 	b->stg[i] = nullptr;
 	b->slot_pending[i] = false;
 }
@@ -1173,12 +1216,13 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 /* enqueue the copy of picture buffer `cur` into slot's staging buffer on stream s (after what s waits for) */
 int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
 {
-	if (!b->stg[slot] && !(b->stg[slot] = g_stage.take(b->stg_size))) {
+	if (!b->stg[slot] && !(b->stg[slot] = g_stage.take(b->stg_size + kStgTail))) {
 		fprintf(stderr, "m2dec_amd: no pinned staging memory\n");
 		return -1;
 	}
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][0], s));
 	CHECK(hipMemcpyAsync(b->stg[slot], cur, b->stg_size, hipMemcpyDeviceToHost, s));
+	CHECK(hipMemcpyAsync(b->stg[slot] + b->stg_size, b->sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][1], s));
 	CHECK(hipEventRecord(b->slot_ev[slot], s));
 	b->slot_pending[slot] = true;
@@ -1421,7 +1465,14 @@ int be_sync(void *self, int slot)
 		m2d_tl('Y', slot, 0);
 		CHECK(hipEventSynchronize(b->slot_ev[slot]));
 		m2d_tl('y', slot, 0);
-		if (b->sc.check_err() < 0) return -1;
+		/* the error word copied behind the picture on its stream (a synchronous hipMemcpy here queues behind
+		 * whatever shares the null stream's hardware queue, per frame) */
+		int e;
+		memcpy(&e, b->stg[slot] + b->stg_size, sizeof(e));
+		if (e) {
+			fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e);
+			return -1;
+		}
 		if (b->timing) {
 			float ms;
 			if (hipEventElapsedTime(&ms, b->d2h_ev[slot][0], b->d2h_ev[slot][1]) == hipSuccess) b->sc.tm.d2h_us += ms * 1e3;
@@ -1617,6 +1668,7 @@ extern "C" void m2dec_amd_release_pools(void)
 			(void)hipFree(bl.dev_ptr);
 		}
 		g_arenas.free_blocks.clear();
+		g_arenas.kept = 0;
 	}
 	{
 		std::lock_guard<std::mutex> lk(g_stage.mu);

@@ -2220,7 +2220,10 @@ static void pipe_submit_locked(h265_pipe_t *P)
 		P->submitting = 1;
 		pthread_mutex_unlock(&P->mu);
 		int r = -1;
+		const int tr = getenv("M2DEC_AMD_H265_TRACE") != NULL;
+		if (tr) fprintf(stderr, "h265 job %ld submit %.3f\n", j->seq, h265_now());
 		if (!j->err && P->have_be) r = P->be.submit(P->be.self, &j->w->pic);
+		if (tr) fprintf(stderr, "h265 job %ld submitted %.3f\n", j->seq, h265_now());
 		pthread_mutex_lock(&P->mu);
 		if (r < 0) P->err_seen = 1;
 		P->bins += j->w->cabac_bins;

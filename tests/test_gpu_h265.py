@@ -20,3 +20,20 @@ def test_hip_h265_matches_golden(built, name):
     md5s, err = m2dec_amd.decode_h265(data, device=0)
     assert err == -2
     assert md5s == GOLD[name]["md5"]
+
+
+PB = sorted(GOLD)  # (the intra streams take the row kernel either way)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"M2DEC_AMD_H265_CTU_GRID": "0"}, {"M2DEC_AMD_H265_STREAMS": "1"},
+                                 {"M2DEC_AMD_H265_STREAMS": "8"}], ids=["rows", "one_stream", "eight_streams"])
+def test_hip_h265_inter_variants(built, monkeypatch, env):
+    """P / B pictures through the row kernel (the CTU-grid kernel's predecessor), on one stream (every
+    dependency in stream order) and on 8 streams (every one an event wait): each bit-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name in PB:
+        md5s, err = m2dec_amd.decode_h265(h265_stream(name), device=0)
+        assert err == -2
+        assert md5s == GOLD[name]["md5"], name

@@ -77,6 +77,15 @@ $(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_
 
 stamps: $(DBG_LIB)
 
+# H.265 CTU kernel stamps (tools/stamps_h265.py)
+H5S_LIB := build/dbg/libm2dec_amd_h5stamps.so
+$(H5S_LIB): $(HOST_OBJ) m2dec_amd/csrc/hip/h265_hip.hip $(HIP_HDR) build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -DH265_STAMPS -c m2dec_amd/csrc/hip/h265_hip.hip -o build/dbg/h265_hip_stamps.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/dbg/h265_hip_stamps.o -Wl,--no-undefined
+
+h5stamps: $(H5S_LIB)
+
 # diagnostic variants: make variant V=NAME FLAGS="-DX"
 variant: $(HOST_OBJ) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 	@mkdir -p build/var
@@ -86,7 +95,7 @@ variant: $(HOST_OBJ) build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.
 clean:
 	rm -rf build m2dec_amd/lib oracle/_build tools/_build
 
-.PHONY: all clean stamps variant
+.PHONY: all clean stamps variant h5stamps
 
 # inter MB phase stamps (tools/stamps_interw.py)
 STW_LIB := build/dbg/libm2dec_amd_stampw.so

@@ -32,6 +32,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <vector>
 #include "m2d_recon.h"
 #include "h265_dec.h"
@@ -65,6 +66,27 @@ struct H265Args {
 	size_t fsz;
 	int n_pu;
 };
+
+/* H265_STAMPS (build/dbg/libm2dec_amd_h5stamps.so, tools/stamps_h265.py): the CTU kernels' steps on the
+ * device's constant 100 MHz clock — per CTU its start, the end of its wait for the row above, each wave's last
+ * block and its end; per block its end with the block's size / prediction / residual kind */
+#ifdef H265_STAMPS
+#define H5ST_N (1 << 20)
+__device__ unsigned long long g_h5t[H5ST_N];
+__device__ unsigned g_h5i[H5ST_N];
+__device__ unsigned g_h5n;
+__device__ __forceinline__ void h5st(int kind, int row, int col, int aux)
+{
+	const unsigned i = atomicAdd(&g_h5n, 1u);
+	if (i < H5ST_N) {
+		g_h5t[i] = wall_clock64();
+		g_h5i[i] = (unsigned)kind | ((unsigned)row << 4) | ((unsigned)col << 12) | ((unsigned)aux << 20);
+	}
+}
+#define H5ST(lane, ...) do { if ((lane) == 0) h5st(__VA_ARGS__); } while (0)
+#else
+#define H5ST(lane, ...) do { } while (0)
+#endif
 
 __constant__ int c_cos[33] = {64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67, 64,
                               61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0};
@@ -522,6 +544,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 	for (int col = 0; col < a.ctu_cols; ++col) {
 		const int x0 = col << a.ctb_log2;
 		const int cols_here = min(ctb, a.pic_w - x0);
+		H5ST(tid, 0, row, col, 0);
 		/* the column left of this CTU: the previous CTU's last column (unavailable at col 0) */
 		if (tid < ctb) {
 			tl.ly[tid] = col ? tl.y[tid][ctb - 1] : 128;
@@ -581,6 +604,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 			}
 		}
 		__syncthreads();
+		H5ST(tid, 1, row, col, above);
 		/* the CTU's blocks, luma on wave 0, chroma on wave 1, in decoding order */
 		{
 			const CtuSamples src{tl, x0, y0};
@@ -598,9 +622,11 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 					const h265r_tu_t t = recs[k];
 					if (t.plane != wave) continue;
 					do_block(a, t, s, lane, src, cb, clo);
+					H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
 				}
 			}
 		}
+		H5ST(lane, 2, row, col, wave);
 		__syncthreads();
 		/* out: the CTU's samples (inside the picture) as write-through words, drained, then the progress word */
 		{
@@ -617,6 +643,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 			__syncthreads();
 			if (tid == 0) __hip_atomic_store((gi32 *)&a.progress[row], col + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			H5ST(tid, 3, row, col, 0);
 		}
 	}
 	(void)cctb;
@@ -1070,6 +1097,7 @@ struct H265Gpu {
 	int64_t record_bytes = 0, frame_bytes = 0;
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
+	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
 };
 
@@ -1184,6 +1212,18 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		}
 	}
 	H265_CHECK(hipSetDevice(g->dev));
+	/* M2DEC_AMD_H265_TRACE: the steps of this call that took over 0.5 ms */
+	struct timespec ts0;
+	clock_gettime(CLOCK_MONOTONIC, &ts0);
+	double tp = ts0.tv_sec * 1e3 + ts0.tv_nsec * 1e-6;
+	auto lap = [&](const char *what) {
+		if (!g->trace) return;
+		struct timespec ts;
+		clock_gettime(CLOCK_MONOTONIC, &ts);
+		const double t = ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+		if (t - tp > 0.5) fprintf(stderr, "h265 submit slot %d: %s %.2f ms\n", pic->slot, what, t - tp);
+		tp = t;
+	};
 	/* the stream: the first idle one after the last, else round robin */
 	int k = g->rr;
 	for (int i = 0; i < g->ns; ++i) {
@@ -1218,7 +1258,9 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	 * set_frames / destroy (hipFree waits for the whole device) */
 	H265Gpu::Arena &a = ln.ar[ln.next];
 	ln.next ^= 1;
+	lap("stream pick");
 	H265_CHECK(hipEventSynchronize(a.used));
+	lap("arena free");
 	if (a.size < total) {
 		if (a.host) g->grave_host.push_back(a.host);
 		if (a.dev) g->grave_dev.push_back(a.dev);
@@ -1229,12 +1271,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		H265_CHECK(hipMalloc((void **)&a.dev, sz));
 		a.size = sz;
 	}
-	/* dependencies on other streams' pictures */
-	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
-		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
-	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
-	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
-	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
+	lap("arena alloc");
 	memcpy(a.host + o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
 	memcpy(a.host + o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
 	memcpy(a.host + o_map, pic->map, sizeof(int32_t) * units);
@@ -1275,10 +1312,21 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.n_pu = pic->n_pu;
 	memcpy(a.host + o_args, &h, sizeof(h));
 	const H265Args *args = (const H265Args *)(a.dev + o_args);
+	lap("record copy");
 	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
+	lap("upload");
 	g->record_bytes += (int64_t)o_args;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
 	H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
+	lap("memset");
+	/* dependencies on other streams' pictures, after the uploads (a copy behind a wait on another stream's
+	 * picture can hold this thread until that picture completes: 8-10 ms per decode in the round-5 trace) */
+	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
+		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
+	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
+	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
+	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
+	lap("event waits");
 	H265Gpu::Timing &tm = g->tr[g->tr_next];
 	g->tr_next = (g->tr_next + 1) % 32;
 	flush_timing(g, tm);
@@ -1312,6 +1360,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		hipLaunchKernelGGL(k_h265_sao, dim3((nsa + 255) / 256), dim3(256), 0, s, args);
 		H265_CHECK(hipGetLastError());
 	}
+	lap("kernels");
 	H265_CHECK(hipEventRecord(tm.t1, s));
 	tm.pending = true;
 	H265_CHECK(hipEventRecord(a.used, s));
@@ -1331,6 +1380,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
 	H265_CHECK(hipMemcpyAsync(&g->err_host[c], g->err, sizeof(int), hipMemcpyDeviceToHost, s));
 	H265_CHECK(hipEventRecord(g->ev[c], s));
+	lap("copy-out");
 	g->pend[c] = true;
 	g->pictures++;
 	return 0;
@@ -1407,6 +1457,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	g->cus = prop.multiProcessorCount;
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
+	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");
 		g->ns = q && atoi(q) >= 8 ? 8 : 4;
@@ -1466,4 +1517,26 @@ extern "C" int m2dec_amd_h265_hip_timing(const h265r_backend_t *be, double *kern
 		g->pictures = 0;
 	}
 	return 0;
+}
+
+/* the H265_STAMPS events so far (and the count reset): returns how many, -1 in a build without them */
+extern "C" int m2dec_amd_h265_stamps(unsigned long long *t, unsigned *info, int max)
+{
+#ifdef H265_STAMPS
+	unsigned n = 0;
+	if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_h5n), sizeof(n), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+	if (n > H5ST_N) n = H5ST_N;
+	if ((int)n > max) n = (unsigned)max;
+	if (n && (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_h5t), sizeof(*t) * n, 0, hipMemcpyDeviceToHost) != hipSuccess ||
+	          hipMemcpyFromSymbol(info, HIP_SYMBOL(g_h5i), sizeof(*info) * n, 0, hipMemcpyDeviceToHost) != hipSuccess))
+		return -1;
+	const unsigned z = 0;
+	if (hipMemcpyToSymbol(HIP_SYMBOL(g_h5n), &z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+	return (int)n;
+#else
+	(void)t;
+	(void)info;
+	(void)max;
+	return -1;
+#endif
 }

@@ -637,7 +637,8 @@ struct Sched {
 	 * reads are over.  Inside the launch a picture that overwrites a slot an earlier one of the launch
 	 * read or wrote waits for it on the device (war / war_writer on the completion counters), as in a
 	 * replay batch; workgroups are dispatched in block order, so every such wait points backwards. */
-	int launch_multi(int k, const PicJob *jobs, int n, hipEvent_t *tev, hipEvent_t *inter_done, hipEvent_t *tstart = nullptr)
+	int launch_multi(int k, const PicJob *jobs, int n, hipEvent_t *tev, hipEvent_t *inter_done, hipEvent_t *tstart = nullptr,
+	                 bool slot_waits = false)
 	{
 		if (n < 1 || n > BMAX) return -1;
 		hipStream_t s = st[k];
@@ -700,6 +701,12 @@ struct Sched {
 		CHECK(hipMemsetAsync(words, 0, sizeof(int) * (2 * BMAX + (size_t)n * SCR_WORDS(Hmb, Wmb)), s));
 		/* the arguments go to device memory (pageable source: staged by the copy call) */
 		CHECK(hipMemcpyAsync(pargs + (size_t)k * BMAX, ha, sizeof(PictureArgs) * n, hipMemcpyHostToDevice, s));
+		/* slot_waits: the pictures' write-after-read / -write waits go in here, after the copies — a copy behind a
+		 * wait on another stream's launch can hold this thread until that launch completes (round-5 H.265
+		 * trace: a 4 MB record upload behind such waits returned after 8-10 ms) */
+		if (slot_waits)
+			for (int p = 0; p < n; ++p)
+				if (waits(k, jobs[p].slot, jobs[p].refs) < 0) return -1;
 		{
 			/* the device-wide workgroup budget (SlotBudget): reserve, launch, register the release */
 			SlotBudget &bg = g_budget[dev & 15];
@@ -1371,10 +1378,7 @@ int launch_held(HipBackend *b)
 	hipStream_t s = sc.st[k];
 	m2d_tl('L', n, k);
 	PicJob jobs[BMAX];
-	for (int i = 0; i < n; ++i) {
-		jobs[i] = b->held[i].j;
-		if (sc.waits(k, jobs[i].slot, jobs[i].refs) < 0) return -1;
-	}
+	for (int i = 0; i < n; ++i) jobs[i] = b->held[i].j; /* (their slot waits: launch_multi, after the uploads) */
 	TimingSlot *ts = nullptr;
 	if (b->timing) {
 		ts = &b->tr[b->tr_next];
@@ -1394,7 +1398,7 @@ int launch_held(HipBackend *b)
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	m2d_tl('M', n, k);
 	hipEvent_t inter_done;
-	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done, ts ? ts->e + 3 : nullptr) < 0) return -1;
+	if (sc.launch_multi(k, jobs, n, ts ? ts->e + 2 : nullptr, &inter_done, ts ? ts->e + 3 : nullptr, true) < 0) return -1;
 	if (sc.mark_busy(k) < 0) return -1;
 	m2d_tl('N', n, k);
 	const size_t ls = (size_t)sc.W * sc.H;

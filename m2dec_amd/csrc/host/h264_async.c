@@ -306,16 +306,25 @@ static long long g_pool_pinned; /* page-locked bytes of the pooled jobs' arenas 
 static h264_job_t *pool_take(int i);
 
 /* the pool is bounded by the page-locked bytes it keeps, not only by its job count: at ~8.5 MB per
- * 1080p job and ~27 MB per 4K job, 320 pooled jobs would keep up to 8.6 GB locked.  M2DEC_AMD_POOL_PINNED_MB
- * (default 2048: the eight concurrent 1080p streams of the bench leg keep ~1.4 GB of jobs in flight). */
+ * 1080p job and ~27 MB per 4K job, 320 pooled jobs would keep up to 8.6 GB locked.  The bound is what the
+ * process's pipelines had in flight at their peak (so the next streams of the same workload find every job
+ * they need pinned already: r5, a fixed 2 GB under the eight concurrent 1080p streams' 2.8 GB peak re-pinned
+ * ~90 jobs per pass, 8 streams 1156 fps vs 1812 before the cap), at least 2 GB, at most
+ * M2DEC_AMD_POOL_PINNED_MAX_MB (default 8192).  M2DEC_AMD_POOL_PINNED_MB fixes it instead. */
+static long long g_inuse_peak; /* page-locked bytes of jobs outside the pool, most seen (g_parse.mu) */
 static long long pool_pinned_cap(void)
 {
-	static long long cap = -1;
-	if (cap < 0) {
+	static long long fixed = -2, hard = -1;
+	if (fixed == -2) {
 		const char *e = getenv("M2DEC_AMD_POOL_PINNED_MB");
-		cap = (e && *e ? atoll(e) : 2048) << 20;
+		fixed = e && *e ? atoll(e) << 20 : -1;
+		const char *h = getenv("M2DEC_AMD_POOL_PINNED_MAX_MB");
+		hard = (h && *h ? atoll(h) : 8192) << 20;
 	}
-	return cap;
+	if (fixed >= 0) return fixed;
+	const long long base = (long long)2048 << 20;
+	const long long want = g_inuse_peak > base ? g_inuse_peak : base;
+	return want < hard ? want : hard;
 }
 
 static void job_release(h264_job_t *j) /* (mutex held; the back end no longer reads its arena) */
@@ -323,6 +332,10 @@ static void job_release(h264_job_t *j) /* (mutex held; the back end no longer re
 	if (!j) return;
 	job_clear(j);
 	const long long pin = j->arena_pinned ? (long long)j->arena_size : 0;
+	{
+		const long long inuse = __atomic_load_n(&g_pinned_bytes, __ATOMIC_RELAXED) - g_pool_pinned;
+		if (inuse > g_inuse_peak) g_inuse_peak = inuse;
+	}
 	if (pin > pool_pinned_cap()) {
 		job_free(j);
 		return;

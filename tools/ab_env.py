@@ -10,7 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r"""
 import os, sys, statistics
-sys.path.insert(0, %r)
+sys.path.insert(0, os.environ.get('AB_ROOT') or %r)
 import m2dec_amd
 from tests._streams import stream, GOLDEN
 NAME = os.environ.get('AB_STREAM', 'c3_1080p_s1')

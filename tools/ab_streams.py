@@ -11,7 +11,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r"""
 import os, sys, time, resource
-sys.path.insert(0, %r)
+sys.path.insert(0, os.environ.get('AB_ROOT') or %r)
 import m2dec_amd
 from tests._streams import stream, GOLDEN
 names = ["c3_1080p_s1"] + ["c4_1080p_s%%d" %% i for i in range(2, 9)]

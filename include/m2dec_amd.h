@@ -174,6 +174,7 @@ int m2dec_amd_share_try(void *s, int units);
 void m2dec_amd_share_release(void *s, int units);
 int m2dec_amd_share_state(void *s, int *cap, int *total, int *mine, int *procs, long *reclaimed);
 void m2dec_amd_share_close(void *s);
+int m2dec_amd_share_others_waiting(void *s);
 
 /* NV12 output MD5 exactly as FileWriterMd5 (filewrite.h:11-29, 99-124): 32 hex chars + "\r\n". */
 void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35]);

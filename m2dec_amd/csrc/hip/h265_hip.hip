@@ -161,7 +161,7 @@ __device__ __forceinline__ void wsync()
  * multiplies.  Lane: line a = lane & (N - 1) (its N inputs held in registers), output pairs b =
  * (lane >> log2 N) + k 64 / N.  COLS: pass 1 (line = column x: in[j] = src[j][x], out to dst[b][x] as
  * sat16((v + 64) >> 7)); else pass 2 (line = row y: in[j] = src[y][j], dst[y][b] += sat16((v + 2048) >> 12)). */
-template <int N, bool COLS>
+template <int N, bool COLS, bool ACC = true>
 __device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_t *mat32, int lane)
 {
 	constexpr int L = N == 8 ? 3 : (N == 16 ? 4 : 5), PAIRS = N * N / 2, PPL = PAIRS < 64 ? 1 : PAIRS / 64;
@@ -182,20 +182,23 @@ __device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_
 			if (COLS) {
 				dst[b * N + a] = sat16((e + o + 64) >> 7);
 				dst[(N - 1 - b) * N + a] = sat16((e - o + 64) >> 7);
-			} else {
+			} else if (ACC) {
 				dst[a * N + b] += sat16((e + o + 2048) >> 12);
 				dst[a * N + N - 1 - b] += sat16((e - o + 2048) >> 12);
+			} else {
+				dst[a * N + b] = sat16((e + o + 2048) >> 12);
+				dst[a * N + N - 1 - b] = sat16((e - o + 2048) >> 12);
 			}
 		}
 	}
 }
 
-template <int N>
+template <int N, bool ACC = true>
 __device__ __forceinline__ void idct_block(int *t0, int *tmp, int *pred, const int16_t *mat32, int lane)
 {
 	idct_pass<N, true>(t0, tmp, mat32, lane);
 	wsync();
-	idct_pass<N, false>(tmp, pred, mat32, lane);
+	idct_pass<N, false, ACC>(tmp, pred, mat32, lane);
 	wsync();
 }
 
@@ -467,6 +470,222 @@ struct CtuSamples {
 	}
 };
 
+/* the record with every field in scalar registers (all lanes read the same LDS record: without this the
+ * compiler keeps them in VGPRs and every size / mode / kind test is a divergent branch) */
+__device__ __forceinline__ h265r_tu_t uniform_tu(const h265r_tu_t &r)
+{
+	static_assert(sizeof(h265r_tu_t) == 24, "h265r_tu_t layout");
+	h265r_tu_t t;
+	const uint32_t *src = (const uint32_t *)&r;
+	uint32_t *dst = (uint32_t *)&t;
+#pragma unroll
+	for (int i = 0; i < 6; ++i) dst[i] = __builtin_amdgcn_readfirstlane(src[i]);
+	return t;
+}
+
+/* One block of a CTU kernel (wave-wide), the same integers as do_block in fewer wave-serial phases (round-5
+ * stamps: a 4x4 block cost ~2 us of phase latency, the CTU's ~25 luma blocks one after another):
+ *   1. the residual first, into s.pred (it does not depend on the prediction): full / DST transforms;
+ *      DC-only and transform-skip are added per sample in phase 3;
+ *   2. reference samples gathered AND filtered in one pass (each lane reads the up to three unfiltered
+ *      neighbours it needs straight from the tile), both chroma components side by side;
+ *   3. prediction + residual, clipped and stored straight into the tile, a dword per lane (4 luma samples of
+ *      a row, or 2 CbCr pairs: byte stores of neighbouring lanes collide in the LDS banks).
+ * An inter block (no prediction) adds its residual to the motion-compensated tile samples in place, or does
+ * nothing without one. */
+__device__ void do_block_ctu(const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lane, int x0, int y0, const int16_t *cbase,
+                             uint32_t clo)
+{
+	const h265r_tu_t t = uniform_tu(rec);
+	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
+	const bool luma = t.plane == 0;
+	const int ncomp = luma ? 1 : 2;
+	const int bx = luma ? t.x - x0 : t.x - (x0 >> 1), by = luma ? t.y - y0 : t.y - (y0 >> 1);
+	const CtuSamples src{tl, x0, y0};
+	/* ---- 1. transforms into s.pred[c] (residual only) */
+	int dcv[2] = {0, 0};
+	bool any_res = false;
+	for (int c = 0; c < ncomp; ++c) {
+		const int kind = t.res[c];
+		if (kind == H265R_RES_NONE) continue;
+		any_res = true;
+		const int16_t *d = cbase + (t.coef[c] - clo);
+		if (kind == H265R_RES_DC) {
+			dcv[c] = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
+			continue;
+		}
+		if (kind == H265R_RES_SKIP) continue; /* (per sample in phase 3) */
+		int *res = s.pred[c];
+		for (int i = lane; i < n2; i += 64) s.t0[i] = d[i];
+		const bool dstm = kind == H265R_RES_DST;
+		if (!dstm && n >= 8) {
+			wsync();
+			if (n == 8) idct_block<8, false>(s.t0, s.mat, res, s.mat32, lane);
+			else if (n == 16) idct_block<16, false>(s.t0, s.mat, res, s.mat32, lane);
+			else idct_block<32, false>(s.t0, s.mat, res, s.mat32, lane);
+			continue;
+		}
+		for (int i = lane; i < n2; i += 64) {
+			const int k = i >> log2, sm = i & (n - 1);
+			s.mat[i] = dstm ? c_dst[k * 4 + sm] : s.mat32[(k << (5 - log2)) * 32 + sm];
+		}
+		wsync();
+		int g[16];
+		for (int r = 0, i = lane; i < n2; i += 64, ++r) {
+			const int x = i & (n - 1), y = i >> log2;
+			int e = 0;
+			for (int j = 0; j < n; ++j) e += s.mat[j * n + y] * s.t0[j * n + x];
+			g[r] = sat16((e + 64) >> 7);
+		}
+		wsync();
+		for (int r = 0, i = lane; i < n2; i += 64, ++r) s.t0[i] = g[r];
+		wsync();
+		for (int i = lane; i < n2; i += 64) {
+			const int x = i & (n - 1), y = i >> log2;
+			int e = 0;
+			for (int j = 0; j < n; ++j) e += s.mat[j * n + x] * s.t0[y * n + j];
+			res[i] = sat16((e + 2048) >> 12);
+		}
+		wsync();
+	}
+	auto resid = [&](int c, int i) -> int {
+		const int kind = t.res[c];
+		if (kind == H265R_RES_NONE) return 0;
+		if (kind == H265R_RES_DC) return dcv[c];
+		if (kind == H265R_RES_SKIP) return (cbase[t.coef[c] - clo + i] + 16) >> 5;
+		return s.pred[c][i];
+	};
+	if (!(t.flags & H265R_TU_PRED)) {
+		/* inter: the residual onto the motion-compensated samples, a dword (4 luma samples / 2 CbCr pairs) per lane */
+		if (any_res) {
+			const int wpr = luma ? n >> 2 : n >> 1;
+			for (int w = lane; w < wpr * n; w += 64) {
+				const int y = w / wpr, xw = (w - y * wpr) * (luma ? 4 : 2);
+				uint32_t *q = luma ? (uint32_t *)&tl.y[by + y][bx + xw] : (uint32_t *)&tl.c[by + y][2 * (bx + xw)];
+				const uint32_t in = *q;
+				uint32_t out = 0;
+#pragma unroll
+				for (int b = 0; b < 4; ++b) {
+					const int c = luma ? 0 : (b & 1), x = luma ? xw + b : xw + (b >> 1);
+					const int v = (int)((in >> (8 * b)) & 255) + resid(c, y * n + x);
+					out |= (uint32_t)clampi(v, 0, 255) << (8 * b);
+				}
+				*q = out;
+			}
+			wsync();
+		}
+		return;
+	}
+	/* ---- 2. reference samples, filtered (both components side by side) */
+	const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
+	const bool top = at > 0, left = al > 0;
+	const int corner = 2 * n, last = 4 * n;
+	const int lo = left ? corner - al : (top ? corner + 1 : 0);
+	const int hi = top ? corner + at : (left ? corner - 1 : 0);
+	auto raw = [&](int c, int k) -> int {
+		if (!top && !left) return 128;
+		const int kk = clampi(k, lo, hi);
+		const int xx = kk < corner ? -1 : (kk == corner ? -1 : kk - corner - 1);
+		const int yy = kk < corner ? corner - 1 - kk : -1;
+		return src.ld(t.plane, c, t.x + xx, t.y + yy);
+	};
+	const int mode = t.mode;
+	bool filt = false;
+	if (luma && mode != 1 && n != 4) {
+		const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+		const int dist = d26 < d10 ? d26 : d10;
+		const int thres = n == 8 ? 7 : (n == 16 ? 1 : 0);
+		filt = mode == 0 || dist > thres;
+	}
+	bool strong = false;
+	int cc = 0, bl = 0, tr = 0;
+	if (filt && t.strong && n == 32) {
+		cc = raw(0, corner);
+		bl = raw(0, 0);
+		tr = raw(0, last);
+		strong = abs(cc + tr - 2 * raw(0, corner + n)) < 8 && abs(cc + bl - 2 * raw(0, corner - n)) < 8;
+	}
+	for (int i = lane; i < ncomp * (last + 1); i += 64) {
+		const int c = i > last, k = i - c * (last + 1);
+		int v;
+		if (strong) {
+			if (k > 0 && k < corner) v = ((63 - (corner - 1 - k)) * cc + (corner - k) * bl + 32) >> 6;
+			else if (k > corner && k < last) v = ((63 - (k - corner - 1)) * cc + (k - corner) * tr + 32) >> 6;
+			else v = raw(c, k);
+		} else if (filt && k > 0 && k < last) {
+			v = (raw(c, k - 1) + 2 * raw(c, k) + raw(c, k + 1) + 2) >> 2;
+		} else {
+			v = raw(c, k);
+		}
+		s.seq[c][k] = (int16_t)v;
+	}
+	wsync();
+	/* ---- 3. prediction + residual into the tile */
+#define LL(c, yy) ((int)s.seq[c][corner - 1 - (yy)]) /* p[-1][y], y >= -1 */
+#define TT(c, xx) ((int)s.seq[c][corner + 1 + (xx)]) /* p[x][-1], x >= -1 */
+	int dc[2] = {0, 0};
+	if (mode == 1) {
+		int sum0 = 0, sum1 = 0;
+		if (lane < n) {
+			sum0 = TT(0, lane) + LL(0, lane);
+			if (ncomp == 2) sum1 = TT(1, lane) + LL(1, lane);
+		}
+		for (int o = 32; o > 0; o >>= 1) {
+			sum0 += __shfl_xor(sum0, o);
+			sum1 += __shfl_xor(sum1, o);
+		}
+		dc[0] = (sum0 + n) >> (log2 + 1);
+		dc[1] = (sum1 + n) >> (log2 + 1);
+	}
+	const int ang = c_ang[mode], inv = c_inv[mode];
+	const bool vert = mode >= 18;
+	auto predict = [&](int c, int x, int y) -> int {
+		int v;
+		if (mode == 0) {
+			v = ((n - 1 - x) * LL(c, y) + (x + 1) * TT(c, n) + (n - 1 - y) * TT(c, x) + (y + 1) * LL(c, n) + n) >> (log2 + 1);
+		} else if (mode == 1) {
+			v = dc[c];
+			if (luma && n < 32) {
+				if (x == 0 && y == 0) v = (LL(c, 0) + 2 * dc[c] + TT(c, 0) + 2) >> 2;
+				else if (y == 0) v = (TT(c, x) + 3 * dc[c] + 2) >> 2;
+				else if (x == 0) v = (LL(c, y) + 3 * dc[c] + 2) >> 2;
+			}
+		} else {
+			const int p = vert ? y : x, qq = vert ? x : y;
+			const int idx = ((p + 1) * ang) >> 5, fr = ((p + 1) * ang) & 31;
+			const int k = qq + idx + 1;
+			int r1, r2;
+			if (k >= 0) r1 = vert ? TT(c, k - 1) : LL(c, k - 1);
+			else r1 = vert ? LL(c, -1 + ((k * inv + 128) >> 8)) : TT(c, -1 + ((k * inv + 128) >> 8));
+			const int k2 = k + 1;
+			if (k2 >= 0) r2 = vert ? TT(c, k2 - 1) : LL(c, k2 - 1);
+			else r2 = vert ? LL(c, -1 + ((k2 * inv + 128) >> 8)) : TT(c, -1 + ((k2 * inv + 128) >> 8));
+			v = fr ? ((32 - fr) * r1 + fr * r2 + 16) >> 5 : r1;
+			if (luma && n < 32) {
+				if (mode == 26 && x == 0) v = clampi(TT(c, 0) + ((LL(c, y) - LL(c, -1)) >> 1), 0, 255);
+				if (mode == 10 && y == 0) v = clampi(LL(c, 0) + ((TT(c, x) - TT(c, -1)) >> 1), 0, 255);
+			}
+		}
+		return clampi(v + resid(c, y * n + x), 0, 255);
+	};
+	/* a dword per lane: 4 luma samples of a row, or 2 CbCr pairs (both components) */
+	const int wpr = luma ? n >> 2 : n >> 1;
+	for (int w = lane; w < wpr * n; w += 64) {
+		const int y = w / wpr, xw = (w - y * wpr) * (luma ? 4 : 2);
+		uint32_t out = 0;
+#pragma unroll
+		for (int b = 0; b < 4; ++b) {
+			const int c = luma ? 0 : (b & 1), x = luma ? xw + b : xw + (b >> 1);
+			out |= (uint32_t)predict(c, x, y) << (8 * b);
+		}
+		if (luma) *(uint32_t *)&tl.y[by + y][bx + xw] = out;
+		else *(uint32_t *)&tl.c[by + y][2 * (bx + xw)] = out;
+	}
+#undef LL
+#undef TT
+	wsync();
+}
+
 /* the coefficients of records [c0, c0 + m) (staged in recs) into LDS when their pool range fits: one bulk
  * coalesced read per CTU instead of one dependent global round trip per block.  Returns the base / offset the
  * blocks read through. */
@@ -621,7 +840,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 				for (int k = 0; k < m; ++k) {
 					const h265r_tu_t t = recs[k];
 					if (t.plane != wave) continue;
-					do_block(a, t, s, lane, src, cb, clo);
+					do_block_ctu(t, tl, s, lane, x0, y0, cb, clo);
 					H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
 				}
 			}
@@ -755,7 +974,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
 			for (int k = 0; k < m; ++k) {
 				const h265r_tu_t t = recs[k];
 				if (t.plane != wave) continue;
-				do_block(a, t, s, lane, src, cb, clo);
+				do_block_ctu(t, tl, s, lane, x0, y0, cb, clo);
 			}
 		}
 		__syncthreads();

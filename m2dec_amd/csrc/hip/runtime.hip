@@ -234,8 +234,9 @@ struct SlotBudget {
 		cv.notify_one();
 	}
 
-	/* the reaper: returns the units of completed launches, polling the pending launches' events every 100 us
-	 * (hipEventQuery) and sleeping on the condition variable while nothing is pending.  Not
+	/* the reaper: while another process waits for units, returns the units of completed launches, polling the
+	 * pending launches' events every 100 us (hipEventQuery); sleeps on the condition variable while nothing is
+	 * pending or nobody else waits.  Not
 	 * hipEventSynchronize: a thread blocked in it holds up other threads' HIP calls on that launch's stream
 	 * (the first reaper serialised every submission behind the previous picture's completion: the end-to-end
 	 * C3 decode fell from 31 to 72 ms, one picture per launch) */
@@ -245,6 +246,13 @@ struct SlotBudget {
 		std::vector<hipEvent_t> snap, done;
 		for (;;) {
 			cv.wait(lk, [this] { return !pend.empty(); });
+			/* nobody else waiting: this process's own reservations retire what completed (retire()); the reaper
+			 * only looks again in 2 ms — its event queries contend with the decode threads' HIP calls (r123: 8
+			 * concurrent streams ~10 % slower with the reaper polling every 100 us) */
+			if (!m2d_share_others_waiting(share)) {
+				cv.wait_for(lk, std::chrono::milliseconds(2));
+				continue;
+			}
 			/* the queries outside the mutex: the submitting threads reserve under it */
 			snap.clear();
 			for (auto &p : pend) snap.push_back(p.first);

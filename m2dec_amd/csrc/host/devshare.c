@@ -40,14 +40,14 @@
 #include "devshare.h"
 
 #define SHARE_MAGIC 0x6d326462u /* "m2db" */
-#define SHARE_VERSION 1
+#define SHARE_VERSION 2
 #define SHARE_LEASES 256
 
 typedef struct {
 	int32_t pid;
 	int32_t units;    /* workgroup units this process holds now */
 	int32_t contexts; /* live decode-path back ends of this process on the device */
-	int32_t pad;
+	int32_t wait_ms;  /* CLOCK_MONOTONIC ms (| 1) of this process's last reservation that did not fit; 0: none */
 	uint64_t start;   /* /proc/<pid>/stat start time: a recycled pid is another process */
 } lease_t;
 
@@ -71,6 +71,13 @@ struct m2d_share {
 
 static pthread_mutex_t g_open_mu = PTHREAD_MUTEX_INITIALIZER;
 static m2d_share_t *g_open;
+
+static int32_t now_ms(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (int32_t)((uint32_t)((uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u) | 1u);
+}
 
 static uint64_t proc_start(int pid)
 {
@@ -279,6 +286,7 @@ int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 		}
 		if (pass == 0 && !sweep(g, s->idx)) break;
 	}
+	g->lease[s->idx].wait_ms = ok ? 0 : now_ms(); /* (m2d_share_others_waiting) */
 	if (total) *total = g->total;
 	if (procs) { /* processes holding units now (diagnostics: the concurrency the budget saw) */
 		int np = 0;
@@ -298,6 +306,20 @@ void m2d_share_release(m2d_share_t *s, int units)
 	l->units -= units;
 	g->total -= units;
 	pthread_mutex_unlock(&g->mu);
+}
+
+/* 1 when another process's reservation did not fit within the last 100 ms (it retries every 50 us while it
+ * waits): this process's reaper then returns completed launches' units at once.  Lock-free read. */
+int m2d_share_others_waiting(m2d_share_t *s)
+{
+	const seg_t *g = s->seg;
+	const int32_t now = now_ms();
+	for (int i = 0; i < SHARE_LEASES; ++i) {
+		if (i == s->idx) continue;
+		const int32_t w = __atomic_load_n(&g->lease[i].wait_ms, __ATOMIC_RELAXED);
+		if (w && (int32_t)((uint32_t)now - (uint32_t)w) < 100) return 1;
+	}
+	return 0;
 }
 
 int m2d_share_contexts(m2d_share_t *s, int delta)
@@ -396,3 +418,4 @@ int m2dec_amd_share_state(void *s, int *cap, int *total, int *mine, int *procs, 
 	return s ? m2d_share_state((m2d_share_t *)s, cap, total, mine, procs, reclaimed) : -1;
 }
 void m2dec_amd_share_close(void *s) { m2d_share_close((m2d_share_t *)s); }
+int m2dec_amd_share_others_waiting(void *s) { return s ? m2d_share_others_waiting((m2d_share_t *)s) : 0; }

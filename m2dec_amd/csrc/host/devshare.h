@@ -17,6 +17,8 @@ m2d_share_t *m2d_share_open(const char *key, int cap_units);
  * first).  total / procs (optional): the units in use and the processes holding some, after the call */
 int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs);
 void m2d_share_release(m2d_share_t *s, int units);
+/* 1 when another process waits for units (a reservation of its that did not fit, within the last 100 ms) */
+int m2d_share_others_waiting(m2d_share_t *s);
 /* add `delta` to this process's live decode contexts; returns the device-wide count */
 int m2d_share_contexts(m2d_share_t *s, int delta);
 int m2d_share_state(m2d_share_t *s, int *cap, int *total, int *mine, int *procs, long *reclaimed);

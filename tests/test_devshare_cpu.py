@@ -72,6 +72,13 @@ elif mode == "hold":
     assert L.m2dec_amd_share_try(s, int(sys.argv[6]))
     print("holding", flush=True)
     time.sleep(600)
+elif mode == "starve":  # a reservation that never fits, retried like SlotBudget::reserve for a while
+    print("starving", flush=True)
+    t_end = time.time() + float(sys.argv[6])
+    while time.time() < t_end:
+        assert not L.m2dec_amd_share_try(s, cap + 1)
+        time.sleep(0.001)
+    print("done", flush=True)
 """
 
 
@@ -84,6 +91,7 @@ def _lib():
     L.m2dec_amd_share_state.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_int)] * 4 + \
         [ctypes.POINTER(ctypes.c_long)]
     L.m2dec_amd_share_close.argtypes = [ctypes.c_void_p]
+    L.m2dec_amd_share_others_waiting.argtypes = [ctypes.c_void_p]
     return L
 
 
@@ -190,3 +198,28 @@ def test_library_load_leaves_hw_queues_alone(built):
     env["GPU_MAX_HW_QUEUES"] = "6"
     r = subprocess.run([sys.executable, "-c", code2, LIB], env=env, capture_output=True, text=True, check=True)
     assert r.stdout.split() == ["6", "6"]
+
+
+def test_reaper_wakes_only_while_another_process_waits(share_env):
+    """A process's budget reaper returns completed launches' units only while another process waits for units
+    (its event queries otherwise contend with the decode threads' HIP calls); a waiter is seen while it retries
+    and forgotten 100 ms after its last failed reservation."""
+    L = _lib()
+    key, cap = f"wait{os.getpid()}", 60
+    s = L.m2dec_amd_share_open(key.encode(), cap)
+    assert s
+    try:
+        assert L.m2dec_amd_share_others_waiting(s) == 0
+        assert not L.m2dec_amd_share_try(s, cap + 1)  # this process's own failed reservation does not count
+        assert L.m2dec_amd_share_others_waiting(s) == 0
+        p = subprocess.Popen([sys.executable, "-c", WORKER, LIB, key, str(cap), "starve", "/dev/null", "1.0"],
+                             stdout=subprocess.PIPE, text=True)
+        assert p.stdout.readline().strip() == "starving"
+        time.sleep(0.2)
+        assert L.m2dec_amd_share_others_waiting(s) == 1
+        assert p.stdout.readline().strip() == "done"
+        p.wait(timeout=30)
+        time.sleep(0.25)
+        assert L.m2dec_amd_share_others_waiting(s) == 0
+    finally:
+        L.m2dec_amd_share_close(s)

@@ -66,6 +66,7 @@ struct m2d_share {
 	int32_t pid;
 	uint64_t start;
 	char path[160];
+	int exited;             /* process exit dropped the lease; the mapping stays for threads still running */
 	struct m2d_share *next; /* open handles of this process (closed at exit) */
 };
 
@@ -274,6 +275,7 @@ m2d_share_t *m2d_share_open(const char *key, int cap_units)
 
 int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 {
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return 1;
 	seg_t *g = s->seg;
 	if (lock(g) != 0) return 0;
 	int ok = 0;
@@ -299,6 +301,7 @@ int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 
 void m2d_share_release(m2d_share_t *s, int units)
 {
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return;
 	seg_t *g = s->seg;
 	if (units <= 0 || lock(g) != 0) return;
 	lease_t *l = &g->lease[s->idx];
@@ -312,6 +315,7 @@ void m2d_share_release(m2d_share_t *s, int units)
  * waits): this process's reaper then returns completed launches' units at once.  Lock-free read. */
 int m2d_share_others_waiting(m2d_share_t *s)
 {
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return 0;
 	const seg_t *g = s->seg;
 	const int32_t now = now_ms();
 	for (int i = 0; i < SHARE_LEASES; ++i) {
@@ -324,6 +328,7 @@ int m2d_share_others_waiting(m2d_share_t *s)
 
 int m2d_share_contexts(m2d_share_t *s, int delta)
 {
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return 1;
 	seg_t *g = s->seg;
 	if (lock(g) != 0) return 1;
 	g->lease[s->idx].contexts += delta;
@@ -358,7 +363,7 @@ int m2d_share_cap(const m2d_share_t *s)
 
 /* drop this process's lease; the last live user retires the segment (magic cleared under the lock, so an
  * opener that mapped it meanwhile opens anew) and removes its file, so nothing is left in /dev/shm */
-static void share_drop(m2d_share_t *s)
+static void share_drop(m2d_share_t *s, int unmap)
 {
 	seg_t *g = s->seg;
 	if (lock(g) == 0) {
@@ -374,7 +379,7 @@ static void share_drop(m2d_share_t *s)
 		}
 		pthread_mutex_unlock(&g->mu);
 	}
-	munmap(g, sizeof(seg_t));
+	if (unmap) munmap(g, sizeof(seg_t));
 }
 
 void m2d_share_close(m2d_share_t *s)
@@ -387,22 +392,23 @@ void m2d_share_close(m2d_share_t *s)
 			break;
 		}
 	pthread_mutex_unlock(&g_open_mu);
-	share_drop(s);
+	share_drop(s, 1);
 	free(s);
 }
 
-/* process exit: the runtime keeps its per-device handles for the life of the process */
+/* process exit: the runtime keeps its per-device handles for the life of the process.  The lease goes (its
+ * units back to the other processes, the file removed by the last user) but the handle and its mapping stay:
+ * library threads still running through exit (the budget reaper) keep using them, and any reservation after
+ * this point is granted without touching the segment (the process is leaving) */
 __attribute__((destructor)) static void share_exit(void)
 {
 	pthread_mutex_lock(&g_open_mu);
 	m2d_share_t *s = g_open;
 	g_open = NULL;
 	pthread_mutex_unlock(&g_open_mu);
-	while (s) {
-		m2d_share_t *n = s->next;
-		share_drop(s);
-		free(s);
-		s = n;
+	for (; s; s = s->next) {
+		__atomic_store_n(&s->exited, 1, __ATOMIC_RELEASE);
+		share_drop(s, 0);
 	}
 }
 

@@ -223,3 +223,4 @@ def test_reaper_wakes_only_while_another_process_waits(share_env):
         assert L.m2dec_amd_share_others_waiting(s) == 0
     finally:
         L.m2dec_amd_share_close(s)
+

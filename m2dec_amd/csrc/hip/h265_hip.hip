@@ -489,14 +489,20 @@ __device__ __forceinline__ h265r_tu_t uniform_tu(const h265r_tu_t &r)
  *      DC-only and transform-skip are added per sample in phase 3;
  *   2. reference samples gathered AND filtered in one pass (each lane reads the up to three unfiltered
  *      neighbours it needs straight from the tile), both chroma components side by side;
- *   3. prediction + residual, clipped and stored straight into the tile, a dword per lane (4 luma samples of
- *      a row, or 2 CbCr pairs: byte stores of neighbouring lanes collide in the LDS banks).
+ *   3. prediction + residual, clipped and stored straight into the tile, one sample per lane.
+ * For 4 x 4 and 8 x 8 blocks (the many): 16 x 16 and 32 x 32 go through do_block.
  * An inter block (no prediction) adds its residual to the motion-compensated tile samples in place, or does
  * nothing without one. */
-__device__ void do_block_ctu(const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lane, int x0, int y0, const int16_t *cbase,
-                             uint32_t clo)
+__device__ void do_block_ctu(const H265Args &a, const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lane, int x0, int y0,
+                             const int16_t *cbase, uint32_t clo)
 {
 	const h265r_tu_t t = uniform_tu(rec);
+	if (t.log2 >= 4) {
+		/* 16 x 16 and 32 x 32: do_block's phases (its gathered reference row and packed stores measured faster for
+		 * them, r124 stamps: 32 x 32 with a residual 13.5 us vs 16.4) */
+		do_block(a, t, s, lane, CtuSamples{tl, x0, y0}, cbase, clo);
+		return;
+	}
 	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
 	const bool luma = t.plane == 0;
 	const int ncomp = luma ? 1 : 2;
@@ -556,21 +562,12 @@ __device__ void do_block_ctu(const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lan
 		return s.pred[c][i];
 	};
 	if (!(t.flags & H265R_TU_PRED)) {
-		/* inter: the residual onto the motion-compensated samples, a dword (4 luma samples / 2 CbCr pairs) per lane */
+		/* inter: the residual onto the motion-compensated samples */
 		if (any_res) {
-			const int wpr = luma ? n >> 2 : n >> 1;
-			for (int w = lane; w < wpr * n; w += 64) {
-				const int y = w / wpr, xw = (w - y * wpr) * (luma ? 4 : 2);
-				uint32_t *q = luma ? (uint32_t *)&tl.y[by + y][bx + xw] : (uint32_t *)&tl.c[by + y][2 * (bx + xw)];
-				const uint32_t in = *q;
-				uint32_t out = 0;
-#pragma unroll
-				for (int b = 0; b < 4; ++b) {
-					const int c = luma ? 0 : (b & 1), x = luma ? xw + b : xw + (b >> 1);
-					const int v = (int)((in >> (8 * b)) & 255) + resid(c, y * n + x);
-					out |= (uint32_t)clampi(v, 0, 255) << (8 * b);
-				}
-				*q = out;
+			for (int i = lane; i < ncomp * n2; i += 64) {
+				const int c = i >= n2, j = i - c * n2, x = j & (n - 1), y = j >> log2;
+				uint8_t &p = luma ? tl.y[by + y][bx + x] : tl.c[by + y][2 * (bx + x) + c];
+				p = (uint8_t)clampi((int)p + resid(c, j), 0, 255);
 			}
 			wsync();
 		}
@@ -668,18 +665,13 @@ __device__ void do_block_ctu(const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lan
 		}
 		return clampi(v + resid(c, y * n + x), 0, 255);
 	};
-	/* a dword per lane: 4 luma samples of a row, or 2 CbCr pairs (both components) */
-	const int wpr = luma ? n >> 2 : n >> 1;
-	for (int w = lane; w < wpr * n; w += 64) {
-		const int y = w / wpr, xw = (w - y * wpr) * (luma ? 4 : 2);
-		uint32_t out = 0;
-#pragma unroll
-		for (int b = 0; b < 4; ++b) {
-			const int c = luma ? 0 : (b & 1), x = luma ? xw + b : xw + (b >> 1);
-			out |= (uint32_t)predict(c, x, y) << (8 * b);
-		}
-		if (luma) *(uint32_t *)&tl.y[by + y][bx + xw] = out;
-		else *(uint32_t *)&tl.c[by + y][2 * (bx + xw)] = out;
+	/* one sample per lane, stored as a byte (small blocks: lanes, not the LDS store width, bound them — a dword
+	 * of 4 samples per lane measured slower for 4 x 4 and 8 x 8 blocks, r124 stamps) */
+	for (int i = lane; i < ncomp * n2; i += 64) {
+		const int c = i >= n2, j = i - c * n2, x = j & (n - 1), y = j >> log2;
+		const uint8_t v = (uint8_t)predict(c, x, y);
+		if (luma) tl.y[by + y][bx + x] = v;
+		else tl.c[by + y][2 * (bx + x) + c] = v;
 	}
 #undef LL
 #undef TT
@@ -840,7 +832,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 				for (int k = 0; k < m; ++k) {
 					const h265r_tu_t t = recs[k];
 					if (t.plane != wave) continue;
-					do_block_ctu(t, tl, s, lane, x0, y0, cb, clo);
+					do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
 					H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
 				}
 			}
@@ -974,7 +966,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
 			for (int k = 0; k < m; ++k) {
 				const h265r_tu_t t = recs[k];
 				if (t.plane != wave) continue;
-				do_block_ctu(t, tl, s, lane, x0, y0, cb, clo);
+				do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
 			}
 		}
 		__syncthreads();

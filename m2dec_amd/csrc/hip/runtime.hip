@@ -229,7 +229,9 @@ struct SlotBudget {
 		pend.emplace_back(e, n);
 		if (share && !reaper_on) {
 			reaper_on = true;
-			std::thread([this] { reap(); }).detach();
+			std::thread th([this] { reap(); });
+			(void)pthread_setname_np(th.native_handle(), "m2d-reaper");
+			th.detach();
 		}
 		cv.notify_one();
 	}
@@ -1132,6 +1134,14 @@ struct StagePool {
  * inside sync_frame, i.e. inside peek / get_decoded_frame.  Between API calls nothing in flight
  * points into caller memory. */
 const size_t kStgTail = 64;
+/* M2DEC_AMD_ERR_SYNC=1: the error word read by a synchronous hipMemcpy per frame (round 4) instead of copied
+ * behind the frame (A/B) */
+static bool err_sync()
+{
+	static int v = -1;
+	if (v < 0) v = dbg_knob("M2DEC_AMD_ERR_SYNC");
+	return v != 0;
+}
 
 struct HipBackend {
 	Sched sc;
@@ -1237,7 +1247,7 @@ int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
 	}
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][0], s));
 	CHECK(hipMemcpyAsync(b->stg[slot], cur, b->stg_size, hipMemcpyDeviceToHost, s));
-	CHECK(hipMemcpyAsync(b->stg[slot] + b->stg_size, b->sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
+	if (!err_sync()) CHECK(hipMemcpyAsync(b->stg[slot] + b->stg_size, b->sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][1], s));
 	CHECK(hipEventRecord(b->slot_ev[slot], s));
 	b->slot_pending[slot] = true;
@@ -1479,11 +1489,15 @@ int be_sync(void *self, int slot)
 		m2d_tl('y', slot, 0);
 		/* the error word copied behind the picture on its stream (a synchronous hipMemcpy here queues behind
 		 * whatever shares the null stream's hardware queue, per frame) */
-		int e;
-		memcpy(&e, b->stg[slot] + b->stg_size, sizeof(e));
-		if (e) {
-			fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e);
-			return -1;
+		if (err_sync()) {
+			if (b->sc.check_err() < 0) return -1;
+		} else {
+			int e;
+			memcpy(&e, b->stg[slot] + b->stg_size, sizeof(e));
+			if (e) {
+				fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e);
+				return -1;
+			}
 		}
 		if (b->timing) {
 			float ms;

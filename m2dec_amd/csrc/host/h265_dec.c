@@ -15,6 +15,7 @@
  *   - the slice's POC from the previous slice's lsb / msb (h265.cpp:736-750);
  *   - the sign-hidden coefficient is negated after dequantisation (h265.cpp:1645-1647).
  */
+#define _GNU_SOURCE /* pthread_setname_np */
 #include <limits.h>
 #include <pthread.h>
 #include <setjmp.h>
@@ -2253,6 +2254,7 @@ static void job_run(h265_pipe_t *P, h265_job_t *j)
 static void *pipe_worker(void *arg)
 {
 	h265_pipe_t *P = (h265_pipe_t *)arg;
+	pthread_setname_np(pthread_self(), "m2d-h265");
 	pthread_mutex_lock(&P->mu);
 	for (;;) {
 		h265_job_t *j = NULL;

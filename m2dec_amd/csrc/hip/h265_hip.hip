@@ -1309,6 +1309,7 @@ struct H265Gpu {
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
+	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
 };
 
@@ -1589,7 +1590,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
 	if (!g->stg[c]) H265_CHECK(hipHostMalloc((void **)&g->stg[c], bytes, hipHostMallocDefault));
 	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
-	H265_CHECK(hipMemcpyAsync(&g->err_host[c], g->err, sizeof(int), hipMemcpyDeviceToHost, s));
+	if (g->err_async) H265_CHECK(hipMemcpyAsync(&g->err_host[c], g->err, sizeof(int), hipMemcpyDeviceToHost, s));
 	H265_CHECK(hipEventRecord(g->ev[c], s));
 	lap("copy-out");
 	g->pend[c] = true;
@@ -1605,9 +1606,11 @@ int h_sync(void *p, int slot)
 	H265_CHECK(hipEventSynchronize(g->ev[slot]));
 	{
 		/* a block hand-off that never came (bounded spin): the sticky error word */
-		/* (copied behind the frame on its stream: a synchronous hipMemcpy here would queue behind whatever shares
-		 * the null stream's hardware queue, and hold up the submitting thread meanwhile) */
-		const int err = __atomic_load_n(&g->err_host[slot], __ATOMIC_ACQUIRE);
+		/* (copied behind the frame on its stream with M2DEC_AMD_H265_ERR_ASYNC=1, else a synchronous read as the
+		 * H.264 back end does: a 4-byte copy per frame on the copy engines measured slower there) */
+		int err = 0;
+		if (g->err_async) err = __atomic_load_n(&g->err_host[slot], __ATOMIC_ACQUIRE);
+		else H265_CHECK(hipMemcpy(&err, g->err, sizeof(int), hipMemcpyDeviceToHost));
 		if (err) {
 			fprintf(stderr, "m2dec_amd: H.265 block hand-off timed out on the GPU\n");
 			return -1;
@@ -1669,6 +1672,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
+	if (const char *e = getenv("M2DEC_AMD_H265_ERR_ASYNC")) g->err_async = atoi(e) != 0;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");
 		g->ns = q && atoi(q) >= 8 ? 8 : 4;

@@ -1134,12 +1134,18 @@ struct StagePool {
  * inside sync_frame, i.e. inside peek / get_decoded_frame.  Between API calls nothing in flight
  * points into caller memory. */
 const size_t kStgTail = 64;
-/* M2DEC_AMD_ERR_SYNC=1: the error word read by a synchronous hipMemcpy per frame (round 4) instead of copied
- * behind the frame (A/B) */
+/* The error word reaches the host by a synchronous 4-byte hipMemcpy per frame (on the null stream, which the
+ * non-blocking decode streams do not wait for).  M2DEC_AMD_ERR_SYNC=0 copies it behind the frame on the
+ * picture's stream into the staging buffer's tail instead — measured 15 % slower on 8 concurrent streams (1539
+ * vs 1813 fps, 1.2 CPU-ms more per frame, profiles/r125_ab_streams_err.txt): a 4-byte D2H per frame on the
+ * copy engines costs more than the synchronous read */
 static bool err_sync()
 {
 	static int v = -1;
-	if (v < 0) v = dbg_knob("M2DEC_AMD_ERR_SYNC");
+	if (v < 0) {
+		const char *e = getenv("M2DEC_AMD_ERR_SYNC");
+		v = e && *e ? atoi(e) != 0 : 1;
+	}
 	return v != 0;
 }
 

@@ -682,11 +682,12 @@ __device__ void do_block_ctu(const H265Args &a, const h265r_tu_t &rec, CtuTile &
  * coalesced read per CTU instead of one dependent global round trip per block.  Returns the base / offset the
  * blocks read through. */
 #define H265_CTU_COEF 6144 /* a 64 x 64 CTU's luma + chroma coefficients */
+template <int NT>
 __device__ __forceinline__ const int16_t *stage_coef(const H265Args &a, const h265r_tu_t *recs, int m, int16_t *cc, int *red,
                                                      int tid, uint32_t &clo)
 {
 	uint32_t lo = 0xffffffffu, hi = 0;
-	for (int k = tid; k < m; k += 128) {
+	for (int k = tid; k < m; k += NT) {
 		const h265r_tu_t &t = recs[k];
 		const uint32_t n2 = 1u << (2 * t.log2);
 		for (int c = 0; c < 2; ++c)
@@ -713,10 +714,109 @@ __device__ __forceinline__ const int16_t *stage_coef(const H265Args &a, const h2
 	}
 	const uint32_t base = lo & ~1u, nw = (hi - base + 1) >> 1; /* whole dwords from an even offset */
 	const uint32_t *src = (const uint32_t *)(a.coef + base);
-	for (uint32_t w = tid; w < nw; w += 128) ((uint32_t *)cc)[w] = src[w];
+	for (uint32_t w = tid; w < nw; w += NT) ((uint32_t *)cc)[w] = src[w];
 	__syncthreads();
 	clo = base;
 	return cc;
+}
+
+/* ---- the blocks of one chunk of a CTU's records.
+ * NT = 128: wave 0 the luma blocks, wave 1 the chroma blocks, each in decoding order.
+ * NT = 256 (M2DEC_AMD_H265_WAVES=4): two waves per plane.  A wave takes the plane's next block (an LDS
+ * counter over the plane's records in decoding order), waits until the blocks that own the samples it reads
+ * inside the CTU are done (the chunk's 4 x 4-unit owner maps; samples outside the CTU — the row above, the
+ * left CTU — are final before the chunk starts), reconstructs it and raises its done flag.  Every wait points
+ * at an earlier block of the plane, so the earliest unfinished block always runs.  Blocks of a CTU that do not
+ * read each other (an inter block's residual, intra blocks whose neighbours are done) then overlap: a CTU's
+ * luma wave was the per-CTU bound (r123 stamps: ~75 us of a ~105 us CTU step). */
+struct CtuSched {
+	uint16_t own[2][16 * 16]; /* per plane, the 4 x 4 units of the CTU (chroma: the 8 x 8 corner): the chunk record writing it, 0xffff none */
+	uint16_t list[2][H265_CTU_RECS]; /* the chunk's records of each plane, in decoding order */
+	int n[2], next[2];
+	int done[H265_CTU_RECS];
+};
+
+template <int NT>
+__device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *recs, int m, CtuTile &tl, Lds *ls, CtuSched &sc,
+                                           int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col)
+{
+	const int lane = tid & 63;
+	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6;
+	if (NT == 128) {
+		Lds &s = ls[wave];
+		for (int k = 0; k < m; ++k) {
+			const h265r_tu_t t = recs[k];
+			if (t.plane != wave) continue;
+			do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
+			H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
+		}
+		(void)sc;
+		return;
+	}
+	const int plane = wave >> 1;
+	Lds &s = ls[wave];
+	/* the chunk's plane lists, owner maps and done flags */
+	for (int i = tid; i < 2 * 16 * 16; i += NT) (&sc.own[0][0])[i] = 0xffff;
+	for (int k = tid; k < m; k += NT) sc.done[k] = 0;
+	if ((wave & 1) == 0) {
+		int cnt = 0;
+		for (int base = 0; base < m; base += 64) {
+			const int k = base + lane;
+			const bool mine = k < m && recs[k].plane == plane;
+			const unsigned long long mask = __ballot(mine);
+			if (mine) sc.list[plane][cnt + __popcll(mask & ((1ull << lane) - 1))] = (uint16_t)k;
+			cnt += __popcll(mask);
+		}
+		if (lane == 0) {
+			sc.n[plane] = cnt;
+			sc.next[plane] = 0;
+		}
+	}
+	__syncthreads();
+	for (int k = tid; k < m; k += NT) {
+		const h265r_tu_t &t = recs[k];
+		const int u = (1 << t.log2) >> 2;
+		const int ux = (t.plane ? t.x - (x0 >> 1) : t.x - x0) >> 2, uy = (t.plane ? t.y - (y0 >> 1) : t.y - y0) >> 2;
+		for (int j = 0; j < u * u; ++j) sc.own[t.plane][(uy + j / u) * 16 + ux + j % u] = (uint16_t)k;
+	}
+	__syncthreads();
+	for (;;) {
+		int pos = 0;
+		if (lane == 0) pos = atomicAdd(&sc.next[plane], 1);
+		pos = __shfl(pos, 0);
+		if (pos >= sc.n[plane]) break;
+		const int k = sc.list[plane][pos];
+		const h265r_tu_t t = uniform_tu(recs[k]);
+		if (t.flags & H265R_TU_PRED) {
+			/* the owners of the samples it reads inside the CTU: lane i < ntop the units above, then the units to the
+			 * left, then the corner */
+			const int n = 1 << t.log2;
+			const int bx = t.plane ? t.x - (x0 >> 1) : t.x - x0, by = t.plane ? t.y - (y0 >> 1) : t.y - y0;
+			const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
+			const int ntop = (by > 0 && at > 0) ? (at + 3) >> 2 : 0, nleft = (bx > 0 && al > 0) ? (al + 3) >> 2 : 0;
+			const bool corner = bx > 0 && by > 0 && at > 0 && al > 0;
+			int unit = -1;
+			if (lane < ntop) unit = ((by >> 2) - 1) * 16 + (bx >> 2) + lane;
+			else if (lane < ntop + nleft) unit = ((by >> 2) + lane - ntop) * 16 + (bx >> 2) - 1;
+			else if (lane == ntop + nleft && corner) unit = ((by >> 2) - 1) * 16 + (bx >> 2) - 1;
+			const int o = unit >= 0 && unit < 256 ? sc.own[t.plane][unit] : 0xffff;
+			unsigned spins = 0;
+			for (;;) {
+				const bool ok = o == 0xffff || o >= k || __hip_atomic_load(&sc.done[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+				if (__all(ok)) break;
+				if (++spins > H265_SPIN_LIMIT) {
+					__hip_atomic_store((gi32 *)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+					break;
+				}
+				__builtin_amdgcn_s_sleep(1);
+			}
+			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+		}
+		do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
+		H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (plane << 7) | ((t.mode & 63) << 8));
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+		if (lane == 0) __hip_atomic_store(&sc.done[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+	}
 }
 
 /* first record of every CTU (records are in decoding order, CTUs in raster order) */
@@ -736,16 +836,18 @@ __global__ __launch_bounds__(256) void k_h265_ctu_index(const H265Args *ap)
 	for (int c = prev + 1; c <= cur && c <= nctu; ++c) a.ctu_first[c] = i;
 }
 
-__global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_h265_ctu_rows(const H265Args *ap)
 {
 	const H265Args a = *ap;
-	__shared__ Lds ls[2];
+	__shared__ Lds ls[NT / 64];
 	__shared__ CtuTile tl;
-	__shared__ h265r_tu_t recs[H265_CTU_RECS]; /* the CTU's records, staged (both waves read all of them) */
+	__shared__ h265r_tu_t recs[H265_CTU_RECS]; /* the CTU's records, staged (every wave reads all of them) */
 	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
 	__shared__ int red[2];
+	__shared__ CtuSched sch;
 	const int tid = threadIdx.x, lane = tid & 63;
-	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
+	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* NT 128: 0 luma, 1 chroma; NT 256: 0-1 luma, 2-3 chroma */
 	const int row = blockIdx.x;
 	const int ctb = 1 << a.ctb_log2, cctb = ctb >> 1;
 	Lds &s = ls[wave];
@@ -765,11 +867,11 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 		if (a.n_pu) {
 			__syncthreads(); /* (the previous CTU's last column is in tl.ly) */
 			const int wpr = (cols_here + 3) >> 2;
-			for (int w = tid; w < wpr * rows_here; w += 128) {
+			for (int w = tid; w < wpr * rows_here; w += NT) {
 				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
 			}
-			for (int w = tid; w < wpr * crows; w += 128) {
+			for (int w = tid; w < wpr * crows; w += NT) {
 				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
 			}
@@ -781,7 +883,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 		int above = 0;
 		if (row > 0) {
 			const int c = row * a.ctu_cols + col;
-			for (int k = a.ctu_first[c] + tid; k < a.ctu_first[c + 1]; k += 128) {
+			for (int k = a.ctu_first[c] + tid; k < a.ctu_first[c + 1]; k += NT) {
 				const h265r_tu_t &t = a.tu[k];
 				if ((t.flags & H265R_TU_PRED) && (t.plane ? 2 * t.y : t.y) == y0) above = 1;
 			}
@@ -805,11 +907,11 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 			}
 			__syncthreads();
-			for (int i = tid; i <= 2 * ctb; i += 128) {
+			for (int i = tid; i <= 2 * ctb; i += NT) {
 				const int x = x0 - 1 + i;
 				tl.ty[i] = (x >= 0 && x < a.pic_w) ? (uint8_t)ld_px(a, 0, 0, x, y0 - 1) : 128;
 			}
-			for (int i = tid; i < 2 * (ctb + 1); i += 128) {
+			for (int i = tid; i < 2 * (ctb + 1); i += NT) {
 				const int x = (x0 >> 1) - 1 + (i >> 1);
 				tl.tc[i] = (x >= 0 && x < (a.pic_w >> 1)) ? (uint8_t)ld_px(a, 1, i & 1, x, (y0 >> 1) - 1) : 128;
 			}
@@ -824,17 +926,12 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 			for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
 				const int m = min(H265_CTU_RECS, i1 - c0);
 				__syncthreads(); /* (the previous chunk is consumed) */
-				for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += 128)
+				for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += NT)
 					((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
 				__syncthreads();
 				uint32_t clo;
-				const int16_t *cb = stage_coef(a, recs, m, ccoef, red, tid, clo);
-				for (int k = 0; k < m; ++k) {
-					const h265r_tu_t t = recs[k];
-					if (t.plane != wave) continue;
-					do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
-					H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
-				}
+				const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
+				ctu_blocks<NT>(a, recs, m, tl, ls, sch, tid, x0, y0, cb, clo, row, col);
 			}
 		}
 		H5ST(lane, 2, row, col, wave);
@@ -842,12 +939,12 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
 		/* out: the CTU's samples (inside the picture) as write-through words, drained, then the progress word */
 		{
 			const int wpr = (cols_here + 3) >> 2;
-			for (int w = tid; w < wpr * rows_here; w += 128) {
+			for (int w = tid; w < wpr * rows_here; w += NT) {
 				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 				st_word(plane_px(a, 0, 0, x0 + xx, y0 + yy), *(const uint32_t *)&tl.y[yy][xx]);
 			}
 			const int cw = (cols_here + 3) >> 2; /* words of CbCr pairs per chroma row: cols_here bytes */
-			for (int w = tid; w < cw * crows; w += 128) {
+			for (int w = tid; w < cw * crows; w += NT) {
 				const int yy = w / cw, xx = (w - yy * cw) * 4;
 				st_word(plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy), *(const uint32_t *)&tl.c[yy][xx]);
 			}
@@ -866,14 +963,16 @@ __global__ __launch_bounds__(128) void k_h265_ctu_rows(const H265Args *ap)
  * neighbour CTUs that block reads (left, above-left, above, above-right: lower raster indices, i.e. workgroups
  * dispatched earlier, so a wait always ends) and loads their published edge samples; the row kernel's 17
  * workgroups of a 1080p picture instead walked their 30 CTUs one after another. */
-__global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_h265_ctu_grid(const H265Args *ap)
 {
 	const H265Args a = *ap;
-	__shared__ Lds ls[2];
+	__shared__ Lds ls[NT / 64];
 	__shared__ CtuTile tl;
 	__shared__ h265r_tu_t recs[H265_CTU_RECS];
 	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
 	__shared__ int red[2];
+	__shared__ CtuSched sch;
 	const int tid = threadIdx.x, lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* 0 luma, 1 chroma */
 	const int c = blockIdx.x, row = c / a.ctu_cols, col = c - row * a.ctu_cols;
@@ -890,7 +989,7 @@ __global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
 		int need = 0;
 		if (tid == 0) s_need = 0;
 		__syncthreads();
-		for (int k = i0 + tid; k < i1; k += 128) {
+		for (int k = i0 + tid; k < i1; k += NT) {
 			const h265r_tu_t &t = a.tu[k];
 			if (!(t.flags & H265R_TU_PRED)) continue;
 			const int n = 1 << t.log2, sc = t.plane ? 2 : 1, lx = sc * t.x, ly = sc * t.y;
@@ -927,28 +1026,28 @@ __global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
 		/* the motion-compensated samples (k_h265_mc, an earlier launch) */
 		if (a.n_pu) {
 			const int wpr = (cols_here + 3) >> 2;
-			for (int w = tid; w < wpr * rows_here; w += 128) {
+			for (int w = tid; w < wpr * rows_here; w += NT) {
 				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
 			}
-			for (int w = tid; w < wpr * crows; w += 128) {
+			for (int w = tid; w < wpr * crows; w += NT) {
 				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
 			}
 		}
 		/* the neighbours' edge samples (published as write-through words: read at agent scope) */
 		if (need & 1)
-			for (int i = tid; i < 2 * ctb; i += 128) {
+			for (int i = tid; i < 2 * ctb; i += NT) {
 				if (i < ctb) tl.ly[i] = i < rows_here ? (uint8_t)ld_px(a, 0, 0, x0 - 1, y0 + i) : 128;
 				else tl.lc[i - ctb] = (i - ctb) < rows_here ? (uint8_t)ld_px(a, 1, (i - ctb) & 1, (x0 >> 1) - 1, (y0 >> 1) + ((i - ctb) >> 1)) : 128;
 			}
 		if (need & 14) {
-			for (int i = tid; i <= 2 * ctb; i += 128) {
+			for (int i = tid; i <= 2 * ctb; i += NT) {
 				const int x = x0 - 1 + i;
 				const bool in = x >= 0 && x < a.pic_w && (i > 0 || (need & 2)) && (i <= ctb || (need & 8));
 				tl.ty[i] = in ? (uint8_t)ld_px(a, 0, 0, x, y0 - 1) : 128;
 			}
-			for (int i = tid; i < 2 * (ctb + 1); i += 128) {
+			for (int i = tid; i < 2 * (ctb + 1); i += NT) {
 				const int x = (x0 >> 1) - 1 + (i >> 1);
 				const bool in = x >= 0 && x < (a.pic_w >> 1) && (i > 1 || (need & 2)) && (i < ctb + 2 || (need & 8));
 				tl.tc[i] = in ? (uint8_t)ld_px(a, 1, i & 1, x, (y0 >> 1) - 1) : 128;
@@ -959,24 +1058,20 @@ __global__ __launch_bounds__(128) void k_h265_ctu_grid(const H265Args *ap)
 		for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
 			const int m = min(H265_CTU_RECS, i1 - c0);
 			__syncthreads(); /* (the tile / the previous chunk) */
-			for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += 128) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
+			for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += NT) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
 			__syncthreads();
 			uint32_t clo;
-			const int16_t *cb = stage_coef(a, recs, m, ccoef, red, tid, clo);
-			for (int k = 0; k < m; ++k) {
-				const h265r_tu_t t = recs[k];
-				if (t.plane != wave) continue;
-				do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
-			}
+			const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
+			ctu_blocks<NT>(a, recs, m, tl, ls, sch, tid, x0, y0, cb, clo, row, col);
 		}
 		__syncthreads();
 		/* out: the CTU's samples as write-through words, drained before the done flag */
 		const int wpr = (cols_here + 3) >> 2;
-		for (int w = tid; w < wpr * rows_here; w += 128) {
+		for (int w = tid; w < wpr * rows_here; w += NT) {
 			const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 			st_word(plane_px(a, 0, 0, x0 + xx, y0 + yy), *(const uint32_t *)&tl.y[yy][xx]);
 		}
-		for (int w = tid; w < wpr * crows; w += 128) {
+		for (int w = tid; w < wpr * crows; w += NT) {
 			const int yy = w / wpr, xx = (w - yy * wpr) * 4;
 			st_word(plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy), *(const uint32_t *)&tl.c[yy][xx]);
 		}
@@ -1309,6 +1404,7 @@ struct H265Gpu {
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
+	bool waves4 = true;        /* CTU kernels with two waves per plane (M2DEC_AMD_H265_WAVES=2: one) */
 	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
 };
@@ -1554,10 +1650,14 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		H265_CHECK(hipGetLastError());
 	} else if (pic->n_tu) {
 		hipLaunchKernelGGL(k_h265_ctu_index, dim3(pic->n_tu / 256 + 1), dim3(256), 0, s, args);
-		if (pic->n_pu && g->ctu_grid)
-			hipLaunchKernelGGL(k_h265_ctu_grid, dim3(nctu), dim3(128), 0, s, args);
-		else
-			hipLaunchKernelGGL(k_h265_ctu_rows, dim3(rows), dim3(128), 0, s, args);
+		if (pic->n_pu && g->ctu_grid) {
+			if (g->waves4) hipLaunchKernelGGL(k_h265_ctu_grid<256>, dim3(nctu), dim3(256), 0, s, args);
+			else hipLaunchKernelGGL(k_h265_ctu_grid<128>, dim3(nctu), dim3(128), 0, s, args);
+		} else if (g->waves4) {
+			hipLaunchKernelGGL(k_h265_ctu_rows<256>, dim3(rows), dim3(256), 0, s, args);
+		} else {
+			hipLaunchKernelGGL(k_h265_ctu_rows<128>, dim3(rows), dim3(128), 0, s, args);
+		}
 		H265_CHECK(hipGetLastError());
 	}
 	if (pic->flags & H265R_PIC_DEBLOCK) {
@@ -1672,6 +1772,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
+	if (const char *e = getenv("M2DEC_AMD_H265_WAVES")) g->waves4 = atoi(e) >= 4;
 	if (const char *e = getenv("M2DEC_AMD_H265_ERR_ASYNC")) g->err_async = atoi(e) != 0;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");

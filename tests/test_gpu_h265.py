@@ -27,10 +27,13 @@ PB = sorted(GOLD)  # (the intra streams take the row kernel either way)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"M2DEC_AMD_H265_CTU_GRID": "0"}, {"M2DEC_AMD_H265_STREAMS": "1"},
-                                 {"M2DEC_AMD_H265_STREAMS": "8"}], ids=["rows", "one_stream", "eight_streams"])
+                                 {"M2DEC_AMD_H265_STREAMS": "8"}, {"M2DEC_AMD_H265_WAVES": "2"},
+                                 {"M2DEC_AMD_H265_WAVES": "2", "M2DEC_AMD_H265_CTU_GRID": "0"}],
+                         ids=["rows", "one_stream", "eight_streams", "one_wave_per_plane", "one_wave_rows"])
 def test_hip_h265_inter_variants(built, monkeypatch, env):
     """P / B pictures through the row kernel (the CTU-grid kernel's predecessor), on one stream (every
-    dependency in stream order) and on 8 streams (every one an event wait): each bit-exact."""
+    dependency in stream order), on 8 streams (every one an event wait), and with one wave per plane in the
+    CTU kernels instead of two (no intra-CTU block scheduler): each bit-exact."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     for name in PB:

@@ -54,19 +54,23 @@ for pi, p in enumerate(pics[:2]):
         elif k == 2:
             ctu[(r, c)][f"w{aux}"] = t
         elif k == 4:
-            w = (aux >> 7) & 1
+            w = (aux >> 7) & 1  # (the plane; with two waves per plane a block's duration spans the other wave's too)
             st = last.get((r, c, w), t)
             blocks.append((aux & 7, (aux >> 3) & 1, (aux >> 4) & 7, w, us(t - st)))
             last[(r, c, w)] = t
     waits = [us(v[1] - v[0]) for v in ctu.values() if 0 in v and 1 in v]
-    body0 = [us(v["w0"] - v[1]) for v in ctu.values() if 1 in v and "w0" in v]
-    body1 = [us(v["w1"] - v[1]) for v in ctu.values() if 1 in v and "w1" in v]
-    tail = [us(v[3] - max(v.get("w0", 0), v.get("w1", 0))) for v in ctu.values() if 3 in v and "w0" in v]
+    # per plane: the last of its waves (two waves per plane when the kernel runs 4 waves: w2 / w3 seen)
+    four = any("w2" in v for v in ctu.values())
+    luma_w, chroma_w = (("w0", "w1"), ("w2", "w3")) if four else (("w0",), ("w1",))
+    end = lambda v, ws: max(v[w] for w in ws if w in v) if any(w in v for w in ws) else None  # noqa: E731
+    body0 = [us(end(v, luma_w) - v[1]) for v in ctu.values() if 1 in v and end(v, luma_w)]
+    body1 = [us(end(v, chroma_w) - v[1]) for v in ctu.values() if 1 in v and end(v, chroma_w)]
+    tail = [us(v[3] - max(end(v, luma_w) or 0, end(v, chroma_w) or 0)) for v in ctu.values() if 3 in v and end(v, luma_w)]
     print(f"\npicture {pi}: span {span:.0f} us, {len(ctu)} CTUs, {len(blocks)} blocks")
     q = lambda xs: f"median {statistics.median(xs):6.1f} mean {statistics.mean(xs):6.1f} max {max(xs):7.1f}" if xs else "-"  # noqa: E731
     print(f"  CTU wait for the row above + row load  {q(waits)} us")
-    print(f"  CTU luma blocks (wave 0)              {q(body0)} us")
-    print(f"  CTU chroma blocks (wave 1)            {q(body1)} us")
+    print(f"  CTU luma blocks ({'waves 0-1' if four else 'wave 0'})           {q(body0)} us")
+    print(f"  CTU chroma blocks ({'waves 2-3' if four else 'wave 1'})         {q(body1)} us")
     print(f"  CTU join + store + progress           {q(tail)} us")
     print("  blocks by (plane, log2, intra, residual kind): n, median us, sum us")
     groups = defaultdict(list)

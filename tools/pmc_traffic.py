@@ -59,12 +59,12 @@ def h265(root, label, out):
     out["write_bytes"] = int(w * 1024)
     by = {}
     for v in fetch:
-        k = v["_name"].replace("(anonymous namespace)::", "").split("(")[0]
+        k = v["_name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         by[k] = by.get(k, 0.0) + v["FETCH_SIZE"] * 1024 / pics_f
     out["read_bytes_raw_by_kernel"] = {k: int(x) for k, x in sorted(by.items())}
     bw = {}
     for v in write:
-        k = v["_name"].replace("(anonymous namespace)::", "").split("(")[0]
+        k = v["_name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         bw[k] = bw.get(k, 0.0) + v["WRITE_SIZE"] * 1024 / pics_w
     out["write_bytes_by_kernel"] = {k: int(x) for k, x in sorted(bw.items())}
     # FETCH_SIZE x 2 holds for wide coalesced streaming reads (MI355X_MICROARCH.md §HBM); the deblocking and
@@ -128,7 +128,7 @@ def main():
     sq = per_dispatch(os.path.join(root, "SQ_WAVES_SQ_WAVE_CYCLES_SQ_WAIT_ANY_SQ_WAIT_INST_ANY_SQ_ACTIVE_INST_ANY_"
                                          "SQ_ACTIVE_INST_VALU_SQ_INSTS_VALU_SQ_BUSY_CYCLES_GRBM_GUI_ACTIVE"))
     if sq:
-        med = {k: statistics.median(v.get(k, 0.0) for v in sq) for k in sq[0]}
+        med = {k: statistics.median(v.get(k, 0.0) for v in sq) for k in sq[0] if not k.startswith("_")}
         wc = max(1.0, med.get("SQ_WAVE_CYCLES", 0.0))
         out["sq"] = {k: int(v) for k, v in sorted(med.items())}
         # fractions of wave-resident time (quad-cycles): parked on waitcnt / barrier, stalled at issue,

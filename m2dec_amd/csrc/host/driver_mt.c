@@ -64,6 +64,7 @@ typedef struct md5_pipe {
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
+	int tail_share;          /* frames a thread takes in tail mode (M2DEC_AMD_MD5_TAIL_SHARE, default 4; 0: queue / threads) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
@@ -107,10 +108,15 @@ static void *md5_worker(void *arg)
 			ts.tv_nsec %= 1000000000L;
 			pthread_cond_timedwait(&p->cv_job, &p->mu, &ts);
 		}
-		/* frames per thread: in tail mode one each (the threads still hashing finish within ~3 ms and take
-		 * the rest; a thread that took all queued frames alone ran 6.7 ms past the last frame: r97), more
-		 * only when the queue outnumbers the threads */
-		const int share = tail ? (p->head - p->next + p->nth - 1) / p->nth : MD5_BATCH;
+		/* frames per thread: in tail mode up to p->tail_share (default 4) each — the 4-lane MD5 kernel hashes
+		 * 2-4 frames in about one frame's time, so the tail's latency stays that of one frame at a quarter of
+		 * the CPU (before it: one each, 3.3 ms of a core per 1080p frame; a thread that took all queued frames
+		 * on the 16-lane kernel ran 6.7 ms past the last frame: r97); M2DEC_AMD_MD5_TAIL_SHARE=0 spreads the
+		 * queue over the threads as before */
+		const int queued = p->head - p->next;
+		const int share = !tail ? MD5_BATCH
+		                        : (p->tail_share > 0 ? (queued < p->tail_share ? queued : p->tail_share)
+		                                             : (queued + p->nth - 1) / p->nth);
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];
@@ -201,6 +207,7 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	p->tail_mode = getenv("M2DEC_AMD_MD5_TAIL") ? atoi(getenv("M2DEC_AMD_MD5_TAIL")) != 0 : 1;
+	p->tail_share = getenv("M2DEC_AMD_MD5_TAIL_SHARE") ? atoi(getenv("M2DEC_AMD_MD5_TAIL_SHARE")) : 4;
 	p->streams = streams;
 	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)
 		if (pthread_create(&p->th[p->nth], NULL, md5_worker, p) != 0) break;

@@ -33,6 +33,7 @@
                               9575F, one frame alone 3.3 ms (tools/md5_batch_bench.py, profiles/r85_md5_batch.txt);
                               most threads only work in tail mode (below); M2DEC_AMD_MD5_THREADS */
 #define MD5_TAIL_PARSE_BUSY 4 /* tail mode once at most this many parse workers are busy */
+#define MD5_BIG_FRAME ((size_t)6 << 20) /* frames above this (4K) are not batched short of min_batch */
 
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
  * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
@@ -64,7 +65,6 @@ typedef struct md5_pipe {
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
-	int tail_share;          /* frames a thread takes in tail mode (M2DEC_AMD_MD5_TAIL_SHARE, default 4; 0: queue / threads) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
@@ -108,15 +108,17 @@ static void *md5_worker(void *arg)
 			ts.tv_nsec %= 1000000000L;
 			pthread_cond_timedwait(&p->cv_job, &p->mu, &ts);
 		}
-		/* frames per thread: in tail mode up to p->tail_share (default 4) each — the 4-lane MD5 kernel hashes
-		 * 2-4 frames in about one frame's time, so the tail's latency stays that of one frame at a quarter of
-		 * the CPU (before it: one each, 3.3 ms of a core per 1080p frame; a thread that took all queued frames
-		 * on the 16-lane kernel ran 6.7 ms past the last frame: r97); M2DEC_AMD_MD5_TAIL_SHARE=0 spreads the
-		 * queue over the threads as before */
+		/* frames per thread: in tail mode one each (the threads still hashing finish within ~3 ms and take
+		 * the rest; a thread that took all queued frames alone ran 6.7 ms past the last frame: r97), more
+		 * only when the queue outnumbers the threads.  Outside the tail, a batch short of min_batch (the wait
+		 * timed out) of large frames goes one frame per thread too: any batch of 2-16 costs about twice one
+		 * frame's time on the 16-lane kernel (6.3-6.5 ms for 1080p on the box, profiles/r128_md5_batch.txt),
+		 * and for a 4K frame (12.4 MB, ~13 ms alone) a 3-frame batch taken while the parse was still busy
+		 * ran 25 ms and ended the C5 decode (profiles/r127_timeline_c5.txt) */
 		const int queued = p->head - p->next;
-		const int share = !tail ? MD5_BATCH
-		                        : (p->tail_share > 0 ? (queued < p->tail_share ? queued : p->tail_share)
-		                                             : (queued + p->nth - 1) / p->nth);
+		const size_t fbytes = (size_t)p->frm[p->next % MD5_RING].width * (size_t)p->frm[p->next % MD5_RING].height * 3 / 2;
+		const int share = tail ? (queued + p->nth - 1) / p->nth
+		                       : ((queued < p->min_batch && fbytes > MD5_BIG_FRAME) ? 1 : MD5_BATCH);
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];
@@ -207,7 +209,6 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	p->tail_mode = getenv("M2DEC_AMD_MD5_TAIL") ? atoi(getenv("M2DEC_AMD_MD5_TAIL")) != 0 : 1;
-	p->tail_share = getenv("M2DEC_AMD_MD5_TAIL_SHARE") ? atoi(getenv("M2DEC_AMD_MD5_TAIL_SHARE")) : 4;
 	p->streams = streams;
 	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)
 		if (pthread_create(&p->th[p->nth], NULL, md5_worker, p) != 0) break;

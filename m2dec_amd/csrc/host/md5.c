@@ -208,73 +208,6 @@ void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
 		a = _mm512_add_epi32(a, _mm512_ternarylogic_epi32(b, c, d, imm)); \
 		a = _mm512_add_epi32(_mm512_rol_epi32(a, s), b); \
 	} while (0)
-/* the 64 steps of one block, for a step macro STEP(logic, a, b, c, d, word, constant, rotation) */
-#define MD5_STEPS(STEP) \
-	STEP(TF, a, b, c, d, 0, 0xd76aa478u, 7); \
-	STEP(TF, d, a, b, c, 1, 0xe8c7b756u, 12); \
-	STEP(TF, c, d, a, b, 2, 0x242070dbu, 17); \
-	STEP(TF, b, c, d, a, 3, 0xc1bdceeeu, 22); \
-	STEP(TF, a, b, c, d, 4, 0xf57c0fafu, 7); \
-	STEP(TF, d, a, b, c, 5, 0x4787c62au, 12); \
-	STEP(TF, c, d, a, b, 6, 0xa8304613u, 17); \
-	STEP(TF, b, c, d, a, 7, 0xfd469501u, 22); \
-	STEP(TF, a, b, c, d, 8, 0x698098d8u, 7); \
-	STEP(TF, d, a, b, c, 9, 0x8b44f7afu, 12); \
-	STEP(TF, c, d, a, b, 10, 0xffff5bb1u, 17); \
-	STEP(TF, b, c, d, a, 11, 0x895cd7beu, 22); \
-	STEP(TF, a, b, c, d, 12, 0x6b901122u, 7); \
-	STEP(TF, d, a, b, c, 13, 0xfd987193u, 12); \
-	STEP(TF, c, d, a, b, 14, 0xa679438eu, 17); \
-	STEP(TF, b, c, d, a, 15, 0x49b40821u, 22); \
-	STEP(TG, a, b, c, d, 1, 0xf61e2562u, 5); \
-	STEP(TG, d, a, b, c, 6, 0xc040b340u, 9); \
-	STEP(TG, c, d, a, b, 11, 0x265e5a51u, 14); \
-	STEP(TG, b, c, d, a, 0, 0xe9b6c7aau, 20); \
-	STEP(TG, a, b, c, d, 5, 0xd62f105du, 5); \
-	STEP(TG, d, a, b, c, 10, 0x02441453u, 9); \
-	STEP(TG, c, d, a, b, 15, 0xd8a1e681u, 14); \
-	STEP(TG, b, c, d, a, 4, 0xe7d3fbc8u, 20); \
-	STEP(TG, a, b, c, d, 9, 0x21e1cde6u, 5); \
-	STEP(TG, d, a, b, c, 14, 0xc33707d6u, 9); \
-	STEP(TG, c, d, a, b, 3, 0xf4d50d87u, 14); \
-	STEP(TG, b, c, d, a, 8, 0x455a14edu, 20); \
-	STEP(TG, a, b, c, d, 13, 0xa9e3e905u, 5); \
-	STEP(TG, d, a, b, c, 2, 0xfcefa3f8u, 9); \
-	STEP(TG, c, d, a, b, 7, 0x676f02d9u, 14); \
-	STEP(TG, b, c, d, a, 12, 0x8d2a4c8au, 20); \
-	STEP(TH, a, b, c, d, 5, 0xfffa3942u, 4); \
-	STEP(TH, d, a, b, c, 8, 0x8771f681u, 11); \
-	STEP(TH, c, d, a, b, 11, 0x6d9d6122u, 16); \
-	STEP(TH, b, c, d, a, 14, 0xfde5380cu, 23); \
-	STEP(TH, a, b, c, d, 1, 0xa4beea44u, 4); \
-	STEP(TH, d, a, b, c, 4, 0x4bdecfa9u, 11); \
-	STEP(TH, c, d, a, b, 7, 0xf6bb4b60u, 16); \
-	STEP(TH, b, c, d, a, 10, 0xbebfbc70u, 23); \
-	STEP(TH, a, b, c, d, 13, 0x289b7ec6u, 4); \
-	STEP(TH, d, a, b, c, 0, 0xeaa127fau, 11); \
-	STEP(TH, c, d, a, b, 3, 0xd4ef3085u, 16); \
-	STEP(TH, b, c, d, a, 6, 0x04881d05u, 23); \
-	STEP(TH, a, b, c, d, 9, 0xd9d4d039u, 4); \
-	STEP(TH, d, a, b, c, 12, 0xe6db99e5u, 11); \
-	STEP(TH, c, d, a, b, 15, 0x1fa27cf8u, 16); \
-	STEP(TH, b, c, d, a, 2, 0xc4ac5665u, 23); \
-	STEP(TI, a, b, c, d, 0, 0xf4292244u, 6); \
-	STEP(TI, d, a, b, c, 7, 0x432aff97u, 10); \
-	STEP(TI, c, d, a, b, 14, 0xab9423a7u, 15); \
-	STEP(TI, b, c, d, a, 5, 0xfc93a039u, 21); \
-	STEP(TI, a, b, c, d, 12, 0x655b59c3u, 6); \
-	STEP(TI, d, a, b, c, 3, 0x8f0ccc92u, 10); \
-	STEP(TI, c, d, a, b, 10, 0xffeff47du, 15); \
-	STEP(TI, b, c, d, a, 1, 0x85845dd1u, 21); \
-	STEP(TI, a, b, c, d, 8, 0x6fa87e4fu, 6); \
-	STEP(TI, d, a, b, c, 15, 0xfe2ce6e0u, 10); \
-	STEP(TI, c, d, a, b, 6, 0xa3014314u, 15); \
-	STEP(TI, b, c, d, a, 13, 0x4e0811a1u, 21); \
-	STEP(TI, a, b, c, d, 4, 0xf7537e82u, 6); \
-	STEP(TI, d, a, b, c, 11, 0xbd3af235u, 10); \
-	STEP(TI, c, d, a, b, 2, 0x2ad7d2bbu, 15); \
-	STEP(TI, b, c, d, a, 9, 0xeb86d391u, 21);
-
 /* ternary-logic truth tables over (b, c, d): F = b ? c : d, G = d ? b : c, H = b ^ c ^ d, I = c ^ (b | ~d) */
 #define TF 0xca
 #define TG 0xe4
@@ -318,7 +251,70 @@ __attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16],
 		__m512i a = va, b = vb, c = vc, d = vd;
 		for (int l = 0; l < 16; ++l) w[l] = _mm512_loadu_si512(lp[l] + 64 * n);
 		transpose16(w);
-		MD5_STEPS(VSTEP);
+		VSTEP(TF, a, b, c, d, 0, 0xd76aa478u, 7);
+		VSTEP(TF, d, a, b, c, 1, 0xe8c7b756u, 12);
+		VSTEP(TF, c, d, a, b, 2, 0x242070dbu, 17);
+		VSTEP(TF, b, c, d, a, 3, 0xc1bdceeeu, 22);
+		VSTEP(TF, a, b, c, d, 4, 0xf57c0fafu, 7);
+		VSTEP(TF, d, a, b, c, 5, 0x4787c62au, 12);
+		VSTEP(TF, c, d, a, b, 6, 0xa8304613u, 17);
+		VSTEP(TF, b, c, d, a, 7, 0xfd469501u, 22);
+		VSTEP(TF, a, b, c, d, 8, 0x698098d8u, 7);
+		VSTEP(TF, d, a, b, c, 9, 0x8b44f7afu, 12);
+		VSTEP(TF, c, d, a, b, 10, 0xffff5bb1u, 17);
+		VSTEP(TF, b, c, d, a, 11, 0x895cd7beu, 22);
+		VSTEP(TF, a, b, c, d, 12, 0x6b901122u, 7);
+		VSTEP(TF, d, a, b, c, 13, 0xfd987193u, 12);
+		VSTEP(TF, c, d, a, b, 14, 0xa679438eu, 17);
+		VSTEP(TF, b, c, d, a, 15, 0x49b40821u, 22);
+		VSTEP(TG, a, b, c, d, 1, 0xf61e2562u, 5);
+		VSTEP(TG, d, a, b, c, 6, 0xc040b340u, 9);
+		VSTEP(TG, c, d, a, b, 11, 0x265e5a51u, 14);
+		VSTEP(TG, b, c, d, a, 0, 0xe9b6c7aau, 20);
+		VSTEP(TG, a, b, c, d, 5, 0xd62f105du, 5);
+		VSTEP(TG, d, a, b, c, 10, 0x02441453u, 9);
+		VSTEP(TG, c, d, a, b, 15, 0xd8a1e681u, 14);
+		VSTEP(TG, b, c, d, a, 4, 0xe7d3fbc8u, 20);
+		VSTEP(TG, a, b, c, d, 9, 0x21e1cde6u, 5);
+		VSTEP(TG, d, a, b, c, 14, 0xc33707d6u, 9);
+		VSTEP(TG, c, d, a, b, 3, 0xf4d50d87u, 14);
+		VSTEP(TG, b, c, d, a, 8, 0x455a14edu, 20);
+		VSTEP(TG, a, b, c, d, 13, 0xa9e3e905u, 5);
+		VSTEP(TG, d, a, b, c, 2, 0xfcefa3f8u, 9);
+		VSTEP(TG, c, d, a, b, 7, 0x676f02d9u, 14);
+		VSTEP(TG, b, c, d, a, 12, 0x8d2a4c8au, 20);
+		VSTEP(TH, a, b, c, d, 5, 0xfffa3942u, 4);
+		VSTEP(TH, d, a, b, c, 8, 0x8771f681u, 11);
+		VSTEP(TH, c, d, a, b, 11, 0x6d9d6122u, 16);
+		VSTEP(TH, b, c, d, a, 14, 0xfde5380cu, 23);
+		VSTEP(TH, a, b, c, d, 1, 0xa4beea44u, 4);
+		VSTEP(TH, d, a, b, c, 4, 0x4bdecfa9u, 11);
+		VSTEP(TH, c, d, a, b, 7, 0xf6bb4b60u, 16);
+		VSTEP(TH, b, c, d, a, 10, 0xbebfbc70u, 23);
+		VSTEP(TH, a, b, c, d, 13, 0x289b7ec6u, 4);
+		VSTEP(TH, d, a, b, c, 0, 0xeaa127fau, 11);
+		VSTEP(TH, c, d, a, b, 3, 0xd4ef3085u, 16);
+		VSTEP(TH, b, c, d, a, 6, 0x04881d05u, 23);
+		VSTEP(TH, a, b, c, d, 9, 0xd9d4d039u, 4);
+		VSTEP(TH, d, a, b, c, 12, 0xe6db99e5u, 11);
+		VSTEP(TH, c, d, a, b, 15, 0x1fa27cf8u, 16);
+		VSTEP(TH, b, c, d, a, 2, 0xc4ac5665u, 23);
+		VSTEP(TI, a, b, c, d, 0, 0xf4292244u, 6);
+		VSTEP(TI, d, a, b, c, 7, 0x432aff97u, 10);
+		VSTEP(TI, c, d, a, b, 14, 0xab9423a7u, 15);
+		VSTEP(TI, b, c, d, a, 5, 0xfc93a039u, 21);
+		VSTEP(TI, a, b, c, d, 12, 0x655b59c3u, 6);
+		VSTEP(TI, d, a, b, c, 3, 0x8f0ccc92u, 10);
+		VSTEP(TI, c, d, a, b, 10, 0xffeff47du, 15);
+		VSTEP(TI, b, c, d, a, 1, 0x85845dd1u, 21);
+		VSTEP(TI, a, b, c, d, 8, 0x6fa87e4fu, 6);
+		VSTEP(TI, d, a, b, c, 15, 0xfe2ce6e0u, 10);
+		VSTEP(TI, c, d, a, b, 6, 0xa3014314u, 15);
+		VSTEP(TI, b, c, d, a, 13, 0x4e0811a1u, 21);
+		VSTEP(TI, a, b, c, d, 4, 0xf7537e82u, 6);
+		VSTEP(TI, d, a, b, c, 11, 0xbd3af235u, 10);
+		VSTEP(TI, c, d, a, b, 2, 0x2ad7d2bbu, 15);
+		VSTEP(TI, b, c, d, a, 9, 0xeb86d391u, 21);
 		va = _mm512_add_epi32(va, a);
 		vb = _mm512_add_epi32(vb, b);
 		vc = _mm512_add_epi32(vc, c);
@@ -328,60 +324,6 @@ __attribute__((target("avx512f"))) static void md5x16_blocks(uint32_t st[4][16],
 	_mm512_storeu_si512(st[1], vb);
 	_mm512_storeu_si512(st[2], vc);
 	_mm512_storeu_si512(st[3], vd);
-}
-
-/* 4 frames at once in 128-bit registers (AVX-512VL ternary logic / rotate): the same per-block latency as one
- * frame's scalar chain, so a batch of 2-4 frames finishes as fast as a single frame (the 16-lane kernel takes
- * about twice as long as one frame for any batch: its 16 x 16 transposes) */
-#define XSTEP(imm, a, b, c, d, wi, k, s) \
-	do { \
-		a = _mm_add_epi32(a, _mm_add_epi32(w[wi], _mm_set1_epi32((int)(k)))); \
-		a = _mm_add_epi32(a, _mm_ternarylogic_epi32(b, c, d, imm)); \
-		a = _mm_add_epi32(_mm_rol_epi32(a, s), b); \
-	} while (0)
-
-__attribute__((target("avx512f,avx512vl"))) static void md5x4_blocks(uint32_t st[4][16], const uint8_t *const lp[16],
-                                                                    size_t nblocks)
-{
-	__m128i va = _mm_loadu_si128((const __m128i *)st[0]), vb = _mm_loadu_si128((const __m128i *)st[1]);
-	__m128i vc = _mm_loadu_si128((const __m128i *)st[2]), vd = _mm_loadu_si128((const __m128i *)st[3]);
-	for (size_t n = 0; n < nblocks; ++n) {
-		__m128i w[16];
-		__m128i a = va, b = vb, c = vc, d = vd;
-		for (int g = 0; g < 4; ++g) {
-			/* words 4g .. 4g + 3 of the 4 lanes' blocks, transposed: w[4g + i] lane l = lane l's word 4g + i */
-			const __m128i r0 = _mm_loadu_si128((const __m128i *)(lp[0] + 64 * n + 16 * g));
-			const __m128i r1 = _mm_loadu_si128((const __m128i *)(lp[1] + 64 * n + 16 * g));
-			const __m128i r2 = _mm_loadu_si128((const __m128i *)(lp[2] + 64 * n + 16 * g));
-			const __m128i r3 = _mm_loadu_si128((const __m128i *)(lp[3] + 64 * n + 16 * g));
-			const __m128i t0 = _mm_unpacklo_epi32(r0, r1), t1 = _mm_unpackhi_epi32(r0, r1);
-			const __m128i t2 = _mm_unpacklo_epi32(r2, r3), t3 = _mm_unpackhi_epi32(r2, r3);
-			w[4 * g + 0] = _mm_unpacklo_epi64(t0, t2);
-			w[4 * g + 1] = _mm_unpackhi_epi64(t0, t2);
-			w[4 * g + 2] = _mm_unpacklo_epi64(t1, t3);
-			w[4 * g + 3] = _mm_unpackhi_epi64(t1, t3);
-		}
-		MD5_STEPS(XSTEP);
-		va = _mm_add_epi32(va, a);
-		vb = _mm_add_epi32(vb, b);
-		vc = _mm_add_epi32(vc, c);
-		vd = _mm_add_epi32(vd, d);
-	}
-	_mm_storeu_si128((__m128i *)st[0], va);
-	_mm_storeu_si128((__m128i *)st[1], vb);
-	_mm_storeu_si128((__m128i *)st[2], vc);
-	_mm_storeu_si128((__m128i *)st[3], vd);
-}
-
-static int have_avx512vl(void)
-{
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("M2DEC_AMD_MD5_NO_X4"); /* (A/B: batches of 2-4 on the 16-lane kernel) */
-		__builtin_cpu_init();
-		v = __builtin_cpu_supports("avx512vl") && !(e && atoi(e));
-	}
-	return v;
 }
 
 static int have_avx512(void)
@@ -420,13 +362,8 @@ int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
 			pb[l] = g->chroma + (size_t)stride * (f[0].crop[2] >> 1);
 			for (int k = 0; k < 4; ++k) st[k][l] = iv[k];
 		}
-		if (n <= 4 && have_avx512vl()) { /* (lanes 0-3 of st / pa / pb) */
-			md5x4_blocks(st, pa, na);
-			md5x4_blocks(st, pb, nb);
-		} else {
-			md5x16_blocks(st, pa, na);
-			md5x16_blocks(st, pb, nb);
-		}
+		md5x16_blocks(st, pa, na);
+		md5x16_blocks(st, pb, nb);
 		for (int l = 0; l < n; ++l) {
 			md5_t m;
 			uint8_t dg[16];

@@ -44,7 +44,7 @@ def lines(frames, n):
 
 @pytest.mark.parametrize("w,h,crop", [(1920, 1088, (0, 0, 0, 8)), (1280, 720, (0, 0, 0, 0)), (176, 144, (0, 0, 2, 6)),
                                       (48, 32, (0, 0, 0, 0)), (208, 120, (4, 6, 2, 2)), (16, 16, (0, 0, 0, 2))])
-@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 16])  # (2-4: the 4-lane kernel, 5-16: the 16-lane one)
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 16])
 def test_frames_md5_matches_hashlib(built, w, h, crop, n):
     rng = np.random.default_rng(w * 31 + n)
     _mem, frames = make_frames(rng, n, w, h, crop)

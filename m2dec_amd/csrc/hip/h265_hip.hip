@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <algorithm>
 #include <vector>
 #include "m2d_recon.h"
 #include "h265_dec.h"
@@ -1081,6 +1082,12 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_grid(const H265Args *ap)
 	if (tid == 0) __hip_atomic_store(&done[c], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+/* ---- the picture's records from the pinned arena into device memory (16 bytes per thread, grid-stride) */
+__global__ __launch_bounds__(256) void k_h265_upload(const uint4 *src, uint4 *dst, size_t n16)
+{
+	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
 /* ---- motion compensation (h265.cpp:3132-3595; oracle/h265_oracle.c mc_picture) */
 __constant__ int8_t c_luma_fir[4][8] = {{0, 0, 0, 64, 0, 0, 0, 0}, {-1, 4, -10, 58, 17, -5, 1, 0}, {-1, 4, -11, 40, 40, -11, 4, -1}, {0, 1, -5, 17, 58, -10, 4, -1}};
 __constant__ int8_t c_chroma_fir[8][4] = {{0, 64, 0, 0}, {2, 58, 10, 2}, {4, 54, 16, 2}, {6, 46, 28, 4}, {4, 36, 36, 4}, {4, 28, 46, 6}, {2, 16, 54, 4}, {2, 10, 58, 2}};
@@ -1353,8 +1360,8 @@ __global__ __launch_bounds__(256) void k_h265_sao(const H265Args *ap)
 
 /* ------------------------------------------------------------------ runtime
  * Pictures are dealt over up to 8 HIP streams (M2DEC_AMD_H265_STREAMS; default 8 when the process has 8 hardware
- * queues — GPU_MAX_HW_QUEUES, m2dec_amd_configure_queues — else 4), each with its own record
- * arenas, scratch words and SAO copy buffer.  Dependencies between pictures are host-ordered with events (no
+ * queues — GPU_MAX_HW_QUEUES, m2dec_amd_configure_queues — else 4), each with its own scratch words and SAO copy
+ * buffer; the record arenas are one ring.  Dependencies between pictures are host-ordered with events (no
  * kernel waits on another launch, so nothing here needs a workgroup budget):
  *   - read-after-write: a P / B picture's stream waits for the kernels of every reference frame's last picture;
  *   - write-after-read / -write: a picture's stream waits for the pictures that read its frame's previous
@@ -1381,15 +1388,16 @@ struct H265Gpu {
 	int *err_host = nullptr; /* page-locked: the error word as of each frame's copy-out ([H265R_MAX_FRAMES]) */
 	struct Arena {
 		uint8_t *host = nullptr, *dev = nullptr;
+		const uint8_t *host_dev = nullptr; /* the pinned host buffer's device address (k_h265_upload reads it) */
 		size_t size = 0;
 		hipEvent_t used = nullptr;
 	};
+	Arena ring[2 * NS]; /* record arenas, used in turn by every lane */
+	int ring_next = 0;
 	struct Lane {
 		uint8_t *copy = nullptr; /* the deblocked frame (SAO input) */
 		int *scratch = nullptr;  /* done flags + the block counter + CTU progress */
 		size_t scratch_n = 0;
-		Arena ar[2];
-		int next = 0;
 	} lane[NS];
 	int rr = 0;
 	/* timing: per picture, its kernels' start / end on its stream */
@@ -1404,6 +1412,8 @@ struct H265Gpu {
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
+	bool kcopy = true;         /* record upload by k_h265_upload (M2DEC_AMD_H265_KCOPY=0: hipMemcpyAsync) */
+	size_t max_total = 0;      /* the largest picture's arena bytes so far */
 	bool waves4 = true;        /* CTU kernels with two waves per plane (M2DEC_AMD_H265_WAVES=2: one) */
 	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
@@ -1564,8 +1574,10 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	/* the lane's arena: free once its last picture's upload and kernels are done (its own event: no wait on
 	 * the dependencies below); a larger one replaces it with headroom, the old one freed at the next
 	 * set_frames / destroy (hipFree waits for the whole device) */
-	H265Gpu::Arena &a = ln.ar[ln.next];
-	ln.next ^= 1;
+	/* the arenas are one ring for all lanes (each is reused every 2 NS pictures, so all of them soon hold the
+	 * largest picture's size and none is reallocated while decoding) */
+	H265Gpu::Arena &a = g->ring[g->ring_next];
+	g->ring_next = (g->ring_next + 1) % (2 * H265Gpu::NS);
 	lap("stream pick");
 	H265_CHECK(hipEventSynchronize(a.used));
 	lap("arena free");
@@ -1574,11 +1586,17 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		if (a.dev) g->grave_dev.push_back(a.dev);
 		a.host = a.dev = nullptr;
 		a.size = 0;
-		const size_t sz = al16(total + total / 4);
+		/* at least the largest picture seen so far, with headroom: every arena soon holds an intra picture */
+		const size_t want = total > g->max_total ? total : g->max_total;
+		const size_t sz = al16(want + want / 4);
 		H265_CHECK(hipHostMalloc((void **)&a.host, sz, hipHostMallocDefault));
 		H265_CHECK(hipMalloc((void **)&a.dev, sz));
+		void *hd = nullptr;
+		H265_CHECK(hipHostGetDevicePointer(&hd, a.host, 0));
+		a.host_dev = (const uint8_t *)hd;
 		a.size = sz;
 	}
+	if (total > g->max_total) g->max_total = total;
 	lap("arena alloc");
 	memcpy(a.host + o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
 	memcpy(a.host + o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
@@ -1621,7 +1639,17 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	memcpy(a.host + o_args, &h, sizeof(h));
 	const H265Args *args = (const H265Args *)(a.dev + o_args);
 	lap("record copy");
-	H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
+	if (g->kcopy) {
+		/* the upload as a kernel reading the pinned records over the host link: an SDMA copy queued behind an
+		 * earlier picture's copy-out (itself waiting for that picture's kernels) held this thread 8-10 ms once
+		 * per decode, the GPU idling meanwhile (round-5 H.265 timelines) */
+		const size_t n16 = total / 16;
+		const int grid = (int)std::min<size_t>(512, (n16 + 255) / 256);
+		hipLaunchKernelGGL(k_h265_upload, dim3(grid), dim3(256), 0, s, (const uint4 *)a.host_dev, (uint4 *)a.dev, n16);
+		H265_CHECK(hipGetLastError());
+	} else {
+		H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
+	}
 	lap("upload");
 	g->record_bytes += (int64_t)o_args;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
@@ -1729,12 +1757,12 @@ void h_destroy(void *p)
 	if (!g) return;
 	(void)hipSetDevice(g->dev);
 	(void)sync_all(g);
+	for (auto &a : g->ring) {
+		if (a.host) (void)hipHostFree(a.host);
+		if (a.dev) (void)hipFree(a.dev);
+		if (a.used) (void)hipEventDestroy(a.used);
+	}
 	for (auto &l : g->lane) {
-		for (auto &a : l.ar) {
-			if (a.host) (void)hipHostFree(a.host);
-			if (a.dev) (void)hipFree(a.dev);
-			if (a.used) (void)hipEventDestroy(a.used);
-		}
 		if (l.scratch) (void)hipFree(l.scratch);
 		if (l.copy) (void)hipFree(l.copy);
 	}
@@ -1773,6 +1801,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
 	if (const char *e = getenv("M2DEC_AMD_H265_WAVES")) g->waves4 = atoi(e) >= 4;
+	if (const char *e = getenv("M2DEC_AMD_H265_KCOPY")) g->kcopy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_ERR_ASYNC")) g->err_async = atoi(e) != 0;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");
@@ -1793,10 +1822,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 		(void)hipEventCreate(&t.t0);
 		(void)hipEventCreate(&t.t1);
 	}
-	for (int k = 0; k < g->ns; ++k)
-		for (auto &a : g->lane[k].ar) {
-			(void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
-		}
+	for (auto &a : g->ring) (void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
 	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess ||
 	    hipHostMalloc((void **)&g->err_host, sizeof(int) * H265R_MAX_FRAMES, hipHostMallocDefault) != hipSuccess) {
 		h_destroy(g);

@@ -122,9 +122,11 @@ struct Lds {
 	int16_t seq[2][132];   /* reference samples per component: [0 .. 4n] substitution order, filtered */
 	int16_t raw[132];      /* unfiltered copy (filter input) */
 	int16_t mat32[32 * 32]; /* the 32-point DCT matrix (built once per workgroup) */
-	int mat[32 * 32];      /* transform matrix of this block's size: mat[k * n + s] */
-	int t0[32 * 32];       /* coefficients, then the first-stage output */
-	int pred[2][32 * 32];  /* prediction, then prediction + residual */
+	int16_t mat[32 * 32];  /* transform matrix of this block's size: mat[k * n + s]; the butterfly's first-pass output */
+	int16_t t0[32 * 32];   /* coefficients, then the first-stage output */
+	int16_t pred[2][32 * 32]; /* prediction, then prediction + residual, saturated to int16 (the store clamps to
+	                           * 0..255: clamp(sat16(x)) == clamp(x)); the CTU kernels' small blocks: the residual.
+	                           * int16 keeps a wave's LDS at ~11 KB: the 4-wave CTU kernels fit two per CU */
 };
 
 __device__ __forceinline__ uint8_t *plane_px(const H265Args &a, int plane, int comp, int x, int y)
@@ -163,7 +165,7 @@ __device__ __forceinline__ void wsync()
  * (lane >> log2 N) + k 64 / N.  COLS: pass 1 (line = column x: in[j] = src[j][x], out to dst[b][x] as
  * sat16((v + 64) >> 7)); else pass 2 (line = row y: in[j] = src[y][j], dst[y][b] += sat16((v + 2048) >> 12)). */
 template <int N, bool COLS, bool ACC = true>
-__device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_t *mat32, int lane)
+__device__ __forceinline__ void idct_pass(const int16_t *src, int16_t *dst, const int16_t *mat32, int lane)
 {
 	constexpr int L = N == 8 ? 3 : (N == 16 ? 4 : 5), PAIRS = N * N / 2, PPL = PAIRS < 64 ? 1 : PAIRS / 64;
 	const int a = lane & (N - 1);
@@ -184,8 +186,8 @@ __device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_
 				dst[b * N + a] = sat16((e + o + 64) >> 7);
 				dst[(N - 1 - b) * N + a] = sat16((e - o + 64) >> 7);
 			} else if (ACC) {
-				dst[a * N + b] += sat16((e + o + 2048) >> 12);
-				dst[a * N + N - 1 - b] += sat16((e - o + 2048) >> 12);
+				dst[a * N + b] = (int16_t)sat16(dst[a * N + b] + sat16((e + o + 2048) >> 12));
+				dst[a * N + N - 1 - b] = (int16_t)sat16(dst[a * N + N - 1 - b] + sat16((e - o + 2048) >> 12));
 			} else {
 				dst[a * N + b] = sat16((e + o + 2048) >> 12);
 				dst[a * N + N - 1 - b] = sat16((e - o + 2048) >> 12);
@@ -195,7 +197,7 @@ __device__ __forceinline__ void idct_pass(const int *src, int *dst, const int16_
 }
 
 template <int N, bool ACC = true>
-__device__ __forceinline__ void idct_block(int *t0, int *tmp, int *pred, const int16_t *mat32, int lane)
+__device__ __forceinline__ void idct_block(int16_t *t0, int16_t *tmp, int16_t *pred, const int16_t *mat32, int lane)
 {
 	idct_pass<N, true>(t0, tmp, mat32, lane);
 	wsync();
@@ -220,7 +222,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 	const bool luma = t.plane == 0;
 	/* ---- prediction */
 	for (int c = 0; c < ncomp; ++c) {
-		int *pred = s.pred[c];
+		int16_t *pred = s.pred[c];
 		if (!(t.flags & H265R_TU_PRED)) {
 			for (int i = lane; i < n2; i += 64) pred[i] = src.ld(t.plane, c, t.x + (i & (n - 1)), t.y + (i >> log2));
 			continue;
@@ -323,16 +325,16 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 	/* ---- residual */
 	for (int c = 0; c < ncomp; ++c) {
 		const int kind = t.res[c];
-		int *pred = s.pred[c];
+		int16_t *pred = s.pred[c];
 		if (kind == H265R_RES_NONE) continue;
 		const int16_t *d = cbase + (t.coef[c] - clo); /* (the pool, or the CTU's coefficients staged in LDS) */
 		if (kind == H265R_RES_DC) {
 			const int dc = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
-			for (int i = lane; i < n2; i += 64) pred[i] += dc;
+			for (int i = lane; i < n2; i += 64) pred[i] = (int16_t)sat16(pred[i] + dc);
 			continue;
 		}
 		if (kind == H265R_RES_SKIP) {
-			for (int i = lane; i < n2; i += 64) pred[i] += (d[i] + 16) >> 5;
+			for (int i = lane; i < n2; i += 64) pred[i] = (int16_t)sat16(pred[i] + ((d[i] + 16) >> 5));
 			continue;
 		}
 		for (int i = lane; i < n2; i += 64) s.t0[i] = d[i];
@@ -365,7 +367,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 			const int x = i & (n - 1), y = i >> log2;
 			int e = 0;
 			for (int j = 0; j < n; ++j) e += s.mat[j * n + x] * s.t0[y * n + j];
-			pred[i] += sat16((e + 2048) >> 12);
+			pred[i] = (int16_t)sat16(pred[i] + sat16((e + 2048) >> 12));
 		}
 		wsync();
 	}
@@ -374,7 +376,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 		const int wpr = n >> 2;
 		for (int w = lane; w < n2 >> 2; w += 64) {
 			const int y = w / wpr, x = (w - y * wpr) * 4;
-			const int *q = s.pred[0] + y * n + x;
+			const int16_t *q = s.pred[0] + y * n + x;
 			const uint32_t v = (uint32_t)clampi(q[0], 0, 255) | ((uint32_t)clampi(q[1], 0, 255) << 8) |
 			                   ((uint32_t)clampi(q[2], 0, 255) << 16) | ((uint32_t)clampi(q[3], 0, 255) << 24);
 			src.st(0, t.x + x, t.y + y, v);
@@ -383,7 +385,7 @@ __device__ void do_block(const H265Args &a, const h265r_tu_t &t, Lds &s, int lan
 		const int wpr = n >> 1;
 		for (int w = lane; w < n2 >> 1; w += 64) {
 			const int y = w / wpr, x = (w - y * wpr) * 2;
-			const int *cb = s.pred[0] + y * n + x, *cr = s.pred[1] + y * n + x;
+			const int16_t *cb = s.pred[0] + y * n + x, *cr = s.pred[1] + y * n + x;
 			const uint32_t v = (uint32_t)clampi(cb[0], 0, 255) | ((uint32_t)clampi(cr[0], 0, 255) << 8) |
 			                   ((uint32_t)clampi(cb[1], 0, 255) << 16) | ((uint32_t)clampi(cr[1], 0, 255) << 24);
 			src.st(1, t.x + x, t.y + y, v);
@@ -522,7 +524,7 @@ __device__ void do_block_ctu(const H265Args &a, const h265r_tu_t &rec, CtuTile &
 			continue;
 		}
 		if (kind == H265R_RES_SKIP) continue; /* (per sample in phase 3) */
-		int *res = s.pred[c];
+		int16_t *res = s.pred[c];
 		for (int i = lane; i < n2; i += 64) s.t0[i] = d[i];
 		const bool dstm = kind == H265R_RES_DST;
 		if (!dstm && n >= 8) {

@@ -1134,6 +1134,46 @@ struct StagePool {
  * inside sync_frame, i.e. inside peek / get_decoded_frame.  Between API calls nothing in flight
  * points into caller memory. */
 const size_t kStgTail = 64;
+
+/* up to 3 ranges per picture x BMAX pictures, copied by k_upload (blockIdx.y = range) */
+struct UploadList {
+	const uint8_t *src[3 * 4];
+	uint8_t *dst[3 * 4];
+	size_t bytes[3 * 4];
+	int n;
+	void add(const uint8_t *s_, uint8_t *d_, size_t b_)
+	{
+		src[n] = s_;
+		dst[n] = d_;
+		bytes[n] = b_;
+		++n;
+	}
+};
+
+/* 16 bytes per thread where source and destination are 16-byte aligned (the arena regions are), the tail bytewise */
+__global__ __launch_bounds__(256) void k_upload(UploadList ul)
+{
+	const int r = blockIdx.y;
+	const uint8_t *src = ul.src[r];
+	uint8_t *dst = ul.dst[r];
+	const size_t bytes = ul.bytes[r];
+	const bool al = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+	const size_t n16 = al ? bytes / 16 : 0;
+	const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+	for (size_t i = t; i < n16; i += stride) ((uint4 *)dst)[i] = ((const uint4 *)src)[i];
+	for (size_t i = n16 * 16 + t; i < bytes; i += stride) dst[i] = src[i];
+}
+
+/* M2DEC_AMD_KCOPY=0: the records go up by hipMemcpyAsync (SDMA) as before round 5 */
+static bool kcopy()
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("M2DEC_AMD_KCOPY");
+		v = e && *e ? atoi(e) != 0 : 1;
+	}
+	return v != 0;
+}
 /* The error word reaches the host by a synchronous 4-byte hipMemcpy per frame (on the null stream, which the
  * non-blocking decode streams do not wait for).  M2DEC_AMD_ERR_SYNC=0 copies it behind the frame on the
  * picture's stream into the staging buffer's tail instead — measured 15 % slower on 8 concurrent streams (1539
@@ -1410,14 +1450,36 @@ int launch_held(HipBackend *b)
 		flush_timing(b, *ts);
 		CHECK(hipEventRecord(ts->e[0], s));
 	}
-	for (int i = 0; i < n; ++i) {
-		/* mb | dbk | used slices in one copy, then the used inter and coefficient prefixes (m2r_arena_layout) */
-		const Arena *a = b->held[i].a;
-		const m2r_picture_t *pic = &a->pic;
-		const uint8_t *src = a->ext ? a->ext : a->host;
-		CHECK(hipMemcpyAsync(a->dev, src, a->off_slice + pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
-		if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, src + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
-		if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, src + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+	if (kcopy()) {
+		/* the records by one kernel reading the pinned arenas over the host link (k_upload): an SDMA upload queued
+		 * behind a copy-out that waits for an earlier picture's kernels can hold this thread for milliseconds
+		 * (the H.265 back end measured 8-10 ms; here launches averaged 0.44 ms of waits + uploads in a slow c3
+		 * decode against 0.07 in a normal one, the GPU idle 7.6 ms of it) */
+		UploadList ul;
+		ul.n = 0;
+		for (int i = 0; i < n; ++i) {
+			const Arena *a = b->held[i].a;
+			const m2r_picture_t *pic = &a->pic;
+			const uint8_t *src = a->ext ? a->ext : a->host;
+			void *dsrc = nullptr;
+			CHECK(hipHostGetDevicePointer(&dsrc, (void *)src, 0));
+			const uint8_t *ds = (const uint8_t *)dsrc;
+			ul.add(ds, a->dev, a->off_slice + pic->n_slices * sizeof(m2r_slice_t));
+			if (pic->n_inter) ul.add(ds + a->off_inter, a->dev + a->off_inter, pic->n_inter * sizeof(m2r_inter_t));
+			if (pic->n_coef) ul.add(ds + a->off_coef, a->dev + a->off_coef, pic->n_coef * sizeof(int16_t));
+		}
+		hipLaunchKernelGGL(k_upload, dim3(64, ul.n), dim3(256), 0, s, ul);
+		CHECK(hipGetLastError());
+	} else {
+		for (int i = 0; i < n; ++i) {
+			/* mb | dbk | used slices in one copy, then the used inter and coefficient prefixes (m2r_arena_layout) */
+			const Arena *a = b->held[i].a;
+			const m2r_picture_t *pic = &a->pic;
+			const uint8_t *src = a->ext ? a->ext : a->host;
+			CHECK(hipMemcpyAsync(a->dev, src, a->off_slice + pic->n_slices * sizeof(m2r_slice_t), hipMemcpyHostToDevice, s));
+			if (pic->n_inter) CHECK(hipMemcpyAsync(a->dev + a->off_inter, src + a->off_inter, pic->n_inter * sizeof(m2r_inter_t), hipMemcpyHostToDevice, s));
+			if (pic->n_coef) CHECK(hipMemcpyAsync(a->dev + a->off_coef, src + a->off_coef, pic->n_coef * sizeof(int16_t), hipMemcpyHostToDevice, s));
+		}
 	}
 	if (ts) CHECK(hipEventRecord(ts->e[1], s));
 	m2d_tl('M', n, k);

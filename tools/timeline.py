@@ -12,8 +12,18 @@ ev = [(int(r["t_ns"]), r["kind"], int(r["a"]), int(r["b"])) for r in host]
 ev.sort()
 starts = [e for e in ev if e[1] == "D"]
 ends = [e for e in ev if e[1] == "d"]
-t0, t1 = starts[-1][0], ends[-1][0]
-win = [e for e in ev if t0 <= e[0] <= t1 + 50_000_000]
+# TL_DECODE=k: the k-th decode of the run (default the last); TL_DECODE=slowest: the longest one
+_sel = os.environ.get("TL_DECODE")
+TAIL_NS = 100_000 if _sel is not None else 50_000_000  # (a chosen decode: nothing of the next one)
+_pairs = list(zip([e[0] for e in starts], [e[0] for e in ends]))
+print("decode intervals (ms):", [round((b - a) / 1e6, 2) for a, b in _pairs])
+if _sel == "slowest":
+    t0, t1 = max(_pairs, key=lambda p: p[1] - p[0])
+elif _sel is not None:
+    t0, t1 = _pairs[int(_sel)]
+else:
+    t0, t1 = starts[-1][0], ends[-1][0]
+win = [e for e in ev if t0 <= e[0] <= t1 + TAIL_NS]
 ms = lambda t: (t - t0) / 1e6  # noqa: E731
 
 
@@ -22,8 +32,8 @@ def trace(pat):
     return list(csv.DictReader(open(f[0]))) if f else []
 
 
-kern = [r for r in trace("*kernel_trace.csv") if int(r["Start_Timestamp"]) >= t0 - 1_000_000 and int(r["End_Timestamp"]) <= t1 + 50_000_000]
-copies = [r for r in trace("*memory_copy_trace.csv") if t0 - 1_000_000 <= int(r["Start_Timestamp"]) <= t1 + 50_000_000]
+kern = [r for r in trace("*kernel_trace.csv") if int(r["Start_Timestamp"]) >= t0 - 1_000_000 and int(r["End_Timestamp"]) <= t1 + TAIL_NS]
+copies = [r for r in trace("*memory_copy_trace.csv") if t0 - 1_000_000 <= int(r["Start_Timestamp"]) <= t1 + TAIL_NS]
 print(f"decode interval {ms(t1):.2f} ms  ({len(kern)} kernels, {len(copies)} copies in the window)")
 
 parse = {}

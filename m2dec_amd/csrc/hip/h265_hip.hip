@@ -1415,6 +1415,7 @@ struct H265Gpu {
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
 	bool kcopy = true;         /* record upload by k_h265_upload (M2DEC_AMD_H265_KCOPY=0: hipMemcpyAsync) */
+	bool kcopy_d2h = false;    /* M2DEC_AMD_KCOPY_D2H=1: the frame down by k_h265_upload writing the pinned staging buffer */
 	size_t max_total = 0;      /* the largest picture's arena bytes so far */
 	bool waves4 = true;        /* CTU kernels with two waves per plane (M2DEC_AMD_H265_WAVES=2: one) */
 	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
@@ -1719,7 +1720,14 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	const int c = pic->slot;
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
 	if (!g->stg[c]) H265_CHECK(hipHostMalloc((void **)&g->stg[c], bytes, hipHostMallocDefault));
-	H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
+	if (g->kcopy_d2h && bytes % 16 == 0) {
+		void *dh = nullptr;
+		H265_CHECK(hipHostGetDevicePointer(&dh, g->stg[c], 0));
+		hipLaunchKernelGGL(k_h265_upload, dim3(256), dim3(256), 0, s, (const uint4 *)h.frame, (uint4 *)dh, bytes / 16);
+		H265_CHECK(hipGetLastError());
+	} else {
+		H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
+	}
 	if (g->err_async) H265_CHECK(hipMemcpyAsync(&g->err_host[c], g->err, sizeof(int), hipMemcpyDeviceToHost, s));
 	H265_CHECK(hipEventRecord(g->ev[c], s));
 	lap("copy-out");
@@ -1804,6 +1812,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
 	if (const char *e = getenv("M2DEC_AMD_H265_WAVES")) g->waves4 = atoi(e) >= 4;
 	if (const char *e = getenv("M2DEC_AMD_H265_KCOPY")) g->kcopy = atoi(e) != 0;
+	if (const char *e = getenv("M2DEC_AMD_KCOPY_D2H")) g->kcopy_d2h = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_ERR_ASYNC")) g->err_async = atoi(e) != 0;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");

@@ -1174,6 +1174,20 @@ static bool kcopy()
 	}
 	return v != 0;
 }
+/* The frame goes down by k_upload writing the pinned staging buffer over the host link instead of an SDMA copy
+ * while more than one decoder context of this process is live on the device: 8 concurrent c3 streams 2120 vs
+ * 2007 fps, but one c3 decode 30.5 vs 29.6 ms and C5 46.7 vs 44.2 ms (the SDMA engine writes host memory faster
+ * than the CUs do; profiles/r131_ab_kd2h.txt).  M2DEC_AMD_KCOPY_D2H=0 never, =1 always */
+static bool kcopy_d2h(int dev)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("M2DEC_AMD_KCOPY_D2H");
+		v = e && *e ? atoi(e) : 2;
+	}
+	if (v == 2) return g_live_backends[dev & 15].load(std::memory_order_relaxed) > 1;
+	return v != 0;
+}
 /* The error word reaches the host by a synchronous 4-byte hipMemcpy per frame (on the null stream, which the
  * non-blocking decode streams do not wait for).  M2DEC_AMD_ERR_SYNC=0 copies it behind the frame on the
  * picture's stream into the staging buffer's tail instead — measured 15 % slower on 8 concurrent streams (1539
@@ -1292,7 +1306,17 @@ int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
 		return -1;
 	}
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][0], s));
-	CHECK(hipMemcpyAsync(b->stg[slot], cur, b->stg_size, hipMemcpyDeviceToHost, s));
+	if (kcopy_d2h(b->sc.dev)) {
+		void *dh = nullptr;
+		CHECK(hipHostGetDevicePointer(&dh, b->stg[slot], 0));
+		UploadList ul;
+		ul.n = 0;
+		ul.add(cur, (uint8_t *)dh, b->stg_size);
+		hipLaunchKernelGGL(k_upload, dim3(256, 1), dim3(256), 0, s, ul);
+		CHECK(hipGetLastError());
+	} else {
+		CHECK(hipMemcpyAsync(b->stg[slot], cur, b->stg_size, hipMemcpyDeviceToHost, s));
+	}
 	if (!err_sync()) CHECK(hipMemcpyAsync(b->stg[slot] + b->stg_size, b->sc.err, sizeof(int), hipMemcpyDeviceToHost, s));
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][1], s));
 	CHECK(hipEventRecord(b->slot_ev[slot], s));

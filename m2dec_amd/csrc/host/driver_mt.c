@@ -28,6 +28,10 @@
 #define MD5_MIN_BATCH 8    /* a batch costs about the same CPU time for 2 or 16 frames: a thread waits for
                               this many (or MD5_WAIT_S after the oldest was queued, or the end) */
 #define MD5_WAIT_S 0.004
+/* the shared pipe of several concurrent streams: frames arrive ~4x as fast, so full 16-frame batches cost half
+ * the CPU time per frame of 8-frame ones (8 streams 2142 vs 2059 fps, profiles/r131_ab_md5_streams.txt) */
+#define MD5_MIN_BATCH_STREAMS 16
+#define MD5_WAIT_S_STREAMS 0.008
 #define MD5_THREADS_MAX 16
 #define MD5_THREADS 16     /* one stream: a 16-frame batch of 1080p takes one core ~6.5 ms on the box's EPYC
                               9575F, one frame alone 3.3 ms (tools/md5_batch_bench.py, profiles/r85_md5_batch.txt);
@@ -201,8 +205,8 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	pthread_cond_init(&p->cv_job, NULL);
 	pthread_cond_init(&p->cv_free, NULL);
 	if (getenv("M2DEC_AMD_MD5_DELAY_US")) p->delay_us = atoi(getenv("M2DEC_AMD_MD5_DELAY_US"));
-	p->min_batch = MD5_MIN_BATCH;
-	p->wait_s = MD5_WAIT_S;
+	p->min_batch = streams > 1 ? MD5_MIN_BATCH_STREAMS : MD5_MIN_BATCH;
+	p->wait_s = streams > 1 ? MD5_WAIT_S_STREAMS : MD5_WAIT_S;
 	if (getenv("M2DEC_AMD_MD5_MIN_BATCH")) p->min_batch = atoi(getenv("M2DEC_AMD_MD5_MIN_BATCH")); /* tuning */
 	if (getenv("M2DEC_AMD_MD5_WAIT_US")) p->wait_s = 1e-6 * atoi(getenv("M2DEC_AMD_MD5_WAIT_US"));
 	if (p->min_batch < 1) p->min_batch = 1;

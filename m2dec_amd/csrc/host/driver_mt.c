@@ -22,6 +22,19 @@
 #include "h264_dec.h"
 #include "m2dec_amd.h"
 
+/* M2DEC_AMD_THREAD_CPU=1: a driver thread prints its CPU time when it ends (tools/thread_cpu.py reads it: an
+ * exited thread is gone from /proc/self/task) */
+static void thread_cpu_report(const char *name)
+{
+	static int on = -1;
+	if (on < 0) on = getenv("M2DEC_AMD_THREAD_CPU") && atoi(getenv("M2DEC_AMD_THREAD_CPU"));
+	if (on) {
+		struct timespec ts;
+		clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+		fprintf(stderr, "thread-cpu %s %.3f\n", name, 1e3 * ts.tv_sec + 1e-6 * ts.tv_nsec);
+	}
+}
+
 #define MD5_RING 64        /* frames queued or being hashed (all streams of a pipe) */
 #define MD5_EXTRA 40       /* frames a stream's decoder gets beyond its need (held by queued MD5s meanwhile) */
 #define MD5_BATCH 16       /* frames one thread hashes together (m2dec_amd_frames_md5 lanes) */
@@ -158,6 +171,7 @@ static void *md5_worker(void *arg)
 		pthread_cond_broadcast(&p->cv_free);
 	}
 	pthread_mutex_unlock(&p->mu);
+	thread_cpu_report("m2d-md5");
 	return NULL;
 }
 
@@ -396,6 +410,7 @@ static void *stream_worker(void *arg)
 	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS");
 	const int pt = e && atoi(e) > 0 ? atoi(e) : 8; /* profiles/r59_sweep_e2e.txt: 8 streams, 3 -> ~1440, 8 -> ~1490 fps */
 	j->result = stream_md5(j->pipe, j->data, j->len, NULL, j->device, -1, pt, j->md5s, j->max, NULL);
+	thread_cpu_report("m2d-stream");
 	return NULL;
 }
 

@@ -718,6 +718,9 @@ static h264_job_t *pick_job(struct h264_async *as, h264_job_t **slice_of, int *s
 	return NULL;
 }
 
+/* pool workers driving pipelines after their jobs, wall and thread CPU time (M2DEC_AMD_ASYNC_STATS) */
+static long long g_drive_ns, g_drive_cpu_ns, g_job_cpu_ns;
+
 /* pool workers inside a job or slice, all pipelines (m2dec_parse_busy: the MD5 pipe's tail mode) */
 static int g_parse_running;
 
@@ -761,6 +764,8 @@ static void *pool_worker(void *arg)
 			pj->sl_done++;
 		} else {
 			const double tp = now_s(); /* (two clock reads per picture: the parse time is always kept) */
+			struct timespec jc0;
+			if (as->stats) clock_gettime(CLOCK_THREAD_CPUTIME_ID, &jc0);
 			m2d_tl('P', j->seq, j->snap[0]->sh.slice_type);
 			if (dep_err) {
 				j->err = 1;
@@ -776,6 +781,12 @@ static void *pool_worker(void *arg)
 			}
 			if (!j->err) pic_refs(&j->pic);
 			if (g_nonref_delay_us && j->nonref) usleep((useconds_t)g_nonref_delay_us);
+			if (as->stats) {
+				struct timespec jc1;
+				clock_gettime(CLOCK_THREAD_CPUTIME_ID, &jc1);
+				__atomic_fetch_add(&g_job_cpu_ns, (long long)(jc1.tv_sec - jc0.tv_sec) * 1000000000LL + (jc1.tv_nsec - jc0.tv_nsec),
+				                   __ATOMIC_RELAXED);
+			}
 			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
 			m2d_tl('p', j->seq, j->snap[0]->sh.slice_type);
@@ -789,7 +800,20 @@ static void *pool_worker(void *arg)
 		as->running--;
 		__atomic_fetch_sub(&g_parse_running, 1, __ATOMIC_RELAXED);
 		pthread_cond_broadcast(&as->cv_done);
-		if (j) pipe_drive(as);
+		if (j) {
+			if (as->stats) { /* (process-wide: `as` may be gone once the drive returns) */
+				struct timespec c0, c1;
+				const double w0 = now_s();
+				clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c0);
+				pipe_drive(as);
+				clock_gettime(CLOCK_THREAD_CPUTIME_ID, &c1);
+				__atomic_fetch_add(&g_drive_ns, (long long)(1e9 * (now_s() - w0)), __ATOMIC_RELAXED);
+				__atomic_fetch_add(&g_drive_cpu_ns, (long long)(c1.tv_sec - c0.tv_sec) * 1000000000LL + (c1.tv_nsec - c0.tv_nsec),
+				                   __ATOMIC_RELAXED);
+			} else {
+				pipe_drive(as);
+			}
+		}
 	}
 	return NULL;
 }
@@ -978,10 +1002,12 @@ void h264_async_stop(h264_dec_t *d)
 		fprintf(stderr, "async: %ld jobs, depth %d; caller: lookahead %.3f s (col-store waits %.3f s, slice copies "
 		                "%.3f s), oldest-done waits %.3f s, record copies %.3f s, back-end submit %.3f s; workers "
 		                "parse %.3f s; jobs created so far in the process %ld; early submissions %ld; page-locked job "
-		                "arenas %.1f MB (pooled %.1f MB)\n",
+		                "arenas %.1f MB (pooled %.1f MB); co-located row waits in the process %.3f s; workers driving in the process %.3f s (CPU %.3f s), job CPU %.3f s\n",
 		        as->seq, as->depth, as->t_la, as->t_col_wait, as->t_slice, as->t_done_wait, as->t_copy, as->t_submit,
 		        as->t_parse, g_jobs_new, as->n_early, (double)__atomic_load_n(&g_pinned_bytes, __ATOMIC_RELAXED) / 1e6,
-		        (double)g_pool_pinned / 1e6);
+		        (double)g_pool_pinned / 1e6, 1e-9 * (double)h264_col_spin_ns(), 1e-9 * (double)__atomic_load_n(&g_drive_ns, __ATOMIC_RELAXED),
+		        1e-9 * (double)__atomic_load_n(&g_drive_cpu_ns, __ATOMIC_RELAXED),
+		        1e-9 * (double)__atomic_load_n(&g_job_cpu_ns, __ATOMIC_RELAXED));
 	/* no pool worker starts anything of this pipeline any more; wait for the ones inside it */
 	pthread_mutex_lock(as->mu);
 	as->quit = 1;

@@ -405,6 +405,7 @@ int h264_dpb_pop(h264_dpb_t *dpb, int bypass);
 
 /* h264_mb.c */
 int h264_slice_data(h264_dec_t *d);
+long long h264_col_spin_ns(void); /* time parse workers spent waiting for co-located rows (col_wait) */
 
 /* h264_async.c */
 /* h264_syntax.c: reference-picture path counters (m2dec_amd_h264_parser_hits) */

@@ -14,6 +14,7 @@
 #include <string.h>
 #include <sched.h>
 #include <unistd.h>
+#include <time.h>
 #include "h264_dec.h"
 
 /* blkIdx -> 4x4 position (spec 6.4.3) and inverse */
@@ -662,21 +663,35 @@ static void spatial_ref_mv(slice_ctx_t *s)
 	s->direct_ready = 1;
 }
 
+/* thread time spent waiting in col_wait, process-wide (M2DEC_AMD_ASYNC_STATS) */
+static long long g_col_spin_ns;
+long long h264_col_spin_ns(void) { return __atomic_load_n(&g_col_spin_ns, __ATOMIC_RELAXED); }
+
+static long long mono_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+
 /* the co-located MB of the current one is stored: wait for the parse writing it (row pipelining) */
 static void col_wait(slice_ctx_t *s)
 {
 	h264_dec_t *d = s->d;
+	long long t0 = 0;
 	for (int spins = 0;; ++spins) {
 		const int v = __atomic_load_n(d->col_sub, __ATOMIC_ACQUIRE);
-		if (v < 0) { /* that parse failed: this picture fails too (job_run) */
-			d->col_sub_fail = 1;
-			d->col_sub_ok = 1 << 30;
+		if (v < 0 || v > s->addr) {
+			if (spins) __atomic_fetch_add(&g_col_spin_ns, mono_ns() - t0, __ATOMIC_RELAXED);
+			if (v < 0) { /* that parse failed: this picture fails too (job_run) */
+				d->col_sub_fail = 1;
+				d->col_sub_ok = 1 << 30;
+			} else {
+				d->col_sub_ok = v;
+			}
 			return;
 		}
-		if (v > s->addr) {
-			d->col_sub_ok = v;
-			return;
-		}
+		if (!spins) t0 = mono_ns();
 		if (spins < 64) __builtin_ia32_pause();
 		else sched_yield(); /* (the writer may be waiting for a CPU) */
 	}

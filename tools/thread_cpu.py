@@ -43,6 +43,14 @@ def run():
 
 run()
 run()
+# threads that end inside the timed passes (each pass's m2d-stream / m2d-md5 threads) are gone from
+# /proc/self/task: with M2DEC_AMD_THREAD_CPU=1 the library prints their CPU time on stderr as they end
+exited = os.environ.get("M2DEC_AMD_THREAD_CPU") == "1"
+if exited:
+    sys.stderr.flush()
+    log = open("/tmp/thread_cpu_%d.log" % os.getpid(), "w+")
+    saved = os.dup(2)
+    os.dup2(log.fileno(), 2)
 a = snap()
 t0, fr = time.perf_counter(), 0
 r0 = os.times()
@@ -56,6 +64,14 @@ nth = collections.Counter()
 for t, (name, cpu) in b.items():
     by[name] += cpu - a.get(t, (name, 0.0))[1]
     nth[name] += 1
+if exited:
+    os.dup2(saved, 2)
+    log.seek(0)
+    for line in log:
+        f = line.split()
+        if len(f) == 3 and f[0] == "thread-cpu":
+            by[f[1] + " (exited)"] += float(f[2]) / 1e3
+            nth[f[1] + " (exited)"] += 1
 proc = (r1.user - r0.user) + (r1.system - r0.system)
 print(f"{mode}: {fr / dt:.1f} fps, {proc / dt:.2f} cores busy ({(r1.system - r0.system) / dt:.2f} system), "
       f"{1e3 * proc / fr:.2f} CPU-ms per frame")

@@ -1164,29 +1164,25 @@ __global__ __launch_bounds__(256) void k_upload(UploadList ul)
 	for (size_t i = n16 * 16 + t; i < bytes; i += stride) dst[i] = src[i];
 }
 
-/* M2DEC_AMD_KCOPY=0: the records go up by hipMemcpyAsync (SDMA) as before round 5 */
-static bool kcopy()
+/* M2DEC_AMD_KCOPY=0: the records go up by hipMemcpyAsync (SDMA) as before round 5 (read per back end) */
+static bool kcopy_knob()
 {
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("M2DEC_AMD_KCOPY");
-		v = e && *e ? atoi(e) != 0 : 1;
-	}
-	return v != 0;
+	const char *e = getenv("M2DEC_AMD_KCOPY");
+	return e && *e ? atoi(e) != 0 : true;
 }
 /* The frame goes down by k_upload writing the pinned staging buffer over the host link instead of an SDMA copy
  * while more than one decoder context of this process is live on the device: 8 concurrent c3 streams 2120 vs
  * 2007 fps, but one c3 decode 30.5 vs 29.6 ms and C5 46.7 vs 44.2 ms (the SDMA engine writes host memory faster
- * than the CUs do; profiles/r131_ab_kd2h.txt).  M2DEC_AMD_KCOPY_D2H=0 never, =1 always */
-static bool kcopy_d2h(int dev)
+ * than the CUs do; profiles/r131_ab_kd2h.txt).  M2DEC_AMD_KCOPY_D2H=0 never, =1 always (read per back end) */
+static int kcopy_d2h_knob()
 {
-	static int v = -1;
-	if (v < 0) {
-		const char *e = getenv("M2DEC_AMD_KCOPY_D2H");
-		v = e && *e ? atoi(e) : 2;
-	}
-	if (v == 2) return g_live_backends[dev & 15].load(std::memory_order_relaxed) > 1;
-	return v != 0;
+	const char *e = getenv("M2DEC_AMD_KCOPY_D2H");
+	return e && *e ? atoi(e) : 2;
+}
+static bool kcopy_d2h(int mode, int dev)
+{
+	if (mode == 2) return g_live_backends[dev & 15].load(std::memory_order_relaxed) > 1;
+	return mode != 0;
 }
 /* The error word reaches the host by a synchronous 4-byte hipMemcpy per frame (on the null stream, which the
  * non-blocking decode streams do not wait for).  M2DEC_AMD_ERR_SYNC=0 copies it behind the frame on the
@@ -1234,6 +1230,8 @@ struct HipBackend {
 	TimingSlot tr[16];
 	int tr_next = 0;
 	bool timing = true;
+	bool kcopy = true; /* records up by k_upload (M2DEC_AMD_KCOPY) */
+	int kd2h = 2;      /* frames down: 0 SDMA, 1 k_upload, 2 k_upload while several back ends live (M2DEC_AMD_KCOPY_D2H) */
 	/* guards Arena::held / pending / ext: records_busy reads them from any thread while the decoder's
 	 * serial calls (acquire, submit, flush, bind) change them */
 	std::mutex arena_mu;
@@ -1306,7 +1304,7 @@ int stage_copy(HipBackend *b, const uint8_t *cur, int slot, hipStream_t s)
 		return -1;
 	}
 	if (b->timing) CHECK(hipEventRecord(b->d2h_ev[slot][0], s));
-	if (kcopy_d2h(b->sc.dev)) {
+	if (kcopy_d2h(b->kd2h, b->sc.dev)) {
 		void *dh = nullptr;
 		CHECK(hipHostGetDevicePointer(&dh, b->stg[slot], 0));
 		UploadList ul;
@@ -1474,7 +1472,7 @@ int launch_held(HipBackend *b)
 		flush_timing(b, *ts);
 		CHECK(hipEventRecord(ts->e[0], s));
 	}
-	if (kcopy()) {
+	if (b->kcopy) {
 		/* the records by one kernel reading the pinned arenas over the host link (k_upload): an SDMA upload queued
 		 * behind a copy-out that waits for an earlier picture's kernels can hold this thread for milliseconds
 		 * (the H.265 back end measured 8-10 ms; here launches averaged 0.44 ms of waits + uploads in a slow c3
@@ -1730,6 +1728,8 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 		for (auto &e : t.e) CHECK(g_pool.event(device, true, &e));
 	const char *tm = getenv("M2DEC_AMD_TIMING");
 	b->timing = tm ? atoi(tm) != 0 : true;
+	b->kcopy = kcopy_knob();
+	b->kd2h = kcopy_d2h_knob();
 	out->self = b;
 	out->set_frames = be_set_frames;
 	out->acquire = be_acquire;

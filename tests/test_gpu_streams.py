@@ -43,6 +43,24 @@ def test_hip_md5_driver_matches_golden(built):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [
+    {"M2DEC_AMD_KCOPY": "0"},        # records up by SDMA copies instead of k_upload
+    {"M2DEC_AMD_KCOPY_D2H": "1"},    # frames down by k_upload on a single decoder too
+    {"M2DEC_AMD_KCOPY_D2H": "0"},    # frames down by SDMA with concurrent decoders too
+], ids=["records_sdma", "frames_kernel", "frames_sdma"])
+def test_hip_copy_variants_match_golden(built, monkeypatch, env):
+    """The upload / copy-out variants (read when a back end is created): one stream alone and two
+    concurrent ones (several live back ends: the default copy-out is then k_upload), each bit-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert m2dec_amd.decode_stream_md5(stream("c2_720p_s1")) == GOLDEN["c2_720p_s1"]["md5"]
+    names = ["cov_tools_s1", "c3_1080p_s1"]
+    got = m2dec_amd.decode_streams([stream(n) for n in names])
+    for n, g in zip(names, got):
+        assert g == GOLDEN[n]["md5"], n
+
+
+@pytest.mark.gpu
 def test_hip_concurrent_streams_match_golden(built):
     """Eight independent streams (the C4 set: c3 seeds 1..8) decoded at once on one GPU, one host
     thread and decoder context each (m2dec_amd_decode_streams_md5); every frame bit-exact."""

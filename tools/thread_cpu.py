@@ -18,6 +18,9 @@ def snap():
     for t in os.listdir("/proc/self/task"):
         try:
             name = open(f"/proc/self/task/{t}/comm").read().strip()
+            if int(t) == os.getpid():
+                name += " (main)"  # the caller's thread: the decoder's API / lookahead side; the others of that
+                # name are the HIP runtime's
             f = open(f"/proc/self/task/{t}/stat").read().rsplit(")", 1)[1].split()
             out[t] = (name, (int(f[11]) + int(f[12])) / TCK)
         except OSError:

@@ -107,10 +107,11 @@ static void cab_build(void)
 	}
 }
 
-/* branch-free on the MPS/LPS outcome, which is unpredictable for residual bins */
-static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
+/* branch-free on the MPS/LPS outcome, which is unpredictable for residual bins; the context state in and out
+ * through *st (a run of bins of one context keeps it in a register: no store-to-load forwarding per bin) */
+static inline int eng_decide(h264_cabac_eng_t *e, uint32_t *st)
 {
-	const uint32_t s = ctx[ctxidx];
+	const uint32_t s = *st;
 	const uint32_t lps = h264_range_lps[s >> 1][(e->range >> 6) & 3];
 	uint32_t range = e->range - lps;
 	const uint64_t scaled = (uint64_t)range << e->bits;
@@ -118,7 +119,7 @@ static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
 	const uint64_t m = (uint64_t)0 - is_lps;
 	e->value -= scaled & m;
 	range ^= (range ^ lps) & (uint32_t)m;
-	ctx[ctxidx] = cab_next[(is_lps << 7) | s];
+	*st = cab_next[(is_lps << 7) | s];
 	{
 		const int n = __builtin_clz(range) - 23;
 		e->range = range << n;
@@ -126,6 +127,14 @@ static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
 		eng_refill(e);
 	}
 	return (int)((s & 1) ^ is_lps);
+}
+
+static inline int eng_decision(h264_cabac_eng_t *e, uint8_t *ctx, int ctxidx)
+{
+	uint32_t st = ctx[ctxidx];
+	const int bin = eng_decide(e, &st);
+	ctx[ctxidx] = (uint8_t)st;
+	return bin;
 }
 
 /* branch-free: bypass bins (signs, suffixes) are coin flips to a branch predictor */
@@ -385,9 +394,11 @@ done:
 			lvl = 1;
 			eq1++;
 		} else {
-			int ctx2 = abase + 5 + imin(4 - (cat == 3), gt1);
+			const int ctx2 = abase + 5 + imin(4 - (cat == 3), gt1);
+			uint32_t st = ctx[ctx2];
 			lvl = 2;
-			while (lvl < 15 && eng_decision(&e, ctx, ctx2)) lvl++;
+			while (lvl < 15 && eng_decide(&e, &st)) lvl++;
+			ctx[ctx2] = (uint8_t)st;
 			if (lvl == 15) {
 				/* UEG0 suffix (9.3.2.3): unary prefix and k fixed bits in batches */
 				int k2 = 0;

@@ -979,12 +979,19 @@ static int cabac_mvd(h264_cabac_t *c, int base, int sum)
 	if (!cabac_decision(c, base + inc)) return 0;
 	e = c->e;
 	mvd = 1;
-	ci = base + 3;
-	while (eng_decision(&e, ctx, ci)) {
-		if (mvd < 4) ci++;
+	/* prefix bins 2..4 on contexts base + 3..5, bins 5..9 all on base + 6 (its state kept in a register) */
+	for (ci = base + 3; ci < base + 6; ++ci) {
+		if (!eng_decision(&e, ctx, ci)) goto sign;
 		mvd++;
-		if (mvd >= 9) {
-			/* UEG3 suffix: unary prefix of bypass 1s, then k fixed bits, in batches (9.3.2.3) */
+	}
+	{
+		uint32_t st = ctx[base + 6];
+		int more;
+		while ((more = eng_decide(&e, &st)) && ++mvd < 9)
+			;
+		ctx[base + 6] = (uint8_t)st;
+		if (more) {
+			/* mvd 9: UEG3 suffix, a unary prefix of bypass 1s, then k fixed bits, in batches (9.3.2.3) */
 			int k = 3;
 			const int ones = eng_bypass_ones(&e);
 			if (ones >= 0 && ones <= 13) {
@@ -999,9 +1006,9 @@ static int cabac_mvd(h264_cabac_t *c, int base, int sum)
 				}
 				while (k-- > 0) mvd += eng_bypass(&e) << k;
 			}
-			break;
 		}
 	}
+sign:
 	mvd = eng_bypass_sign(&e, mvd);
 	c->e = e;
 	return mvd;

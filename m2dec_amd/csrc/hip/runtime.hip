@@ -458,7 +458,9 @@ struct Sched {
 	int seq = 0;               /* pictures launched */
 	SlotSeq slot_seq;          /* seq + 1 of the picture held by each slot */
 	int inter_grid = 80;       /* persistent inter workers per picture (5/16 of the CUs) */
-	int row_wgs = 12;          /* row-pair workgroups of a P / B picture (pairs taken from a queue) */
+	int row_wgs = 16;          /* row-pair workgroups of a P / B picture (pairs taken from a queue); r133 sweep on
+	                            * the round-5 kernels: 8 / 12 / 16 / 20 / 24 -> replay ~6800 / 7640 / 7745 / 7615 /
+	                            * 7590 fps, c3 decode median 30.06 (12) vs 29.49 ms (16), profiles/r133_sweep_replay_grid.txt */
 	int rr = 0;
 	int pics_fit = 1;          /* pictures per decode-path launch that keep NSTREAMS launches within the budget */
 	int resident_per_cu = 0;   /* k_picture workgroups resident per CU at this geometry */

@@ -49,7 +49,11 @@ static void thread_cpu_report(const char *name)
 #define MD5_THREADS 16     /* one stream: a 16-frame batch of 1080p takes one core ~6.5 ms on the box's EPYC
                               9575F, one frame alone 3.3 ms (tools/md5_batch_bench.py, profiles/r85_md5_batch.txt);
                               most threads only work in tail mode (below); M2DEC_AMD_MD5_THREADS */
-#define MD5_TAIL_PARSE_BUSY 4 /* tail mode once at most this many parse workers are busy */
+/* tail mode once at most this many parse workers are busy: one stream 12 (c3 medians 28.83 vs 29.21 and 29.77 vs
+ * 30.97 ms against 4 on two boxes, profiles/r137_ab_md5_tail_busy.txt; 16 = always: 30.15 ms), the shared pipe of
+ * concurrent streams 4 (their pool stays busy until near the end) */
+#define MD5_TAIL_PARSE_BUSY 12
+#define MD5_TAIL_PARSE_BUSY_STREAMS 4
 #define MD5_BIG_FRAME ((size_t)6 << 20) /* frames above this (4K) are not batched short of min_batch */
 
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
@@ -82,6 +86,7 @@ typedef struct md5_pipe {
 	int delay_us;            /* M2DEC_AMD_MD5_DELAY_US (tests) */
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
+	int tail_busy;           /* tail mode at most this many busy parse workers (M2DEC_AMD_MD5_TAIL_BUSY) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
@@ -113,7 +118,7 @@ static void *md5_worker(void *arg)
 		 * busy, batches keep the MD5 CPU time small. */
 		int tail = 0;
 		for (;;) { /* (the tail test is redone on every wake: the parse pool may finish while a thread waits) */
-			tail = p->tail_mode && m2dec_parse_busy() <= MD5_TAIL_PARSE_BUSY;
+			tail = p->tail_mode && m2dec_parse_busy() <= p->tail_busy;
 			if (tail || p->quit || p->ended || p->head - p->next >= p->min_batch) break;
 			double left = p->t_queued[p->next % MD5_RING] + p->wait_s - now_s();
 			if (left <= 0) break;
@@ -227,6 +232,8 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	p->tail_mode = getenv("M2DEC_AMD_MD5_TAIL") ? atoi(getenv("M2DEC_AMD_MD5_TAIL")) != 0 : 1;
+	p->tail_busy = getenv("M2DEC_AMD_MD5_TAIL_BUSY") ? atoi(getenv("M2DEC_AMD_MD5_TAIL_BUSY"))
+	                                                 : (streams > 1 ? MD5_TAIL_PARSE_BUSY_STREAMS : MD5_TAIL_PARSE_BUSY);
 	p->streams = streams;
 	for (; p->nth < threads && p->nth < MD5_THREADS_MAX; ++p->nth)
 		if (pthread_create(&p->th[p->nth], NULL, md5_worker, p) != 0) break;

@@ -167,6 +167,14 @@ long long m2dec_amd_pinned_bytes(long long *pooled);
 int m2dec_amd_numa_cpus(const char *sysfs_root, const char *pci_bus_id, int *cpus, int max, int *node);
 int m2dec_amd_numa_node(void);
 
+/* The host CPU share (cpushare.c): affinity ∩ cgroup CPU quota (v2 cpu.max up the hierarchy, v1 cfs quota)
+ * ÷ the node's GPU ranks (ranks <= 0: LOCAL_WORLD_SIZE / M2DEC_AMD_LOCAL_RANKS) for a fake tree under
+ * sysfs_root ("" = the real one) and an affinity of aff_cpus CPUs (<= 0: this process's).  *quota_milli: the
+ * quota in milli-CPUs (-1 none).  m2dec_amd_cpu_gate: the share this process runs with, its busy-thread slots
+ * (parse pool size; MD5 batches wait for a free one), the MD5 batches that waited so far, parse / MD5 work now. */
+int m2dec_amd_cpu_share(const char *sysfs_root, int ranks, int aff_cpus, long *quota_milli, int *aff_out);
+int m2dec_amd_cpu_gate(int *slots, unsigned long *waits, int *primary, int *busy);
+
 /* The device-wide workgroup budget segment (devshare.c) under an arbitrary key, for tests and
  * diagnostics: open (creating it with cap_units), reserve (1 / 0), release, state, close. */
 void *m2dec_amd_share_open(const char *key, int cap_units);
@@ -334,6 +342,9 @@ int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_hip_timing_
 /* One checked pass: after every picture, download it and write its MD5 line (35 bytes per picture,
  * decoding order) into md5s. */
 int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s);
+/* Diagnostic: the same checked pass, every picture's raw NV12 bytes (W x H x 3 / 2, uncropped, decoding
+ * order) into out (n bytes, at least npics times that); tools/replay_diff.py locates wrong macroblocks. */
+int m2dec_amd_hip_replay_capture(m2dec_amd_hip_replay_t *r, unsigned char *out, size_t n);
 void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r);
 
 #ifdef __cplusplus

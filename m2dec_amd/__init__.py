@@ -166,6 +166,8 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_replay_timing.restype = ctypes.c_int
         L.m2dec_amd_hip_replay_md5.argtypes = [vp, ctypes.c_char_p]
         L.m2dec_amd_hip_replay_md5.restype = ctypes.c_int
+        L.m2dec_amd_hip_replay_capture.argtypes = [vp, ctypes.c_void_p, ctypes.c_size_t]
+        L.m2dec_amd_hip_replay_capture.restype = ctypes.c_int
         L.m2dec_amd_decode_table.argtypes = [vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ON_FRAME, vp, ctypes.POINTER(ctypes.c_int)]
         L.m2dec_amd_decode_table.restype = ctypes.c_int
@@ -186,6 +188,18 @@ def lib() -> ctypes.CDLL:
         L.m2dec_amd_hip_replay_destroy.restype = None
         _lib = L
     return _lib
+
+
+def cpu_gate() -> dict:
+    """The host CPU share this process runs with (cpushare.c): share, busy-thread slots (= parse pool), how
+    often an MD5 batch waited for a free slot, and the parse / MD5 work running now."""
+    L = lib()
+    sl, pr, bu = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    w = ctypes.c_ulong()
+    L.m2dec_amd_cpu_gate.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_ulong),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    share = L.m2dec_amd_cpu_gate(ctypes.byref(sl), ctypes.byref(w), ctypes.byref(pr), ctypes.byref(bu))
+    return {"share": share, "slots": sl.value, "md5_waits": w.value, "parse_now": pr.value, "md5_now": bu.value}
 
 
 def hip_available() -> bool:
@@ -496,6 +510,14 @@ class HipReplay:
             raise RuntimeError("m2dec_amd: replay md5 pass failed")
         raw = buf.raw
         return [raw[35 * i:35 * i + 32].decode() for i in range(self.npics)]
+
+    def capture(self) -> bytes:
+        """Raw NV12 pictures (uncropped) of one checked pass, decoding order, concatenated."""
+        fb = self.trace.width * self.trace.height * 3 // 2
+        buf = ctypes.create_string_buffer(fb * self.npics)
+        if lib().m2dec_amd_hip_replay_capture(self.h, buf, len(buf)) < 0:
+            raise RuntimeError("m2dec_amd: replay capture pass failed")
+        return buf.raw
 
     def md5_output_order(self):
         """One stream: its frames' MD5s in output order; several: one such list per stream."""

@@ -91,6 +91,12 @@ __device__ unsigned long long g_dstamps[160][3][128];
 /* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
 #define STAMPX(x, k) do { if ((x) < 16 && part == 0) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
+#ifdef M2DEC_DBG_INTRA
+/* diagnostic (-DM2DEC_DBG_INTRA, never in the product build): the first I picture's MB (0, 0) luma context
+ * before and after its reconstruction, read back with m2dec_amd_debug_intra (tools/replay_diff.py) */
+__device__ int g_dbg[2048];
+#endif
+
 /* ======================================================================== motion compensation */
 struct RefPlane {
 	const uint8_t *p;
@@ -789,7 +795,12 @@ __device__ __forceinline__ int ipred_taps(uint32_t w, int bits, const int *nv)
  * wave(s) with do_chroma (disjoint LDS: L, R[0..255], DC, F, HV / C, R[256..383]).  q: the MB's pool
  * segment (staged in LDS).  Reference: mb_intra4x4 / intraNxN / intra16x16 / intrapcm
  * (h264.cpp:3121-3254, 4083-4127, 4407-4555, 4708-4761), residual_chroma (2374-2461). */
-__device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *q, const int t_in, const bool do_luma,
+#ifdef M2DEC_BODY_NOINLINE
+#define M2DEC_BODY_ATTR __attribute__((noinline))
+#else
+#define M2DEC_BODY_ATTR __forceinline__
+#endif
+__device__ M2DEC_BODY_ATTR void intra_mb_body(const m2r_mb_t &m, const int16_t *q, const int t_in, const bool do_luma,
                                               const bool do_chroma, IntraLDS *ctx, const IntraTables *tabs)
 {
 	/* the lane index laundered per call: inside intra_row's MB loop every lane-dependent address
@@ -1143,7 +1154,12 @@ __device__ __forceinline__ void intra_mb_body(const m2r_mb_t &m, const int16_t *
 	}
 }
 
-__device__ __attribute__((noinline)) void intra_row(const int y, const int t, const int part, lds_u8 *lds, const int wave,
+#ifdef M2DEC_INTRA_ROW_INLINE
+#define M2DEC_INTRA_ROW_ATTR __attribute__((always_inline))
+#else
+#define M2DEC_INTRA_ROW_ATTR __attribute__((noinline))
+#endif
+__device__ M2DEC_INTRA_ROW_ATTR void intra_row(const int y, const int t, const int part, lds_u8 *lds, const int wave,
                           const m2r_mb_t *__restrict__ mbs, const int16_t *__restrict__ pool, uint8_t *cur, int W, int H, int Wmb,
                           uint8_t *hbi, const uint32_t tag, int *err)
 {
@@ -1284,7 +1300,28 @@ __device__ __attribute__((noinline)) void intra_row(const int y, const int t, co
 		WSYNC();
 		STAMPX(x, 0);
 
+#ifdef M2DEC_DBG_INTRA
+		const bool dbg_dump = x == 0 && y == 0 && do_luma && __builtin_amdgcn_readfirstlane(g_dbg[14]) != 12345;
+		if (dbg_dump) {
+			if (t < 8) g_dbg[t] = ((const int *)&m)[t];
+			for (int k = t; k < M2R_MB_COEF_MAX; k += 64) g_dbg[16 + k] = q[k];
+			for (int k = t; k < 17 * LW; k += 64) g_dbg[512 + k] = (&L[0][0])[k];
+			if (t == 0) g_dbg[15] = qb;
+		}
+		WSYNC();
+#endif
 		intra_mb_body(m, q, t, do_luma, do_chroma, ctx, tabs);
+#ifdef M2DEC_DBG_INTRA
+		WSYNC();
+		if (dbg_dump) {
+			for (int k = t; k < 17 * LW; k += 64) g_dbg[1024 + k] = (&L[0][0])[k];
+			for (int k = t; k < 384; k += 64) g_dbg[1536 + k] = R[k];
+			if (t < 16) g_dbg[1936 + t] = DC[t];
+			if (t < 4) g_dbg[1952 + t] = HV[t];
+			if (t == 0) g_dbg[14] = 12345;
+		}
+		WSYNC();
+#endif
 		STAMPX(x, 3);
 		/* ---- write back and hand off the bottom rows */
 		if (do_luma)
@@ -1746,6 +1783,9 @@ __device__ uint32_t bs_of(const m2r_mb_t *__restrict__ mbs, const m2r_inter_t *_
 	return str;
 }
 
+#ifdef M2DEC_DBK_NOINLINE
+__attribute__((noinline))
+#endif
 __device__ void deblock_pair(const int yA, const bool hasB, uint8_t *smem, const m2r_deblock_t *__restrict__ dbk, uint8_t *cur,
                              int W, int H, int Wmb, int Hmb, uint8_t *hbd, int *progress, int *err,
                              unsigned long long *rowflag, int seq, const int *segdone,
@@ -2417,6 +2457,19 @@ extern "C" int m2dec_amd_debug_dstamps(unsigned long long *out, size_t n)
 	if (n < 160 * 3 * 128) return -1;
 	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dstamps), sizeof(unsigned long long) * 160 * 3 * 128, 0, hipMemcpyDeviceToHost));
 	return 160 * 3 * 128;
+#else
+	(void)out;
+	(void)n;
+	return -1;
+#endif
+}
+
+extern "C" int m2dec_amd_debug_intra(int *out, size_t n)
+{
+#ifdef M2DEC_DBG_INTRA
+	if (n < 2048) return -1;
+	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(int) * 2048, 0, hipMemcpyDeviceToHost));
+	return 2048;
 #else
 	(void)out;
 	(void)n;

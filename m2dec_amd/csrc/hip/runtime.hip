@@ -2180,6 +2180,27 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	return 0;
 }
 
+/* The raw NV12 pictures (W x H luma, then W x H / 2 interleaved chroma, uncropped) in decode order from ONE
+ * batch launch of the whole trace, exactly as m2dec_amd_hip_replay_md5 runs it: a diagnostic for locating the
+ * first wrong macroblock of a picture (tools/replay_diff.py).  out holds npics * W * H * 3 / 2 bytes. */
+extern "C" int m2dec_amd_hip_replay_capture(m2dec_amd_hip_replay_t *r, uint8_t *out, size_t n)
+{
+	if (!r || !out) return -1;
+	Sched &sc = r->sc;
+	const size_t fb = (size_t)sc.W * sc.H * 3 / 2;
+	if (n < fb * (size_t)r->npics) return -1;
+	CHECK(hipSetDevice(sc.dev));
+	if (sc.sync_all() < 0) return -1;
+	uint8_t *cap = nullptr;
+	CHECK(hipMalloc(&cap, sc.fsz * (size_t)r->npics));
+	int rc = 0;
+	if (replay_batches(r, 0, r->npics, false, cap) < 0 || m2dec_amd_hip_replay_sync(r) < 0) rc = -1;
+	for (int i = 0; rc == 0 && i < r->npics; ++i)
+		if (hipMemcpy(out + fb * (size_t)i, cap + (size_t)i * sc.fsz, fb, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
+	(void)hipFree(cap);
+	return rc;
+}
+
 extern "C" int m2dec_amd_hip_replay_stream(const m2dec_amd_hip_replay_t *r, int i)
 {
 	if (!r || i < 0 || i >= r->npics) return -1;

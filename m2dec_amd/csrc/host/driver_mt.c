@@ -56,6 +56,13 @@ static void thread_cpu_report(const char *name)
 #define MD5_TAIL_PARSE_BUSY_STREAMS 4
 #define MD5_BIG_FRAME ((size_t)6 << 20) /* frames above this (4K) are not batched short of min_batch */
 
+/* one stream's MD5 threads: MD5_THREADS, at most the process's CPU share (cpushare.c) */
+static int md5_threads_default(void)
+{
+	const int s = m2d_cpu_share();
+	return s < MD5_THREADS ? s : MD5_THREADS;
+}
+
 /* The MD5 threads hash the decoder's frame buffers in place: on_frame holds the frame (the decoder
  * does not reuse it until it is released, h264_dec.h m2dec_hold_t) and queues it; no copy on the
  * caller's thread.  One pipe may serve several streams (m2dec_amd_decode_streams_md5): their frames
@@ -157,10 +164,12 @@ static void *md5_worker(void *arg)
 		pthread_mutex_unlock(&p->mu);
 		if (p->delay_us) usleep((useconds_t)p->delay_us); /* (tests: MD5 slower than the decoder) */
 		char lines[MD5_BATCH][35];
+		m2d_cpu_enter(); /* (cpushare.c: within the busy-thread slots the parse leaves free) */
 		const double th = now_s();
 		m2d_tl('H', n, n ? ix[0] : -1);
 		m2dec_amd_frames_md5(f, n, lines);
 		m2d_tl('h', n, n ? ix[0] : -1);
+		m2d_cpu_leave();
 		const double th1 = now_s();
 		const double t = now_s();
 		pthread_mutex_lock(&p->mu);
@@ -297,7 +306,7 @@ int m2dec_amd_decode_stream_md5(const uint8_t *data, size_t len, int device, int
                                 m2dec_amd_stats_t *stats)
 {
 	const char *e = getenv("M2DEC_AMD_MD5_THREADS");
-	return decode_md5(data, len, NULL, device, dpb, -1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS, md5s, max, stats);
+	return decode_md5(data, len, NULL, device, dpb, -1, e && atoi(e) > 0 ? atoi(e) : md5_threads_default(), md5s, max, stats);
 }
 
 int m2dec_amd_decode_stream_md5_backend(const uint8_t *data, size_t len, const m2r_backend_t *backend, int parse_threads,
@@ -358,7 +367,7 @@ static int copy_md5(int codec, const uint8_t *data, size_t len, const h265r_back
 	h265_md5_t h;
 	int err = 0, r;
 	const char *e = getenv("M2DEC_AMD_MD5_THREADS");
-	if (pipe_open(&p, 1, e && atoi(e) > 0 ? atoi(e) : MD5_THREADS) < 0) return -1;
+	if (pipe_open(&p, 1, e && atoi(e) > 0 ? atoi(e) : md5_threads_default()) < 0) return -1;
 	memset(&s, 0, sizeof(s));
 	s.pipe = &p;
 	s.md5s = md5s;
@@ -415,7 +424,8 @@ static void *stream_worker(void *arg)
 	stream_job_t *j = (stream_job_t *)arg;
 	/* parse-ahead workers a stream may occupy in the shared pool (M2DEC_AMD_STREAM_PARSE_THREADS) */
 	const char *e = getenv("M2DEC_AMD_STREAM_PARSE_THREADS");
-	const int pt = e && atoi(e) > 0 ? atoi(e) : 8; /* profiles/r59_sweep_e2e.txt: 8 streams, 3 -> ~1440, 8 -> ~1490 fps */
+	/* profiles/r59_sweep_e2e.txt: 8 streams, 3 -> ~1440, 8 -> ~1490 fps; at most the CPU share (cpushare.c) */
+	const int pt = e && atoi(e) > 0 ? atoi(e) : (m2d_cpu_share() < 8 ? m2d_cpu_share() : 8);
 	j->result = stream_md5(j->pipe, j->data, j->len, NULL, j->device, -1, pt, j->md5s, j->max, NULL);
 	thread_cpu_report("m2d-stream");
 	return NULL;
@@ -432,7 +442,8 @@ int m2dec_amd_decode_streams_md5(int n, const uint8_t *const *datas, const size_
 	if (n <= 0) return -1;
 	{
 		const char *m = getenv("M2DEC_AMD_STREAM_MD5_THREADS"); /* MD5 threads of the shared pipe */
-		const int mt = m && atoi(m) > 0 ? atoi(m) : (n + 1) / 2 + 1;
+		int mt = m && atoi(m) > 0 ? atoi(m) : (n + 1) / 2 + 1;
+		if (!(m && atoi(m) > 0) && mt > m2d_cpu_share()) mt = m2d_cpu_share();
 		if (pipe_open(&pipe, n, mt) < 0) return -1;
 	}
 	jobs = (stream_job_t *)calloc((size_t)n, sizeof(*jobs));

@@ -248,7 +248,7 @@ static int ensure_backend(h264_dec_t *d)
 		d->have_backend = 1;
 		if (d->parse_threads < 0) { /* default for the product path: parse ahead on the pool */
 			const char *e = getenv("M2DEC_AMD_PARSE_THREADS");
-			d->parse_threads = e ? atoi(e) : 16; /* profiles/r48*_threads.txt: 14-20 within noise of each other, 12 ~8 % lower */
+			d->parse_threads = e ? atoi(e) : m2d_cpu_share(); /* the CPU share (cpushare.c); profiles/r48*_threads.txt: 14-20 within noise, 12 ~8 % lower */
 		}
 	}
 	if (d->parse_threads > 0 && !d->as && h264_async_start(d, d->parse_threads) < 0) return -1;

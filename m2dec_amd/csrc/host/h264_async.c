@@ -584,10 +584,13 @@ static int job_run_par(struct h264_async *as, h264_job_t *j)
 	}
 	{
 		const double tw = now_s();
+		const int waits = j->sl_done < nsl;
+		if (waits) m2d_cpu_primary(-1); /* (not busy while the helpers finish: cpushare.c) */
 		while (j->sl_done < nsl) pthread_cond_wait(&as->cv_done, as->mu);
 		as->t_parse -= now_s() - tw; /* the worker's job time counts parse work only */
+		pthread_mutex_unlock(as->mu);
+		if (waits) m2d_cpu_primary(1);
 	}
-	pthread_mutex_unlock(as->mu);
 
 	/* every slice parsed exactly its MB range, in order, the last one ending the picture */
 	for (int k = 0; k < nsl; ++k) {
@@ -755,9 +758,11 @@ static void *pool_worker(void *arg)
 		as->running++;
 		__atomic_fetch_add(&g_parse_running, 1, __ATOMIC_RELAXED);
 		pthread_mutex_unlock(&g_parse.mu);
+		m2d_cpu_primary(1); /* (cpushare.c: MD5 batches use the slots the parse leaves free) */
 		if (pj) {
 			const double ts = now_s();
 			slice_run(pj, k);
+			m2d_cpu_primary(-1);
 			const double te = now_s();
 			pthread_mutex_lock(&g_parse.mu);
 			as->t_parse += te - ts;
@@ -787,6 +792,7 @@ static void *pool_worker(void *arg)
 				__atomic_fetch_add(&g_job_cpu_ns, (long long)(jc1.tv_sec - jc0.tv_sec) * 1000000000LL + (jc1.tv_nsec - jc0.tv_nsec),
 				                   __ATOMIC_RELAXED);
 			}
+			m2d_cpu_primary(-1);
 			pthread_mutex_lock(&g_parse.mu);
 			const double te = now_s();
 			m2d_tl('p', j->seq, j->snap[0]->sh.slice_type);
@@ -931,10 +937,11 @@ int h264_async_start(h264_dec_t *d, int threads)
 	as->ahead_all = getenv("M2DEC_AMD_AHEAD_ALL") && atoi(getenv("M2DEC_AMD_AHEAD_ALL"));
 	pthread_mutex_lock(&g_parse.mu);
 	{
-		/* the pool is sized for the host share, not per pipeline: M2DEC_AMD_POOL_THREADS, default 16 (the
-		 * GPU box's CPU share per job; profiles/r48*_threads.txt), at least what a pipeline asks for */
+		/* the pool is sized for the host share, not per pipeline: M2DEC_AMD_POOL_THREADS, default the process's
+		 * CPU share (cpushare.c: affinity ∩ cgroup quota ÷ the node's GPU ranks; 16 on the GPU box,
+		 * profiles/r48*_threads.txt), at least what a pipeline asks for */
 		const char *e = getenv("M2DEC_AMD_POOL_THREADS");
-		const int want = e && atoi(e) > 0 ? atoi(e) : 16;
+		const int want = e && atoi(e) > 0 ? atoi(e) : m2d_cpu_slots() > 0 ? m2d_cpu_slots() : m2d_cpu_share();
 		pool_grow(want > threads ? want : threads);
 	}
 	as->nth = g_parse.nth < threads ? g_parse.nth : threads;

@@ -452,6 +452,15 @@ void h264_async_pool_release(void);
  * hipDeviceGetPCIBusId); each library thread calls m2d_place_self before its work */
 void m2d_place_device(const char *bus_id);
 void m2d_place_self(void);
+/* cpushare.c: this process's host CPU share (affinity ∩ cgroup quota ÷ the node's GPU ranks), and the gate that
+ * keeps parse work (m2d_cpu_primary, counted) and MD5 batches (m2d_cpu_enter / leave, waiting) within
+ * m2d_cpu_slots() busy threads */
+int m2d_cpu_share(void);
+int m2d_cpu_slots(void);
+void m2d_cpu_primary(int delta);
+void m2d_cpu_enter(void);
+void m2d_cpu_leave(void);
+int m2d_cpu_share_probe(const char *root, int ranks, int aff_cpus, long *quota_milli, int *aff_out);
 long long h264_async_pinned_bytes(long long *pooled);
 
 /* bitio.c */

@@ -2170,7 +2170,7 @@ static int pipe_threads(const h265_dec_t *d)
 {
 	if (d->threads >= 0) return d->threads > 16 ? 16 : d->threads;
 	const char *e = getenv("M2DEC_AMD_H265_THREADS");
-	const int n = e && *e ? atoi(e) : 8;
+	const int n = e && *e ? atoi(e) : (m2d_cpu_share() < 8 ? m2d_cpu_share() : 8); /* (cpushare.c) */
 	return n < 0 ? 0 : (n > 16 ? 16 : n);
 }
 

@@ -74,7 +74,8 @@ static void *crew_main(void *arg)
 static void crews_start(void)
 {
 	const char *e = getenv("M2DEC_AMD_COPY_CREW");
-	const int n = e ? atoi(e) : PAR_CREW;
+	/* (a share below 8 CPUs: one helper, below 4: none; cpushare.c) */
+	const int n = e ? atoi(e) : (m2d_cpu_share() >= 8 ? PAR_CREW : (m2d_cpu_share() >= 4 ? 1 : 0));
 	for (int w = 0; w < M2DEC_CREWS; ++w) {
 		par_crew_t *c = &g_crews[w];
 		pthread_mutex_init(&c->mu, NULL);

@@ -186,3 +186,90 @@ def all_ranks(dist, world: int, ok: bool, device: str) -> bool:
     t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
+
+
+# ---- host CPUs per rank.  Each rank's decode is host-bound (~8 CPU-ms per 1080p frame:
+# CABAC parse 5, MD5 2, the rest ~1), so at N GPUs per node the ranks must not share cores: each rank gets a
+# disjoint slice of its GPU's NUMA node's CPUs (∩ the job's affinity), the slices of one node equal in size.  The
+# library then sizes its parse pool and MD5 helpers from that slice ∩ the cgroup quota ÷ the node's ranks
+# (cpushare.c), and numa.c keeps its threads on it.  Unmeasured on an 8-GPU node (no scaling run was available).
+
+def parse_cpulist(s: str) -> List[int]:
+    out: List[int] = []
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def node_cpus(sysfs_root: str = "") -> dict:
+    """{NUMA node: its CPUs} from <root>/sys/devices/system/node/node<n>/cpulist."""
+    import os
+    base = os.path.join(sysfs_root or "/", "sys", "devices", "system", "node")
+    out = {}
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for n in names:
+        if n.startswith("node") and n[4:].isdigit():
+            try:
+                out[int(n[4:])] = parse_cpulist(open(os.path.join(base, n, "cpulist")).read())
+            except (OSError, ValueError):
+                pass
+    return out
+
+
+def gpu_numa_node(bus_id: str, sysfs_root: str = "") -> int:
+    """The NUMA node of a PCI device (<root>/sys/bus/pci/devices/<bus id>/numa_node), -1 if unknown."""
+    import os
+    try:
+        return int(open(os.path.join(sysfs_root or "/", "sys", "bus", "pci", "devices", bus_id.lower(),
+                                     "numa_node")).read())
+    except (OSError, ValueError):
+        return -1
+
+
+def cpu_plan(nodes: Sequence[int], cpus_of_node: dict, allowed) -> List[List[int]]:
+    """Disjoint CPU slices per rank: rank r's GPU sits on NUMA node nodes[r]; the ranks of one node split that
+    node's allowed CPUs into equal contiguous slices (rank order).  When some rank's node is unknown or holds
+    none of the allowed CPUs, all allowed CPUs are split among all ranks instead.  A rank gets at least one CPU
+    (slices then overlap only when there are fewer CPUs than ranks)."""
+    allowed = sorted(set(allowed))
+    world = len(nodes)
+
+    def split(pool: List[int], ranks: List[int], out: List[List[int]]):
+        k = len(ranks)
+        for i, r in enumerate(ranks):
+            lo, hi = len(pool) * i // k, len(pool) * (i + 1) // k
+            out[r] = pool[lo:hi] if len(pool) >= k else [pool[i % len(pool)]]
+
+    out: List[List[int]] = [[] for _ in range(world)]
+    pools = {n: sorted(set(cpus_of_node.get(n, [])) & set(allowed)) for n in set(nodes)}
+    if any(n < 0 or not pools[n] for n in nodes):
+        split(allowed, list(range(world)), out)
+        return out
+    for n in sorted(set(nodes)):
+        split(pools[n], [r for r in range(world) if nodes[r] == n], out)
+    return out
+
+
+def place_rank(dist, world: int, rank: int, bus_id: Optional[str], device: str, sysfs_root: str = "") -> Optional[List[int]]:
+    """All-gather every rank's GPU NUMA node, take this rank's slice of cpu_plan and bind the calling thread to
+    it (the library's threads, created later by it, inherit the mask).  Returns the slice (None at world 1)."""
+    import os
+    if dist is None or world == 1:
+        return None
+    import torch
+
+    node = gpu_numa_node(bus_id, sysfs_root) if bus_id else -1
+    t = torch.tensor([node], dtype=torch.int64, device=device)
+    outs = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    nodes = [int(o.item()) for o in outs]
+    mine = cpu_plan(nodes, node_cpus(sysfs_root), os.sched_getaffinity(0))[rank]
+    if mine:
+        os.sched_setaffinity(0, mine)
+    return mine

@@ -1,0 +1,63 @@
+#!/bin/bash
+# One GPU call = a list of steps, each under its own time limit, stopping at the first failure (gpurun rules:
+# no GPU step after a fault, an abort or a time limit).  Replaces the one-shot tools/gpu_round5*.sh scripts.
+#
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+#
+# steps (outputs under gpurun_out/, named with TAG):
+#   tests            pytest -m gpu (thread timeouts, one process)       -> pytest_TAG.log
+#   smoke            __graft_entry__.smoke()
+#   bench[=ARGS]     python bench.py ARGS (default: the driver's line)   -> bench_TAG.json / .err
+#   bench20          the driver's own command line (--steps 20 --warmup 5)
+#   ab=R,N,CFG;CFG   tools/ab_env.py R N CFG CFG ... (c3 decode medians) -> ab_TAG.txt
+#   diff=V,STREAM    tools/replay_diff.py STREAM with build/var/lib_V.so ("base": the product library)
+#   prof             rocprofv3 --kernel-trace --stats of the default bench (decode path, replay, all legs)
+#   pmc=KERNEL       tools/gpu_pmc.sh TAG KERNEL (FETCH_SIZE / WRITE_SIZE / SQ passes)
+set -o pipefail
+TAG=${1:?tag}
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && mkdir -p gpurun_out
+O=gpurun_out
+for step in "$@"; do
+  name=${step%%=*}
+  arg=""
+  [ "$name" != "$step" ] && arg=${step#*=}
+  echo "== $name $arg ($(date +%T))"
+  case $name in
+    tests)
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > $O/pytest_$TAG.log 2>&1
+      rc=$?; tail -3 $O/pytest_$TAG.log ;;
+    smoke)
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()"; rc=$? ;;
+    bench)
+      timeout -k 10 900 python bench.py $arg > $O/bench_$TAG.json 2> $O/bench_$TAG.err
+      rc=$?; tail -c 600 $O/bench_$TAG.json; echo ;;
+    bench20)
+      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20_$TAG.json 2> $O/bench20_$TAG.err
+      rc=$?; python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('value', d['value'], 'cpu_quota', d.get('cpu_quota'), 'host_cpu', d.get('host_cpu'), 'decode_ms', d.get('decode_ms'))" $O/bench20_$TAG.json ;;
+    ab)
+      IFS=',' read -r rounds n cfgs <<< "$arg"
+      IFS=';' read -ra cl <<< "$cfgs"
+      timeout -k 10 900 python -u tools/ab_env.py $rounds $n "${cl[@]}" > $O/ab_$TAG.txt 2>&1
+      rc=$?; tail -4 $O/ab_$TAG.txt ;;
+    diff)
+      IFS=',' read -r v s <<< "$arg"
+      lib=$R/m2dec_amd/lib/libm2dec_amd.so; [ "$v" != base ] && lib=$R/build/var/lib_$v.so
+      M2DEC_AMD_LIB=$lib timeout -k 10 200 python -u tools/replay_diff.py $s > $O/diff_${TAG}_$v.txt 2>&1
+      rc=$?; grep "pictures differ\|best oracle" $O/diff_${TAG}_$v.txt; tail -2 $O/diff_${TAG}_$v.txt ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$TAG -o run --output-format csv -- \
+         python3 $R/bench.py --no-cpu-baseline > $R/$O/prof_$TAG.log 2>&1)
+      rc=$?; find $O/prof_$TAG -name "*kernel_stats*" ;;
+    pmc)
+      timeout -k 10 900 bash tools/gpu_pmc.sh $TAG $arg; rc=$? ;;
+    *)
+      echo "unknown step $name"; rc=2 ;;
+  esac
+  echo "== $name rc=$rc ($(date +%T))"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0

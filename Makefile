@@ -14,7 +14,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -g -fPIC -std=c++17 $(INC) -Wno-unused-re
 HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)
 HOST_OBJ := $(patsubst m2dec_amd/csrc/host/%.c,build/host/%.o,$(HOST_SRC))
 HIP_SRC := m2dec_amd/csrc/hip/recon_hip.hip
-HIP_HDR := m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h m2dec_amd/csrc/host/h265_dec.h
+HIP_HDR := m2dec_amd/csrc/hip/selftest_data.h m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h m2dec_amd/csrc/host/h265_dec.h
 HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 
 LIB := m2dec_amd/lib/libm2dec_amd.so

@@ -346,6 +346,11 @@ int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s);
  * order) into out (n bytes, at least npics times that); tools/replay_diff.py locates wrong macroblocks. */
 int m2dec_amd_hip_replay_capture(m2dec_amd_hip_replay_t *r, unsigned char *out, size_t n);
 void m2dec_amd_hip_replay_destroy(m2dec_amd_hip_replay_t *r);
+/* The HIP back end's built-in known-answer test (runtime.hip; data: tools/make_selftest.py): two small coverage
+ * streams reconstructed through k_batch and k_picture against their oracle MD5s.  0 = every picture exact,
+ * 1 = a picture differs (the kernels of this build are wrong: the back end refuses to start), -1 = no device.
+ * m2dec_amd_hip_backend_create runs it once per process and device (M2DEC_AMD_SELFTEST=0 skips it). */
+int m2dec_amd_hip_selftest(int device);
 
 #ifdef __cplusplus
 }

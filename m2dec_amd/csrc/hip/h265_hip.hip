@@ -1383,7 +1383,10 @@ struct H265Gpu {
 	hipEvent_t ev[H265R_MAX_FRAMES] = {};   /* the frame's copy to staging is complete */
 	bool pend[H265R_MAX_FRAMES] = {};
 	hipEvent_t kdone[H265R_MAX_FRAMES] = {}; /* the kernels of the frame's last picture are done (null: none) */
-	std::vector<hipEvent_t> readers[H265R_MAX_FRAMES]; /* kernels of the pictures that read the frame's content */
+	/* kernels of the pictures that read the frame's content: the latest one per HIP stream (events of one stream
+	 * complete in order, so an older reader on the same stream is covered; ADVICE r5: a frame that stays a
+	 * reference no longer collects one event per reading picture, which the 512-event ring re-records) */
+	std::vector<std::pair<int, hipEvent_t>> readers[H265R_MAX_FRAMES];
 	hipEvent_t evr[NEV] = {};
 	int ev_next = 0;
 	int *err = nullptr;     /* sticky error word */
@@ -1662,7 +1665,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	 * picture can hold this thread until that picture completes: 8-10 ms per decode in the round-5 trace) */
 	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
 		if (((refs >> r) & 1) && g->kdone[r]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[r], 0));
-	for (hipEvent_t e : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, e, 0));
+	for (const auto &re : g->readers[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, re.second, 0));
 	if (g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->kdone[pic->slot], 0));
 	if (g->pend[pic->slot] || g->kdone[pic->slot]) H265_CHECK(hipStreamWaitEvent(s, g->ev[pic->slot], 0)); /* its copy-out */
 	lap("event waits");
@@ -1713,7 +1716,12 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	if (!kd) return -1;
 	H265_CHECK(hipEventRecord(kd, s));
 	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
-		if ((refs >> r) & 1) g->readers[r].push_back(kd);
+		if ((refs >> r) & 1) {
+			auto &rd = g->readers[r];
+			auto it = std::find_if(rd.begin(), rd.end(), [k](const std::pair<int, hipEvent_t> &x) { return x.first == k; });
+			if (it != rd.end()) it->second = kd;
+			else rd.emplace_back(k, kd);
+		}
 	g->readers[pic->slot].clear();
 	g->kdone[pic->slot] = kd;
 	/* the picture to its staging buffer, behind the kernels */

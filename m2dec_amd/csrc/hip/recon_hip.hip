@@ -91,6 +91,11 @@ __device__ unsigned long long g_dstamps[160][3][128];
 /* intra sub-phase stamps: the first 16 MBs of a row, 6 events each (role 3, idx 160..255) */
 #define STAMPX(x, k) do { if ((x) < 16 && part == 0) STAMP(y, 3, 160 + (x) * 6 + (k), k); } while (0)
 
+#ifdef M2DEC_DBG_ROWS
+/* diagnostic (-DM2DEC_DBG_ROWS, never in the product build): per row workgroup and wave, the row intra_row
+ * reconstructs and where its first MB's samples go (tools/replay_diff.py) */
+__device__ unsigned int g_dbg_rows[256 * 4 * 2];
+#endif
 #ifdef M2DEC_DBG_INTRA
 /* diagnostic (-DM2DEC_DBG_INTRA, never in the product build): the first I picture's MB (0, 0) luma context
  * before and after its reconstruction, read back with m2dec_amd_debug_intra (tools/replay_diff.py) */
@@ -1323,6 +1328,13 @@ __device__ M2DEC_INTRA_ROW_ATTR void intra_row(const int y, const int t, const i
 		WSYNC();
 #endif
 		STAMPX(x, 3);
+#ifdef M2DEC_DBG_ROWS
+		if (x == 0 && t == 0) {
+			const unsigned b = blockIdx.x & 255, wv = (unsigned)__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
+			g_dbg_rows[(b * 4 + wv) * 2] = (unsigned)y | ((unsigned)part << 8) | ((unsigned)wave << 12) | (0xabu << 24);
+			g_dbg_rows[(b * 4 + wv) * 2 + 1] = (unsigned)(y0 & 0xffff) | ((unsigned)m.kind << 16) | ((m.coef & 0xff) << 24);
+		}
+#endif
 		/* ---- write back and hand off the bottom rows */
 		if (do_luma)
 			for (int k = t; k < 256; k += 64) cur[(size_t)(y0 + (k >> 4)) * W + x0 + (k & 15)] = L[1 + (k >> 4)][1 + (k & 15)];
@@ -2457,6 +2469,19 @@ extern "C" int m2dec_amd_debug_dstamps(unsigned long long *out, size_t n)
 	if (n < 160 * 3 * 128) return -1;
 	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dstamps), sizeof(unsigned long long) * 160 * 3 * 128, 0, hipMemcpyDeviceToHost));
 	return 160 * 3 * 128;
+#else
+	(void)out;
+	(void)n;
+	return -1;
+#endif
+}
+
+extern "C" int m2dec_amd_debug_rows(unsigned *out, size_t n)
+{
+#ifdef M2DEC_DBG_ROWS
+	if (n < 256 * 4 * 2) return -1;
+	CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg_rows), sizeof(unsigned) * 256 * 4 * 2, 0, hipMemcpyDeviceToHost));
+	return 256 * 4 * 2;
 #else
 	(void)out;
 	(void)n;

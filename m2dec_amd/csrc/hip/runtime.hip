@@ -99,6 +99,7 @@ struct SlotBudget {
 	bool ready = false;
 	int cap_units = 0;  /* the device's budget: M2D_SHARE_UNITS_PER_CU x CUs (devshare.h) */
 	int used_local = 0; /* process-local account, when no shared segment could be opened */
+	bool refused = false; /* the device's segment exists but is invalid: this process does not launch (devshare.c) */
 	m2d_share_t *share = nullptr; /* the device's cross-process budget (devshare.c), normally */
 	int max_procs = 0, max_total = 0; /* diagnostics: the most processes / units seen holding the budget */
 	std::deque<std::pair<hipEvent_t, int>> pend; /* completion event of a launch, its units */
@@ -124,8 +125,10 @@ struct SlotBudget {
 		if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev) != hipSuccess) bus[0] = 0;
 		if (bus[0]) m2d_place_device(bus); /* (numa.c: the library's threads near this GPU) */
 		if (!e || atoi(e)) {
-			if (bus[0]) share = m2d_share_open(bus, cap_units);
+			int why = M2D_SHARE_UNAVAILABLE;
+			if (bus[0]) share = m2d_share_open(bus, cap_units, &why);
 			if (share) cap_units = std::min(cap_units, m2d_share_cap(share));
+			else if (why == M2D_SHARE_REFUSED) refused = true; /* (reported by devshare.c: no decode on a private budget) */
 			else fprintf(stderr, "m2dec_amd: no shared workgroup budget for device %d (%s): process-local budget\n", dev, bus);
 		}
 	}
@@ -135,20 +138,27 @@ struct SlotBudget {
 		setup_locked(dev);
 	}
 
-	bool take(int units)
+	/* 1 taken, 0 not now, -1 never (a refused or corrupted segment) */
+	int take(int units)
 	{
+		if (refused) return -1;
 		if (share) {
 			int total = 0, procs = 0;
-			const bool ok = m2d_share_try(share, units, &total, &procs) != 0;
+			const int r = m2d_share_try(share, units, &total, &procs);
+			if (r < 0) {
+				refused = true;
+				return -1;
+			}
+			const bool ok = r != 0;
 			max_procs = std::max(max_procs, procs);
 			if (ok) max_total = std::max(max_total, total);
-			return ok;
+			return ok ? 1 : 0;
 		}
-		if (used_local + units > cap_units) return false;
+		if (used_local + units > cap_units) return 0;
 		used_local += units;
 		max_procs = 1;
 		max_total = std::max(max_total, used_local);
-		return true;
+		return 1;
 	}
 	void give(int units)
 	{
@@ -179,7 +189,9 @@ struct SlotBudget {
 		double t_wait = 0;
 		for (;;) {
 			retire();
-			if (take(want)) break;
+			const int tk = take(want);
+			if (tk < 0) return -1;
+			if (tk) break;
 			if (const char *lp = getenv("M2DEC_AMD_BUDGET_LOG")) { /* diagnostics: a reservation waiting long */
 				const double now = wall_s();
 				if (t_wait == 0) t_wait = now;
@@ -560,6 +572,7 @@ struct Sched {
 			CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
 			per_cu = std::max(1, per_cu);
 			g_budget[dev & 15].setup(dev);
+			if (g_budget[dev & 15].refused) return -1; /* (devshare.c printed why) */
 			resident_per_cu = per_cu;
 			wg_units = (M2D_SHARE_UNITS_PER_CU + per_cu - 1) / per_cu;
 			cap_wg = std::max(1, std::min(per_cu * std::max(1, cus), g_budget[dev & 15].cap_units / wg_units));
@@ -725,6 +738,7 @@ struct Sched {
 			hipEvent_t done = bg.event();
 			if (!done) return -1;
 			const int held = bg.reserve(nb * std::max(1, wg_units));
+			if (held < 0) return -1; /* (a refused / corrupted shared budget: reported by devshare.c) */
 			if (tstart) CHECK(hipEventRecord(*tstart, s)); /* (decode path: TimingSlot e[3], the kernel's start) */
 			hipLaunchKernelGGL(k_picture, dim3(nb), dim3(256), m2r_deblock_lds_bytes(W, Wmb), s,
 			                   (const PictureArgs *)(pargs + (size_t)k * BMAX), n);
@@ -1710,9 +1724,12 @@ extern "C" int m2dec_amd_hip_available(void)
 	return n > 0;
 }
 
+static int selftest_once(int device);
+
 extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 {
 	if (!out || !m2dec_amd_hip_available()) return -1;
+	if (selftest_once(device) < 0) return -1; /* (the built-in known-answer test, once per process and device) */
 	const double t0 = wall_s();
 	HipBackend *b = new HipBackend();
 	memset(b->stg, 0, sizeof(b->stg));
@@ -2138,10 +2155,10 @@ extern "C" int m2dec_amd_hip_replay_timing(m2dec_amd_hip_replay_t *r, m2dec_amd_
 	return 0;
 }
 
-/* MD5 of every picture in decode order.  Default: ONE batch launch of the whole trace, exactly as
- * replay_run runs it, each picture copied out by its last row workgroup before its slot is reused;
- * M2DEC_AMD_DEBUG=1: one k_picture launch per picture, synchronised (the decode path's kernel). */
-extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
+/* MD5 of every picture in decode order.  per_picture false: ONE batch launch of the whole trace (k_batch),
+ * exactly as replay_run runs it, each picture copied out by its last row workgroup before its slot is reused;
+ * true: one k_picture launch per picture, synchronised (the decode path's kernel). */
+static int replay_md5_impl(m2dec_amd_hip_replay_t *r, char *md5s, bool dbg)
 {
 	if (!r || !md5s) return -1;
 	Sched &sc = r->sc;
@@ -2149,7 +2166,6 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	std::vector<uint8_t> host(ls * 3 / 2);
 	CHECK(hipSetDevice(sc.dev));
 	if (sc.sync_all() < 0) return -1; /* no earlier work of either launch path may still run */
-	const bool dbg = getenv("M2DEC_AMD_DEBUG") != nullptr;
 	uint8_t *cap = nullptr;
 	if (!dbg) {
 		CHECK(hipMalloc(&cap, sc.fsz * (size_t)r->npics));
@@ -2160,7 +2176,8 @@ extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
 	}
 	for (int i = 0; i < r->npics; ++i) {
 		if (dbg) {
-			fprintf(stderr, "replay_md5: picture %d slot %d n_inter %d n_intra %d\n", i, r->pics[i].slot, r->pics[i].n_inter, r->pics[i].n_intra);
+			if (getenv("M2DEC_AMD_DEBUG"))
+				fprintf(stderr, "replay_md5: picture %d slot %d n_inter %d n_intra %d\n", i, r->pics[i].slot, r->pics[i].n_inter, r->pics[i].n_intra);
 			if (replay_enqueue(r, i, false) < 0 || m2dec_amd_hip_replay_sync(r) < 0) return -1;
 			CHECK(hipMemcpy(host.data(), sc.frames + (size_t)r->pics[i].slot * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost));
 		} else if (hipMemcpy(host.data(), cap + (size_t)i * sc.fsz, ls * 3 / 2, hipMemcpyDeviceToHost) != hipSuccess) {
@@ -2199,6 +2216,72 @@ extern "C" int m2dec_amd_hip_replay_capture(m2dec_amd_hip_replay_t *r, uint8_t *
 		if (hipMemcpy(out + fb * (size_t)i, cap + (size_t)i * sc.fsz, fb, hipMemcpyDeviceToHost) != hipSuccess) rc = -1;
 	(void)hipFree(cap);
 	return rc;
+}
+
+/* Default: the batch path (k_batch); M2DEC_AMD_DEBUG=1: the decode path's kernel, one picture per launch */
+extern "C" int m2dec_amd_hip_replay_md5(m2dec_amd_hip_replay_t *r, char *md5s)
+{
+	return replay_md5_impl(r, md5s, getenv("M2DEC_AMD_DEBUG") != nullptr);
+}
+
+/* ---- the built-in known-answer test.  Round 5 found that intra_row inlined into row_pair
+ * reconstructed every I picture wrongly; round 6 showed the optimized LLVM IR of that build identical to one that
+ * reconstructs bit-exactly and differing only in the register budget it is compiled for (waves-per-eu 4 = 128
+ * VGPRs: wrong or faulting code; 3 = 168 VGPRs: exact; DESIGN.md §5 "Compiler hazards"): the AMDGPU back end
+ * miscompiled that code.  A product library whose kernels were compiled wrongly must not decode anything, so
+ * the first HIP back end of a process on a device reconstructs the known-answer streams of selftest_data.h
+ * (tools/make_selftest.py: h264gen coverage streams, I P B B with PCM, constrained intra, deblocking idc 2,
+ * explicit weights; MD5s from the CPU oracle) through both launch paths — k_batch and k_picture — and refuses
+ * to start if any picture differs.  M2DEC_AMD_SELFTEST=0 skips it. */
+#include "selftest_data.h"
+
+extern "C" int m2dec_amd_hip_selftest(int device)
+{
+	int bad = 0;
+	for (size_t k = 0; k < sizeof(k_selftest) / sizeof(k_selftest[0]) && !bad; ++k) {
+		const SelftestStream &st = k_selftest[k];
+		m2dec_amd_trace_t *t = nullptr;
+		if (m2dec_amd_trace_capture(st.data, st.len, &t) != st.npics) {
+			m2dec_amd_trace_free(t);
+			return -1;
+		}
+		m2dec_amd_hip_replay_t *r = nullptr;
+		if (m2dec_amd_hip_replay_create(t, device, &r) < 0) {
+			m2dec_amd_trace_free(t);
+			return -1;
+		}
+		std::vector<char> md5(35 * (size_t)st.npics + 1);
+		for (int path = 0; path < 2 && !bad; ++path) {
+			if (replay_md5_impl(r, md5.data(), path == 1) < 0) {
+				bad = -1;
+				break;
+			}
+			for (int i = 0; i < st.npics; ++i)
+				if (memcmp(md5.data() + 35 * (size_t)i, st.md5[i], 32) != 0) {
+					fprintf(stderr, "m2dec_amd: SELF-TEST FAILED on device %d: %s picture %d through %s reconstructs to %.32s, "
+					        "expected %s — the gfx950 kernels of this build are wrong (compiler?); refusing to decode\n",
+					        device, st.name, i, path ? "k_picture" : "k_batch", md5.data() + 35 * (size_t)i, st.md5[i]);
+					bad = 1;
+					break;
+				}
+		}
+		m2dec_amd_hip_replay_destroy(r);
+		m2dec_amd_trace_free(t);
+	}
+	return bad;
+}
+
+/* once per device and process: 0 passed (or skipped), otherwise the back end is not created */
+static int selftest_once(int device)
+{
+	static std::mutex mu;
+	static int state[16]; /* 0 not run, 1 passed, 2 failed */
+	if (device < 0 || device >= 16) return -1;
+	const char *e = getenv("M2DEC_AMD_SELFTEST");
+	if (e && atoi(e) == 0) return 0;
+	std::lock_guard<std::mutex> lk(mu);
+	if (!state[device]) state[device] = m2dec_amd_hip_selftest(device) == 0 ? 1 : 2;
+	return state[device] == 1 ? 0 : -1;
 }
 
 extern "C" int m2dec_amd_hip_replay_stream(const m2dec_amd_hip_replay_t *r, int i)

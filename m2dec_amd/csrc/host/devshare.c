@@ -10,13 +10,22 @@
  * the budget has to be the DEVICE's, not the process's: two processes with private budgets could together
  * fill the device with spinners whose producers never get a slot.
  *
- * So the budget lives in a small shared-memory segment named after the GPU's PCI bus id
- * (/dev/shm/m2dec_amd.budget.<bus id>).  Each process holds one lease {pid, start time, units, contexts};
- * the segment's total is the sum of the leases.  A robust process-shared mutex guards it (a holder that dies
- * inside the critical section leaves EOWNERDEAD: the next locker recomputes the total from the leases).  A
- * lease whose process is gone (kill(pid, 0) = ESRCH, or the pid now names a process started at another
- * time) is reclaimed when a reservation does not fit: its launches died with their process (the driver
- * tears down a dead process's queues), so its units are free again.
+ * So the budget lives in a small shared-memory segment named after the GPU's PCI bus id and the owner
+ * (/dev/shm/m2dec_amd.budget.<bus id>.u<uid>, mode 0600; M2DEC_AMD_SHARE_GROUP=1: .g<gid>, 0660, for several
+ * users of one group on one GPU).  Each process holds one lease {pid, start time, units, contexts}; the
+ * segment's total is the sum of the leases.  A robust process-shared mutex guards it (a holder that dies
+ * inside the critical section leaves EOWNERDEAD: the next locker recomputes the total from the leases).
+ * Liveness (round 6): each lease holder keeps an open-file-description write lock on one byte of
+ * the segment file per lease (F_OFD_SETLK at offset sizeof(seg_t) + lease index).  The kernel drops it when the
+ * holder dies, in any PID namespace, so a lease whose byte nobody locks is dead (a pid check would misread
+ * processes of another namespace sharing /dev/shm); a dead lease is reclaimed when a reservation does not fit:
+ * its launches died with their process (the driver tears down a dead process's queues).
+ *
+ * The segment is validated on open (magic, layout version, capacity = this device's, every lease within the
+ * capacity, total = the sum of the leases) and its total on every reservation.  A segment that fails (corrupted,
+ * another layout version, or every lease held by a live process) is refused LOUDLY: the back end does not
+ * start, rather than silently falling back to a private budget that brings back the cross-process starvation
+ * hazard.  M2DEC_AMD_SHARE=0 is the explicit opt-out (a process-local budget).
  *
  * Units: k_picture's workgroups cost ceil(M2D_SHARE_UNITS_PER_CU / resident-per-CU) units each and the
  * capacity is M2D_SHARE_UNITS_PER_CU x CUs, so contexts whose occupancy differs (LDS per picture width)
@@ -40,7 +49,7 @@
 #include "devshare.h"
 
 #define SHARE_MAGIC 0x6d326462u /* "m2db" */
-#define SHARE_VERSION 2
+#define SHARE_VERSION 3
 #define SHARE_LEASES 256
 
 typedef struct {
@@ -48,7 +57,7 @@ typedef struct {
 	int32_t units;    /* workgroup units this process holds now */
 	int32_t contexts; /* live decode-path back ends of this process on the device */
 	int32_t wait_ms;  /* CLOCK_MONOTONIC ms (| 1) of this process's last reservation that did not fit; 0: none */
-	uint64_t start;   /* /proc/<pid>/stat start time: a recycled pid is another process */
+	uint64_t start;   /* /proc/<pid>/stat start time (diagnostics) */
 } lease_t;
 
 typedef struct {
@@ -62,11 +71,14 @@ typedef struct {
 
 struct m2d_share {
 	seg_t *seg;
+	int fd;            /* the segment file, kept open for the lease byte locks */
 	int idx;           /* this process's lease */
 	int32_t pid;
 	uint64_t start;
-	char path[160];
+	int32_t cap;       /* the capacity this process opened with */
+	char path[200];
 	int exited;             /* process exit dropped the lease; the mapping stays for threads still running */
+	int32_t local_used;     /* after exit: reservations are accounted here, within cap */
 	struct m2d_share *next; /* open handles of this process (closed at exit) */
 };
 
@@ -99,12 +111,48 @@ static uint64_t proc_start(int pid)
 	return strtoull(s, NULL, 10);
 }
 
-static int lease_dead(const lease_t *l)
+static off_t lease_byte(int i) { return (off_t)sizeof(seg_t) + i; }
+
+/* the holder of lease i is alive iff some open file description holds the write lock on its byte */
+static int lease_dead(int fd, const lease_t *l, int i)
 {
 	if (l->pid <= 0) return 1;
-	if (kill(l->pid, 0) < 0 && errno == ESRCH) return 1;
-	const uint64_t st = proc_start(l->pid);
-	return st && l->start && st != l->start;
+	struct flock fl;
+	memset(&fl, 0, sizeof fl);
+	fl.l_type = F_WRLCK;
+	fl.l_whence = SEEK_SET;
+	fl.l_start = lease_byte(i);
+	fl.l_len = 1;
+	if (fcntl(fd, F_OFD_GETLK, &fl) < 0) return kill(l->pid, 0) < 0 && errno == ESRCH; /* (no OFD locks: pid) */
+	return fl.l_type == F_UNLCK;
+}
+
+static int lease_lock(int fd, int i, int type)
+{
+	struct flock fl;
+	memset(&fl, 0, sizeof fl);
+	fl.l_type = (short)type;
+	fl.l_whence = SEEK_SET;
+	fl.l_start = lease_byte(i);
+	fl.l_len = 1;
+	return fcntl(fd, F_OFD_SETLK, &fl);
+}
+
+/* the layout is this version's and every field is within its range: 0 ok, else why not */
+static const char *seg_check(const seg_t *g, int cap)
+{
+	if (__atomic_load_n(&g->magic, __ATOMIC_ACQUIRE) != SHARE_MAGIC) return "bad magic";
+	if (g->version != SHARE_VERSION) return "another layout version (another m2dec_amd build decodes on this GPU)";
+	if (g->cap != cap) return "capacity differs from this device's";
+	int64_t sum = 0;
+	for (int i = 0; i < SHARE_LEASES; ++i) {
+		const lease_t *l = &g->lease[i];
+		if (l->pid < 0 || l->units < 0 || l->units > g->cap || l->contexts < 0 || (!l->pid && (l->units || l->contexts)))
+			return "a lease out of range";
+		sum += l->units;
+	}
+	if (g->total != sum || g->total < 0 || g->total > g->cap) return "total is not the sum of the leases";
+	return NULL;
 }
 
 static void recount(seg_t *g)
@@ -126,13 +174,13 @@ static int lock(seg_t *g)
 }
 
 /* reclaim the leases of processes that are gone; returns the units freed */
-static int sweep(seg_t *g, int self)
+static int sweep(int fd, seg_t *g, int self)
 {
 	int freed = 0;
 	for (int i = 0; i < SHARE_LEASES; ++i) {
 		lease_t *l = &g->lease[i];
 		if (i == self || l->pid == 0) continue;
-		if (lease_dead(l)) {
+		if (lease_dead(fd, l, i)) {
 			freed += l->units;
 			memset(l, 0, sizeof *l);
 		}
@@ -165,36 +213,44 @@ static seg_t *map_fd(int fd)
 }
 
 /* Publish an initialised segment atomically: build it under a private name, then link() it to the final name
- * (fails if another process published first: then use theirs). */
-static seg_t *open_seg(const char *path, int cap)
+ * (fails if another process published first: then use theirs).  *fd_out: the open file (kept for the lease
+ * locks).  *why: M2D_SHARE_UNAVAILABLE (no shared memory here) or M2D_SHARE_REFUSED (a file that is not a
+ * valid segment of this version: checked by the caller under the lock). */
+static seg_t *open_seg(const char *path, int cap, int mode, int *fd_out, int *why)
 {
+	*why = M2D_SHARE_UNAVAILABLE;
 	for (int attempt = 0; attempt < 50; ++attempt) {
 		int fd = open(path, O_RDWR | O_CLOEXEC);
 		if (fd >= 0) {
 			struct stat sb;
 			seg_t *g = NULL;
 			if (fstat(fd, &sb) == 0 && (size_t)sb.st_size >= sizeof(seg_t)) g = map_fd(fd);
-			close(fd);
-			if (g && __atomic_load_n(&g->magic, __ATOMIC_ACQUIRE) == SHARE_MAGIC && g->version == SHARE_VERSION)
-				return g;
-			if (g) munmap(g, sizeof(seg_t));
-			/* a segment of another layout version: leave it alone, use a private budget */
+			if (!g || __atomic_load_n(&g->magic, __ATOMIC_ACQUIRE) != SHARE_MAGIC) {
+				if (g) munmap(g, sizeof(seg_t));
+				close(fd);
+				*why = M2D_SHARE_REFUSED; /* (a half-published segment is never visible: link() publishes) */
+				return NULL;
+			}
+			*fd_out = fd;
+			return g;
+		}
+		if (errno != ENOENT) {
+			if (errno == EACCES) *why = M2D_SHARE_REFUSED; /* (someone else's file under our name) */
 			return NULL;
 		}
-		if (errno != ENOENT) return NULL;
-		char tmp[200];
+		char tmp[240];
 		snprintf(tmp, sizeof tmp, "%s.%d.tmp", path, (int)getpid());
-		int tfd = open(tmp, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
+		int tfd = open(tmp, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, (mode_t)mode);
 		if (tfd < 0) return NULL;
-		(void)fchmod(tfd, 0666); /* processes of other users decode on the same GPU too */
+		(void)fchmod(tfd, (mode_t)mode); /* (the umask does not widen or narrow it) */
 		if (ftruncate(tfd, sizeof(seg_t)) != 0) {
 			close(tfd);
 			unlink(tmp);
 			return NULL;
 		}
 		seg_t *g = map_fd(tfd);
-		close(tfd);
 		if (!g) {
+			close(tfd);
 			unlink(tmp);
 			return NULL;
 		}
@@ -202,43 +258,72 @@ static seg_t *open_seg(const char *path, int cap)
 		const int linked = link(tmp, path) == 0;
 		const int link_errno = errno;
 		unlink(tmp);
-		if (linked) return g;
+		if (linked) {
+			*fd_out = tfd;
+			return g;
+		}
 		munmap(g, sizeof(seg_t));
+		close(tfd);
 		if (link_errno != EEXIST) return NULL;
 		/* lost the race: open theirs */
 	}
 	return NULL;
 }
 
-m2d_share_t *m2d_share_open(const char *key, int cap_units)
+m2d_share_t *m2d_share_open(const char *key, int cap_units, int *why)
 {
+	int dummy;
+	if (!why) why = &dummy;
+	*why = M2D_SHARE_UNAVAILABLE;
 	if (!key || cap_units <= 0) return NULL;
 	m2d_share_t *s = (m2d_share_t *)calloc(1, sizeof *s);
 	if (!s) return NULL;
 	const char *dir = getenv("M2DEC_AMD_SHARE_DIR");
 	if (!dir) dir = access("/dev/shm", W_OK) == 0 ? "/dev/shm" : "/tmp";
-	snprintf(s->path, sizeof s->path, "%s/m2dec_amd.budget.%s", dir, key);
+	const char *gm = getenv("M2DEC_AMD_SHARE_GROUP"); /* opt-in: the processes of one group share the budget */
+	const int group = gm && atoi(gm);
+	snprintf(s->path, sizeof s->path, "%s/m2dec_amd.budget.%s.%c%u", dir, key, group ? 'g' : 'u',
+	         group ? (unsigned)getgid() : (unsigned)getuid());
 	for (char *c = s->path + strlen(dir) + 1; *c; ++c)
 		if (*c == '/') *c = '_';
 	s->pid = (int32_t)getpid();
 	s->start = proc_start(s->pid);
 	s->idx = -1;
+	s->fd = -1;
+	s->cap = cap_units;
 	seg_t *g = NULL;
+	const char *bad = NULL;
 	for (int attempt = 0; attempt < 50 && !g; ++attempt) {
-		g = open_seg(s->path, cap_units);
+		g = open_seg(s->path, cap_units, group ? 0660 : 0600, &s->fd, why);
 		if (!g) break;
 		if (lock(g) != 0) {
 			munmap(g, sizeof(seg_t));
+			close(s->fd);
 			g = NULL;
 			break;
 		}
 		if (g->magic != SHARE_MAGIC) { /* retired by its last user between our open and lock: open anew */
 			pthread_mutex_unlock(&g->mu);
 			munmap(g, sizeof(seg_t));
+			close(s->fd);
 			g = NULL;
+			continue;
+		}
+		if ((bad = seg_check(g, cap_units)) != NULL) {
+			pthread_mutex_unlock(&g->mu);
+			munmap(g, sizeof(seg_t));
+			close(s->fd);
+			g = NULL;
+			*why = M2D_SHARE_REFUSED;
+			break;
 		}
 	}
 	if (!g) {
+		if (*why == M2D_SHARE_REFUSED)
+			fprintf(stderr, "m2dec_amd: REFUSING the shared workgroup budget %s: %s.  A private budget would let another "
+			        "process's waiting workgroups starve this one's (DESIGN.md §5); remove the file if no decoder uses it, "
+			        "or set M2DEC_AMD_SHARE=0 to run with a process-local budget\n",
+			        s->path, bad ? bad : "not a valid segment (or not ours)");
 		free(s);
 		return NULL;
 	}
@@ -252,7 +337,11 @@ m2d_share_t *m2d_share_open(const char *key, int cap_units)
 				break;
 			}
 		}
-		if (s->idx < 0 && pass == 0) sweep(g, -1);
+		if (s->idx < 0 && pass == 0) sweep(s->fd, g, -1);
+	}
+	if (s->idx >= 0 && lease_lock(s->fd, s->idx, F_WRLCK) < 0 && errno != EINVAL &&
+	    g->lease[s->idx].pid != s->pid) { /* (this process's other handle holds the byte of its own lease) */
+		s->idx = -1; /* a free entry whose byte a live holder still locks: the table is not trustworthy */
 	}
 	if (s->idx >= 0 && g->lease[s->idx].pid != s->pid) {
 		lease_t *l = &g->lease[s->idx];
@@ -261,11 +350,16 @@ m2d_share_t *m2d_share_open(const char *key, int cap_units)
 		l->start = s->start;
 	}
 	pthread_mutex_unlock(&g->mu);
-	if (s->idx < 0) { /* 256 live decoding processes on one GPU: fall back to a private budget */
+	if (s->idx < 0) {
+		fprintf(stderr, "m2dec_amd: REFUSING the shared workgroup budget %s: all %d leases are held by live processes\n",
+		        s->path, SHARE_LEASES);
+		*why = M2D_SHARE_REFUSED;
 		munmap(g, sizeof(seg_t));
+		close(s->fd);
 		free(s);
 		return NULL;
 	}
+	*why = 0;
 	pthread_mutex_lock(&g_open_mu);
 	s->next = g_open;
 	g_open = s;
@@ -275,9 +369,19 @@ m2d_share_t *m2d_share_open(const char *key, int cap_units)
 
 int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 {
-	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return 1;
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) { /* after exit: this process's own account, within cap */
+		if (__atomic_add_fetch(&s->local_used, units, __ATOMIC_ACQ_REL) <= s->cap) return 1;
+		__atomic_sub_fetch(&s->local_used, units, __ATOMIC_ACQ_REL);
+		return 0;
+	}
 	seg_t *g = s->seg;
 	if (lock(g) != 0) return 0;
+	if (g->total < 0 || g->total > g->cap || g->cap != s->cap || g->lease[s->idx].pid != s->pid) {
+		pthread_mutex_unlock(&g->mu);
+		fprintf(stderr, "m2dec_amd: the shared workgroup budget %s is corrupted (cap %d, total %d): refusing to launch\n",
+		        s->path, g->cap, g->total);
+		return -1;
+	}
 	int ok = 0;
 	for (int pass = 0; pass < 2; ++pass) {
 		if (g->total + units <= g->cap) {
@@ -286,7 +390,7 @@ int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 			ok = 1;
 			break;
 		}
-		if (pass == 0 && !sweep(g, s->idx)) break;
+		if (pass == 0 && !sweep(s->fd, g, s->idx)) break;
 	}
 	g->lease[s->idx].wait_ms = ok ? 0 : now_ms(); /* (m2d_share_others_waiting) */
 	if (total) *total = g->total;
@@ -301,7 +405,11 @@ int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs)
 
 void m2d_share_release(m2d_share_t *s, int units)
 {
-	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) return;
+	if (__atomic_load_n(&s->exited, __ATOMIC_ACQUIRE)) {
+		__atomic_sub_fetch(&s->local_used, units, __ATOMIC_ACQ_REL); /* (units taken before exit were never local:
+		                                                                 the account may go negative, never above cap) */
+		return;
+	}
 	seg_t *g = s->seg;
 	if (units <= 0 || lock(g) != 0) return;
 	lease_t *l = &g->lease[s->idx];
@@ -335,7 +443,7 @@ int m2d_share_contexts(m2d_share_t *s, int delta)
 	if (g->lease[s->idx].contexts < 0) g->lease[s->idx].contexts = 0;
 	int n = 0;
 	for (int i = 0; i < SHARE_LEASES; ++i)
-		if (g->lease[i].pid && (i == s->idx || !lease_dead(&g->lease[i]))) n += g->lease[i].contexts;
+		if (g->lease[i].pid && (i == s->idx || !lease_dead(s->fd, &g->lease[i], i))) n += g->lease[i].contexts;
 	pthread_mutex_unlock(&g->mu);
 	return n;
 }
@@ -372,14 +480,18 @@ static void share_drop(m2d_share_t *s, int unmap)
 		memset(l, 0, sizeof *l);
 		int live = 0;
 		for (int i = 0; i < SHARE_LEASES; ++i)
-			live += g->lease[i].pid != 0 && !lease_dead(&g->lease[i]);
+			live += g->lease[i].pid != 0 && i != s->idx && !lease_dead(s->fd, &g->lease[i], i);
 		if (!live) {
 			g->magic = 0;
 			unlink(s->path);
 		}
+		(void)lease_lock(s->fd, s->idx, F_UNLCK);
 		pthread_mutex_unlock(&g->mu);
 	}
-	if (unmap) munmap(g, sizeof(seg_t));
+	if (unmap) {
+		munmap(g, sizeof(seg_t));
+		close(s->fd);
+	}
 }
 
 void m2d_share_close(m2d_share_t *s)
@@ -413,7 +525,14 @@ __attribute__((destructor)) static void share_exit(void)
 }
 
 /* ---- C-ABI for tests and diagnostics (include/m2dec_amd.h) */
-void *m2dec_amd_share_open(const char *key, int cap_units) { return m2d_share_open(key, cap_units); }
+void *m2dec_amd_share_open(const char *key, int cap_units) { return m2d_share_open(key, cap_units, NULL); }
+void *m2dec_amd_share_open2(const char *key, int cap_units, int *why) { return m2d_share_open(key, cap_units, why); }
+int m2dec_amd_share_path(void *s, char *out, int n)
+{
+	if (!s || !out || n <= 0) return -1;
+	snprintf(out, (size_t)n, "%s", ((m2d_share_t *)s)->path);
+	return 0;
+}
 int m2dec_amd_share_try(void *s, int units) { return s ? m2d_share_try((m2d_share_t *)s, units, NULL, NULL) : 0; }
 void m2dec_amd_share_release(void *s, int units)
 {

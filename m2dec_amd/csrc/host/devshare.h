@@ -10,11 +10,16 @@ extern "C" {
 #define M2D_SHARE_UNITS_PER_CU 60
 
 typedef struct m2d_share m2d_share_t;
-/* the segment of device `key` (its PCI bus id), created with `cap_units` if it does not exist; NULL when
- * shared memory is unavailable (the caller then keeps a process-local budget) */
-m2d_share_t *m2d_share_open(const char *key, int cap_units);
+/* the segment of device `key` (its PCI bus id) for this user (or group), created with `cap_units` if it does not
+ * exist.  NULL with *why (optional) = M2D_SHARE_UNAVAILABLE when shared memory is unavailable here (the caller may
+ * keep a process-local budget), M2D_SHARE_REFUSED when the file is not a valid segment of this version or its
+ * leases are all held (reported on stderr: the caller must not decode with a private budget) */
+#define M2D_SHARE_UNAVAILABLE 1
+#define M2D_SHARE_REFUSED 2
+m2d_share_t *m2d_share_open(const char *key, int cap_units, int *why);
 /* 1: `units` reserved for this process; 0: they do not fit now (the leases of dead processes were reclaimed
- * first).  total / procs (optional): the units in use and the processes holding some, after the call */
+ * first); -1: the segment is corrupted (reported).  total / procs (optional): the units in use and the
+ * processes holding some, after the call */
 int m2d_share_try(m2d_share_t *s, int units, int *total, int *procs);
 void m2d_share_release(m2d_share_t *s, int units);
 /* 1 when another process waits for units (a reservation of its that did not fit, within the last 100 ms) */

@@ -2055,8 +2055,13 @@ static void find_empty_frame(h265_dec_t *d)
 	d->index = max_idx;
 }
 
+static long pipe_last_seq(const h265_dec_t *d);
+
+static void pipe_note_insert(h265_dec_t *d);
+
 static void insert_dpb(h265_dec_t *d, int frame_idx, int poc, int is_idr)
 {
+	pipe_note_insert(d);
 	int size = d->dpb_size, pos;
 	if (d->dpb_max <= size) {
 		size -= 1;
@@ -2072,6 +2077,7 @@ static void insert_dpb(h265_dec_t *d, int frame_idx, int poc, int is_idr)
 	d->dpb[pos].frame_idx = (int8_t)frame_idx;
 	d->dpb[pos].poc = poc;
 	d->dpb[pos].is_idr = (uint8_t)is_idr;
+	d->dpb[pos].seq = pipe_last_seq(d); /* (slice_layer dispatched the picture just before) */
 	d->dpb_size = size + 1;
 }
 
@@ -2156,8 +2162,36 @@ typedef struct h265_pipe {
 	h265r_backend_t be;
 	int have_be;
 	int err_seen;                  /* a picture failed: decode_picture returns -2 from now on */
+	long fail_seq;                 /* the first picture that failed (LONG_MAX: none): it and every later one
+	                                  are never output, as the sequential path never decodes past it */
+	/* the caller's DPB as it was before each dispatched picture's insert_dpb, and the entries get popped since
+	 * (caller's thread only): on a failure the DPB goes back to its state before the failed picture, less what
+	 * was output meanwhile — exactly the sequential path's DPB when its decode_picture returned -2 there */
+	struct {
+		h265_dpb_elem_t dpb[16];
+		int size;
+		long npop, seq;
+	} hist[H265_RING];
+	long popped[4 * H265_RING];
+	long npop;
+	int rolled_back;
 	uint64_t bins;
 } h265_pipe_t;
+
+/* the sequence number of the picture dispatched last (-1: sequential path) */
+static long pipe_last_seq(const h265_dec_t *d) { return d->pipe ? d->pipe->head - 1 : -1; }
+
+/* parse ahead: the DPB before the dispatched picture's insert (pipe_purge_failed) */
+static void pipe_note_insert(h265_dec_t *d)
+{
+	h265_pipe_t *P = d->pipe;
+	if (!P || P->head <= 0) return;
+	const int h = (int)((P->head - 1) % H265_RING);
+	memcpy(P->hist[h].dpb, d->dpb, sizeof(d->dpb));
+	P->hist[h].size = d->dpb_size;
+	P->hist[h].npop = P->npop;
+	P->hist[h].seq = P->head - 1;
+}
 
 static double h265_now(void)
 {
@@ -2186,6 +2220,7 @@ static int pipe_on(h265_dec_t *d)
 	pthread_cond_init(&P->cv_done, NULL);
 	P->nth = pipe_threads(d);
 	for (int i = 0; i < H265R_MAX_FRAMES; ++i) P->col_writer[i] = P->col_reader[i] = P->frame_seq[i] = -1;
+	P->fail_seq = LONG_MAX;
 	for (int i = 0; i < H265_RING; ++i) P->jobs[i].P = P;
 	P->be = d->be;
 	P->have_be = d->have_be;
@@ -2223,10 +2258,15 @@ static void pipe_submit_locked(h265_pipe_t *P)
 		int r = -1;
 		const int tr = getenv("M2DEC_AMD_H265_TRACE") != NULL;
 		if (tr) fprintf(stderr, "h265 job %ld submit %.3f\n", j->seq, h265_now());
-		if (!j->err && P->have_be) r = P->be.submit(P->be.self, &j->w->pic);
+		/* (nothing after a failed picture reaches the back end: the sequential path never decodes it, so the frames
+		 * it would overwrite keep their content for the output that follows) */
+		if (!j->err && P->have_be && j->seq < P->fail_seq) r = P->be.submit(P->be.self, &j->w->pic);
 		if (tr) fprintf(stderr, "h265 job %ld submitted %.3f\n", j->seq, h265_now());
 		pthread_mutex_lock(&P->mu);
-		if (r < 0) P->err_seen = 1;
+		if (r < 0) { /* a slice-data error on a worker (j->err) or a refused submission */
+			P->err_seen = 1;
+			if (j->seq < P->fail_seq) P->fail_seq = j->seq;
+		}
 		P->bins += j->w->cabac_bins;
 		j->state = JOB_FREE;
 		P->sub++;
@@ -2386,7 +2426,13 @@ static int pipe_dispatch(perr_t *e, const h265_sps_t *s, const h265_pps_t *p, si
 		if (pthread_create(&P->th[P->started], NULL, pipe_worker, P) != 0) break;
 		P->started++;
 	}
-	if (!P->started) { /* no thread: parse it here */
+	if (!P->started) { /* no worker could be started: the picture fails here (decode_picture returns -2, as for a
+	                     * slice-data error) and is retired at once, so no drain waits for a job nobody runs */
+		j->err = 1;
+		j->state = JOB_PARSED;
+		j->rows_done = INT_MAX;
+		while (P->parsed_below < P->head && P->jobs[P->parsed_below % H265_RING].state == JOB_PARSED) P->parsed_below++;
+		pipe_submit_locked(P);
 		pthread_mutex_unlock(&P->mu);
 		return -1;
 	}
@@ -2432,14 +2478,44 @@ static void pipe_stop(h265_dec_t *d)
 	d->pipe = NULL;
 }
 
-/* peek / get: the picture of frame idx was submitted (its reconstruction is the back end's to wait for) */
-static void pipe_wait_frame(h265_dec_t *d, int idx)
+/* peek / get: the last picture dispatched into frame idx was retired (submitted, its reconstruction the back
+ * end's to wait for, or failed).  Returns 1 when some picture failed on a worker: the sequential path (and the
+ * reference, h265.cpp:4904) stops at the failing picture, so it and every picture dispatched after it are never
+ * output (pipe_purge_failed). */
+static int pipe_wait_frame(h265_dec_t *d, int idx)
 {
 	h265_pipe_t *P = d->pipe;
-	if (!P || idx < 0 || idx >= H265R_MAX_FRAMES) return;
+	if (!P || idx < 0 || idx >= H265R_MAX_FRAMES) return 0;
 	pthread_mutex_lock(&P->mu);
 	while (P->frame_seq[idx] >= P->sub) pthread_cond_wait(&P->cv_done, &P->mu);
+	const int failed = P->fail_seq != LONG_MAX;
 	pthread_mutex_unlock(&P->mu);
+	return failed;
+}
+
+/* after a failure: the DPB back to its state before the failed picture's insert, less the entries get popped
+ * since (caller's thread, once); 1 if it changed */
+static int pipe_purge_failed(h265_dec_t *d)
+{
+	h265_pipe_t *P = d->pipe;
+	if (P->rolled_back) return 0;
+	pthread_mutex_lock(&P->mu);
+	const long f = P->fail_seq;
+	pthread_mutex_unlock(&P->mu);
+	if (f == LONG_MAX || f >= P->head) return 0;
+	P->rolled_back = 1;
+	const int h = (int)(f % H265_RING);
+	if (P->hist[h].seq != f) return 0; /* (failed in its dispatch: never inserted, nothing after it either) */
+	int k = 0;
+	for (int i = 0; i < P->hist[h].size; ++i) {
+		const h265_dpb_elem_t *el = &P->hist[h].dpb[i];
+		int gone = 0;
+		for (long q = P->hist[h].npop; q < P->npop && !gone; ++q) gone = P->popped[q % (4 * H265_RING)] == el->seq;
+		if (!gone) d->dpb[k++] = *el;
+	}
+	d->dpb_size = k;
+	d->dpb_output = -1;
+	return 1;
 }
 
 /* slice_layer (h265.cpp:4849-4866) */
@@ -2621,9 +2697,13 @@ static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
 {
 	h265_dec_t *d = CTX(ctx);
 	if (!d || !frame) return -1;
-	const int idx = peek_idx(d, bypass);
+	int idx = peek_idx(d, bypass);
 	if (idx < 0) return 0;
-	pipe_wait_frame(d, idx);
+	if (pipe_wait_frame(d, idx) && pipe_purge_failed(d)) {
+		idx = peek_idx(d, bypass);
+		if (idx < 0) return 0;
+		(void)pipe_wait_frame(d, idx);
+	}
 	if (d->have_be && d->be.sync_frame(d->be.self, idx) < 0) return -1;
 	*frame = d->frames[idx];
 	return 1;
@@ -2635,6 +2715,7 @@ static int api_get(void *ctx, m2d_frame_t *frame, int bypass)
 	const int r = api_peek(ctx, frame, bypass);
 	if (r < 0) return -1;
 	if (d->dpb_size > 0) { /* force_pop_dpb, whether a frame was returned or not (h265.cpp:4969-4976, 5000-5008) */
+		if (d->pipe) d->pipe->popped[d->pipe->npop++ % (4 * H265_RING)] = d->dpb[0].seq;
 		memmove(&d->dpb[0], &d->dpb[1], sizeof(d->dpb[0]) * (size_t)d->dpb_size);
 		d->dpb_size--;
 		d->dpb_output = -1;

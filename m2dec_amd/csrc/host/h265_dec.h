@@ -124,6 +124,7 @@ typedef struct {
 	int poc;
 	int8_t frame_idx;
 	uint8_t is_idr;
+	long seq; /* parse ahead: the dispatched picture's sequence number (-1 on the sequential path) */
 } h265_dpb_elem_t;
 
 /* prediction info of a block (pred_info_t, h265modules.h:420-423): compared with memcmp by the merge list */

@@ -224,3 +224,122 @@ def test_reaper_wakes_only_while_another_process_waits(share_env):
     finally:
         L.m2dec_amd_share_close(s)
 
+
+
+# ---- round 6 hardening: owner-only segments, validated on open, liveness by lock
+
+SEG_HEAD = 8  # magic, version (uint32 each), then the robust mutex (40 bytes on x86-64 glibc), cap, total
+
+
+def _seg_file(share_env):
+    files = [f for f in os.listdir(share_env) if f.startswith("m2dec_amd.budget.") and not f.endswith(".tmp")]
+    assert len(files) == 1, files
+    return share_env / files[0]
+
+
+def _open2(L, key, cap):
+    L.m2dec_amd_share_open2.restype = ctypes.c_void_p
+    L.m2dec_amd_share_open2.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    why = ctypes.c_int(-1)
+    s = L.m2dec_amd_share_open2(key.encode(), cap, ctypes.byref(why))
+    return s, why.value
+
+
+def _hold_in_child(share_env, key, cap, units):
+    (share_env / "c").write_bytes(b"\0" * 16)
+    p = subprocess.Popen([sys.executable, "-c", WORKER, LIB, key, str(cap), "hold", str(share_env / "c"), str(units)],
+                         stdout=subprocess.PIPE, text=True, start_new_session=True)
+    assert p.stdout.readline().strip() == "holding"
+    return p
+
+
+def test_segment_is_owner_only_and_named_per_user(share_env):
+    L = _lib()
+    s = L.m2dec_amd_share_open(f"mode{os.getpid()}".encode(), 60)
+    assert s
+    f = _seg_file(share_env)
+    assert f.name.endswith(f".u{os.getuid()}")
+    assert (f.stat().st_mode & 0o777) == 0o600
+    L.m2dec_amd_share_close(s)
+
+
+def test_group_mode_is_opt_in(share_env, monkeypatch):
+    monkeypatch.setenv("M2DEC_AMD_SHARE_GROUP", "1")
+    L = _lib()
+    s = L.m2dec_amd_share_open(f"grp{os.getpid()}".encode(), 60)
+    assert s
+    f = _seg_file(share_env)
+    assert f.name.endswith(f".g{os.getgid()}") and (f.stat().st_mode & 0o777) == 0o660
+    L.m2dec_amd_share_close(s)
+
+
+@pytest.mark.parametrize("damage", ["cap", "total", "lease_units", "version", "magic", "short"])
+def test_corrupted_or_foreign_segment_is_refused_loudly(share_env, damage):
+    """A segment file that is not a valid segment of this layout (another build's version, garbage in cap, total
+    or a lease) is refused with a message, not silently replaced by a private budget; the back end then does not
+    start (runtime.hip SlotBudget.refused)."""
+    import struct
+    L = _lib()
+    key, cap = f"bad{damage}{os.getpid()}", 120
+    p = _hold_in_child(share_env, key, cap, 30)  # a live user keeps the segment while the test damages it
+    try:
+        f = _seg_file(share_env)
+        raw = bytearray(f.read_bytes())
+        magic, version = struct.unpack_from("<II", raw, 0)
+        cap_off = 8 + 40  # (after the pthread mutex)
+        assert struct.unpack_from("<ii", raw, cap_off) == (cap, 30)
+        lease0 = cap_off + 8 + 8  # cap, total, reclaimed (int64)
+        if damage == "cap":
+            struct.pack_into("<i", raw, cap_off, 10 ** 6)
+        elif damage == "total":
+            struct.pack_into("<i", raw, cap_off + 4, -5)
+        elif damage == "lease_units":
+            i = next(k for k in range(256) if struct.unpack_from("<i", raw, lease0 + 24 * k)[0] != 0)
+            struct.pack_into("<i", raw, lease0 + 24 * i + 4, cap + 1)
+        elif damage == "version":
+            struct.pack_into("<I", raw, 4, version + 1)
+        elif damage == "magic":
+            struct.pack_into("<I", raw, 0, 0xdeadbeef)
+        if damage == "short":
+            f.write_bytes(bytes(raw[:100]))
+        else:
+            f.write_bytes(bytes(raw))
+        r = subprocess.run([sys.executable, "-c",
+                            "import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); L.m2dec_amd_share_open2.restype = ctypes.c_void_p;"
+                            "w = ctypes.c_int(-1); s = L.m2dec_amd_share_open2(sys.argv[2].encode(), int(sys.argv[3]), ctypes.byref(w));"
+                            "print(bool(s), w.value)", LIB, key, str(cap)],
+                           capture_output=True, text=True, timeout=60, env=dict(os.environ))
+        assert r.stdout.split() == ["False", "2"], (r.stdout, r.stderr)
+        assert "REFUSING the shared workgroup budget" in r.stderr
+    finally:
+        os.kill(p.pid, signal.SIGKILL)
+        p.wait(timeout=30)
+
+
+def test_dead_holder_found_by_its_lock_not_its_pid(share_env):
+    """Liveness is the lease byte's open-file-description lock (dropped by the kernel at death, in any PID
+    namespace): a lease whose pid names a live process but whose byte nobody locks is reclaimed."""
+    import struct
+    L = _lib()
+    key, cap = f"lk{os.getpid()}", 120
+    p = _hold_in_child(share_env, key, cap, 100)
+    try:
+        s = L.m2dec_amd_share_open(key.encode(), cap)
+        assert not L.m2dec_amd_share_try(s, 30)  # the child's lock says it is alive
+        # forge: the child's lease now names pid 1 (alive, not us) and the child dies: its lock goes
+        f = _seg_file(share_env)
+        os.kill(p.pid, signal.SIGKILL)
+        p.wait(timeout=30)
+        raw = bytearray(f.read_bytes())
+        lease0 = 8 + 40 + 16
+        i = next(k for k in range(256) if struct.unpack_from("<ii", raw, lease0 + 24 * k)[1] == 100)
+        struct.pack_into("<i", raw, lease0 + 24 * i, 1)
+        f.write_bytes(bytes(raw))
+        assert L.m2dec_amd_share_try(s, 100), "a lease without its lock must be reclaimed even if its pid is alive"
+        assert _state(L, s)["reclaimed"] == 100
+        L.m2dec_amd_share_release(s, 100)
+        L.m2dec_amd_share_close(s)
+    finally:
+        if p.poll() is None:
+            os.kill(p.pid, signal.SIGKILL)
+            p.wait(timeout=30)

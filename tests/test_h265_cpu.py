@@ -160,3 +160,42 @@ def test_few_rps_sets_intra_stream(built, rps, tmp_path):
         md5s, err = m2dec_amd.decode_h265(data, backend=o.be)
     assert err == -2
     assert md5s and set(md5s) <= set(g["md5"]), md5s
+
+
+def test_worker_parse_error_matches_sequential(built, monkeypatch):
+    """a slice-data error found by a parse-ahead worker.  The sequential path (and the reference,
+    h265.cpp:4904) returns -2 at the failing picture and never outputs it or anything after it; with 8 workers
+    decode_picture has already returned for later pictures, so the pipe rolls the DPB back to its state before
+    the failed picture (less what was output meanwhile) and submits nothing after it.  Single-bit corruptions of
+    the slice data that make the sequential parse fail: both paths give the same MD5 list and the same -2."""
+    import random
+    data = bytes(h265_stream("cov_h265_a_long_s3"))
+    sc = b"\x00\x00\x00\x01"
+    pos, i = [], data.find(sc)
+    while i >= 0:
+        pos.append(i)
+        i = data.find(sc, i + 4)
+    nals = [(p, (data[p + 4] >> 1) & 63) for p in pos]
+    slices = [k for k, (_, t) in enumerate(nals) if t in (0, 1, 19)]
+    with Oracle265Backend() as o:
+        full, _ = m2dec_amd.decode_h265(data, backend=o.be)
+    rng = random.Random(1)
+    found = 0
+    for _ in range(200):
+        k = slices[rng.randrange(1, len(slices))]
+        a, b = nals[k][0], nals[k + 1][0] if k + 1 < len(nals) else len(data)
+        off = rng.randrange(a + 12, b - 2)
+        bad = data[:off] + bytes([data[off] ^ (1 << rng.randrange(8))]) + data[off + 1:]
+        monkeypatch.setenv("M2DEC_AMD_H265_THREADS", "0")
+        with Oracle265Backend() as o:
+            m0, e0 = m2dec_amd.decode_h265(bad, backend=o.be)
+        if len(m0) >= len(full):
+            continue  # (this corruption decodes to the end)
+        monkeypatch.setenv("M2DEC_AMD_H265_THREADS", "8")
+        with Oracle265Backend() as o:
+            m8, e8 = m2dec_amd.decode_h265(bad, backend=o.be)
+        assert (m8, e8) == (m0, e0) and e0 == -2
+        found += 1
+        if found == 6:
+            break
+    assert found == 6

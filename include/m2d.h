@@ -106,8 +106,8 @@ enum {
 
 /* The H.264 decoder: GPU reconstruction behind the reference's function table. */
 extern const m2d_func_table_t * const h264d_func;
-/* The MPEG-1/2 video decoder (mpeg2.cpp:1800-1811; mpeg2.h): intra pictures on the CPU
- * (BASELINE.json configs[0]); P / B pictures are reported as errors. */
+/* The MPEG-1/2 video decoder (mpeg2.cpp:1800-1811; mpeg2.h): I, P and B frame pictures, reconstructed on the
+ * CPU (BASELINE.json configs[0], the reference's own configuration) or on gfx950 (m2dec_amd_m2v_use_gpu). */
 extern const m2d_func_table_t * const m2d_func;
 /* h265.h:37, h265.cpp:5010-5025 (m2dec_amd/csrc/host/h265_dec.c) */
 extern const m2d_func_table_t * const h265d_func;

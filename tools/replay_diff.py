@@ -62,6 +62,30 @@ def intra_dump(tr, recs):
     print(" DC:", d[1936:1952].tolist(), " HV:", d[1952:1956].tolist())
 
 
+def rows_dump(tr, recs):
+    """-DM2DEC_DBG_ROWS builds: per row workgroup / wave of the I picture, the row intra_row worked on and its
+    first MB's record kind / coefficient offset, against the expected row of that workgroup and wave."""
+    L = m2dec_amd.lib()
+    L.m2dec_amd_debug_rows.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    buf = (ctypes.c_uint * 2048)()
+    if L.m2dec_amd_debug_rows(buf, 2048) < 0:
+        print("no row dump in this build")
+        return
+    d = list(buf)
+    p = tr.pics[0]
+    Wmb = tr.width // 16
+    for b in range(256):
+        for w in range(4):
+            a, c = d[(b * 4 + w) * 2], d[(b * 4 + w) * 2 + 1]
+            if (a >> 24) != 0xab:
+                continue
+            y, part, wave = a & 0xff, (a >> 8) & 0xf, (a >> 12) & 0xf
+            want_kind = recs[p.off_mb + 32 * (y * Wmb)]
+            want_coef = int.from_bytes(recs[p.off_mb + 32 * (y * Wmb) + 20:p.off_mb + 32 * (y * Wmb) + 24], "little")
+            print(f"block {b} wave {w}: y {y} part {part} wave-arg {wave} y0 {c & 0xffff} kind {(c >> 16) & 0xff} "
+                  f"(record {want_kind}) coef&255 {c >> 24} (record {want_coef & 255})")
+
+
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "c3_1080p_s1"
     before = int(sys.argv[2]) if len(sys.argv) > 2 else 0
@@ -116,6 +140,8 @@ def main():
     print(f"{name}: {nbad} of {tr.npics} pictures differ", flush=True)
     if os.environ.get("DBG_INTRA"):
         intra_dump(tr, recs)
+    if os.environ.get("DBG_ROWS"):
+        rows_dump(tr, recs)
     rp.close()
 
 

@@ -1220,12 +1220,15 @@ struct HipBackend {
 	hipStream_t copy = nullptr; /* decode ahead: bind's copies out of the picture buffers */
 	m2d_frame_t frames[64];
 	int nframes = 0;
-	uint8_t *stg[64];          /* staging buffer holding / receiving slot i's picture (null: none) */
+	/* staging: [0, 64) caller slots; [64, 128) decode ahead, picture buffer (virtual id) i - 64 copied out right
+	 * behind its kernel, before the API context binds it to a slot (be_bind then moves the buffer to the slot) */
+	uint8_t *stg[128];         /* staging buffer holding / receiving index i's picture (null: none) */
 	size_t stg_size = 0;       /* picture bytes per staging buffer (1.5 W H); the buffer has kStgTail more: the
 	                            * error word as of the copy (read after the copy's event, no hipMemcpy) */
-	hipEvent_t slot_ev[64];    /* the copy into stg[i] is complete */
-	hipEvent_t d2h_ev[64][2];  /* timing: start / end of that copy */
-	bool slot_pending[64];     /* stg[i] holds a picture not yet copied to the caller's frame */
+	hipEvent_t slot_ev[128];   /* the copy into stg[i] is complete */
+	hipEvent_t d2h_ev[128][2]; /* timing: start / end of that copy */
+	bool slot_pending[128];    /* stg[i] holds a picture not yet copied to the caller's frame */
+	int prestaged = 0;         /* [64, 128) entries holding a picture (at most kPrestageMax) */
 	Arena ar[kArenas];
 	int next = 0;
 	/* submitted pictures not launched yet (decode order); launched together by be_flush */
@@ -1255,6 +1258,15 @@ struct HipBackend {
 
 int launch_held(HipBackend *b);
 
+/* decode ahead: pictures copied out to staging behind their kernels (M2DEC_AMD_PRESTAGE=0: at bind, as before
+ * round 6), at most kPrestageMax of a back end at a time (pinned memory: 64 x 3 MB at 1080p) */
+static const int kPrestageMax = 32;
+static bool prestage_on()
+{
+	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 1;
+	return on != 0;
+}
+
 void flush_timing(HipBackend *b, TimingSlot &t)
 {
 	if (!t.pending) return;
@@ -1275,6 +1287,7 @@ void flush_timing(HipBackend *b, TimingSlot &t)
 /* slot i's staging buffer goes back to the pool (its copy, if any, is complete) */
 void stage_drop(HipBackend *b, int i)
 {
+	if (i >= 64 && b->stg[i]) b->prestaged--;
 	g_stage.give(b->stg[i], b->stg_size + kStgTail);
 	b->stg[i] = nullptr;
 	b->slot_pending[i] = false;
@@ -1293,8 +1306,8 @@ int be_set_frames(void *self, int n, const m2d_frame_t *frames, int width, int h
 	const size_t stg = (size_t)width * height * 3 / 2;
 	/* pictures bound but not yet handed out keep their staging (they reach the new frames) unless the
 	 * picture size changed — the reference would hand out the new, unwritten frames then */
-	for (int i = 0; i < 64; ++i)
-		if (b->stg[i] && (stg != b->stg_size || i >= n)) stage_drop(b, i);
+	for (int i = 0; i < 128; ++i)
+		if (b->stg[i] && (stg != b->stg_size || (i < 64 && i >= n) || i >= 64)) stage_drop(b, i);
 	b->stg_size = stg;
 	/* one device picture buffer per virtual id (decode ahead) — a caller slot also names one */
 	if (b->sc.configure(width, height, 64) < 0) return -1;
@@ -1547,6 +1560,26 @@ int launch_held(HipBackend *b)
 		sc.tm.ref_bytes += h.ref_bytes;
 		sc.tm.frame_bytes += (int64_t)(ls * 3 / 2);
 	}
+	/* decode ahead: each picture out to pinned staging right behind its kernel, before the API context binds it
+	 * (r139 timeline: with the copy issued at bind, the API thread waited on every frame's copy in turn — 60 copies
+	 * of ~0.3 ms each from the bind to the frame's peek, the last one 6.2 ms after the last kernel) */
+	for (int i = 0; i < n && prestage_on(); ++i) {
+		const HipBackend::Held &h = b->held[i];
+		if (!h.virt || b->prestaged >= kPrestageMax) continue;
+		const int v = 64 + h.j.slot;
+		if (b->stg[v]) { /* (an earlier picture of this buffer never bound — ahead_ok orders reuse after the bind) */
+			if (b->slot_pending[v]) CHECK(hipEventSynchronize(b->slot_ev[v]));
+			stage_drop(b, v);
+		}
+		if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
+		CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[h.j.slot], 0));
+		if (stage_copy(b, sc.frames + (size_t)h.j.slot * sc.fsz, v, b->copy) < 0) return -1;
+		b->prestaged++;
+		hipEvent_t r = sc.next_event(); /* (a reader of the buffer: its next writer waits for the copy) */
+		if (!r) return -1;
+		CHECK(hipEventRecord(r, b->copy));
+		sc.readers[h.j.slot].push_back(r);
+	}
 	m2d_tl('l', n, k);
 	return 0;
 }
@@ -1570,6 +1603,21 @@ int be_bind(void *self, int vid, int slot)
 		return -1;
 	}
 	CHECK(hipSetDevice(sc.dev));
+	if (b->slot_pending[64 + vid]) { /* copied out behind its kernel (launch_held): the slot takes that buffer */
+		if (b->stg[slot]) {
+			if (b->slot_pending[slot]) CHECK(hipEventSynchronize(b->slot_ev[slot])); /* (a picture never handed out) */
+			stage_drop(b, slot);
+		}
+		const int v = 64 + vid;
+		std::swap(b->stg[slot], b->stg[v]);
+		std::swap(b->slot_ev[slot], b->slot_ev[v]);
+		std::swap(b->d2h_ev[slot][0], b->d2h_ev[v][0]);
+		std::swap(b->d2h_ev[slot][1], b->d2h_ev[v][1]);
+		b->slot_pending[slot] = true;
+		b->slot_pending[v] = false;
+		b->prestaged--;
+		return 0;
+	}
 	if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
 	CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[vid], 0));
 	if (stage_copy(b, sc.frames + (size_t)vid * sc.fsz, slot, b->copy) < 0) return -1;
@@ -1676,12 +1724,12 @@ void be_destroy(void *self)
 	const double t1 = wall_s();
 	g_pool.put_stream(b->sc.dev, b->copy); /* (synchronises it: every staging copy is complete) */
 	b->copy = nullptr;
-	for (int i = 0; i < 64; ++i) stage_drop(b, i);
+	for (int i = 0; i < 128; ++i) stage_drop(b, i);
 	for (auto &a : b->ar) {
 		g_arenas.give(b->sc.dev, a); /* (every kernel reading it finished: sync_all above) */
 		g_pool.put_event(b->sc.dev, false, a.consumed);
 	}
-	for (int i = 0; i < 64; ++i) {
+	for (int i = 0; i < 128; ++i) {
 		g_pool.put_event(b->sc.dev, false, b->slot_ev[i]);
 		g_pool.put_event(b->sc.dev, true, b->d2h_ev[i][0]);
 		g_pool.put_event(b->sc.dev, true, b->d2h_ev[i][1]);
@@ -1738,7 +1786,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 		delete b;
 		return -1;
 	}
-	for (int i = 0; i < 64; ++i) {
+	for (int i = 0; i < 128; ++i) {
 		CHECK(g_pool.event(device, false, &b->slot_ev[i]));
 		CHECK(g_pool.event(device, true, &b->d2h_ev[i][0]));
 		CHECK(g_pool.event(device, true, &b->d2h_ev[i][1]));

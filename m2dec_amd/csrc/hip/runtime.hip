@@ -1263,7 +1263,7 @@ int launch_held(HipBackend *b);
 static const int kPrestageMax = 32;
 static bool prestage_on()
 {
-	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 1;
+	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 0;
 	return on != 0;
 }
 

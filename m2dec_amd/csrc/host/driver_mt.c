@@ -53,6 +53,7 @@ static void thread_cpu_report(const char *name)
  * 30.97 ms against 4 on two boxes, profiles/r137_ab_md5_tail_busy.txt; 16 = always: 30.15 ms), the shared pipe of
  * concurrent streams 4 (their pool stays busy until near the end) */
 #define MD5_TAIL_PARSE_BUSY 12
+#define MD5_TAIL_TAKE 2
 #define MD5_TAIL_PARSE_BUSY_STREAMS 4
 #define MD5_BIG_FRAME ((size_t)6 << 20) /* frames above this (4K) are not batched short of min_batch */
 
@@ -94,6 +95,7 @@ typedef struct md5_pipe {
 	int min_batch;           /* frames a thread waits for (M2DEC_AMD_MD5_MIN_BATCH, default MD5_MIN_BATCH) */
 	int tail_mode;           /* M2DEC_AMD_MD5_TAIL (default 1) */
 	int tail_busy;           /* tail mode at most this many busy parse workers (M2DEC_AMD_MD5_TAIL_BUSY) */
+	int tail_take;           /* frames a thread takes together in tail mode (M2DEC_AMD_MD5_TAIL_TAKE, 1-3) */
 	double wait_s;           /* ... or this long after the oldest was queued (M2DEC_AMD_MD5_WAIT_US) */
 	double t_wait;           /* callers: waiting for a free queue slot */
 	double t_hash;           /* MD5 threads: time hashing */
@@ -146,8 +148,14 @@ static void *md5_worker(void *arg)
 		 * ran 25 ms and ended the C5 decode (profiles/r127_timeline_c5.txt) */
 		const int queued = p->head - p->next;
 		const size_t fbytes = (size_t)p->frm[p->next % MD5_RING].width * (size_t)p->frm[p->next % MD5_RING].height * 3 / 2;
-		const int share = tail ? (queued + p->nth - 1) / p->nth
-		                       : ((queued < p->min_batch && fbytes > MD5_BIG_FRAME) ? 1 : MD5_BATCH);
+		int share = tail ? (queued + p->nth - 1) / p->nth
+		                 : ((queued < p->min_batch && fbytes > MD5_BIG_FRAME) ? 1 : MD5_BATCH);
+		/* tail: up to tail_take frames side by side on one core (md5.c stitched chains: 2 frames of 1080p in
+		 * 3.13 ms, 3 in 3.39 ms against 3.24 ms for one on the box's host, profiles/r141_md5host.txt), so the
+		 * tail's frames need a third to half of the cores.  c3 median decode 29.00 vs 30.68 ms with pairs;
+		 * 4K frames stay one per thread (C5 47.5 vs 45.9 ms with pairs, profiles/r141_ab_tail_take_*.txt) */
+		if (tail && share < p->tail_take && fbytes <= MD5_BIG_FRAME)
+			share = queued < p->tail_take ? queued : p->tail_take;
 		if (p->next == p->head) continue; /* (another thread took them) */
 		m2d_frame_t f[MD5_BATCH];
 		md5_stream_t *sof[MD5_BATCH];
@@ -241,6 +249,9 @@ static int pipe_open(md5_pipe_t *p, int streams, int threads)
 	if (p->min_batch > MD5_BATCH) p->min_batch = MD5_BATCH;
 	p->stats = getenv("M2DEC_AMD_ASYNC_STATS") != NULL;
 	p->tail_mode = getenv("M2DEC_AMD_MD5_TAIL") ? atoi(getenv("M2DEC_AMD_MD5_TAIL")) != 0 : 1;
+	p->tail_take = getenv("M2DEC_AMD_MD5_TAIL_TAKE") ? atoi(getenv("M2DEC_AMD_MD5_TAIL_TAKE")) : MD5_TAIL_TAKE;
+	if (p->tail_take < 1) p->tail_take = 1;
+	if (p->tail_take > 3) p->tail_take = 3;
 	p->tail_busy = getenv("M2DEC_AMD_MD5_TAIL_BUSY") ? atoi(getenv("M2DEC_AMD_MD5_TAIL_BUSY"))
 	                                                 : (streams > 1 ? MD5_TAIL_PARSE_BUSY_STREAMS : MD5_TAIL_PARSE_BUSY);
 	p->streams = streams;

@@ -191,6 +191,110 @@ void m2dec_amd_frame_md5(const m2d_frame_t *f, char out[35])
 	md5_line(dg, out);
 }
 
+/* ---------------------------------------------------------------- 2-3 frames on one core, scalar
+ * The scalar chain is latency-bound (~5 dependent ALU operations per step) and leaves most of the
+ * core's integer ports idle: two or three frames' chains stepped side by side run at about the latency
+ * of one (the 16-lane AVX-512 kernel below takes twice that for any batch of 2-16).  The tail of a
+ * stream (frames hashed as they leave the decoder, one thread each) is where this pays: two frames per
+ * core instead of one. */
+#define SSTEP(f, a, b, c, d, wi, k, s) \
+	do { \
+		for (int j = 0; j < NCH; ++j) { \
+			uint32_t x_; \
+			memcpy(&x_, lp[j] + 64 * n + 4 * (wi), 4); \
+			a[j] += f(b[j], c[j], d[j]) + x_ + (k); \
+			a[j] = ROTL(a[j], s) + b[j]; \
+		} \
+	} while (0)
+#define MD5XN_BLOCKS(name, NCH_) \
+	static void name(uint32_t st[][4], const uint8_t *const lp[], size_t nblocks) \
+	{ \
+		enum { NCH = NCH_ }; \
+		for (size_t n = 0; n < nblocks; ++n) { \
+			uint32_t a[NCH], b[NCH], c[NCH], d[NCH]; \
+			for (int j = 0; j < NCH; ++j) { \
+				a[j] = st[j][0]; \
+				b[j] = st[j][1]; \
+				c[j] = st[j][2]; \
+				d[j] = st[j][3]; \
+			} \
+			MD5XN_STEPS \
+			for (int j = 0; j < NCH; ++j) { \
+				st[j][0] += a[j]; \
+				st[j][1] += b[j]; \
+				st[j][2] += c[j]; \
+				st[j][3] += d[j]; \
+			} \
+		} \
+	}
+#define MD5XN_STEPS \
+SSTEP(F, a, b, c, d, 0, 0xd76aa478u, 7); \
+SSTEP(F, d, a, b, c, 1, 0xe8c7b756u, 12); \
+SSTEP(F, c, d, a, b, 2, 0x242070dbu, 17); \
+SSTEP(F, b, c, d, a, 3, 0xc1bdceeeu, 22); \
+SSTEP(F, a, b, c, d, 4, 0xf57c0fafu, 7); \
+SSTEP(F, d, a, b, c, 5, 0x4787c62au, 12); \
+SSTEP(F, c, d, a, b, 6, 0xa8304613u, 17); \
+SSTEP(F, b, c, d, a, 7, 0xfd469501u, 22); \
+SSTEP(F, a, b, c, d, 8, 0x698098d8u, 7); \
+SSTEP(F, d, a, b, c, 9, 0x8b44f7afu, 12); \
+SSTEP(F, c, d, a, b, 10, 0xffff5bb1u, 17); \
+SSTEP(F, b, c, d, a, 11, 0x895cd7beu, 22); \
+SSTEP(F, a, b, c, d, 12, 0x6b901122u, 7); \
+SSTEP(F, d, a, b, c, 13, 0xfd987193u, 12); \
+SSTEP(F, c, d, a, b, 14, 0xa679438eu, 17); \
+SSTEP(F, b, c, d, a, 15, 0x49b40821u, 22); \
+SSTEP(G, a, b, c, d, 1, 0xf61e2562u, 5); \
+SSTEP(G, d, a, b, c, 6, 0xc040b340u, 9); \
+SSTEP(G, c, d, a, b, 11, 0x265e5a51u, 14); \
+SSTEP(G, b, c, d, a, 0, 0xe9b6c7aau, 20); \
+SSTEP(G, a, b, c, d, 5, 0xd62f105du, 5); \
+SSTEP(G, d, a, b, c, 10, 0x02441453u, 9); \
+SSTEP(G, c, d, a, b, 15, 0xd8a1e681u, 14); \
+SSTEP(G, b, c, d, a, 4, 0xe7d3fbc8u, 20); \
+SSTEP(G, a, b, c, d, 9, 0x21e1cde6u, 5); \
+SSTEP(G, d, a, b, c, 14, 0xc33707d6u, 9); \
+SSTEP(G, c, d, a, b, 3, 0xf4d50d87u, 14); \
+SSTEP(G, b, c, d, a, 8, 0x455a14edu, 20); \
+SSTEP(G, a, b, c, d, 13, 0xa9e3e905u, 5); \
+SSTEP(G, d, a, b, c, 2, 0xfcefa3f8u, 9); \
+SSTEP(G, c, d, a, b, 7, 0x676f02d9u, 14); \
+SSTEP(G, b, c, d, a, 12, 0x8d2a4c8au, 20); \
+SSTEP(H, a, b, c, d, 5, 0xfffa3942u, 4); \
+SSTEP(H, d, a, b, c, 8, 0x8771f681u, 11); \
+SSTEP(H, c, d, a, b, 11, 0x6d9d6122u, 16); \
+SSTEP(H, b, c, d, a, 14, 0xfde5380cu, 23); \
+SSTEP(H, a, b, c, d, 1, 0xa4beea44u, 4); \
+SSTEP(H, d, a, b, c, 4, 0x4bdecfa9u, 11); \
+SSTEP(H, c, d, a, b, 7, 0xf6bb4b60u, 16); \
+SSTEP(H, b, c, d, a, 10, 0xbebfbc70u, 23); \
+SSTEP(H, a, b, c, d, 13, 0x289b7ec6u, 4); \
+SSTEP(H, d, a, b, c, 0, 0xeaa127fau, 11); \
+SSTEP(H, c, d, a, b, 3, 0xd4ef3085u, 16); \
+SSTEP(H, b, c, d, a, 6, 0x04881d05u, 23); \
+SSTEP(H, a, b, c, d, 9, 0xd9d4d039u, 4); \
+SSTEP(H, d, a, b, c, 12, 0xe6db99e5u, 11); \
+SSTEP(H, c, d, a, b, 15, 0x1fa27cf8u, 16); \
+SSTEP(H, b, c, d, a, 2, 0xc4ac5665u, 23); \
+SSTEP(I, a, b, c, d, 0, 0xf4292244u, 6); \
+SSTEP(I, d, a, b, c, 7, 0x432aff97u, 10); \
+SSTEP(I, c, d, a, b, 14, 0xab9423a7u, 15); \
+SSTEP(I, b, c, d, a, 5, 0xfc93a039u, 21); \
+SSTEP(I, a, b, c, d, 12, 0x655b59c3u, 6); \
+SSTEP(I, d, a, b, c, 3, 0x8f0ccc92u, 10); \
+SSTEP(I, c, d, a, b, 10, 0xffeff47du, 15); \
+SSTEP(I, b, c, d, a, 1, 0x85845dd1u, 21); \
+SSTEP(I, a, b, c, d, 8, 0x6fa87e4fu, 6); \
+SSTEP(I, d, a, b, c, 15, 0xfe2ce6e0u, 10); \
+SSTEP(I, c, d, a, b, 6, 0xa3014314u, 15); \
+SSTEP(I, b, c, d, a, 13, 0x4e0811a1u, 21); \
+SSTEP(I, a, b, c, d, 4, 0xf7537e82u, 6); \
+SSTEP(I, d, a, b, c, 11, 0xbd3af235u, 10); \
+SSTEP(I, c, d, a, b, 2, 0x2ad7d2bbu, 15); \
+SSTEP(I, b, c, d, a, 9, 0xeb86d391u, 21);
+MD5XN_BLOCKS(md5x2_blocks, 2)
+MD5XN_BLOCKS(md5x3_blocks, 3)
+
 /* ---------------------------------------------------------------- 16 frames at once (AVX-512F)
  * Multi-buffer MD5: lane l of every 512-bit register carries frame l's chain, so one core runs 16
  * independent MD5s at about the latency of one (the per-frame MD5 of FileWriterMd5 is a sequential
@@ -338,46 +442,89 @@ static int have_avx512(void)
 }
 #endif
 
+/* one geometry, rows contiguous (no horizontal crop): each frame's message is a luma run then a chroma run */
+static int same_runs(const m2d_frame_t *f, int n)
+{
+	for (int i = 0; i < n; ++i) {
+		const m2d_frame_t *g = &f[i];
+		if (g->width != f[0].width || g->height != f[0].height || g->crop[2] != f[0].crop[2] ||
+		    g->crop[3] != f[0].crop[3] || g->crop[0] || g->crop[1])
+			return 0;
+	}
+	return f[0].height - f[0].crop[2] - f[0].crop[3] > 0;
+}
+
+/* the scalar tail of lane l after its full blocks: the last partial block, the padding, the line */
+static void lane_finish(const uint32_t h[4], const uint8_t *pa, const uint8_t *pb, size_t la, size_t lb, size_t na,
+                        size_t nb, char out[35])
+{
+	md5_t m;
+	uint8_t dg[16];
+	for (int k = 0; k < 4; ++k) m.h[k] = h[k];
+	m.len = (uint64_t)(na + nb) * 64;
+	m.fill = 0;
+	if (nb) {
+		md5_update(&m, pb + nb * 64, lb - nb * 64);
+	} else {
+		md5_update(&m, pa + na * 64, la - na * 64);
+		md5_update(&m, pb, lb);
+	}
+	md5_final(&m, dg);
+	md5_line(dg, out);
+}
+
+static const uint32_t md5_iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+
+static int stitch_on(void)
+{
+	static int v = -1;
+	if (v < 0) {
+		const char *e = getenv("M2DEC_AMD_MD5_STITCH"); /* (A/B: 0 = batches of 2-3 on the 16-lane kernel) */
+		v = !(e && atoi(e) == 0);
+	}
+	return v;
+}
+
 int m2dec_amd_frames_md5(const m2d_frame_t *f, int n, char (*out)[35])
 {
 	if (n <= 0 || n > 16) return -1;
-#if defined(__x86_64__)
-	int lanes_ok = n >= 2 && have_avx512();
+	const int runs = n >= 2 && same_runs(f, n);
 	const int stride = f[0].width, h = f[0].height - f[0].crop[2] - f[0].crop[3];
-	for (int i = 0; i < n && lanes_ok; ++i) {
-		const m2d_frame_t *g = &f[i];
-		/* one geometry; rows contiguous (no horizontal crop) */
-		lanes_ok = g->width == stride && g->height == f[0].height && g->crop[2] == f[0].crop[2] &&
-		           g->crop[3] == f[0].crop[3] && g->crop[0] == 0 && g->crop[1] == 0;
+	const size_t la = (size_t)stride * (size_t)(h > 0 ? h : 0), lb = (size_t)stride * (size_t)(h > 0 ? h >> 1 : 0);
+	const size_t na = la / 64, nb = (la % 64) ? 0 : lb / 64;
+	if (runs && n <= 3 && stitch_on()) {
+		uint32_t st[3][4];
+		const uint8_t *pa[3], *pb[3];
+		for (int l = 0; l < n; ++l) {
+			pa[l] = f[l].luma + (size_t)stride * f[0].crop[2];
+			pb[l] = f[l].chroma + (size_t)stride * (f[0].crop[2] >> 1);
+			memcpy(st[l], md5_iv, sizeof(md5_iv));
+		}
+		if (n == 2) {
+			md5x2_blocks(st, pa, na);
+			md5x2_blocks(st, pb, nb);
+		} else {
+			md5x3_blocks(st, pa, na);
+			md5x3_blocks(st, pb, nb);
+		}
+		for (int l = 0; l < n; ++l) lane_finish(st[l], pa[l], pb[l], la, lb, na, nb, out[l]);
+		return 0;
 	}
-	if (lanes_ok && h > 0) {
-		const size_t la = (size_t)stride * (size_t)h, lb = (size_t)stride * (size_t)(h >> 1);
-		const size_t na = la / 64, nb = (la % 64) ? 0 : lb / 64;
+#if defined(__x86_64__)
+	if (runs && have_avx512()) {
 		uint32_t st[4][16];
 		const uint8_t *pa[16], *pb[16];
-		static const uint32_t iv[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
 		for (int l = 0; l < 16; ++l) {
 			const m2d_frame_t *g = &f[l < n ? l : 0]; /* idle lanes repeat lane 0 */
 			pa[l] = g->luma + (size_t)stride * f[0].crop[2];
 			pb[l] = g->chroma + (size_t)stride * (f[0].crop[2] >> 1);
-			for (int k = 0; k < 4; ++k) st[k][l] = iv[k];
+			for (int k = 0; k < 4; ++k) st[k][l] = md5_iv[k];
 		}
 		md5x16_blocks(st, pa, na);
 		md5x16_blocks(st, pb, nb);
 		for (int l = 0; l < n; ++l) {
-			md5_t m;
-			uint8_t dg[16];
-			for (int k = 0; k < 4; ++k) m.h[k] = st[k][l];
-			m.len = (uint64_t)(na + nb) * 64;
-			m.fill = 0;
-			if (nb) {
-				md5_update(&m, pb[l] + nb * 64, lb - nb * 64);
-			} else {
-				md5_update(&m, pa[l] + na * 64, la - na * 64);
-				md5_update(&m, pb[l], lb);
-			}
-			md5_final(&m, dg);
-			md5_line(dg, out[l]);
+			const uint32_t hl[4] = {st[0][l], st[1][l], st[2][l], st[3][l]};
+			lane_finish(hl, pa[l], pb[l], la, lb, na, nb, out[l]);
 		}
 		return 0;
 	}

@@ -1,5 +1,5 @@
 """FileWriterMd5 lines (reference filewrite.h:11-29, 99-105): the cropped NV12 rows of a frame, luma then
-chroma, through RFC 1321 MD5 — the scalar path and the 16-lane multi-buffer path
+chroma, through RFC 1321 MD5 — the scalar path, the stitched 2-3 frame path and the 16-lane multi-buffer path
 (m2dec_amd_frames_md5, m2dec_amd/csrc/host/md5.c) against Python's hashlib on the same bytes."""
 import ctypes
 import hashlib

@@ -13,6 +13,8 @@
 #   diff=V,STREAM    tools/replay_diff.py STREAM with build/var/lib_V.so ("base": the product library)
 #   prof             rocprofv3 --kernel-trace --stats of the default bench (decode path, replay, all legs)
 #   pmc=KERNEL       tools/gpu_pmc.sh TAG KERNEL (FETCH_SIZE / WRITE_SIZE / SQ passes)
+#   md5host          tools/md5_batch_bench.py with and without the stitched 2-3 frame kernel -> md5host_TAG.txt
+#   md5gpu[=N]       tools/_build/md5_gpu_probe N (one MD5 chain per wave / per lane on the GPU) -> md5gpu_TAG.txt
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -52,6 +54,13 @@ for step in "$@"; do
        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$TAG -o run --output-format csv -- \
          python3 $R/bench.py --no-cpu-baseline > $R/$O/prof_$TAG.log 2>&1)
       rc=$?; find $O/prof_$TAG -name "*kernel_stats*" ;;
+    md5host)
+      { for st in 1 0; do echo "M2DEC_AMD_MD5_STITCH=$st"; M2DEC_AMD_MD5_STITCH=$st timeout -k 10 120 python tools/md5_batch_bench.py || exit 1; done; } \
+        > $O/md5host_$TAG.txt 2>&1
+      rc=$?; cat $O/md5host_$TAG.txt ;;
+    md5gpu)
+      timeout -k 10 300 tools/_build/md5_gpu_probe ${arg:-64} > $O/md5gpu_$TAG.txt 2>&1
+      rc=$?; cat $O/md5gpu_$TAG.txt ;;
     pmc)
       timeout -k 10 900 bash tools/gpu_pmc.sh $TAG $arg; rc=$? ;;
     *)

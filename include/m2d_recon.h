@@ -301,6 +301,11 @@ typedef struct h265r_backend {
 	int (*submit)(void *self, const h265r_picture_t *pic);
 	int (*sync_frame)(void *self, int slot); /* the picture last submitted into `slot` is in the caller's frame */
 	void (*destroy)(void *self);
+	/* optional (H.265 ABI revision 2): a parse worker hands a parsed picture to the back end before its submit,
+	 * from any thread and concurrently with the other calls, so that copies of its records are off the serial
+	 * submission path; the same `pic` (its record buffers unchanged) is then submitted, or handed again with
+	 * discard = 1 when it never will be.  NULL: submit takes every picture as it is. */
+	int (*stage)(void *self, const h265r_picture_t *pic, int discard);
 } h265r_backend_t;
 
 #ifdef __cplusplus

@@ -543,7 +543,7 @@ class HipReplay:
 class Backend265(ctypes.Structure):
     """h265r_backend_t (include/m2d_recon.h)."""
     _fields_ = [("self", ctypes.c_void_p), ("set_frames", ctypes.c_void_p), ("submit", ctypes.c_void_p),
-                ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p)]
+                ("sync_frame", ctypes.c_void_p), ("destroy", ctypes.c_void_p), ("stage", ctypes.c_void_p)]
 
 
 def decode_h265(data: bytes, backend: Optional[Backend265] = None, device: int = 0, emptify: bool = False,

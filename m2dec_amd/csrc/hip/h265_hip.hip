@@ -34,9 +34,13 @@
 #include <string.h>
 #include <time.h>
 #include <algorithm>
+#include <mutex>
 #include <vector>
 #include "m2d_recon.h"
 #include "h265_dec.h"
+
+extern "C" void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
+enum { M2DEC_CREW_SYNC_ = 1 }; /* = M2DEC_CREW_SYNC (h264_dec.h) */
 
 #define H265_CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 #define H265_SPIN_LIMIT (1 << 22)
@@ -1391,14 +1395,34 @@ struct H265Gpu {
 	int ev_next = 0;
 	int *err = nullptr;     /* sticky error word */
 	int *err_host = nullptr; /* page-locked: the error word as of each frame's copy-out ([H265R_MAX_FRAMES]) */
+	/* record arenas: a picture's records in page-locked memory (read by k_h265_upload), filled either by a parse
+	 * worker right after its parse (stage: in parallel, off the serial submission) or by submit itself.  An arena
+	 * is reserved from its fill until its upload is queued, then free again once `used` fires. */
 	struct Arena {
 		uint8_t *host = nullptr, *dev = nullptr;
 		const uint8_t *host_dev = nullptr; /* the pinned host buffer's device address (k_h265_upload reads it) */
 		size_t size = 0;
 		hipEvent_t used = nullptr;
+		bool recorded = false; /* `used` was recorded at least once */
+		bool reserved = false; /* being filled, staged, or being submitted */
+		long last = 0;         /* submission order of its last use */
 	};
-	Arena ring[2 * NS]; /* record arenas, used in turn by every lane */
-	int ring_next = 0;
+	static const int NARENA = 48; /* > the parse pipeline's 16 staged pictures + the pictures in flight */
+	Arena pool[NARENA];
+	int npool = 0;
+	long arena_clock = 0;
+	/* pictures staged by a parse worker, found again by submit from the same record buffers */
+	struct Staged {
+		const void *tu = nullptr, *coef = nullptr;
+		int n_tu = 0, n_coef = 0, n_pu = 0, slot = -1, width = 0, height = 0;
+		int arena = -1; /* -1: entry free */
+		unsigned refs = 0;
+		long seq = 0;
+	};
+	Staged staged[32];
+	long stage_clock = 0;
+	int64_t staged_pictures = 0, staged_used = 0;
+	std::mutex amu; /* pool, staged, grave_*, max_total */
 	struct Lane {
 		uint8_t *copy = nullptr; /* the deblocked frame (SAO input) */
 		int *scratch = nullptr;  /* done flags + the block counter + CTU progress */
@@ -1423,6 +1447,7 @@ struct H265Gpu {
 	bool waves4 = true;        /* CTU kernels with two waves per plane (M2DEC_AMD_H265_WAVES=2: one) */
 	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
+	bool no_stage = false;     /* M2DEC_AMD_H265_STAGE=0: records copied by submit only (A/B) */
 };
 
 static size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -1459,10 +1484,19 @@ int h_set_frames(void *p, int n, const m2d_frame_t *frames, int width, int heigh
 		for (int k = 0; k < g->ns; ++k) H265_CHECK(hipMalloc((void **)&g->lane[k].copy, fsz));
 		H265_CHECK(hipMemset(g->frames, 0, fsz * (size_t)n));
 	}
-	for (uint8_t *p : g->grave_host) (void)hipHostFree(p);
-	for (uint8_t *p : g->grave_dev) (void)hipFree(p);
-	g->grave_host.clear();
-	g->grave_dev.clear();
+	{
+		/* (the decoder drains its parse pipeline before set_frames: nothing is staged or being staged now) */
+		std::lock_guard<std::mutex> lk(g->amu);
+		for (uint8_t *p : g->grave_host) (void)hipHostFree(p);
+		for (uint8_t *p : g->grave_dev) (void)hipFree(p);
+		g->grave_host.clear();
+		g->grave_dev.clear();
+		for (auto &e : g->staged)
+			if (e.arena >= 0) {
+				g->pool[e.arena].reserved = false;
+				e.arena = -1;
+			}
+	}
 	{
 		/* scratch words of the largest picture the frame holds: 4 x 4 luma and chroma blocks, 16 x 16 CTUs */
 		const size_t sn = (size_t)(width / 4) * (height / 4) + (size_t)(width / 8) * (height / 8) + 2 + (size_t)(height / 16 + 1) +
@@ -1502,13 +1536,13 @@ static hipEvent_t next_event(H265Gpu *g)
 	return e;
 }
 
-int h_submit(void *p, const h265r_picture_t *pic)
+/* host-side checks of what the kernels assume; refs = the frames the picture's prediction blocks read */
+static int check_picture(const H265Gpu *g, const h265r_picture_t *pic, unsigned *refs_out)
 {
-	H265Gpu *g = (H265Gpu *)p;
-	if (!g || !g->frames || pic->width != g->W || pic->height != g->H || pic->slot < 0 || pic->slot >= g->n || pic->n_tu < 0)
+	if (!g->frames || pic->width != g->W || pic->height != g->H || pic->slot < 0 || pic->slot >= g->n || pic->n_tu < 0)
 		return -1;
-	/* host-side checks of what the kernels assume: blocks inside the frame and inside one CTU, CTUs in raster
-	 * order (the CTU kernel's per-CTU record ranges and LDS tile), coefficients inside the pool */
+	/* blocks inside the frame and inside one CTU, CTUs in raster order (the CTU kernel's per-CTU record ranges and
+	 * LDS tile), coefficients inside the pool */
 	if (pic->ctb_log2 < 4 || pic->ctb_log2 > 6 || pic->pic_w > g->W || pic->pic_h > g->H) return -1;
 	for (int i = 0, last_ctu = 0; i < pic->n_tu; ++i) {
 		const h265r_tu_t &t = pic->tu[i];
@@ -1535,7 +1569,194 @@ int h_submit(void *p, const h265r_picture_t *pic)
 			if (u.ref[l] >= 0) refs |= 1u << u.ref[l];
 		}
 	}
+	*refs_out = refs;
+	return 0;
+}
+
+/* where a picture's records sit in its arena */
+struct ArenaLayout {
+	int cols, rows;
+	size_t units, nbs, o_tu, o_coef, o_map, o_bsv, o_bsh, o_sao, o_pu, o_args, total;
+};
+
+static ArenaLayout layout_of(const h265r_picture_t *pic)
+{
+	ArenaLayout L;
+	L.units = (size_t)(pic->width / 4) * (pic->height / 4) + (size_t)(pic->width / 8) * (pic->height / 8);
+	L.nbs = (size_t)(pic->height / 4) * (pic->width / 8);
+	L.cols = (pic->pic_w + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
+	L.rows = (pic->pic_h + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
+	L.o_tu = 0;
+	L.o_coef = al16(L.o_tu + sizeof(h265r_tu_t) * (size_t)pic->n_tu);
+	L.o_map = al16(L.o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
+	L.o_bsv = al16(L.o_map + sizeof(int32_t) * L.units);
+	L.o_bsh = al16(L.o_bsv + L.nbs);
+	L.o_sao = al16(L.o_bsh + L.nbs);
+	L.o_pu = al16(L.o_sao + sizeof(h265r_sao_t) * (size_t)(L.cols * L.rows));
+	/* the kernels' argument block rides in the arena (one upload from page-locked memory: a hipMemcpyAsync
+	 * from the stack is a pageable copy, which can block this thread until the stream — waiting on other
+	 * streams' pictures — reaches it) */
+	L.o_args = al16(L.o_pu + sizeof(h265r_pu_t) * (size_t)pic->n_pu);
+	L.total = al16(L.o_args + sizeof(H265Args));
+	return L;
+}
+
+static void arena_release(H265Gpu *g, int i);
+
+/* a free arena of at least `total` bytes, reserved for the caller (any thread): one whose last upload is done,
+ * else a new one, else the oldest in flight (waited for); -1 on a HIP error */
+static int arena_acquire(H265Gpu *g, size_t total)
+{
+	int pick = -1;
+	bool wait = false;
+	{
+		std::lock_guard<std::mutex> lk(g->amu);
+		int small = -1, oldest = -1;
+		for (int i = 0; i < g->npool; ++i) {
+			H265Gpu::Arena &a = g->pool[i];
+			if (a.reserved) continue;
+			if (a.recorded && hipEventQuery(a.used) != hipSuccess) {
+				if (oldest < 0 || a.last < g->pool[oldest].last) oldest = i;
+				continue;
+			}
+			if (a.size >= total) {
+				pick = i;
+				break;
+			}
+			if (small < 0) small = i;
+		}
+		if (pick < 0 && g->npool < H265Gpu::NARENA) {
+			H265Gpu::Arena &a = g->pool[g->npool];
+			if (!a.used && hipEventCreateWithFlags(&a.used, hipEventDisableTiming) != hipSuccess) return -1;
+			pick = g->npool++;
+		}
+		if (pick < 0) pick = small;
+		if (pick < 0) {
+			pick = oldest;
+			wait = true;
+		}
+		if (pick < 0) return -1; /* (every arena reserved: more staged pictures than the pipeline can hold) */
+		g->pool[pick].reserved = true;
+	}
+	H265Gpu::Arena &a = g->pool[pick];
+	if (wait && hipEventSynchronize(a.used) != hipSuccess) {
+		arena_release(g, pick);
+		return -1;
+	}
+	if (a.size < total) {
+		std::lock_guard<std::mutex> lk(g->amu);
+		if (a.host) g->grave_host.push_back(a.host);
+		if (a.dev) g->grave_dev.push_back(a.dev);
+		a.host = a.dev = nullptr;
+		a.size = 0;
+		/* at least the largest picture seen so far, with headroom: every arena soon holds an intra picture */
+		const size_t want = total > g->max_total ? total : g->max_total;
+		const size_t sz = al16(want + want / 4);
+		if (hipHostMalloc((void **)&a.host, sz, hipHostMallocDefault) != hipSuccess || hipMalloc((void **)&a.dev, sz) != hipSuccess) {
+			a.reserved = false;
+			return -1;
+		}
+		void *hd = nullptr;
+		if (hipHostGetDevicePointer(&hd, a.host, 0) != hipSuccess) {
+			a.reserved = false;
+			return -1;
+		}
+		a.host_dev = (const uint8_t *)hd;
+		a.size = sz;
+	}
+	{
+		std::lock_guard<std::mutex> lk(g->amu);
+		if (total > g->max_total) g->max_total = total;
+	}
+	return pick;
+}
+
+static void arena_release(H265Gpu *g, int i)
+{
+	std::lock_guard<std::mutex> lk(g->amu);
+	g->pool[i].reserved = false;
+}
+
+static void arena_fill(H265Gpu::Arena &a, const h265r_picture_t *pic, const ArenaLayout &L)
+{
+	memcpy(a.host + L.o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
+	memcpy(a.host + L.o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
+	memcpy(a.host + L.o_map, pic->map, sizeof(int32_t) * L.units);
+	memcpy(a.host + L.o_bsv, pic->bs_v, L.nbs);
+	memcpy(a.host + L.o_bsh, pic->bs_h, L.nbs);
+	memcpy(a.host + L.o_sao, pic->sao, sizeof(h265r_sao_t) * (size_t)(L.cols * L.rows));
+	if (pic->n_pu) memcpy(a.host + L.o_pu, pic->pu, sizeof(h265r_pu_t) * (size_t)pic->n_pu);
+}
+
+static bool staged_match(const H265Gpu::Staged &e, const h265r_picture_t *pic)
+{
+	return e.arena >= 0 && e.tu == (const void *)pic->tu && e.coef == (const void *)pic->coef && e.n_tu == pic->n_tu &&
+	       e.n_coef == pic->n_coef && e.n_pu == pic->n_pu && e.slot == pic->slot && e.width == pic->width && e.height == pic->height;
+}
+
+/* h265r_backend_t.stage: a parse worker hands over a parsed picture before its (serial, decode-order) submit:
+ * its checks and the copy of its records into a page-locked arena happen here, on the worker, in parallel with
+ * the other workers and the submissions (the round-5 intra timeline: 0.4-0.9 ms of copies per picture on the
+ * submitting thread, the eighth picture's kernels starting 4.5 ms after the parse ended).  discard = 1: the
+ * picture will not be submitted (a failed or abandoned job): its arena goes back.  A picture that cannot be
+ * staged is simply copied by submit. */
+int h_stage(void *p, const h265r_picture_t *pic, int discard)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g || !pic) return -1;
+	if (discard) {
+		std::lock_guard<std::mutex> lk(g->amu);
+		for (auto &e : g->staged)
+			if (staged_match(e, pic)) {
+				g->pool[e.arena].reserved = false;
+				e.arena = -1;
+			}
+		return 0;
+	}
+	if (g->no_stage) return 0;
+	unsigned refs = 0;
+	if (check_picture(g, pic, &refs) < 0) return 0; /* (submit checks again and refuses it) */
 	H265_CHECK(hipSetDevice(g->dev));
+	const ArenaLayout L = layout_of(pic);
+	const int ai = arena_acquire(g, L.total);
+	if (ai < 0) return 0;
+	arena_fill(g->pool[ai], pic, L);
+	std::lock_guard<std::mutex> lk(g->amu);
+	int slot = -1;
+	for (int i = 0; i < 32; ++i) {
+		H265Gpu::Staged &e = g->staged[i];
+		if (staged_match(e, pic) || (e.tu == (const void *)pic->tu && e.arena >= 0)) { /* (the same job staged again) */
+			g->pool[e.arena].reserved = false;
+			e.arena = -1;
+		}
+		if (e.arena < 0 && slot < 0) slot = i;
+	}
+	if (slot < 0) { /* (cannot happen with the pipeline's 16 jobs: the oldest entry goes) */
+		slot = 0;
+		for (int i = 1; i < 32; ++i)
+			if (g->staged[i].seq < g->staged[slot].seq) slot = i;
+		g->pool[g->staged[slot].arena].reserved = false;
+	}
+	H265Gpu::Staged &e = g->staged[slot];
+	e.tu = pic->tu;
+	e.coef = pic->coef;
+	e.n_tu = pic->n_tu;
+	e.n_coef = pic->n_coef;
+	e.n_pu = pic->n_pu;
+	e.slot = pic->slot;
+	e.width = pic->width;
+	e.height = pic->height;
+	e.refs = refs;
+	e.arena = ai;
+	e.seq = ++g->stage_clock;
+	g->staged_pictures++;
+	return 0;
+}
+
+int h_submit(void *p, const h265r_picture_t *pic)
+{
+	H265Gpu *g = (H265Gpu *)p;
+	if (!g || !pic) return -1;
 	/* M2DEC_AMD_H265_TRACE: the steps of this call that took over 0.5 ms */
 	struct timespec ts0;
 	clock_gettime(CLOCK_MONOTONIC, &ts0);
@@ -1548,6 +1769,35 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		if (t - tp > 0.5) fprintf(stderr, "h265 submit slot %d: %s %.2f ms\n", pic->slot, what, t - tp);
 		tp = t;
 	};
+	unsigned refs = 0;
+	int ai = -1;
+	{
+		std::lock_guard<std::mutex> lk(g->amu);
+		for (auto &e : g->staged)
+			if (staged_match(e, pic)) {
+				ai = e.arena;
+				refs = e.refs;
+				e.arena = -1;
+				g->staged_used++;
+				break;
+			}
+	}
+	if (ai < 0 && check_picture(g, pic, &refs) < 0) return -1;
+	H265_CHECK(hipSetDevice(g->dev));
+	const ArenaLayout L = layout_of(pic);
+	if (ai < 0) {
+		ai = arena_acquire(g, L.total);
+		if (ai < 0) return -1;
+		arena_fill(g->pool[ai], pic, L);
+	}
+	/* (the arena goes back to the pool on every return below; after its `used` event on success) */
+	struct Release {
+		H265Gpu *g;
+		int i;
+		~Release() { arena_release(g, i); }
+	} release{g, ai};
+	H265Gpu::Arena &a = g->pool[ai];
+	lap("records");
 	/* the stream: the first idle one after the last, else round robin */
 	int k = g->rr;
 	for (int i = 0; i < g->ns; ++i) {
@@ -1560,57 +1810,14 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	g->rr = (k + 1) % g->ns;
 	hipStream_t s = g->st[k];
 	H265Gpu::Lane &ln = g->lane[k];
-	const size_t units = (size_t)(g->W / 4) * (g->H / 4) + (size_t)(g->W / 8) * (g->H / 8);
-	const size_t nbs = (size_t)(g->H / 4) * (g->W / 8);
-	const int cols = (pic->pic_w + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2, rows = (pic->pic_h + (1 << pic->ctb_log2) - 1) >> pic->ctb_log2;
-	const size_t o_tu = 0, o_coef = al16(o_tu + sizeof(h265r_tu_t) * (size_t)pic->n_tu);
-	const size_t o_map = al16(o_coef + sizeof(int16_t) * (size_t)pic->n_coef);
-	const size_t o_bsv = al16(o_map + sizeof(int32_t) * units), o_bsh = al16(o_bsv + nbs);
-	const size_t o_sao = al16(o_bsh + nbs), o_pu = al16(o_sao + sizeof(h265r_sao_t) * (size_t)(cols * rows));
-	/* the kernels' argument block rides in the arena (one upload from page-locked memory: a hipMemcpyAsync
-	 * from the stack is a pageable copy, which can block this thread until the stream — waiting on other
-	 * streams' pictures — reaches it) */
-	const size_t o_args = al16(o_pu + sizeof(h265r_pu_t) * (size_t)pic->n_pu);
-	const size_t total = al16(o_args + sizeof(H265Args));
+	const int cols = L.cols, rows = L.rows;
+	const size_t o_tu = L.o_tu, o_coef = L.o_coef, o_map = L.o_map, o_bsv = L.o_bsv, o_bsh = L.o_bsh, o_sao = L.o_sao,
+	             o_pu = L.o_pu, o_args = L.o_args, total = L.total;
 	/* per-block done flags + 2 counters, then the CTU rows' progress words, the CTUs' first records and the CTUs'
 	 * done flags (sized for the frame at set_frames: a block is at least 4 x 4) */
 	const int nctu = cols * rows;
 	const size_t sn = (size_t)pic->n_tu + 2 + (size_t)rows + 2 * (size_t)nctu + 1;
 	if (sn > ln.scratch_n) return -1;
-	/* the lane's arena: free once its last picture's upload and kernels are done (its own event: no wait on
-	 * the dependencies below); a larger one replaces it with headroom, the old one freed at the next
-	 * set_frames / destroy (hipFree waits for the whole device) */
-	/* the arenas are one ring for all lanes (each is reused every 2 NS pictures, so all of them soon hold the
-	 * largest picture's size and none is reallocated while decoding) */
-	H265Gpu::Arena &a = g->ring[g->ring_next];
-	g->ring_next = (g->ring_next + 1) % (2 * H265Gpu::NS);
-	lap("stream pick");
-	H265_CHECK(hipEventSynchronize(a.used));
-	lap("arena free");
-	if (a.size < total) {
-		if (a.host) g->grave_host.push_back(a.host);
-		if (a.dev) g->grave_dev.push_back(a.dev);
-		a.host = a.dev = nullptr;
-		a.size = 0;
-		/* at least the largest picture seen so far, with headroom: every arena soon holds an intra picture */
-		const size_t want = total > g->max_total ? total : g->max_total;
-		const size_t sz = al16(want + want / 4);
-		H265_CHECK(hipHostMalloc((void **)&a.host, sz, hipHostMallocDefault));
-		H265_CHECK(hipMalloc((void **)&a.dev, sz));
-		void *hd = nullptr;
-		H265_CHECK(hipHostGetDevicePointer(&hd, a.host, 0));
-		a.host_dev = (const uint8_t *)hd;
-		a.size = sz;
-	}
-	if (total > g->max_total) g->max_total = total;
-	lap("arena alloc");
-	memcpy(a.host + o_tu, pic->tu, sizeof(h265r_tu_t) * (size_t)pic->n_tu);
-	memcpy(a.host + o_coef, pic->coef, sizeof(int16_t) * (size_t)pic->n_coef);
-	memcpy(a.host + o_map, pic->map, sizeof(int32_t) * units);
-	memcpy(a.host + o_bsv, pic->bs_v, nbs);
-	memcpy(a.host + o_bsh, pic->bs_h, nbs);
-	memcpy(a.host + o_sao, pic->sao, sizeof(h265r_sao_t) * (size_t)(cols * rows));
-	if (pic->n_pu) memcpy(a.host + o_pu, pic->pu, sizeof(h265r_pu_t) * (size_t)pic->n_pu);
 	H265Args h;
 	h.tu = (const h265r_tu_t *)(a.dev + o_tu);
 	h.coef = (const int16_t *)(a.dev + o_coef);
@@ -1710,6 +1917,11 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	H265_CHECK(hipEventRecord(tm.t1, s));
 	tm.pending = true;
 	H265_CHECK(hipEventRecord(a.used, s));
+	{
+		std::lock_guard<std::mutex> lk(g->amu);
+		a.recorded = true;
+		a.last = ++g->arena_clock;
+	}
 	/* this picture's kernels: what later readers of its frame wait for, and what the next writers of its
 	 * references' frames wait for */
 	hipEvent_t kd = next_event(g);
@@ -1763,8 +1975,11 @@ int h_sync(void *p, int slot)
 		}
 	}
 	const size_t ls = (size_t)g->W * g->H;
-	memcpy(g->caller[slot].luma, g->stg[slot], ls);
-	memcpy(g->caller[slot].chroma, g->stg[slot] + ls, ls / 2);
+	/* (the sync crew, parcopy.c: a 3.1 MB frame over several cores, as the H.264 back end's be_sync) */
+	void *to[2] = {g->caller[slot].luma, g->caller[slot].chroma};
+	const void *from[2] = {g->stg[slot], g->stg[slot] + ls};
+	const size_t len[2] = {ls, ls / 2};
+	m2dec_par_memcpy(M2DEC_CREW_SYNC_, 2, to, from, len);
 	g->pend[slot] = false;
 	return 0;
 }
@@ -1775,7 +1990,7 @@ void h_destroy(void *p)
 	if (!g) return;
 	(void)hipSetDevice(g->dev);
 	(void)sync_all(g);
-	for (auto &a : g->ring) {
+	for (auto &a : g->pool) {
 		if (a.host) (void)hipHostFree(a.host);
 		if (a.dev) (void)hipFree(a.dev);
 		if (a.used) (void)hipEventDestroy(a.used);
@@ -1822,6 +2037,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_KCOPY")) g->kcopy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_KCOPY_D2H")) g->kcopy_d2h = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_ERR_ASYNC")) g->err_async = atoi(e) != 0;
+	if (const char *e = getenv("M2DEC_AMD_H265_STAGE")) g->no_stage = atoi(e) == 0;
 	{
 		const char *q = getenv("GPU_MAX_HW_QUEUES");
 		g->ns = q && atoi(q) >= 8 ? 8 : 4;
@@ -1841,7 +2057,6 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 		(void)hipEventCreate(&t.t0);
 		(void)hipEventCreate(&t.t1);
 	}
-	for (auto &a : g->ring) (void)hipEventCreateWithFlags(&a.used, hipEventDisableTiming);
 	if (hipMalloc((void **)&g->err, sizeof(int)) != hipSuccess || hipMemset(g->err, 0, sizeof(int)) != hipSuccess ||
 	    hipHostMalloc((void **)&g->err_host, sizeof(int) * H265R_MAX_FRAMES, hipHostMallocDefault) != hipSuccess) {
 		h_destroy(g);
@@ -1853,6 +2068,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	out->submit = h_submit;
 	out->sync_frame = h_sync;
 	out->destroy = h_destroy;
+	out->stage = h_stage;
 	return 0;
 }
 

@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include "m2dec_amd.h"
+#include "h264_dec.h"
+#include "h265_dec.h"
 
 #define MAX_HDR 256
 
@@ -32,6 +34,7 @@ typedef struct {
 	uint8_t *second;
 	size_t second_len;
 	int failed;
+	m2dec_hold_t *hold; /* H.265: frames the caller still reads after get (m2dec_amd_decode_h265_held) */
 } drv_t;
 
 static int reread(void *arg)
@@ -57,6 +60,7 @@ static int reread(void *arg)
 
 static void frames_free(drv_t *v)
 {
+	if (v->hold) m2dec_hold_wait_idle(v->hold); /* (nobody reads the frames any more) */
 	for (int i = 0; i < v->nframes; ++i) {
 		free(v->mem[i][0]);
 		free(v->mem[i][1]);
@@ -176,24 +180,37 @@ static int decode_core(const m2d_func_table_t *func, int h264, const uint8_t *da
                        void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
 
 static int decode_core265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
-                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error);
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_hold_t *hold,
+                          int *last_error);
 
 /* H.265 through h265d_func (M2Decoder with MODE_H265, m2decoder.h:180-182): the back end `be` (borrowed;
  * NULL: the gfx950 one on `device`) */
 int m2dec_amd_decode_h265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
                           void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
 {
-	return decode_core265(data, len, be, device, emptify, on_frame, arg, last_error);
+	return decode_core265(data, len, be, device, emptify, on_frame, arg, NULL, last_error);
+}
+
+/* the same with `hold`: on_frame may keep reading a frame after it returns until it releases it from `hold`;
+ * the decoder does not write that frame (sync_frame waits) nor frees it meanwhile.  Only for a back end that
+ * writes the caller's frames inside sync_frame alone (the gfx950 one: NULL, or one with `stage`) */
+int m2dec_amd_decode_h265_held(const uint8_t *data, size_t len, const h265r_backend_t *be, int device,
+                               void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_hold_t *hold,
+                               int *last_error)
+{
+	return decode_core265(data, len, be, device, 0, on_frame, arg, hold, last_error);
 }
 
 static int decode_loop(drv_t *v, int emptify, void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg);
 
 static int decode_core265(const uint8_t *data, size_t len, const h265r_backend_t *be, int device, int emptify,
-                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, int *last_error)
+                          void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, m2dec_hold_t *hold,
+                          int *last_error)
 {
 	drv_t v;
 	int err;
 	memset(&v, 0, sizeof(v));
+	v.hold = hold;
 	v.func = h265d_func;
 	v.h265 = 1;
 	v.data = data;
@@ -203,6 +220,7 @@ static int decode_core265(const uint8_t *data, size_t len, const h265r_backend_t
 	h265d_func->init(v.ctx, -1, header_cb, &v);
 	if (be) m2dec_amd_h265_set_backend(v.ctx, be);
 	else m2dec_amd_h265_set_device(v.ctx, device);
+	h265_set_hold(v.ctx, hold);
 	dec_bits_set_callback(h265d_func->stream_pos(v.ctx), reread, &v);
 	err = decode_loop(&v, emptify, on_frame, arg);
 	if (last_error) *last_error = err;

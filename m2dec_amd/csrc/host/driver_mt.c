@@ -20,6 +20,7 @@
 #include <time.h>
 #include <unistd.h>
 #include "h264_dec.h"
+#include "h265_dec.h"
 #include "m2dec_amd.h"
 
 /* M2DEC_AMD_THREAD_CPU=1: a driver thread prints its CPU time when it ends (tools/thread_cpu.py reads it: an
@@ -337,6 +338,14 @@ typedef struct {
 	int failed;
 } h265_md5_t;
 
+/* the gfx950 H.265 back end writes the caller's frames only inside sync_frame, which waits for their holds:
+ * the frame is hashed in place (m2dec_amd_decode_h265_held) */
+static void h265_md5_in_place(void *arg, const m2d_frame_t *f)
+{
+	h265_md5_t *h = (h265_md5_t *)arg;
+	md5_on_frame(h->s, f);
+}
+
 static void h265_md5_on_frame(void *arg, const m2d_frame_t *f)
 {
 	h265_md5_t *h = (h265_md5_t *)arg;
@@ -360,8 +369,12 @@ static void h265_md5_on_frame(void *arg, const m2d_frame_t *f)
 	pthread_mutex_lock(&h->s->hold.mu); /* the buffer's previous frame is hashed */
 	while (m2dec_hold_busy(&h->s->hold, b)) pthread_cond_wait(&h->s->hold.cv, &h->s->hold.mu);
 	pthread_mutex_unlock(&h->s->hold.mu);
-	memcpy(b, f->luma, ls);
-	memcpy(b + ls, f->chroma, ls / 2);
+	{
+		void *to[2] = {b, b + ls};
+		const void *from[2] = {f->luma, f->chroma};
+		const size_t len[2] = {ls, ls / 2};
+		m2dec_par_memcpy(M2DEC_CREW_SYNC, 2, to, from, len); /* (parcopy.c) */
+	}
 	{
 		m2d_frame_t c = *f;
 		c.luma = b;
@@ -386,7 +399,10 @@ static int copy_md5(int codec, const uint8_t *data, size_t len, const h265r_back
 	m2dec_hold_init(&s.hold);
 	memset(&h, 0, sizeof(h));
 	h.s = &s;
-	if (codec == 265) r = m2dec_amd_decode_h265(data, len, be, device, 0, h265_md5_on_frame, &h, &err);
+	const char *ip = getenv("M2DEC_AMD_H265_MD5_IN_PLACE"); /* (A/B: 0 = copy every frame first) */
+	if (codec == 265 && (!be || be->stage) && !(ip && atoi(ip) == 0))
+		r = m2dec_amd_decode_h265_held(data, len, be, device, h265_md5_in_place, &h, &s.hold, &err);
+	else if (codec == 265) r = m2dec_amd_decode_h265(data, len, be, device, 0, h265_md5_on_frame, &h, &err);
 	else r = m2dec_amd_decode_m2v(data, len, device, 0, h265_md5_on_frame, &h, &err);
 	md5_on_end(&s);
 	m2dec_hold_wait_idle(&s.hold); /* every queued MD5 is written */

@@ -2053,6 +2053,7 @@ static void find_empty_frame(h265_dec_t *d)
 		}
 	d->lru[max_idx] = 0;
 	d->index = max_idx;
+	d->fresh[max_idx] = 1;
 }
 
 static long pipe_last_seq(const h265_dec_t *d);
@@ -2261,6 +2262,7 @@ static void pipe_submit_locked(h265_pipe_t *P)
 		/* (nothing after a failed picture reaches the back end: the sequential path never decodes it, so the frames
 		 * it would overwrite keep their content for the output that follows) */
 		if (!j->err && P->have_be && j->seq < P->fail_seq) r = P->be.submit(P->be.self, &j->w->pic);
+		else if (P->have_be && P->be.stage) P->be.stage(P->be.self, &j->w->pic, 1); /* (its staged arena back) */
 		if (tr) fprintf(stderr, "h265 job %ld submitted %.3f\n", j->seq, h265_now());
 		pthread_mutex_lock(&P->mu);
 		if (r < 0) { /* a slice-data error on a worker (j->err) or a refused submission */
@@ -2316,6 +2318,9 @@ static void *pipe_worker(void *arg)
 		m2d_place_self(); /* (numa.c) */
 		if (getenv("M2DEC_AMD_H265_TRACE")) fprintf(stderr, "h265 job %ld start %.3f\n", j->seq, h265_now());
 		job_run(P, j);
+		/* the records into the back end's page-locked arena here, in parallel, rather than on the serial
+		 * submission (h265r_backend_t.stage) */
+		if (!j->err && P->have_be && P->be.stage) P->be.stage(P->be.self, &j->w->pic, 0);
 		if (getenv("M2DEC_AMD_H265_TRACE")) fprintf(stderr, "h265 job %ld end %.3f\n", j->seq, h265_now());
 		pthread_mutex_lock(&P->mu);
 		j->state = JOB_PARSED;
@@ -2704,7 +2709,18 @@ static int api_peek(void *ctx, m2d_frame_t *frame, int bypass)
 		if (idx < 0) return 0;
 		(void)pipe_wait_frame(d, idx);
 	}
+	if (d->hold && idx < 16 && d->fresh[idx]) { /* the frame's previous content is still read by the caller (driver_mt.c: its MD5) */
+		pthread_mutex_lock(&d->hold->mu);
+		while (m2dec_hold_busy(d->hold, d->frames[idx].luma)) {
+			d->hold->waits++;
+			pthread_cond_wait(&d->hold->cv, &d->hold->mu);
+		}
+		pthread_mutex_unlock(&d->hold->mu);
+	}
+	m2d_tl('Y', idx, 0);
 	if (d->have_be && d->be.sync_frame(d->be.self, idx) < 0) return -1;
+	if (idx < 16) d->fresh[idx] = 0;
+	m2d_tl('y', idx, 0);
 	*frame = d->frames[idx];
 	return 1;
 }
@@ -2730,6 +2746,12 @@ static const m2d_func_table_t h265d_func_ = {
 const m2d_func_table_t *const h265d_func = &h265d_func_;
 
 /* ------------------------------------------------------------------ extra C ABI */
+void h265_set_hold(void *ctx, struct m2dec_hold *hold)
+{
+	h265_dec_t *d = CTX(ctx);
+	if (d) d->hold = hold;
+}
+
 int m2dec_amd_h265_set_backend(void *ctx, const h265r_backend_t *be)
 {
 	h265_dec_t *d = CTX(ctx);

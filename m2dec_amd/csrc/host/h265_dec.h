@@ -185,7 +185,17 @@ typedef struct h265_dec {
 	/* parse-ahead pipeline (h265_dec.c "parse-ahead"): heap state, never caller memory; NULL = sequential */
 	struct h265_pipe *pipe;
 	int threads;              /* parse workers: -1 default (M2DEC_AMD_H265_THREADS, 8), 0 sequential */
+	struct m2dec_hold *hold;  /* frames the caller reads after get (h264_dec.h m2dec_hold_t; NULL none): a
+	                             sync_frame into such a frame waits for its release */
+	uint8_t fresh[16];        /* frames given a new picture since their last sync_frame (only those are written) */
 } h265_dec_t;
+
+/* the caller's held frames (the MD5 driver hashing them in place; NULL: none) */
+void h265_set_hold(void *ctx, struct m2dec_hold *hold);
+/* driver.c: m2dec_amd_decode_h265 with held frames (driver_mt.c, the MD5 driver hashing in place) */
+int m2dec_amd_decode_h265_held(const uint8_t *data, size_t len, const h265r_backend_t *be, int device,
+                               void (*on_frame)(void *arg, const m2d_frame_t *f), void *arg, struct m2dec_hold *hold,
+                               int *last_error);
 
 /* default back end: the gfx950 reconstruction (m2dec_amd/csrc/hip/h265_hip.hip) */
 int h265_hip_backend_create(h265r_backend_t *out, int device);

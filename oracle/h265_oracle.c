@@ -619,5 +619,6 @@ int h265_oracle_backend_create(h265r_backend_t *out)
 	out->submit = o_submit;
 	out->sync_frame = o_sync;
 	out->destroy = o_destroy;
+	out->stage = NULL;
 	return 0;
 }

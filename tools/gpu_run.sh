@@ -5,7 +5,7 @@
 #   bash tools/gpu_run.sh TAG STEP [STEP ...]
 #
 # steps (outputs under gpurun_out/, named with TAG):
-#   tests            pytest -m gpu (thread timeouts, one process)       -> pytest_TAG.log
+#   tests[=KEXPR]    pytest -m gpu (thread timeouts, one process; -k KEXPR) -> pytest_TAG.log
 #   smoke            __graft_entry__.smoke()
 #   bench[=ARGS]     python bench.py ARGS (default: the driver's line)   -> bench_TAG.json / .err
 #   bench20          the driver's own command line (--steps 20 --warmup 5)
@@ -13,6 +13,8 @@
 #   diff=V,STREAM    tools/replay_diff.py STREAM with build/var/lib_V.so ("base": the product library)
 #   prof             rocprofv3 --kernel-trace --stats of the default bench (decode path, replay, all legs)
 #   pmc=KERNEL       tools/gpu_pmc.sh TAG KERNEL (FETCH_SIZE / WRITE_SIZE / SQ passes)
+#   h265ab=R,VAR,A,B interleaved A/B of VAR=A / VAR=B on the bench's two H.265 legs (R rounds)  -> h265ab_TAG.txt
+#   h265tl=N,STREAM  tools/h265_timeline.sh (rocprof kernel trace + parse jobs of N decodes)   -> h5tl_TAG.txt
 #   md5host          tools/md5_batch_bench.py with and without the stitched 2-3 frame kernel -> md5host_TAG.txt
 #   md5gpu[=N]       tools/_build/md5_gpu_probe N (one MD5 chain per wave / per lane on the GPU) -> md5gpu_TAG.txt
 set -o pipefail
@@ -28,7 +30,7 @@ for step in "$@"; do
   echo "== $name $arg ($(date +%T))"
   case $name in
     tests)
-      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${arg:+-k "$arg"} \
         > $O/pytest_$TAG.log 2>&1
       rc=$?; tail -3 $O/pytest_$TAG.log ;;
     smoke)
@@ -54,6 +56,17 @@ for step in "$@"; do
        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof_$TAG -o run --output-format csv -- \
          python3 $R/bench.py --no-cpu-baseline > $R/$O/prof_$TAG.log 2>&1)
       rc=$?; find $O/prof_$TAG -name "*kernel_stats*" ;;
+    h265ab)
+      IFS=',' read -r rounds var va vb <<< "$arg"
+      for ((i = 0; i < rounds; i++)); do
+        for v in $va $vb; do
+          echo "$var=$v $(env $var=$v timeout -k 10 300 python tools/h265_bench.py 10)" >> $O/h265ab_$TAG.txt || exit 1
+        done
+      done
+      rc=$?; python3 tools/h265_ab_summary.py $O/h265ab_$TAG.txt ;;
+    h265tl)
+      IFS=',' read -r n st <<< "$arg"
+      timeout -k 10 400 bash tools/h265_timeline.sh $TAG ${n:-4} ${st:-c_h265_1080p_s1}; rc=$? ;;
     md5host)
       { for st in 1 0; do echo "M2DEC_AMD_MD5_STITCH=$st"; M2DEC_AMD_MD5_STITCH=$st timeout -k 10 120 python tools/md5_batch_bench.py || exit 1; done; } \
         > $O/md5host_$TAG.txt 2>&1

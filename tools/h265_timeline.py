@@ -35,3 +35,15 @@ for r in (csv.DictReader(open(f[0])) if f else []):
 print("\nkernel                      queue   start ..   end   (us)")
 for a, b, nm, q in sorted(kern):
     print(f"{nm:26s} {q:>6s} {a:7.2f} .. {b:7.2f} ({(b - a) * 1e3:7.1f})")
+
+# host events (timeline.c) of the same decode: frames handed to the writer (O), sync_frame (Y/y), MD5 batches (H/h)
+tl = os.path.join(d, "host_tl.csv")
+if os.path.exists(tl):
+    ev = []
+    for r in csv.DictReader(open(tl)):
+        t = int(r["t_ns"]) / 1e6
+        if t0 <= t <= t1:
+            ev.append((t - t0, r["kind"], int(r["a"]), int(r["b"])))
+    ev.sort()
+    print("\nhost events (ms): O frame out (a = index), Y/y sync_frame (a = slot), H/h MD5 batch (a = frames, b = first)")
+    print("  " + "  ".join(f"{k}{a}/{b}@{t:.2f}" for t, k, a, b in ev if k in "OYyHh"))

@@ -7,6 +7,8 @@ import sys
 import time
 
 os.environ["M2DEC_AMD_H265_TRACE"] = "1"
+if len(sys.argv) > 3:  # the host event timeline (timeline.c: frames out, MD5 batches, sync_frame) to this CSV
+    os.environ["M2DEC_AMD_TIMELINE"] = sys.argv[3]
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 import m2dec_amd  # noqa: E402

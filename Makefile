@@ -14,7 +14,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -g -fPIC -std=c++17 $(INC) -Wno-unused-re
 HOST_SRC := $(wildcard m2dec_amd/csrc/host/*.c)
 HOST_OBJ := $(patsubst m2dec_amd/csrc/host/%.c,build/host/%.o,$(HOST_SRC))
 HIP_SRC := m2dec_amd/csrc/hip/recon_hip.hip
-HIP_HDR := m2dec_amd/csrc/hip/selftest_data.h m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h m2dec_amd/csrc/host/h265_dec.h
+HIP_HDR := m2dec_amd/csrc/hip/h265_mfma.h m2dec_amd/csrc/hip/selftest_data.h m2dec_amd/csrc/hip/recon_kernels.h m2dec_amd/csrc/hip/recon_internal.h m2dec_amd/csrc/host/h265_dec.h
 HIP_OBJ := build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/hip/h265_hip.o
 
 LIB := m2dec_amd/lib/libm2dec_amd.so
@@ -78,11 +78,11 @@ $(DBG_LIB): $(HOST_OBJ) $(HIP_SRC) $(HIP_HDR) build/hip/runtime.o build/hip/m2v_
 stamps: $(DBG_LIB)
 
 # H.265 CTU kernel stamps (tools/stamps_h265.py)
-H5S_LIB := build/dbg/libm2dec_amd_h5stamps.so
+H5S_LIB := build/h5s/libm2dec_amd_h5stamps.so
 $(H5S_LIB): $(HOST_OBJ) m2dec_amd/csrc/hip/h265_hip.hip $(HIP_HDR) build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -DH265_STAMPS -c m2dec_amd/csrc/hip/h265_hip.hip -o build/dbg/h265_hip_stamps.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/dbg/h265_hip_stamps.o -Wl,--no-undefined
+	$(HIPCC) $(HIPFLAGS) -DH265_STAMPS -c m2dec_amd/csrc/hip/h265_hip.hip -o build/h5s/h265_hip_stamps.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HOST_OBJ) build/hip/recon_hip.o build/hip/runtime.o build/hip/m2v_hip.o build/h5s/h265_hip_stamps.o -Wl,--no-undefined
 
 h5stamps: $(H5S_LIB)
 

@@ -38,6 +38,7 @@
 #include <vector>
 #include "m2d_recon.h"
 #include "h265_dec.h"
+#include "h265_mfma.h"
 
 extern "C" void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *const *src, const size_t *len);
 enum { M2DEC_CREW_SYNC_ = 1 }; /* = M2DEC_CREW_SYNC (h264_dec.h) */
@@ -89,7 +90,15 @@ __device__ __forceinline__ void h5st(int kind, int row, int col, int aux)
 	}
 }
 #define H5ST(lane, ...) do { if ((lane) == 0) h5st(__VA_ARGS__); } while (0)
+/* block phases (kind 5, H265_STAMPS_PHASES: heavy, ~0.3 us per stamp): per workgroup and wave, phase 0 = the block
+ * starts, 1 its residual, 4 its neighbours done, 2 its reference samples, 3 its end; aux = phase << 8 | plane << 3 | log2 */
+#ifdef H265_STAMPS_PHASES
+#define H5PH(lane, t, ph) H5ST(lane, 5, __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6, blockIdx.x & 255, ((ph) << 8) | ((t).plane << 3) | (t).log2)
 #else
+#define H5PH(lane, t, ph) do { } while (0)
+#endif
+#else
+#define H5PH(lane, t, ph) do { } while (0)
 #define H5ST(lane, ...) do { } while (0)
 #endif
 
@@ -132,6 +141,66 @@ struct Lds {
 	                           * 0..255: clamp(sat16(x)) == clamp(x)); the CTU kernels' small blocks: the residual.
 	                           * int16 keeps a wave's LDS at ~11 KB: the 4-wave CTU kernels fit two per CU */
 };
+
+/* wave-private LDS of the CTU kernels' blocks: only the reference samples — the transforms stay in registers
+ * (4 x 4 / 8 x 8: cross-lane DPP / swizzle, small_block; 16 x 16 / 32 x 32: the matrix cores, big_block) */
+struct LdsCtu {
+	int16_t seq[2][132]; /* reference samples per component: [0 .. 4n] substitution order, filtered */
+};
+/* per workgroup, read by all its waves: the 32-point DCT matrix and the MFMA lane fragments (h265_mfma.h) */
+struct CtuConst {
+	int16_t mat32[32 * 32];
+	int16_t dst4[16], dct4[16]; /* M[j][n] = m[j * 4 + n] */
+	h265mfma::Tabs tb;
+};
+__device__ __forceinline__ void ctu_const_init(CtuConst &k, int tid, int nt)
+{
+	for (int i = tid; i < 32 * 32; i += nt) k.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+	if (tid < 16) {
+		k.dst4[tid] = (int16_t)c_dst[tid];
+		k.dct4[tid] = (int16_t)dct32_coef((tid >> 2) << 3, tid & 3);
+	}
+	h265mfma::tabs_init(k.tb, tid, nt);
+}
+
+/* 4 x 4 inverse DST / DCT in registers: lane y 4 + x (lanes 0..15; the others compute a copy) holds r[y][x].
+ * Pass 1 reads its column of coefficients; pass 2 takes row y of the first-stage output from the lanes of its quad
+ * (DPP quad_perm broadcasts, no LDS).  m[j * 4 + n] = M[j][n]. */
+__device__ __forceinline__ int tr4_regs(const int16_t *d, const int16_t *m, int lane)
+{
+	const int x = lane & 3, y = (lane >> 2) & 3;
+	int e = 0;
+#pragma unroll
+	for (int j = 0; j < 4; ++j) e += m[j * 4 + y] * d[j * 4 + x];
+	const int g = sat16((e + 64) >> 7);
+	const int g0 = __builtin_amdgcn_mov_dpp(g, 0x00, 0xf, 0xf, false), g1 = __builtin_amdgcn_mov_dpp(g, 0x55, 0xf, 0xf, false);
+	const int g2 = __builtin_amdgcn_mov_dpp(g, 0xaa, 0xf, 0xf, false), g3 = __builtin_amdgcn_mov_dpp(g, 0xff, 0xf, 0xf, false);
+	return sat16((m[x] * g0 + m[4 + x] * g1 + m[8 + x] * g2 + m[12 + x] * g3 + 2048) >> 12);
+}
+
+/* 8 x 8 inverse DCT in registers: lane y 8 + x holds r[y][x]; pass 2 takes row y of the first-stage output from the 8
+ * lanes of its group (ds_swizzle bit mode: lane (l & 0x18) | j within each 32, no memory access) */
+__device__ __forceinline__ int tr8_regs(const int16_t *d, const int16_t *mat32, int lane)
+{
+	const int x = lane & 7, y = lane >> 3;
+	int e = 0;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) e += mat32[(j << 2) * 32 + y] * d[j * 8 + x];
+	const int g = sat16((e + 64) >> 7);
+	int gr[8];
+	gr[0] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (0 << 5));
+	gr[1] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (1 << 5));
+	gr[2] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (2 << 5));
+	gr[3] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (3 << 5));
+	gr[4] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (4 << 5));
+	gr[5] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (5 << 5));
+	gr[6] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (6 << 5));
+	gr[7] = __builtin_amdgcn_ds_swizzle(g, 0x18 | (7 << 5));
+	int f = 0;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) f += mat32[(j << 2) * 32 + x] * gr[j];
+	return sat16((f + 2048) >> 12);
+}
 
 __device__ __forceinline__ uint8_t *plane_px(const H265Args &a, int plane, int comp, int x, int y)
 {
@@ -490,199 +559,333 @@ __device__ __forceinline__ h265r_tu_t uniform_tu(const h265r_tu_t &r)
 	return t;
 }
 
-/* One block of a CTU kernel (wave-wide), the same integers as do_block in fewer wave-serial phases (round-5
- * stamps: a 4x4 block cost ~2 us of phase latency, the CTU's ~25 luma blocks one after another):
- *   1. the residual first, into s.pred (it does not depend on the prediction): full / DST transforms;
- *      DC-only and transform-skip are added per sample in phase 3;
- *   2. reference samples gathered AND filtered in one pass (each lane reads the up to three unfiltered
- *      neighbours it needs straight from the tile), both chroma components side by side;
- *   3. prediction + residual, clipped and stored straight into the tile, one sample per lane.
- * For 4 x 4 and 8 x 8 blocks (the many): 16 x 16 and 32 x 32 go through do_block.
- * An inter block (no prediction) adds its residual to the motion-compensated tile samples in place, or does
- * nothing without one. */
-__device__ void do_block_ctu(const H265Args &a, const h265r_tu_t &rec, CtuTile &tl, Lds &s, int lane, int x0, int y0,
-                             const int16_t *cbase, uint32_t clo)
+/* 16 x 16 and 32 x 32 blocks of the CTU kernels (N; chroma: 16 x 16 CbCr pairs), sample-parallel in the matrix
+ * cores' accumulator layout: lane l owns the samples (h265mfma::acc_row<N>(i, l), acc_col<N>(l)), i < N N / 64, of
+ * each component.  The residual of a full transform comes out of h265mfma::idct in exactly those registers (int8
+ * MFMAs, bit-exact), so the prediction, the residual add, the clip and the tile store of a sample happen in one
+ * lane with no LDS round trip between them; only the reference samples go through LDS, gathered and filtered in
+ * one pass (as do_block_ctu's phase 2).  The loops have compile-time trip counts: a lane's samples issue their
+ * LDS reads together instead of one dependent round trip per 64 samples (r124 stamps: a 32 x 32 intra block with
+ * a residual 13.6 us, of which ~7.7 us the two butterfly passes on one wave). */
+/* LDS byte offset (from the tile's start) of sample (dx, dy) relative to the CTU's origin, dy = -1 the row above,
+ * dx = -1 the column left (chroma: CbCr pairs, component comp); selects, not branches, so that a lane's reads of
+ * several samples issue together */
+__device__ __forceinline__ int tile_off(bool luma, int comp, int dx, int dy)
 {
-	const h265r_tu_t t = uniform_tu(rec);
-	if (t.log2 >= 4) {
-		/* 16 x 16 and 32 x 32: do_block's phases (its gathered reference row and packed stores measured faster for
-		 * them, r124 stamps: 32 x 32 with a residual 13.5 us vs 16.4) */
-		do_block(a, t, s, lane, CtuSamples{tl, x0, y0}, cbase, clo);
-		return;
-	}
-	const int n = 1 << t.log2, log2 = t.log2, n2 = n * n;
-	const bool luma = t.plane == 0;
-	const int ncomp = luma ? 1 : 2;
-	const int bx = luma ? t.x - x0 : t.x - (x0 >> 1), by = luma ? t.y - y0 : t.y - (y0 >> 1);
-	const CtuSamples src{tl, x0, y0};
-	/* ---- 1. transforms into s.pred[c] (residual only) */
-	int dcv[2] = {0, 0};
-	bool any_res = false;
-	for (int c = 0; c < ncomp; ++c) {
-		const int kind = t.res[c];
-		if (kind == H265R_RES_NONE) continue;
-		any_res = true;
-		const int16_t *d = cbase + (t.coef[c] - clo);
-		if (kind == H265R_RES_DC) {
-			dcv[c] = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
-			continue;
-		}
-		if (kind == H265R_RES_SKIP) continue; /* (per sample in phase 3) */
-		int16_t *res = s.pred[c];
-		for (int i = lane; i < n2; i += 64) s.t0[i] = d[i];
-		const bool dstm = kind == H265R_RES_DST;
-		if (!dstm && n >= 8) {
-			wsync();
-			if (n == 8) idct_block<8, false>(s.t0, s.mat, res, s.mat32, lane);
-			else if (n == 16) idct_block<16, false>(s.t0, s.mat, res, s.mat32, lane);
-			else idct_block<32, false>(s.t0, s.mat, res, s.mat32, lane);
-			continue;
-		}
-		for (int i = lane; i < n2; i += 64) {
-			const int k = i >> log2, sm = i & (n - 1);
-			s.mat[i] = dstm ? c_dst[k * 4 + sm] : s.mat32[(k << (5 - log2)) * 32 + sm];
-		}
-		wsync();
-		int g[16];
-		for (int r = 0, i = lane; i < n2; i += 64, ++r) {
-			const int x = i & (n - 1), y = i >> log2;
-			int e = 0;
-			for (int j = 0; j < n; ++j) e += s.mat[j * n + y] * s.t0[j * n + x];
-			g[r] = sat16((e + 64) >> 7);
-		}
-		wsync();
-		for (int r = 0, i = lane; i < n2; i += 64, ++r) s.t0[i] = g[r];
-		wsync();
-		for (int i = lane; i < n2; i += 64) {
-			const int x = i & (n - 1), y = i >> log2;
-			int e = 0;
-			for (int j = 0; j < n; ++j) e += s.mat[j * n + x] * s.t0[y * n + j];
-			res[i] = sat16((e + 2048) >> 12);
-		}
-		wsync();
-	}
-	auto resid = [&](int c, int i) -> int {
-		const int kind = t.res[c];
-		if (kind == H265R_RES_NONE) return 0;
-		if (kind == H265R_RES_DC) return dcv[c];
-		if (kind == H265R_RES_SKIP) return (cbase[t.coef[c] - clo + i] + 16) >> 5;
-		return s.pred[c][i];
+	if (luma) return dy < 0 ? (int)offsetof(CtuTile, ty) + dx + 1 : (dx < 0 ? (int)offsetof(CtuTile, ly) + dy : dy * H265_CTB_MAX + dx);
+	return dy < 0 ? (int)offsetof(CtuTile, tc) + 2 * (dx + 1) + comp
+	              : (dx < 0 ? (int)offsetof(CtuTile, lc) + 2 * dy + comp : (int)offsetof(CtuTile, c) + dy * H265_CTB_MAX + 2 * dx + comp);
+}
+
+/* The reference samples of an intra block into seq[c][0 .. 4n] (substitution order, unavailable ones substituted by
+ * clamping the index into the available run), [1 2 1] or strong smoothing folded in: each lane reads the up to three
+ * unfiltered samples it needs straight from the tile.  NC components side by side.  Ends with wsync. */
+template <int N, int NC, bool LUMA>
+__device__ __forceinline__ void ref_samples(const h265r_tu_t &t, const CtuTile &tl, LdsCtu &s, int lane, int bx, int by)
+{
+	const uint8_t *tb = (const uint8_t *)&tl;
+	constexpr int corner = 2 * N, last = 4 * N, NREF = NC * (last + 1);
+	const int at = t.avail_top > 2 * N ? 2 * N : t.avail_top, al = t.avail_left > 2 * N ? 2 * N : t.avail_left;
+	const bool top = at > 0, left = al > 0;
+	const int lo = left ? corner - al : (top ? corner + 1 : 0);
+	const int hi = top ? corner + at : (left ? corner - 1 : 0);
+	const bool none = !top && !left;
+	auto raw = [&](int c, int k) -> int {
+		const int kk = clampi(k, lo, hi);
+		const int xx = max(kk - corner - 1, -1), yy = max(corner - 1 - kk, -1);
+		return none ? 128 : (int)tb[tile_off(LUMA, c, bx + xx, by + yy)];
 	};
+	const int mode = t.mode;
+	bool filt = false;
+	if (LUMA && N > 4 && mode != 1) {
+		const int d26 = abs(mode - 26), d10 = abs(mode - 10);
+		const int dist = d26 < d10 ? d26 : d10;
+		filt = mode == 0 || dist > (N == 8 ? 7 : (N == 16 ? 1 : 0));
+	}
+	if (N == 32 && filt && t.strong) {
+		const int cc = raw(0, corner), bl = raw(0, 0), tr = raw(0, last);
+		if (abs(cc + tr - 2 * raw(0, corner + N)) < 8 && abs(cc + bl - 2 * raw(0, corner - N)) < 8) {
+#pragma unroll
+			for (int r = 0; r < (NREF + 63) / 64; ++r) {
+				const int k = lane + 64 * r;
+				if (k <= last) {
+					int v;
+					if (k > 0 && k < corner) v = ((63 - (corner - 1 - k)) * cc + (corner - k) * bl + 32) >> 6;
+					else if (k > corner && k < last) v = ((63 - (k - corner - 1)) * cc + (k - corner) * tr + 32) >> 6;
+					else v = k == 0 ? bl : (k == corner ? cc : tr);
+					s.seq[0][k] = (int16_t)v;
+				}
+			}
+			wsync();
+			return;
+		}
+	}
+#pragma unroll
+	for (int r = 0; r < (NREF + 63) / 64; ++r) {
+		const int i = lane + 64 * r;
+		if (i < NREF) {
+			const int c = NC == 2 && i > last, k = i - c * (last + 1);
+			const int v0 = raw(c, k);
+			int v = v0;
+			if (filt) {
+				const int vm = raw(c, k - 1), vp = raw(c, k + 1);
+				if (k > 0 && k < last) v = (vm + 2 * v0 + vp + 2) >> 2;
+			}
+			s.seq[c][k] = (int16_t)v;
+		}
+	}
+	wsync();
+}
+
+/* seq index of the angular predictor's reference k (spec 8.4.4.2.6: the projected row / column for k < 0) */
+__device__ __forceinline__ int ang_idx(int corner, bool vert, int k, int inv)
+{
+	const int off = k >= 0 ? k : -((k * inv + 128) >> 8);
+	return vert ? corner + off : corner - off;
+}
+
+/* Prediction of the samples (x, ys[i]) of one lane, NS of them, component c (q = seq[c]), into pv: the mode is
+ * uniform, so the loops are per mode and carry no branch (selects only) */
+template <int N, int NS, bool EDGE>
+__device__ __forceinline__ void predict_samples(const int16_t *q, int mode, int x, const int *ys, int dcv, int *pv)
+{
+	constexpr int corner = 2 * N, LOG2 = N == 4 ? 2 : (N == 8 ? 3 : (N == 16 ? 4 : 5));
+#define LL(yy) ((int)q[corner - 1 - (yy)]) /* p[-1][y], y >= -1 */
+#define TT(xx) ((int)q[corner + 1 + (xx)]) /* p[x][-1], x >= -1 */
+	if (mode == 0) {
+		const int tn = TT(N), ln = LL(N), tx = TT(x);
+#pragma unroll
+		for (int i = 0; i < NS; ++i) {
+			const int y = ys[i];
+			pv[i] = ((N - 1 - x) * LL(y) + (x + 1) * tn + (N - 1 - y) * tx + (y + 1) * ln + N) >> (LOG2 + 1);
+		}
+	} else if (mode == 1) {
+		if (EDGE) {
+			const int tx = TT(x), l0 = LL(0), t0 = TT(0);
+#pragma unroll
+			for (int i = 0; i < NS; ++i) {
+				const int y = ys[i], ly = LL(y);
+				pv[i] = x == 0 && y == 0 ? (l0 + 2 * dcv + t0 + 2) >> 2
+				                         : (y == 0 ? (tx + 3 * dcv + 2) >> 2 : (x == 0 ? (ly + 3 * dcv + 2) >> 2 : dcv));
+			}
+		} else {
+#pragma unroll
+			for (int i = 0; i < NS; ++i) pv[i] = dcv;
+		}
+	} else {
+		const int ang = c_ang[mode], inv = c_inv[mode];
+		const bool vert = mode >= 18;
+#pragma unroll
+		for (int i = 0; i < NS; ++i) {
+			const int y = ys[i];
+			const int p = vert ? y : x, qq = vert ? x : y;
+			const int idx = ((p + 1) * ang) >> 5, fr = ((p + 1) * ang) & 31;
+			const int k = qq + idx + 1;
+			const int r1 = q[ang_idx(corner, vert, k, inv)], r2 = q[ang_idx(corner, vert, k + 1, inv)];
+			pv[i] = fr ? ((32 - fr) * r1 + fr * r2 + 16) >> 5 : r1;
+		}
+		if (EDGE && (mode == 26 || mode == 10)) {
+			const int t0 = TT(0), l0 = LL(0), c0 = LL(-1), tx = TT(x);
+#pragma unroll
+			for (int i = 0; i < NS; ++i) {
+				const int y = ys[i], ly = LL(y);
+				if (mode == 26) pv[i] = x == 0 ? clampi(t0 + ((ly - c0) >> 1), 0, 255) : pv[i];
+				else pv[i] = y == 0 ? clampi(l0 + ((tx - c0) >> 1), 0, 255) : pv[i];
+			}
+		}
+	}
+#undef LL
+#undef TT
+}
+
+/* DC value of component c (lanes 0..N-1 add their top + left sample; wave-wide butterfly) */
+template <int N>
+__device__ __forceinline__ int dc_value(const int16_t *q, int lane)
+{
+	constexpr int corner = 2 * N, LOG2 = N == 4 ? 2 : (N == 8 ? 3 : (N == 16 ? 4 : 5));
+	int sum = lane < N ? (int)q[corner + 1 + lane] + (int)q[corner - 1 - lane] : 0;
+	for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+	return (sum + N) >> (LOG2 + 1);
+}
+
+template <int N, bool LUMA, class Wait>
+__device__ void big_block(const h265r_tu_t &t, CtuTile &tl, LdsCtu &s, const h265mfma::Tabs &tb, int lane, int x0, int y0,
+                          const int16_t *cbase, uint32_t clo, const Wait &wait)
+{
+	constexpr int PL = N * N / 64, NC = LUMA ? 1 : 2, LOG2 = N == 16 ? 4 : 5;
+	const int bx = LUMA ? t.x - x0 : t.x - (x0 >> 1), by = LUMA ? t.y - y0 : t.y - (y0 >> 1);
+	const int x = h265mfma::acc_col<N>(lane);
+	/* ---- 1. the residual of each component, in the lane's samples */
+	int res[NC][PL];
+	bool any_res = false;
+#pragma unroll
+	for (int c = 0; c < NC; ++c) {
+		const int kind = t.res[c];
+		const int16_t *d = cbase + (t.coef[c] - clo);
+		if (kind == H265R_RES_FULL) {
+			h265mfma::idct<N>(d, tb, lane, res[c]);
+		} else if (kind == H265R_RES_DC) {
+			const int dc = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
+#pragma unroll
+			for (int i = 0; i < PL; ++i) res[c][i] = dc;
+		} else if (kind == H265R_RES_SKIP) {
+#pragma unroll
+			for (int i = 0; i < PL; ++i) res[c][i] = (d[h265mfma::acc_row<N>(i, lane) * N + x] + 16) >> 5;
+		} else {
+#pragma unroll
+			for (int i = 0; i < PL; ++i) res[c][i] = 0;
+		}
+		any_res |= kind != H265R_RES_NONE;
+	}
+	H5PH(lane, t, 1);
+	wait(); /* (the residual does not depend on the neighbours: computed before their done flags) */
+	H5PH(lane, t, 4);
 	if (!(t.flags & H265R_TU_PRED)) {
 		/* inter: the residual onto the motion-compensated samples */
 		if (any_res) {
-			for (int i = lane; i < ncomp * n2; i += 64) {
-				const int c = i >= n2, j = i - c * n2, x = j & (n - 1), y = j >> log2;
-				uint8_t &p = luma ? tl.y[by + y][bx + x] : tl.c[by + y][2 * (bx + x) + c];
-				p = (uint8_t)clampi((int)p + resid(c, j), 0, 255);
+#pragma unroll
+			for (int i = 0; i < PL; ++i) {
+				const int y = h265mfma::acc_row<N>(i, lane);
+				if (LUMA) {
+					uint8_t &p = tl.y[by + y][bx + x];
+					p = (uint8_t)clampi((int)p + res[0][i], 0, 255);
+				} else {
+					uint16_t &p = *(uint16_t *)&tl.c[by + y][2 * (bx + x)];
+					const int cb = clampi((int)(p & 255) + res[0][i], 0, 255), cr = clampi((int)(p >> 8) + res[NC - 1][i], 0, 255);
+					p = (uint16_t)(cb | (cr << 8));
+				}
+			}
+			wsync();
+		}
+		return;
+	}
+	/* ---- 2. reference samples, filtered (both chroma components side by side) */
+	ref_samples<N, NC, LUMA>(t, tl, s, lane, bx, by);
+	H5PH(lane, t, 2);
+	/* ---- 3. prediction + residual, clipped, into the tile */
+	int ys[PL];
+#pragma unroll
+	for (int i = 0; i < PL; ++i) ys[i] = h265mfma::acc_row<N>(i, lane);
+	int pv[NC][PL];
+#pragma unroll
+	for (int c = 0; c < NC; ++c) {
+		const int dcv = t.mode == 1 ? dc_value<N>(s.seq[c], lane) : 0;
+		predict_samples<N, PL, LUMA && N < 32>(s.seq[c], t.mode, x, ys, dcv, pv[c]);
+	}
+#pragma unroll
+	for (int i = 0; i < PL; ++i) {
+		const int y = ys[i];
+		if (LUMA) {
+			tl.y[by + y][bx + x] = (uint8_t)clampi(pv[0][i] + res[0][i], 0, 255);
+		} else {
+			const int cb = clampi(pv[0][i] + res[0][i], 0, 255), cr = clampi(pv[NC - 1][i] + res[NC - 1][i], 0, 255);
+			*(uint16_t *)&tl.c[by + y][2 * (bx + x)] = (uint16_t)(cb | (cr << 8));
+		}
+	}
+	wsync();
+	H5PH(lane, t, 3);
+}
+
+/* 4 x 4 and 8 x 8 blocks of the CTU kernels (the many: three quarters of a picture's blocks), the same integers as
+ * do_block in three wave-serial phases (round-5 stamps: a 4x4 block cost ~2 us of phase latency, the CTU's ~25 luma
+ * blocks one after another):
+ *   1. the residual first, into s.pred (it does not depend on the prediction): full / DST transforms;
+ *      DC-only and transform-skip are added per sample in phase 3;
+ *   2. reference samples gathered AND filtered in one pass (ref_samples), both chroma components side by side;
+ *   3. prediction + residual, clipped and stored straight into the tile: lane l owns sample (l & (N - 1), l >> log2 N)
+ *      of every component (lanes past N N idle).
+ * An inter block (no prediction) adds its residual to the motion-compensated tile samples in place, or does
+ * nothing without one. */
+template <int N, bool LUMA, class Wait>
+__device__ void small_block(const h265r_tu_t &t, CtuTile &tl, LdsCtu &s, const CtuConst &kc, int lane, int x0, int y0,
+                            const int16_t *cbase, uint32_t clo, const Wait &wait)
+{
+	constexpr int LOG2 = N == 4 ? 2 : 3, N2 = N * N, NC = LUMA ? 1 : 2;
+	const int bx = LUMA ? t.x - x0 : t.x - (x0 >> 1), by = LUMA ? t.y - y0 : t.y - (y0 >> 1);
+	/* ---- 1. full / DST transforms in registers (lane l: sample (l & (N - 1), l >> log2 N)) */
+	int tres[NC];
+#pragma unroll
+	for (int c = 0; c < NC; ++c) {
+		const int kind = t.res[c];
+		tres[c] = 0;
+		if (kind != H265R_RES_FULL && kind != H265R_RES_DST) continue;
+		const int16_t *d = cbase + (t.coef[c] - clo);
+		if (N == 8) tres[c] = tr8_regs(d, kc.mat32, lane);
+		else if (kind == H265R_RES_DST) tres[c] = tr4_regs(d, kc.dst4, lane);
+		else tres[c] = tr4_regs(d, kc.dct4, lane);
+	}
+	H5PH(lane, t, 1);
+	wait(); /* (the residual does not depend on the neighbours: computed before their done flags) */
+	H5PH(lane, t, 4);
+	const bool act = lane < N2;
+	const int x = lane & (N - 1), y = (lane >> LOG2) & (N - 1);
+	int res[NC];
+#pragma unroll
+	for (int c = 0; c < NC; ++c) {
+		const int kind = t.res[c];
+		const int16_t *d = cbase + (t.coef[c] - clo);
+		if (kind == H265R_RES_NONE) res[c] = 0;
+		else if (kind == H265R_RES_DC) res[c] = (d[0] + 64) >> 7; /* acNxNtransform_dconly<N, 7> (m2d.h:306-341) */
+		else if (kind == H265R_RES_SKIP) res[c] = (d[y * N + x] + 16) >> 5;
+		else res[c] = tres[c];
+	}
+	if (!(t.flags & H265R_TU_PRED)) {
+		/* inter: the residual onto the motion-compensated samples */
+		if (t.res[0] != H265R_RES_NONE || (NC == 2 && t.res[1] != H265R_RES_NONE)) {
+			if (act) {
+				if (LUMA) {
+					uint8_t &p = tl.y[by + y][bx + x];
+					p = (uint8_t)clampi((int)p + res[0], 0, 255);
+				} else {
+					uint16_t &p = *(uint16_t *)&tl.c[by + y][2 * (bx + x)];
+					const int cb = clampi((int)(p & 255) + res[0], 0, 255), cr = clampi((int)(p >> 8) + res[NC - 1], 0, 255);
+					p = (uint16_t)(cb | (cr << 8));
+				}
 			}
 			wsync();
 		}
 		return;
 	}
 	/* ---- 2. reference samples, filtered (both components side by side) */
-	const int at = t.avail_top > 2 * n ? 2 * n : t.avail_top, al = t.avail_left > 2 * n ? 2 * n : t.avail_left;
-	const bool top = at > 0, left = al > 0;
-	const int corner = 2 * n, last = 4 * n;
-	const int lo = left ? corner - al : (top ? corner + 1 : 0);
-	const int hi = top ? corner + at : (left ? corner - 1 : 0);
-	auto raw = [&](int c, int k) -> int {
-		if (!top && !left) return 128;
-		const int kk = clampi(k, lo, hi);
-		const int xx = kk < corner ? -1 : (kk == corner ? -1 : kk - corner - 1);
-		const int yy = kk < corner ? corner - 1 - kk : -1;
-		return src.ld(t.plane, c, t.x + xx, t.y + yy);
-	};
-	const int mode = t.mode;
-	bool filt = false;
-	if (luma && mode != 1 && n != 4) {
-		const int d26 = abs(mode - 26), d10 = abs(mode - 10);
-		const int dist = d26 < d10 ? d26 : d10;
-		const int thres = n == 8 ? 7 : (n == 16 ? 1 : 0);
-		filt = mode == 0 || dist > thres;
-	}
-	bool strong = false;
-	int cc = 0, bl = 0, tr = 0;
-	if (filt && t.strong && n == 32) {
-		cc = raw(0, corner);
-		bl = raw(0, 0);
-		tr = raw(0, last);
-		strong = abs(cc + tr - 2 * raw(0, corner + n)) < 8 && abs(cc + bl - 2 * raw(0, corner - n)) < 8;
-	}
-	for (int i = lane; i < ncomp * (last + 1); i += 64) {
-		const int c = i > last, k = i - c * (last + 1);
-		int v;
-		if (strong) {
-			if (k > 0 && k < corner) v = ((63 - (corner - 1 - k)) * cc + (corner - k) * bl + 32) >> 6;
-			else if (k > corner && k < last) v = ((63 - (k - corner - 1)) * cc + (k - corner) * tr + 32) >> 6;
-			else v = raw(c, k);
-		} else if (filt && k > 0 && k < last) {
-			v = (raw(c, k - 1) + 2 * raw(c, k) + raw(c, k + 1) + 2) >> 2;
-		} else {
-			v = raw(c, k);
-		}
-		s.seq[c][k] = (int16_t)v;
-	}
-	wsync();
+	ref_samples<N, NC, LUMA>(t, tl, s, lane, bx, by);
+	H5PH(lane, t, 2);
 	/* ---- 3. prediction + residual into the tile */
-#define LL(c, yy) ((int)s.seq[c][corner - 1 - (yy)]) /* p[-1][y], y >= -1 */
-#define TT(c, xx) ((int)s.seq[c][corner + 1 + (xx)]) /* p[x][-1], x >= -1 */
-	int dc[2] = {0, 0};
-	if (mode == 1) {
-		int sum0 = 0, sum1 = 0;
-		if (lane < n) {
-			sum0 = TT(0, lane) + LL(0, lane);
-			if (ncomp == 2) sum1 = TT(1, lane) + LL(1, lane);
-		}
-		for (int o = 32; o > 0; o >>= 1) {
-			sum0 += __shfl_xor(sum0, o);
-			sum1 += __shfl_xor(sum1, o);
-		}
-		dc[0] = (sum0 + n) >> (log2 + 1);
-		dc[1] = (sum1 + n) >> (log2 + 1);
+	int pv[NC];
+#pragma unroll
+	for (int c = 0; c < NC; ++c) {
+		const int dcv = t.mode == 1 ? dc_value<N>(s.seq[c], lane) : 0;
+		predict_samples<N, 1, LUMA>(s.seq[c], t.mode, x, &y, dcv, &pv[c]);
 	}
-	const int ang = c_ang[mode], inv = c_inv[mode];
-	const bool vert = mode >= 18;
-	auto predict = [&](int c, int x, int y) -> int {
-		int v;
-		if (mode == 0) {
-			v = ((n - 1 - x) * LL(c, y) + (x + 1) * TT(c, n) + (n - 1 - y) * TT(c, x) + (y + 1) * LL(c, n) + n) >> (log2 + 1);
-		} else if (mode == 1) {
-			v = dc[c];
-			if (luma && n < 32) {
-				if (x == 0 && y == 0) v = (LL(c, 0) + 2 * dc[c] + TT(c, 0) + 2) >> 2;
-				else if (y == 0) v = (TT(c, x) + 3 * dc[c] + 2) >> 2;
-				else if (x == 0) v = (LL(c, y) + 3 * dc[c] + 2) >> 2;
-			}
+	if (act) {
+		if (LUMA) {
+			tl.y[by + y][bx + x] = (uint8_t)clampi(pv[0] + res[0], 0, 255);
 		} else {
-			const int p = vert ? y : x, qq = vert ? x : y;
-			const int idx = ((p + 1) * ang) >> 5, fr = ((p + 1) * ang) & 31;
-			const int k = qq + idx + 1;
-			int r1, r2;
-			if (k >= 0) r1 = vert ? TT(c, k - 1) : LL(c, k - 1);
-			else r1 = vert ? LL(c, -1 + ((k * inv + 128) >> 8)) : TT(c, -1 + ((k * inv + 128) >> 8));
-			const int k2 = k + 1;
-			if (k2 >= 0) r2 = vert ? TT(c, k2 - 1) : LL(c, k2 - 1);
-			else r2 = vert ? LL(c, -1 + ((k2 * inv + 128) >> 8)) : TT(c, -1 + ((k2 * inv + 128) >> 8));
-			v = fr ? ((32 - fr) * r1 + fr * r2 + 16) >> 5 : r1;
-			if (luma && n < 32) {
-				if (mode == 26 && x == 0) v = clampi(TT(c, 0) + ((LL(c, y) - LL(c, -1)) >> 1), 0, 255);
-				if (mode == 10 && y == 0) v = clampi(LL(c, 0) + ((TT(c, x) - TT(c, -1)) >> 1), 0, 255);
-			}
+			const int cb = clampi(pv[0] + res[0], 0, 255), cr = clampi(pv[NC - 1] + res[NC - 1], 0, 255);
+			*(uint16_t *)&tl.c[by + y][2 * (bx + x)] = (uint16_t)(cb | (cr << 8));
 		}
-		return clampi(v + resid(c, y * n + x), 0, 255);
-	};
-	/* one sample per lane, stored as a byte (small blocks: lanes, not the LDS store width, bound them — a dword
-	 * of 4 samples per lane measured slower for 4 x 4 and 8 x 8 blocks, r124 stamps) */
-	for (int i = lane; i < ncomp * n2; i += 64) {
-		const int c = i >= n2, j = i - c * n2, x = j & (n - 1), y = j >> log2;
-		const uint8_t v = (uint8_t)predict(c, x, y);
-		if (luma) tl.y[by + y][bx + x] = v;
-		else tl.c[by + y][2 * (bx + x) + c] = v;
 	}
-#undef LL
-#undef TT
 	wsync();
+	H5PH(lane, t, 3);
+}
+
+/* One block of a CTU kernel (wave-wide): dispatch on size and plane (uniform).  wait() returns once the blocks whose
+ * samples this one reads are done; it runs between the residual and the reference samples. */
+template <class Wait>
+__device__ void do_block_ctu(const h265r_tu_t &t, CtuTile &tl, LdsCtu &s, const CtuConst &kc, int lane, int x0, int y0,
+                             const int16_t *cbase, uint32_t clo, const Wait &wait)
+{
+	H5PH(lane, t, 0);
+	/* (chroma blocks are at most 16 x 16) */
+	if (t.plane) {
+		if (t.log2 == 2) small_block<4, false>(t, tl, s, kc, lane, x0, y0, cbase, clo, wait);
+		else if (t.log2 == 3) small_block<8, false>(t, tl, s, kc, lane, x0, y0, cbase, clo, wait);
+		else big_block<16, false>(t, tl, s, kc.tb, lane, x0, y0, cbase, clo, wait);
+	} else {
+		if (t.log2 == 2) small_block<4, true>(t, tl, s, kc, lane, x0, y0, cbase, clo, wait);
+		else if (t.log2 == 3) small_block<8, true>(t, tl, s, kc, lane, x0, y0, cbase, clo, wait);
+		else if (t.log2 == 4) big_block<16, true>(t, tl, s, kc.tb, lane, x0, y0, cbase, clo, wait);
+		else big_block<32, true>(t, tl, s, kc.tb, lane, x0, y0, cbase, clo, wait);
+	}
 }
 
 /* the coefficients of records [c0, c0 + m) (staged in recs) into LDS when their pool range fits: one bulk
@@ -744,24 +947,24 @@ struct CtuSched {
 };
 
 template <int NT>
-__device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *recs, int m, CtuTile &tl, Lds *ls, CtuSched &sc,
-                                           int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col)
+__device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *recs, int m, CtuTile &tl, LdsCtu *ls, const CtuConst &kc,
+                                           CtuSched &sc, int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col)
 {
 	const int lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6;
 	if (NT == 128) {
-		Lds &s = ls[wave];
+		LdsCtu &s = ls[wave];
 		for (int k = 0; k < m; ++k) {
-			const h265r_tu_t t = recs[k];
-			if (t.plane != wave) continue;
-			do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
+			if (recs[k].plane != wave) continue;
+			const h265r_tu_t t = uniform_tu(recs[k]);
+			do_block_ctu(t, tl, s, kc, lane, x0, y0, cb, clo, [] {});
 			H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
 		}
 		(void)sc;
 		return;
 	}
 	const int plane = wave >> 1;
-	Lds &s = ls[wave];
+	LdsCtu &s = ls[wave];
 	/* the chunk's plane lists, owner maps and done flags */
 	for (int i = tid; i < 2 * 16 * 16; i += NT) (&sc.own[0][0])[i] = 0xffff;
 	for (int k = tid; k < m; k += NT) sc.done[k] = 0;
@@ -788,13 +991,14 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 	}
 	__syncthreads();
 	for (;;) {
-		int pos = 0;
-		if (lane == 0) pos = atomicAdd(&sc.next[plane], 1);
-		pos = __shfl(pos, 0);
-		if (pos >= sc.n[plane]) break;
-		const int k = sc.list[plane][pos];
+		/* (every lane adds, lane 0 by 1, and the wave takes lane 0's value: no single-lane section inside the
+		 * persistent loop — DESIGN §5 compiler hazards) */
+		const int pos = __builtin_amdgcn_readfirstlane(atomicAdd(&sc.next[plane], lane == 0 ? 1 : 0));
+		if (pos >= __builtin_amdgcn_readfirstlane(sc.n[plane])) break;
+		const int k = __builtin_amdgcn_readfirstlane(sc.list[plane][pos]);
 		const h265r_tu_t t = uniform_tu(recs[k]);
-		if (t.flags & H265R_TU_PRED) {
+		auto wait = [&] {
+			if (!(t.flags & H265R_TU_PRED)) return;
 			/* the owners of the samples it reads inside the CTU: lane i < ntop the units above, then the units to the
 			 * left, then the corner */
 			const int n = 1 << t.log2;
@@ -815,14 +1019,20 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 					__hip_atomic_store((gi32 *)a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 					break;
 				}
+				if ((spins & 255) == 0 && __hip_atomic_load((gi32 *)a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
 				__builtin_amdgcn_s_sleep(1);
 			}
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-		}
-		do_block_ctu(a, t, tl, s, lane, x0, y0, cb, clo);
+		};
+#ifdef H265_WAIT_FIRST
+		wait();
+		do_block_ctu(t, tl, s, kc, lane, x0, y0, cb, clo, [] {});
+#else
+		do_block_ctu(t, tl, s, kc, lane, x0, y0, cb, clo, wait);
+#endif
 		H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (plane << 7) | ((t.mode & 63) << 8));
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-		if (lane == 0) __hip_atomic_store(&sc.done[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		__hip_atomic_store(&sc.done[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); /* (every lane: the same word) */
 	}
 }
 
@@ -844,10 +1054,11 @@ __global__ __launch_bounds__(256) void k_h265_ctu_index(const H265Args *ap)
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_h265_ctu_rows(const H265Args *ap)
+__global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 {
 	const H265Args a = *ap;
-	__shared__ Lds ls[NT / 64];
+	__shared__ LdsCtu ls[NT / 64];
+	__shared__ CtuConst kc;
 	__shared__ CtuTile tl;
 	__shared__ h265r_tu_t recs[H265_CTU_RECS]; /* the CTU's records, staged (every wave reads all of them) */
 	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
@@ -857,8 +1068,7 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_rows(const H265Args *ap)
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6; /* NT 128: 0 luma, 1 chroma; NT 256: 0-1 luma, 2-3 chroma */
 	const int row = blockIdx.x;
 	const int ctb = 1 << a.ctb_log2, cctb = ctb >> 1;
-	Lds &s = ls[wave];
-	for (int i = lane; i < 32 * 32; i += 64) s.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+	ctu_const_init(kc, tid, NT); /* (read after the barrier ahead of the first CTU's blocks) */
 	const int y0 = row << a.ctb_log2;
 	const int rows_here = min(ctb, a.pic_h - y0), crows = rows_here >> 1;
 	for (int col = 0; col < a.ctu_cols; ++col) {
@@ -938,7 +1148,7 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_rows(const H265Args *ap)
 				__syncthreads();
 				uint32_t clo;
 				const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
-				ctu_blocks<NT>(a, recs, m, tl, ls, sch, tid, x0, y0, cb, clo, row, col);
+				ctu_blocks<NT>(a, recs, m, tl, ls, kc, sch, tid, x0, y0, cb, clo, row, col);
 			}
 		}
 		H5ST(lane, 2, row, col, wave);
@@ -971,10 +1181,11 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_rows(const H265Args *ap)
  * dispatched earlier, so a wait always ends) and loads their published edge samples; the row kernel's 17
  * workgroups of a 1080p picture instead walked their 30 CTUs one after another. */
 template <int NT>
-__global__ __launch_bounds__(NT) void k_h265_ctu_grid(const H265Args *ap)
+__global__ __launch_bounds__(NT, 2) void k_h265_ctu_grid(const H265Args *ap)
 {
 	const H265Args a = *ap;
-	__shared__ Lds ls[NT / 64];
+	__shared__ LdsCtu ls[NT / 64];
+	__shared__ CtuConst kc;
 	__shared__ CtuTile tl;
 	__shared__ h265r_tu_t recs[H265_CTU_RECS];
 	__shared__ __attribute__((aligned(16))) int16_t ccoef[H265_CTU_COEF + 2];
@@ -990,8 +1201,7 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_grid(const H265Args *ap)
 	gi32 *done = (gi32 *)(a.ctu_first + a.ctu_cols * a.ctu_rows + 1);
 	__shared__ int s_need;
 	if (i0 < i1) {
-		Lds &s = ls[wave];
-		for (int i = lane; i < 32 * 32; i += 64) s.mat32[i] = (int16_t)dct32_coef(i >> 5, i & 31);
+		ctu_const_init(kc, tid, NT);
 		/* the neighbour CTUs the CTU's edge intra blocks read: 1 left, 2 above-left, 4 above, 8 above-right */
 		int need = 0;
 		if (tid == 0) s_need = 0;
@@ -1069,7 +1279,7 @@ __global__ __launch_bounds__(NT) void k_h265_ctu_grid(const H265Args *ap)
 			__syncthreads();
 			uint32_t clo;
 			const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
-			ctu_blocks<NT>(a, recs, m, tl, ls, sch, tid, x0, y0, cb, clo, row, col);
+			ctu_blocks<NT>(a, recs, m, tl, ls, kc, sch, tid, x0, y0, cb, clo, row, col);
 		}
 		__syncthreads();
 		/* out: the CTU's samples as write-through words, drained before the done flag */

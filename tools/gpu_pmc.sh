@@ -25,7 +25,10 @@ fi
 # WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ WAVE_CYCLES) plus VALU issue and the clock
 CGROUPS=(FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" \
   "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE")
-case "$K" in h265*) CGROUPS=(FETCH_SIZE WRITE_SIZE) ;; esac
+# H.265: traffic, plus the CTU kernel's wave states (LDS issue / waits split out) and instruction mix
+case "$K" in h265*) CGROUPS=(FETCH_SIZE WRITE_SIZE \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
+  "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_IFETCH SQ_BUSY_CYCLES") ;; esac
 for C in "${CGROUPS[@]}"; do
   N=$(echo $C | tr ' ' '_')
   timeout -s KILL 240 rocprofv3 --pmc $C -d $R/gpurun_out/pmc_$TAG/$N -o run --output-format csv -- $CMD \

@@ -15,6 +15,7 @@
 #   pmc=KERNEL       tools/gpu_pmc.sh TAG KERNEL (FETCH_SIZE / WRITE_SIZE / SQ passes)
 #   h265ab=R,VAR,A,B interleaved A/B of VAR=A / VAR=B on the bench's two H.265 legs (R rounds)  -> h265ab_TAG.txt
 #   h265tl=N,STREAM  tools/h265_timeline.sh (rocprof kernel trace + parse jobs of N decodes)   -> h5tl_TAG.txt
+#   h5stamps[=STREAM] tools/stamps_h265.py with the stamps build (make h5stamps: build/h5s/, delete after use) -> h5stamps_TAG.txt
 #   md5host          tools/md5_batch_bench.py with and without the stitched 2-3 frame kernel -> md5host_TAG.txt
 #   md5gpu[=N]       tools/_build/md5_gpu_probe N (one MD5 chain per wave / per lane on the GPU) -> md5gpu_TAG.txt
 set -o pipefail
@@ -67,6 +68,10 @@ for step in "$@"; do
     h265tl)
       IFS=',' read -r n st <<< "$arg"
       timeout -k 10 400 bash tools/h265_timeline.sh $TAG ${n:-4} ${st:-c_h265_1080p_s1}; rc=$? ;;
+    h5stamps)
+      M2DEC_AMD_LIB=$R/build/h5s/libm2dec_amd_h5stamps.so M2DEC_AMD_H265_STREAMS=1 timeout -k 10 200 \
+        python -u tools/stamps_h265.py ${arg:-c_h265_1080p_s1} > $O/h5stamps_$TAG.txt 2>&1
+      rc=$?; head -30 $O/h5stamps_$TAG.txt ;;
     md5host)
       { for st in 1 0; do echo "M2DEC_AMD_MD5_STITCH=$st"; M2DEC_AMD_MD5_STITCH=$st timeout -k 10 120 python tools/md5_batch_bench.py || exit 1; done; } \
         > $O/md5host_$TAG.txt 2>&1

@@ -72,6 +72,25 @@ def h265(root, label, out):
     # the doubled figure (the upper bound) as the traffic
     out["traffic_bytes_per_picture"] = out["read_bytes_doubled"] + out["write_bytes"]
     out["traffic_bytes_per_picture_raw"] = out["read_bytes_raw"] + out["write_bytes"]
+    # the CTU kernels' wave states and instruction mix (SQ groups, when collected): sums over their dispatches, per
+    # picture; the wave-cycle counters are quad-cycles (MI355X_MICROARCH.md §PMC: WAIT_ANY + WAIT_INST_ANY +
+    # ACTIVE_INST_ANY ~ WAVE_CYCLES)
+    sq = {}
+    for d in sorted(glob.glob(os.path.join(root, "SQ_*"))):
+        for v in per_dispatch(d):
+            if "k_h265_ctu_" not in v["_name"]:
+                continue
+            for k, x in v.items():
+                if k.startswith("SQ_") or k.startswith("GRBM_"):
+                    sq[k] = sq.get(k, 0.0) + x
+    if sq:
+        n = max(1, pics_f)
+        out["ctu_kernel_counters_per_picture"] = {k: round(x / n, 1) for k, x in sorted(sq.items())}
+        wc = sq.get("SQ_WAVE_CYCLES", 0.0)
+        if wc:
+            out["ctu_kernel_wave_state_fractions"] = {k: round(sq.get(k, 0.0) / wc, 4) for k in (
+                "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
+                "SQ_WAIT_INST_LDS")}
 
 
 def main():

@@ -79,6 +79,42 @@ for pi, p in enumerate(pics[:2]):
     for key in sorted(groups, key=lambda k: -sum(groups[k]))[:14]:
         xs = groups[key]
         print(f"    plane {key[0]} n{1 << key[1]:2d} pred {key[2]} res {key[3]}: {len(xs):5d}  {statistics.median(xs):6.2f}  {sum(xs):8.0f}")
+    # block phases (kind 5, per workgroup and wave): start -> residual -> reference samples -> prediction + store;
+    # "gap" = from the wave's previous block end to this block's start (next record, dependency waits)
+    seqs = defaultdict(list)
+    for t, k, r, c, aux in p:
+        if k == 5:
+            seqs[(c, r)].append((t, aux >> 8, aux & 255))
+    ph = defaultdict(lambda: [[], [], [], [], []])
+    for key, evs in seqs.items():
+        evs.sort()
+        prev_end, cur = None, None
+        for t, phase, sz in evs:
+            if phase == 0:
+                cur = {0: t, "sz": sz, "gap": us(t - prev_end) if prev_end is not None else None}
+            elif cur is not None:
+                cur[phase] = t
+                if phase == 3:
+                    g = ph[(sz >> 3, 1 << (sz & 7))]
+                    w = cur.get(4, cur.get(1))
+                    if 1 in cur:
+                        g[0].append(us(cur[1] - cur[0]))
+                    if 4 in cur and 1 in cur:
+                        g[1].append(us(cur[4] - cur[1]))
+                    if 2 in cur and w is not None:
+                        g[2].append(us(cur[2] - w))
+                    if 2 in cur:
+                        g[3].append(us(t - cur[2]))
+                    if cur["gap"] is not None:
+                        g[4].append(cur["gap"])
+                    prev_end, cur = t, None
+    if ph:
+        print("  intra block phases (median us): plane, size: n, residual, wait for neighbours, reference samples, "
+              "prediction + store, gap before")
+        md = lambda xs: f"{statistics.median(xs):6.2f}" if xs else "     -"  # noqa: E731
+        for key in sorted(ph):
+            g = ph[key]
+            print(f"    plane {key[0]} n{key[1]:2d}: {len(g[3]):5d}  {md(g[0])}  {md(g[1])}  {md(g[2])}  {md(g[3])}  {md(g[4])}")
     # the chain: the CTU finishing last, and per row when its last CTU ended
     rows = defaultdict(list)
     for (r, c), v in ctu.items():

@@ -26,7 +26,14 @@ M2VGEN := tools/_build/m2vgen
 APP := m2dec_amd/lib/h264dec
 HARNESS := tools/_build/m2decoder_like
 
-all: $(LIB) $(ORACLE) $(GEN) $(GEN265) $(M2VGEN) $(APP) $(HARNESS)
+MFMA_PROBE := tools/_build/mfma_idct_probe
+
+all: $(LIB) $(ORACLE) $(GEN) $(GEN265) $(M2VGEN) $(APP) $(HARNESS) $(MFMA_PROBE)
+
+# the H.265 int8-MFMA inverse DCT against the reference's integer transform on the GPU (tests/test_gpu_h265.py)
+$(MFMA_PROBE): tools/mfma_idct_probe.hip m2dec_amd/csrc/hip/h265_mfma.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -Im2dec_amd/csrc/hip -o $@ $<
 
 # test harness: drives h264d_func the way src/app/m2decoder.h does (no release call)
 $(HARNESS): tests/harness/m2decoder_like.cpp $(LIB) include/m2dec_amd.h include/m2d.h

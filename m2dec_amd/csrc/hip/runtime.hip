@@ -1258,12 +1258,15 @@ struct HipBackend {
 
 int launch_held(HipBackend *b);
 
-/* decode ahead: pictures copied out to staging behind their kernels (M2DEC_AMD_PRESTAGE=0: at bind, as before
- * round 6), at most kPrestageMax of a back end at a time (pinned memory: 64 x 3 MB at 1080p) */
+/* decode ahead: pictures copied out to staging right behind their kernels, on the launch's own stream
+ * (M2DEC_AMD_PRESTAGE=0: at bind, on the copy stream, as before round 6), at most kPrestageMax of a back end at a
+ * time (pinned memory: 32 x 3 MB at 1080p).  Interleaved A/Bs (r158): C5 46.2 -> 43.4 ms per decode, c3 29.0 ms
+ * both ways; on the shared copy stream instead (r140, r156) the copies waiting for their kernels held up the binds'
+ * copies of frames the caller takes first, 1-4 % slower */
 static const int kPrestageMax = 32;
 static bool prestage_on()
 {
-	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 0;
+	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 1;
 	return on != 0;
 }
 
@@ -1563,21 +1566,21 @@ int launch_held(HipBackend *b)
 	/* decode ahead: each picture out to pinned staging right behind its kernel, before the API context binds it
 	 * (r139 timeline: with the copy issued at bind, the API thread waited on every frame's copy in turn — 60 copies
 	 * of ~0.3 ms each from the bind to the frame's peek, the last one 6.2 ms after the last kernel) */
-	for (int i = 0; i < n && prestage_on(); ++i) {
+	for (int i = 0; i < n; ++i) {
 		const HipBackend::Held &h = b->held[i];
-		if (!h.virt || b->prestaged >= kPrestageMax) continue;
+		if (!h.virt || b->prestaged >= kPrestageMax || !prestage_on()) continue;
 		const int v = 64 + h.j.slot;
 		if (b->stg[v]) { /* (an earlier picture of this buffer never bound — ahead_ok orders reuse after the bind) */
 			if (b->slot_pending[v]) CHECK(hipEventSynchronize(b->slot_ev[v]));
 			stage_drop(b, v);
 		}
-		if (!b->copy) CHECK(g_pool.stream(sc.dev, &b->copy));
-		CHECK(hipStreamWaitEvent(b->copy, sc.slot_write[h.j.slot], 0));
-		if (stage_copy(b, sc.frames + (size_t)h.j.slot * sc.fsz, v, b->copy) < 0) return -1;
+		/* on the launch's own stream, right behind it: on the shared copy stream a copy waiting for its kernel held
+		 * up the binds' copies of frames the caller takes first (r156: every copy-ahead setting slower) */
+		if (stage_copy(b, sc.frames + (size_t)h.j.slot * sc.fsz, v, s) < 0) return -1;
 		b->prestaged++;
 		hipEvent_t r = sc.next_event(); /* (a reader of the buffer: its next writer waits for the copy) */
 		if (!r) return -1;
-		CHECK(hipEventRecord(r, b->copy));
+		CHECK(hipEventRecord(r, s));
 		sc.readers[h.j.slot].push_back(r);
 	}
 	m2d_tl('l', n, k);

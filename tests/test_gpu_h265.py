@@ -40,3 +40,15 @@ def test_hip_h265_inter_variants(built, monkeypatch, env):
         md5s, err = m2dec_amd.decode_h265(h265_stream(name), device=0)
         assert err == -2
         assert md5s == GOLD[name]["md5"], name
+
+
+@pytest.mark.gpu
+def test_mfma_idct_probe(built):
+    """The 16 x 16 / 32 x 32 inverse DCT on the int8 matrix cores (m2dec_amd/csrc/hip/h265_mfma.h, the CTU kernels'
+    path) equals the reference's two-pass integer transform on 1000 random blocks per size, int16 extremes
+    included (tools/mfma_idct_probe.hip; the decomposition itself: tests/test_h265_mfma_cpu.py)."""
+    import subprocess
+    probe = os.path.join(ROOT, "tools", "_build", "mfma_idct_probe")
+    r = subprocess.run([probe, "1000"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "N=16: 0 of 1000 blocks differ" in r.stdout and "N=32: 0 of 1000 blocks differ" in r.stdout

@@ -1093,15 +1093,24 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
 			}
 		}
+		/* the CTU's first chunk of records and its coefficients into LDS before the wait for the row above: the
+		 * staging (two dependent global round trips) overlaps that wait, which is the wavefront's critical path */
+		const int c = row * a.ctu_cols + col;
+		const int i0 = a.ctu_first[c], i1 = a.ctu_first[c + 1];
+		const int m0 = min(H265_CTU_RECS, i1 - i0);
+		__syncthreads(); /* (the previous CTU's records / coefficients are consumed) */
+		for (int k = tid; k < m0 * (int)(sizeof(h265r_tu_t) / 4); k += NT) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + i0))[k];
+		__syncthreads();
+		uint32_t clo0;
+		const int16_t *cb0 = stage_coef<NT>(a, recs, m0, ccoef, red, tid, clo0);
 		/* does a block of this CTU read the row above?  Only an intra-predicted block on the CTU's top edge does
 		 * (a block below it reads the tile; inter blocks start from the motion-compensated samples, an earlier
 		 * launch).  A CTU without one neither waits for the row above nor loads it: in P / B pictures, where
 		 * most CTUs hold only inter blocks, the CTU rows run side by side instead of as a 2-CTU-lag wavefront */
 		int above = 0;
 		if (row > 0) {
-			const int c = row * a.ctu_cols + col;
-			for (int k = a.ctu_first[c] + tid; k < a.ctu_first[c + 1]; k += NT) {
-				const h265r_tu_t &t = a.tu[k];
+			for (int k = tid; k < i1 - i0; k += NT) {
+				const h265r_tu_t &t = k < m0 ? recs[k] : a.tu[i0 + k];
 				if ((t.flags & H265R_TU_PRED) && (t.plane ? 2 * t.y : t.y) == y0) above = 1;
 			}
 			above = __syncthreads_or(above);
@@ -1135,21 +1144,18 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 		}
 		__syncthreads();
 		H5ST(tid, 1, row, col, above);
-		/* the CTU's blocks, luma on wave 0, chroma on wave 1, in decoding order */
-		{
-			const CtuSamples src{tl, x0, y0};
-			const int c = row * a.ctu_cols + col;
-			const int i0 = a.ctu_first[c], i1 = a.ctu_first[c + 1];
-			for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
-				const int m = min(H265_CTU_RECS, i1 - c0);
-				__syncthreads(); /* (the previous chunk is consumed) */
-				for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += NT)
-					((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
-				__syncthreads();
-				uint32_t clo;
-				const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
-				ctu_blocks<NT>(a, recs, m, tl, ls, kc, sch, tid, x0, y0, cb, clo, row, col);
-			}
+		/* the CTU's blocks (luma on waves 0-1, chroma on waves 2-3, each plane in decoding order): the staged first
+		 * chunk, then any further chunk of a CTU with more than H265_CTU_RECS records */
+		if (m0 > 0) ctu_blocks<NT>(a, recs, m0, tl, ls, kc, sch, tid, x0, y0, cb0, clo0, row, col);
+		for (int c0 = i0 + m0; c0 < i1; c0 += H265_CTU_RECS) {
+			const int m = min(H265_CTU_RECS, i1 - c0);
+			__syncthreads(); /* (the previous chunk is consumed) */
+			for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += NT)
+				((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
+			__syncthreads();
+			uint32_t clo;
+			const int16_t *cb = stage_coef<NT>(a, recs, m, ccoef, red, tid, clo);
+			ctu_blocks<NT>(a, recs, m, tl, ls, kc, sch, tid, x0, y0, cb, clo, row, col);
 		}
 		H5ST(lane, 2, row, col, wave);
 		__syncthreads();

@@ -948,14 +948,17 @@ struct CtuSched {
 
 template <int NT>
 __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *recs, int m, CtuTile &tl, LdsCtu *ls, const CtuConst &kc,
-                                           CtuSched &sc, int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col)
+                                           CtuSched &sc, int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col,
+                                           int which = 0)
 {
+	/* which: 0 every record, 1 the residual-only (inter) ones, 2 the intra-predicted ones (the inter ones done) */
+	auto take = [&](const h265r_tu_t &t) { return which == 0 || ((t.flags & H265R_TU_PRED) ? 2 : 1) == which; };
 	const int lane = tid & 63;
 	const int wave = __builtin_amdgcn_readfirstlane(tid) >> 6;
 	if (NT == 128) {
 		LdsCtu &s = ls[wave];
 		for (int k = 0; k < m; ++k) {
-			if (recs[k].plane != wave) continue;
+			if (recs[k].plane != wave || !take(recs[k])) continue;
 			const h265r_tu_t t = uniform_tu(recs[k]);
 			do_block_ctu(t, tl, s, kc, lane, x0, y0, cb, clo, [] {});
 			H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (wave << 7) | ((t.mode & 63) << 8));
@@ -967,12 +970,12 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 	LdsCtu &s = ls[wave];
 	/* the chunk's plane lists, owner maps and done flags */
 	for (int i = tid; i < 2 * 16 * 16; i += NT) (&sc.own[0][0])[i] = 0xffff;
-	for (int k = tid; k < m; k += NT) sc.done[k] = 0;
+	for (int k = tid; k < m; k += NT) sc.done[k] = which == 2 && !(recs[k].flags & H265R_TU_PRED);
 	if ((wave & 1) == 0) {
 		int cnt = 0;
 		for (int base = 0; base < m; base += 64) {
 			const int k = base + lane;
-			const bool mine = k < m && recs[k].plane == plane;
+			const bool mine = k < m && recs[k].plane == plane && take(recs[k]);
 			const unsigned long long mask = __ballot(mine);
 			if (mine) sc.list[plane][cnt + __popcll(mask & ((1ull << lane) - 1))] = (uint16_t)k;
 			cnt += __popcll(mask);
@@ -1225,8 +1228,35 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_grid(const H265Args *ap)
 		if (need) atomicOr(&s_need, need);
 		__syncthreads();
 		need = s_need;
+		/* the motion-compensated samples (k_h265_mc, an earlier launch) */
+		if (a.n_pu) {
+			const int wpr = (cols_here + 3) >> 2;
+			for (int w = tid; w < wpr * rows_here; w += NT) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
+			}
+			for (int w = tid; w < wpr * crows; w += NT) {
+				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
+				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
+			}
+		}
+		/* A CTU whose intra blocks wait for neighbour CTUs first adds the residuals of its inter blocks (which read
+		 * nothing outside themselves), then waits, then reconstructs its intra blocks in decoding order (an intra
+		 * block reads only earlier blocks' samples: the inter ones are final by then): the inter work leaves the
+		 * chain of intra CTUs (r166: the neighbour waits were ~75 % of the 1080p P / B CTU pass).  A CTU with more
+		 * records than one LDS chunk keeps the single pass. */
+		const bool split = need && i1 - i0 <= H265_CTU_RECS && !(a.flags & (1 << 29));
+		uint32_t clo0 = 0;
+		const int16_t *cb0 = nullptr;
+		if (split) {
+			__syncthreads(); /* (the tile) */
+			for (int k = tid; k < (i1 - i0) * (int)(sizeof(h265r_tu_t) / 4); k += NT) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + i0))[k];
+			__syncthreads();
+			cb0 = stage_coef<NT>(a, recs, i1 - i0, ccoef, red, tid, clo0);
+			ctu_blocks<NT>(a, recs, i1 - i0, tl, ls, kc, sch, tid, x0, y0, cb0, clo0, row, col, 1);
+		}
 		/* wave 0 lanes 0..3 poll one neighbour each */
-		if (wave == 0 && need) {
+		if (wave == 0 && need && !(a.flags & (1 << 30))) {
 			int dep = -1;
 			if (lane == 0 && (need & 1)) dep = c - 1;
 			if (lane == 1 && (need & 2)) dep = c - a.ctu_cols - 1;
@@ -1246,18 +1276,6 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_grid(const H265Args *ap)
 			__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 		}
 		__syncthreads();
-		/* the motion-compensated samples (k_h265_mc, an earlier launch) */
-		if (a.n_pu) {
-			const int wpr = (cols_here + 3) >> 2;
-			for (int w = tid; w < wpr * rows_here; w += NT) {
-				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
-				*(uint32_t *)&tl.y[yy][xx] = *(const uint32_t *)plane_px(a, 0, 0, x0 + xx, y0 + yy);
-			}
-			for (int w = tid; w < wpr * crows; w += NT) {
-				const int yy = w / wpr, xx = (w - yy * wpr) * 4;
-				*(uint32_t *)&tl.c[yy][xx] = *(const uint32_t *)plane_px(a, 1, 0, (x0 >> 1) + (xx >> 1), (y0 >> 1) + yy);
-			}
-		}
 		/* the neighbours' edge samples (published as write-through words: read at agent scope) */
 		if (need & 1)
 			for (int i = tid; i < 2 * ctb; i += NT) {
@@ -1276,9 +1294,13 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_grid(const H265Args *ap)
 				tl.tc[i] = in ? (uint8_t)ld_px(a, 1, i & 1, x, (y0 >> 1) - 1) : 128;
 			}
 		}
-		/* the CTU's blocks, luma on wave 0, chroma on wave 1, in decoding order */
-		const CtuSamples src{tl, x0, y0};
-		for (int c0 = i0; c0 < i1; c0 += H265_CTU_RECS) {
+		/* the CTU's blocks (luma on waves 0-1, chroma on waves 2-3, each plane in decoding order): the intra ones of a
+		 * split CTU, else all of them */
+		if (split) {
+			__syncthreads(); /* (the edge samples) */
+			ctu_blocks<NT>(a, recs, i1 - i0, tl, ls, kc, sch, tid, x0, y0, cb0, clo0, row, col, 2);
+		}
+		for (int c0 = i0; c0 < i1 && !split; c0 += H265_CTU_RECS) {
 			const int m = min(H265_CTU_RECS, i1 - c0);
 			__syncthreads(); /* (the tile / the previous chunk) */
 			for (int k = tid; k < m * (int)(sizeof(h265r_tu_t) / 4); k += NT) ((uint32_t *)recs)[k] = ((const uint32_t *)(a.tu + c0))[k];
@@ -2057,6 +2079,8 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.ctb_log2 = pic->ctb_log2;
 	h.n_tu = pic->n_tu;
 	h.flags = pic->flags;
+	if (getenv("M2DEC_AMD_H265_DIAG_NOWAIT")) h.flags |= 1 << 30; /* (diagnostic: CTU-grid neighbour waits skipped — wrong output) */
+	if (getenv("M2DEC_AMD_H265_GRID_ONEPASS")) h.flags |= 1 << 29; /* (A/B: no inter-first split of the CTU-grid blocks) */
 	h.beta_offset = pic->beta_offset;
 	h.tc_offset = pic->tc_offset;
 	h.cb_qp_offset = pic->cb_qp_offset;

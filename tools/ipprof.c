@@ -1,8 +1,8 @@
-/* Cycle-sampling profile of the H.264 host parse (null back end), for hosts without a perf tool:
+/* Cycle-sampling profile of the H.264 / H.265 host parse (null back end), for hosts without a perf tool:
  * perf_event_open sampling of the instruction pointer every PERIOD cycles, reported as offsets into
  * libm2dec_amd.so (resolve them with addr2line -f -i -e m2dec_amd/lib/libm2dec_amd.so).
- *   tools/ipprof.c <stream.264> [reps] [bm] > samples.txt      (lines: "offset count"; bm: sample branch
- *   misses instead of cycles) */
+ *   tools/ipprof.c <stream.264|stream.265> [reps] [bm] > samples.txt      (lines: "offset count"; bm: sample branch
+ *   misses instead of cycles; an H.265 stream is parsed on the caller's thread: M2DEC_AMD_H265_THREADS=0) */
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <linux/perf_event.h>
@@ -21,6 +21,12 @@
 #define MAXOFF (1 << 24)
 
 static uint32_t hist[MAXOFF];
+
+/* H.265: a back end whose calls do nothing (only the parser is sampled) */
+static int n265_frames(void *self, int n, const m2d_frame_t *f, int w, int h) { (void)self; (void)n; (void)f; (void)w; (void)h; return 0; }
+static int n265_submit(void *self, const h265r_picture_t *p) { (void)self; (void)p; return 0; }
+static int n265_sync(void *self, int slot) { (void)self; (void)slot; return 0; }
+static void n265_destroy(void *self) { (void)self; }
 static long other;
 
 static void drain(struct perf_event_mmap_page *mp, uintptr_t base)
@@ -75,7 +81,23 @@ int main(int argc, char **argv)
 	const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
 	struct perf_event_mmap_page *mp = mmap(NULL, (PAGES + 1) * pg, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
 	if (mp == MAP_FAILED) { perror("mmap"); return 1; }
-	for (int r = 0; r < reps; ++r) {
+	const int h265 = strlen(argv[1]) > 4 && !strcmp(argv[1] + strlen(argv[1]) - 4, ".265");
+	if (h265) setenv("M2DEC_AMD_H265_THREADS", "0", 1);
+	for (int r = 0; r < reps && h265; ++r) {
+		h265r_backend_t be;
+		memset(&be, 0, sizeof be);
+		be.set_frames = n265_frames;
+		be.submit = n265_submit;
+		be.sync_frame = n265_sync;
+		be.destroy = n265_destroy;
+		int last = 0;
+		ioctl(fd, PERF_EVENT_IOC_ENABLE, 0);
+		const int fr = m2dec_amd_decode_h265(d, (size_t)n, &be, 0, 0, NULL, NULL, &last);
+		ioctl(fd, PERF_EVENT_IOC_DISABLE, 0);
+		drain(mp, base);
+		fprintf(stderr, "rep %d: %d (last %d)\n", r, fr, last);
+	}
+	for (int r = 0; r < reps && !h265; ++r) {
 		m2r_backend_t be;
 		m2dec_amd_null_backend_create(&be);
 		/* (one pass of the stream fits the ring: ~13k samples of 16 bytes at PERIOD) */

@@ -1251,6 +1251,7 @@ struct HipBackend {
 	bool timing = true;
 	bool kcopy = true; /* records up by k_upload (M2DEC_AMD_KCOPY) */
 	int kd2h = 2;      /* frames down: 0 SDMA, 1 k_upload, 2 k_upload while several back ends live (M2DEC_AMD_KCOPY_D2H) */
+	bool prestage = true; /* decode ahead: copy-out right behind the kernel (M2DEC_AMD_PRESTAGE) */
 	/* guards Arena::held / pending / ext: records_busy reads them from any thread while the decoder's
 	 * serial calls (acquire, submit, flush, bind) change them */
 	std::mutex arena_mu;
@@ -1264,10 +1265,10 @@ int launch_held(HipBackend *b);
  * both ways; on the shared copy stream instead (r140, r156) the copies waiting for their kernels held up the binds'
  * copies of frames the caller takes first, 1-4 % slower */
 static const int kPrestageMax = 32;
-static bool prestage_on()
+static bool prestage_knob()
 {
-	static const int on = getenv("M2DEC_AMD_PRESTAGE") ? atoi(getenv("M2DEC_AMD_PRESTAGE")) : 1;
-	return on != 0;
+	const char *e = getenv("M2DEC_AMD_PRESTAGE");
+	return e && *e ? atoi(e) != 0 : true;
 }
 
 void flush_timing(HipBackend *b, TimingSlot &t)
@@ -1568,7 +1569,7 @@ int launch_held(HipBackend *b)
 	 * of ~0.3 ms each from the bind to the frame's peek, the last one 6.2 ms after the last kernel) */
 	for (int i = 0; i < n; ++i) {
 		const HipBackend::Held &h = b->held[i];
-		if (!h.virt || b->prestaged >= kPrestageMax || !prestage_on()) continue;
+		if (!h.virt || b->prestaged >= kPrestageMax || !b->prestage) continue;
 		const int v = 64 + h.j.slot;
 		if (b->stg[v]) { /* (an earlier picture of this buffer never bound — ahead_ok orders reuse after the bind) */
 			if (b->slot_pending[v]) CHECK(hipEventSynchronize(b->slot_ev[v]));
@@ -1800,6 +1801,7 @@ extern "C" int m2dec_amd_hip_backend_create(m2r_backend_t *out, int device)
 	b->timing = tm ? atoi(tm) != 0 : true;
 	b->kcopy = kcopy_knob();
 	b->kd2h = kcopy_d2h_knob();
+	b->prestage = prestage_knob();
 	out->self = b;
 	out->set_frames = be_set_frames;
 	out->acquire = be_acquire;

@@ -47,7 +47,8 @@ def test_hip_md5_driver_matches_golden(built):
     {"M2DEC_AMD_KCOPY": "0"},        # records up by SDMA copies instead of k_upload
     {"M2DEC_AMD_KCOPY_D2H": "1"},    # frames down by k_upload on a single decoder too
     {"M2DEC_AMD_KCOPY_D2H": "0"},    # frames down by SDMA with concurrent decoders too
-], ids=["records_sdma", "frames_kernel", "frames_sdma"])
+    {"M2DEC_AMD_PRESTAGE": "0"},     # frames copied out at bind on the copy stream (round 5), not behind the kernel
+], ids=["records_sdma", "frames_kernel", "frames_sdma", "copy_at_bind"])
 def test_hip_copy_variants_match_golden(built, monkeypatch, env):
     """The upload / copy-out variants (read when a back end is created): one stream alone and two
     concurrent ones (several live back ends: the default copy-out is then k_upload), each bit-exact."""

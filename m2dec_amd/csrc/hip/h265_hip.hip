@@ -944,12 +944,13 @@ struct CtuSched {
 	uint16_t list[2][H265_CTU_RECS]; /* the chunk's records of each plane, in decoding order */
 	int n[2], next[2];
 	int done[H265_CTU_RECS];
+	int bl_total, bl_cnt; /* the blocks holding the left half of the CTU's last sample row (luma and chroma), done of them */
 };
 
 template <int NT>
 __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *recs, int m, CtuTile &tl, LdsCtu *ls, const CtuConst &kc,
                                            CtuSched &sc, int tid, int x0, int y0, const int16_t *cb, uint32_t clo, int row, int col,
-                                           int which = 0)
+                                           int which = 0, bool pub = false)
 {
 	/* which: 0 every record, 1 the residual-only (inter) ones, 2 the intra-predicted ones (the inter ones done) */
 	auto take = [&](const h265r_tu_t &t) { return which == 0 || ((t.flags & H265R_TU_PRED) ? 2 : 1) == which; };
@@ -970,6 +971,14 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 	LdsCtu &s = ls[wave];
 	/* the chunk's plane lists, owner maps and done flags */
 	for (int i = tid; i < 2 * 16 * 16; i += NT) (&sc.own[0][0])[i] = 0xffff;
+	if (tid == 0) sc.bl_total = sc.bl_cnt = 0;
+	/* pub (the row kernel, 64 x 64 CTBs): the left half of the CTU's last sample row goes out as soon as the blocks
+	 * holding it are done, for the CTU row below (its top-right blocks read at most 32 samples into this CTU) */
+	const int ctb = 1 << a.ctb_log2, rows_here = min(ctb, a.pic_h - y0), crows = rows_here >> 1;
+	auto in_bl = [&](const h265r_tu_t &t) {
+		const int n = 1 << t.log2;
+		return t.plane ? (t.y - (y0 >> 1) + n >= crows && t.x - (x0 >> 1) < 16) : (t.y - y0 + n >= rows_here && t.x - x0 < 32);
+	};
 	for (int k = tid; k < m; k += NT) sc.done[k] = which == 2 && !(recs[k].flags & H265R_TU_PRED);
 	if ((wave & 1) == 0) {
 		int cnt = 0;
@@ -986,12 +995,15 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 		}
 	}
 	__syncthreads();
+	int nbl = 0;
 	for (int k = tid; k < m; k += NT) {
 		const h265r_tu_t &t = recs[k];
 		const int u = (1 << t.log2) >> 2;
 		const int ux = (t.plane ? t.x - (x0 >> 1) : t.x - x0) >> 2, uy = (t.plane ? t.y - (y0 >> 1) : t.y - y0) >> 2;
 		for (int j = 0; j < u * u; ++j) sc.own[t.plane][(uy + j / u) * 16 + ux + j % u] = (uint16_t)k;
+		nbl += pub && in_bl(t);
 	}
+	if (nbl) atomicAdd(&sc.bl_total, nbl);
 	__syncthreads();
 	for (;;) {
 		/* (every lane adds, lane 0 by 1, and the wave takes lane 0's value: no single-lane section inside the
@@ -1036,6 +1048,20 @@ __device__ __forceinline__ void ctu_blocks(const H265Args &a, const h265r_tu_t *
 		H5ST(lane, 4, row, col, t.log2 | ((t.flags & H265R_TU_PRED) << 3) | (t.res[0] << 4) | (plane << 7) | ((t.mode & 63) << 8));
 		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 		__hip_atomic_store(&sc.done[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); /* (every lane: the same word) */
+		if (pub && in_bl(t)) {
+			const int seen = __builtin_amdgcn_readfirstlane(atomicAdd(&sc.bl_cnt, lane == 0 ? 1 : 0));
+			if (seen + 1 == __builtin_amdgcn_readfirstlane(sc.bl_total)) {
+				/* the last of them: every other one's tile writes were released before its count */
+				__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+				if (lane < 16) {
+					const int c = lane >> 3, w = lane & 7; /* 8 luma words, then 8 words of CbCr pairs */
+					if (c == 0) st_word(plane_px(a, 0, 0, x0 + 4 * w, y0 + rows_here - 1), *(const uint32_t *)&tl.y[rows_here - 1][4 * w]);
+					else st_word(plane_px(a, 1, 0, (x0 >> 1) + 2 * w, (y0 >> 1) + crows - 1), *(const uint32_t *)&tl.c[crows - 1][4 * w]);
+				}
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+				__hip_atomic_store((gi32 *)&a.progress[row], 2 * col + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			}
+		}
 	}
 }
 
@@ -1121,7 +1147,11 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 		/* the row above, once that CTU row finished the CTU above-right */
 		if (above) {
 			if (wave == 0) {
-				const int need = min(col + 2, a.ctu_cols);
+				/* progress is in half CTUs: 2 c + 1 once CTU c's last row's left half is out (64 x 64 CTBs only), 2 (c + 1)
+				 * once CTU c is done; with 64 x 64 CTBs (transform blocks <= 32) a CTU reads the row above at most 32
+				 * samples into the CTU above-right, with smaller CTBs possibly all of it (then no half step is
+				 * published and the wait is for the whole CTU) */
+				const int need = col + 1 < a.ctu_cols ? 2 * (col + 1) + 1 : 2 * a.ctu_cols;
 				unsigned spins = 0;
 				for (;;) {
 					const int got = __hip_atomic_load((gi32 *)&a.progress[row - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1149,7 +1179,9 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 		H5ST(tid, 1, row, col, above);
 		/* the CTU's blocks (luma on waves 0-1, chroma on waves 2-3, each plane in decoding order): the staged first
 		 * chunk, then any further chunk of a CTU with more than H265_CTU_RECS records */
-		if (m0 > 0) ctu_blocks<NT>(a, recs, m0, tl, ls, kc, sch, tid, x0, y0, cb0, clo0, row, col);
+		if (m0 > 0)
+			ctu_blocks<NT>(a, recs, m0, tl, ls, kc, sch, tid, x0, y0, cb0, clo0, row, col, 0,
+			               m0 == i1 - i0 && row + 1 < a.ctu_rows && a.ctb_log2 == 6 && !(a.flags & (1 << 28)));
 		for (int c0 = i0 + m0; c0 < i1; c0 += H265_CTU_RECS) {
 			const int m = min(H265_CTU_RECS, i1 - c0);
 			__syncthreads(); /* (the previous chunk is consumed) */
@@ -1176,7 +1208,7 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_rows(const H265Args *ap)
 			}
 			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 			__syncthreads();
-			if (tid == 0) __hip_atomic_store((gi32 *)&a.progress[row], col + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			if (tid == 0) __hip_atomic_store((gi32 *)&a.progress[row], 2 * (col + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 			H5ST(tid, 3, row, col, 0);
 		}
 	}
@@ -2081,6 +2113,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	h.flags = pic->flags;
 	if (getenv("M2DEC_AMD_H265_DIAG_NOWAIT")) h.flags |= 1 << 30; /* (diagnostic: CTU-grid neighbour waits skipped — wrong output) */
 	if (getenv("M2DEC_AMD_H265_GRID_ONEPASS")) h.flags |= 1 << 29; /* (A/B: no inter-first split of the CTU-grid blocks) */
+	if (getenv("M2DEC_AMD_H265_NO_HALF_ROW")) h.flags |= 1 << 28;   /* (A/B: a CTU's last row published only with the CTU) */
 	h.beta_offset = pic->beta_offset;
 	h.tc_offset = pic->tc_offset;
 	h.cb_qp_offset = pic->cb_qp_offset;

@@ -49,7 +49,13 @@ template <typename T> __device__ __forceinline__ T *lds_ptr(lds_u8 *p) { return 
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
 
-#define SPIN_LIMIT (1 << 20) /* ~1 s of polling: a hand-off that never comes is an error, not a hang */
+/* A wait for a hand-off ends in an error only after SPIN_ABORT polls (~30-60 s): every producer a wait points at
+ * holds a workgroup reservation of the device budget (SlotBudget), so a slow hand-off means the GPU is shared with
+ * other work and waiting is the recovery; only one that never comes (a bug) ends the decode.  After g_spin_report
+ * polls (~1 s; M2DEC_AMD_SPIN_REPORT) a wait is reported in err[1] — the host prints it once — and goes on
+ * (round 5 ended the decode there). */
+#define SPIN_ABORT (1u << 26)
+__device__ unsigned g_spin_report = 1u << 20;
 
 /* Diagnostic timestamps (build with -DM2DEC_STAMPS; never in the product build): per MB row and
  * role, s_memrealtime (100 MHz) at events, read back with m2dec_amd_debug_stamps(). */
@@ -276,11 +282,19 @@ __device__ __forceinline__ bool spin_ok(unsigned &spins, int *err, int code)
 	__builtin_amdgcn_s_sleep(1);
 	++spins;
 	if ((spins & 255) == 0 && __hip_atomic_load((gi32 *)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-	if (spins > SPIN_LIMIT) {
+	if (__builtin_expect(spins == g_spin_report, 0) && (threadIdx.x & 63) == 0) atomicOr(err + 1, code); /* (reported, waits on) */
+	if (spins > SPIN_ABORT) {
 		if ((threadIdx.x & 63) == 0) atomicOr(err, code);
 		return false;
 	}
 	return true;
+}
+
+/* the polls after which a wait is reported (M2DEC_AMD_SPIN_REPORT), on the current device */
+extern "C" int m2dec_amd_hip_set_spin_report(unsigned polls)
+{
+	CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_report), &polls, sizeof(polls), 0, hipMemcpyHostToDevice));
+	return 0;
 }
 
 __device__ __forceinline__ bool poll_ge(int *flag, int need, int *err)

@@ -103,3 +103,5 @@ static inline int picture_blocks_dp(int inter_workers, int row_wgs, int Hmb, boo
 /* dynamic LDS bytes of one k_deblock workgroup for a W-sample-wide picture */
 size_t m2r_deblock_lds_bytes(int W, int Wmb);
 extern "C" int m2dec_amd_debug_stamps_clear(void); /* no-op unless built with M2DEC_STAMPS */
+/* polls after which a hand-off wait is reported in err[1] (and goes on) on the current device; abort: ~2^26 polls */
+extern "C" int m2dec_amd_hip_set_spin_report(unsigned polls);

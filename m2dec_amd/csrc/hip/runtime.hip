@@ -496,8 +496,10 @@ struct Sched {
 			CHECK(g_pool.stream(dev, &st[k])); /* (the rest stay null) */
 			CHECK(g_pool.event(dev, false, &busy[k]));
 		}
-		CHECK(hipMalloc(&err, 16)); /* (the sync events are created on first use: next_event) */
+		CHECK(hipMalloc(&err, 16)); /* [0] a failed hand-off, [1] a reported slow one (the sync events: next_event) */
 		CHECK(hipMemset(err, 0, 16));
+		if (const char *e = getenv("M2DEC_AMD_SPIN_REPORT")) /* (tests: force the slow-wait path) */
+			if (atoi(e) > 0 && m2dec_amd_hip_set_spin_report((unsigned)atoi(e)) < 0) return -1;
 		memset(&slot_seq, 0, sizeof(slot_seq));
 		int cus = 0;
 		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -930,12 +932,18 @@ struct Sched {
 		return 0;
 	}
 
+	bool stall_told = false;
 	int check_err()
 	{
-		int e = 0;
-		CHECK(hipMemcpy(&e, err, sizeof(int), hipMemcpyDeviceToHost));
-		if (e) {
-			fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e);
+		int e[2] = {0, 0};
+		CHECK(hipMemcpy(e, err, sizeof(e), hipMemcpyDeviceToHost));
+		if (e[1] && !stall_told) {
+			stall_told = true;
+			fprintf(stderr, "m2dec_amd: device %d: a wavefront hand-off waited past the report threshold (code %d; the GPU "
+			        "is shared with other work?) — waited on, the decode goes on\n", dev, e[1]);
+		}
+		if (e[0]) {
+			fprintf(stderr, "m2dec_amd: wavefront hand-off failed (err=%d)\n", e[0]);
 			return -1;
 		}
 		return 0;

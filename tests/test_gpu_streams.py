@@ -1,9 +1,13 @@
 """Synthetic streams through the product path (host parser -> HIP back end) on the GPU: every
 frame's MD5 must equal the CPU oracle's golden."""
+import os
+
 import pytest
 
 import m2dec_amd
 from tests._streams import GOLDEN, stream
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
@@ -96,3 +100,21 @@ def test_hip_multistream_batch_replay_matches_golden(built, names):
         want = GOLDEN[n]["md5"]
         bad = [i for i, (a, b) in enumerate(zip(g, want)) if a != b]
         assert len(g) == len(want) and not bad, f"{n}: frames {bad[:10]} differ (of {len(want)})"
+
+
+@pytest.mark.gpu
+def test_forced_slow_waits_still_match_golden(built):
+    """a hand-off wait past the report threshold (~1 s of polls by default; here every wait that
+    polls at all, M2DEC_AMD_SPIN_REPORT=1) is reported once and waited on — every producer a wait points at holds
+    a device-budget reservation, so waiting is the recovery — instead of ending the decode with an error as in
+    round 5.  The stream still matches its golden, and the report reaches stderr.  (A separate process: the
+    threshold is set when the process's first back end starts.)"""
+    import subprocess
+    import sys
+    code = ("import m2dec_amd; from tests._streams import stream, GOLDEN; "
+            "n = 'c3_1080p_s1'; print('OK' if m2dec_amd.decode_stream_md5(stream(n)) == GOLDEN[n]['md5'] else 'BAD')")
+    env = dict(os.environ, M2DEC_AMD_SPIN_REPORT="1")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith("OK"), r.stdout + r.stderr[-2000:]
+    assert "waited past the report threshold" in r.stderr

@@ -44,7 +44,7 @@ extern "C" void m2dec_par_memcpy(int crew, int n, void *const *dst, const void *
 enum { M2DEC_CREW_SYNC_ = 1 }; /* = M2DEC_CREW_SYNC (h264_dec.h) */
 
 #define H265_CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "m2dec_amd HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -1; } } while (0)
-#define H265_SPIN_LIMIT (1 << 22)
+#define H265_SPIN_LIMIT (1 << 26) /* ~30-60 s of polls: every wait points at a workgroup dispatched earlier (a slow one means a shared GPU: waited on); only a bug ends the picture */
 
 namespace {
 

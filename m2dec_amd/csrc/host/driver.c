@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include "m2dec_amd.h"
 #include "h264_dec.h"
 #include "h265_dec.h"
@@ -58,12 +59,74 @@ static int reread(void *arg)
 	return -1;
 }
 
+/* Frame memory kept across decodes, process-wide.  A frame-sized malloc is fresh zero pages, so the first copy of a
+ * picture into it takes ~760 page faults per 1080p frame (~0.4 ms, serial in the thread that syncs the picture):
+ * the H.265 output tail of the r176 timeline.  A process decoding stream after stream takes the same buffers back
+ * (by exact size; at most POOL_CAP bytes are parked, the oldest sizes go first).  The decoders write every sample
+ * of a picture before it is output or referenced, as with a fresh buffer. */
+#define POOL_MAX 256
+#define POOL_CAP ((size_t)1 << 30)
+static pthread_mutex_t pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+	uint8_t *p;
+	size_t n;
+} pool[POOL_MAX];
+static int pool_n;
+static size_t pool_bytes;
+
+static uint8_t *pool_take(size_t n)
+{
+	pthread_mutex_lock(&pool_mu);
+	for (int i = pool_n - 1; i >= 0; --i)
+		if (pool[i].n == n) {
+			uint8_t *p = pool[i].p;
+			memmove(&pool[i], &pool[i + 1], (size_t)(pool_n - 1 - i) * sizeof(pool[0]));
+			--pool_n;
+			pool_bytes -= n;
+			pthread_mutex_unlock(&pool_mu);
+			return p;
+		}
+	pthread_mutex_unlock(&pool_mu);
+	return (uint8_t *)malloc(n);
+}
+
+static int pool_on(void)
+{
+	static int on = -1; /* M2DEC_AMD_FRAME_POOL=0: every decode mallocs and frees its own frames */
+	if (on < 0) {
+		const char *e = getenv("M2DEC_AMD_FRAME_POOL");
+		on = !(e && e[0] == '0');
+	}
+	return on;
+}
+
+static void pool_give(uint8_t *p, size_t n)
+{
+	if (!p) return;
+	if (n > POOL_CAP || !pool_on()) {
+		free(p);
+		return;
+	}
+	pthread_mutex_lock(&pool_mu);
+	while (pool_n && (pool_n == POOL_MAX || pool_bytes + n > POOL_CAP)) { /* the oldest go */
+		free(pool[0].p);
+		pool_bytes -= pool[0].n;
+		memmove(&pool[0], &pool[1], (size_t)(pool_n - 1) * sizeof(pool[0]));
+		--pool_n;
+	}
+	pool[pool_n].p = p;
+	pool[pool_n].n = n;
+	++pool_n;
+	pool_bytes += n;
+	pthread_mutex_unlock(&pool_mu);
+}
+
 static void frames_free(drv_t *v)
 {
 	if (v->hold) m2dec_hold_wait_idle(v->hold); /* (nobody reads the frames any more) */
 	for (int i = 0; i < v->nframes; ++i) {
-		free(v->mem[i][0]);
-		free(v->mem[i][1]);
+		pool_give(v->mem[i][0], v->luma_len + 15);
+		pool_give(v->mem[i][1], (v->luma_len >> 1) + 15);
 	}
 	free(v->second);
 	v->second = NULL;
@@ -96,8 +159,8 @@ static int header_cb(void *arg, void *id)
 	v->second_len = info.additional_size ? (size_t)info.additional_size : 1;
 	v->second = (uint8_t *)calloc(1, v->second_len);
 	for (int i = 0; i < bufnum; ++i) {
-		v->mem[i][0] = (uint8_t *)malloc(luma_len + 15);
-		v->mem[i][1] = (uint8_t *)malloc((luma_len >> 1) + 15);
+		v->mem[i][0] = pool_take(luma_len + 15);
+		v->mem[i][1] = pool_take((luma_len >> 1) + 15);
 		memset(&v->frames[i], 0, sizeof(v->frames[i]));
 		v->frames[i].luma = (uint8_t *)(((uintptr_t)v->mem[i][0] + 15) & ~(uintptr_t)15);
 		v->frames[i].chroma = (uint8_t *)(((uintptr_t)v->mem[i][1] + 15) & ~(uintptr_t)15);

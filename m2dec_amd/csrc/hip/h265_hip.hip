@@ -1711,11 +1711,12 @@ struct H265Gpu {
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
+	double trace_ms = 0.5;     /* M2DEC_AMD_H265_TRACE_MS: the submit steps reported above this */
 	bool kcopy = true;         /* record upload by k_h265_upload (M2DEC_AMD_H265_KCOPY=0: hipMemcpyAsync) */
 	bool kcopy_d2h = false;    /* M2DEC_AMD_KCOPY_D2H=1: the frame down by k_h265_upload writing the pinned staging buffer */
 	size_t max_total = 0;      /* the largest picture's arena bytes so far */
 	bool waves4 = true;        /* CTU kernels with two waves per plane (M2DEC_AMD_H265_WAVES=2: one) */
-	bool err_async = false;    /* M2DEC_AMD_H265_ERR_ASYNC=1 (A/B) */
+	bool err_async = true;     /* error word copied behind each frame (M2DEC_AMD_H265_ERR_ASYNC=0: read in sync) */
 	bool ctu_grid = true;      /* P / B pictures: one workgroup per CTU (M2DEC_AMD_H265_CTU_GRID=0: the row kernel) */
 	bool no_stage = false;     /* M2DEC_AMD_H265_STAGE=0: records copied by submit only (A/B) */
 };
@@ -2036,7 +2037,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		struct timespec ts;
 		clock_gettime(CLOCK_MONOTONIC, &ts);
 		const double t = ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
-		if (t - tp > 0.5) fprintf(stderr, "h265 submit slot %d: %s %.2f ms\n", pic->slot, what, t - tp);
+		if (t - tp > g->trace_ms) fprintf(stderr, "h265 submit slot %d: %s %.3f ms\n", pic->slot, what, t - tp);
 		tp = t;
 	};
 	unsigned refs = 0;
@@ -2153,6 +2154,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	g->tr_next = (g->tr_next + 1) % 32;
 	flush_timing(g, tm);
 	H265_CHECK(hipEventRecord(tm.t0, s));
+	lap("timing");
 	if (pic->n_pu) {
 		const int grid = pic->n_pu < g->cus * 8 ? pic->n_pu : g->cus * 8;
 		hipLaunchKernelGGL(k_h265_mc, dim3(grid), dim3(64), 0, s, args);
@@ -2174,12 +2176,14 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		}
 		H265_CHECK(hipGetLastError());
 	}
+	lap("ctu kernels");
 	if (pic->flags & H265R_PIC_DEBLOCK) {
 		const int nv = (g->H / 4) * (g->W / 8), nh = (g->H / 8) * (g->W / 4);
 		hipLaunchKernelGGL(k_h265_deblock, dim3((nv + 255) / 256), dim3(256), 0, s, args, 0);
 		hipLaunchKernelGGL(k_h265_deblock, dim3((nh + 255) / 256), dim3(256), 0, s, args, 1);
 		H265_CHECK(hipGetLastError());
 	}
+	lap("deblock");
 	if (pic->flags & (H265R_PIC_SAO_LUMA | H265R_PIC_SAO_CHROMA)) {
 		H265_CHECK(hipMemcpyAsync(ln.copy, h.frame, (size_t)g->W * g->H * 3 / 2, hipMemcpyDeviceToDevice, s));
 		const int nsa = (pic->pic_h + (pic->pic_h >> 1)) * (g->W >> 2); /* (4 bytes of a row per thread) */
@@ -2209,6 +2213,7 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		}
 	g->readers[pic->slot].clear();
 	g->kdone[pic->slot] = kd;
+	lap("events");
 	/* the picture to its staging buffer, behind the kernels */
 	const int c = pic->slot;
 	const size_t bytes = (size_t)g->W * g->H * 3 / 2;
@@ -2236,9 +2241,10 @@ int h_sync(void *p, int slot)
 	if (!g->pend[slot]) return 0;
 	H265_CHECK(hipEventSynchronize(g->ev[slot]));
 	{
-		/* a block hand-off that never came (bounded spin): the sticky error word */
-		/* (copied behind the frame on its stream with M2DEC_AMD_H265_ERR_ASYNC=1, else a synchronous read as the
-		 * H.264 back end does: a 4-byte copy per frame on the copy engines measured slower there) */
+		/* a block hand-off that never came (bounded spin): the sticky error word, copied behind the frame on its
+		 * stream as the H.264 back end does.  M2DEC_AMD_H265_ERR_ASYNC=0 reads it here with a synchronous hipMemcpy,
+		 * whose blit runs on the null stream's hardware queue, shared with one of the picture streams: every frame
+		 * then waited for that stream's last kernel (r179 timeline: frame 0 out 3.3 ms after its copy-out) */
 		int err = 0;
 		if (g->err_async) err = __atomic_load_n(&g->err_host[slot], __ATOMIC_ACQUIRE);
 		else H265_CHECK(hipMemcpy(&err, g->err, sizeof(int), hipMemcpyDeviceToHost));
@@ -2306,6 +2312,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_BLOCKS")) g->block_kernel = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
+	if (const char *e = getenv("M2DEC_AMD_H265_TRACE_MS")) g->trace_ms = atof(e);
 	if (const char *e = getenv("M2DEC_AMD_H265_WAVES")) g->waves4 = atoi(e) >= 4;
 	if (const char *e = getenv("M2DEC_AMD_H265_KCOPY")) g->kcopy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_KCOPY_D2H")) g->kcopy_d2h = atoi(e) != 0;

@@ -1359,9 +1359,13 @@ __global__ __launch_bounds__(NT, 2) void k_h265_ctu_grid(const H265Args *ap)
 }
 
 /* ---- the picture's records from the pinned arena into device memory (16 bytes per thread, grid-stride) */
-__global__ __launch_bounds__(256) void k_h265_upload(const uint4 *src, uint4 *dst, size_t n16)
+/* a copy by a kernel (records up from the pinned arena, frames down to pinned staging); `zero` (nzero ints): the
+ * picture's scratch words cleared in the same launch (one HIP call fewer per picture on the serial submission) */
+__global__ __launch_bounds__(256) void k_h265_upload(const uint4 *src, uint4 *dst, size_t n16, int *zero, size_t nzero)
 {
-	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) dst[i] = src[i];
+	const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, step = (size_t)gridDim.x * blockDim.x;
+	for (size_t i = t; i < n16; i += step) dst[i] = src[i];
+	for (size_t i = t; i < nzero; i += step) zero[i] = 0;
 }
 
 /* ---- motion compensation (h265.cpp:3132-3595; oracle/h265_oracle.c mc_picture) */
@@ -1711,6 +1715,7 @@ struct H265Gpu {
 	std::vector<uint8_t *> grave_host, grave_dev; /* outgrown arenas (freed at set_frames / destroy) */
 	bool block_kernel = false; /* M2DEC_AMD_H265_BLOCKS=1: the per-block dependency-graph kernel */
 	bool trace = false;        /* M2DEC_AMD_H265_TRACE */
+	bool upload_zero = true;   /* scratch cleared by the upload kernel (M2DEC_AMD_H265_UPLOAD_ZERO=0: hipMemsetAsync, A/B) */
 	double trace_ms = 0.5;     /* M2DEC_AMD_H265_TRACE_MS: the submit steps reported above this */
 	bool kcopy = true;         /* record upload by k_h265_upload (M2DEC_AMD_H265_KCOPY=0: hipMemcpyAsync) */
 	bool kcopy_d2h = false;    /* M2DEC_AMD_KCOPY_D2H=1: the frame down by k_h265_upload writing the pinned staging buffer */
@@ -2132,16 +2137,17 @@ int h_submit(void *p, const h265r_picture_t *pic)
 		 * per decode, the GPU idling meanwhile (round-5 H.265 timelines) */
 		const size_t n16 = total / 16;
 		const int grid = (int)std::min<size_t>(512, (n16 + 255) / 256);
-		hipLaunchKernelGGL(k_h265_upload, dim3(grid), dim3(256), 0, s, (const uint4 *)a.host_dev, (uint4 *)a.dev, n16);
+		hipLaunchKernelGGL(k_h265_upload, dim3(grid), dim3(256), 0, s, (const uint4 *)a.host_dev, (uint4 *)a.dev, n16,
+		                   g->upload_zero ? ln.scratch : (int *)nullptr, g->upload_zero ? sn : (size_t)0);
 		H265_CHECK(hipGetLastError());
+		if (!g->upload_zero) H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
 	} else {
 		H265_CHECK(hipMemcpyAsync(a.dev, a.host, total, hipMemcpyHostToDevice, s));
+		H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
 	}
 	lap("upload");
 	g->record_bytes += (int64_t)o_args;
 	g->frame_bytes += (int64_t)g->W * g->H * 3 / 2;
-	H265_CHECK(hipMemsetAsync(ln.scratch, 0, sizeof(int) * sn, s));
-	lap("memset");
 	/* dependencies on other streams' pictures, after the uploads (a copy behind a wait on another stream's
 	 * picture can hold this thread until that picture completes: 8-10 ms per decode in the round-5 trace) */
 	for (int r = 0; r < H265R_MAX_FRAMES; ++r)
@@ -2221,7 +2227,8 @@ int h_submit(void *p, const h265r_picture_t *pic)
 	if (g->kcopy_d2h && bytes % 16 == 0) {
 		void *dh = nullptr;
 		H265_CHECK(hipHostGetDevicePointer(&dh, g->stg[c], 0));
-		hipLaunchKernelGGL(k_h265_upload, dim3(256), dim3(256), 0, s, (const uint4 *)h.frame, (uint4 *)dh, bytes / 16);
+		hipLaunchKernelGGL(k_h265_upload, dim3(256), dim3(256), 0, s, (const uint4 *)h.frame, (uint4 *)dh, bytes / 16,
+		                   (int *)nullptr, (size_t)0);
 		H265_CHECK(hipGetLastError());
 	} else {
 		H265_CHECK(hipMemcpyAsync(g->stg[c], h.frame, bytes, hipMemcpyDeviceToHost, s));
@@ -2313,6 +2320,7 @@ extern "C" int h265_hip_backend_create(h265r_backend_t *out, int device)
 	if (const char *e = getenv("M2DEC_AMD_H265_CTU_GRID")) g->ctu_grid = atoi(e) != 0;
 	g->trace = getenv("M2DEC_AMD_H265_TRACE") != nullptr;
 	if (const char *e = getenv("M2DEC_AMD_H265_TRACE_MS")) g->trace_ms = atof(e);
+	if (const char *e = getenv("M2DEC_AMD_H265_UPLOAD_ZERO")) g->upload_zero = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_H265_WAVES")) g->waves4 = atoi(e) >= 4;
 	if (const char *e = getenv("M2DEC_AMD_H265_KCOPY")) g->kcopy = atoi(e) != 0;
 	if (const char *e = getenv("M2DEC_AMD_KCOPY_D2H")) g->kcopy_d2h = atoi(e) != 0;
